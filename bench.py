@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark: Count-Min update throughput on device-resident synthetic traffic.
+
+Metric (BASELINE.json): "Mpackets/s CMS update (device-resident, d=4 w=2^20)
+at 1/2/4/8 MI355X".  Workload = configs[1]: Count-Min d=4 w=2^20, 100M Zipf(1.1)
+5-tuple header records (64 B + 4 B wire length) resident in HBM; one step =
+one pass of the full hot path (parse -> flow key -> flow id -> 4 MurmurHash3
+rows -> bucket updates) over the 100M-packet batch; the sketch state carries
+over from step to step like a live measurement period.
+
+Multi-GPU (torchrun, one rank per GPU over RCCL): each rank owns the flows
+whose SrcIP hashes to it and processes its own 100M-packet shard stream (weak
+scaling, no data-path collective); after the timed region the ranks
+all-gather their heavy-hitter candidates (the per-window exchange).
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PACKETS = 100_000_000
+WIDTH, DEPTH = 1 << 20, 4
+FIELDS = ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"]
+BYTES_PER_PKT = 68          # SURVEY §8d convention A: 64-B header + 4-B wire length
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def row_seeds(d):
+    s, out = 0x9747B28C, []
+    for _ in range(d):
+        s = (s + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        z = s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+        out.append((z ^ (z >> 31)) & 0xFFFFFFFF)
+    return np.array(out, np.uint32)
+
+
+def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0):
+    """Timed CPU restatements on a bounded prefix of the same stream (rank 0)."""
+    from oracle import oracle as orc
+    n = min(int(wl_dev.shape[0]), 24_000_000)
+    hdr = hdr_dev[:n].cpu().numpy()
+    wl = wl_dev[:n].cpu().numpy().view(np.uint32)
+    seeds = row_seeds(DEPTH)
+    # (1) sequential oracle, 1 thread
+    cm = orc.CountMin(WIDTH, DEPTH, 1 << 20, 1000, 37, seeds)
+    chunk, done, t0 = 1_000_000, 0, time.perf_counter()
+    while done < n and time.perf_counter() - t0 < seconds:
+        m = min(chunk, n - done)
+        cm.insert_hdr64(hdr[done:done + m], wl[done:done + m], FIELDS)
+        done += m
+    seq_rate = done / (time.perf_counter() - t0) / 1e6
+    seq_n = done
+    del cm
+    # (2) restatement of the Go worker pool (shared sketch, CAS loops, shared cursor)
+    threads = int(os.environ.get("GNS_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    cm = orc.CountMin(WIDTH, DEPTH, 1 << 20, 1000, 37, seeds)
+    done, t0 = 0, time.perf_counter()
+    chunk = 4_000_000
+    while done < n and time.perf_counter() - t0 < seconds / 2:
+        m = min(chunk, n - done)
+        cm.insert_hdr64_pool(hdr[done:done + m], wl[done:done + m], FIELDS, threads)
+        done += m
+    pool_rate = done / (time.perf_counter() - t0) / 1e6
+    return {
+        "value": round(pool_rate, 3), "unit": "Mpackets/s", "cores": threads, "kind": "port",
+        "sample": f"first {done:,} packets of the same synthetic stream; C restatement of the Go worker pool "
+                  f"(count_min.go CAS loops + parse/encode, {threads} threads, shared cursor)",
+        "sequential_oracle": {"value": round(seq_rate, 3), "cores": 1, "packets": seq_n},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--packets", type=int, default=PACKETS)
+    ap.add_argument("--batch", type=int, default=0, help="device batch (packets); 0 = whole step")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    from go2netspectra_amd import CountMin, SyntheticTraffic
+
+    n = args.packets
+    syn = SyntheticTraffic(shard=rank, nshards=world, device=local)
+    hdr, wl = syn.generate(n)
+    batch = args.batch or n
+    cm = CountMin(WIDTH, DEPTH, 1 << 20, 1000, flow_fields=FIELDS, seeds=row_seeds(DEPTH),
+                  max_flows=1 << 21, batch_packets=batch, device=local)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        cm.insert_headers(hdr, wl)
+        cm.flush()
+    cm.set_timing(True)
+    cm.stage_times(reset=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cm.insert_headers(hdr, wl)
+    cm.flush()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    stages = cm.stage_times()
+
+    # per-window exchange: all-gather heavy-hitter candidates (not timed)
+    hh = cm.heavy_hitters()
+    if world > 1:
+        from go2netspectra_amd.dist import allgather_heavy
+        hh = allgather_heavy(hh, world)
+
+    total_pkts = n * args.steps * world
+    value = total_pkts / elapsed / 1e6
+    # dominant kernel and its roofline (HIP events on the engine stream)
+    kern = {k: v for k, v in stages.items() if k in ("extract", "resolve", "scan", "scatter", "apply")}
+    dom = max(kern, key=lambda k: kern[k][0])
+    dom_ms, dom_launches = kern[dom]
+    avg_ms = dom_ms / max(dom_launches, 1)
+    pkts_per_launch = n * args.steps / max(dom_launches, 1)
+    achieved = BYTES_PER_PKT * pkts_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    if os.path.exists(tfile):
+        try:
+            traffic = json.load(open(tfile)).get(dom)
+        except Exception:
+            traffic = None
+
+    line = {
+        "metric": "Mpackets/s CMS update (device-resident, d=4 w=2^20) at 1/2/4/8 MI355X",
+        "value": round(value, 2), "unit": "Mpackets/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (Zipf 1.1 over 2^20 5-tuples, 64-B Ethernet/IPv4/TCP|UDP records, on-device generator)",
+        "config": {"workload": "configs[1]: Count-Min d=4 w=2^20, 100M Zipf(1.1) 5-tuple headers in HBM per GPU, "
+                               "bit-exact counters", "packets_per_step_per_gpu": n, "device_batch": batch,
+                   "key": "5-tuple (37 B)", "parallelism": f"flow-hash shards x{world}"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "bytes_per_packet": BYTES_PER_PKT, "kernel_avg_ms": round(avg_ms, 4),
+                     "pipeline_frac": round(BYTES_PER_PKT * n * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4)},
+        "stage_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()},
+        "heavy_hitters": {"count": len(hh.Count), "size": len(hh.Size or [])},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(hdr, wl)
+    elif rank == 0:
+        line["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,20 @@
+"""go2netspectra_amd -- MI355X-native sketch hot path for Go2NetSpectra.
+
+Drop-in for the reference's per-packet sketch path (internal/engine/impl/sketch):
+header parse -> flow-key encode -> d seeded MurmurHash3 -> fingerprinted
+Count-Min / SuperSpread bucket updates, executed by hand-written gfx950 HIP
+kernels behind the C ABI in include/gns_sketch.h (libgns_sketch.so).
+"""
+from ._lib import GnsError, build, load
+from .config import Config, SketchTaskDef, load_config, parse_config
+from .factory import Manager, TaskGroup, create, register_aggregator
+from .packets import HeaderBatch, PacketBatch, SyntheticTraffic, ip_slot, read_pcap, write_pcap
+from .sketch import CountMin, HeavyCount, HeavyRecord, HeavySize, SuperSpread
+from .task import New, SketchTask, decode_flow
+
+__all__ = [
+    "GnsError", "build", "load", "Config", "SketchTaskDef", "load_config", "parse_config", "Manager",
+    "TaskGroup", "create", "register_aggregator", "HeaderBatch", "PacketBatch", "SyntheticTraffic",
+    "ip_slot", "read_pcap", "write_pcap", "CountMin", "HeavyCount", "HeavyRecord", "HeavySize",
+    "SuperSpread", "New", "SketchTask", "decode_flow",
+]

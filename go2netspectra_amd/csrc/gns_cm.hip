@@ -1,0 +1,1249 @@
+// gns_cm.hip -- MI355X (gfx950) engine for Go2NetSpectra's fingerprinted
+// "CountMin" (internal/engine/impl/sketch/statistic/count_min.go).
+//
+// Semantics: the device state after a sequence of inserts is bit-identical to
+// count_min.go fed the same packets in the same order by ONE worker with the
+// same row seeds.  Each bucket holds two independent
+// (fingerprint, counter) pairs whose update rules are ORDER-DEPENDENT
+// (count_min.go:180-235), so the engine never scatters with plain atomics.
+//
+// Pipeline per device batch:
+//   K1 k_extract  : packet -> flow key (registers) -> flow id (exact dictionary)
+//                   -> d row indices; per-block (row, tile) histograms.
+//   K1b k_resolve : re-probe packets whose dictionary slot was claimed in the
+//                   same launch (rare after the first batch).
+//   K2 k_scan*    : exclusive scan of the histograms -> stable bin offsets.
+//   K3 k_scatter  : stable partition of 8-byte bucket updates into (row, tile)
+//                   bins (LDS-staged so every bin receives contiguous runs).
+//   K4 k_apply    : one workgroup per bin; the tile's bucket state lives in
+//                   LDS; updates are applied chunk by chunk in stream order:
+//                   order-free aggregate fast path where provably exact,
+//                   sequential replay for the buckets where it is not.
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "gns_common.hpp"
+
+namespace gns {
+
+constexpr uint32_t kTileBitsMax = 12;
+constexpr uint32_t kTileMax = 1u << kTileBitsMax;   // buckets per LDS tile
+constexpr uint32_t kMaxTilesPerRow = 1024;
+constexpr uint32_t kSizeEsc = 0xFFFFFu;             // 20-bit size field escape
+constexpr uint32_t kOvfFlag = 0x80000000u;
+constexpr uint32_t kOvfCap = 1u << 20;
+constexpr int kExThreads = 256;
+constexpr uint32_t kChunk = 16384;                  // packets per K1/K3 block
+constexpr int kScThreads = 256;
+constexpr int kScItems = 8;
+constexpr uint32_t kScRound = 4 * 64 * kScItems;    // 2048 packets per K3 round
+constexpr int kApThreads = 1024;
+constexpr int kApItems = 4;
+constexpr uint32_t kApChunk = kApThreads * kApItems; // 4096 updates per K4 step
+constexpr uint32_t kScanSeg = 4096;
+
+struct CmGeom {
+    uint32_t w, d, wmask, pow2;
+    uint32_t tile_bits, ntiles, nbins, nbits;  // nbits = ceil_log2(ntiles)
+    uint32_t seeds[8];
+};
+
+__device__ __forceinline__ uint32_t row_index(const CmGeom &g, uint32_t h) {
+    return g.pow2 ? (h & g.wmask) : (h % g.w);  // count_min.go:177 `% t.w`
+}
+
+// Counter words of stats[]: 0 inserted, 1 dropped, 2 unsupported, 3 dict-full, 4 ovf-full
+struct ExtractArgs {
+    InputDesc in;
+    uint64_t n;
+    KeyPlanN kp;
+    CmGeom g;
+    DictDev D;
+    uint32_t epoch;
+    uint32_t *keyid;
+    uint32_t *idx;       // [d][n]
+    uint64_t *pend;      // per-block regions of kChunk
+    uint32_t *pend_cnt;  // [nblk]
+    uint32_t *pend_total;
+    uint32_t *hist;      // [nbins][nblk]
+    uint32_t nblk;
+    unsigned long long *stats;
+};
+
+template <int KIND, int MODE>
+__device__ __forceinline__ int packet_key(const InputDesc &in, uint32_t K, const uint8_t *s_src,
+                                          uint64_t p, uint32_t (&kw)[GNS_KWMAX]) {
+    if constexpr (KIND == IN_KEYS) {
+        load_key_bytes<GNS_KWMAX>(in.keys + p * in.stride, K, (in.aligned & 1u) != 0, kw);
+        return PARSE_OK;
+    } else {
+        uint32_t tw[10];
+        const int st = load_tuple<KIND>(in, p, tw);
+        if (st != PARSE_OK) return st;
+        make_key_m<MODE, GNS_KWMAX>(K, s_src, tw, kw);
+        return PARSE_OK;
+    }
+}
+
+// K1: parse/encode, dictionary, row hashes, block histogram.
+template <int KIND, int MODE>
+__global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
+    extern __shared__ uint32_t s_hist[];
+    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
+    __shared__ uint8_t s_src[80];
+    const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    stage_plan<MODE>(a.kp, s_src);
+    const uint32_t K = a.kp.K;
+    for (uint32_t i = tid; i < a.g.nbins; i += kExThreads) s_hist[i] = 0;
+    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; }
+    __syncthreads();
+    const uint64_t beg = (uint64_t)blk * kChunk;
+    const uint64_t end = min(a.n, beg + kChunk);
+    uint32_t n_ok = 0;
+    for (uint64_t p = beg + tid; p < end; p += kExThreads) {
+        uint32_t kw[GNS_KWMAX];
+        const int st = packet_key<KIND, MODE>(a.in, K, s_src, p, kw);
+        if (st != PARSE_OK) {
+            a.keyid[p] = GNS_ID_NONE;
+            atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
+            continue;
+        }
+        uint32_t out;
+        const uint32_t slot0 = mm3_n<GNS_KWMAX>(kw, K, a.D.seed) & a.D.mask;
+        const int r = dict_find_or_claim(a.D, kw, slot0, a.epoch, &out);
+        if (r == DICT_FULL) {
+            a.keyid[p] = GNS_ID_NONE;
+            atomicAdd(&s_full, 1u);
+            continue;
+        }
+        if (r == DICT_FOUND) {
+            a.keyid[p] = out;
+        } else {
+            a.keyid[p] = GNS_ID_NONE;  // set by k_resolve
+            const uint32_t q = atomicAdd(&s_pend, 1u);
+            a.pend[beg + q] = (uint64_t)(p - beg) << 32 | out;
+        }
+        n_ok++;
+#pragma unroll
+        for (uint32_t rr = 0; rr < 8; rr++) {
+            if (rr >= a.g.d) break;
+            const uint32_t b = row_index(a.g, mm3_n<GNS_KWMAX>(kw, K, a.g.seeds[rr]));
+            a.idx[(uint64_t)rr * a.n + p] = b;
+            atomicAdd(&s_hist[rr * a.g.ntiles + (b >> a.g.tile_bits)], 1u);
+        }
+    }
+    atomicAdd(&s_ok, n_ok);
+    __syncthreads();
+    for (uint32_t i = tid; i < a.g.nbins; i += kExThreads) a.hist[(uint64_t)i * a.nblk + blk] = s_hist[i];
+    if (tid == 0) {
+        a.pend_cnt[blk] = s_pend;
+        if (s_pend) atomicAdd(a.pend_total, s_pend);
+        if (s_ok) atomicAdd(&a.stats[0], (unsigned long long)s_ok);
+        if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
+        if (s_unsup) atomicAdd(&a.stats[2], (unsigned long long)s_unsup);
+        if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+    }
+}
+
+struct ResolveArgs {
+    InputDesc in;
+    uint64_t n;
+    KeyPlanN kp;
+    DictDev D;
+    uint32_t epoch;
+    uint32_t *keyid;
+    const uint64_t *pend_in;
+    const uint32_t *cnt_in;
+    uint64_t *pend_out;
+    uint32_t *cnt_out;
+    uint32_t *total_out;
+    unsigned long long *stats;
+};
+
+// K1b: packets parked on a slot claimed in the previous launch.
+template <int KIND, int MODE>
+__global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
+    __shared__ uint32_t s_cnt, s_full;
+    __shared__ uint8_t s_src[80];
+    const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    stage_plan<MODE>(a.kp, s_src);
+    if (tid == 0) { s_cnt = 0; s_full = 0; }
+    __syncthreads();
+    const uint32_t cnt = a.cnt_in[blk];
+    const uint64_t beg = (uint64_t)blk * kChunk;
+    for (uint32_t i = tid; i < cnt; i += kExThreads) {
+        const uint64_t v = a.pend_in[beg + i];
+        const uint64_t p = beg + (v >> 32);
+        uint32_t kw[GNS_KWMAX];
+        (void)packet_key<KIND, MODE>(a.in, a.kp.K, s_src, p, kw);
+        uint32_t out;
+        const int r = dict_find_or_claim(a.D, kw, (uint32_t)v, a.epoch, &out);
+        if (r == DICT_FOUND) {
+            a.keyid[p] = out;
+        } else if (r == DICT_PENDING) {
+            const uint32_t q = atomicAdd(&s_cnt, 1u);
+            a.pend_out[beg + q] = (v & 0xFFFFFFFF00000000ull) | out;
+        } else {
+            atomicAdd(&s_full, 1u);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.cnt_out[blk] = s_cnt;
+        if (s_cnt) atomicAdd(a.total_out, s_cnt);
+        if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2: exclusive scan (three phases) of hist[nbins*nblk] in place.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= (uint32_t)o) v += t;
+    }
+    return v;
+}
+
+// block (256 threads) exclusive scan; returns exclusive prefix, *total = sum
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *s_w, uint32_t *total) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; w++) {
+        const uint32_t x = s_w[w];
+        if (w < wave) base += x;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t *x, uint64_t N, uint32_t *part) {
+    __shared__ uint32_t s_w[4];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanSeg;
+    uint32_t sum = 0;
+    for (uint32_t i = threadIdx.x; i < kScanSeg; i += 256)
+        if (base + i < N) sum += x[base + i];
+    uint32_t tot;
+    (void)block_excl_scan256(sum, s_w, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_scan_parts(uint32_t *part, uint32_t nseg, uint32_t *total) {
+    __shared__ uint32_t s_w[4];
+    // each thread scans a contiguous run of ceil(nseg/256) parts
+    const uint32_t per = (nseg + 255) / 256;
+    const uint32_t b0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t i = 0; i < per; i++)
+        if (b0 + i < nseg) sum += part[b0 + i];
+    uint32_t tot;
+    uint32_t run = block_excl_scan256(sum, s_w, &tot);
+    for (uint32_t i = 0; i < per; i++)
+        if (b0 + i < nseg) { const uint32_t v = part[b0 + i]; part[b0 + i] = run; run += v; }
+    if (threadIdx.x == 0) *total = tot;
+}
+
+__global__ __launch_bounds__(256) void k_scan_down(uint32_t *x, uint64_t N, const uint32_t *part) {
+    __shared__ uint32_t s_w[4];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanSeg;
+    constexpr uint32_t per = kScanSeg / 256;  // 16 contiguous per thread
+    const uint64_t t0 = base + threadIdx.x * per;
+    uint32_t v[per];
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < per; i++) { v[i] = (t0 + i < N) ? x[t0 + i] : 0u; sum += v[i]; }
+    uint32_t tot;
+    uint32_t run = block_excl_scan256(sum, s_w, &tot) + part[blockIdx.x];
+#pragma unroll
+    for (uint32_t i = 0; i < per; i++)
+        if (t0 + i < N) { x[t0 + i] = run; run += v[i]; }
+}
+
+// ---------------------------------------------------------------------------
+// K3: stable partition of row r's bucket updates into its tile bins.
+// Entry (u64): lo = flow id (or kOvfFlag|ovf slot), hi = size<<12 | bucket&(tile-1)
+// ---------------------------------------------------------------------------
+struct ScatterArgs {
+    uint64_t n;
+    CmGeom g;
+    const uint32_t *keyid;
+    const uint32_t *idx;
+    const uint32_t *sizes;
+    const uint32_t *offsets;  // scanned hist
+    uint32_t nblk;
+    uint64_t *entries;
+    uint64_t *ovf;
+    uint32_t *ovf_cnt;
+    unsigned long long *stats;
+};
+
+__global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
+    __shared__ uint32_t s_cnt[4][kMaxTilesPerRow];   // per-wave running counts (this round)
+    __shared__ uint32_t s_rstart[kMaxTilesPerRow];
+    __shared__ uint32_t s_goff[kMaxTilesPerRow];
+    __shared__ uint64_t s_ent[kScRound];
+    __shared__ uint32_t s_pos[kScRound];
+    __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_total;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t blk = blockIdx.x, r = blockIdx.y;
+    const uint32_t NT = a.g.ntiles;
+    const uint32_t tmask = (1u << a.g.tile_bits) - 1u;
+    for (uint32_t t = tid; t < NT; t += kScThreads) {
+        s_goff[t] = a.offsets[(uint64_t)(r * NT + t) * a.nblk + blk];
+        s_cnt[0][t] = 0; s_cnt[1][t] = 0; s_cnt[2][t] = 0; s_cnt[3][t] = 0;
+    }
+    const uint64_t beg = (uint64_t)blk * kChunk;
+    const uint64_t end = min(a.n, beg + kChunk);
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint64_t rb = beg; rb < end; rb += kScRound) {
+        __syncthreads();
+        uint64_t ent[kScItems];
+        uint32_t tile[kScItems], rank[kScItems];
+        // phase 1: per-wave stable ranks (order: slot i, then lane)
+#pragma unroll
+        for (int i = 0; i < kScItems; i++) {
+            const uint64_t p = rb + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
+            bool valid = false;
+            uint32_t t = 0;
+            uint64_t e = 0;
+            if (p < end) {
+                const uint32_t id = a.keyid[p];
+                if (id != GNS_ID_NONE) {
+                    valid = true;
+                    const uint32_t b = a.idx[(uint64_t)r * a.n + p];
+                    t = b >> a.g.tile_bits;
+                    const uint32_t sz = a.sizes[p];
+                    uint32_t lo = id, sf = sz;
+                    if (sz >= kSizeEsc) {
+                        const uint32_t q = atomicAdd(a.ovf_cnt, 1u);
+                        if (q < kOvfCap) {
+                            a.ovf[q] = (uint64_t)sz << 32 | id;
+                            lo = kOvfFlag | q;
+                        } else {
+                            atomicAdd(&a.stats[4], 1ull);
+                            lo = kOvfFlag | (kOvfCap - 1);
+                        }
+                        sf = kSizeEsc;
+                    }
+                    e = (uint64_t)((sf << 12) | (b & tmask)) << 32 | lo;
+                }
+            }
+            uint64_t peers = __ballot(valid);
+            for (uint32_t bit = 0; bit < a.g.nbits; bit++) {
+                const uint64_t m = __ballot(valid && ((t >> bit) & 1u));
+                peers &= ((t >> bit) & 1u) ? m : ~m;
+            }
+            uint32_t rk = 0;
+            if (valid) {
+                const uint32_t before = __popcll(peers & lt_mask);
+                rk = s_cnt[wave][t] + before;
+                if (before == 0) s_cnt[wave][t] += __popcll(peers);
+            }
+            ent[i] = e;
+            tile[i] = valid ? t : 0xFFFFFFFFu;
+            rank[i] = rk;
+        }
+        __syncthreads();
+        // phase 2: wave prefix per tile, then block scan over tiles
+        constexpr uint32_t TPT = kMaxTilesPerRow / kScThreads;  // 4 tiles per thread
+        uint32_t tot[TPT];
+        uint32_t lsum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < TPT; j++) {
+            const uint32_t t = tid * TPT + j;
+            uint32_t c = 0;
+            if (t < NT) {
+                const uint32_t c0 = s_cnt[0][t], c1 = s_cnt[1][t], c2 = s_cnt[2][t], c3 = s_cnt[3][t];
+                s_cnt[0][t] = 0; s_cnt[1][t] = c0; s_cnt[2][t] = c0 + c1; s_cnt[3][t] = c0 + c1 + c2;
+                c = c0 + c1 + c2 + c3;
+            }
+            tot[j] = c;
+            lsum += c;
+        }
+        uint32_t rtotal;
+        uint32_t run = block_excl_scan256(lsum, s_w, &rtotal);
+#pragma unroll
+        for (uint32_t j = 0; j < TPT; j++) {
+            const uint32_t t = tid * TPT + j;
+            if (t < NT) s_rstart[t] = run;
+            run += tot[j];
+        }
+        if (tid == 0) s_total = rtotal;
+        __syncthreads();
+        // phase 3: stage in bin order
+#pragma unroll
+        for (int i = 0; i < kScItems; i++) {
+            if (tile[i] != 0xFFFFFFFFu) {
+                const uint32_t t = tile[i];
+                const uint32_t within = s_cnt[wave][t] + rank[i];
+                const uint32_t l = s_rstart[t] + within;
+                s_ent[l] = ent[i];
+                s_pos[l] = s_goff[t] + within;
+            }
+        }
+        __syncthreads();
+        // phase 4: contiguous runs per bin to global
+        const uint32_t tot_r = s_total;
+        for (uint32_t s = tid; s < tot_r; s += kScThreads) a.entries[s_pos[s]] = s_ent[s];
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < TPT; j++) {
+            const uint32_t t = tid * TPT + j;
+            if (t < NT) {
+                s_goff[t] += tot[j];
+                s_cnt[0][t] = 0; s_cnt[1][t] = 0; s_cnt[2][t] = 0; s_cnt[3][t] = 0;
+            }
+        }
+    }
+}
+
+// Order bins by size (largest first) so the heavy bins start first.
+__global__ __launch_bounds__(1024) void k_order(const uint32_t *offsets, uint32_t nblk, uint32_t nbins,
+                                                const uint32_t *total, uint32_t *order) {
+    __shared__ uint32_t s_sz[4096];
+    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
+        const uint32_t s0 = offsets[(uint64_t)b * nblk];
+        const uint32_t s1 = (b + 1 < nbins) ? offsets[(uint64_t)(b + 1) * nblk] : *total;
+        s_sz[b] = s1 - s0;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
+        const uint32_t mine = s_sz[b];
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < nbins; j++) {
+            const uint32_t o = s_sz[j];
+            rank += (o > mine) || (o == mine && j < b);
+        }
+        order[rank] = b;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K4: apply one bin's updates to its LDS-resident tile, in stream order.
+// ---------------------------------------------------------------------------
+struct ApplyArgs {
+    const uint64_t *entries;
+    const uint32_t *offsets;
+    uint32_t nblk, nbins;
+    const uint32_t *total;
+    const uint32_t *order;
+    const uint64_t *ovf;
+    CmGeom g;
+    uint32_t *C, *Fc, *S, *Fs;
+};
+
+constexpr uint64_t kM21 = (1ull << 21) - 1;
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
+    __shared__ uint32_t sC[kTileMax], sFc[kTileMax], sS[kTileMax], sFs[kTileMax];
+    __shared__ unsigned long long accN[kTileMax];  // n | n_oth_c<<21 | n_oth_s<<42 | force<<63
+    __shared__ unsigned long long accS[kTileMax];  // sum_own | sum_oth<<32 ; replay owner words
+    __shared__ uint16_t s_list[kApChunk];
+    __shared__ uint32_t s_wc[kApItems * 16];
+    __shared__ uint32_t s_any, s_nlist;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const CmGeom &g = a.g;
+    const uint32_t bin = a.order ? a.order[blockIdx.x] : blockIdx.x;
+    const uint32_t beg = a.offsets[(uint64_t)bin * a.nblk];
+    const uint32_t end = (bin + 1 < a.nbins) ? a.offsets[(uint64_t)(bin + 1) * a.nblk] : *a.total;
+    if (beg >= end) return;
+    const uint32_t r = bin / g.ntiles, t = bin % g.ntiles;
+    const uint32_t tbase = t << g.tile_bits;
+    const uint32_t tn = min(1u << g.tile_bits, g.w - tbase);
+    const uint64_t cbase = (uint64_t)r * g.w + tbase;
+    for (uint32_t i = tid; i < tn; i += kApThreads) {
+        sC[i] = a.C[cbase + i]; sFc[i] = a.Fc[cbase + i];
+        sS[i] = a.S[cbase + i]; sFs[i] = a.Fs[cbase + i];
+        accN[i] = 0; accS[i] = 0;
+    }
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t *own = reinterpret_cast<uint32_t *>(accS);  // replay: lowest-lane arbitration
+    for (uint32_t cb = beg; cb < end; cb += kApChunk) {
+        if (tid == 0) s_any = 0;
+        __syncthreads();
+        uint64_t e[kApItems];
+        bool v[kApItems];
+        // --- classify against the chunk-entry state, aggregate per bucket ---
+#pragma unroll
+        for (int j = 0; j < kApItems; j++) {
+            const uint32_t q = cb + j * kApThreads + tid;
+            v[j] = q < end;
+            e[j] = v[j] ? a.entries[q] : 0ull;
+            const uint32_t lo = (uint32_t)e[j];
+            const uint32_t hi = (uint32_t)(e[j] >> 32);
+            const uint32_t b = hi & (kTileMax - 1u);
+            const bool ovf = (lo & kOvfFlag) != 0;
+            uint64_t incN = 0, incS = 0;
+            if (v[j] && !ovf) {
+                const uint32_t s = hi >> 12;
+                const bool oc = lo != sFc[b], os = lo != sFs[b];
+                incN = 1ull | (uint64_t)oc << 21 | (uint64_t)os << 42;
+                incS = os ? (uint64_t)s << 32 : (uint64_t)s;
+            }
+            // heavy bins: most lanes of a wave hit one bucket -> one LDS atomic
+            const uint32_t b0 = __builtin_amdgcn_readfirstlane(b);
+            const bool m0 = v[j] && !ovf && b == b0;
+            const uint64_t mm = __ballot(m0);
+            if (__popcll(mm) >= 16) {
+                const uint64_t sN = wave_sum64(m0 ? incN : 0ull);
+                const uint64_t sS_ = wave_sum64(m0 ? incS : 0ull);
+                if (lane == (uint32_t)__ffsll((long long)mm) - 1) {
+                    atomicAdd(&accN[b0], (unsigned long long)sN);
+                    atomicAdd(&accS[b0], (unsigned long long)sS_);
+                }
+                if (v[j] && !ovf && !m0) {
+                    atomicAdd(&accN[b], (unsigned long long)incN);
+                    atomicAdd(&accS[b], (unsigned long long)incS);
+                }
+            } else if (v[j] && !ovf) {
+                atomicAdd(&accN[b], (unsigned long long)incN);
+                atomicAdd(&accS[b], (unsigned long long)incS);
+            }
+            if (v[j] && ovf) {  // size >= 2^20-1: always replayed
+                atomicAdd(&accN[b], 1ull);
+                atomicOr(&accN[b], 1ull << 63);
+            }
+        }
+        __syncthreads();
+        // --- per bucket: exact aggregate update or mark for replay ---
+        for (uint32_t i = tid; i < tn; i += kApThreads) {
+            const uint64_t an = accN[i];
+            if (!an) continue;
+            const uint32_t n = (uint32_t)(an & kM21);
+            const uint32_t noc = (uint32_t)((an >> 21) & kM21);
+            const uint32_t nos = (uint32_t)((an >> 42) & kM21);
+            const bool force = (an >> 63) != 0;
+            const uint64_t as = accS[i];
+            const uint32_t so = (uint32_t)as, sx = (uint32_t)(as >> 32);
+            uint32_t rep = 0;
+            if (!force) {
+                // count half: C > n_oth keeps C >= 2 before every foreign packet
+                // (count_min.go:145-151 never reaches 0) and no wrap.
+                const uint32_t C = sC[i];
+                const uint32_t nown = n - noc;
+                if (C > noc && (uint64_t)C + nown < (1ull << 32)) sC[i] = C + nown - noc;
+                else rep |= 1u;
+                // size half: all-own is pure addition (:109-114, u32 wrap ok);
+                // otherwise S > sum_oth keeps S > s before every foreign packet
+                // (:115-125 never replaces) and no wrap.
+                const uint32_t S = sS[i];
+                if (nos == 0) sS[i] = S + so;
+                else if (S > sx && (uint64_t)S + so < (1ull << 32)) sS[i] = S + so - sx;
+                else rep |= 2u;
+            } else {
+                rep = 3u;
+            }
+            accS[i] = 0;
+            accN[i] = rep;
+            if (rep) s_any = 1;
+        }
+        __syncthreads();
+        if (s_any) {
+            // --- stable compaction of the updates that need replay ---
+            bool need[kApItems];
+            uint64_t bal[kApItems];
+#pragma unroll
+            for (int j = 0; j < kApItems; j++) {
+                const uint32_t b = (uint32_t)(e[j] >> 32) & (kTileMax - 1u);
+                need[j] = v[j] && accN[b] != 0;
+                bal[j] = __ballot(need[j]);
+                if (lane == 0) s_wc[j * 16 + wave] = __popcll(bal[j]);
+            }
+            __syncthreads();
+            if (wave == 0) {
+                const uint32_t x = s_wc[lane];
+                const uint32_t inc = wave_incl_scan(x);
+                s_wc[lane] = inc - x;
+                if (lane == 63) s_nlist = inc;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kApItems; j++)
+                if (need[j]) s_list[s_wc[j * 16 + wave] + __popcll(bal[j] & lt_mask)] = (uint16_t)(j * kApThreads + tid);
+            __syncthreads();
+            const uint32_t nlist = s_nlist;
+            // --- sequential replay (count_min.go:180-235) by wave 0, in order;
+            //     lanes of one 64-item group hitting distinct buckets run in
+            //     parallel, same-bucket lanes in lane order ---
+            if (wave == 0) {
+                for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
+                    const uint32_t i = g0 + lane;
+                    bool pending = i < nlist;
+                    uint32_t b = 0, k = 0, s = 0, rf = 0;
+                    if (pending) {
+                        const uint64_t ee = a.entries[cb + s_list[i]];
+                        const uint32_t lo = (uint32_t)ee, hi = (uint32_t)(ee >> 32);
+                        b = hi & (kTileMax - 1u);
+                        if (lo & kOvfFlag) {
+                            const uint64_t ov = a.ovf[lo & ~kOvfFlag];
+                            k = (uint32_t)ov; s = (uint32_t)(ov >> 32);
+                        } else {
+                            k = lo; s = hi >> 12;
+                        }
+                        rf = (uint32_t)accN[b];
+                    }
+                    while (__ballot(pending)) {
+                        if (pending) atomicMax(&own[b], 64u - lane);
+                        const bool win = pending && own[b] == 64u - lane;
+                        if (win) {
+                            if (rf & 2u) {  // size half, count_min.go:181-209
+                                uint32_t S = sS[b], F = sFs[b];
+                                if (S == 0) { S = s; F = k; }
+                                else if (F == k) S = S + s;
+                                else if (s > S) { S = s; F = k; }
+                                else S = S - s;
+                                sS[b] = S; sFs[b] = F;
+                            }
+                            if (rf & 1u) {  // count half, count_min.go:211-235
+                                uint32_t C = sC[b], F = sFc[b];
+                                if (C == 0) { C = 1; F = k; }
+                                else if (F == k) C = C + 1;
+                                else { C = C - 1; if (C == 0) F = k; }
+                                sC[b] = C; sFc[b] = F;
+                            }
+                            own[b] = 0;
+                            pending = false;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            for (uint32_t i = tid; i < nlist; i += kApThreads) {
+                const uint32_t pos = s_list[i];
+                const uint32_t b = (uint32_t)(a.entries[cb + pos] >> 32) & (kTileMax - 1u);
+                accN[b] = 0;
+            }
+        }
+        __syncthreads();
+    }
+    for (uint32_t i = tid; i < tn; i += kApThreads) {
+        a.C[cbase + i] = sC[i]; a.Fc[cbase + i] = sFc[i];
+        a.S[cbase + i] = sS[i]; a.Fs[cbase + i] = sFs[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Query (count_min.go:240-254), export, heavy-hitter candidates
+// ---------------------------------------------------------------------------
+struct QueryArgs {
+    const uint8_t *keys;
+    uint32_t stride, aligned;
+    uint64_t n;
+    uint32_t K;
+    CmGeom g;
+    DictDev D;
+    const uint32_t *C, *Fc, *S, *Fs;
+    uint64_t *out;
+};
+
+__global__ __launch_bounds__(256) void k_query(QueryArgs a) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= a.n) return;
+    uint32_t kw[GNS_KWMAX];
+    load_key_bytes<GNS_KWMAX>(a.keys + p * a.stride, a.K, a.aligned != 0, kw);
+    const uint32_t id = dict_lookup(a.D, kw);
+    uint32_t sz = 0, ct = 0;
+    if (id != GNS_ID_NONE) {
+        for (uint32_t rr = 0; rr < a.g.d; rr++) {
+            const uint64_t c = (uint64_t)rr * a.g.w + row_index(a.g, mm3_n<GNS_KWMAX>(kw, a.K, a.g.seeds[rr]));
+            if (a.Fs[c] == id) sz = max(sz, a.S[c]);
+            if (a.Fc[c] == id) ct = max(ct, a.C[c]);
+        }
+    }
+    a.out[p] = (uint64_t)ct << 32 | sz;
+}
+
+// flow ids -> key bytes (GNS_ID_NONE -> zero bytes, the reference's reset FP)
+__global__ __launch_bounds__(256) void k_ids_to_bytes(const uint32_t *ids, uint64_t n, DictDev D,
+                                                      uint8_t *out) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t id = ids[p];
+    uint32_t r[12];
+    if (id != GNS_ID_NONE) load_record(D, id, r);
+    for (uint32_t j = 0; j < D.K; j++) {
+        const uint32_t w = id != GNS_ID_NONE ? r[1 + (j >> 2)] : 0u;
+        out[p * D.K + j] = (uint8_t)(w >> (8 * (j & 3)));
+    }
+}
+
+// cells whose counter >= thr -> (value<<32 | id) candidate list
+__global__ __launch_bounds__(256) void k_hh_candidates(const uint32_t *val, const uint32_t *fp,
+                                                       uint64_t cells, uint32_t thr,
+                                                       uint64_t *cand, uint32_t *ncand, uint32_t cap) {
+    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= cells) return;
+    const uint32_t v = val[c];
+    if (v > 0 && v >= thr) {
+        const uint32_t q = atomicAdd(ncand, 1u);
+        if (q < cap) cand[q] = (uint64_t)v << 32 | fp[c];
+    }
+}
+
+__global__ void k_fill_u32(uint32_t *p, uint64_t n, uint32_t v) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+
+}  // namespace gns
+
+// ===========================================================================
+// Host side
+// ===========================================================================
+using namespace gns;
+
+struct gns_cm {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    CmGeom g{};
+    KeyPlanN kp{};
+    uint32_t K = 0, st = 0, ct = 0;
+    uint32_t *C = nullptr, *S = nullptr, *Fc = nullptr, *Fs = nullptr;
+    DictDev D{};
+    uint64_t dict_slots = 0;
+    uint32_t epoch = 0;
+    uint64_t bmax = 0;
+    uint32_t nblk_max = 0;
+    uint32_t *keyid = nullptr, *idx = nullptr;
+    uint64_t *pend[2] = {nullptr, nullptr};
+    uint32_t *pcnt[2] = {nullptr, nullptr};
+    uint32_t *ptotal = nullptr;        // [2]
+    uint32_t *hist = nullptr, *part = nullptr, *total = nullptr, *order = nullptr;
+    uint64_t *entries = nullptr;
+    uint64_t *ovf = nullptr;
+    uint32_t *ovf_cnt = nullptr;
+    unsigned long long *stats = nullptr;  // [8]
+    uint32_t *h_pin = nullptr;            // pinned host mirror of small counters
+    // staging for host inputs
+    uint8_t *stage = nullptr;
+    size_t stage_bytes = 0;
+    StageTimer timer;
+};
+
+namespace {
+
+int stage_reserve(gns_cm *cm, size_t bytes) {
+    if (cm->stage_bytes >= bytes) return GNS_OK;
+    dfree(cm->stage);
+    cm->stage = nullptr;
+    cm->stage_bytes = 0;
+    GNS_TRY(dalloc(reinterpret_cast<void **>(&cm->stage), bytes));
+    cm->stage_bytes = bytes;
+    return GNS_OK;
+}
+
+int set_dev(gns_cm *cm) {
+    GNS_HIP(hipSetDevice(cm->device));
+    return GNS_OK;
+}
+
+int cm_free_all(gns_cm *cm) {
+    dfree(cm->C); dfree(cm->S); dfree(cm->Fc); dfree(cm->Fs);
+    dfree(cm->D.rec);
+    dfree(cm->keyid); dfree(cm->idx);
+    dfree(cm->pend[0]); dfree(cm->pend[1]); dfree(cm->pcnt[0]); dfree(cm->pcnt[1]);
+    dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
+    dfree(cm->entries); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats); dfree(cm->stage);
+    if (cm->h_pin) (void)hipHostFree(cm->h_pin);
+    cm->timer.destroy();
+    if (cm->stream) (void)hipStreamDestroy(cm->stream);
+    return GNS_OK;
+}
+
+int cm_reset_state(gns_cm *cm) {
+    const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
+    GNS_HIP(hipMemsetAsync(cm->C, 0, cells * 4, cm->stream));
+    GNS_HIP(hipMemsetAsync(cm->S, 0, cells * 4, cm->stream));
+    GNS_HIP(hipMemsetAsync(cm->Fc, 0xFF, cells * 4, cm->stream));
+    GNS_HIP(hipMemsetAsync(cm->Fs, 0xFF, cells * 4, cm->stream));
+    GNS_HIP(hipMemsetAsync(cm->D.rec, 0, cm->dict_slots * cm->D.RW * 4, cm->stream));
+    return GNS_OK;
+}
+
+// One device batch: n <= bmax packets, inputs already device-resident.
+template <int KIND, int MODE>
+int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
+    if (n == 0) return GNS_OK;
+    hipStream_t s = cm->stream;
+    const uint32_t nblk = (uint32_t)((n + kChunk - 1) / kChunk);
+    const CmGeom &g = cm->g;
+    ScopedStage total_stage(cm->timer, 5);
+    // K1
+    GNS_HIP(hipMemsetAsync(cm->ptotal, 0, 8, s));
+    if (++cm->epoch == 0) cm->epoch = 1;
+    {
+        ExtractArgs a{};
+        a.in = in; a.n = n; a.kp = cm->kp; a.g = g; a.D = cm->D; a.epoch = cm->epoch;
+        a.keyid = cm->keyid; a.idx = cm->idx; a.pend = cm->pend[0]; a.pend_cnt = cm->pcnt[0];
+        a.pend_total = cm->ptotal; a.hist = cm->hist; a.nblk = nblk; a.stats = cm->stats;
+        ScopedStage st(cm->timer, 0);
+        hipLaunchKernelGGL((k_extract<KIND, MODE>), dim3(nblk), dim3(kExThreads), g.nbins * 4, s, a);
+        GNS_HIP(hipGetLastError());
+    }
+    // K1b: resolve parked packets until none remain
+    int cur = 0;
+    for (int round = 0;; round++) {
+        GNS_HIP(hipMemcpyAsync(cm->h_pin, cm->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
+        GNS_HIP(hipMemcpyAsync(cm->h_pin + 2, cm->stats + 3, 8, hipMemcpyDeviceToHost, s));
+        GNS_HIP(hipStreamSynchronize(s));
+        if (cm->h_pin[2] | cm->h_pin[3]) {
+            set_error("flow dictionary full (%llu slots); raise max_flows",
+                      (unsigned long long)cm->dict_slots);
+            return GNS_E_FULL;
+        }
+        if (cm->h_pin[0] == 0) break;
+        if (round > 64) { set_error("dictionary resolve did not converge"); return GNS_E_FULL; }
+        GNS_HIP(hipMemsetAsync(cm->ptotal + (cur ^ 1), 0, 4, s));
+        if (++cm->epoch == 0) cm->epoch = 1;
+        ResolveArgs a{};
+        a.in = in; a.n = n; a.kp = cm->kp; a.D = cm->D; a.epoch = cm->epoch; a.keyid = cm->keyid;
+        a.pend_in = cm->pend[cur]; a.cnt_in = cm->pcnt[cur];
+        a.pend_out = cm->pend[cur ^ 1]; a.cnt_out = cm->pcnt[cur ^ 1]; a.total_out = cm->ptotal + (cur ^ 1);
+        a.stats = cm->stats;
+        ScopedStage st(cm->timer, 1);
+        hipLaunchKernelGGL((k_resolve<KIND, MODE>), dim3(nblk), dim3(kExThreads), 0, s, a);
+        GNS_HIP(hipGetLastError());
+        cur ^= 1;
+    }
+    // K2
+    const uint64_t N = (uint64_t)g.nbins * nblk;
+    const uint32_t nseg = (uint32_t)((N + kScanSeg - 1) / kScanSeg);
+    {
+        ScopedStage st(cm->timer, 2);
+        hipLaunchKernelGGL(k_scan_reduce, dim3(nseg), dim3(256), 0, s, cm->hist, N, cm->part);
+        hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(256), 0, s, cm->part, nseg, cm->total);
+        hipLaunchKernelGGL(k_scan_down, dim3(nseg), dim3(256), 0, s, cm->hist, N, cm->part);
+        GNS_HIP(hipGetLastError());
+    }
+    // K3
+    GNS_HIP(hipMemsetAsync(cm->ovf_cnt, 0, 4, s));
+    {
+        ScatterArgs a{};
+        a.n = n; a.g = g; a.keyid = cm->keyid; a.idx = cm->idx; a.sizes = in.sizes;
+        a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
+        a.ovf_cnt = cm->ovf_cnt; a.stats = cm->stats;
+        ScopedStage st(cm->timer, 3);
+        hipLaunchKernelGGL(k_scatter, dim3(nblk, g.d), dim3(kScThreads), 0, s, a);
+        GNS_HIP(hipGetLastError());
+    }
+    // K4
+    {
+        const bool ordered = g.nbins <= 4096;
+        if (ordered)
+            hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, s, cm->hist, nblk, g.nbins, cm->total, cm->order);
+        ApplyArgs a{};
+        a.entries = cm->entries; a.offsets = cm->hist; a.nblk = nblk; a.nbins = g.nbins;
+        a.total = cm->total; a.order = ordered ? cm->order : nullptr; a.ovf = cm->ovf; a.g = g;
+        a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs;
+        ScopedStage st(cm->timer, 4);
+        hipLaunchKernelGGL(k_apply, dim3(g.nbins), dim3(kApThreads), 0, s, a);
+        GNS_HIP(hipGetLastError());
+    }
+    return GNS_OK;
+}
+
+template <int KIND>
+int cm_insert(gns_cm *cm, InputDesc in, uint64_t n, gns_mem where) {
+    GNS_TRY(set_dev(cm));
+    for (uint64_t off = 0; off < n; off += cm->bmax) {
+        const uint64_t m = std::min<uint64_t>(cm->bmax, n - off);
+        InputDesc d = in;
+        if (where == GNS_MEM_DEVICE) {
+            if (d.hdr) d.hdr += off * 16;
+            if (d.src16) d.src16 += off * 16;
+            if (d.dst16) d.dst16 += off * 16;
+            if (d.sport) d.sport += off;
+            if (d.dport) d.dport += off;
+            if (d.proto) d.proto += off;
+            if (d.keys) d.keys += off * d.stride;
+            if (d.sizes) d.sizes += off;
+        } else {
+            // stage host arrays into one device buffer (16-byte aligned pieces)
+            const void *src[7] = {in.hdr ? (const void *)(in.hdr + off * 16) : nullptr,
+                                  in.src16 ? (const void *)(in.src16 + off * 16) : nullptr,
+                                  in.dst16 ? (const void *)(in.dst16 + off * 16) : nullptr,
+                                  in.sport ? (const void *)(in.sport + off) : nullptr,
+                                  in.dport ? (const void *)(in.dport + off) : nullptr,
+                                  in.proto ? (const void *)(in.proto + off) : nullptr,
+                                  in.keys ? (const void *)(in.keys + off * in.stride) : nullptr};
+            size_t bytes[7] = {in.hdr ? m * 64 : 0, in.src16 ? m * 16 : 0, in.dst16 ? m * 16 : 0,
+                               in.sport ? m * 2 : 0, in.dport ? m * 2 : 0, in.proto ? m : 0,
+                               in.keys ? m * in.stride : 0};
+            size_t tot = 0;
+            for (int i = 0; i < 7; i++) tot += (bytes[i] + 15) & ~size_t(15);
+            tot += (m * 4 + 15) & ~size_t(15);
+            GNS_TRY(stage_reserve(cm, tot));
+            uint8_t *p = cm->stage;
+            const void **dst[7] = {(const void **)&d.hdr, (const void **)&d.src16, (const void **)&d.dst16,
+                                   (const void **)&d.sport, (const void **)&d.dport, (const void **)&d.proto,
+                                   (const void **)&d.keys};
+            for (int i = 0; i < 7; i++) {
+                if (!bytes[i]) continue;
+                GNS_HIP(hipMemcpyAsync(p, src[i], bytes[i], hipMemcpyHostToDevice, cm->stream));
+                *dst[i] = p;
+                p += (bytes[i] + 15) & ~size_t(15);
+            }
+            GNS_HIP(hipMemcpyAsync(p, in.sizes + off, m * 4, hipMemcpyHostToDevice, cm->stream));
+            d.sizes = reinterpret_cast<const uint32_t *>(p);
+            if (d.keys) d.aligned = (d.stride % 4 == 0 && d.stride >= ((cm->K + 3) & ~3u)) ? 1u : 0u;
+        }
+        if constexpr (KIND == IN_KEYS) {
+            GNS_TRY((cm_run_batch<KIND, PLAN_SLICE0>(cm, d, m)));
+        } else {
+            switch (plan_mode(cm->kp)) {
+            case PLAN_SLICE0: GNS_TRY((cm_run_batch<KIND, PLAN_SLICE0>(cm, d, m))); break;
+            case PLAN_SLICE4: GNS_TRY((cm_run_batch<KIND, PLAN_SLICE4>(cm, d, m))); break;
+            default: GNS_TRY((cm_run_batch<KIND, PLAN_GENERIC>(cm, d, m))); break;
+            }
+        }
+    }
+    return GNS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
+    if (!p || !out) { set_error("null argument"); return GNS_E_ARG; }
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device available");
+        return GNS_E_NODEV;
+    }
+    if (p->device < 0 || p->device >= ndev) { set_error("device %d out of range", p->device); return GNS_E_ARG; }
+    gns_cm *cm = new gns_cm();
+    cm->device = p->device;
+    int rc = GNS_OK;
+    do {
+        if ((rc = set_dev(cm)) != GNS_OK) break;
+        // count_min.go:128-140 defaults
+        CmGeom &g = cm->g;
+        g.w = p->width ? p->width : (1u << 20);
+        g.d = p->depth ? p->depth : 3u;
+        cm->st = p->size_threshold ? p->size_threshold : 512u * 1024u;
+        cm->ct = p->count_threshold ? p->count_threshold : 512u;
+        if (g.d > 8) { set_error("depth %u > 8 not supported", g.d); rc = GNS_E_ARG; break; }
+        if ((rc = make_plan(p->flow, p->key_bytes, &cm->kp)) != GNS_OK) break;
+        cm->K = cm->kp.K;
+        g.pow2 = (g.w & (g.w - 1)) == 0;
+        g.wmask = g.pow2 ? g.w - 1 : 0;
+        uint32_t tb = kTileBitsMax;
+        while (tb > 8 && (uint64_t)g.d * ((g.w + (1u << tb) - 1) >> tb) < 1024) tb--;
+        g.tile_bits = tb;
+        g.ntiles = (g.w + (1u << tb) - 1) >> tb;
+        if (g.ntiles > kMaxTilesPerRow) {
+            set_error("width %u needs %u tiles per row (max %u): widths above 2^22 not yet supported",
+                      g.w, g.ntiles, kMaxTilesPerRow);
+            rc = GNS_E_RANGE;
+            break;
+        }
+        g.nbins = g.d * g.ntiles;
+        g.nbits = ceil_log2(g.ntiles);
+        if (p->seeds) for (uint32_t i = 0; i < g.d; i++) g.seeds[i] = p->seeds[i];
+        else default_seeds(g.seeds, g.d);
+        if (hipStreamCreateWithFlags(&cm->stream, hipStreamNonBlocking) != hipSuccess) {
+            set_error("hipStreamCreate failed"); rc = GNS_E_HIP; break;
+        }
+        cm->timer.stream = cm->stream;
+        const uint64_t cells = (uint64_t)g.d * g.w;
+        if ((rc = dalloc_t(&cm->C, cells)) || (rc = dalloc_t(&cm->S, cells)) ||
+            (rc = dalloc_t(&cm->Fc, cells)) || (rc = dalloc_t(&cm->Fs, cells)))
+            break;
+        // flow dictionary: power of two >= 2 * max_flows
+        const uint64_t mf = p->max_flows ? p->max_flows : (4ull << 20);
+        uint64_t slots = 1;
+        while (slots < 2 * mf) slots <<= 1;
+        if (slots > (1ull << 30)) { set_error("max_flows too large"); rc = GNS_E_ARG; break; }
+        cm->dict_slots = slots;
+        cm->D.mask = (uint32_t)(slots - 1);
+        cm->D.K = cm->K;
+        cm->D.RW = ((1 + (cm->K + 3) / 4) + 3) & ~3u;
+        cm->D.seed = 0x2545F491u;
+        if ((rc = dalloc_t(&cm->D.rec, slots * cm->D.RW)) != GNS_OK) break;
+        // batch buffers
+        cm->bmax = p->batch_packets ? p->batch_packets : (16ull << 20);
+        cm->bmax = ((cm->bmax + kChunk - 1) / kChunk) * kChunk;
+        if (cm->bmax > (1ull << 31)) { set_error("batch_packets too large"); rc = GNS_E_ARG; break; }
+        cm->nblk_max = (uint32_t)(cm->bmax / kChunk);
+        const uint64_t nseg = ((uint64_t)g.nbins * cm->nblk_max + kScanSeg - 1) / kScanSeg;
+        if ((rc = dalloc_t(&cm->keyid, cm->bmax)) || (rc = dalloc_t(&cm->idx, cm->bmax * g.d)) ||
+            (rc = dalloc_t(&cm->pend[0], cm->bmax)) || (rc = dalloc_t(&cm->pend[1], cm->bmax)) ||
+            (rc = dalloc_t(&cm->pcnt[0], cm->nblk_max)) || (rc = dalloc_t(&cm->pcnt[1], cm->nblk_max)) ||
+            (rc = dalloc_t(&cm->ptotal, 2)) || (rc = dalloc_t(&cm->hist, (uint64_t)g.nbins * cm->nblk_max)) ||
+            (rc = dalloc_t(&cm->part, nseg + 1)) || (rc = dalloc_t(&cm->total, 1)) ||
+            (rc = dalloc_t(&cm->order, g.nbins)) || (rc = dalloc_t(&cm->entries, cm->bmax * g.d)) ||
+            (rc = dalloc_t(&cm->ovf, kOvfCap)) || (rc = dalloc_t(&cm->ovf_cnt, 1)) ||
+            (rc = dalloc_t(&cm->stats, 8)))
+            break;
+        if (hipHostMalloc(reinterpret_cast<void **>(&cm->h_pin), 64, 0) != hipSuccess) {
+            set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
+        }
+        if (hipMemsetAsync(cm->stats, 0, 64, cm->stream) != hipSuccess) { rc = GNS_E_HIP; break; }
+        if ((rc = cm_reset_state(cm)) != GNS_OK) break;
+        if (hipStreamSynchronize(cm->stream) != hipSuccess) { set_error("sync failed"); rc = GNS_E_HIP; break; }
+    } while (0);
+    if (rc != GNS_OK) {
+        cm_free_all(cm);
+        delete cm;
+        return rc;
+    }
+    *out = cm;
+    return GNS_OK;
+}
+
+int gns_cm_destroy(gns_cm *cm) {
+    if (!cm) return GNS_OK;
+    (void)hipSetDevice(cm->device);
+    if (cm->stream) (void)hipStreamSynchronize(cm->stream);
+    cm_free_all(cm);
+    delete cm;
+    return GNS_OK;
+}
+
+int gns_cm_insert_keys(gns_cm *cm, const uint8_t *keys, uint32_t stride, const uint32_t *sizes,
+                       uint64_t n, gns_mem where) {
+    if (!cm || (n && (!keys || !sizes))) { set_error("null argument"); return GNS_E_ARG; }
+    if (stride < cm->K) { set_error("stride %u < key_bytes %u", stride, cm->K); return GNS_E_ARG; }
+    InputDesc in{};
+    in.keys = keys; in.stride = stride; in.sizes = sizes;
+    in.aligned = (stride % 4 == 0 && (reinterpret_cast<uintptr_t>(keys) & 3) == 0 &&
+                  stride >= ((cm->K + 3) & ~3u)) ? 1u : 0u;
+    return cm_insert<IN_KEYS>(cm, in, n, where);
+}
+
+int gns_cm_insert_tuples(gns_cm *cm, const gns_tuples *t, uint64_t n, gns_mem where) {
+    if (!cm || !t) { set_error("null argument"); return GNS_E_ARG; }
+    if (n && (!t->src16 || !t->dst16 || !t->sport || !t->dport || !t->proto || !t->length)) {
+        set_error("null tuple array"); return GNS_E_ARG;
+    }
+    InputDesc in{};
+    in.src16 = t->src16; in.dst16 = t->dst16; in.sport = t->sport; in.dport = t->dport;
+    in.proto = t->proto; in.sizes = t->length;
+    return cm_insert<IN_TUPLE>(cm, in, n, where);
+}
+
+int gns_cm_insert_headers(gns_cm *cm, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
+                          gns_mem where) {
+    if (!cm || (n && (!hdr || !wirelen))) { set_error("null argument"); return GNS_E_ARG; }
+    InputDesc in{};
+    in.hdr = reinterpret_cast<const uint32_t *>(hdr);
+    in.sizes = wirelen;
+    return cm_insert<IN_HDR>(cm, in, n, where);
+}
+
+int gns_cm_flush(gns_cm *cm) {
+    if (!cm) return GNS_E_ARG;
+    GNS_TRY(set_dev(cm));
+    GNS_HIP(hipStreamSynchronize(cm->stream));
+    cm->timer.collect();
+    GNS_HIP(hipMemcpy(cm->h_pin, cm->stats + 4, 8, hipMemcpyDeviceToHost));
+    if (cm->h_pin[0] | cm->h_pin[1]) {
+        set_error("more than %u packets of size >= 2^20-1 in one batch", kOvfCap);
+        return GNS_E_RANGE;
+    }
+    return GNS_OK;
+}
+
+int gns_cm_query(gns_cm *cm, const uint8_t *keys, uint32_t stride, uint64_t n, uint64_t *out) {
+    if (!cm || (n && (!keys || !out))) { set_error("null argument"); return GNS_E_ARG; }
+    if (n == 0) return GNS_OK;
+    if (stride < cm->K) { set_error("stride < key_bytes"); return GNS_E_ARG; }
+    GNS_TRY(set_dev(cm));
+    uint8_t *dk = nullptr;
+    uint64_t *dout = nullptr;
+    GNS_TRY(dalloc(reinterpret_cast<void **>(&dk), n * stride));
+    int rc = dalloc(reinterpret_cast<void **>(&dout), n * 8);
+    if (rc != GNS_OK) { dfree(dk); return rc; }
+    QueryArgs a{};
+    a.keys = dk; a.stride = stride; a.aligned = (stride % 4 == 0 && stride >= ((cm->K + 3) & ~3u));
+    a.n = n; a.K = cm->K; a.g = cm->g; a.D = cm->D;
+    a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs; a.out = dout;
+    hipError_t e = hipMemcpyAsync(dk, keys, n * stride, hipMemcpyHostToDevice, cm->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_query, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, cm->stream, a);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, cm->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(cm->stream);
+    dfree(dk);
+    dfree(dout);
+    if (e != hipSuccess) { set_error("query: %s", hipGetErrorString(e)); return GNS_E_HIP; }
+    return GNS_OK;
+}
+
+static int cm_ids_to_host_bytes(gns_cm *cm, const uint32_t *d_ids, uint64_t n, uint8_t *host) {
+    if (n == 0 || cm->K == 0) return GNS_OK;
+    uint8_t *d = nullptr;
+    GNS_TRY(dalloc(reinterpret_cast<void **>(&d), n * cm->K));
+    hipLaunchKernelGGL(k_ids_to_bytes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, cm->stream,
+                       d_ids, n, cm->D, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(host, d, n * cm->K, hipMemcpyDeviceToHost, cm->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(cm->stream);
+    dfree(d);
+    if (e != hipSuccess) { set_error("ids_to_bytes: %s", hipGetErrorString(e)); return GNS_E_HIP; }
+    return GNS_OK;
+}
+
+int gns_cm_export_state(gns_cm *cm, uint32_t *C, uint32_t *S, uint8_t *FPc, uint8_t *FPs) {
+    if (!cm) return GNS_E_ARG;
+    GNS_TRY(set_dev(cm));
+    GNS_HIP(hipStreamSynchronize(cm->stream));
+    const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
+    if (C) GNS_HIP(hipMemcpy(C, cm->C, cells * 4, hipMemcpyDeviceToHost));
+    if (S) GNS_HIP(hipMemcpy(S, cm->S, cells * 4, hipMemcpyDeviceToHost));
+    if (FPc) GNS_TRY(cm_ids_to_host_bytes(cm, cm->Fc, cells, FPc));
+    if (FPs) GNS_TRY(cm_ids_to_host_bytes(cm, cm->Fs, cells, FPs));
+    return GNS_OK;
+}
+
+// HeavyHitters (count_min.go:259-327): a flow's max over its buckets reaches the
+// threshold iff one of its buckets does, so only cells >= threshold are
+// candidates; dedupe by fingerprint keeping the max; sort value desc.
+static int cm_heavy_one(gns_cm *cm, const uint32_t *val, const uint32_t *fp, uint32_t thr,
+                        uint8_t *flows, uint32_t *vals, uint64_t *n_io) {
+    const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
+    uint64_t *cand = nullptr;
+    uint32_t *ncand = nullptr;
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(cells, 1ull << 26);
+    GNS_TRY(dalloc(reinterpret_cast<void **>(&cand), (uint64_t)cap * 8));
+    int rc = dalloc(reinterpret_cast<void **>(&ncand), 16);
+    if (rc) { dfree(cand); return rc; }
+    std::vector<uint64_t> h;
+    uint32_t nc = 0;
+    hipError_t e = hipMemsetAsync(ncand, 0, 4, cm->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_hh_candidates, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, cm->stream,
+                           val, fp, cells, thr, cand, ncand, cap);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&nc, ncand, 4, hipMemcpyDeviceToHost, cm->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(cm->stream);
+    if (e == hipSuccess && nc) {
+        nc = std::min(nc, cap);
+        h.resize(nc);
+        e = hipMemcpy(h.data(), cand, (uint64_t)nc * 8, hipMemcpyDeviceToHost);
+    }
+    dfree(cand);
+    dfree(ncand);
+    if (e != hipSuccess) { set_error("heavy: %s", hipGetErrorString(e)); return GNS_E_HIP; }
+    // dedupe by id keeping max value
+    std::sort(h.begin(), h.end(), [](uint64_t a, uint64_t b) {
+        const uint32_t ia = (uint32_t)a, ib = (uint32_t)b;
+        return ia != ib ? ia < ib : (a >> 32) > (b >> 32);
+    });
+    std::vector<uint64_t> u;
+    for (size_t i = 0; i < h.size(); i++)
+        if (i == 0 || (uint32_t)h[i] != (uint32_t)h[i - 1]) u.push_back(h[i]);
+    // fetch key bytes for the unique ids
+    const uint32_t K = cm->K;
+    std::vector<uint32_t> ids(u.size());
+    for (size_t i = 0; i < u.size(); i++) ids[i] = (uint32_t)u[i];
+    std::vector<uint8_t> kb(u.size() * (K ? K : 1));
+    if (!u.empty() && K) {
+        uint32_t *dids = nullptr;
+        GNS_TRY(dalloc(reinterpret_cast<void **>(&dids), ids.size() * 4));
+        e = hipMemcpy(dids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice);
+        rc = e == hipSuccess ? cm_ids_to_host_bytes(cm, dids, ids.size(), kb.data()) : GNS_E_HIP;
+        dfree(dids);
+        if (rc) return rc;
+    }
+    std::vector<uint32_t> perm(u.size());
+    for (size_t i = 0; i < perm.size(); i++) perm[i] = (uint32_t)i;
+    std::sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) {
+        const uint32_t vx = (uint32_t)(u[x] >> 32), vy = (uint32_t)(u[y] >> 32);
+        if (vx != vy) return vx > vy;
+        return memcmp(&kb[(size_t)x * K], &kb[(size_t)y * K], K) < 0;
+    });
+    const uint64_t capn = *n_io;
+    for (size_t i = 0; i < perm.size() && i < capn; i++) {
+        if (flows && K) memcpy(flows + i * K, &kb[(size_t)perm[i] * K], K);
+        if (vals) vals[i] = (uint32_t)(u[perm[i]] >> 32);
+    }
+    *n_io = perm.size();
+    return GNS_OK;
+}
+
+int gns_cm_heavy_hitters(gns_cm *cm, uint8_t *count_flows, uint32_t *counts, uint64_t *n_count,
+                         uint8_t *size_flows, uint32_t *sizes, uint64_t *n_size) {
+    if (!cm || !n_count || !n_size) { set_error("null argument"); return GNS_E_ARG; }
+    GNS_TRY(set_dev(cm));
+    GNS_HIP(hipStreamSynchronize(cm->stream));
+    GNS_TRY(cm_heavy_one(cm, cm->C, cm->Fc, cm->ct, count_flows, counts, n_count));
+    GNS_TRY(cm_heavy_one(cm, cm->S, cm->Fs, cm->st, size_flows, sizes, n_size));
+    return GNS_OK;
+}
+
+int gns_cm_reset(gns_cm *cm) {
+    if (!cm) return GNS_E_ARG;
+    GNS_TRY(set_dev(cm));
+    GNS_TRY(cm_reset_state(cm));
+    GNS_HIP(hipStreamSynchronize(cm->stream));
+    return GNS_OK;
+}
+
+int gns_cm_stats(gns_cm *cm, uint64_t stats[4]) {
+    if (!cm || !stats) return GNS_E_ARG;
+    GNS_TRY(set_dev(cm));
+    GNS_HIP(hipStreamSynchronize(cm->stream));
+    unsigned long long h[8];
+    GNS_HIP(hipMemcpy(h, cm->stats, sizeof(h), hipMemcpyDeviceToHost));
+    stats[0] = h[0]; stats[1] = h[1]; stats[2] = h[2];
+    // distinct flows = occupied dictionary slots
+    std::vector<uint32_t> tags;
+    uint64_t occ = 0;
+    const uint64_t chunk = 1 << 20;
+    std::vector<uint32_t> buf;
+    for (uint64_t s0 = 0; s0 < cm->dict_slots; s0 += chunk) {
+        const uint64_t m = std::min(chunk, cm->dict_slots - s0);
+        buf.resize(m * cm->D.RW);
+        GNS_HIP(hipMemcpy(buf.data(), cm->D.rec + s0 * cm->D.RW, m * cm->D.RW * 4, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < m; i++) occ += buf[i * cm->D.RW] != 0;
+    }
+    stats[3] = occ;
+    return GNS_OK;
+}
+
+int gns_cm_set_timing(gns_cm *cm, int on) {
+    if (!cm) return GNS_E_ARG;
+    cm->timer.on = on != 0;
+    return GNS_OK;
+}
+
+int gns_cm_stage_times(gns_cm *cm, double ms[8], uint64_t launches[8], int reset) {
+    if (!cm) return GNS_E_ARG;
+    GNS_TRY(set_dev(cm));
+    cm->timer.collect();
+    for (int i = 0; i < 8; i++) {
+        if (ms) ms[i] = cm->timer.ms[i];
+        if (launches) launches[i] = cm->timer.launches[i];
+    }
+    if (reset) {
+        for (int i = 0; i < 8; i++) { cm->timer.ms[i] = 0; cm->timer.launches[i] = 0; }
+    }
+    return GNS_OK;
+}
+
+void *gns_cm_stream(gns_cm *cm) { return cm ? (void *)cm->stream : nullptr; }
+
+}  // extern "C"

@@ -1,0 +1,85 @@
+// gns_common.hpp -- host-side plumbing shared by the Count-Min and SuperSpread
+// engines: error reporting, device buffers, per-stage HIP-event timing, and
+// staging of host inputs into device memory.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gns_sketch.h"
+#include "gns_device.cuh"
+#include "gns_keys.cuh"
+
+namespace gns {
+
+void set_error(const char *fmt, ...);
+
+#define GNS_HIP(call)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            ::gns::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call,                \
+                             hipGetErrorString(e_));                                   \
+            return GNS_E_HIP;                                                          \
+        }                                                                              \
+    } while (0)
+
+#define GNS_TRY(expr)                  \
+    do {                               \
+        int r_ = (expr);               \
+        if (r_ != GNS_OK) return r_;   \
+    } while (0)
+
+// Device allocation that reports OOM as GNS_E_OOM.
+int dalloc(void **p, size_t bytes);
+template <class T>
+int dalloc_t(T **p, size_t count) {
+    return dalloc(reinterpret_cast<void **>(p), count * sizeof(T) + 16);
+}
+void dfree(void *p);
+
+// Flow-key plan from a configured layout (task.go:265-300, :327-338).
+int make_plan(const gns_layout &l, uint32_t key_bytes, KeyPlanN *out);
+// plan for the concatenation a ‖ b (SuperSpread merged key, super_spread.go:183-190)
+int make_plan2(const gns_layout &a, const gns_layout &b, KeyPlanN *out);
+uint32_t layout_bytes(const gns_layout &l);
+
+// Per-stage timing with HIP events recorded on the engine stream.
+struct StageTimer {
+    enum { kStages = 8 };
+    bool on = false;
+    double ms[kStages] = {};
+    uint64_t launches[kStages] = {};
+    std::vector<hipEvent_t> pool;
+    struct Pending { hipEvent_t a, b; int stage; };
+    std::vector<Pending> pending;
+    hipStream_t stream = nullptr;
+
+    hipEvent_t get();
+    void begin(int stage, hipEvent_t *a);
+    void end(int stage, hipEvent_t a);
+    int collect();  // synchronizes pending events and accumulates
+    void destroy();
+};
+
+struct ScopedStage {
+    StageTimer &t; int stage; hipEvent_t a = nullptr;
+    ScopedStage(StageTimer &tt, int s) : t(tt), stage(s) { t.begin(stage, &a); }
+    ~ScopedStage() { t.end(stage, a); }
+};
+
+// splitmix64 row seeds used when the caller passes none.
+void default_seeds(uint32_t *out, uint32_t n);
+
+inline uint32_t ceil_log2(uint64_t x) {
+    uint32_t b = 0;
+    while ((1ull << b) < x) b++;
+    return b;
+}
+
+}  // namespace gns

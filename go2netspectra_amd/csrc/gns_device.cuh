@@ -1,0 +1,199 @@
+// gns_device.cuh -- gfx950 device helpers for the sketch hot path.
+//
+//   * MurmurHash3_x86_32 over a key held in registers as little-endian u32 words
+//     (reference: internal/engine/impl/sketch/statistic/hash.go:13-53).
+//   * 64-byte header record -> canonical 5-tuple words
+//     (reference: internal/protocol/parser.go:23-67 over gopacket layers; the
+//     record contract is DESIGN.md "Header records").
+//   * flow-key assembly from the 5-tuple (reference: task.go:265-300).
+//
+// Canonical tuple words tw[10] (37 meaningful bytes, little-endian words):
+//   bytes  0..15  SrcIP slot  (IPv4 left-aligned, 12 zero bytes; task.go:281-286)
+//   bytes 16..31  DstIP slot
+//   bytes 32..33  SrcPort big-endian, 34..35 DstPort big-endian
+//   byte  36      Protocol
+// Every flow-key layout is a byte selection from this 37-byte string.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GNS_KWMAX 10        // ceil(37 / 4): longest key the reference allows (task.go:74)
+#define GNS_ID_NONE 0xFFFFFFFFu
+
+namespace gns {
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+// hash.go:13-53; key bytes k[0..K) packed little-endian in kw[], bytes >= K zero.
+__device__ __forceinline__ uint32_t mm3_words(const uint32_t (&kw)[GNS_KWMAX], uint32_t K,
+                                              uint32_t seed) {
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    uint32_t h = seed;
+    const uint32_t nb = K >> 2;
+#pragma unroll
+    for (int i = 0; i < GNS_KWMAX; i++) {
+        uint32_t k = kw[i];
+        if ((uint32_t)i < nb) {
+            k *= c1; k = rotl32(k, 15); k *= c2;
+            h ^= k; h = rotl32(h, 13); h = h * 5u + 0xe6546b64u;
+        } else if ((uint32_t)i == nb && (K & 3u)) {
+            k *= c1; k = rotl32(k, 15); k *= c2;
+            h ^= k;
+        }
+    }
+    h ^= K;
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
+}
+
+// ---------------------------------------------------------------------------
+// byte access into a 64-byte record held as 16 little-endian words
+// ---------------------------------------------------------------------------
+template <int B>
+__device__ __forceinline__ uint32_t rec_byte(const uint32_t (&w)[16]) {
+    static_assert(B >= 0 && B < 64, "record byte out of range");
+    return (w[B / 4] >> (8 * (B % 4))) & 0xFFu;
+}
+template <int B>
+__device__ __forceinline__ uint32_t rec_be16(const uint32_t (&w)[16]) {
+    return (rec_byte<B>(w) << 8) | rec_byte<B + 1>(w);
+}
+template <int B>
+__device__ __forceinline__ uint32_t rec_u32(const uint32_t (&w)[16]) {  // bytes B..B+3, LE
+    static_assert(B >= 0 && B + 3 < 64, "record word out of range");
+    if constexpr (B % 4 == 0) return w[B / 4];
+    else return (uint32_t)(((uint64_t)w[B / 4 + 1] << 32 | w[B / 4]) >> (8 * (B % 4)));
+}
+
+enum { PARSE_OK = 0, PARSE_DROP = 1, PARSE_UNSUPPORTED = 2 };
+
+__device__ __forceinline__ bool udp_tunnel_port(uint32_t p) {
+    return p == 4789u || p == 6081u || p == 2152u;
+}
+
+__device__ __forceinline__ void set_ports(uint32_t (&tw)[10], uint32_t sport, uint32_t dport,
+                                          uint32_t proto) {
+    // bytes 32..35 = sport BE, dport BE; byte 36 = proto
+    tw[8] = (sport >> 8) | ((sport & 0xFFu) << 8) | ((dport >> 8) << 16) | ((dport & 0xFFu) << 24);
+    tw[9] = proto;
+}
+
+// L3/L4 decode at L2 header length OFF (14 / 18 / 22 bytes).
+template <int OFF>
+__device__ __forceinline__ int parse_l3(const uint32_t (&w)[16], uint32_t type, uint32_t wirelen,
+                                        uint32_t (&tw)[10]) {
+    const uint32_t l2len = wirelen > (uint32_t)OFF ? wirelen - OFF : 0u;
+    if (type == 0x0800u) {  // gopacket IPv4.DecodeFromBytes
+        const uint32_t ihl = rec_byte<OFF>(w) & 15u;
+        uint32_t tot = rec_be16<OFF + 2>(w);
+        if (tot == 0) tot = l2len;  // TSO
+        if (ihl < 5) return PARSE_DROP;
+        if (ihl > 5) return PARSE_UNSUPPORTED;
+        if (tot < 20 || l2len < 20) return PARSE_DROP;
+        const uint32_t proto = rec_byte<OFF + 9>(w);
+        tw[0] = rec_u32<OFF + 12>(w);  // parser.go:40-41: 4-byte IPv4, left-aligned slot
+        tw[4] = rec_u32<OFF + 16>(w);
+        tw[9] = proto;
+        const uint32_t frag = rec_be16<OFF + 6>(w);
+        if (frag & 0x3FFFu) return PARSE_OK;  // MF or offset: LayerTypeFragment, ports 0
+        const uint32_t avail = (tot < l2len ? tot : l2len) - 20u;
+        if (proto == 6u) {
+            if (avail < 20) return PARSE_OK;
+            const uint32_t doff = rec_byte<OFF + 32>(w) >> 4;  // inside the record for OFF<=22
+            if (doff < 5 || doff * 4 > avail) return PARSE_OK;
+            set_ports(tw, rec_be16<OFF + 20>(w), rec_be16<OFF + 22>(w), proto);
+            return PARSE_OK;
+        }
+        if (proto == 17u) {
+            if (avail < 8) return PARSE_OK;
+            const uint32_t sp = rec_be16<OFF + 20>(w), dp = rec_be16<OFF + 22>(w);
+            if (udp_tunnel_port(sp) || udp_tunnel_port(dp)) return PARSE_UNSUPPORTED;
+            set_ports(tw, sp, dp, proto);
+            return PARSE_OK;
+        }
+        if (proto == 4u || proto == 41u || proto == 47u || proto == 51u || proto == 137u)
+            return PARSE_UNSUPPORTED;
+        return PARSE_OK;
+    }
+    if (type == 0x86DDu) {  // gopacket IPv6.DecodeFromBytes
+        if (l2len < 40) return PARSE_DROP;
+        const uint32_t plen = rec_be16<OFF + 4>(w);
+        const uint32_t nh = rec_byte<OFF + 6>(w);
+        if (plen == 0) return PARSE_UNSUPPORTED;
+        tw[0] = rec_u32<OFF + 8>(w);  tw[1] = rec_u32<OFF + 12>(w);
+        tw[2] = rec_u32<OFF + 16>(w); tw[3] = rec_u32<OFF + 20>(w);
+        tw[4] = rec_u32<OFF + 24>(w); tw[5] = rec_u32<OFF + 28>(w);
+        tw[6] = rec_u32<OFF + 32>(w); tw[7] = rec_u32<OFF + 36>(w);
+        tw[9] = nh;  // parser.go:47: first NextHeader
+        const uint32_t cap = l2len - 40u;
+        const uint32_t avail = plen < cap ? plen : cap;
+        switch (nh) {
+        case 0: case 43: case 44: case 51: case 60: case 135: case 139: case 140: case 253:
+        case 254: case 4: case 41: case 47: case 137:
+            return PARSE_UNSUPPORTED;
+        default: break;
+        }
+        if (nh == 6u || nh == 17u) {
+            if (avail < (nh == 6u ? 20u : 8u)) return PARSE_OK;
+            if constexpr (OFF + 40 + 4 > 64) {
+                return PARSE_UNSUPPORTED;  // ports beyond the record
+            } else {
+                const uint32_t sp = rec_be16<OFF + 40>(w), dp = rec_be16<OFF + 42>(w);
+                if constexpr (OFF + 40 + 12 < 64) {
+                    if (nh == 6u) {
+                        const uint32_t doff = rec_byte<OFF + 52>(w) >> 4;
+                        if (doff < 5 || doff * 4 > avail) return PARSE_OK;
+                    }
+                }
+                if (nh == 17u && (udp_tunnel_port(sp) || udp_tunnel_port(dp)))
+                    return PARSE_UNSUPPORTED;
+                set_ports(tw, sp, dp, nh);
+                return PARSE_OK;
+            }
+        }
+        return PARSE_OK;
+    }
+    switch (type) {  // parser.go:48-49 "not an IP packet"
+    case 0x0806: case 0x8035: case 0x88CC: case 0x8808: case 0x888E: case 0x88F7: case 0x8863:
+        return PARSE_DROP;
+    default:
+        return PARSE_UNSUPPORTED;
+    }
+}
+
+// 64-byte record -> canonical tuple words. Returns PARSE_*.
+__device__ __forceinline__ int parse_record(const uint32_t (&w)[16], uint32_t wirelen,
+                                            uint32_t (&tw)[10]) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) tw[i] = 0;
+    const uint32_t t0 = rec_be16<12>(w);
+    if (t0 == 0x88B5u) {  // pre-parsed record (host packer escape)
+        if (rec_byte<14>(w) != 1u) return PARSE_UNSUPPORTED;
+        tw[0] = w[4]; tw[1] = w[5]; tw[2] = w[6];  tw[3] = w[7];
+        tw[4] = w[8]; tw[5] = w[9]; tw[6] = w[10]; tw[7] = w[11];
+        set_ports(tw, rec_be16<48>(w), rec_be16<50>(w), rec_byte<52>(w));
+        return PARSE_OK;
+    }
+    if (t0 != 0x8100u && t0 != 0x88A8u) return parse_l3<14>(w, t0, wirelen, tw);
+    const uint32_t t1 = rec_be16<16>(w);
+    if (t1 != 0x8100u && t1 != 0x88A8u) return parse_l3<18>(w, t1, wirelen, tw);
+    const uint32_t t2 = rec_be16<20>(w);
+    if (t2 != 0x8100u && t2 != 0x88A8u) return parse_l3<22>(w, t2, wirelen, tw);
+    return PARSE_UNSUPPORTED;
+}
+
+// byte idx (0..36) of the canonical tuple; 255 (or >= 40) -> 0
+__device__ __forceinline__ uint32_t tuple_byte(const uint32_t (&tw)[10], uint32_t idx) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) w = ((idx >> 2) == (uint32_t)i) ? tw[i] : w;
+    return idx < 40u ? (w >> ((idx & 3u) * 8u)) & 0xFFu : 0u;
+}
+
+// mask of the bytes of word i that are < K
+__device__ __forceinline__ uint32_t tail_mask(uint32_t K, int i) {
+    const int rem = (int)K - 4 * i;
+    return rem >= 4 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << (8 * rem)) - 1u));
+}
+
+}  // namespace gns

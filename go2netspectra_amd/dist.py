@@ -1,0 +1,116 @@
+"""Multi-GPU sharding of the sketch path (one process per GPU, torch.distributed).
+
+Count-Min buckets are (fingerprint, counter) pairs under order-dependent
+majority-vote rules (count_min.go:180-235): they are NOT additive, so summing
+counter rows across GPUs (all-reduce) would not produce the sketch of the
+union stream.  The path therefore shards by flow: packets are routed to the
+GPU that owns their SrcIP (every flow of a source lands on one GPU, SURVEY.md
+§8e), each GPU runs an exact sketch of its sub-stream, queries go to the owner
+shard, and the only collective is the per-window all-gather of heavy-hitter
+candidates (flows are disjoint across shards, so the global list is a union).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .sketch import HeavyCount, HeavyRecord, HeavySize
+
+SHARD_SEED = 0xA5A5A5A5
+
+
+def _mm3_16(slots: np.ndarray, seed: int) -> np.ndarray:
+    """MurmurHash3_x86_32 of [n,16] uint8 rows (vectorised; hash.go:13-53)."""
+    c1, c2 = np.uint32(0xCC9E2D51), np.uint32(0x1B873593)
+    w = np.ascontiguousarray(slots, np.uint8).view("<u4").reshape(-1, 4)
+    h = np.full(w.shape[0], seed, np.uint32)
+    with np.errstate(over="ignore"):
+        for i in range(4):
+            k = w[:, i].astype(np.uint32) * c1
+            k = (k << np.uint32(15)) | (k >> np.uint32(17))
+            k = k * c2
+            h ^= k
+            h = (h << np.uint32(13)) | (h >> np.uint32(19))
+            h = h * np.uint32(5) + np.uint32(0xE6546B64)
+        h ^= np.uint32(16)
+        h ^= h >> np.uint32(16)
+        h = h * np.uint32(0x85EBCA6B)
+        h ^= h >> np.uint32(13)
+        h = h * np.uint32(0xC2B2AE35)
+        h ^= h >> np.uint32(16)
+    return h
+
+
+def shard_of(src16: np.ndarray, world: int) -> np.ndarray:
+    """Owner GPU of each packet: mm3(SrcIP slot, 0xA5A5A5A5) % world."""
+    if world <= 1:
+        return np.zeros(len(src16), np.int64)
+    return (_mm3_16(src16, SHARD_SEED) % np.uint32(world)).astype(np.int64)
+
+
+def split_batch(batch, world: int):
+    """Stable split of a host PacketBatch into per-shard batches (order kept)."""
+    from .packets import PacketBatch
+    owner = shard_of(np.asarray(batch.src16), world)
+    out = []
+    for g in range(world):
+        m = owner == g
+        out.append(PacketBatch(batch.src16[m], batch.dst16[m], batch.sport[m], batch.dport[m],
+                               batch.proto[m], batch.length[m]))
+    return out
+
+
+def _pack(items, K: int) -> np.ndarray:
+    buf = np.zeros((len(items), K + 4), np.uint8)
+    for i, (f, v) in enumerate(items):
+        buf[i, :K] = np.frombuffer(f, np.uint8)
+        buf[i, K:] = np.frombuffer(np.uint32(v).tobytes(), np.uint8)
+    return buf
+
+
+def _unpack(buf: np.ndarray, K: int):
+    return [(bytes(r[:K]), int(np.frombuffer(r[K:K + 4].tobytes(), np.uint32)[0])) for r in buf]
+
+
+def _allgather_rows(rows: np.ndarray, world: int) -> np.ndarray:
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    cap = max(int(x.item()) for x in ns)
+    width = rows.shape[1]
+    mine = torch.zeros((max(cap, 1), width), dtype=torch.uint8, device=dev)
+    if rows.shape[0]:
+        mine[: rows.shape[0]] = torch.from_numpy(rows).to(dev)
+    parts = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine)
+    out = [p[: int(c.item())].cpu().numpy() for p, c in zip(parts, ns)]
+    return np.concatenate(out, axis=0) if out else rows
+
+
+def merge_heavy(lists):
+    """Union of disjoint per-shard lists, max per flow, sorted value desc / flow asc."""
+    best = {}
+    for items in lists:
+        for f, v in items:
+            best[f] = max(best.get(f, 0), v)
+    return sorted(best.items(), key=lambda fv: (-fv[1], fv[0]))
+
+
+def allgather_heavy(hh: HeavyRecord, world: int) -> HeavyRecord:
+    """Per-window exchange: all-gather every shard's heavy hitters (RCCL on GPU)."""
+    K = len(hh.Count[0].Flow) if hh.Count else (len(hh.Size[0].Flow) if hh.Size else 0)
+    import torch
+    import torch.distributed as dist
+    kt = torch.tensor([K], dtype=torch.int64,
+                      device="cuda" if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+    K = int(kt.item())
+    cnt = _unpack(_allgather_rows(_pack([(h.Flow, h.Count) for h in hh.Count], K), world), K)
+    merged_c = merge_heavy([cnt])
+    if hh.Size is None:
+        return HeavyRecord(Size=None, Count=[HeavyCount(f, v) for f, v in merged_c])
+    sz = _unpack(_allgather_rows(_pack([(h.Flow, h.Size) for h in hh.Size], K), world), K)
+    merged_s = merge_heavy([sz])
+    return HeavyRecord(Size=[HeavySize(f, v) for f, v in merged_s], Count=[HeavyCount(f, v) for f, v in merged_c])

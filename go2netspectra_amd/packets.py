@@ -1,0 +1,176 @@
+"""Packet batches: the inputs of the sketch hot path.
+
+* PacketBatch -- model.PacketInfo (internal/model/packet.go:9-22) as SoA arrays,
+  the batched form of Task.ProcessPacket's argument.  IP addresses are stored
+  as the 16-byte slots EncodeFlow writes (task.go:281-286): IPv4 left-aligned
+  with 12 zero bytes, IPv6 as-is.
+* HeaderBatch -- 64-byte frame records + wire lengths, what the fused-parse
+  entry point consumes; read_pcap() builds one from a pcap file
+  (pkg/pcap/reader.go:35-49).
+* SyntheticTraffic -- the benchmark's Zipf 5-tuple stream,
+  generated on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import ipaddress
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+
+def ip_slot(ip) -> bytes:
+    """16-byte EncodeFlow slot of an address (bytes of len 4/16, str or ipaddress)."""
+    if isinstance(ip, str):
+        ip = ipaddress.ip_address(ip).packed
+    elif isinstance(ip, (ipaddress.IPv4Address, ipaddress.IPv6Address)):
+        ip = ip.packed
+    ip = bytes(ip)[:16]
+    return ip + bytes(16 - len(ip))
+
+
+@dataclass
+class PacketBatch:
+    src16: "np.ndarray"   # [n,16] uint8
+    dst16: "np.ndarray"   # [n,16] uint8
+    sport: "np.ndarray"   # [n] uint16
+    dport: "np.ndarray"   # [n] uint16
+    proto: "np.ndarray"   # [n] uint8
+    length: "np.ndarray"  # [n] uint32 (uint32(PacketInfo.Length), task.go:168)
+
+    def __len__(self) -> int:
+        return int(self.length.shape[0])
+
+    @classmethod
+    def from_packets(cls, packets) -> "PacketBatch":
+        """packets: iterable of (src, dst, sport, dport, proto, length)."""
+        rows = list(packets)
+        n = len(rows)
+        b = cls(np.zeros((n, 16), np.uint8), np.zeros((n, 16), np.uint8), np.zeros(n, np.uint16),
+                np.zeros(n, np.uint16), np.zeros(n, np.uint8), np.zeros(n, np.uint32))
+        for i, (s, d, sp, dp, pr, ln) in enumerate(rows):
+            b.src16[i] = np.frombuffer(ip_slot(s), np.uint8)
+            b.dst16[i] = np.frombuffer(ip_slot(d), np.uint8)
+            b.sport[i], b.dport[i], b.proto[i], b.length[i] = sp, dp, pr, ln & 0xFFFFFFFF
+        return b
+
+    def to(self, device):
+        """Copy to a torch device (device-resident batches skip the H2D stage)."""
+        import torch
+        f = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+        return PacketBatch(f(self.src16), f(self.dst16), f(self.sport.view(np.int16)),
+                           f(self.dport.view(np.int16)), f(self.proto), f(self.length.view(np.int32)))
+
+    def c_struct(self):
+        arrs = [self.src16, self.dst16, self.sport, self.dport, self.proto, self.length]
+        dev = [hasattr(a, "data_ptr") and getattr(a, "is_cuda", False) for a in arrs]
+        if all(dev):
+            t = _lib.Tuples(*[a.data_ptr() for a in arrs])
+            return t, arrs, _lib.MEM_DEVICE
+        if any(dev):
+            raise ValueError("mix of host and device arrays")
+        keep = [np.ascontiguousarray(a) for a in arrs]
+        t = _lib.Tuples(*[a.ctypes.data for a in keep])
+        return t, keep, _lib.MEM_HOST
+
+    def keys(self, fields) -> np.ndarray:
+        """EncodeFlow over the configured fields for every packet -> [n, K] uint8."""
+        parts = []
+        for f in fields:
+            if f == "SrcIP":
+                parts.append(np.asarray(self.src16, np.uint8))
+            elif f == "DstIP":
+                parts.append(np.asarray(self.dst16, np.uint8))
+            elif f == "SrcPort":
+                parts.append(np.asarray(self.sport, ">u2").view(np.uint8).reshape(-1, 2))
+            elif f == "DstPort":
+                parts.append(np.asarray(self.dport, ">u2").view(np.uint8).reshape(-1, 2))
+            elif f == "Protocol":
+                parts.append(np.asarray(self.proto, np.uint8).reshape(-1, 1))
+        if not parts:
+            return np.zeros((len(self), 0), np.uint8)
+        return np.ascontiguousarray(np.concatenate(parts, axis=1))
+
+
+@dataclass
+class HeaderBatch:
+    hdr: "np.ndarray"      # [n,64] uint8
+    wirelen: "np.ndarray"  # [n] uint32
+
+    def __len__(self) -> int:
+        return int(self.wirelen.shape[0])
+
+
+def read_pcap(path: str, limit: Optional[int] = None) -> HeaderBatch:
+    """pcap -> 64-byte records (C++ packer, one pass, no per-packet objects)."""
+    L = _lib.load()
+    total = ct.c_uint64(0)
+    if limit is None:
+        r = L.gns_pack_pcap(os.fsencode(path), None, None, 0, ct.byref(total))
+        if r < 0:
+            check(int(r))
+        limit = total.value
+    hdr = np.zeros((limit, 64), np.uint8)
+    wl = np.zeros(limit, np.uint32)
+    r = L.gns_pack_pcap(os.fsencode(path), hdr.ctypes.data, wl.ctypes.data, limit, ct.byref(total))
+    if r < 0:
+        check(int(r))
+    return HeaderBatch(hdr[:r], wl[:r])
+
+
+def write_pcap(path: str, frames, wirelens=None, snaplen: int = 65536) -> None:
+    """Classic little-endian pcap writer (tests / tools)."""
+    import struct
+    with open(path, "wb") as f:
+        f.write(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, snaplen, 1))
+        for i, fr in enumerate(frames):
+            fr = bytes(fr)
+            wl = len(fr) if wirelens is None else int(wirelens[i])
+            f.write(struct.pack("<IIII", i, 0, len(fr), wl))
+            f.write(fr)
+
+
+class SyntheticTraffic:
+    """Zipf 5-tuple header stream generated on the GPU (gns_synth_*)."""
+
+    def __init__(self, flows: int = 1 << 20, zipf_s: float = 1.1, shard: int = 0, nshards: int = 1,
+                 device: int = 0, tuple_seed: int = 0x5EED0001, rank_seed: int = 0x5EED0002,
+                 len_seed: int = 0x5EED0003):
+        self._L = _lib.load()
+        p = _lib.SynthParams(flows, zipf_s, tuple_seed, rank_seed, len_seed, shard, nshards, device)
+        h = ct.c_void_p()
+        check(self._L.gns_synth_create(ct.byref(p), ct.byref(h)))
+        self._h = h
+        self.device = device
+        nf = ct.c_uint32(0)
+        check(self._L.gns_synth_flows(self._h, ct.byref(nf)))
+        self.shard_flows = nf.value
+
+    def fill(self, hdr, wirelen, first: int = 0) -> None:
+        """Fill device tensors hdr[n,64] (uint8) and wirelen[n] (int32/uint32 view)."""
+        n = int(wirelen.shape[0])
+        check(self._L.gns_synth_fill(self._h, hdr.data_ptr(), wirelen.data_ptr(), first, n))
+
+    def generate(self, n: int, first: int = 0):
+        import torch
+        dev = torch.device("cuda", self.device)
+        hdr = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+        wl = torch.empty((n,), dtype=torch.int32, device=dev)
+        self.fill(hdr, wl, first)
+        return hdr, wl
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.gns_synth_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

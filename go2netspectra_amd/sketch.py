@@ -1,0 +1,357 @@
+"""statistic.Sketch mirror backed by the MI355X engine.
+
+Reference: internal/engine/impl/sketch/statistic/sketch.go:5-28
+    type Sketch interface {
+        Insert(flow, elem []byte, size uint32)
+        Query(flow []byte) uint64
+        HeavyHitters() HeavyRecord
+        Reset()
+    }
+
+CountMin (count_min.go) and SuperSpread (super_spread.go) keep those four
+methods (Go names kept as aliases) and add the batched entry points the GPU
+needs: insert_keys / insert_tuples / insert_headers take whole packet batches,
+host (numpy) or device-resident (torch tensors on the handle's GPU).
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+
+# --- sketch.go:13-28 -------------------------------------------------------
+@dataclass
+class HeavySize:
+    Flow: bytes
+    Size: int
+
+
+@dataclass
+class HeavyCount:
+    Flow: bytes
+    Count: int
+
+
+@dataclass
+class HeavyRecord:
+    """HeavyRecord{Size, Count}.  Size is None for SuperSpread (writers use
+    `Size is not None` to tell Count-Min from SuperSpread, writer_text.go:45-93)."""
+    Size: Optional[List[HeavySize]] = field(default_factory=list)
+    Count: List[HeavyCount] = field(default_factory=list)
+
+
+def _is_device(x) -> bool:
+    return hasattr(x, "data_ptr") and getattr(x, "is_cuda", False)
+
+
+def _ptr(x) -> int:
+    if _is_device(x):
+        if not x.is_contiguous():
+            raise ValueError("device tensors must be contiguous")
+        return x.data_ptr()
+    return x.ctypes.data
+
+
+def _host(x, dtype) -> np.ndarray:
+    return np.ascontiguousarray(x, dtype=dtype)
+
+
+def _where(*arrays) -> int:
+    dev = [_is_device(a) for a in arrays if a is not None]
+    if dev and all(dev):
+        return _lib.MEM_DEVICE
+    if any(dev):
+        raise ValueError("mix of host and device arrays in one call")
+    return _lib.MEM_HOST
+
+
+def _seeds_arg(seeds, depth):
+    if seeds is None:
+        return None, None
+    arr = np.ascontiguousarray(seeds, dtype=np.uint32)
+    if depth and arr.shape[0] < depth:
+        raise ValueError(f"need {depth} seeds, got {arr.shape[0]}")
+    return arr, arr.ctypes.data
+
+
+class CountMin:
+    """Fingerprinted majority-vote "CountMin" of count_min.go on one GPU.
+
+    Defaults mirror NewCountMin (count_min.go:128-140).  Row seeds are injected
+    (the reference draws them from math/rand/v2, count_min.go:142-145)."""
+
+    def __init__(self, width: int = 0, depth: int = 0, size_threshold: int = 0,
+                 count_threshold: int = 0, flow_fields: Optional[Sequence[str]] = None,
+                 key_bytes: Optional[int] = None, seeds=None, max_flows: int = 0,
+                 batch_packets: int = 0, device: int = 0):
+        self._L = _lib.load()
+        self.flow_fields = list(flow_fields or [])
+        kb = key_bytes if key_bytes is not None else _lib.layout_bytes(self.flow_fields)
+        p = _lib.CmParams()
+        p.width, p.depth = width, depth
+        p.size_threshold, p.count_threshold = size_threshold, count_threshold
+        p.flow = _lib.Layout.of(self.flow_fields)
+        p.key_bytes = kb
+        self._seeds, p.seeds = _seeds_arg(seeds, depth or 3)
+        p.max_flows, p.batch_packets, p.device = max_flows, batch_packets, device
+        h = ct.c_void_p()
+        check(self._L.gns_cm_create(ct.byref(p), ct.byref(h)))
+        self._h = h
+        self.width = width or (1 << 20)
+        self.depth = depth or 3
+        self.size_threshold = size_threshold or 512 * 1024
+        self.count_threshold = count_threshold or 512
+        self.key_bytes = kb
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.gns_cm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- batched inserts (stream order = call order, then array order) ---
+    def insert_keys(self, keys, sizes) -> None:
+        """Sketch.Insert for a batch: keys[n, stride] uint8 (first key_bytes used)."""
+        where = _where(keys, sizes)
+        if where == _lib.MEM_HOST:
+            keys = _host(keys, np.uint8).reshape(len(sizes), -1)
+            sizes = _host(sizes, np.uint32)
+        n = int(sizes.shape[0])
+        stride = int(keys.shape[1]) if n else max(self.key_bytes, 1)
+        check(self._L.gns_cm_insert_keys(self._h, _ptr(keys), stride, _ptr(sizes), n, where))
+
+    def insert_tuples(self, batch) -> None:
+        """Task.ProcessPacket for a PacketBatch (packets.PacketBatch)."""
+        t, keep, where = batch.c_struct()
+        check(self._L.gns_cm_insert_tuples(self._h, ct.byref(t), len(batch), where))
+        del keep
+
+    def insert_headers(self, hdr, wirelen) -> None:
+        """64-byte header records [n, 64] uint8 + wire lengths [n] uint32."""
+        where = _where(hdr, wirelen)
+        if where == _lib.MEM_HOST:
+            hdr = _host(hdr, np.uint8)
+            wirelen = _host(wirelen, np.uint32)
+        n = int(wirelen.shape[0])
+        check(self._L.gns_cm_insert_headers(self._h, _ptr(hdr), _ptr(wirelen), n, where))
+
+    def flush(self) -> None:
+        check(self._L.gns_cm_flush(self._h))
+
+    # --- statistic.Sketch ---
+    def insert(self, flow: bytes, elem: bytes = b"", size: int = 0) -> None:
+        """Insert(flow, elem, size); elem is unused by CountMin (count_min.go:175)."""
+        k = np.frombuffer(bytes(flow), dtype=np.uint8).reshape(1, -1)
+        self.insert_keys(k, np.array([size], dtype=np.uint32))
+
+    def query_many(self, keys) -> np.ndarray:
+        keys = _host(keys, np.uint8)
+        n = keys.shape[0]
+        out = np.zeros(n, dtype=np.uint64)
+        if n:
+            keys = keys.reshape(n, -1)
+            check(self._L.gns_cm_query(self._h, keys.ctypes.data, keys.shape[1], n, out.ctypes.data))
+        return out
+
+    def query(self, flow: bytes) -> int:
+        """Query(flow) = count<<32 | size (count_min.go:240-254)."""
+        if len(flow) != self.key_bytes:
+            return 0  # bytes.Equal against FS-byte fingerprints never matches
+        return int(self.query_many(np.frombuffer(bytes(flow), np.uint8).reshape(1, -1))[0])
+
+    def heavy_hitters(self) -> HeavyRecord:
+        nc, ns = ct.c_uint64(0), ct.c_uint64(0)
+        check(self._L.gns_cm_heavy_hitters(self._h, None, None, ct.byref(nc), None, None, ct.byref(ns)))
+        K = max(self.key_bytes, 1)
+        cf = np.zeros((max(nc.value, 1), K), np.uint8)
+        cv = np.zeros(max(nc.value, 1), np.uint32)
+        sf = np.zeros((max(ns.value, 1), K), np.uint8)
+        sv = np.zeros(max(ns.value, 1), np.uint32)
+        nc2, ns2 = ct.c_uint64(nc.value), ct.c_uint64(ns.value)
+        check(self._L.gns_cm_heavy_hitters(self._h, cf.ctypes.data, cv.ctypes.data, ct.byref(nc2),
+                                           sf.ctypes.data, sv.ctypes.data, ct.byref(ns2)))
+        kb = self.key_bytes
+        return HeavyRecord(
+            Size=[HeavySize(bytes(sf[i, :kb]), int(sv[i])) for i in range(min(ns.value, ns2.value))],
+            Count=[HeavyCount(bytes(cf[i, :kb]), int(cv[i])) for i in range(min(nc.value, nc2.value))])
+
+    def reset(self) -> None:
+        check(self._L.gns_cm_reset(self._h))
+
+    # Go-style names (statistic.Sketch)
+    Insert = insert
+    Query = query
+    HeavyHitters = heavy_hitters
+    Reset = reset
+
+    # --- parity / observability ---
+    def export_state(self):
+        n = self.depth * self.width
+        K = max(self.key_bytes, 1)
+        C = np.empty(n, np.uint32)
+        S = np.empty(n, np.uint32)
+        Fc = np.empty((n, K), np.uint8)
+        Fs = np.empty((n, K), np.uint8)
+        check(self._L.gns_cm_export_state(self._h, C.ctypes.data, S.ctypes.data, Fc.ctypes.data,
+                                          Fs.ctypes.data))
+        return C, S, Fc[:, : self.key_bytes], Fs[:, : self.key_bytes]
+
+    def stats(self) -> dict:
+        s = (ct.c_uint64 * 4)()
+        check(self._L.gns_cm_stats(self._h, s))
+        return {"inserted": s[0], "dropped": s[1], "unsupported": s[2], "flows": s[3]}
+
+    def set_timing(self, on: bool = True) -> None:
+        check(self._L.gns_cm_set_timing(self._h, 1 if on else 0))
+
+    STAGES = ["extract", "resolve", "scan", "scatter", "apply", "insert"]
+
+    def stage_times(self, reset: bool = False) -> dict:
+        ms = (ct.c_double * 8)()
+        ln = (ct.c_uint64 * 8)()
+        check(self._L.gns_cm_stage_times(self._h, ms, ln, 1 if reset else 0))
+        return {name: (ms[i], ln[i]) for i, name in enumerate(self.STAGES)}
+
+    def stream(self) -> int:
+        return int(self._L.gns_cm_stream(self._h) or 0)
+
+
+class SuperSpread:
+    """SuperSpread of super_spread.go on one GPU (declared RNG, injected HLL seeds)."""
+
+    def __init__(self, width: int = 0, depth: int = 0, threshold: int = 0, m: int = 0, size: int = 0,
+                 base: float = 0.0, b: float = 0.0, flow_fields: Optional[Sequence[str]] = None,
+                 elem_fields: Optional[Sequence[str]] = None, flow_bytes: Optional[int] = None,
+                 elem_bytes: Optional[int] = None, seeds=None, hll_master: int = 0x1234ABCD5678EF01,
+                 rng_seed: int = 0x0DDBA11CAFEF00D5, batch_packets: int = 0, device: int = 0):
+        self._L = _lib.load()
+        self.flow_fields = list(flow_fields or [])
+        self.elem_fields = list(elem_fields or [])
+        fb = flow_bytes if flow_bytes is not None else _lib.layout_bytes(self.flow_fields)
+        eb = elem_bytes if elem_bytes is not None else _lib.layout_bytes(self.elem_fields)
+        p = _lib.SsParams()
+        p.width, p.depth, p.threshold, p.m, p.size = width, depth, threshold, m, size
+        p.base, p.b = base, b
+        p.flow, p.elem = _lib.Layout.of(self.flow_fields), _lib.Layout.of(self.elem_fields)
+        p.flow_bytes, p.elem_bytes = fb, eb
+        self._seeds, p.seeds = _seeds_arg(seeds, depth or 3)
+        p.hll_master, p.rng_seed, p.batch_packets, p.device = hll_master, rng_seed, batch_packets, device
+        h = ct.c_void_p()
+        check(self._L.gns_ss_create(ct.byref(p), ct.byref(h)))
+        self._h = h
+        self.width, self.depth = width or (1 << 20), depth or 3
+        self.threshold, self.m = threshold or 4096, m or 128
+        self.flow_bytes, self.elem_bytes = fb, eb
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.gns_ss_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def insert_keys(self, flows, elems) -> None:
+        where = _where(flows, elems)
+        if where == _lib.MEM_HOST:
+            flows = _host(flows, np.uint8).reshape(len(flows), -1)
+            elems = _host(elems, np.uint8).reshape(len(elems), -1)
+        n = int(flows.shape[0])
+        fs = int(flows.shape[1]) if n else max(self.flow_bytes, 1)
+        es = int(elems.shape[1]) if n else max(self.elem_bytes, 1)
+        check(self._L.gns_ss_insert_keys(self._h, _ptr(flows), fs, _ptr(elems), es, n, where))
+
+    def insert_tuples(self, batch) -> None:
+        t, keep, where = batch.c_struct()
+        check(self._L.gns_ss_insert_tuples(self._h, ct.byref(t), len(batch), where))
+        del keep
+
+    def insert_headers(self, hdr, wirelen) -> None:
+        where = _where(hdr, wirelen)
+        if where == _lib.MEM_HOST:
+            hdr = _host(hdr, np.uint8)
+            wirelen = _host(wirelen, np.uint32)
+        check(self._L.gns_ss_insert_headers(self._h, _ptr(hdr), _ptr(wirelen), int(wirelen.shape[0]), where))
+
+    def flush(self) -> None:
+        check(self._L.gns_ss_flush(self._h))
+
+    def insert(self, flow: bytes, elem: bytes, size: int = 0) -> None:
+        self.insert_keys(np.frombuffer(bytes(flow), np.uint8).reshape(1, -1),
+                         np.frombuffer(bytes(elem), np.uint8).reshape(1, -1))
+
+    def query_many(self, flows) -> np.ndarray:
+        flows = _host(flows, np.uint8)
+        n = flows.shape[0]
+        out = np.zeros(n, dtype=np.uint64)
+        if n:
+            flows = flows.reshape(n, -1)
+            check(self._L.gns_ss_query(self._h, flows.ctypes.data, flows.shape[1], n, out.ctypes.data))
+        return out
+
+    def query(self, flow: bytes) -> int:
+        """max(1, spread estimate), super_spread.go:238-249."""
+        if len(flow) != self.flow_bytes:
+            return 1
+        return int(self.query_many(np.frombuffer(bytes(flow), np.uint8).reshape(1, -1))[0])
+
+    def heavy_hitters(self) -> HeavyRecord:
+        n = ct.c_uint64(0)
+        check(self._L.gns_ss_heavy_hitters(self._h, None, None, ct.byref(n)))
+        K = max(self.flow_bytes, 1)
+        f = np.zeros((max(n.value, 1), K), np.uint8)
+        v = np.zeros(max(n.value, 1), np.uint32)
+        n2 = ct.c_uint64(n.value)
+        check(self._L.gns_ss_heavy_hitters(self._h, f.ctypes.data, v.ctypes.data, ct.byref(n2)))
+        return HeavyRecord(Size=None, Count=[HeavyCount(bytes(f[i, : self.flow_bytes]), int(v[i]))
+                                             for i in range(min(n.value, n2.value))])
+
+    def reset(self) -> None:
+        check(self._L.gns_ss_reset(self._h))
+
+    Insert = insert
+    Query = query
+    HeavyHitters = heavy_hitters
+    Reset = reset
+
+    def export_state(self):
+        n = self.depth * self.width
+        values = np.empty(n, np.uint32)
+        keys = np.empty((n, max(self.flow_bytes, 1)), np.uint8)
+        regs = np.empty((n, self.m), np.uint8)
+        pbits = np.empty(n, np.float64)
+        check(self._L.gns_ss_export_state(self._h, values.ctypes.data, keys.ctypes.data, regs.ctypes.data,
+                                          pbits.ctypes.data))
+        return values, keys[:, : self.flow_bytes], regs, pbits
+
+    def stats(self) -> dict:
+        s = (ct.c_uint64 * 4)()
+        check(self._L.gns_ss_stats(self._h, s))
+        return {"inserted": s[0], "dropped": s[1], "unsupported": s[2], "encodes": s[3]}
+
+    def set_timing(self, on: bool = True) -> None:
+        check(self._L.gns_ss_set_timing(self._h, 1 if on else 0))
+
+    STAGES = ["extract", "candidates", "group", "replay", "apply", "insert"]
+
+    def stage_times(self, reset: bool = False) -> dict:
+        ms = (ct.c_double * 8)()
+        ln = (ct.c_uint64 * 8)()
+        check(self._L.gns_ss_stage_times(self._h, ms, ln, 1 if reset else 0))
+        return {name: (ms[i], ln[i]) for i, name in enumerate(self.STAGES)}

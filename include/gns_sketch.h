@@ -1,0 +1,205 @@
+/*
+ * gns_sketch.h -- C ABI of the MI355X sketch engine (libgns_sketch.so).
+ *
+ * Drop-in boundary for Go2NetSpectra's sketch hot path.  Each entry point names
+ * the reference interface it replaces (paths relative to the reference repo):
+ *
+ *   statistic.Sketch.Insert(flow, elem, size)  internal/engine/impl/sketch/statistic/sketch.go:6
+ *       -> gns_cm_insert_keys / gns_ss_insert_keys           (batched, stream-ordered)
+ *   sketch.Task.ProcessPacket(*PacketInfo)     internal/engine/impl/sketch/task.go:156-169
+ *       -> gns_cm_insert_tuples / gns_ss_insert_tuples       (EncodeFlow fused on device)
+ *   pcap.Reader.ReadPackets + ParsePacketInto  pkg/pcap/reader.go:35-49, internal/protocol/parser.go:23-67
+ *       -> gns_cm_insert_headers / gns_ss_insert_headers     (64-byte records, parse fused)
+ *   statistic.Sketch.Query(flow)               sketch.go:7; count_min.go:240-254; super_spread.go:238-249
+ *       -> gns_cm_query / gns_ss_query
+ *   statistic.Sketch.HeavyHitters()            sketch.go:8; count_min.go:259-327; super_spread.go:254-294
+ *       -> gns_cm_heavy_hitters / gns_ss_heavy_hitters
+ *   statistic.Sketch.Reset()                   sketch.go:9; count_min.go:330-346; super_spread.go:297-311
+ *       -> gns_cm_reset / gns_ss_reset
+ *   statistic.NewCountMin / NewSuperSpread     count_min.go:128-172; super_spread.go:127-179
+ *       -> gns_cm_create / gns_ss_create (seeds injected, see below)
+ *
+ * Rules:
+ *   - Every call returns GNS_OK (0) or a negative gns_status; gns_last_error()
+ *     returns the thread-local message of the last failure.
+ *   - Calls on one handle must be serialized by the caller (one goroutine per
+ *     handle).  Inserts are applied in call order, packets in array order:
+ *     the device state equals the reference sketch fed the same stream by ONE
+ *     worker (num_workers: 1) with the same seeds.
+ *   - Pointers flagged GNS_MEM_HOST are read before the call returns (the
+ *     caller keeps ownership).  GNS_MEM_DEVICE pointers must be device memory
+ *     of the handle's device and stay valid until gns_*_flush() returns.
+ *   - Flow keys are the reference EncodeFlow bytes (task.go:279-300): IP slots
+ *     of 16 bytes with IPv4 left-aligned and zero padded, ports big-endian,
+ *     protocol one byte; key_bytes <= 37 (task.go:74).
+ */
+#ifndef GNS_SKETCH_H
+#define GNS_SKETCH_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum gns_status {
+    GNS_OK = 0,
+    GNS_E_ARG = -1,    /* bad argument (log.Fatalf / panic sites in the reference) */
+    GNS_E_HIP = -2,    /* HIP runtime error */
+    GNS_E_OOM = -3,    /* device allocation failed */
+    GNS_E_FULL = -4,   /* flow dictionary capacity exhausted (raise max_flows) */
+    GNS_E_RANGE = -5,  /* batch exceeds an internal limit (see message) */
+    GNS_E_NODEV = -6   /* no usable HIP device */
+} gns_status;
+
+typedef enum gns_mem { GNS_MEM_HOST = 0, GNS_MEM_DEVICE = 1 } gns_mem;
+
+/* task.go:279-300 field names -> ids; fieldByteSize task.go:327-338 */
+typedef enum gns_field {
+    GNS_F_NONE = 0, GNS_F_SRCIP = 1, GNS_F_DSTIP = 2, GNS_F_SRCPORT = 3, GNS_F_DSTPORT = 4,
+    GNS_F_PROTO = 5
+} gns_field;
+
+typedef struct gns_layout {
+    uint32_t n_fields;
+    uint8_t fields[8]; /* gns_field, in configured order (SketchTaskDef.FlowFields) */
+} gns_layout;
+
+/* Pre-parsed packets: model.PacketInfo (internal/model/packet.go:9-22) as SoA.
+ * src16/dst16 hold the 16-byte slots exactly as EncodeFlow lays them out. */
+typedef struct gns_tuples {
+    const uint8_t *src16;   /* n*16 */
+    const uint8_t *dst16;   /* n*16 */
+    const uint16_t *sport;  /* n */
+    const uint16_t *dport;  /* n */
+    const uint8_t *proto;   /* n */
+    const uint32_t *length; /* n, uint32(PacketInfo.Length) (task.go:168) */
+} gns_tuples;
+
+/* ------------------------------------------------------------------ */
+/* Count-Min (count_min.go)                                           */
+/* ------------------------------------------------------------------ */
+typedef struct gns_cm gns_cm;
+
+typedef struct gns_cm_params {
+    uint32_t width, depth;                    /* 0 -> 2^20 / 3 (count_min.go:128-134) */
+    uint32_t size_threshold, count_threshold; /* 0 -> 512 KiB / 512 (count_min.go:135-140) */
+    gns_layout flow;                          /* flow key layout (for tuples/headers input) */
+    uint32_t key_bytes;                       /* FS; must equal the layout's byte size when
+                                                 n_fields > 0; used alone for keys input */
+    const uint32_t *seeds;                    /* depth row seeds (count_min.go:142-145 draws
+                                                 them with rand.Uint32; here injected).
+                                                 NULL -> splitmix64(0x9747B28C) stream */
+    uint64_t max_flows;                       /* distinct flows per measurement period
+                                                 (flow dictionary capacity); 0 -> 4M */
+    uint64_t batch_packets;                   /* device batch size; 0 -> 16M packets */
+    int device;                               /* HIP device ordinal */
+} gns_cm_params;
+
+int gns_cm_create(const gns_cm_params *p, gns_cm **out);
+int gns_cm_destroy(gns_cm *cm);
+/* statistic.Sketch.Insert batch: keys[n*stride] (first key_bytes used), sizes[n] */
+int gns_cm_insert_keys(gns_cm *cm, const uint8_t *keys, uint32_t stride, const uint32_t *sizes,
+                       uint64_t n, gns_mem where);
+/* Task.ProcessPacket batch over pre-parsed PacketInfo */
+int gns_cm_insert_tuples(gns_cm *cm, const gns_tuples *t, uint64_t n, gns_mem where);
+/* fused parse: hdr[n*64] = first 64 bytes of each frame (zero padded),
+ * wirelen[n] = capture orig_len (= PacketInfo.Length, parser.go:30-33).
+ * Records outside the fast-parse subset are skipped and counted
+ * (gns_cm_stats); the host packer (gns_pack_pcap) never emits them. */
+int gns_cm_insert_headers(gns_cm *cm, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
+                          gns_mem where);
+int gns_cm_flush(gns_cm *cm);
+/* out[i] = count<<32 | size, count_min.go:240-254 */
+int gns_cm_query(gns_cm *cm, const uint8_t *keys, uint32_t stride, uint64_t n, uint64_t *out);
+/* HeavyHitters, count_min.go:259-327.  Lists are sorted value-descending with
+ * ties broken by flow bytes ascending (the reference leaves ties unordered).
+ * On input *n_count / *n_size hold the capacities (entries); on output the
+ * full list lengths (call again with larger buffers if they exceed the
+ * capacities).  flows_* are n*key_bytes. */
+int gns_cm_heavy_hitters(gns_cm *cm, uint8_t *count_flows, uint32_t *counts, uint64_t *n_count,
+                         uint8_t *size_flows, uint32_t *sizes, uint64_t *n_size);
+int gns_cm_reset(gns_cm *cm);
+/* Full state for parity: C/S [depth*width], FPc/FPs [depth*width*key_bytes]
+ * (any pointer may be NULL). */
+int gns_cm_export_state(gns_cm *cm, uint32_t *C, uint32_t *S, uint8_t *FPc, uint8_t *FPs);
+/* stats[0]=packets inserted, [1]=records dropped (not IP), [2]=records outside
+ * the fast-parse subset, [3]=distinct flows in the dictionary */
+int gns_cm_stats(gns_cm *cm, uint64_t stats[4]);
+/* Per-stage device time (ms, HIP events on the handle's stream), accumulated
+ * since the last call with reset != 0.  Stages: 0 extract, 1 resolve, 2 scan,
+ * 3 scatter, 4 apply, 5 total insert.  Enabled by gns_cm_set_timing(cm, 1). */
+int gns_cm_set_timing(gns_cm *cm, int on);
+int gns_cm_stage_times(gns_cm *cm, double ms[8], uint64_t launches[8], int reset);
+void *gns_cm_stream(gns_cm *cm); /* hipStream_t the handle launches on */
+
+/* ------------------------------------------------------------------ */
+/* SuperSpread (super_spread.go)                                      */
+/* ------------------------------------------------------------------ */
+typedef struct gns_ss gns_ss;
+
+typedef struct gns_ss_params {
+    uint32_t width, depth, threshold;  /* 0 -> 2^20 / 3 / 4096 (super_spread.go:12-20) */
+    uint32_t m, size;                  /* 0 -> 128 / 5; size <= 8 */
+    double base, b;                    /* 0 -> 0.5 / 1.08 */
+    gns_layout flow, elem;             /* FlowFields / ElementFields */
+    uint32_t flow_bytes, elem_bytes;
+    const uint32_t *seeds;             /* depth row seeds (super_spread.go:175); NULL -> default */
+    uint64_t hll_master;               /* derives each GeneralHLL's seeds[0..1] */
+    uint64_t rng_seed;                 /* keys the declared generator replacing rand.Float64 */
+    uint64_t batch_packets;
+    int device;
+} gns_ss_params;
+
+int gns_ss_create(const gns_ss_params *p, gns_ss **out);
+int gns_ss_destroy(gns_ss *ss);
+int gns_ss_insert_keys(gns_ss *ss, const uint8_t *flows, uint32_t fstride, const uint8_t *elems,
+                       uint32_t estride, uint64_t n, gns_mem where);
+int gns_ss_insert_tuples(gns_ss *ss, const gns_tuples *t, uint64_t n, gns_mem where);
+int gns_ss_insert_headers(gns_ss *ss, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
+                          gns_mem where);
+int gns_ss_flush(gns_ss *ss);
+int gns_ss_query(gns_ss *ss, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out);
+int gns_ss_heavy_hitters(gns_ss *ss, uint8_t *flows, uint32_t *spreads, uint64_t *n);
+int gns_ss_reset(gns_ss *ss);
+/* values[d*w], keys[d*w*flow_bytes], regs[d*w*m] (u8), pbits[d*w] */
+int gns_ss_export_state(gns_ss *ss, uint32_t *values, uint8_t *keys, uint8_t *regs, double *pbits);
+int gns_ss_stats(gns_ss *ss, uint64_t stats[4]);
+int gns_ss_set_timing(gns_ss *ss, int on);
+int gns_ss_stage_times(gns_ss *ss, double ms[8], uint64_t launches[8], int reset);
+
+/* ------------------------------------------------------------------ */
+/* Inputs: synthetic traffic and the pcap packer           */
+/* ------------------------------------------------------------------ */
+typedef struct gns_synth gns_synth;
+typedef struct gns_synth_params {
+    uint32_t flows;        /* flow universe F (default 2^20) */
+    double zipf_s;         /* default 1.1 */
+    uint64_t tuple_seed;   /* default 0x5EED0001 */
+    uint64_t rank_seed;    /* default 0x5EED0002 */
+    uint64_t len_seed;     /* default 0x5EED0003 */
+    uint32_t shard, nshards; /* keep only flows whose src slot hashes to `shard` */
+    int device;
+} gns_synth_params;
+int gns_synth_create(const gns_synth_params *p, gns_synth **out);
+int gns_synth_destroy(gns_synth *s);
+/* Fill device buffers hdr[n*64], wirelen[n] with packets first..first+n-1 of
+ * the (shard's) stream.  Deterministic, counter-based. */
+int gns_synth_fill(gns_synth *s, uint8_t *hdr_dev, uint32_t *wirelen_dev, uint64_t first,
+                   uint64_t n);
+/* flow tuple of each shard-local flow (for tests): src16,dst16 [flows*16] etc */
+int gns_synth_flows(gns_synth *s, uint32_t *n_flows);
+
+/* pcap file -> 64-byte records + wirelen (pkg/pcap/reader.go:35-49).
+ * Returns the number of records written (<= cap) or a negative status;
+ * *total = packets in the file. */
+int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirelen, uint64_t cap,
+                      uint64_t *total);
+
+const char *gns_last_error(void);
+const char *gns_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,219 @@
+"""ctypes binding of the C oracle (TEST INFRASTRUCTURE / CPU BASELINE ONLY).
+
+Loads oracle/libgns_oracle.so (built by `make -C oracle` or __graft_entry__.build()).
+Product code in go2netspectra_amd/ must never import this module.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libgns_oracle.so")
+_lib = None
+
+FIELD_IDS = {"SrcIP": 1, "DstIP": 2, "SrcPort": 3, "DstPort": 4, "Protocol": 5}
+
+u8p = ct.POINTER(ct.c_uint8)
+u32p = ct.POINTER(ct.c_uint32)
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        build()
+    L = ct.CDLL(_LIB_PATH)
+    L.or_mm3.restype = ct.c_uint32
+    L.or_mm3.argtypes = [ct.c_void_p, ct.c_uint32, ct.c_uint32]
+    L.or_parse_hdr64_len.restype = ct.c_int
+    L.or_parse_hdr64_len.argtypes = [ct.c_void_p, ct.c_uint32, ct.c_void_p]
+    L.or_encode_key.restype = ct.c_uint32
+    L.or_encode_key.argtypes = [ct.c_void_p, ct.c_uint32, ct.c_void_p, ct.c_void_p]
+    L.or_cm_new.restype = ct.c_void_p
+    L.or_cm_new.argtypes = [ct.c_uint32] * 5 + [ct.c_void_p]
+    L.or_cm_free.argtypes = [ct.c_void_p]
+    L.or_cm_params.argtypes = [ct.c_void_p] + [ct.c_void_p] * 4
+    L.or_cm_insert.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_uint32]
+    L.or_cm_insert_batch.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_uint32, ct.c_void_p, ct.c_uint64]
+    L.or_cm_insert_hdr64.restype = ct.c_uint64
+    L.or_cm_insert_hdr64.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_uint64, ct.c_void_p,
+                                     ct.c_uint32]
+    L.or_cm_insert_hdr64_pool.restype = ct.c_uint64
+    L.or_cm_insert_hdr64_pool.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_uint64,
+                                          ct.c_void_p, ct.c_uint32, ct.c_int]
+    L.or_cm_query.restype = ct.c_uint64
+    L.or_cm_query.argtypes = [ct.c_void_p, ct.c_void_p]
+    L.or_cm_export.argtypes = [ct.c_void_p] + [ct.c_void_p] * 4
+    L.or_cm_import.argtypes = [ct.c_void_p] + [ct.c_void_p] * 4
+    L.or_cm_heavy.restype = ct.c_uint32
+    L.or_cm_heavy.argtypes = [ct.c_void_p, ct.c_int, ct.c_void_p, ct.c_void_p, ct.c_uint32]
+    L.or_cm_reset.argtypes = [ct.c_void_p]
+    L.or_ss_new.restype = ct.c_void_p
+    L.or_ss_new.argtypes = [ct.c_uint32] * 5 + [ct.c_double, ct.c_double, ct.c_uint32, ct.c_uint32,
+                                                ct.c_void_p, ct.c_uint64, ct.c_uint64]
+    L.or_ss_free.argtypes = [ct.c_void_p]
+    L.or_ss_insert.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_void_p]
+    L.or_ss_insert_batch.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_uint32, ct.c_void_p, ct.c_uint32,
+                                     ct.c_uint64]
+    L.or_ss_query.restype = ct.c_uint64
+    L.or_ss_query.argtypes = [ct.c_void_p, ct.c_void_p]
+    L.or_ss_heavy.restype = ct.c_uint32
+    L.or_ss_heavy.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_uint32]
+    L.or_ss_export.argtypes = [ct.c_void_p] + [ct.c_void_p] * 4
+    L.or_ss_reset.argtypes = [ct.c_void_p]
+    L.or_ss_packets.restype = ct.c_uint64
+    L.or_ss_packets.argtypes = [ct.c_void_p]
+    L.or_mix64.restype = ct.c_uint64
+    L.or_mix64.argtypes = [ct.c_uint64]
+    L.or_ss_uniform.restype = ct.c_double
+    L.or_ss_uniform.argtypes = [ct.c_uint64, ct.c_uint64, ct.c_uint32, ct.c_uint32]
+    L.or_go_pow.restype = ct.c_double
+    L.or_go_pow.argtypes = [ct.c_double, ct.c_double]
+    _lib = L
+    return L
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ct.c_void_p)
+
+
+def mm3(data: bytes, seed: int) -> int:
+    buf = (ct.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    return lib().or_mm3(buf, len(data), seed & 0xFFFFFFFF)
+
+
+class TupleRec(ct.Structure):
+    _fields_ = [("src", ct.c_uint8 * 16), ("dst", ct.c_uint8 * 16), ("sport", ct.c_uint16),
+                ("dport", ct.c_uint16), ("proto", ct.c_uint8), ("ipver", ct.c_uint8)]
+
+
+def parse_hdr64(rec: bytes, wirelen: int):
+    """-> (status, src16, dst16, sport, dport, proto)"""
+    assert len(rec) == 64
+    buf = (ct.c_uint8 * 64).from_buffer_copy(rec)
+    t = TupleRec()
+    st = lib().or_parse_hdr64_len(buf, wirelen & 0xFFFFFFFF, ct.byref(t))
+    return st, bytes(t.src), bytes(t.dst), t.sport, t.dport, t.proto
+
+
+def field_ids(fields) -> np.ndarray:
+    return np.array([FIELD_IDS.get(f, 0) for f in fields] or [0], dtype=np.uint8)
+
+
+class CountMin:
+    """Sequential oracle CountMin (count_min.go) over injected seeds."""
+
+    def __init__(self, width, depth, st, ct_, key_bytes, seeds):
+        self.L = lib()
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        self.h = self.L.or_cm_new(width, depth, st, ct_, key_bytes, _p(seeds))
+        w, d, s, c = (ct.c_uint32(), ct.c_uint32(), ct.c_uint32(), ct.c_uint32())
+        self.L.or_cm_params(self.h, ct.byref(w), ct.byref(d), ct.byref(s), ct.byref(c))
+        self.w, self.d, self.st, self.ct, self.K = w.value, d.value, s.value, c.value, key_bytes
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.or_cm_free(self.h)
+            self.h = None
+
+    def insert_keys(self, keys: np.ndarray, sizes: np.ndarray):
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        sizes = np.ascontiguousarray(sizes, dtype=np.uint32)
+        n = sizes.shape[0]
+        stride = keys.shape[1] if keys.ndim == 2 else self.K
+        self.L.or_cm_insert_batch(self.h, _p(keys), stride, _p(sizes), n)
+
+    def insert_hdr64(self, hdr: np.ndarray, wirelen: np.ndarray, fields) -> int:
+        hdr = np.ascontiguousarray(hdr, dtype=np.uint8)
+        wirelen = np.ascontiguousarray(wirelen, dtype=np.uint32)
+        f = field_ids(fields)
+        return self.L.or_cm_insert_hdr64(self.h, _p(hdr), _p(wirelen), wirelen.shape[0], _p(f), len(fields))
+
+    def insert_hdr64_pool(self, hdr, wirelen, fields, nthreads: int) -> int:
+        hdr = np.ascontiguousarray(hdr, dtype=np.uint8)
+        wirelen = np.ascontiguousarray(wirelen, dtype=np.uint32)
+        f = field_ids(fields)
+        return self.L.or_cm_insert_hdr64_pool(self.h, _p(hdr), _p(wirelen), wirelen.shape[0], _p(f),
+                                              len(fields), nthreads)
+
+    def query(self, key: bytes) -> int:
+        buf = (ct.c_uint8 * max(1, len(key))).from_buffer_copy(key or b"\0")
+        return self.L.or_cm_query(self.h, buf)
+
+    def export(self):
+        n = self.d * self.w
+        C = np.empty(n, np.uint32)
+        S = np.empty(n, np.uint32)
+        Fc = np.empty((n, max(self.K, 1)), np.uint8)
+        Fs = np.empty((n, max(self.K, 1)), np.uint8)
+        self.L.or_cm_export(self.h, _p(C), _p(S), _p(Fc), _p(Fs))
+        return C, S, Fc[:, : self.K], Fs[:, : self.K]
+
+    def heavy(self, which: str):
+        w = 0 if which == "count" else 1
+        n = self.L.or_cm_heavy(self.h, w, None, None, 0)
+        flows = np.empty((max(n, 1), max(self.K, 1)), np.uint8)
+        vals = np.empty(max(n, 1), np.uint32)
+        self.L.or_cm_heavy(self.h, w, _p(flows), _p(vals), n)
+        return [(bytes(flows[i, : self.K]), int(vals[i])) for i in range(n)]
+
+    def reset(self):
+        self.L.or_cm_reset(self.h)
+
+
+class SuperSpread:
+    def __init__(self, width, depth, threshold, m, size, base, b, kf, ke, seeds, hll_master, rng_seed):
+        self.L = lib()
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        self.h = self.L.or_ss_new(width, depth, threshold, m, size, base, b, kf, ke, _p(seeds),
+                                  hll_master, rng_seed)
+        if not self.h:
+            raise ValueError("bad SuperSpread parameters")
+        self.w = width or (1 << 20)
+        self.d = depth or 3
+        self.m = m or 128
+        self.kf, self.ke = kf, ke
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.or_ss_free(self.h)
+            self.h = None
+
+    def insert(self, flows: np.ndarray, elems: np.ndarray):
+        flows = np.ascontiguousarray(flows, dtype=np.uint8)
+        elems = np.ascontiguousarray(elems, dtype=np.uint8)
+        n = flows.shape[0]
+        self.L.or_ss_insert_batch(self.h, _p(flows), self.kf, _p(elems), self.ke, n)
+
+    def query(self, flow: bytes) -> int:
+        buf = (ct.c_uint8 * max(1, len(flow))).from_buffer_copy(flow or b"\0")
+        return self.L.or_ss_query(self.h, buf)
+
+    def heavy(self):
+        n = self.L.or_ss_heavy(self.h, None, None, 0)
+        flows = np.empty((max(n, 1), max(self.kf, 1)), np.uint8)
+        vals = np.empty(max(n, 1), np.uint32)
+        self.L.or_ss_heavy(self.h, _p(flows), _p(vals), n)
+        return [(bytes(flows[i, : self.kf]), int(vals[i])) for i in range(n)]
+
+    def export(self):
+        n = self.d * self.w
+        values = np.empty(n, np.uint32)
+        keys = np.empty((n, max(self.kf, 1)), np.uint8)
+        regs = np.empty((n, self.m), np.uint8)
+        pbits = np.empty(n, np.float64)
+        self.L.or_ss_export(self.h, _p(values), _p(keys), _p(regs), _p(pbits))
+        return values, keys[:, : self.kf], regs, pbits
+
+    def reset(self):
+        self.L.or_ss_reset(self.h)

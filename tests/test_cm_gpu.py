@@ -1,0 +1,148 @@
+"""Count-Min parity on the GPU: every test compares the device state exported
+through the C ABI with the sequential C oracle fed the same stream
+(bit-exact: C, S and both fingerprint arrays)."""
+import numpy as np
+import pytest
+
+from helpers import frames_from_tuples, random_tuples, sizes_u32, zipf_keys
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_same_state(cm, orc):
+    C, S, Fc, Fs = cm.export_state()
+    oC, oS, oFc, oFs = orc.export()
+    for name, a, b in (("C", C, oC), ("S", S, oS), ("FPc", Fc, oFc), ("FPs", Fs, oFs)):
+        if not np.array_equal(a, b):
+            bad = np.nonzero(a != b)[0] if a.ndim == 1 else np.nonzero((a != b).any(axis=1))[0]
+            raise AssertionError(f"{name} differs in {len(bad)} cells, first {bad[:5]}: "
+                                 f"gpu={a[bad[:3]]} oracle={b[bad[:3]]}")
+
+
+def make_pair(oracle, w, d, K, st=1000, ct=10, seed=1, **kw):
+    from go2netspectra_amd import CountMin
+    seeds = np.random.default_rng(seed).integers(0, 2**32, d, dtype=np.uint64).astype(np.uint32)
+    cm = CountMin(w, d, st, ct, key_bytes=K, seeds=seeds, **kw)
+    orc = oracle.CountMin(w, d, st, ct, K, seeds)
+    return cm, orc
+
+
+@pytest.mark.parametrize("w,d,K,nflows,n,batch", [
+    (256, 2, 16, 2000, 100_000, 0),        # heavy collisions: replay path
+    (65536, 4, 37, 50_000, 1_000_000, 0),  # C1 geometry
+    (1000, 3, 13, 5000, 200_000, 0),       # non power-of-two width, odd key
+    (1, 1, 4, 50, 60_000, 0),              # every packet in one bucket
+    (4096, 2, 16, 3000, 300_000, 32768),   # multi-batch (state carried across batches)
+    (1 << 20, 4, 37, 1 << 18, 2_000_000, 0),
+])
+def test_insert_keys_parity(gpu, oracle, w, d, K, nflows, n, batch):
+    rng = np.random.default_rng(w * 7 + d)
+    cm, orc = make_pair(oracle, w, d, K, batch_packets=batch)
+    keys, _, _ = zipf_keys(rng, n, nflows, K)
+    sizes = sizes_u32(rng, n)
+    cm.insert_keys(keys, sizes)
+    cm.flush()
+    orc.insert_keys(keys, sizes)
+    assert_same_state(cm, orc)
+
+
+def test_many_calls_and_reset(gpu, oracle):
+    rng = np.random.default_rng(5)
+    cm, orc = make_pair(oracle, 512, 3, 16, st=5000, ct=20)
+    for _ in range(4):
+        keys, _, _ = zipf_keys(rng, 20_000, 700, 16)
+        sizes = sizes_u32(rng, 20_000)
+        cm.insert_keys(keys, sizes)
+        orc.insert_keys(keys, sizes)
+    cm.flush()
+    assert_same_state(cm, orc)
+    cm.reset()
+    orc.reset()
+    assert_same_state(cm, orc)
+    keys, _, _ = zipf_keys(rng, 30_000, 300, 16)
+    sizes = sizes_u32(rng, 30_000)
+    cm.insert_keys(keys, sizes)
+    orc.insert_keys(keys, sizes)
+    cm.flush()
+    assert_same_state(cm, orc)
+
+
+def test_sizes_wrap_and_overflow(gpu, oracle):
+    """sizes >= 2^20-1 take the overflow path; u32 wrap of S (count_min.go:191)."""
+    rng = np.random.default_rng(9)
+    cm, orc = make_pair(oracle, 128, 2, 8)
+    keys, _, _ = zipf_keys(rng, 50_000, 40, 8, s=1.5)
+    sizes = sizes_u32(rng, 50_000, big_frac=0.05)
+    sizes[:100] = 0
+    sizes[100:200] = 0xFFFFFFFF
+    cm.insert_keys(keys, sizes)
+    orc.insert_keys(keys, sizes)
+    cm.flush()
+    assert_same_state(cm, orc)
+
+
+def test_query_and_heavy_hitters(gpu, oracle):
+    rng = np.random.default_rng(11)
+    cm, orc = make_pair(oracle, 4096, 3, 16, st=20_000, ct=50)
+    keys, flows, _ = zipf_keys(rng, 200_000, 20_000, 16)
+    sizes = sizes_u32(rng, 200_000)
+    cm.insert_keys(keys, sizes)
+    orc.insert_keys(keys, sizes)
+    cm.flush()
+    q = cm.query_many(flows[:5000])
+    want = np.array([orc.query(bytes(f)) for f in flows[:5000]], dtype=np.uint64)
+    assert np.array_equal(q, want)
+    absent = rng.integers(0, 256, (100, 16), dtype=np.uint8)
+    assert np.array_equal(cm.query_many(absent), np.array([orc.query(bytes(f)) for f in absent], np.uint64))
+    hh = cm.heavy_hitters()
+    assert [(h.Flow, h.Count) for h in hh.Count] == orc.heavy("count")
+    assert [(h.Flow, h.Size) for h in hh.Size] == orc.heavy("size")
+    assert hh.Size is not None
+
+
+@pytest.mark.parametrize("fields", [
+    ["SrcIP"], ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"],
+    ["DstIP", "SrcPort", "DstPort", "Protocol"], ["SrcPort", "SrcIP", "Protocol"], ["DstPort"],
+])
+def test_tuples_and_headers_parity(gpu, oracle, fields):
+    from go2netspectra_amd import CountMin, PacketBatch
+    rng = np.random.default_rng(len(fields))
+    t = random_tuples(rng, 60_000, 3000, v6_frac=0.2)
+    K = sum({"SrcIP": 16, "DstIP": 16, "SrcPort": 2, "DstPort": 2, "Protocol": 1}[f] for f in fields)
+    seeds = np.array([0x1111, 0x2222, 0x3333], np.uint32)
+    batch = PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"])
+    cm = CountMin(2048, 3, 10_000, 30, flow_fields=fields, seeds=seeds)
+    cm.insert_tuples(batch)
+    cm.flush()
+    orc = oracle.CountMin(2048, 3, 10_000, 30, K, seeds)
+    orc.insert_keys(batch.keys(fields), t["length"])
+    assert_same_state(cm, orc)
+    # same packets as 64-byte frame records through the fused parser
+    hdr = frames_from_tuples(t, rng, vlan_frac=0.3)
+    cm2 = CountMin(2048, 3, 10_000, 30, flow_fields=fields, seeds=seeds)
+    cm2.insert_headers(hdr, t["length"])
+    cm2.flush()
+    orc2 = oracle.CountMin(2048, 3, 10_000, 30, K, seeds)
+    done = orc2.insert_hdr64(hdr, t["length"], fields)
+    assert done == 60_000 - cm2.stats()["unsupported"] - cm2.stats()["dropped"]
+    assert_same_state(cm2, orc2)
+
+
+def test_synthetic_device_resident_parity(gpu, oracle):
+    """C2 geometry on device-resident synthetic Zipf headers (2M packets)."""
+    import torch
+    from go2netspectra_amd import CountMin, SyntheticTraffic
+    fields = ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"]
+    syn = SyntheticTraffic()
+    hdr, wl = syn.generate(2_000_000)
+    seeds = np.array([0xA1, 0xB2, 0xC3, 0xD4], np.uint32)
+    cm = CountMin(1 << 20, 4, 1 << 20, 1000, flow_fields=fields, seeds=seeds, max_flows=1 << 21)
+    cm.insert_headers(hdr, wl)
+    cm.flush()
+    torch.cuda.synchronize()
+    orc = oracle.CountMin(1 << 20, 4, 1 << 20, 1000, 37, seeds)
+    h = hdr.cpu().numpy()
+    w = wl.cpu().numpy().view(np.uint32)
+    assert orc.insert_hdr64(h, w, fields) == 2_000_000
+    assert_same_state(cm, orc)
+    assert cm.stats()["inserted"] == 2_000_000
