@@ -42,12 +42,54 @@ constexpr int kApThreads = 1024;
 constexpr int kApItems = 4;
 constexpr uint32_t kApChunk = kApThreads * kApItems; // 4096 updates per K4 step
 constexpr uint32_t kScanSeg = 4096;
+constexpr uint32_t kHot = 64;                       // designated hot buckets per row
+constexpr uint32_t kHotTab = 512;                   // LDS hash slots per row (load <= 1/8)
+constexpr uint32_t kMaxLB = 1280;                   // local bins per row: tiles + hot (<= 1024 + 64)
+constexpr uint32_t kHotMinBits = 11;                // designate only buckets with C >= 1024
 
 struct CmGeom {
     uint32_t w, d, wmask, pow2;
-    uint32_t tile_bits, ntiles, nbins, nbits;  // nbits = ceil_log2(ntiles)
+    uint32_t tile_bits, ntiles, nbins, nbits;  // nbits = ceil_log2(ntiles + kHot)
+    uint32_t nbins_all;                        // nbins + d*kHot (hot bins follow the tile bins)
     uint32_t seeds[8];
 };
+
+// ---------------------------------------------------------------------------
+// Designated hot buckets.  After every batch the buckets with the largest
+// counters (a heavy flow's buckets) are designated for the next batch; their
+// updates go to one bin per bucket, which the whole chip aggregates in
+// parallel instead of one workgroup walking it.  Designation only moves work;
+// exactness comes from the verify/fallback steps (k_hot_verify, k_hot_fallback).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t hot_hash(uint32_t b) { return (b * 0x9E3779B1u) >> 23; }  // 0..511
+
+// LDS table rows [r0, r0+nrows): value = bucket<<7 | h, empty = ~0
+__device__ __forceinline__ void build_hot_tab(const uint32_t *hot_ids, uint32_t r0, uint32_t nrows,
+                                              uint32_t *tab) {
+    for (uint32_t i = threadIdx.x; i < nrows * kHotTab; i += blockDim.x) tab[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nrows * kHot; i += blockDim.x) {
+        const uint32_t r = i / kHot, h = i % kHot;
+        const uint32_t id = hot_ids[(r0 + r) * kHot + h];
+        if (id == GNS_ID_NONE) continue;
+        uint32_t slot = hot_hash(id);
+        for (;;) {
+            if (atomicCAS(&tab[r * kHotTab + slot], 0xFFFFFFFFu, id << 7 | h) == 0xFFFFFFFFu) break;
+            slot = (slot + 1) & (kHotTab - 1);
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int hot_lookup(const uint32_t *tabrow, uint32_t b) {
+    uint32_t slot = hot_hash(b);
+    for (;;) {
+        const uint32_t v = tabrow[slot];
+        if (v == 0xFFFFFFFFu) return -1;
+        if ((v >> 7) == b) return (int)(v & 127u);
+        slot = (slot + 1) & (kHotTab - 1);
+    }
+}
 
 __device__ __forceinline__ uint32_t row_index(const CmGeom &g, uint32_t h) {
     return g.pow2 ? (h & g.wmask) : (h % g.w);  // count_min.go:177 `% t.w`
@@ -66,8 +108,9 @@ struct ExtractArgs {
     uint64_t *pend;      // per-block regions of kChunk
     uint32_t *pend_cnt;  // [nblk]
     uint32_t *pend_total;
-    uint32_t *hist;      // [nbins][nblk]
+    uint32_t *hist;      // [nbins_all][nblk]
     uint32_t nblk;
+    const uint32_t *hot_ids;  // [d][kHot]
     unsigned long long *stats;
 };
 
@@ -95,7 +138,9 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
     stage_plan<MODE>(a.kp, s_src);
     const uint32_t K = a.kp.K;
-    for (uint32_t i = tid; i < a.g.nbins; i += kExThreads) s_hist[i] = 0;
+    uint32_t *s_tab = s_hist + a.g.nbins_all;
+    build_hot_tab(a.hot_ids, 0, a.g.d, s_tab);
+    for (uint32_t i = tid; i < a.g.nbins_all; i += kExThreads) s_hist[i] = 0;
     if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; }
     __syncthreads();
     const uint64_t beg = (uint64_t)blk * kChunk;
@@ -129,13 +174,15 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
         for (uint32_t rr = 0; rr < 8; rr++) {
             if (rr >= a.g.d) break;
             const uint32_t b = row_index(a.g, mm3_n<GNS_KWMAX>(kw, K, a.g.seeds[rr]));
-            a.idx[(uint64_t)rr * a.n + p] = b;
-            atomicAdd(&s_hist[rr * a.g.ntiles + (b >> a.g.tile_bits)], 1u);
+            const int h = hot_lookup(s_tab + rr * kHotTab, b);
+            // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
+            a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
+            atomicAdd(&s_hist[h >= 0 ? a.g.nbins + rr * kHot + h : rr * a.g.ntiles + (b >> a.g.tile_bits)], 1u);
         }
     }
     atomicAdd(&s_ok, n_ok);
     __syncthreads();
-    for (uint32_t i = tid; i < a.g.nbins; i += kExThreads) a.hist[(uint64_t)i * a.nblk + blk] = s_hist[i];
+    for (uint32_t i = tid; i < a.g.nbins_all; i += kExThreads) a.hist[(uint64_t)i * a.nblk + blk] = s_hist[i];
     if (tid == 0) {
         a.pend_cnt[blk] = s_pend;
         if (s_pend) atomicAdd(a.pend_total, s_pend);
@@ -284,23 +331,25 @@ struct ScatterArgs {
     uint64_t *entries;
     uint64_t *ovf;
     uint32_t *ovf_cnt;
+    const uint32_t *hot_ids;
     unsigned long long *stats;
 };
 
 __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
-    __shared__ uint32_t s_cnt[4][kMaxTilesPerRow];   // per-wave running counts (this round)
-    __shared__ uint32_t s_rstart[kMaxTilesPerRow];
-    __shared__ uint32_t s_goff[kMaxTilesPerRow];
+    __shared__ uint32_t s_cnt[4][kMaxLB];   // per-wave running counts (this round)
+    __shared__ uint32_t s_rstart[kMaxLB];
+    __shared__ uint32_t s_goff[kMaxLB];
     __shared__ uint64_t s_ent[kScRound];
     __shared__ uint32_t s_pos[kScRound];
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_total;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t blk = blockIdx.x, r = blockIdx.y;
-    const uint32_t NT = a.g.ntiles;
+    const uint32_t NT = a.g.ntiles + kHot;  // local bins: tiles, then this row's hot buckets
     const uint32_t tmask = (1u << a.g.tile_bits) - 1u;
     for (uint32_t t = tid; t < NT; t += kScThreads) {
-        s_goff[t] = a.offsets[(uint64_t)(r * NT + t) * a.nblk + blk];
+        const uint64_t gb = t < a.g.ntiles ? (uint64_t)(r * a.g.ntiles + t) : (uint64_t)(a.g.nbins + r * kHot + (t - a.g.ntiles));
+        s_goff[t] = a.offsets[gb * a.nblk + blk];
         s_cnt[0][t] = 0; s_cnt[1][t] = 0; s_cnt[2][t] = 0; s_cnt[3][t] = 0;
     }
     const uint64_t beg = (uint64_t)blk * kChunk;
@@ -322,7 +371,10 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                 if (id != GNS_ID_NONE) {
                     valid = true;
                     const uint32_t b = a.idx[(uint64_t)r * a.n + p];
-                    t = b >> a.g.tile_bits;
+                    const bool hot = (b >> 31) != 0;
+                    const uint32_t h = b & 0x7FFFFFFFu;
+                    t = hot ? a.g.ntiles + h : (b >> a.g.tile_bits);
+                    const uint32_t low = hot ? r * kHot + h : (b & tmask);
                     const uint32_t sz = a.sizes[p];
                     uint32_t lo = id, sf = sz;
                     if (sz >= kSizeEsc) {
@@ -336,7 +388,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                         }
                         sf = kSizeEsc;
                     }
-                    e = (uint64_t)((sf << 12) | (b & tmask)) << 32 | lo;
+                    e = (uint64_t)((sf << 12) | low) << 32 | lo;
                 }
             }
             uint64_t peers = __ballot(valid);
@@ -356,7 +408,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
         }
         __syncthreads();
         // phase 2: wave prefix per tile, then block scan over tiles
-        constexpr uint32_t TPT = kMaxTilesPerRow / kScThreads;  // 4 tiles per thread
+        constexpr uint32_t TPT = kMaxLB / kScThreads;  // 5 local bins per thread
         uint32_t tot[TPT];
         uint32_t lsum = 0;
 #pragma unroll
@@ -410,11 +462,11 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
 
 // Order bins by size (largest first) so the heavy bins start first.
 __global__ __launch_bounds__(1024) void k_order(const uint32_t *offsets, uint32_t nblk, uint32_t nbins,
-                                                const uint32_t *total, uint32_t *order) {
+                                                uint32_t nall, const uint32_t *total, uint32_t *order) {
     __shared__ uint32_t s_sz[4096];
     for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
         const uint32_t s0 = offsets[(uint64_t)b * nblk];
-        const uint32_t s1 = (b + 1 < nbins) ? offsets[(uint64_t)(b + 1) * nblk] : *total;
+        const uint32_t s1 = (b + 1 < nall) ? offsets[(uint64_t)(b + 1) * nblk] : *total;
         s_sz[b] = s1 - s0;
     }
     __syncthreads();
@@ -462,7 +514,7 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
     const CmGeom &g = a.g;
     const uint32_t bin = a.order ? a.order[blockIdx.x] : blockIdx.x;
     const uint32_t beg = a.offsets[(uint64_t)bin * a.nblk];
-    const uint32_t end = (bin + 1 < a.nbins) ? a.offsets[(uint64_t)(bin + 1) * a.nblk] : *a.total;
+    const uint32_t end = (bin + 1 < g.nbins_all) ? a.offsets[(uint64_t)(bin + 1) * a.nblk] : *a.total;
     if (beg >= end) return;
     const uint32_t r = bin / g.ntiles, t = bin % g.ntiles;
     const uint32_t tbase = t << g.tile_bits;
@@ -640,6 +692,306 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Exact wave-parallel sequence for ONE bucket (count_min.go:180-235): 64
+// updates per step; a prefix sum gives the counter before every update, the
+// first update that would leave the linear regime (an "event": fingerprint
+// take-over, counter wrap) is applied explicitly and the scan restarts after
+// it.  Steps per 64 updates = events + 1.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t t = __shfl_up(v, o, 64);
+        if (lane >= (uint32_t)o) v += t;
+    }
+    return v;
+}
+
+// count half; F, C wave-uniform
+__device__ __forceinline__ void count_seq64(bool valid, uint32_t k, uint32_t &F, uint32_t &C) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t start = 0;
+    for (;;) {
+        const bool act = valid && lane >= start;
+        const bool own = k == F;
+        const int64_t dlt = act ? (own ? 1 : -1) : 0;
+        const int64_t P = wave_incl_scan64(dlt);
+        const int64_t Cb = (int64_t)C + P - dlt;
+        const bool ev = act && ((!own && Cb <= 1) || (own && Cb >= 0xFFFFFFFFll));
+        const uint64_t m = __ballot(ev);
+        if (!m) {
+            C = (uint32_t)((int64_t)C + __shfl(P, 63, 64));
+            return;
+        }
+        const uint32_t t = (uint32_t)__ffsll((long long)m) - 1;
+        const int64_t cbt = __shfl(Cb, t, 64);
+        const uint32_t kt = __shfl(k, t, 64);
+        const bool ownt = kt == F;
+        if (ownt) { C = 0; }                        // C+1 wraps to 0 (u32), F kept
+        else if (cbt == 0) { C = 1; F = kt; }       // :214-218
+        else { C = 0; F = kt; }                     // :226-231 reaches 0, F := flow
+        start = t + 1;
+        if (start >= 64) return;
+    }
+}
+
+// size half; F, S wave-uniform
+__device__ __forceinline__ void size_seq64(bool valid, uint32_t k, uint32_t s, uint32_t &F, uint32_t &S) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t start = 0;
+    for (;;) {
+        const bool act = valid && lane >= start;
+        const bool own = k == F;
+        const int64_t dlt = act ? (own ? (int64_t)s : -(int64_t)s) : 0;
+        const int64_t W = wave_incl_scan64(dlt);
+        const int64_t Sb = (int64_t)S + W - dlt;
+        const bool ev = act && ((!own && (Sb == 0 || (int64_t)s > Sb)) || (own && Sb + (int64_t)s > 0xFFFFFFFFll));
+        const uint64_t m = __ballot(ev);
+        if (!m) {
+            S = (uint32_t)((int64_t)S + __shfl(W, 63, 64));
+            return;
+        }
+        const uint32_t t = (uint32_t)__ffsll((long long)m) - 1;
+        const int64_t sbt = __shfl(Sb, t, 64);
+        const uint32_t kt = __shfl(k, t, 64), st = __shfl(s, t, 64);
+        if (kt == F) { S = (uint32_t)((uint64_t)sbt + st); }   // u32 wrap, F kept
+        else { S = st; F = kt; }                               // :184-188 / :196-200
+        start = t + 1;
+        if (start >= 64) return;
+    }
+}
+
+constexpr uint32_t kHotSegs = 64;   // segments per hot bin (blocks working on one bucket)
+
+struct HotArgs {
+    const uint64_t *entries;
+    const uint32_t *offsets;
+    uint32_t nblk;
+    const uint32_t *total;
+    const uint64_t *ovf;
+    const uint32_t *hot_ids;
+    CmGeom g;
+    uint32_t *C, *Fc, *S, *Fs;
+    long long *segtot;  // [d*kHot][kHotSegs][2]: count walk, size walk of each segment
+    uint32_t *hflag;    // [d*kHot]: bit0/bit1 = count/size half saw an event (needs replay)
+};
+
+__device__ __forceinline__ void hot_bin_range(const HotArgs &a, uint32_t hb, uint32_t &beg, uint32_t &end) {
+    const uint32_t bin = a.g.nbins + hb;
+    beg = a.offsets[(uint64_t)bin * a.nblk];
+    end = (bin + 1 < a.g.nbins_all) ? a.offsets[(uint64_t)(bin + 1) * a.nblk] : *a.total;
+}
+
+__device__ __forceinline__ void hot_seg_range(uint32_t beg, uint32_t end, uint32_t sidx, uint32_t &sb,
+                                              uint32_t &se) {
+    const uint32_t len = end - beg;
+    const uint32_t per = (((len + kHotSegs - 1) / kHotSegs) + 3u) & ~3u;
+    sb = min(end, beg + sidx * per);
+    se = min(end, sb + per);
+}
+
+__device__ __forceinline__ void decode_entry(const uint64_t *ovf, uint64_t e, uint32_t &k, uint32_t &s) {
+    const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+    if (lo & kOvfFlag) {
+        const uint64_t ov = ovf[lo & ~kOvfFlag];
+        k = (uint32_t)ov; s = (uint32_t)(ov >> 32);
+    } else {
+        k = lo; s = hi >> 12;
+    }
+}
+
+// block (256) reduction of two int64
+__device__ __forceinline__ void block_sum2(long long &x, long long &y, long long *sh /*8*/) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    x = (long long)wave_sum64((uint64_t)x);
+    y = (long long)wave_sum64((uint64_t)y);
+    if (lane == 0) { sh[wave] = x; sh[4 + wave] = y; }
+    __syncthreads();
+    x = sh[0] + sh[1] + sh[2] + sh[3];
+    y = sh[4] + sh[5] + sh[6] + sh[7];
+    __syncthreads();
+}
+
+// H1: walk totals of every segment of every hot bin (owner = batch-entry fingerprint)
+__global__ __launch_bounds__(256) void k_hot_sum(HotArgs a) {
+    __shared__ long long sh[8];
+    const uint32_t hb = blockIdx.y, sidx = blockIdx.x;
+    const uint32_t id = a.hot_ids[hb];
+    if (id == GNS_ID_NONE) return;
+    uint32_t beg, end, sb, se;
+    hot_bin_range(a, hb, beg, end);
+    hot_seg_range(beg, end, sidx, sb, se);
+    const uint64_t cell = (uint64_t)(hb / kHot) * a.g.w + id;
+    const uint32_t F_c = a.Fc[cell], F_s = a.Fs[cell];
+    long long wc = 0, ws = 0;
+    for (uint32_t q = sb + threadIdx.x; q < se; q += 256) {
+        uint32_t k, s;
+        decode_entry(a.ovf, a.entries[q], k, s);
+        wc += (k == F_c) ? 1 : -1;
+        ws += (k == F_s) ? (long long)s : -(long long)s;
+    }
+    block_sum2(wc, ws, sh);
+    if (threadIdx.x == 0) {
+        a.segtot[((size_t)hb * kHotSegs + sidx) * 2] = wc;
+        a.segtot[((size_t)hb * kHotSegs + sidx) * 2 + 1] = ws;
+    }
+}
+
+// H2: exact check.  With no event the owner never changes and every counter
+// follows u32 arithmetic on the running walk (count_min.go:190-193 owner adds
+// wrap mod 2^32 exactly like the walk); an event is a foreign update that
+// would find C <= 1 (:226-231 take-over) or S == 0 / s > S (:184-200).
+__global__ __launch_bounds__(256) void k_hot_verify(HotArgs a) {
+    __shared__ long long sh_w[2][4];
+    const uint32_t hb = blockIdx.y, sidx = blockIdx.x, tid = threadIdx.x;
+    const uint32_t lane = tid & 63u, wave = tid >> 6;
+    const uint32_t id = a.hot_ids[hb];
+    if (id == GNS_ID_NONE) return;
+    uint32_t beg, end, sb, se;
+    hot_bin_range(a, hb, beg, end);
+    hot_seg_range(beg, end, sidx, sb, se);
+    if (sb >= se) return;
+    const uint64_t cell = (uint64_t)(hb / kHot) * a.g.w + id;
+    const uint32_t F_c = a.Fc[cell], F_s = a.Fs[cell];
+    long long run_c = a.C[cell], run_s = a.S[cell];
+    for (uint32_t j = 0; j < sidx; j++) {
+        run_c += a.segtot[((size_t)hb * kHotSegs + j) * 2];
+        run_s += a.segtot[((size_t)hb * kHotSegs + j) * 2 + 1];
+    }
+    uint32_t ev = 0;
+    for (uint32_t q0 = sb; q0 < se; q0 += 1024) {  // 4 consecutive entries per thread
+        uint32_t k[4], s[4];
+        bool v[4];
+        long long dc[4], ds[4], tc = 0, ts = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t q = q0 + tid * 4 + i;
+            v[i] = q < se;
+            k[i] = 0; s[i] = 0;
+            if (v[i]) decode_entry(a.ovf, a.entries[q], k[i], s[i]);
+            dc[i] = v[i] ? ((k[i] == F_c) ? 1 : -1) : 0;
+            ds[i] = v[i] ? ((k[i] == F_s) ? (long long)s[i] : -(long long)s[i]) : 0;
+            tc += dc[i]; ts += ds[i];
+        }
+        const long long ic = wave_incl_scan64(tc), is = wave_incl_scan64(ts);
+        if (lane == 63) { sh_w[0][wave] = ic; sh_w[1][wave] = is; }
+        __syncthreads();
+        long long bc = 0, bs = 0, allc = 0, alls = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 4; w++) {
+            if (w < wave) { bc += sh_w[0][w]; bs += sh_w[1][w]; }
+            allc += sh_w[0][w]; alls += sh_w[1][w];
+        }
+        __syncthreads();
+        long long pc = run_c + bc + ic - tc, ps = run_s + bs + is - ts;  // before my first entry
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if (v[i]) {
+                const uint32_t Cb = (uint32_t)pc, Sb = (uint32_t)ps;
+                if (k[i] != F_c && Cb <= 1u) ev |= 1u;
+                if (k[i] != F_s && (Sb == 0u || s[i] > Sb)) ev |= 2u;
+            }
+            pc += dc[i]; ps += ds[i];
+        }
+        run_c += allc; run_s += alls;
+    }
+    const uint32_t any = (uint32_t)(__ballot(ev & 1u) != 0) | ((uint32_t)(__ballot(ev & 2u) != 0) << 1);
+    if (lane == 0 && any) atomicOr(&a.hflag[hb], any);
+}
+
+// H3: apply the verified halves; flagged halves keep the batch-entry state
+// for the in-order fallback.
+__global__ __launch_bounds__(512) void k_hot_apply(HotArgs a) {
+    const uint32_t hb = threadIdx.x;
+    if (hb >= a.g.d * kHot) return;
+    const uint32_t id = a.hot_ids[hb];
+    if (id == GNS_ID_NONE) return;
+    uint32_t beg, end;
+    hot_bin_range(a, hb, beg, end);
+    if (beg >= end) return;
+    long long tc = 0, ts = 0;
+    for (uint32_t j = 0; j < kHotSegs; j++) {
+        tc += a.segtot[((size_t)hb * kHotSegs + j) * 2];
+        ts += a.segtot[((size_t)hb * kHotSegs + j) * 2 + 1];
+    }
+    const uint64_t cell = (uint64_t)(hb / kHot) * a.g.w + id;
+    const uint32_t f = a.hflag[hb];
+    if (!(f & 1u)) a.C[cell] = (uint32_t)((long long)a.C[cell] + tc);
+    if (!(f & 2u)) a.S[cell] = (uint32_t)((long long)a.S[cell] + ts);
+}
+
+// Exact in-order replay of one hot bin (cold start / ownership change).
+__global__ __launch_bounds__(64) void k_hot_fallback(HotArgs a) {
+    const uint32_t i = blockIdx.x, lane = threadIdx.x;
+    const uint32_t rep = a.hflag[i];
+    if (!rep) return;
+    const uint32_t id = a.hot_ids[i];
+    const uint64_t cell = (uint64_t)(i / kHot) * a.g.w + id;
+    uint32_t beg, end;
+    hot_bin_range(a, i, beg, end);
+    uint32_t Fc = a.Fc[cell], C = a.C[cell], Fs = a.Fs[cell], S = a.S[cell];
+    for (uint32_t cb = beg; cb < end; cb += 64) {
+        const uint32_t q = cb + lane;
+        const bool v = q < end;
+        uint32_t k = 0, s = 0;
+        if (v) decode_entry(a.ovf, a.entries[q], k, s);
+        if (rep & 1u) count_seq64(v, k, Fc, C);
+        if (rep & 2u) size_seq64(v, k, s, Fs, S);
+    }
+    if (lane == 0) {
+        if (rep & 1u) { a.C[cell] = C; a.Fc[cell] = Fc; }
+        if (rep & 2u) { a.S[cell] = S; a.Fs[cell] = Fs; }
+    }
+}
+
+// Designation for the next batch: per row, the buckets whose counter bit
+// length is in the top band holding at most kHot buckets (and >= 2^(kHotMinBits-1)).
+__global__ __launch_bounds__(256) void k_hot_hist(const uint32_t *C, CmGeom g, uint32_t *hh /*[d][33]*/) {
+    __shared__ uint32_t s[8 * 33];
+    for (uint32_t i = threadIdx.x; i < g.d * 33; i += 256) s[i] = 0;
+    __syncthreads();
+    const uint64_t cells = (uint64_t)g.d * g.w;
+    for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += (uint64_t)gridDim.x * 256) {
+        const uint32_t v = C[c];
+        const uint32_t bits = v ? 32u - __clz(v) : 0u;
+        if (bits >= kHotMinBits) atomicAdd(&s[(c / g.w) * 33 + bits], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < g.d * 33; i += 256) if (s[i]) atomicAdd(&hh[i], s[i]);
+}
+
+__global__ void k_hot_pick(uint32_t *hh, CmGeom g, uint32_t *thr, uint32_t *hcnt, uint32_t *hot_ids) {
+    const uint32_t r = threadIdx.x;
+    for (uint32_t i = threadIdx.x; i < g.d * kHot; i += blockDim.x) hot_ids[i] = GNS_ID_NONE;
+    if (r < g.d) {
+        uint32_t cum = 0, t = 33;
+        for (int b = 32; b >= (int)kHotMinBits; b--) {
+            cum += hh[r * 33 + b];
+            if (cum > kHot) break;
+            t = (uint32_t)b;
+        }
+        thr[r] = t;
+        hcnt[r] = 0;
+        for (int b = 0; b < 33; b++) hh[r * 33 + b] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_hot_collect(const uint32_t *C, CmGeom g, const uint32_t *thr,
+                                                      uint32_t *hcnt, uint32_t *hot_ids) {
+    const uint64_t cells = (uint64_t)g.d * g.w;
+    for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += (uint64_t)gridDim.x * 256) {
+        const uint32_t v = C[c];
+        const uint32_t r = (uint32_t)(c / g.w);
+        const uint32_t bits = v ? 32u - __clz(v) : 0u;
+        if (bits >= thr[r] && bits >= kHotMinBits) {
+            const uint32_t q = atomicAdd(&hcnt[r], 1u);
+            if (q < kHot) hot_ids[r * kHot + q] = (uint32_t)(c - (uint64_t)r * g.w);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Query (count_min.go:240-254), export, heavy-hitter candidates
 // ---------------------------------------------------------------------------
 struct QueryArgs {
@@ -730,6 +1082,10 @@ struct gns_cm {
     uint64_t *ovf = nullptr;
     uint32_t *ovf_cnt = nullptr;
     unsigned long long *stats = nullptr;  // [8]
+    uint32_t *hot_ids = nullptr;          // [d][kHot] designated buckets for the next batch
+    long long *segtot = nullptr;          // [d*kHot][kHotSegs][2]
+    uint32_t *hflag = nullptr, *hhist = nullptr, *hthr = nullptr, *hcnt = nullptr;
+    bool warm = false;                    // a batch has run since create/reset
     uint32_t *h_pin = nullptr;            // pinned host mirror of small counters
     // staging for host inputs
     uint8_t *stage = nullptr;
@@ -761,6 +1117,7 @@ int cm_free_all(gns_cm *cm) {
     dfree(cm->pend[0]); dfree(cm->pend[1]); dfree(cm->pcnt[0]); dfree(cm->pcnt[1]);
     dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
     dfree(cm->entries); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats); dfree(cm->stage);
+    dfree(cm->hot_ids); dfree(cm->segtot); dfree(cm->hflag); dfree(cm->hhist); dfree(cm->hthr); dfree(cm->hcnt);
     if (cm->h_pin) (void)hipHostFree(cm->h_pin);
     cm->timer.destroy();
     if (cm->stream) (void)hipStreamDestroy(cm->stream);
@@ -774,6 +1131,9 @@ int cm_reset_state(gns_cm *cm) {
     GNS_HIP(hipMemsetAsync(cm->Fc, 0xFF, cells * 4, cm->stream));
     GNS_HIP(hipMemsetAsync(cm->Fs, 0xFF, cells * 4, cm->stream));
     GNS_HIP(hipMemsetAsync(cm->D.rec, 0, cm->dict_slots * cm->D.RW * 4, cm->stream));
+    GNS_HIP(hipMemsetAsync(cm->hot_ids, 0xFF, (size_t)cm->g.d * kHot * 4, cm->stream));
+    GNS_HIP(hipMemsetAsync(cm->hhist, 0, (size_t)cm->g.d * 33 * 4, cm->stream));
+    cm->warm = false;
     return GNS_OK;
 }
 
@@ -792,9 +1152,11 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         ExtractArgs a{};
         a.in = in; a.n = n; a.kp = cm->kp; a.g = g; a.D = cm->D; a.epoch = cm->epoch;
         a.keyid = cm->keyid; a.idx = cm->idx; a.pend = cm->pend[0]; a.pend_cnt = cm->pcnt[0];
-        a.pend_total = cm->ptotal; a.hist = cm->hist; a.nblk = nblk; a.stats = cm->stats;
+        a.pend_total = cm->ptotal; a.hist = cm->hist; a.nblk = nblk; a.hot_ids = cm->hot_ids;
+        a.stats = cm->stats;
         ScopedStage st(cm->timer, 0);
-        hipLaunchKernelGGL((k_extract<KIND, MODE>), dim3(nblk), dim3(kExThreads), g.nbins * 4, s, a);
+        hipLaunchKernelGGL((k_extract<KIND, MODE>), dim3(nblk), dim3(kExThreads),
+                           (g.nbins_all + g.d * kHotTab) * 4, s, a);
         GNS_HIP(hipGetLastError());
     }
     // K1b: resolve parked packets until none remain
@@ -823,7 +1185,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         cur ^= 1;
     }
     // K2
-    const uint64_t N = (uint64_t)g.nbins * nblk;
+    const uint64_t N = (uint64_t)g.nbins_all * nblk;
     const uint32_t nseg = (uint32_t)((N + kScanSeg - 1) / kScanSeg);
     {
         ScopedStage st(cm->timer, 2);
@@ -838,7 +1200,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         ScatterArgs a{};
         a.n = n; a.g = g; a.keyid = cm->keyid; a.idx = cm->idx; a.sizes = in.sizes;
         a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
-        a.ovf_cnt = cm->ovf_cnt; a.stats = cm->stats;
+        a.ovf_cnt = cm->ovf_cnt; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
         ScopedStage st(cm->timer, 3);
         hipLaunchKernelGGL(k_scatter, dim3(nblk, g.d), dim3(kScThreads), 0, s, a);
         GNS_HIP(hipGetLastError());
@@ -847,7 +1209,8 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
     {
         const bool ordered = g.nbins <= 4096;
         if (ordered)
-            hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, s, cm->hist, nblk, g.nbins, cm->total, cm->order);
+            hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, s, cm->hist, nblk, g.nbins, g.nbins_all,
+                               cm->total, cm->order);
         ApplyArgs a{};
         a.entries = cm->entries; a.offsets = cm->hist; a.nblk = nblk; a.nbins = g.nbins;
         a.total = cm->total; a.order = ordered ? cm->order : nullptr; a.ovf = cm->ovf; a.g = g;
@@ -856,14 +1219,41 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         hipLaunchKernelGGL(k_apply, dim3(g.nbins), dim3(kApThreads), 0, s, a);
         GNS_HIP(hipGetLastError());
     }
+    // hot bins: chip-wide aggregate, exact decide, in-order fallback
+    {
+        HotArgs h{};
+        h.entries = cm->entries; h.offsets = cm->hist; h.nblk = nblk; h.total = cm->total; h.ovf = cm->ovf;
+        h.hot_ids = cm->hot_ids; h.g = g; h.C = cm->C; h.Fc = cm->Fc; h.S = cm->S; h.Fs = cm->Fs;
+        h.segtot = cm->segtot; h.hflag = cm->hflag;
+        ScopedStage st(cm->timer, 6);
+        GNS_HIP(hipMemsetAsync(cm->hflag, 0, (size_t)g.d * kHot * 4, s));
+        hipLaunchKernelGGL(k_hot_sum, dim3(kHotSegs, g.d * kHot), dim3(256), 0, s, h);
+        hipLaunchKernelGGL(k_hot_verify, dim3(kHotSegs, g.d * kHot), dim3(256), 0, s, h);
+        hipLaunchKernelGGL(k_hot_apply, dim3(1), dim3(512), 0, s, h);
+        hipLaunchKernelGGL(k_hot_fallback, dim3(g.d * kHot), dim3(64), 0, s, h);
+        GNS_HIP(hipGetLastError());
+    }
+    // designate the next batch's hot buckets from the counters
+    {
+        ScopedStage st(cm->timer, 7);
+        const uint64_t cells = (uint64_t)g.d * g.w;
+        const unsigned grid = (unsigned)std::min<uint64_t>(2048, (cells + 255) / 256);
+        hipLaunchKernelGGL(k_hot_hist, dim3(grid), dim3(256), 0, s, cm->C, g, cm->hhist);
+        hipLaunchKernelGGL(k_hot_pick, dim3(1), dim3(512), 0, s, cm->hhist, g, cm->hthr, cm->hcnt, cm->hot_ids);
+        hipLaunchKernelGGL(k_hot_collect, dim3(grid), dim3(256), 0, s, cm->C, g, cm->hthr, cm->hcnt, cm->hot_ids);
+        GNS_HIP(hipGetLastError());
+    }
+    cm->warm = true;
     return GNS_OK;
 }
 
 template <int KIND>
 int cm_insert(gns_cm *cm, InputDesc in, uint64_t n, gns_mem where) {
     GNS_TRY(set_dev(cm));
-    for (uint64_t off = 0; off < n; off += cm->bmax) {
-        const uint64_t m = std::min<uint64_t>(cm->bmax, n - off);
+    for (uint64_t off = 0, m = 0; off < n; off += m) {
+        m = std::min<uint64_t>(cm->bmax, n - off);
+        // cold start: a small first batch designates the heavy buckets early
+        if (!cm->warm) m = std::min<uint64_t>(m, std::max<uint64_t>(kChunk * 64, cm->bmax / 32));
         InputDesc d = in;
         if (where == GNS_MEM_DEVICE) {
             if (d.hdr) d.hdr += off * 16;
@@ -958,7 +1348,8 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             break;
         }
         g.nbins = g.d * g.ntiles;
-        g.nbits = ceil_log2(g.ntiles);
+        g.nbins_all = g.nbins + g.d * kHot;
+        g.nbits = ceil_log2(g.ntiles + kHot);
         if (p->seeds) for (uint32_t i = 0; i < g.d; i++) g.seeds[i] = p->seeds[i];
         else default_seeds(g.seeds, g.d);
         if (hipStreamCreateWithFlags(&cm->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -985,15 +1376,17 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         cm->bmax = ((cm->bmax + kChunk - 1) / kChunk) * kChunk;
         if (cm->bmax > (1ull << 31)) { set_error("batch_packets too large"); rc = GNS_E_ARG; break; }
         cm->nblk_max = (uint32_t)(cm->bmax / kChunk);
-        const uint64_t nseg = ((uint64_t)g.nbins * cm->nblk_max + kScanSeg - 1) / kScanSeg;
+        const uint64_t nseg = ((uint64_t)g.nbins_all * cm->nblk_max + kScanSeg - 1) / kScanSeg;
         if ((rc = dalloc_t(&cm->keyid, cm->bmax)) || (rc = dalloc_t(&cm->idx, cm->bmax * g.d)) ||
             (rc = dalloc_t(&cm->pend[0], cm->bmax)) || (rc = dalloc_t(&cm->pend[1], cm->bmax)) ||
             (rc = dalloc_t(&cm->pcnt[0], cm->nblk_max)) || (rc = dalloc_t(&cm->pcnt[1], cm->nblk_max)) ||
-            (rc = dalloc_t(&cm->ptotal, 2)) || (rc = dalloc_t(&cm->hist, (uint64_t)g.nbins * cm->nblk_max)) ||
+            (rc = dalloc_t(&cm->ptotal, 2)) || (rc = dalloc_t(&cm->hist, (uint64_t)g.nbins_all * cm->nblk_max)) ||
             (rc = dalloc_t(&cm->part, nseg + 1)) || (rc = dalloc_t(&cm->total, 1)) ||
             (rc = dalloc_t(&cm->order, g.nbins)) || (rc = dalloc_t(&cm->entries, cm->bmax * g.d)) ||
             (rc = dalloc_t(&cm->ovf, kOvfCap)) || (rc = dalloc_t(&cm->ovf_cnt, 1)) ||
-            (rc = dalloc_t(&cm->stats, 8)))
+            (rc = dalloc_t(&cm->stats, 8)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
+            (rc = dalloc_t(&cm->segtot, (size_t)g.d * kHot * kHotSegs * 2)) || (rc = dalloc_t(&cm->hflag, g.d * kHot)) ||
+            (rc = dalloc_t(&cm->hhist, g.d * 33)) || (rc = dalloc_t(&cm->hthr, 8)) || (rc = dalloc_t(&cm->hcnt, 8)))
             break;
         if (hipHostMalloc(reinterpret_cast<void **>(&cm->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;

@@ -142,8 +142,14 @@ int gns_synth_create(const gns_synth_params *p, gns_synth **out) {
         st += 0x9E3779B97F4A7C15ull; const uint64_t r1 = mix64_h(st);
         st += 0x9E3779B97F4A7C15ull; const uint64_t r2 = mix64_h(st);
         fsrc[f] = (uint32_t)r1; fdst[f] = (uint32_t)(r1 >> 32);
-        fports[f] = (uint32_t)(r2 & 0xFFFFFFFFu);
+        uint32_t sp = (uint32_t)(r2 >> 16) & 0xFFFFu, dp = (uint32_t)r2 & 0xFFFFu;
         fproto[f] = ((r2 >> 32) % 10) < 8 ? 6 : 17;
+        if (fproto[f] == 17) {  // keep UDP off the tunnel ports gopacket decodes further
+            auto tun = [](uint32_t p) { return p == 4789u || p == 6081u || p == 2152u; };
+            if (tun(sp)) sp += 1;
+            if (tun(dp)) dp += 1;
+        }
+        fports[f] = sp << 16 | dp;
     }
     // rank -> flow permutation (Fisher-Yates)
     std::vector<uint32_t> perm(F);

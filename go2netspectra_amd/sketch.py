@@ -216,7 +216,7 @@ class CountMin:
     def set_timing(self, on: bool = True) -> None:
         check(self._L.gns_cm_set_timing(self._h, 1 if on else 0))
 
-    STAGES = ["extract", "resolve", "scan", "scatter", "apply", "insert"]
+    STAGES = ["extract", "resolve", "scan", "scatter", "apply", "insert", "hot", "designate"]
 
     def stage_times(self, reset: bool = False) -> dict:
         ms = (ct.c_double * 8)()

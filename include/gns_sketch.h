@@ -128,7 +128,8 @@ int gns_cm_export_state(gns_cm *cm, uint32_t *C, uint32_t *S, uint8_t *FPc, uint
 int gns_cm_stats(gns_cm *cm, uint64_t stats[4]);
 /* Per-stage device time (ms, HIP events on the handle's stream), accumulated
  * since the last call with reset != 0.  Stages: 0 extract, 1 resolve, 2 scan,
- * 3 scatter, 4 apply, 5 total insert.  Enabled by gns_cm_set_timing(cm, 1). */
+ * 3 scatter, 4 apply, 5 total insert, 6 hot-bucket aggregate/decide/fallback,
+ * 7 hot-bucket designation.  Enabled by gns_cm_set_timing(cm, 1). */
 int gns_cm_set_timing(gns_cm *cm, int on);
 int gns_cm_stage_times(gns_cm *cm, double ms[8], uint64_t launches[8], int reset);
 void *gns_cm_stream(gns_cm *cm); /* hipStream_t the handle launches on */

@@ -146,3 +146,27 @@ def test_synthetic_device_resident_parity(gpu, oracle):
     assert orc.insert_hdr64(h, w, fields) == 2_000_000
     assert_same_state(cm, orc)
     assert cm.stats()["inserted"] == 2_000_000
+
+
+@pytest.mark.parametrize("w", [1, 16, 4096])
+def test_hot_designation_takeover(gpu, oracle, w):
+    """Designated hot buckets whose owner changes between calls: the batch-level
+    decision fails and the exact in-order fallback must reproduce the oracle."""
+    rng = np.random.default_rng(w)
+    cm, orc = make_pair(oracle, w, 2, 8, st=1 << 20, ct=100)
+    flows = rng.integers(0, 256, (40, 8), dtype=np.uint8)
+    for phase in range(5):
+        n = 300_000
+        # phase-dependent heavy flow (70%), the rest spread over the others
+        heavy = np.full(n, phase % len(flows))
+        idx = np.where(rng.random(n) < 0.7, heavy, rng.integers(0, len(flows), n))
+        keys = np.ascontiguousarray(flows[idx])
+        sizes = sizes_u32(rng, n)
+        if phase == 3:
+            sizes[::7] = rng.integers(1 << 21, 1 << 31, len(sizes[::7]))
+        cm.insert_keys(keys, sizes)
+        orc.insert_keys(keys, sizes)
+        cm.flush()
+        assert_same_state(cm, orc)
+    st = cm.stage_times()
+    assert "hot" in st
