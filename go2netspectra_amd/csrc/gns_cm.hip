@@ -35,16 +35,16 @@ constexpr uint32_t kOvfFlag = 0x80000000u;
 constexpr uint32_t kOvfCap = 1u << 20;
 constexpr int kExThreads = 256;
 constexpr uint32_t kChunk = 16384;                  // packets per K1/K3 block
-constexpr int kScThreads = 256;
-constexpr int kScItems = 8;
-constexpr uint32_t kScRound = 4 * 64 * kScItems;    // 2048 packets per K3 round
+constexpr int kScThreads = 512;                     // K3: 8 waves
+constexpr int kScWaves = kScThreads / 64;
+constexpr int kScItems = 16;
+constexpr uint32_t kScRound = kScThreads * kScItems; // 8192 updates staged in LDS per round
 constexpr int kApThreads = 1024;
 constexpr int kApItems = 4;
 constexpr uint32_t kApChunk = kApThreads * kApItems; // 4096 updates per K4 step
 constexpr uint32_t kScanSeg = 4096;
 constexpr uint32_t kHot = 64;                       // designated hot buckets per row
 constexpr uint32_t kHotTab = 512;                   // LDS hash slots per row (load <= 1/8)
-constexpr uint32_t kMaxLB = 1280;                   // local bins per row: tiles + hot (<= 1024 + 64)
 constexpr uint32_t kHotMinBits = 11;                // designate only buckets with C >= 1024
 
 struct CmGeom {
@@ -146,38 +146,59 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
     const uint64_t beg = (uint64_t)blk * kChunk;
     const uint64_t end = min(a.n, beg + kChunk);
     uint32_t n_ok = 0;
-    for (uint64_t p = beg + tid; p < end; p += kExThreads) {
+    for (uint64_t p0 = beg; p0 < end; p0 += kExThreads) {  // wave-uniform trip count
+        const uint64_t p = p0 + tid;
+        bool ok = p < end;
         uint32_t kw[GNS_KWMAX];
-        const int st = packet_key<KIND, MODE>(a.in, K, s_src, p, kw);
-        if (st != PARSE_OK) {
-            a.keyid[p] = GNS_ID_NONE;
-            atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
-            continue;
+        if (ok) {
+            const int st = packet_key<KIND, MODE>(a.in, K, s_src, p, kw);
+            if (st != PARSE_OK) {
+                a.keyid[p] = GNS_ID_NONE;
+                atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
+                ok = false;
+            }
         }
-        uint32_t out;
-        const uint32_t slot0 = mm3_n<GNS_KWMAX>(kw, K, a.D.seed) & a.D.mask;
-        const int r = dict_find_or_claim(a.D, kw, slot0, a.epoch, &out);
-        if (r == DICT_FULL) {
-            a.keyid[p] = GNS_ID_NONE;
-            atomicAdd(&s_full, 1u);
-            continue;
+        uint32_t mk[GNS_KWMAX];
+        mm3_premix<GNS_KWMAX>(kw, K, mk);
+        if (ok) {
+            uint32_t out;
+            const uint32_t slot0 = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
+            const int r = dict_find_or_claim(a.D, kw, slot0, a.epoch, &out);
+            if (r == DICT_FULL) {
+                a.keyid[p] = GNS_ID_NONE;
+                atomicAdd(&s_full, 1u);
+                ok = false;
+            } else if (r == DICT_FOUND) {
+                a.keyid[p] = out;
+            } else {
+                a.keyid[p] = GNS_ID_NONE;  // set by k_resolve
+                const uint32_t q = atomicAdd(&s_pend, 1u);
+                a.pend[beg + q] = (uint64_t)(p - beg) << 32 | out;
+            }
         }
-        if (r == DICT_FOUND) {
-            a.keyid[p] = out;
-        } else {
-            a.keyid[p] = GNS_ID_NONE;  // set by k_resolve
-            const uint32_t q = atomicAdd(&s_pend, 1u);
-            a.pend[beg + q] = (uint64_t)(p - beg) << 32 | out;
-        }
-        n_ok++;
+        n_ok += ok ? 1u : 0u;
 #pragma unroll
         for (uint32_t rr = 0; rr < 8; rr++) {
             if (rr >= a.g.d) break;
-            const uint32_t b = row_index(a.g, mm3_n<GNS_KWMAX>(kw, K, a.g.seeds[rr]));
-            const int h = hot_lookup(s_tab + rr * kHotTab, b);
-            // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
-            a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
-            atomicAdd(&s_hist[h >= 0 ? a.g.nbins + rr * kHot + h : rr * a.g.ntiles + (b >> a.g.tile_bits)], 1u);
+            uint32_t binid = 0xFFFFFFFFu;
+            if (ok) {
+                const uint32_t b = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, K, a.g.seeds[rr]));
+                const int h = hot_lookup(s_tab + rr * kHotTab, b);
+                // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
+                a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
+                binid = h >= 0 ? a.g.nbins + rr * kHot + (uint32_t)h : rr * a.g.ntiles + (b >> a.g.tile_bits);
+            }
+            // heavy bins: one LDS add for the wave's majority bin
+            const uint32_t b0 = __builtin_amdgcn_readfirstlane(binid);
+            const uint64_t mm = __ballot(binid == b0 && b0 != 0xFFFFFFFFu);
+            const uint32_t cnt = __popcll(mm);
+            if (cnt >= 4) {
+                if (binid == b0 && (uint32_t)__ffsll((long long)mm) - 1 == (threadIdx.x & 63u))
+                    atomicAdd(&s_hist[b0], cnt);
+                if (binid != 0xFFFFFFFFu && binid != b0) atomicAdd(&s_hist[binid], 1u);
+            } else if (binid != 0xFFFFFFFFu) {
+                atomicAdd(&s_hist[binid], 1u);
+            }
         }
     }
     atomicAdd(&s_ok, n_ok);
@@ -335,126 +356,166 @@ struct ScatterArgs {
     unsigned long long *stats;
 };
 
-__global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
-    __shared__ uint32_t s_cnt[4][kMaxLB];   // per-wave running counts (this round)
-    __shared__ uint32_t s_rstart[kMaxLB];
-    __shared__ uint32_t s_goff[kMaxLB];
-    __shared__ uint64_t s_ent[kScRound];
-    __shared__ uint32_t s_pos[kScRound];
-    __shared__ uint32_t s_w[4];
-    __shared__ uint32_t s_total;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t blk = blockIdx.x, r = blockIdx.y;
-    const uint32_t NT = a.g.ntiles + kHot;  // local bins: tiles, then this row's hot buckets
-    const uint32_t tmask = (1u << a.g.tile_bits) - 1u;
-    for (uint32_t t = tid; t < NT; t += kScThreads) {
-        const uint64_t gb = t < a.g.ntiles ? (uint64_t)(r * a.g.ntiles + t) : (uint64_t)(a.g.nbins + r * kHot + (t - a.g.ntiles));
-        s_goff[t] = a.offsets[gb * a.nblk + blk];
-        s_cnt[0][t] = 0; s_cnt[1][t] = 0; s_cnt[2][t] = 0; s_cnt[3][t] = 0;
+// block (NW waves) exclusive scan; *total = sum
+template <int NW>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, uint32_t *total) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; w++) {
+        const uint32_t x = s_w[w];
+        if (w < wave) base += x;
+        tot += x;
     }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+// LDS layout of k_scatter (dynamic): s_cnt[kScWaves][LB], s_rstart[LB], s_goff[LB],
+// s_ent[kScRound] (u64), s_bin[kScRound] (u16)
+__host__ __device__ inline size_t scatter_lds_bytes(uint32_t LB) {
+    return ((size_t)(kScWaves + 2) * LB * 4 + 15) / 16 * 16 + (size_t)kScRound * 8 + (size_t)kScRound * 2;
+}
+
+__global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint32_t s_w[kScWaves];
+    const uint32_t LB = a.g.ntiles + kHot;  // local bins of a row: tiles, then its hot buckets
+    uint32_t *s_cnt = reinterpret_cast<uint32_t *>(smem);
+    uint32_t *s_rstart = s_cnt + kScWaves * LB;
+    uint32_t *s_goff = s_rstart + LB;
+    uint64_t *s_ent = reinterpret_cast<uint64_t *>(smem + ((size_t)(kScWaves + 2) * LB * 4 + 15) / 16 * 16);
+    uint16_t *s_bin = reinterpret_cast<uint16_t *>(s_ent + kScRound);
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t blk = blockIdx.x;
+    const uint32_t tmask = (1u << a.g.tile_bits) - 1u;
     const uint64_t beg = (uint64_t)blk * kChunk;
     const uint64_t end = min(a.n, beg + kChunk);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint64_t rb = beg; rb < end; rb += kScRound) {
+    constexpr uint32_t TPT = 3;  // local bins per thread in the scan (LB <= 1536)
+    for (uint32_t r = 0; r < a.g.d; r++) {
         __syncthreads();
-        uint64_t ent[kScItems];
-        uint32_t tile[kScItems], rank[kScItems];
-        // phase 1: per-wave stable ranks (order: slot i, then lane)
+        for (uint32_t t = tid; t < LB; t += kScThreads) {
+            const uint64_t gb = t < a.g.ntiles ? (uint64_t)(r * a.g.ntiles + t)
+                                               : (uint64_t)(a.g.nbins + r * kHot + (t - a.g.ntiles));
+            s_goff[t] = a.offsets[gb * a.nblk + blk];
+        }
+        for (uint32_t t = tid; t < kScWaves * LB; t += kScThreads) s_cnt[t] = 0;
+        for (uint64_t rb = beg; rb < end; rb += kScRound) {
+            __syncthreads();
+            uint64_t ent[kScItems];
+            uint32_t bin[kScItems], rank[kScItems];
+            // phase 1: stable per-wave ranks; wave w owns packets [rb + w*1024, +1024), order (slot, lane)
+            uint32_t ids[kScItems], bs[kScItems], szs[kScItems];
 #pragma unroll
-        for (int i = 0; i < kScItems; i++) {
-            const uint64_t p = rb + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
-            bool valid = false;
-            uint32_t t = 0;
-            uint64_t e = 0;
-            if (p < end) {
-                const uint32_t id = a.keyid[p];
-                if (id != GNS_ID_NONE) {
-                    valid = true;
-                    const uint32_t b = a.idx[(uint64_t)r * a.n + p];
-                    const bool hot = (b >> 31) != 0;
-                    const uint32_t h = b & 0x7FFFFFFFu;
-                    t = hot ? a.g.ntiles + h : (b >> a.g.tile_bits);
-                    const uint32_t low = hot ? r * kHot + h : (b & tmask);
-                    const uint32_t sz = a.sizes[p];
-                    uint32_t lo = id, sf = sz;
-                    if (sz >= kSizeEsc) {
-                        const uint32_t q = atomicAdd(a.ovf_cnt, 1u);
-                        if (q < kOvfCap) {
-                            a.ovf[q] = (uint64_t)sz << 32 | id;
-                            lo = kOvfFlag | q;
-                        } else {
-                            atomicAdd(&a.stats[4], 1ull);
-                            lo = kOvfFlag | (kOvfCap - 1);
+            for (int i = 0; i < kScItems; i++) {  // all loads up front (clamped), one latency per round
+                const uint64_t p = rb + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
+                const uint64_t pc = p < end ? p : end - 1;
+                ids[i] = a.keyid[pc];
+                bs[i] = a.idx[(uint64_t)r * a.n + pc];
+                szs[i] = a.sizes[pc];
+            }
+#pragma unroll
+            for (int i = 0; i < kScItems; i++) {
+                const uint64_t p = rb + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
+                bool valid = false;
+                uint32_t t = 0;
+                uint64_t e = 0;
+                if (p < end) {
+                    const uint32_t id = ids[i];
+                    if (id != GNS_ID_NONE) {
+                        valid = true;
+                        const uint32_t b = bs[i];
+                        const bool hot = (b >> 31) != 0;
+                        const uint32_t h = b & 0x7FFFFFFFu;
+                        t = hot ? a.g.ntiles + h : (b >> a.g.tile_bits);
+                        const uint32_t low = hot ? r * kHot + h : (b & tmask);
+                        const uint32_t sz = szs[i];
+                        uint32_t lo = id, sf = sz;
+                        if (sz >= kSizeEsc) {
+                            const uint32_t q = atomicAdd(a.ovf_cnt, 1u);
+                            if (q < kOvfCap) {
+                                a.ovf[q] = (uint64_t)sz << 32 | id;
+                                lo = kOvfFlag | q;
+                            } else {
+                                atomicAdd(&a.stats[4], 1ull);
+                                lo = kOvfFlag | (kOvfCap - 1);
+                            }
+                            sf = kSizeEsc;
                         }
-                        sf = kSizeEsc;
+                        e = (uint64_t)((sf << 12) | low) << 32 | lo;
                     }
-                    e = (uint64_t)((sf << 12) | low) << 32 | lo;
+                }
+                uint64_t peers = __ballot(valid);
+                for (uint32_t bit = 0; bit < a.g.nbits; bit++) {
+                    const uint64_t m = __ballot(valid && ((t >> bit) & 1u));
+                    peers &= ((t >> bit) & 1u) ? m : ~m;
+                }
+                uint32_t rk = 0;
+                if (valid) {
+                    const uint32_t before = __popcll(peers & lt_mask);
+                    rk = s_cnt[wave * LB + t] + before;
+                    if (before == 0) s_cnt[wave * LB + t] += __popcll(peers);
+                }
+                ent[i] = e;
+                bin[i] = valid ? t : 0xFFFFFFFFu;
+                rank[i] = rk;
+            }
+            __syncthreads();
+            // phase 2: per bin, exclusive prefix over waves; block scan over bins
+            uint32_t tot[TPT];
+            uint32_t lsum = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < TPT; j++) {
+                const uint32_t t = tid * TPT + j;
+                uint32_t c = 0;
+                if (t < LB) {
+                    for (uint32_t w = 0; w < kScWaves; w++) {
+                        const uint32_t x = s_cnt[w * LB + t];
+                        s_cnt[w * LB + t] = c;
+                        c += x;
+                    }
+                }
+                tot[j] = c;
+                lsum += c;
+            }
+            uint32_t rtotal;
+            uint32_t run = block_excl_scan<kScWaves>(lsum, s_w, &rtotal);
+#pragma unroll
+            for (uint32_t j = 0; j < TPT; j++) {
+                const uint32_t t = tid * TPT + j;
+                if (t < LB) s_rstart[t] = run;
+                run += tot[j];
+            }
+            __syncthreads();
+            // phase 3: stage in bin order
+#pragma unroll
+            for (int i = 0; i < kScItems; i++) {
+                if (bin[i] != 0xFFFFFFFFu) {
+                    const uint32_t t = bin[i];
+                    const uint32_t l = s_rstart[t] + s_cnt[wave * LB + t] + rank[i];
+                    s_ent[l] = ent[i];
+                    s_bin[l] = (uint16_t)t;
                 }
             }
-            uint64_t peers = __ballot(valid);
-            for (uint32_t bit = 0; bit < a.g.nbits; bit++) {
-                const uint64_t m = __ballot(valid && ((t >> bit) & 1u));
-                peers &= ((t >> bit) & 1u) ? m : ~m;
+            __syncthreads();
+            // phase 4: contiguous runs per bin to global
+            for (uint32_t s2 = tid; s2 < rtotal; s2 += kScThreads) {
+                const uint32_t t = s_bin[s2];
+                a.entries[s_goff[t] + (s2 - s_rstart[t])] = s_ent[s2];
             }
-            uint32_t rk = 0;
-            if (valid) {
-                const uint32_t before = __popcll(peers & lt_mask);
-                rk = s_cnt[wave][t] + before;
-                if (before == 0) s_cnt[wave][t] += __popcll(peers);
-            }
-            ent[i] = e;
-            tile[i] = valid ? t : 0xFFFFFFFFu;
-            rank[i] = rk;
-        }
-        __syncthreads();
-        // phase 2: wave prefix per tile, then block scan over tiles
-        constexpr uint32_t TPT = kMaxLB / kScThreads;  // 5 local bins per thread
-        uint32_t tot[TPT];
-        uint32_t lsum = 0;
+            __syncthreads();
 #pragma unroll
-        for (uint32_t j = 0; j < TPT; j++) {
-            const uint32_t t = tid * TPT + j;
-            uint32_t c = 0;
-            if (t < NT) {
-                const uint32_t c0 = s_cnt[0][t], c1 = s_cnt[1][t], c2 = s_cnt[2][t], c3 = s_cnt[3][t];
-                s_cnt[0][t] = 0; s_cnt[1][t] = c0; s_cnt[2][t] = c0 + c1; s_cnt[3][t] = c0 + c1 + c2;
-                c = c0 + c1 + c2 + c3;
-            }
-            tot[j] = c;
-            lsum += c;
-        }
-        uint32_t rtotal;
-        uint32_t run = block_excl_scan256(lsum, s_w, &rtotal);
-#pragma unroll
-        for (uint32_t j = 0; j < TPT; j++) {
-            const uint32_t t = tid * TPT + j;
-            if (t < NT) s_rstart[t] = run;
-            run += tot[j];
-        }
-        if (tid == 0) s_total = rtotal;
-        __syncthreads();
-        // phase 3: stage in bin order
-#pragma unroll
-        for (int i = 0; i < kScItems; i++) {
-            if (tile[i] != 0xFFFFFFFFu) {
-                const uint32_t t = tile[i];
-                const uint32_t within = s_cnt[wave][t] + rank[i];
-                const uint32_t l = s_rstart[t] + within;
-                s_ent[l] = ent[i];
-                s_pos[l] = s_goff[t] + within;
-            }
-        }
-        __syncthreads();
-        // phase 4: contiguous runs per bin to global
-        const uint32_t tot_r = s_total;
-        for (uint32_t s = tid; s < tot_r; s += kScThreads) a.entries[s_pos[s]] = s_ent[s];
-        __syncthreads();
-#pragma unroll
-        for (uint32_t j = 0; j < TPT; j++) {
-            const uint32_t t = tid * TPT + j;
-            if (t < NT) {
-                s_goff[t] += tot[j];
-                s_cnt[0][t] = 0; s_cnt[1][t] = 0; s_cnt[2][t] = 0; s_cnt[3][t] = 0;
+            for (uint32_t j = 0; j < TPT; j++) {
+                const uint32_t t = tid * TPT + j;
+                if (t < LB) {
+                    s_goff[t] += tot[j];
+                    for (uint32_t w = 0; w < kScWaves; w++) s_cnt[w * LB + t] = 0;
+                }
             }
         }
     }
@@ -527,17 +588,21 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
     }
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t *own = reinterpret_cast<uint32_t *>(accS);  // replay: lowest-lane arbitration
+    uint64_t e[kApItems], en[kApItems];
+#pragma unroll
+    for (int j = 0; j < kApItems; j++) {  // first chunk
+        const uint32_t q = beg + j * kApThreads + tid;
+        e[j] = q < end ? a.entries[q] : 0ull;
+    }
     for (uint32_t cb = beg; cb < end; cb += kApChunk) {
         if (tid == 0) s_any = 0;
         __syncthreads();
-        uint64_t e[kApItems];
         bool v[kApItems];
         // --- classify against the chunk-entry state, aggregate per bucket ---
 #pragma unroll
         for (int j = 0; j < kApItems; j++) {
             const uint32_t q = cb + j * kApThreads + tid;
             v[j] = q < end;
-            e[j] = v[j] ? a.entries[q] : 0ull;
             const uint32_t lo = (uint32_t)e[j];
             const uint32_t hi = (uint32_t)(e[j] >> 32);
             const uint32_t b = hi & (kTileMax - 1u);
@@ -572,6 +637,12 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
                 atomicAdd(&accN[b], 1ull);
                 atomicOr(&accN[b], 1ull << 63);
             }
+        }
+        // prefetch the next chunk while this one is decided / replayed
+#pragma unroll
+        for (int j = 0; j < kApItems; j++) {
+            const uint32_t q = cb + kApChunk + j * kApThreads + tid;
+            en[j] = q < end ? a.entries[q] : 0ull;
         }
         __syncthreads();
         // --- per bucket: exact aggregate update or mark for replay ---
@@ -684,6 +755,8 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
             }
         }
         __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kApItems; j++) e[j] = en[j];
     }
     for (uint32_t i = tid; i < tn; i += kApThreads) {
         a.C[cbase + i] = sC[i]; a.Fc[cbase + i] = sFc[i];
@@ -1202,7 +1275,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
         a.ovf_cnt = cm->ovf_cnt; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
         ScopedStage st(cm->timer, 3);
-        hipLaunchKernelGGL(k_scatter, dim3(nblk, g.d), dim3(kScThreads), 0, s, a);
+        hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot), s, a);
         GNS_HIP(hipGetLastError());
     }
     // K4

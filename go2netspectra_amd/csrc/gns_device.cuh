@@ -62,7 +62,7 @@ template <int B>
 __device__ __forceinline__ uint32_t rec_u32(const uint32_t (&w)[16]) {  // bytes B..B+3, LE
     static_assert(B >= 0 && B + 3 < 64, "record word out of range");
     if constexpr (B % 4 == 0) return w[B / 4];
-    else return (uint32_t)(((uint64_t)w[B / 4 + 1] << 32 | w[B / 4]) >> (8 * (B % 4)));
+    else return __builtin_amdgcn_alignbyte(w[B / 4 + 1], w[B / 4], B % 4);  // v_alignbyte_b32 funnel shift
 }
 
 enum { PARSE_OK = 0, PARSE_DROP = 1, PARSE_UNSUPPORTED = 2 };
@@ -78,11 +78,17 @@ __device__ __forceinline__ void set_ports(uint32_t (&tw)[10], uint32_t sport, ui
     tw[9] = proto;
 }
 
-// L3/L4 decode at L2 header length OFF (14 / 18 / 22 bytes).
-template <int OFF>
+// L3/L4 decode of a record whose VLAN tags were shifted out: the ethertype is
+// at bytes 12-13 and the L3 header at byte 14.  nv = number of removed tags
+// (the original L2 header length is 14 + 4*nv); lim = record bytes still
+// present (64 - 4*nv).  Offsets are compile-time constants: no dynamic
+// indexing into the record registers.
 __device__ __forceinline__ int parse_l3(const uint32_t (&w)[16], uint32_t type, uint32_t wirelen,
-                                        uint32_t (&tw)[10]) {
-    const uint32_t l2len = wirelen > (uint32_t)OFF ? wirelen - OFF : 0u;
+                                        uint32_t nv, uint32_t (&tw)[10]) {
+    constexpr int OFF = 14;
+    const uint32_t l2hdr = 14u + 4u * nv;
+    const uint32_t lim = 64u - 4u * nv;
+    const uint32_t l2len = wirelen > l2hdr ? wirelen - l2hdr : 0u;
     if (type == 0x0800u) {  // gopacket IPv4.DecodeFromBytes
         const uint32_t ihl = rec_byte<OFF>(w) & 15u;
         uint32_t tot = rec_be16<OFF + 2>(w);
@@ -99,7 +105,7 @@ __device__ __forceinline__ int parse_l3(const uint32_t (&w)[16], uint32_t type, 
         const uint32_t avail = (tot < l2len ? tot : l2len) - 20u;
         if (proto == 6u) {
             if (avail < 20) return PARSE_OK;
-            const uint32_t doff = rec_byte<OFF + 32>(w) >> 4;  // inside the record for OFF<=22
+            const uint32_t doff = rec_byte<OFF + 32>(w) >> 4;  // byte 46 < lim for nv <= 2
             if (doff < 5 || doff * 4 > avail) return PARSE_OK;
             set_ports(tw, rec_be16<OFF + 20>(w), rec_be16<OFF + 22>(w), proto);
             return PARSE_OK;
@@ -135,21 +141,12 @@ __device__ __forceinline__ int parse_l3(const uint32_t (&w)[16], uint32_t type, 
         }
         if (nh == 6u || nh == 17u) {
             if (avail < (nh == 6u ? 20u : 8u)) return PARSE_OK;
-            if constexpr (OFF + 40 + 4 > 64) {
-                return PARSE_UNSUPPORTED;  // ports beyond the record
-            } else {
-                const uint32_t sp = rec_be16<OFF + 40>(w), dp = rec_be16<OFF + 42>(w);
-                if constexpr (OFF + 40 + 12 < 64) {
-                    if (nh == 6u) {
-                        const uint32_t doff = rec_byte<OFF + 52>(w) >> 4;
-                        if (doff < 5 || doff * 4 > avail) return PARSE_OK;
-                    }
-                }
-                if (nh == 17u && (udp_tunnel_port(sp) || udp_tunnel_port(dp)))
-                    return PARSE_UNSUPPORTED;
-                set_ports(tw, sp, dp, nh);
-                return PARSE_OK;
-            }
+            if (OFF + 40 + 4 > lim) return PARSE_UNSUPPORTED;  // ports beyond the record
+            // the TCP data-offset byte (record byte 66 + 4*nv) is never inside the record
+            const uint32_t sp = rec_be16<OFF + 40>(w), dp = rec_be16<OFF + 42>(w);
+            if (nh == 17u && (udp_tunnel_port(sp) || udp_tunnel_port(dp))) return PARSE_UNSUPPORTED;
+            set_ports(tw, sp, dp, nh);
+            return PARSE_OK;
         }
         return PARSE_OK;
     }
@@ -174,12 +171,26 @@ __device__ __forceinline__ int parse_record(const uint32_t (&w)[16], uint32_t wi
         set_ports(tw, rec_be16<48>(w), rec_be16<50>(w), rec_byte<52>(w));
         return PARSE_OK;
     }
-    if (t0 != 0x8100u && t0 != 0x88A8u) return parse_l3<14>(w, t0, wirelen, tw);
-    const uint32_t t1 = rec_be16<16>(w);
-    if (t1 != 0x8100u && t1 != 0x88A8u) return parse_l3<18>(w, t1, wirelen, tw);
-    const uint32_t t2 = rec_be16<20>(w);
-    if (t2 != 0x8100u && t2 != 0x88A8u) return parse_l3<22>(w, t2, wirelen, tw);
-    return PARSE_UNSUPPORTED;
+    // gopacket Dot1Q: up to two tags (4 bytes = one word each) before the ethertype
+    uint32_t nv = 0, type = t0;
+    if (t0 == 0x8100u || t0 == 0x88A8u) {
+        const uint32_t t1 = rec_be16<16>(w);
+        nv = 1; type = t1;
+        if (t1 == 0x8100u || t1 == 0x88A8u) {
+            const uint32_t t2 = rec_be16<20>(w);
+            nv = 2; type = t2;
+            if (t2 == 0x8100u || t2 == 0x88A8u) return PARSE_UNSUPPORTED;
+        }
+    }
+    // shift the tags out: bytes 12.. move down by 4*nv (whole words from word 3 on)
+    uint32_t ws[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const uint32_t a1 = (i >= 3 && i + 1 < 16) ? w[i + 1 < 16 ? i + 1 : 15] : w[i];
+        const uint32_t a2 = (i >= 3 && i + 2 < 16) ? w[i + 2 < 16 ? i + 2 : 15] : w[i];
+        ws[i] = nv == 0 ? w[i] : (nv == 1 ? a1 : a2);
+    }
+    return parse_l3(ws, type, wirelen, nv, tw);
 }
 
 // byte idx (0..36) of the canonical tuple; 255 (or >= 40) -> 0

@@ -52,6 +52,37 @@ __device__ __forceinline__ uint32_t mm3_n(const uint32_t (&kw)[NW], uint32_t K, 
     return h;
 }
 
+// MurmurHash3 split: the per-block key mixing k*c1, rotl 15, *c2 does not depend
+// on the seed, so a key hashed under several seeds (d rows + the dictionary)
+// is mixed once (mm3_premix) and each seed only runs the cheap h-chain.
+template <int NW>
+__device__ __forceinline__ void mm3_premix(const uint32_t (&kw)[NW], uint32_t K, uint32_t (&mk)[NW]) {
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        uint32_t k = kw[i];
+        k *= c1; k = rotl32(k, 15); k *= c2;
+        mk[i] = (4u * i < K) ? k : 0u;
+    }
+}
+
+template <int NW>
+__device__ __forceinline__ uint32_t mm3_chain(const uint32_t (&mk)[NW], uint32_t K, uint32_t seed) {
+    uint32_t h = seed;
+    const uint32_t nb = K >> 2;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        if ((uint32_t)i < nb) {
+            h ^= mk[i]; h = rotl32(h, 13); h = h * 5u + 0xe6546b64u;
+        } else if ((uint32_t)i == nb && (K & 3u)) {
+            h ^= mk[i];
+        }
+    }
+    h ^= K;
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
+}
+
 // Load K key bytes at p into little-endian words (bytes >= K zero).
 template <int NW>
 __device__ __forceinline__ void load_key_bytes(const uint8_t *p, uint32_t K, bool word_ok,
