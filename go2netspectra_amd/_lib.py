@@ -10,7 +10,7 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgns_sketch.so")
+LIB_PATH = os.environ.get("GNS_LIB") or os.path.join(_HERE, "libgns_sketch.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 GNS_OK = 0
@@ -24,7 +24,7 @@ FIELD_SIZE = {"SrcIP": 16, "DstIP": 16, "SrcPort": 2, "DstPort": 2, "Protocol": 
 EXPORTED = [
     "gns_cm_create", "gns_cm_destroy", "gns_cm_insert_keys", "gns_cm_insert_tuples",
     "gns_cm_insert_headers", "gns_cm_flush", "gns_cm_query", "gns_cm_heavy_hitters", "gns_cm_reset",
-    "gns_cm_export_state", "gns_cm_stats", "gns_cm_set_timing", "gns_cm_stage_times", "gns_cm_stream",
+    "gns_cm_export_state", "gns_cm_stats", "gns_cm_counters", "gns_cm_set_timing", "gns_cm_stage_times", "gns_cm_stream",
     "gns_ss_create", "gns_ss_destroy", "gns_ss_insert_keys", "gns_ss_insert_tuples",
     "gns_ss_insert_headers", "gns_ss_flush", "gns_ss_query", "gns_ss_heavy_hitters", "gns_ss_reset",
     "gns_ss_export_state", "gns_ss_stats", "gns_ss_set_timing", "gns_ss_stage_times",
@@ -109,6 +109,7 @@ def load() -> ct.CDLL:
         "gns_cm_flush": ([vp], i32), "gns_cm_query": ([vp, vp, u32, u64, vp], i32),
         "gns_cm_heavy_hitters": ([vp, vp, vp, vp, vp, vp, vp], i32), "gns_cm_reset": ([vp], i32),
         "gns_cm_export_state": ([vp, vp, vp, vp, vp], i32), "gns_cm_stats": ([vp, vp], i32),
+        "gns_cm_counters": ([vp, vp], i32),
         "gns_cm_set_timing": ([vp, i32], i32), "gns_cm_stage_times": ([vp, vp, vp, i32], i32),
         "gns_cm_stream": ([vp], vp),
         "gns_ss_create": ([vp, vp], i32), "gns_ss_destroy": ([vp], i32),

@@ -35,12 +35,15 @@ constexpr uint32_t kOvfFlag = 0x80000000u;
 constexpr uint32_t kOvfCap = 1u << 20;
 constexpr int kExThreads = 256;
 constexpr uint32_t kChunk = 16384;                  // packets per K1/K3 block
-constexpr int kScThreads = 512;                     // K3: 8 waves
+#ifndef GNS_SC_THREADS
+#define GNS_SC_THREADS 256
+#endif
+constexpr int kScThreads = GNS_SC_THREADS;          // K3 block
 constexpr int kScWaves = kScThreads / 64;
 constexpr int kScItems = 16;
 constexpr uint32_t kScRound = kScThreads * kScItems; // 8192 updates staged in LDS per round
 constexpr int kApThreads = 1024;
-constexpr int kApItems = 4;
+constexpr int kApItems = 8;
 constexpr uint32_t kApChunk = kApThreads * kApItems; // 4096 updates per K4 step
 constexpr uint32_t kScanSeg = 4096;
 constexpr uint32_t kHot = 64;                       // designated hot buckets per row
@@ -375,20 +378,24 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, u
     return base + inc - v;
 }
 
-// LDS layout of k_scatter (dynamic): s_cnt[kScWaves][LB], s_rstart[LB], s_goff[LB],
+// LDS layout of k_scatter (dynamic): s_cnt[kScWaves][LB], s_rstart[LB], s_goff[d][LB],
 // s_ent[kScRound] (u64), s_bin[kScRound] (u16)
-__host__ __device__ inline size_t scatter_lds_bytes(uint32_t LB) {
-    return ((size_t)(kScWaves + 2) * LB * 4 + 15) / 16 * 16 + (size_t)kScRound * 8 + (size_t)kScRound * 2;
+__host__ __device__ inline size_t scatter_lds_head(uint32_t LB, uint32_t d) {
+    return ((size_t)(kScWaves + 1 + d) * LB * 4 + 15) / 16 * 16;
+}
+__host__ __device__ inline size_t scatter_lds_bytes(uint32_t LB, uint32_t d) {
+    return scatter_lds_head(LB, d) + (size_t)kScRound * 8 + (size_t)kScRound * 2;
 }
 
 __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t s_w[kScWaves];
     const uint32_t LB = a.g.ntiles + kHot;  // local bins of a row: tiles, then its hot buckets
+    const uint32_t d = a.g.d;
     uint32_t *s_cnt = reinterpret_cast<uint32_t *>(smem);
     uint32_t *s_rstart = s_cnt + kScWaves * LB;
-    uint32_t *s_goff = s_rstart + LB;
-    uint64_t *s_ent = reinterpret_cast<uint64_t *>(smem + ((size_t)(kScWaves + 2) * LB * 4 + 15) / 16 * 16);
+    uint32_t *s_goff = s_rstart + LB;  // [d][LB]
+    uint64_t *s_ent = reinterpret_cast<uint64_t *>(smem + scatter_lds_head(LB, d));
     uint16_t *s_bin = reinterpret_cast<uint16_t *>(s_ent + kScRound);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t blk = blockIdx.x;
@@ -396,59 +403,60 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
     const uint64_t beg = (uint64_t)blk * kChunk;
     const uint64_t end = min(a.n, beg + kChunk);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    constexpr uint32_t TPT = 3;  // local bins per thread in the scan (LB <= 1536)
-    for (uint32_t r = 0; r < a.g.d; r++) {
-        __syncthreads();
-        for (uint32_t t = tid; t < LB; t += kScThreads) {
-            const uint64_t gb = t < a.g.ntiles ? (uint64_t)(r * a.g.ntiles + t)
-                                               : (uint64_t)(a.g.nbins + r * kHot + (t - a.g.ntiles));
-            s_goff[t] = a.offsets[gb * a.nblk + blk];
-        }
-        for (uint32_t t = tid; t < kScWaves * LB; t += kScThreads) s_cnt[t] = 0;
-        for (uint64_t rb = beg; rb < end; rb += kScRound) {
-            __syncthreads();
-            uint64_t ent[kScItems];
-            uint32_t bin[kScItems], rank[kScItems];
-            // phase 1: stable per-wave ranks; wave w owns packets [rb + w*1024, +1024), order (slot, lane)
-            uint32_t ids[kScItems], bs[kScItems], szs[kScItems];
+    constexpr uint32_t TPT = (1536 + kScThreads - 1) / kScThreads;  // local bins per thread (LB <= 1536)
+    for (uint32_t i = tid; i < d * LB; i += kScThreads) {
+        const uint32_t r = i / LB, t = i % LB;
+        const uint64_t gb = t < a.g.ntiles ? (uint64_t)(r * a.g.ntiles + t)
+                                           : (uint64_t)(a.g.nbins + r * kHot + (t - a.g.ntiles));
+        s_goff[i] = a.offsets[gb * a.nblk + blk];
+    }
+    for (uint32_t t = tid; t < kScWaves * LB; t += kScThreads) s_cnt[t] = 0;
+    for (uint64_t rb = beg; rb < end; rb += kScRound) {
+        // flow ids and sizes once per round (clamped loads, one latency)
+        uint32_t ids[kScItems], szs[kScItems];
 #pragma unroll
-            for (int i = 0; i < kScItems; i++) {  // all loads up front (clamped), one latency per round
-                const uint64_t p = rb + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
-                const uint64_t pc = p < end ? p : end - 1;
-                ids[i] = a.keyid[pc];
-                bs[i] = a.idx[(uint64_t)r * a.n + pc];
-                szs[i] = a.sizes[pc];
-            }
+        for (int i = 0; i < kScItems; i++) {
+            const uint64_t p = rb + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
+            const uint64_t pc = p < end ? p : end - 1;
+            ids[i] = p < end ? a.keyid[pc] : GNS_ID_NONE;
+            szs[i] = a.sizes[pc];
+        }
+        for (uint32_t r = 0; r < d; r++) {
+            __syncthreads();
+            uint32_t bs[kScItems];
 #pragma unroll
             for (int i = 0; i < kScItems; i++) {
                 const uint64_t p = rb + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
-                bool valid = false;
+                bs[i] = a.idx[(uint64_t)r * a.n + (p < end ? p : end - 1)];
+            }
+            uint64_t ent[kScItems];
+            uint32_t bin[kScItems], rank[kScItems];
+            // phase 1: stable per-wave ranks; wave w owns packets [rb + w*64*kScItems, ...), order (slot, lane)
+#pragma unroll
+            for (int i = 0; i < kScItems; i++) {
+                const bool valid = ids[i] != GNS_ID_NONE;
                 uint32_t t = 0;
                 uint64_t e = 0;
-                if (p < end) {
-                    const uint32_t id = ids[i];
-                    if (id != GNS_ID_NONE) {
-                        valid = true;
-                        const uint32_t b = bs[i];
-                        const bool hot = (b >> 31) != 0;
-                        const uint32_t h = b & 0x7FFFFFFFu;
-                        t = hot ? a.g.ntiles + h : (b >> a.g.tile_bits);
-                        const uint32_t low = hot ? r * kHot + h : (b & tmask);
-                        const uint32_t sz = szs[i];
-                        uint32_t lo = id, sf = sz;
-                        if (sz >= kSizeEsc) {
-                            const uint32_t q = atomicAdd(a.ovf_cnt, 1u);
-                            if (q < kOvfCap) {
-                                a.ovf[q] = (uint64_t)sz << 32 | id;
-                                lo = kOvfFlag | q;
-                            } else {
-                                atomicAdd(&a.stats[4], 1ull);
-                                lo = kOvfFlag | (kOvfCap - 1);
-                            }
-                            sf = kSizeEsc;
+                if (valid) {
+                    const uint32_t b = bs[i];
+                    const bool hot = (b >> 31) != 0;
+                    const uint32_t h = b & 0x7FFFFFFFu;
+                    t = hot ? a.g.ntiles + h : (b >> a.g.tile_bits);
+                    const uint32_t low = hot ? r * kHot + h : (b & tmask);
+                    const uint32_t sz = szs[i];
+                    uint32_t lo = ids[i], sf = sz;
+                    if (sz >= kSizeEsc) {
+                        const uint32_t q = atomicAdd(a.ovf_cnt, 1u);
+                        if (q < kOvfCap) {
+                            a.ovf[q] = (uint64_t)sz << 32 | ids[i];
+                            lo = kOvfFlag | q;
+                        } else {
+                            atomicAdd(&a.stats[4], 1ull);
+                            lo = kOvfFlag | (kOvfCap - 1);
                         }
-                        e = (uint64_t)((sf << 12) | low) << 32 | lo;
+                        sf = kSizeEsc;
                     }
+                    e = (uint64_t)((sf << 12) | low) << 32 | lo;
                 }
                 uint64_t peers = __ballot(valid);
                 for (uint32_t bit = 0; bit < a.g.nbits; bit++) {
@@ -474,7 +482,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                 const uint32_t t = tid * TPT + j;
                 uint32_t c = 0;
                 if (t < LB) {
-                    for (uint32_t w = 0; w < kScWaves; w++) {
+                    for (uint32_t w = 0; w < (uint32_t)kScWaves; w++) {
                         const uint32_t x = s_cnt[w * LB + t];
                         s_cnt[w * LB + t] = c;
                         c += x;
@@ -504,17 +512,18 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
             }
             __syncthreads();
             // phase 4: contiguous runs per bin to global
+            uint32_t *goff = s_goff + r * LB;
             for (uint32_t s2 = tid; s2 < rtotal; s2 += kScThreads) {
                 const uint32_t t = s_bin[s2];
-                a.entries[s_goff[t] + (s2 - s_rstart[t])] = s_ent[s2];
+                a.entries[goff[t] + (s2 - s_rstart[t])] = s_ent[s2];
             }
             __syncthreads();
 #pragma unroll
             for (uint32_t j = 0; j < TPT; j++) {
                 const uint32_t t = tid * TPT + j;
                 if (t < LB) {
-                    s_goff[t] += tot[j];
-                    for (uint32_t w = 0; w < kScWaves; w++) s_cnt[w * LB + t] = 0;
+                    goff[t] += tot[j];
+                    for (uint32_t w = 0; w < (uint32_t)kScWaves; w++) s_cnt[w * LB + t] = 0;
                 }
             }
         }
@@ -546,6 +555,7 @@ __global__ __launch_bounds__(1024) void k_order(const uint32_t *offsets, uint32_
 // K4: apply one bin's updates to its LDS-resident tile, in stream order.
 // ---------------------------------------------------------------------------
 struct ApplyArgs {
+    unsigned long long *stats;  // [5] replayed updates, [6] chunks, [7] chunks with a replay
     const uint64_t *entries;
     const uint32_t *offsets;
     uint32_t nblk, nbins;
@@ -595,7 +605,7 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
         e[j] = q < end ? a.entries[q] : 0ull;
     }
     for (uint32_t cb = beg; cb < end; cb += kApChunk) {
-        if (tid == 0) s_any = 0;
+        if (tid == 0) { s_any = 0; atomicAdd(&a.stats[6], 1ull); }
         __syncthreads();
         bool v[kApItems];
         // --- classify against the chunk-entry state, aggregate per bucket ---
@@ -690,10 +700,15 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
                 if (lane == 0) s_wc[j * 16 + wave] = __popcll(bal[j]);
             }
             __syncthreads();
-            if (wave == 0) {
-                const uint32_t x = s_wc[lane];
-                const uint32_t inc = wave_incl_scan(x);
-                s_wc[lane] = inc - x;
+            if (wave == 0) {  // exclusive scan of the kApItems*16 wave counts, (item, wave) order
+                constexpr uint32_t PER = kApItems * 16 / 64;
+                uint32_t x[PER], sum = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < PER; q++) { x[q] = s_wc[lane * PER + q]; sum += x[q]; }
+                const uint32_t inc = wave_incl_scan(sum);
+                uint32_t run = inc - sum;
+#pragma unroll
+                for (uint32_t q = 0; q < PER; q++) { s_wc[lane * PER + q] = run; run += x[q]; }
                 if (lane == 63) s_nlist = inc;
             }
             __syncthreads();
@@ -702,18 +717,22 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
                 if (need[j]) s_list[s_wc[j * 16 + wave] + __popcll(bal[j] & lt_mask)] = (uint16_t)(j * kApThreads + tid);
             __syncthreads();
             const uint32_t nlist = s_nlist;
-            // --- sequential replay (count_min.go:180-235) by wave 0, in order;
-            //     lanes of one 64-item group hitting distinct buckets run in
-            //     parallel, same-bucket lanes in lane order ---
-            if (wave == 0) {
-                for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
-                    const uint32_t i = g0 + lane;
-                    bool pending = i < nlist;
-                    uint32_t b = 0, k = 0, s = 0, rf = 0;
+            if (tid == 0) { atomicAdd(&a.stats[5], (unsigned long long)nlist); atomicAdd(&a.stats[7], 1ull); }
+            // --- sequential replay (count_min.go:180-235), in order.  Buckets are
+            //     partitioned over the 16 waves (b % 16); each wave walks the
+            //     list in order and applies its buckets' updates; lanes of one
+            //     64-item group hitting distinct buckets run in parallel,
+            //     same-bucket lanes in lane order (lowest lane wins a round).
+            for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
+                const uint32_t i = g0 + lane;
+                bool pending = false;
+                uint32_t b = 0, k = 0, s = 0, rf = 0;
+                if (i < nlist) {
+                    const uint64_t ee = a.entries[cb + s_list[i]];
+                    b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
+                    pending = (b & 15u) == wave;
                     if (pending) {
-                        const uint64_t ee = a.entries[cb + s_list[i]];
                         const uint32_t lo = (uint32_t)ee, hi = (uint32_t)(ee >> 32);
-                        b = hi & (kTileMax - 1u);
                         if (lo & kOvfFlag) {
                             const uint64_t ov = a.ovf[lo & ~kOvfFlag];
                             k = (uint32_t)ov; s = (uint32_t)(ov >> 32);
@@ -722,36 +741,38 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
                         }
                         rf = (uint32_t)accN[b];
                     }
-                    while (__ballot(pending)) {
-                        if (pending) atomicMax(&own[b], 64u - lane);
-                        const bool win = pending && own[b] == 64u - lane;
-                        if (win) {
-                            if (rf & 2u) {  // size half, count_min.go:181-209
-                                uint32_t S = sS[b], F = sFs[b];
-                                if (S == 0) { S = s; F = k; }
-                                else if (F == k) S = S + s;
-                                else if (s > S) { S = s; F = k; }
-                                else S = S - s;
-                                sS[b] = S; sFs[b] = F;
-                            }
-                            if (rf & 1u) {  // count half, count_min.go:211-235
-                                uint32_t C = sC[b], F = sFc[b];
-                                if (C == 0) { C = 1; F = k; }
-                                else if (F == k) C = C + 1;
-                                else { C = C - 1; if (C == 0) F = k; }
-                                sC[b] = C; sFc[b] = F;
-                            }
-                            own[b] = 0;
-                            pending = false;
+                }
+                while (__ballot(pending)) {
+                    if (pending) atomicMax(&own[b], 64u - lane);
+                    const bool win = pending && own[b] == 64u - lane;
+                    if (win) {
+                        if (rf & 2u) {  // size half, count_min.go:181-209
+                            uint32_t S = sS[b], F = sFs[b];
+                            if (S == 0) { S = s; F = k; }
+                            else if (F == k) S = S + s;
+                            else if (s > S) { S = s; F = k; }
+                            else S = S - s;
+                            sS[b] = S; sFs[b] = F;
                         }
+                        if (rf & 1u) {  // count half, count_min.go:211-235
+                            uint32_t C = sC[b], F = sFc[b];
+                            if (C == 0) { C = 1; F = k; }
+                            else if (F == k) C = C + 1;
+                            else { C = C - 1; if (C == 0) F = k; }
+                            sC[b] = C; sFc[b] = F;
+                        }
+                        own[b] = 0;
+                        pending = false;
                     }
                 }
             }
-            __syncthreads();
-            for (uint32_t i = tid; i < nlist; i += kApThreads) {
-                const uint32_t pos = s_list[i];
-                const uint32_t b = (uint32_t)(a.entries[cb + pos] >> 32) & (kTileMax - 1u);
-                accN[b] = 0;
+            // this wave's buckets are done: clear their replay flags
+            for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
+                const uint32_t i = g0 + lane;
+                if (i < nlist) {
+                    const uint32_t b = (uint32_t)(a.entries[cb + s_list[i]] >> 32) & (kTileMax - 1u);
+                    if ((b & 15u) == wave) accN[b] = 0;
+                }
             }
         }
         __syncthreads();
@@ -1275,7 +1296,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
         a.ovf_cnt = cm->ovf_cnt; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
         ScopedStage st(cm->timer, 3);
-        hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot), s, a);
+        hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
         GNS_HIP(hipGetLastError());
     }
     // K4
@@ -1285,6 +1306,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
             hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, s, cm->hist, nblk, g.nbins, g.nbins_all,
                                cm->total, cm->order);
         ApplyArgs a{};
+        a.stats = cm->stats;
         a.entries = cm->entries; a.offsets = cm->hist; a.nblk = nblk; a.nbins = g.nbins;
         a.total = cm->total; a.order = ordered ? cm->order : nullptr; a.ovf = cm->ovf; a.g = g;
         a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs;
@@ -1687,6 +1709,16 @@ int gns_cm_stats(gns_cm *cm, uint64_t stats[4]) {
         for (uint64_t i = 0; i < m; i++) occ += buf[i * cm->D.RW] != 0;
     }
     stats[3] = occ;
+    return GNS_OK;
+}
+
+int gns_cm_counters(gns_cm *cm, uint64_t out[8]) {
+    if (!cm || !out) return GNS_E_ARG;
+    GNS_TRY(set_dev(cm));
+    GNS_HIP(hipStreamSynchronize(cm->stream));
+    unsigned long long h[8];
+    GNS_HIP(hipMemcpy(h, cm->stats, sizeof(h), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 8; i++) out[i] = h[i];
     return GNS_OK;
 }
 

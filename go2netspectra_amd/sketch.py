@@ -213,6 +213,13 @@ class CountMin:
         check(self._L.gns_cm_stats(self._h, s))
         return {"inserted": s[0], "dropped": s[1], "unsupported": s[2], "flows": s[3]}
 
+    def counters(self) -> dict:
+        c = (ct.c_uint64 * 8)()
+        check(self._L.gns_cm_counters(self._h, c))
+        names = ["inserted", "dropped", "unsupported", "dict_full", "ovf_full", "replayed", "chunks",
+                 "chunks_replay"]
+        return dict(zip(names, list(c)))
+
     def set_timing(self, on: bool = True) -> None:
         check(self._L.gns_cm_set_timing(self._h, 1 if on else 0))
 

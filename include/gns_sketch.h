@@ -130,6 +130,10 @@ int gns_cm_stats(gns_cm *cm, uint64_t stats[4]);
  * since the last call with reset != 0.  Stages: 0 extract, 1 resolve, 2 scan,
  * 3 scatter, 4 apply, 5 total insert, 6 hot-bucket aggregate/decide/fallback,
  * 7 hot-bucket designation.  Enabled by gns_cm_set_timing(cm, 1). */
+/* raw engine counters: [0] inserted, [1] dropped, [2] unsupported, [3] dictionary
+ * full, [4] size-overflow full, [5] tile updates replayed sequentially,
+ * [6] tile chunks, [7] tile chunks with a replay */
+int gns_cm_counters(gns_cm *cm, uint64_t out[8]);
 int gns_cm_set_timing(gns_cm *cm, int on);
 int gns_cm_stage_times(gns_cm *cm, double ms[8], uint64_t launches[8], int reset);
 void *gns_cm_stream(gns_cm *cm); /* hipStream_t the handle launches on */

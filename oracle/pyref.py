@@ -186,7 +186,10 @@ def go_pow_int(x: float, y: float) -> float:
     if y < 0:
         a1 = 1 / a1
         ae = -ae
-    return math.ldexp(a1, ae)  # exact for the (normal-range) values SuperSpread reaches
+    try:
+        return math.ldexp(a1, ae)  # single rounding, like Go's Ldexp (also for subnormals)
+    except OverflowError:
+        return math.inf
 
 
 class SuperSpreadSeq:

@@ -170,3 +170,50 @@ def test_hot_designation_takeover(gpu, oracle, w):
         assert_same_state(cm, orc)
     st = cm.stage_times()
     assert "hot" in st
+
+
+def test_golden_stream_fixture(gpu):
+    """The committed oracle fixture (tests/golden/cm_stream.npz) through the engine."""
+    import os
+    from go2netspectra_amd import CountMin
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "cm_stream.npz"))
+    w, d, st, ct, K = (int(x) for x in z["params"])
+    cm = CountMin(w, d, st, ct, key_bytes=K, seeds=z["seeds"])
+    cm.insert_keys(z["keys"], z["sizes"])
+    cm.flush()
+    C, S, Fc, Fs = cm.export_state()
+    assert np.array_equal(C, z["C"]) and np.array_equal(S, z["S"])
+    assert np.array_equal(Fc, z["FPc"]) and np.array_equal(Fs, z["FPs"])
+    hh = cm.heavy_hitters()
+    assert [h.Count for h in hh.Count] == z["hh_count"].tolist()
+    assert [h.Flow for h in hh.Count] == [bytes(x).ljust(K, b"\0") for x in z["hh_count_flows"]]
+    assert [h.Size for h in hh.Size] == z["hh_size"].tolist()
+
+
+def test_manager_task_surface(gpu, oracle):
+    """factory -> Manager -> SketchTask path (model.Task surface) on header batches."""
+    from go2netspectra_amd import HeaderBatch, Manager, parse_config
+    cfg = parse_config("""
+aggregator:
+  types: ["sketch"]
+  sketch:
+    tasks:
+      - {name: cm5, skt_type: 0, flow_fields: [SrcIP, DstIP, SrcPort, DstPort, Protocol], width: 4096, depth: 4,
+         size_thereshold: 100000, count_thereshold: 50}
+      - {name: cmsrc, skt_type: 0, flow_fields: [SrcIP], width: 1000, depth: 2, size_thereshold: 200000,
+         count_thereshold: 100}
+""")
+    seeds = np.array([11, 22, 33, 44], np.uint32)
+    mgr = Manager(cfg, seeds=seeds)
+    mgr.start()
+    rng = np.random.default_rng(77)
+    t = random_tuples(rng, 50_000, 2000)
+    hdr = frames_from_tuples(t)
+    mgr.process(HeaderBatch(hdr, t["length"]))
+    snaps = mgr.stop()
+    for task, K, w, d, st, ctr in (("cm5", 37, 4096, 4, 100000, 50), ("cmsrc", 16, 1000, 2, 200000, 100)):
+        fields = [x.FlowFields for x in cfg.Aggregator.Sketch.Tasks if x.Name == task][0]
+        o = oracle.CountMin(w, d, st, ctr, K, seeds)
+        o.insert_hdr64(hdr, t["length"], fields)
+        assert [(h.Flow, h.Count) for h in snaps[task].Count] == o.heavy("count")
+        assert [(h.Flow, h.Size) for h in snaps[task].Size] == o.heavy("size")

@@ -1,0 +1,88 @@
+"""CPU, world_size 2 over gloo: the multi-GPU path's sharding + per-window
+heavy-hitter all-gather.  Each rank runs an exact sketch of its flow shard
+(the C oracle stands in for the GPU engine here) and the merged heavy-hitter
+list must equal the union of the per-shard lists computed in one process."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _stream(n=20_000):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import random_tuples
+    return random_tuples(np.random.default_rng(123), n, 400)
+
+
+def _shard_sketch(batch, rank, world):
+    from go2netspectra_amd.dist import split_batch
+    from go2netspectra_amd.sketch import HeavyCount, HeavyRecord, HeavySize
+    from oracle import oracle as orc
+    part = split_batch(batch, world)[rank]
+    cm = orc.CountMin(512, 3, 50_000, 40, 16, np.array([1, 2, 3], np.uint32))
+    if len(part):
+        cm.insert_keys(part.keys(["SrcIP"]), part.length)
+    return HeavyRecord(Size=[HeavySize(f, v) for f, v in cm.heavy("size")],
+                       Count=[HeavyCount(f, v) for f, v in cm.heavy("count")]), len(part)
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from go2netspectra_amd.dist import allgather_heavy
+    from go2netspectra_amd.packets import PacketBatch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = _stream()
+    batch = PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"])
+    hh, n = _shard_sketch(batch, rank, world)
+    merged = allgather_heavy(hh, world)
+    if rank == 0:
+        q.put(([(h.Flow, h.Count) for h in merged.Count], [(h.Flow, h.Size) for h in merged.Size]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_shard_and_allgather():
+    import sys
+    sys.path.insert(0, ROOT)
+    from go2netspectra_amd.dist import merge_heavy
+    from go2netspectra_amd.packets import PacketBatch
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got_c, got_s = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single-process reference: union of the per-shard lists
+    t = _stream()
+    batch = PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"])
+    lists_c, lists_s, total = [], [], 0
+    for r in range(world):
+        hh, n = _shard_sketch(batch, r, world)
+        lists_c.append([(h.Flow, h.Count) for h in hh.Count])
+        lists_s.append([(h.Flow, h.Size) for h in hh.Size])
+        total += n
+    assert total == len(batch)
+    assert got_c == merge_heavy(lists_c) and got_s == merge_heavy(lists_s)
+    assert len(got_c) > 0

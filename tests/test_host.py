@@ -1,0 +1,145 @@
+"""CPU: the C ABI library loads and exports every declared symbol; host-side
+mirror of the reference plugin surface (config keys, factory, DecodeFlow,
+key encoding, pcap packer, shard routing); the product fails loudly without
+a GPU."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import go2netspectra_amd as g
+from go2netspectra_amd import _lib
+from go2netspectra_amd.dist import shard_of
+from oracle import pyref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "gns_sketch.h")).read()
+    return sorted(set(re.findall(r"\b(gns_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.LIB_PATH
+    assert os.path.exists(lib), "build the library first (__graft_entry__.build())"
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (gns_[a-z0-9_]+)", out))
+    missing = [s for s in header_symbols() if s not in exported]
+    assert not missing, missing
+    assert set(_lib.EXPORTED) <= exported
+    L = g.load()  # binds every signature
+    assert L.gns_version().startswith(b"gns-sketch")
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(g.GnsError) as e:
+        g.CountMin(256, 2, key_bytes=16)
+    assert "NODEV" in str(e.value)
+
+
+def test_config_yaml_keys():
+    cfg = g.parse_config("""
+aggregator:
+  types: ["sketch"]
+  period: "60s"
+  num_workers: 16
+  sketch:
+    tasks:
+      - name: "cm_src_left"
+        skt_type: 0
+        flow_fields: ["SrcIP"]
+        element_fields: ["DstIP", "SrcPort", "DstPort", "Protocol"]
+        width: ${GNS_TEST_WIDTH}
+        depth: 2
+        size_thereshold: 4096000
+        count_thereshold: 4096
+      - name: "ss_src_dst"
+        skt_type: 1
+        flow_fields: ["SrcIP"]
+        element_fields: ["DstIP"]
+        width: 32768
+        depth: 2
+        count_thereshold: 1
+        m : 128
+        size: 5
+        b: 1.08
+        base: 0.5
+""".replace("${GNS_TEST_WIDTH}", "32768"))
+    t0, t1 = cfg.Aggregator.Sketch.Tasks
+    assert (t0.Name, t0.SketchType, t0.Width, t0.Depth, t0.SizeThreshold, t0.CountThreshold) == \
+        ("cm_src_left", 0, 32768, 2, 4096000, 4096)
+    assert (t1.SketchType, t1.M, t1.Size, t1.B, t1.Base, t1.CountThreshold) == (1, 128, 5, 1.08, 0.5, 1)
+    assert cfg.Aggregator.Types == ["sketch"] and cfg.Aggregator.NumWorkers == 16
+
+
+def test_config_env_expansion(monkeypatch):
+    monkeypatch.setenv("GNS_W", "4096")
+    cfg = g.parse_config("aggregator:\n  types: [sketch]\n  sketch:\n    tasks:\n      - name: x\n        width: ${GNS_W}\n")
+    assert cfg.Aggregator.Sketch.Tasks[0].Width == 4096
+
+
+def test_factory_registry():
+    with pytest.raises(RuntimeError):  # task_factory.go:25-27 panics on duplicates
+        g.register_aggregator("sketch", lambda cfg: None)
+    cfg = g.parse_config("aggregator:\n  types: [nosuch]\n")
+    with pytest.raises(KeyError):
+        g.create(cfg)
+
+
+def test_decode_flow_matches_go_formatting():
+    from go2netspectra_amd.packets import ip_slot
+    # an IPv4 key is 4 bytes + 12 zero bytes: Go's net.IP(16 bytes).String() prints it as IPv6
+    flow = ip_slot(bytes([192, 0, 2, 1])) + bytes([0x30, 0x39, 0x01, 0xbb, 6])
+    assert g.decode_flow(flow, ["SrcIP", "SrcPort", "DstPort", "Protocol"]) == "c000:201:: 12345 443 6"
+    mapped = bytes(10) + b"\xff\xff" + bytes([10, 1, 2, 3])
+    assert g.decode_flow(mapped, ["DstIP"]) == "10.1.2.3"
+    v6 = bytes.fromhex("20010db8000000000000000000000001")
+    assert g.decode_flow(v6, ["SrcIP"]) == "2001:db8::1"
+
+
+def test_packet_batch_keys_match_reference_encoding():
+    rng = np.random.default_rng(0)
+    from helpers import random_tuples
+    t = random_tuples(rng, 200, 50, v6_frac=0.3)
+    b = g.PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"])
+    for fields in (["SrcIP"], ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"], ["DstPort", "SrcIP"]):
+        keys = b.keys(fields)
+        for i in range(0, 200, 17):
+            want = pyref.encode_key(fields, bytes(t["src16"][i]), bytes(t["dst16"][i]), int(t["sport"][i]),
+                                    int(t["dport"][i]), int(t["proto"][i]))
+            assert bytes(keys[i]) == want
+
+
+def test_pcap_packer_roundtrip(tmp_path):
+    from helpers import frame64
+    rng = np.random.default_rng(2)
+    frames, wl = [], []
+    for i in range(300):
+        ln = int(rng.integers(60, 1500))
+        full = frame64(rng.integers(0, 256, 16, dtype=np.uint8), rng.integers(0, 256, 16, dtype=np.uint8),
+                       int(rng.integers(0, 65536)), int(rng.integers(0, 65536)), 6, ln) + bytes(max(0, ln - 64))
+        cap = full[: int(rng.integers(40, len(full) + 1))]  # snaplen truncation
+        frames.append(cap)
+        wl.append(ln)
+    path = str(tmp_path / "t.pcap")
+    g.write_pcap(path, frames, wl)
+    hb = g.read_pcap(path)
+    assert len(hb) == 300
+    for i, fr in enumerate(frames):
+        c = min(64, len(fr))
+        assert bytes(hb.hdr[i, :c]) == fr[:c] and not hb.hdr[i, c:].any()
+        assert hb.wirelen[i] == wl[i]
+
+
+def test_shard_of_is_mm3_of_src_slot(oracle):
+    rng = np.random.default_rng(4)
+    src = rng.integers(0, 256, (500, 16), dtype=np.uint8)
+    sh = shard_of(src, 8)
+    for i in range(0, 500, 7):
+        assert sh[i] == oracle.mm3(bytes(src[i]), 0xA5A5A5A5) % 8

@@ -1,0 +1,134 @@
+"""CPU: the oracle pinned against the golden vectors, and the two independent
+restatements (C oracle vs pure-Python pyref) against each other."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import pyref
+from helpers import sizes_u32, zipf_keys
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_mm3_public_kats(oracle):
+    kat = json.load(open(os.path.join(GOLD, "mm3_kat.json")))
+    for v in kat["vectors"]:
+        d = bytes.fromhex(v["data"])
+        want = int(v["hash"], 16)
+        assert oracle.mm3(d, v["seed"]) == want
+        assert pyref.mm3(d, v["seed"]) == want
+
+
+@pytest.mark.parametrize("h", ["c", "py"])
+def test_mm3_smhasher_verification(oracle, h):
+    fn = oracle.mm3 if h == "c" else pyref.mm3
+    key = bytearray(256)
+    hashes = bytearray()
+    for i in range(256):
+        key[i] = i
+        hashes += fn(bytes(key[:i]), 256 - i).to_bytes(4, "little")
+    want = int(json.load(open(os.path.join(GOLD, "mm3_kat.json")))["smhasher_verification"], 16)
+    assert fn(bytes(hashes), 0) == want
+
+
+def test_mm3_random_c_vs_python(oracle):
+    rng = np.random.default_rng(1)
+    for n in list(range(0, 40)) + [74]:
+        for _ in range(5):
+            d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            s = int(rng.integers(0, 2**32))
+            assert oracle.mm3(d, s) == pyref.mm3(d, s)
+
+
+def test_hand_traces(oracle):
+    """count_min.go state machine, hand-derived expectations (tests/golden/cm_traces.json)."""
+    tr = json.load(open(os.path.join(GOLD, "cm_traces.json")))
+    for t in tr["traces"]:
+        c = oracle.CountMin(1, 1, 1, 1, 4, np.array([7], np.uint32))
+        for (k, s), st in zip(t["updates"], t["states"]):
+            c.insert_keys(np.frombuffer(k.encode(), np.uint8).reshape(1, 4), np.array([s], np.uint32))
+            C, S, Fc, Fs = c.export()
+            assert [int(C[0]), bytes(Fc[0]).decode(), int(S[0]), bytes(Fs[0]).decode()] == st, t["name"]
+
+
+def test_parse_vectors(oracle):
+    pv = json.load(open(os.path.join(GOLD, "parse_vectors.json")))
+    for v in pv["vectors"]:
+        st, src, dst, sp, dp, pr = oracle.parse_hdr64(bytes.fromhex(v["record"]), v["wirelen"])
+        assert st == v["status"], v["name"]
+        if st == 0:
+            assert (src.hex(), dst.hex(), sp, dp, pr) == (v["src16"], v["dst16"], v["sport"], v["dport"],
+                                                          v["proto"]), v["name"]
+
+
+@pytest.mark.parametrize("w,d,K,nflows,n", [(16, 2, 4, 30, 3000), (64, 3, 13, 200, 5000), (7, 4, 37, 50, 4000),
+                                            (1, 1, 0, 1, 500)])
+def test_countmin_c_vs_python(oracle, w, d, K, nflows, n):
+    rng = np.random.default_rng(w + K)
+    keys, flows, _ = zipf_keys(rng, n, nflows, K)
+    sizes = sizes_u32(rng, n, big_frac=0.02)
+    seeds = rng.integers(0, 2**32, d, dtype=np.uint64).astype(np.uint32)
+    c = oracle.CountMin(w, d, 500, 5, K, seeds)
+    c.insert_keys(keys, sizes)
+    p = pyref.CountMinSeq(w, d, 500, 5, K, seeds.tolist())
+    for k, s in zip(keys, sizes):
+        p.insert(bytes(k), int(s))
+    C, S, Fc, Fs = c.export()
+    assert C.tolist() == p.C and S.tolist() == p.S
+    assert [bytes(x) for x in Fc] == p.Fc and [bytes(x) for x in Fs] == p.Fs
+    for f in flows[:50]:
+        assert c.query(bytes(f)) == p.query(bytes(f))
+    assert c.heavy("count") == p.heavy("count") and c.heavy("size") == p.heavy("size")
+
+
+def test_superspread_c_vs_python(oracle):
+    rng = np.random.default_rng(3)
+    flows = rng.integers(0, 256, (20, 16), dtype=np.uint8)
+    fl = flows[rng.integers(0, 20, 2000)]
+    el = rng.integers(0, 256, (2000, 8), dtype=np.uint8)
+    seeds = np.array([5, 6, 7], np.uint32)
+    c = oracle.SuperSpread(32, 3, 10, 16, 5, 0.5, 1.08, 16, 8, seeds, 99, 1234)
+    c.insert(fl, el)
+    p = pyref.SuperSpreadSeq(32, 3, 10, 16, 5, 0.5, 1.08, 16, 8, seeds.tolist(), 99, 1234)
+    for f, e in zip(fl, el):
+        p.insert(bytes(f), bytes(e))
+    values, keys, regs, pbits = c.export()
+    assert values.tolist() == p.values
+    assert [bytes(k) for k in keys] == p.keys
+    assert regs.tolist() == p.regs
+    assert pbits.tolist() == p.pbits
+    assert c.heavy() == p.heavy()
+    for f in flows:
+        assert c.query(bytes(f)) == p.query(bytes(f))
+
+
+def test_go_pow_integer_path(oracle):
+    L = oracle.lib()
+    for base in (0.5, 1.08, 2.0, 0.9, 1.5):
+        for e in list(range(-80, 81)) + [-1000, -5000, 300]:
+            got = L.or_go_pow(base, float(e))
+            assert got == pyref.go_pow_int(base, float(e))
+            if base in (0.5, 2.0) and abs(e) <= 1000:
+                assert got == base ** e  # powers of two are exact under any algorithm
+
+
+def test_golden_streams_reproduced(oracle):
+    z = np.load(os.path.join(GOLD, "cm_stream.npz"))
+    w, d, st, ct, K = (int(x) for x in z["params"])
+    c = oracle.CountMin(w, d, st, ct, K, z["seeds"])
+    c.insert_keys(z["keys"], z["sizes"])
+    C, S, Fc, Fs = c.export()
+    assert np.array_equal(C, z["C"]) and np.array_equal(S, z["S"])
+    assert np.array_equal(Fc, z["FPc"]) and np.array_equal(Fs, z["FPs"])
+    assert [v for _, v in c.heavy("count")] == z["hh_count"].tolist()
+    s = np.load(os.path.join(GOLD, "ss_stream.npz"))
+    w, d, thr, m, size, kf, ke = (int(x) for x in s["params"])
+    base, b = (float(x) for x in s["fparams"])
+    hm, rs = (int(x) for x in s["seeds64"])
+    ss = oracle.SuperSpread(w, d, thr, m, size, base, b, kf, ke, s["seeds"], hm, rs)
+    ss.insert(s["flows"], s["elems"])
+    values, keys, regs, pbits = ss.export()
+    assert np.array_equal(values, s["values"]) and np.array_equal(regs, s["regs"])
+    assert np.array_equal(pbits, s["pbits"]) and np.array_equal(keys, s["keys"])
