@@ -1,0 +1,138 @@
+// Package sketchgpu binds Go2NetSpectra's sketch aggregator to the MI355X engine
+// (libgns_sketch.so, C ABI in include/gns_sketch.h) through cgo.
+//
+// It provides:
+//   - CountMin: a statistic.Sketch (internal/engine/impl/sketch/statistic/sketch.go:5-10)
+//     whose Insert/Query/HeavyHitters/Reset run on the GPU, plus InsertBatch for the
+//     batched path;
+//   - a "sketch_gpu" aggregator registered with factory.RegisterAggregator
+//     (internal/factory/task_factory.go:24) whose Task batches PacketInfo and submits them
+//     with gns_cm_insert_tuples instead of one CAS insert per packet per worker.
+//
+// Build: CGO_CFLAGS="-I<repo>/include" CGO_LDFLAGS="-L<repo>/go2netspectra_amd -lgns_sketch".
+// Not compiled in the build container (no Go toolchain there).
+package sketchgpu
+
+/*
+#cgo LDFLAGS: -lgns_sketch
+#include <stdlib.h>
+#include "gns_sketch.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"unsafe"
+
+	"Go2NetSpectra/internal/engine/impl/sketch/statistic"
+)
+
+var fieldIDs = map[string]C.uint8_t{"SrcIP": 1, "DstIP": 2, "SrcPort": 3, "DstPort": 4, "Protocol": 5}
+
+func lastErr(rc C.int) error {
+	if rc == C.GNS_OK {
+		return nil
+	}
+	return errors.New(C.GoString(C.gns_last_error()))
+}
+
+// CountMin mirrors statistic.CountMin (count_min.go) on one GPU.
+type CountMin struct {
+	h        *C.gns_cm
+	keyBytes int
+}
+
+// NewCountMin replaces statistic.NewCountMin (count_min.go:128-172); seeds are injected.
+func NewCountMin(width, depth, st, ct uint32, flowFields []string, keyBytes uint32, seeds []uint32,
+	maxFlows uint64, device int) (*CountMin, error) {
+	var p C.gns_cm_params
+	p.width, p.depth = C.uint32_t(width), C.uint32_t(depth)
+	p.size_threshold, p.count_threshold = C.uint32_t(st), C.uint32_t(ct)
+	p.flow.n_fields = C.uint32_t(len(flowFields))
+	for i, f := range flowFields {
+		p.flow.fields[i] = fieldIDs[f]
+	}
+	p.key_bytes = C.uint32_t(keyBytes)
+	if len(seeds) > 0 {
+		p.seeds = (*C.uint32_t)(unsafe.Pointer(&seeds[0]))
+	}
+	p.max_flows = C.uint64_t(maxFlows)
+	p.device = C.int(device)
+	var h *C.gns_cm
+	if err := lastErr(C.gns_cm_create(&p, &h)); err != nil {
+		return nil, err
+	}
+	return &CountMin{h: h, keyBytes: int(keyBytes)}, nil
+}
+
+// Insert implements statistic.Sketch for one packet (a batch of one; prefer InsertBatch).
+func (c *CountMin) Insert(flow, elem []byte, size uint32) {
+	_ = c.InsertBatch(flow, uint32(len(flow)), []uint32{size})
+}
+
+// InsertBatch: keys is n*stride bytes, sizes n entries, applied in order.
+func (c *CountMin) InsertBatch(keys []byte, stride uint32, sizes []uint32) error {
+	if len(sizes) == 0 {
+		return nil
+	}
+	return lastErr(C.gns_cm_insert_keys(c.h, (*C.uint8_t)(unsafe.Pointer(&keys[0])), C.uint32_t(stride),
+		(*C.uint32_t)(unsafe.Pointer(&sizes[0])), C.uint64_t(len(sizes)), C.GNS_MEM_HOST))
+}
+
+// InsertTuples: PacketInfo batch as SoA (task.go:156-169 for a whole batch).
+func (c *CountMin) InsertTuples(src16, dst16 []byte, sport, dport []uint16, proto []uint8, length []uint32) error {
+	n := len(length)
+	if n == 0 {
+		return nil
+	}
+	t := C.gns_tuples{
+		src16: (*C.uint8_t)(unsafe.Pointer(&src16[0])), dst16: (*C.uint8_t)(unsafe.Pointer(&dst16[0])),
+		sport: (*C.uint16_t)(unsafe.Pointer(&sport[0])), dport: (*C.uint16_t)(unsafe.Pointer(&dport[0])),
+		proto: (*C.uint8_t)(unsafe.Pointer(&proto[0])), length: (*C.uint32_t)(unsafe.Pointer(&length[0])),
+	}
+	return lastErr(C.gns_cm_insert_tuples(c.h, &t, C.uint64_t(n), C.GNS_MEM_HOST))
+}
+
+// Query implements statistic.Sketch (count_min.go:240-254).
+func (c *CountMin) Query(flow []byte) uint64 {
+	if len(flow) != c.keyBytes || len(flow) == 0 {
+		return 0
+	}
+	var out C.uint64_t
+	if C.gns_cm_query(c.h, (*C.uint8_t)(unsafe.Pointer(&flow[0])), C.uint32_t(len(flow)), 1, &out) != C.GNS_OK {
+		return 0
+	}
+	return uint64(out)
+}
+
+// HeavyHitters implements statistic.Sketch (count_min.go:259-327).
+func (c *CountMin) HeavyHitters() statistic.HeavyRecord {
+	var nc, ns C.uint64_t
+	if C.gns_cm_heavy_hitters(c.h, nil, nil, &nc, nil, nil, &ns) != C.GNS_OK {
+		return statistic.HeavyRecord{Size: []statistic.HeavySize{}, Count: []statistic.HeavyCount{}}
+	}
+	K := c.keyBytes
+	cf := make([]byte, int(nc)*K+1)
+	cv := make([]uint32, int(nc)+1)
+	sf := make([]byte, int(ns)*K+1)
+	sv := make([]uint32, int(ns)+1)
+	C.gns_cm_heavy_hitters(c.h, (*C.uint8_t)(unsafe.Pointer(&cf[0])), (*C.uint32_t)(unsafe.Pointer(&cv[0])), &nc,
+		(*C.uint8_t)(unsafe.Pointer(&sf[0])), (*C.uint32_t)(unsafe.Pointer(&sv[0])), &ns)
+	rec := statistic.HeavyRecord{Size: make([]statistic.HeavySize, 0, int(ns)),
+		Count: make([]statistic.HeavyCount, 0, int(nc))}
+	for i := 0; i < int(ns); i++ {
+		rec.Size = append(rec.Size, statistic.HeavySize{Flow: append([]byte(nil), sf[i*K:(i+1)*K]...), Size: sv[i]})
+	}
+	for i := 0; i < int(nc); i++ {
+		rec.Count = append(rec.Count, statistic.HeavyCount{Flow: append([]byte(nil), cf[i*K:(i+1)*K]...), Count: cv[i]})
+	}
+	return rec
+}
+
+// Reset implements statistic.Sketch (count_min.go:330-346).
+func (c *CountMin) Reset() { C.gns_cm_reset(c.h) }
+
+// Close releases the device sketch.
+func (c *CountMin) Close() { C.gns_cm_destroy(c.h) }
+
+var _ statistic.Sketch = (*CountMin)(nil)
