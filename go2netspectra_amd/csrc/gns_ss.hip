@@ -1,23 +1,873 @@
-// gns_ss.hip -- SuperSpread engine (super_spread.go).  Placeholder entry points
-// until the device implementation lands; every call reports GNS_E_RANGE.
-#include "gns_common.hpp"
+// gns_ss.hip -- MI355X engine for Go2NetSpectra's SuperSpread
+// (internal/engine/impl/sketch/statistic/super_spread.go).
+//
+// Semantics: the device state equals super_spread.go fed the same packets in
+// the same order by ONE worker, with each GeneralHLL's seeds[0..1] derived from
+// a master seed and rand.Float64() replaced by the declared counter-based
+// generator ss_uniform(rng_seed, packet, row, draw).
+//
+// What is order-dependent, and how it is made parallel:
+//   * HLL register updates (:90-103): a packet "encodes" iff its geometric
+//     value lz exceeds the register's value at its time, i.e. the exclusive
+//     prefix max of earlier updates to the same (cell, register).  Only
+//     packets with lz > the batch-entry register can encode (registers only
+//     grow): they are emitted as candidates, radix-sorted by (cell, register,
+//     packet) and a segmented inclusive max-scan gives every candidate the
+//     register value it would see.
+//   * pbits (:105-109) and the sampled majority-vote counter (:200-233) are
+//     sequential per cell: the successful encodes (at most maxValue per
+//     register per batch, sparse) are sorted by (cell, packet) and every cell
+//     is walked in stream order by one lane.
+#include <cstring>
+#include <rocprim/rocprim.hpp>
 
+#include <algorithm>
+#include <vector>
+
+#include "gns_common.hpp"
+#include "gns_gomath.cuh"
+
+namespace gns {
+
+constexpr int kSsNW = 20;             // merged key words (flow ‖ elem <= 74 bytes)
+constexpr uint32_t kSsPktBits = 27;   // packet index bits in the sort keys (batch <= 2^27)
+constexpr uint32_t kSsDrawCap = 1u << 24;
+constexpr int kSsThreads = 256;
+constexpr uint32_t kSsChunk = 16384;
+
+struct SsGeom {
+    uint32_t d, w, wmask, pow2, m, maxv, Kf, Km;
+    uint32_t seeds[8];
+    uint64_t hll_master, rng_seed;
+    double base, b;
+};
+
+__device__ __forceinline__ uint32_t ss_row_index(const SsGeom &g, uint32_t h) {
+    return g.pow2 ? (h & g.wmask) : (h % g.w);  // super_spread.go:193 `% ss.w`
+}
+
+struct SsExtractArgs {
+    InputDesc in;
+    uint64_t n;
+    KeyPlanN kpf, kpm;
+    int modef, modem;
+    SsGeom g;
+    DictDev D;
+    uint32_t epoch;
+    const uint8_t *regs;
+    uint32_t *flowid;
+    uint64_t *pend;
+    uint32_t *pend_cnt, *pend_total;
+    uint64_t *ckey;     // candidates: (cell*m + reg) << 27 | packet
+    uint32_t *cval;     // lz
+    uint32_t *ccount;
+    uint32_t ccap;
+    unsigned long long *stats;  // 0 inserted, 1 dropped, 2 unsupported, 3 dict full, 4 cand overflow, 5 encodes
+};
+
+template <int NW>
+__device__ __forceinline__ void make_key_rt(int mode, uint32_t K, const uint8_t *s_src,
+                                            const uint32_t (&tw)[10], uint32_t (&kw)[NW]) {
+    if (mode == PLAN_SLICE0) make_key_m<PLAN_SLICE0, NW>(K, s_src, tw, kw);
+    else if (mode == PLAN_SLICE4) make_key_m<PLAN_SLICE4, NW>(K, s_src, tw, kw);
+    else make_key_m<PLAN_GENERIC, NW>(K, s_src, tw, kw);
+}
+
+// flow key (kwf) and merged key flow‖elem (kwm) of packet p
+template <int KIND>
+__device__ __forceinline__ int ss_keys(const SsExtractArgs &a, const uint8_t *s_srcf, const uint8_t *s_srcm,
+                                       uint64_t p, uint32_t (&kwf)[GNS_KWMAX], uint32_t (&kwm)[kSsNW]) {
+    if constexpr (KIND == IN_KEYS) {
+        const uint8_t *f = a.in.keys + p * a.in.stride;
+        const uint8_t *e = a.in.keys2 + p * a.in.stride2;
+        load_key_bytes<GNS_KWMAX>(f, a.g.Kf, false, kwf);
+#pragma unroll
+        for (int i = 0; i < kSsNW; i++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const uint32_t j = 4 * i + b;
+                uint32_t byte = 0;
+                if (j < a.g.Kf) byte = f[j];
+                else if (j < a.g.Km) byte = e[j - a.g.Kf];
+                v |= byte << (8 * b);
+            }
+            kwm[i] = v;
+        }
+        return PARSE_OK;
+    } else {
+        uint32_t tw[10];
+        const int st = load_tuple<KIND>(a.in, p, tw);
+        if (st != PARSE_OK) return st;
+        make_key_rt<GNS_KWMAX>(a.modef, a.g.Kf, s_srcf, tw, kwf);
+        make_key_rt<kSsNW>(a.modem, a.g.Km, s_srcm, tw, kwm);
+        return PARSE_OK;
+    }
+}
+
+// S1: keys, flow id, per-row HLL encode test against the batch-entry registers
+template <int KIND>
+__global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
+    __shared__ uint8_t s_srcf[80], s_srcm[80];
+    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
+    const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    for (uint32_t j = tid; j < 80; j += kSsThreads) { s_srcf[j] = a.kpf.src[j]; s_srcm[j] = a.kpm.src[j]; }
+    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; }
+    __syncthreads();
+    const uint64_t beg = (uint64_t)blk * kSsChunk;
+    const uint64_t end = min(a.n, beg + kSsChunk);
+    uint32_t n_ok = 0;
+    for (uint64_t p = beg + tid; p < end; p += kSsThreads) {
+        uint32_t kwf[GNS_KWMAX], kwm[kSsNW];
+        const int st = ss_keys<KIND>(a, s_srcf, s_srcm, p, kwf, kwm);
+        if (st != PARSE_OK) {
+            a.flowid[p] = GNS_ID_NONE;
+            atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
+            continue;
+        }
+        uint32_t mkf[GNS_KWMAX], mkm[kSsNW];
+        mm3_premix<GNS_KWMAX>(kwf, a.g.Kf, mkf);
+        mm3_premix<kSsNW>(kwm, a.g.Km, mkm);
+        uint32_t out;
+        const int r = dict_find_or_claim(a.D, kwf, mm3_chain<GNS_KWMAX>(mkf, a.g.Kf, a.D.seed) & a.D.mask,
+                                         a.epoch, &out);
+        if (r == DICT_FULL) {
+            a.flowid[p] = GNS_ID_NONE;
+            atomicAdd(&s_full, 1u);
+            continue;
+        }
+        if (r == DICT_FOUND) {
+            a.flowid[p] = out;
+        } else {
+            a.flowid[p] = GNS_ID_NONE;
+            const uint32_t q = atomicAdd(&s_pend, 1u);
+            a.pend[beg + q] = (uint64_t)(p - beg) << 32 | out;
+        }
+        n_ok++;
+        for (uint32_t rr = 0; rr < a.g.d; rr++) {
+            const uint32_t j = ss_row_index(a.g, mm3_chain<GNS_KWMAX>(mkf, a.g.Kf, a.g.seeds[rr]));
+            const uint64_t cell = (uint64_t)rr * a.g.w + j;
+            uint32_t s0, s1;
+            ss_hll_seeds(a.g.hll_master, cell, s0, s1);
+            const uint32_t h0 = mm3_chain<kSsNW>(mkm, a.g.Km, s0);  // geometricHash :66-70
+            uint32_t lz = (h0 ? (uint32_t)__clz(h0) : 32u) + 1u;
+            if (lz > a.g.maxv) lz = a.g.maxv;
+            const uint32_t idx = mm3_chain<kSsNW>(mkm, a.g.Km, s1) % a.g.m;  // :87-88
+            const uint64_t seg = cell * a.g.m + idx;
+            if (lz > a.regs[seg]) {  // can encode only if above the batch-entry register
+                const uint32_t q = atomicAdd(a.ccount, 1u);
+                if (q < a.ccap) {
+                    a.ckey[q] = seg << kSsPktBits | (p & ((1ull << kSsPktBits) - 1));
+                    a.cval[q] = lz;
+                } else {
+                    atomicAdd(&a.stats[4], 1ull);
+                }
+            }
+        }
+    }
+    atomicAdd(&s_ok, n_ok);
+    __syncthreads();
+    if (tid == 0) {
+        a.pend_cnt[blk] = s_pend;
+        if (s_pend) atomicAdd(a.pend_total, s_pend);
+        if (s_ok) atomicAdd(&a.stats[0], (unsigned long long)s_ok);
+        if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
+        if (s_unsup) atomicAdd(&a.stats[2], (unsigned long long)s_unsup);
+        if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+    }
+}
+
+struct SsResolveArgs {
+    SsExtractArgs x;
+    const uint64_t *pend_in;
+    const uint32_t *cnt_in;
+    uint64_t *pend_out;
+    uint32_t *cnt_out, *total_out;
+};
+
+template <int KIND>
+__global__ __launch_bounds__(kSsThreads) void k_ss_resolve(SsResolveArgs r) {
+    __shared__ uint8_t s_srcf[80], s_srcm[80];
+    __shared__ uint32_t s_cnt, s_full;
+    const SsExtractArgs &a = r.x;
+    const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    for (uint32_t j = tid; j < 80; j += kSsThreads) { s_srcf[j] = a.kpf.src[j]; s_srcm[j] = a.kpm.src[j]; }
+    if (tid == 0) { s_cnt = 0; s_full = 0; }
+    __syncthreads();
+    const uint32_t cnt = r.cnt_in[blk];
+    const uint64_t beg = (uint64_t)blk * kSsChunk;
+    for (uint32_t i = tid; i < cnt; i += kSsThreads) {
+        const uint64_t v = r.pend_in[beg + i];
+        const uint64_t p = beg + (v >> 32);
+        uint32_t kwf[GNS_KWMAX], kwm[kSsNW];
+        (void)ss_keys<KIND>(a, s_srcf, s_srcm, p, kwf, kwm);
+        uint32_t out;
+        const int res = dict_find_or_claim(a.D, kwf, (uint32_t)v, a.epoch, &out);
+        if (res == DICT_FOUND) a.flowid[p] = out;
+        else if (res == DICT_PENDING) r.pend_out[beg + atomicAdd(&s_cnt, 1u)] = (v & 0xFFFFFFFF00000000ull) | out;
+        else atomicAdd(&s_full, 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        r.cnt_out[blk] = s_cnt;
+        if (s_cnt) atomicAdd(r.total_out, s_cnt);
+        if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+    }
+}
+
+// S3: which candidates encode.  inclusive max of lz per (cell, register)
+// segment is in cmax; the register a candidate sees is max(entry register,
+// previous candidate's inclusive max).
+struct SsSuccArgs {
+    const uint64_t *ckey;
+    const uint32_t *cval, *cmax;
+    uint32_t n;
+    const uint8_t *regs;
+    uint32_t m;
+    uint64_t *skey;  // (cell << 27) | packet
+    uint32_t *sval;  // reg | lz << 8 | old << 16
+    uint32_t *scount;
+};
+
+__global__ __launch_bounds__(256) void k_ss_success(SsSuccArgs a) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= a.n) return;
+    const uint64_t key = a.ckey[k];
+    const uint64_t seg = key >> kSsPktBits;
+    const uint32_t lz = a.cval[k];
+    uint32_t old = a.regs[seg];
+    if (k > 0 && (a.ckey[k - 1] >> kSsPktBits) == seg) old = max(old, a.cmax[k - 1]);
+    if (lz > old) {
+        const uint32_t q = atomicAdd(a.scount, 1u);
+        const uint64_t cell = seg / a.m;
+        const uint32_t reg = (uint32_t)(seg % a.m);
+        a.skey[q] = cell << kSsPktBits | (key & ((1ull << kSsPktBits) - 1));
+        a.sval[q] = reg | lz << 8 | old << 16;
+    }
+}
+
+// S5: every cell's encodes in stream order (one lane per cell):
+// register write, pbits (:105-109), sampling (:200-204), MV loop (:206-233).
+struct SsApplyArgs {
+    const uint64_t *skey;
+    const uint32_t *sval;
+    uint32_t n;
+    SsGeom g;
+    uint64_t pkt_base;
+    const uint32_t *flowid;
+    uint8_t *regs;
+    double *pbits;
+    uint32_t *values, *keys;
+};
+
+#pragma clang fp contract(off)
+__global__ __launch_bounds__(256) void k_ss_apply(SsApplyArgs a) {
+    const uint32_t k0 = blockIdx.x * 256 + threadIdx.x;
+    if (k0 >= a.n) return;
+    const uint64_t cell = a.skey[k0] >> kSsPktBits;
+    if (k0 > 0 && (a.skey[k0 - 1] >> kSsPktBits) == cell) return;  // not a segment head
+    const uint32_t row = (uint32_t)(cell / a.g.w);
+    const double mD = (double)a.g.m;
+    double pb = a.pbits[cell];
+    uint32_t val = a.values[cell], key = a.keys[cell];
+    for (uint32_t k = k0; k < a.n && (a.skey[k] >> kSsPktBits) == cell; k++) {
+        const uint64_t p = a.skey[k] & ((1ull << kSsPktBits) - 1);
+        const uint32_t v = a.sval[k];
+        const uint32_t reg = v & 0xFFu, lz = (v >> 8) & 0xFFu, old = (v >> 16) & 0xFFu;
+        a.regs[cell * a.g.m + reg] = (uint8_t)lz;
+        const double tempP = pb;                                            // :105
+        pb = pb + (-go_pow_int(a.g.base, (double)old) / mD);                // :106
+        if (lz < a.g.maxv) pb = pb + go_pow_int(a.g.base, (double)lz) / mD; // :107-109
+        if (tempP == -1.0) continue;                                        // :196
+        const double inv = 1.0 / tempP;
+        const double cv = ceil(inv);
+        const double pCU = inv / cv;                                        // :200
+        const uint64_t pkt = a.pkt_base + p;
+        if (ss_uniform(a.g.rng_seed, pkt, row, 0) >= pCU) continue;          // :201-204
+        int64_t vv = (cv < 9223372036854775808.0) ? (int64_t)cv : INT64_MIN;  // :206, amd64 semantics
+        const uint32_t f = a.flowid[p];
+        uint32_t draw = 1, draws = 0;
+        while (vv > 0) {                                                    // :207-233
+            if (val == 0 || key == f) {  // every remaining iteration increments
+                if (val == 0) key = f;
+                val = (uint32_t)((uint64_t)val + (uint64_t)vv);
+                break;
+            }
+            vv--;
+            if (draws++ >= kSsDrawCap) break;
+            const double ppp = go_pow_int(a.g.b, -(double)val);              // :222
+            if (ss_uniform(a.g.rng_seed, pkt, row, draw++) < ppp) val = val - 1;  // :223-227
+        }
+    }
+    a.pbits[cell] = pb;
+    a.values[cell] = val;
+    a.keys[cell] = key;
+}
+#pragma clang fp contract(on)
+
+// Query (super_spread.go:238-249)
+struct SsQueryArgs {
+    const uint8_t *flows;
+    uint32_t stride;
+    uint64_t n;
+    SsGeom g;
+    DictDev D;
+    const uint32_t *values, *keys;
+    uint64_t *out;
+};
+
+__global__ __launch_bounds__(256) void k_ss_query(SsQueryArgs a) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= a.n) return;
+    uint32_t kw[GNS_KWMAX];
+    load_key_bytes<GNS_KWMAX>(a.flows + p * a.stride, a.g.Kf, false, kw);
+    const uint32_t id = dict_lookup(a.D, kw);
+    uint32_t est = 0;
+    if (id != GNS_ID_NONE) {
+        for (uint32_t r = 0; r < a.g.d; r++) {
+            const uint64_t c = (uint64_t)r * a.g.w + ss_row_index(a.g, mm3_n<GNS_KWMAX>(kw, a.g.Kf, a.g.seeds[r]));
+            if (a.keys[c] == id && a.values[c] > est) est = a.values[c];
+        }
+    }
+    a.out[p] = est > 1 ? est : 1;
+}
+
+__global__ __launch_bounds__(256) void k_ss_ids_to_bytes(const uint32_t *ids, uint64_t n, DictDev D,
+                                                         uint8_t *out) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t id = ids[p];
+    uint32_t r[12];
+    if (id != GNS_ID_NONE) load_record(D, id, r);
+    for (uint32_t j = 0; j < D.K; j++) {
+        const uint32_t w = id != GNS_ID_NONE ? r[1 + (j >> 2)] : 0u;
+        out[p * D.K + j] = (uint8_t)(w >> (8 * (j & 3)));
+    }
+}
+
+struct SegKey {  // (cell*m + reg) of a candidate key
+    __host__ __device__ uint64_t operator()(uint64_t k) const { return k >> kSsPktBits; }
+};
+
+}  // namespace gns
+
+// ===========================================================================
+// Host side
+// ===========================================================================
 using namespace gns;
 
-#define SS_TODO() do { set_error("SuperSpread engine not built yet"); return GNS_E_RANGE; } while (0)
+struct gns_ss {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    SsGeom g{};
+    KeyPlanN kpf{}, kpm{};
+    uint32_t thr = 0;
+    uint8_t *regs = nullptr;
+    double *pbits = nullptr;
+    uint32_t *values = nullptr, *keys = nullptr;
+    DictDev D{};
+    uint64_t dict_slots = 0;
+    uint32_t epoch = 0;
+    uint64_t pkt = 0;     // records inserted since create (RNG packet index)
+    uint64_t bmax = 0;
+    uint32_t nblk_max = 0;
+    uint32_t *flowid = nullptr;
+    uint64_t *pend[2] = {nullptr, nullptr};
+    uint32_t *pcnt[2] = {nullptr, nullptr};
+    uint32_t *ptotal = nullptr;
+    uint64_t ccap = 0;
+    uint64_t *ckey = nullptr, *ckey_s = nullptr, *skey = nullptr, *skey_s = nullptr;
+    uint32_t *cval = nullptr, *cval_s = nullptr, *cmax = nullptr, *sval = nullptr, *sval_s = nullptr;
+    uint32_t *counts = nullptr;  // [0] candidates, [1] successes
+    void *tmp = nullptr;
+    size_t tmp_bytes = 0;
+    unsigned long long *stats = nullptr;
+    uint32_t *h_pin = nullptr;
+    uint8_t *stage = nullptr;
+    size_t stage_bytes = 0;
+    StageTimer timer;
+};
+
+namespace {
+
+int ss_set_dev(gns_ss *ss) {
+    GNS_HIP(hipSetDevice(ss->device));
+    return GNS_OK;
+}
+
+void ss_free_all(gns_ss *ss) {
+    dfree(ss->regs); dfree(ss->pbits); dfree(ss->values); dfree(ss->keys); dfree(ss->D.rec);
+    dfree(ss->flowid); dfree(ss->pend[0]); dfree(ss->pend[1]); dfree(ss->pcnt[0]); dfree(ss->pcnt[1]);
+    dfree(ss->ptotal); dfree(ss->ckey); dfree(ss->ckey_s); dfree(ss->skey); dfree(ss->skey_s);
+    dfree(ss->cval); dfree(ss->cval_s); dfree(ss->cmax); dfree(ss->sval); dfree(ss->sval_s);
+    dfree(ss->counts); dfree(ss->tmp); dfree(ss->stats); dfree(ss->stage);
+    if (ss->h_pin) (void)hipHostFree(ss->h_pin);
+    ss->timer.destroy();
+    if (ss->stream) (void)hipStreamDestroy(ss->stream);
+}
+
+int ss_reset_state(gns_ss *ss, bool init) {
+    const uint64_t cells = (uint64_t)ss->g.d * ss->g.w;
+    GNS_HIP(hipMemsetAsync(ss->regs, 0, cells * ss->g.m, ss->stream));
+    GNS_HIP(hipMemsetAsync(ss->values, 0, cells * 4, ss->stream));
+    GNS_HIP(hipMemsetAsync(ss->keys, 0xFF, cells * 4, ss->stream));
+    GNS_HIP(hipMemsetAsync(ss->D.rec, 0, ss->dict_slots * ss->D.RW * 4, ss->stream));
+    if (init) {  // pbits starts at 1.0 (:44); Reset leaves it untouched (:297-311)
+        std::vector<double> ones(cells, 1.0);
+        GNS_HIP(hipMemcpyAsync(ss->pbits, ones.data(), cells * 8, hipMemcpyHostToDevice, ss->stream));
+        GNS_HIP(hipStreamSynchronize(ss->stream));
+    }
+    return GNS_OK;
+}
+
+size_t ss_tmp_need(gns_ss *ss, uint64_t n) {
+    size_t a = 0, b = 0, c = 0;
+    const unsigned bits = kSsPktBits + ceil_log2((uint64_t)ss->g.d * ss->g.w * ss->g.m) + 1;
+    (void)rocprim::radix_sort_pairs(nullptr, a, ss->ckey, ss->ckey_s, ss->cval, ss->cval_s, (size_t)n, 0u,
+                                    std::min(64u, bits), ss->stream);
+    auto kit = rocprim::make_transform_iterator(ss->ckey_s, SegKey());
+    (void)rocprim::inclusive_scan_by_key(nullptr, b, kit, ss->cval_s, ss->cmax, (size_t)n,
+                                         rocprim::maximum<uint32_t>(), rocprim::equal_to<uint64_t>(),
+                                         ss->stream);
+    (void)c;
+    return std::max(a, b) + 256;
+}
+
+template <int KIND>
+int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
+    if (n == 0) return GNS_OK;
+    hipStream_t s = ss->stream;
+    const uint32_t nblk = (uint32_t)((n + kSsChunk - 1) / kSsChunk);
+    ScopedStage total_stage(ss->timer, 5);
+    GNS_HIP(hipMemsetAsync(ss->ptotal, 0, 8, s));
+    GNS_HIP(hipMemsetAsync(ss->counts, 0, 8, s));
+    if (++ss->epoch == 0) ss->epoch = 1;
+    SsExtractArgs x{};
+    x.in = in; x.n = n; x.kpf = ss->kpf; x.kpm = ss->kpm; x.modef = plan_mode(ss->kpf); x.modem = plan_mode(ss->kpm);
+    x.g = ss->g; x.D = ss->D; x.epoch = ss->epoch; x.regs = ss->regs; x.flowid = ss->flowid;
+    x.pend = ss->pend[0]; x.pend_cnt = ss->pcnt[0]; x.pend_total = ss->ptotal;
+    x.ckey = ss->ckey; x.cval = ss->cval; x.ccount = ss->counts; x.ccap = (uint32_t)ss->ccap; x.stats = ss->stats;
+    {
+        ScopedStage st(ss->timer, 0);
+        hipLaunchKernelGGL(k_ss_extract<KIND>, dim3(nblk), dim3(kSsThreads), 0, s, x);
+        GNS_HIP(hipGetLastError());
+    }
+    int cur = 0;
+    for (int round = 0;; round++) {
+        GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
+        GNS_HIP(hipMemcpyAsync(ss->h_pin + 2, ss->stats + 3, 16, hipMemcpyDeviceToHost, s));
+        GNS_HIP(hipStreamSynchronize(s));
+        if (ss->h_pin[2] | ss->h_pin[3]) { set_error("flow dictionary full; raise max flows"); return GNS_E_FULL; }
+        if (ss->h_pin[4] | ss->h_pin[5]) { set_error("candidate buffer overflow"); return GNS_E_RANGE; }
+        if (ss->h_pin[0] == 0) break;
+        if (round > 64) { set_error("dictionary resolve did not converge"); return GNS_E_FULL; }
+        GNS_HIP(hipMemsetAsync(ss->ptotal + (cur ^ 1), 0, 4, s));
+        if (++ss->epoch == 0) ss->epoch = 1;
+        SsResolveArgs r{};
+        r.x = x; r.x.epoch = ss->epoch;
+        r.pend_in = ss->pend[cur]; r.cnt_in = ss->pcnt[cur];
+        r.pend_out = ss->pend[cur ^ 1]; r.cnt_out = ss->pcnt[cur ^ 1]; r.total_out = ss->ptotal + (cur ^ 1);
+        ScopedStage st(ss->timer, 1);
+        hipLaunchKernelGGL(k_ss_resolve<KIND>, dim3(nblk), dim3(kSsThreads), 0, s, r);
+        GNS_HIP(hipGetLastError());
+        cur ^= 1;
+    }
+    GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->counts, 4, hipMemcpyDeviceToHost, s));
+    GNS_HIP(hipStreamSynchronize(s));
+    const uint32_t nc = ss->h_pin[0];
+    if (nc > 0) {
+        const unsigned bits = std::min(64u, kSsPktBits + ceil_log2((uint64_t)ss->g.d * ss->g.w * ss->g.m) + 1);
+        {
+            ScopedStage st(ss->timer, 2);
+            size_t tb = ss->tmp_bytes;
+            if (rocprim::radix_sort_pairs(ss->tmp, tb, ss->ckey, ss->ckey_s, ss->cval, ss->cval_s, (size_t)nc, 0u,
+                                          bits, s) != hipSuccess) { set_error("candidate sort failed"); return GNS_E_HIP; }
+            auto kit = rocprim::make_transform_iterator(ss->ckey_s, SegKey());
+            tb = ss->tmp_bytes;
+            if (rocprim::inclusive_scan_by_key(ss->tmp, tb, kit, ss->cval_s, ss->cmax, (size_t)nc,
+                                               rocprim::maximum<uint32_t>(), rocprim::equal_to<uint64_t>(),
+                                               s) != hipSuccess) { set_error("segmented max failed"); return GNS_E_HIP; }
+            SsSuccArgs a{ss->ckey_s, ss->cval_s, ss->cmax, nc, ss->regs, ss->g.m, ss->skey, ss->sval, ss->counts + 1};
+            hipLaunchKernelGGL(k_ss_success, dim3((nc + 255) / 256), dim3(256), 0, s, a);
+            GNS_HIP(hipGetLastError());
+        }
+        GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->counts + 1, 4, hipMemcpyDeviceToHost, s));
+        GNS_HIP(hipStreamSynchronize(s));
+        const uint32_t ns = ss->h_pin[0];
+        if (ns > 0) {
+            ScopedStage st(ss->timer, 3);
+            const unsigned bits2 = std::min(64u, kSsPktBits + ceil_log2((uint64_t)ss->g.d * ss->g.w) + 1);
+            size_t tb = ss->tmp_bytes;
+            if (rocprim::radix_sort_pairs(ss->tmp, tb, ss->skey, ss->skey_s, ss->sval, ss->sval_s, (size_t)ns, 0u,
+                                          bits2, s) != hipSuccess) { set_error("encode sort failed"); return GNS_E_HIP; }
+            SsApplyArgs a{ss->skey_s, ss->sval_s, ns, ss->g, ss->pkt, ss->flowid, ss->regs, ss->pbits,
+                          ss->values, ss->keys};
+            hipLaunchKernelGGL(k_ss_apply, dim3((ns + 255) / 256), dim3(256), 0, s, a);
+            GNS_HIP(hipGetLastError());
+        }
+    }
+    ss->pkt += n;  // every record advances the RNG packet index
+    return GNS_OK;
+}
+
+template <int KIND>
+int ss_insert(gns_ss *ss, InputDesc in, uint64_t n, gns_mem where) {
+    GNS_TRY(ss_set_dev(ss));
+    for (uint64_t off = 0; off < n; off += ss->bmax) {
+        const uint64_t m = std::min<uint64_t>(ss->bmax, n - off);
+        InputDesc d = in;
+        if (where == GNS_MEM_DEVICE) {
+            if (d.hdr) d.hdr += off * 16;
+            if (d.src16) d.src16 += off * 16;
+            if (d.dst16) d.dst16 += off * 16;
+            if (d.sport) d.sport += off;
+            if (d.dport) d.dport += off;
+            if (d.proto) d.proto += off;
+            if (d.keys) d.keys += off * d.stride;
+            if (d.keys2) d.keys2 += off * d.stride2;
+            if (d.sizes) d.sizes += off;
+        } else {
+            const void *src[8] = {in.hdr ? (const void *)(in.hdr + off * 16) : nullptr,
+                                  in.src16 ? (const void *)(in.src16 + off * 16) : nullptr,
+                                  in.dst16 ? (const void *)(in.dst16 + off * 16) : nullptr,
+                                  in.sport ? (const void *)(in.sport + off) : nullptr,
+                                  in.dport ? (const void *)(in.dport + off) : nullptr,
+                                  in.proto ? (const void *)(in.proto + off) : nullptr,
+                                  in.keys ? (const void *)(in.keys + off * in.stride) : nullptr,
+                                  in.keys2 ? (const void *)(in.keys2 + off * in.stride2) : nullptr};
+            const size_t bytes[8] = {in.hdr ? m * 64 : 0, in.src16 ? m * 16 : 0, in.dst16 ? m * 16 : 0,
+                                     in.sport ? m * 2 : 0, in.dport ? m * 2 : 0, in.proto ? m : 0,
+                                     in.keys ? m * in.stride : 0, in.keys2 ? m * in.stride2 : 0};
+            size_t tot = 0;
+            for (int i = 0; i < 8; i++) tot += (bytes[i] + 15) & ~size_t(15);
+            tot += (m * 4 + 15) & ~size_t(15);
+            if (ss->stage_bytes < tot) {
+                dfree(ss->stage);
+                ss->stage = nullptr;
+                ss->stage_bytes = 0;
+                GNS_TRY(dalloc(reinterpret_cast<void **>(&ss->stage), tot));
+                ss->stage_bytes = tot;
+            }
+            uint8_t *p = ss->stage;
+            const void **dst[8] = {(const void **)&d.hdr, (const void **)&d.src16, (const void **)&d.dst16,
+                                   (const void **)&d.sport, (const void **)&d.dport, (const void **)&d.proto,
+                                   (const void **)&d.keys, (const void **)&d.keys2};
+            for (int i = 0; i < 8; i++) {
+                if (!bytes[i]) continue;
+                GNS_HIP(hipMemcpyAsync(p, src[i], bytes[i], hipMemcpyHostToDevice, ss->stream));
+                *dst[i] = p;
+                p += (bytes[i] + 15) & ~size_t(15);
+            }
+            if (in.sizes) {
+                GNS_HIP(hipMemcpyAsync(p, in.sizes + off, m * 4, hipMemcpyHostToDevice, ss->stream));
+                d.sizes = reinterpret_cast<const uint32_t *>(p);
+            }
+        }
+        GNS_TRY(ss_run_batch<KIND>(ss, d, m));
+    }
+    return GNS_OK;
+}
+
+}  // namespace
 
 extern "C" {
-int gns_ss_create(const gns_ss_params *, gns_ss **out) { if (out) *out = nullptr; SS_TODO(); }
-int gns_ss_destroy(gns_ss *) { return GNS_OK; }
-int gns_ss_insert_keys(gns_ss *, const uint8_t *, uint32_t, const uint8_t *, uint32_t, uint64_t, gns_mem) { SS_TODO(); }
-int gns_ss_insert_tuples(gns_ss *, const gns_tuples *, uint64_t, gns_mem) { SS_TODO(); }
-int gns_ss_insert_headers(gns_ss *, const uint8_t *, const uint32_t *, uint64_t, gns_mem) { SS_TODO(); }
-int gns_ss_flush(gns_ss *) { SS_TODO(); }
-int gns_ss_query(gns_ss *, const uint8_t *, uint32_t, uint64_t, uint64_t *) { SS_TODO(); }
-int gns_ss_heavy_hitters(gns_ss *, uint8_t *, uint32_t *, uint64_t *) { SS_TODO(); }
-int gns_ss_reset(gns_ss *) { SS_TODO(); }
-int gns_ss_export_state(gns_ss *, uint32_t *, uint8_t *, uint8_t *, double *) { SS_TODO(); }
-int gns_ss_stats(gns_ss *, uint64_t *) { SS_TODO(); }
-int gns_ss_set_timing(gns_ss *, int) { SS_TODO(); }
-int gns_ss_stage_times(gns_ss *, double *, uint64_t *, int) { SS_TODO(); }
+
+int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
+    if (!p || !out) { set_error("null argument"); return GNS_E_ARG; }
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device available");
+        return GNS_E_NODEV;
+    }
+    if (p->device < 0 || p->device >= ndev) { set_error("device %d out of range", p->device); return GNS_E_ARG; }
+    gns_ss *ss = new gns_ss();
+    ss->device = p->device;
+    int rc = GNS_OK;
+    do {
+        if ((rc = ss_set_dev(ss)) != GNS_OK) break;
+        SsGeom &g = ss->g;
+        // super_spread.go:12-20,129-149 defaults
+        g.w = p->width ? p->width : (1u << 20);
+        g.d = p->depth ? p->depth : 3u;
+        ss->thr = p->threshold ? p->threshold : 4096u;
+        g.m = p->m ? p->m : 128u;
+        const uint32_t size = p->size ? p->size : 5u;
+        g.base = p->base != 0 ? p->base : 0.5;
+        g.b = p->b != 0 ? p->b : 1.08;
+        if (g.d > 8 || size > 8 || g.m > 256 || size == 0) {
+            set_error("SuperSpread limits: depth <= 8, 1 <= size <= 8, m <= 256");
+            rc = GNS_E_ARG;
+            break;
+        }
+        g.maxv = (1u << size) - 1;
+        if ((rc = make_plan(p->flow, p->flow_bytes, &ss->kpf)) != GNS_OK) break;
+        KeyPlanN kpe;
+        if ((rc = make_plan(p->elem, p->elem_bytes, &kpe)) != GNS_OK) break;
+        g.Kf = ss->kpf.K;
+        if (p->flow.n_fields || p->elem.n_fields) {
+            if ((rc = make_plan2(p->flow, p->elem, &ss->kpm)) != GNS_OK) break;
+        } else {
+            ss->kpm.K = ss->kpf.K + kpe.K;
+            ss->kpm.woff = -1;
+        }
+        g.Km = ss->kpf.K + kpe.K;
+        if (g.Km > 74) { set_error("flow+elem key of %u bytes exceeds 74 (super_spread.go:20)", g.Km); rc = GNS_E_ARG; break; }
+        g.pow2 = (g.w & (g.w - 1)) == 0;
+        g.wmask = g.pow2 ? g.w - 1 : 0;
+        if (p->seeds) for (uint32_t i = 0; i < g.d; i++) g.seeds[i] = p->seeds[i];
+        else default_seeds(g.seeds, g.d);
+        g.hll_master = p->hll_master;
+        g.rng_seed = p->rng_seed;
+        if ((uint64_t)g.d * g.w * g.m > (1ull << 36)) { set_error("d*w*m too large"); rc = GNS_E_ARG; break; }
+        if (hipStreamCreateWithFlags(&ss->stream, hipStreamNonBlocking) != hipSuccess) {
+            set_error("hipStreamCreate failed"); rc = GNS_E_HIP; break;
+        }
+        ss->timer.stream = ss->stream;
+        const uint64_t cells = (uint64_t)g.d * g.w;
+        if ((rc = dalloc_t(&ss->regs, cells * g.m)) || (rc = dalloc_t(&ss->pbits, cells)) ||
+            (rc = dalloc_t(&ss->values, cells)) || (rc = dalloc_t(&ss->keys, cells)))
+            break;
+        uint64_t slots = 1;
+        const uint64_t mf = 4ull << 20;
+        while (slots < 2 * mf) slots <<= 1;
+        ss->dict_slots = slots;
+        ss->D.mask = (uint32_t)(slots - 1);
+        ss->D.K = g.Kf;
+        ss->D.RW = ((1 + (g.Kf + 3) / 4) + 3) & ~3u;
+        ss->D.seed = 0x2545F491u;
+        if ((rc = dalloc_t(&ss->D.rec, slots * ss->D.RW)) != GNS_OK) break;
+        ss->bmax = p->batch_packets ? p->batch_packets : (8ull << 20);
+        ss->bmax = std::min<uint64_t>(((ss->bmax + kSsChunk - 1) / kSsChunk) * kSsChunk, 1ull << kSsPktBits);
+        ss->nblk_max = (uint32_t)(ss->bmax / kSsChunk);
+        ss->ccap = ss->bmax * g.d;
+        if ((rc = dalloc_t(&ss->flowid, ss->bmax)) || (rc = dalloc_t(&ss->pend[0], ss->bmax)) ||
+            (rc = dalloc_t(&ss->pend[1], ss->bmax)) || (rc = dalloc_t(&ss->pcnt[0], ss->nblk_max)) ||
+            (rc = dalloc_t(&ss->pcnt[1], ss->nblk_max)) || (rc = dalloc_t(&ss->ptotal, 2)) ||
+            (rc = dalloc_t(&ss->ckey, ss->ccap)) || (rc = dalloc_t(&ss->ckey_s, ss->ccap)) ||
+            (rc = dalloc_t(&ss->skey, ss->ccap)) || (rc = dalloc_t(&ss->skey_s, ss->ccap)) ||
+            (rc = dalloc_t(&ss->cval, ss->ccap)) || (rc = dalloc_t(&ss->cval_s, ss->ccap)) ||
+            (rc = dalloc_t(&ss->cmax, ss->ccap)) || (rc = dalloc_t(&ss->sval, ss->ccap)) ||
+            (rc = dalloc_t(&ss->sval_s, ss->ccap)) || (rc = dalloc_t(&ss->counts, 4)) ||
+            (rc = dalloc_t(&ss->stats, 8)))
+            break;
+        ss->tmp_bytes = ss_tmp_need(ss, ss->ccap);
+        if ((rc = dalloc(&ss->tmp, ss->tmp_bytes)) != GNS_OK) break;
+        if (hipHostMalloc(reinterpret_cast<void **>(&ss->h_pin), 64, 0) != hipSuccess) {
+            set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
+        }
+        if (hipMemsetAsync(ss->stats, 0, 64, ss->stream) != hipSuccess) { rc = GNS_E_HIP; break; }
+        if ((rc = ss_reset_state(ss, true)) != GNS_OK) break;
+    } while (0);
+    if (rc != GNS_OK) {
+        ss_free_all(ss);
+        delete ss;
+        return rc;
+    }
+    *out = ss;
+    return GNS_OK;
 }
+
+int gns_ss_destroy(gns_ss *ss) {
+    if (!ss) return GNS_OK;
+    (void)hipSetDevice(ss->device);
+    if (ss->stream) (void)hipStreamSynchronize(ss->stream);
+    ss_free_all(ss);
+    delete ss;
+    return GNS_OK;
+}
+
+int gns_ss_insert_keys(gns_ss *ss, const uint8_t *flows, uint32_t fstride, const uint8_t *elems,
+                       uint32_t estride, uint64_t n, gns_mem where) {
+    if (!ss || (n && (!flows || (!elems && ss->g.Km > ss->g.Kf)))) { set_error("null argument"); return GNS_E_ARG; }
+    if (fstride < ss->g.Kf || estride < ss->g.Km - ss->g.Kf) { set_error("stride smaller than key"); return GNS_E_ARG; }
+    InputDesc in{};
+    in.keys = flows; in.stride = fstride; in.keys2 = elems ? elems : flows; in.stride2 = estride;
+    return ss_insert<IN_KEYS>(ss, in, n, where);
+}
+
+int gns_ss_insert_tuples(gns_ss *ss, const gns_tuples *t, uint64_t n, gns_mem where) {
+    if (!ss || !t) { set_error("null argument"); return GNS_E_ARG; }
+    if (n && (!t->src16 || !t->dst16 || !t->sport || !t->dport || !t->proto)) { set_error("null tuple array"); return GNS_E_ARG; }
+    InputDesc in{};
+    in.src16 = t->src16; in.dst16 = t->dst16; in.sport = t->sport; in.dport = t->dport; in.proto = t->proto;
+    in.sizes = t->length;
+    return ss_insert<IN_TUPLE>(ss, in, n, where);
+}
+
+int gns_ss_insert_headers(gns_ss *ss, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n, gns_mem where) {
+    if (!ss || (n && (!hdr || !wirelen))) { set_error("null argument"); return GNS_E_ARG; }
+    InputDesc in{};
+    in.hdr = reinterpret_cast<const uint32_t *>(hdr);
+    in.sizes = wirelen;
+    return ss_insert<IN_HDR>(ss, in, n, where);
+}
+
+int gns_ss_flush(gns_ss *ss) {
+    if (!ss) return GNS_E_ARG;
+    GNS_TRY(ss_set_dev(ss));
+    GNS_HIP(hipStreamSynchronize(ss->stream));
+    ss->timer.collect();
+    return GNS_OK;
+}
+
+int gns_ss_query(gns_ss *ss, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out) {
+    if (!ss || (n && (!flows || !out))) { set_error("null argument"); return GNS_E_ARG; }
+    if (n == 0) return GNS_OK;
+    if (stride < ss->g.Kf) { set_error("stride < flow_bytes"); return GNS_E_ARG; }
+    GNS_TRY(ss_set_dev(ss));
+    uint8_t *dk = nullptr;
+    uint64_t *dout = nullptr;
+    GNS_TRY(dalloc(reinterpret_cast<void **>(&dk), n * stride));
+    int rc = dalloc(reinterpret_cast<void **>(&dout), n * 8);
+    if (rc) { dfree(dk); return rc; }
+    SsQueryArgs a{dk, stride, n, ss->g, ss->D, ss->values, ss->keys, dout};
+    hipError_t e = hipMemcpyAsync(dk, flows, n * stride, hipMemcpyHostToDevice, ss->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_ss_query, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ss->stream, a);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, ss->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ss->stream);
+    dfree(dk);
+    dfree(dout);
+    if (e != hipSuccess) { set_error("ss query: %s", hipGetErrorString(e)); return GNS_E_HIP; }
+    return GNS_OK;
+}
+
+static int ss_ids_to_bytes(gns_ss *ss, const std::vector<uint32_t> &ids, std::vector<uint8_t> &bytes) {
+    const uint32_t K = ss->g.Kf;
+    bytes.assign(ids.size() * (K ? K : 1), 0);
+    if (ids.empty() || K == 0) return GNS_OK;
+    uint32_t *dids = nullptr;
+    uint8_t *db = nullptr;
+    GNS_TRY(dalloc(reinterpret_cast<void **>(&dids), ids.size() * 4));
+    int rc = dalloc(reinterpret_cast<void **>(&db), ids.size() * K);
+    if (rc) { dfree(dids); return rc; }
+    hipError_t e = hipMemcpy(dids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_ss_ids_to_bytes, dim3((unsigned)((ids.size() + 255) / 256)), dim3(256), 0,
+                           ss->stream, dids, (uint64_t)ids.size(), ss->D, db);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(bytes.data(), db, ids.size() * K, hipMemcpyDeviceToHost, ss->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ss->stream);
+    dfree(dids);
+    dfree(db);
+    if (e != hipSuccess) { set_error("ss ids_to_bytes: %s", hipGetErrorString(e)); return GNS_E_HIP; }
+    return GNS_OK;
+}
+
+static uint32_t mm3_host_bytes(const uint8_t *d, uint32_t len, uint32_t seed) {
+    uint32_t kw[GNS_KWMAX] = {0};
+    for (uint32_t j = 0; j < len; j++) kw[j / 4] |= (uint32_t)d[j] << (8 * (j % 4));
+    uint32_t h = seed;
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    auto rotl = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
+    const uint32_t nb = len / 4;
+    for (uint32_t i = 0; i < nb; i++) {
+        uint32_t k = kw[i] * c1; k = rotl(k, 15); k *= c2;
+        h ^= k; h = rotl(h, 13); h = h * 5 + 0xe6546b64u;
+    }
+    if (len & 3) { uint32_t k = kw[nb] * c1; k = rotl(k, 15); k *= c2; h ^= k; }
+    h ^= len;
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
+}
+
+// HeavyHitters (super_spread.go:254-294): every flow holding a counter > 0 is
+// re-queried; ties ordered by flow bytes (Go sorts with sort.Slice, unstable).
+int gns_ss_heavy_hitters(gns_ss *ss, uint8_t *flows, uint32_t *spreads, uint64_t *n_io) {
+    if (!ss || !n_io) { set_error("null argument"); return GNS_E_ARG; }
+    GNS_TRY(ss_set_dev(ss));
+    GNS_HIP(hipStreamSynchronize(ss->stream));
+    const uint64_t cells = (uint64_t)ss->g.d * ss->g.w;
+    std::vector<uint32_t> vals(cells), ids(cells);
+    GNS_HIP(hipMemcpy(vals.data(), ss->values, cells * 4, hipMemcpyDeviceToHost));
+    GNS_HIP(hipMemcpy(ids.data(), ss->keys, cells * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> uniq;
+    for (uint64_t c = 0; c < cells; c++) if (vals[c] > 0) uniq.push_back(ids[c]);
+    std::sort(uniq.begin(), uniq.end());
+    uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+    std::vector<uint8_t> kb;
+    GNS_TRY(ss_ids_to_bytes(ss, uniq, kb));
+    const uint32_t K = ss->g.Kf;
+    std::vector<std::pair<uint32_t, uint32_t>> res;  // (estimate, index)
+    for (size_t i = 0; i < uniq.size(); i++) {
+        uint32_t est = 0;
+        for (uint32_t r = 0; r < ss->g.d; r++) {
+            const uint32_t h = mm3_host_bytes(&kb[i * K], K, ss->g.seeds[r]);
+            const uint64_t c = (uint64_t)r * ss->g.w + (ss->g.pow2 ? (h & ss->g.wmask) : (h % ss->g.w));
+            if (ids[c] == uniq[i] && vals[c] > est) est = vals[c];
+        }
+        if (est >= ss->thr) res.push_back({est, (uint32_t)i});
+    }
+    std::sort(res.begin(), res.end(), [&](const std::pair<uint32_t, uint32_t> &x, const std::pair<uint32_t, uint32_t> &y) {
+        if (x.first != y.first) return x.first > y.first;
+        return memcmp(&kb[(size_t)x.second * K], &kb[(size_t)y.second * K], K) < 0;
+    });
+    const uint64_t cap = *n_io;
+    for (size_t i = 0; i < res.size() && i < cap; i++) {
+        if (flows && K) memcpy(flows + i * K, &kb[(size_t)res[i].second * K], K);
+        if (spreads) spreads[i] = res[i].first;
+    }
+    *n_io = res.size();
+    return GNS_OK;
+}
+
+int gns_ss_reset(gns_ss *ss) {
+    if (!ss) return GNS_E_ARG;
+    GNS_TRY(ss_set_dev(ss));
+    GNS_TRY(ss_reset_state(ss, false));
+    GNS_HIP(hipStreamSynchronize(ss->stream));
+    return GNS_OK;
+}
+
+int gns_ss_export_state(gns_ss *ss, uint32_t *values, uint8_t *keys, uint8_t *regs, double *pbits) {
+    if (!ss) return GNS_E_ARG;
+    GNS_TRY(ss_set_dev(ss));
+    GNS_HIP(hipStreamSynchronize(ss->stream));
+    const uint64_t cells = (uint64_t)ss->g.d * ss->g.w;
+    if (values) GNS_HIP(hipMemcpy(values, ss->values, cells * 4, hipMemcpyDeviceToHost));
+    if (regs) GNS_HIP(hipMemcpy(regs, ss->regs, cells * ss->g.m, hipMemcpyDeviceToHost));
+    if (pbits) GNS_HIP(hipMemcpy(pbits, ss->pbits, cells * 8, hipMemcpyDeviceToHost));
+    if (keys) {
+        std::vector<uint32_t> ids(cells);
+        GNS_HIP(hipMemcpy(ids.data(), ss->keys, cells * 4, hipMemcpyDeviceToHost));
+        std::vector<uint8_t> kb;
+        GNS_TRY(ss_ids_to_bytes(ss, ids, kb));
+        if (ss->g.Kf) memcpy(keys, kb.data(), cells * ss->g.Kf);
+    }
+    return GNS_OK;
+}
+
+int gns_ss_stats(gns_ss *ss, uint64_t stats[4]) {
+    if (!ss || !stats) return GNS_E_ARG;
+    GNS_TRY(ss_set_dev(ss));
+    GNS_HIP(hipStreamSynchronize(ss->stream));
+    unsigned long long h[8];
+    GNS_HIP(hipMemcpy(h, ss->stats, sizeof(h), hipMemcpyDeviceToHost));
+    stats[0] = h[0]; stats[1] = h[1]; stats[2] = h[2]; stats[3] = ss->pkt;
+    return GNS_OK;
+}
+
+int gns_ss_set_timing(gns_ss *ss, int on) {
+    if (!ss) return GNS_E_ARG;
+    ss->timer.on = on != 0;
+    return GNS_OK;
+}
+
+int gns_ss_stage_times(gns_ss *ss, double ms[8], uint64_t launches[8], int reset) {
+    if (!ss) return GNS_E_ARG;
+    GNS_TRY(ss_set_dev(ss));
+    ss->timer.collect();
+    for (int i = 0; i < 8; i++) {
+        if (ms) ms[i] = ss->timer.ms[i];
+        if (launches) launches[i] = ss->timer.launches[i];
+    }
+    if (reset) for (int i = 0; i < 8; i++) { ss->timer.ms[i] = 0; ss->timer.launches[i] = 0; }
+    return GNS_OK;
+}
+
+}  // extern "C"

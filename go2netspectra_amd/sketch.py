@@ -350,12 +350,12 @@ class SuperSpread:
     def stats(self) -> dict:
         s = (ct.c_uint64 * 4)()
         check(self._L.gns_ss_stats(self._h, s))
-        return {"inserted": s[0], "dropped": s[1], "unsupported": s[2], "encodes": s[3]}
+        return {"inserted": s[0], "dropped": s[1], "unsupported": s[2], "packets": s[3]}
 
     def set_timing(self, on: bool = True) -> None:
         check(self._L.gns_ss_set_timing(self._h, 1 if on else 0))
 
-    STAGES = ["extract", "candidates", "group", "replay", "apply", "insert"]
+    STAGES = ["extract", "resolve", "encode", "apply", "unused", "total"]
 
     def stage_times(self, reset: bool = False) -> dict:
         ms = (ct.c_double * 8)()

@@ -650,6 +650,27 @@ void or_ss_insert_batch(or_ss *ss, const uint8_t *flows, uint32_t fstride, const
     for (uint64_t p = 0; p < n; p++) or_ss_insert(ss, flows + p * fstride, elems + p * estride);
 }
 
+/* Task.ProcessPacket over 64-byte records (task.go:156-169, parser.go:23-67).
+ * Every record advances the declared generator's packet index, also the ones
+ * the parser drops (the engine's convention). */
+uint64_t or_ss_insert_hdr64(or_ss *ss, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
+                            const uint8_t *ffields, uint32_t nff, const uint8_t *efields, uint32_t nef) {
+    uint8_t fk[64], ek[64];
+    uint64_t done = 0;
+    for (uint64_t p = 0; p < n; p++) {
+        or_tuple t;
+        if (or_parse_hdr64_len(hdr + p * 64, wirelen[p], &t) != OR_PARSE_OK) {
+            ss->pkt++;
+            continue;
+        }
+        or_encode_key(ffields, nff, &t, fk);
+        or_encode_key(efields, nef, &t, ek);
+        or_ss_insert(ss, fk, ek);
+        done++;
+    }
+    return done;
+}
+
 static uint32_t ss_estimate(const or_ss *ss, const uint8_t *flow) {
     uint32_t est = 0;
     for (uint32_t i = 0; i < ss->d; i++) {

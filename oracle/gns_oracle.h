@@ -99,6 +99,8 @@ void or_ss_free(or_ss *ss);
 void or_ss_insert(or_ss *ss, const uint8_t *flow, const uint8_t *elem);
 void or_ss_insert_batch(or_ss *ss, const uint8_t *flows, uint32_t fstride, const uint8_t *elems,
                         uint32_t estride, uint64_t n);
+uint64_t or_ss_insert_hdr64(or_ss *ss, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
+                            const uint8_t *ffields, uint32_t nff, const uint8_t *efields, uint32_t nef);
 uint64_t or_ss_query(const or_ss *ss, const uint8_t *flow);
 uint32_t or_ss_heavy(const or_ss *ss, uint8_t *flows, uint32_t *vals, uint32_t cap);
 void or_ss_export(const or_ss *ss, uint32_t *values, uint8_t *keys, uint8_t *regs, double *pbits);

@@ -65,6 +65,9 @@ def lib():
     L.or_ss_insert.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_void_p]
     L.or_ss_insert_batch.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_uint32, ct.c_void_p, ct.c_uint32,
                                      ct.c_uint64]
+    L.or_ss_insert_hdr64.restype = ct.c_uint64
+    L.or_ss_insert_hdr64.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_uint64, ct.c_void_p, ct.c_uint32,
+                                     ct.c_void_p, ct.c_uint32]
     L.or_ss_query.restype = ct.c_uint64
     L.or_ss_query.argtypes = [ct.c_void_p, ct.c_void_p]
     L.or_ss_heavy.restype = ct.c_uint32
@@ -194,6 +197,17 @@ class SuperSpread:
         elems = np.ascontiguousarray(elems, dtype=np.uint8)
         n = flows.shape[0]
         self.L.or_ss_insert_batch(self.h, _p(flows), self.kf, _p(elems), self.ke, n)
+
+    def insert_hdr64(self, hdr, wirelen, flow_fields, elem_fields) -> int:
+        hdr = np.ascontiguousarray(hdr, dtype=np.uint8)
+        wirelen = np.ascontiguousarray(wirelen, dtype=np.uint32)
+        ff = np.array([FIELD_IDS[f] for f in flow_fields] or [0], np.uint8)
+        ef = np.array([FIELD_IDS[f] for f in elem_fields] or [0], np.uint8)
+        return self.L.or_ss_insert_hdr64(self.h, _p(hdr), _p(wirelen), len(wirelen), _p(ff), len(flow_fields),
+                                         _p(ef), len(elem_fields))
+
+    def packets(self) -> int:
+        return self.L.or_ss_packets(self.h)
 
     def query(self, flow: bytes) -> int:
         buf = (ct.c_uint8 * max(1, len(flow))).from_buffer_copy(flow or b"\0")

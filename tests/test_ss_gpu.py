@@ -1,0 +1,175 @@
+"""SuperSpread parity on the GPU: the device state (counter values, owner keys,
+HLL registers and the float64 pbits) exported through the C ABI must equal
+the sequential C oracle (super_spread.go restated, declared RNG) bit for bit."""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import frames_from_tuples, random_tuples, zipf_index
+
+pytestmark = pytest.mark.gpu
+
+HLL_MASTER, RNG_SEED = 0x0123456789ABCDEF, 0x0DDBA11CAFEF00D5
+
+
+def assert_same_ss(ss, orc):
+    got = ss.export_state()
+    want = orc.export()
+    for name, a, b in zip(("values", "keys", "regs", "pbits"), got, want):
+        if name == "pbits":
+            same = np.array_equal(a.view(np.uint64), b.view(np.uint64))  # bit-exact float64
+        else:
+            same = np.array_equal(a, b)
+        if not same:
+            bad = np.nonzero(a != b)[0] if a.ndim == 1 else np.nonzero((a != b).any(axis=1))[0]
+            raise AssertionError(f"{name} differs in {len(bad)} cells, first {bad[:5]}: "
+                                 f"gpu={a[bad[:3]]} oracle={b[bad[:3]]}")
+
+
+def make_pair(oracle, w, d, m, size, Kf, Ke, thr=20, base=0.5, b=1.08, seed=1, **kw):
+    from go2netspectra_amd import SuperSpread
+    seeds = np.random.default_rng(seed).integers(0, 2**32, d, dtype=np.uint64).astype(np.uint32)
+    ss = SuperSpread(w, d, thr, m, size, base, b, flow_bytes=Kf, elem_bytes=Ke, seeds=seeds,
+                     hll_master=HLL_MASTER, rng_seed=RNG_SEED, **kw)
+    orc = oracle.SuperSpread(w, d, thr, m, size, base, b, Kf, Ke, seeds, HLL_MASTER, RNG_SEED)
+    return ss, orc
+
+
+def spread_stream(rng, n, nflows, Kf, Ke, s=1.1, elem_pool=None):
+    """Zipf flows, each packet a random element (drawn from a pool so elements repeat)."""
+    flows = rng.integers(0, 256, (nflows, max(Kf, 1)), dtype=np.uint8)[:, :Kf]
+    fl = np.ascontiguousarray(flows[zipf_index(rng, n, nflows, s)])
+    pool = elem_pool or max(16, n // 4)
+    elems = rng.integers(0, 256, (pool, max(Ke, 1)), dtype=np.uint8)[:, :Ke]
+    el = np.ascontiguousarray(elems[rng.integers(0, pool, n)])
+    return fl, el, flows
+
+
+@pytest.mark.parametrize("w,d,m,size,Kf,Ke,nflows,n,batch,base,b", [
+    (64, 2, 32, 5, 16, 16, 40, 50_000, 0, 0.5, 1.08),          # tiny: many takeovers
+    (4096, 3, 128, 5, 16, 16, 3000, 400_000, 0, 0.5, 1.08),    # reference defaults for m/size
+    (1000, 3, 64, 3, 13, 7, 2000, 200_000, 0, 0.5, 1.08),      # non power-of-two w, saturating regs
+    (1, 1, 16, 8, 4, 4, 30, 30_000, 0, 0.5, 1.08),             # one cell
+    (2048, 2, 128, 5, 16, 16, 1500, 300_000, 16384, 0.5, 1.08),  # multi-batch
+    (512, 4, 32, 4, 8, 2, 800, 150_000, 0, 0.7, 1.2),          # other base / b
+    (256, 2, 1, 5, 16, 16, 300, 80_000, 0, 0.5, 1.08),         # m = 1
+])
+def test_insert_keys_parity(gpu, oracle, w, d, m, size, Kf, Ke, nflows, n, batch, base, b):
+    rng = np.random.default_rng(w + 13 * d + m)
+    ss, orc = make_pair(oracle, w, d, m, size, Kf, Ke, base=base, b=b, batch_packets=batch)
+    fl, el, _ = spread_stream(rng, n, nflows, Kf, Ke)
+    ss.insert_keys(fl, el)
+    ss.flush()
+    orc.insert(fl, el)
+    assert_same_ss(ss, orc)
+
+
+def test_superspreaders_and_queries(gpu, oracle):
+    """A few sources contact many distinct destinations (the C3 shape)."""
+    rng = np.random.default_rng(3)
+    ss, orc = make_pair(oracle, 1 << 14, 3, 128, 5, 16, 16, thr=50)
+    n = 600_000
+    fl, el, flows = spread_stream(rng, n, 20_000, 16, 16, s=1.3, elem_pool=n)
+    for part in np.array_split(np.arange(n), 3):
+        ss.insert_keys(fl[part], el[part])
+        orc.insert(fl[part], el[part])
+    ss.flush()
+    assert_same_ss(ss, orc)
+    q = ss.query_many(flows[:3000])
+    want = np.array([orc.query(bytes(f)) for f in flows[:3000]], np.uint64)
+    assert np.array_equal(q, want)
+    absent = rng.integers(0, 256, (50, 16), dtype=np.uint8)
+    assert np.array_equal(ss.query_many(absent), np.ones(50, np.uint64))
+    hh = ss.heavy_hitters()
+    got = [(h.Flow, h.Count) for h in hh.Count]
+    assert got == orc.heavy() and len(got) > 0
+
+
+def test_reset_keeps_pbits(gpu, oracle):
+    """Reset clears registers/keys/values; pbits is untouched (super_spread.go:297-311)."""
+    rng = np.random.default_rng(4)
+    ss, orc = make_pair(oracle, 256, 2, 32, 5, 8, 8)
+    fl, el, _ = spread_stream(rng, 40_000, 200, 8, 8)
+    ss.insert_keys(fl, el)
+    orc.insert(fl, el)
+    ss.reset()
+    orc.reset()
+    ss.flush()
+    assert_same_ss(ss, orc)
+    fl, el, _ = spread_stream(rng, 40_000, 200, 8, 8)
+    ss.insert_keys(fl, el)
+    orc.insert(fl, el)
+    ss.flush()
+    assert_same_ss(ss, orc)
+
+
+@pytest.mark.parametrize("ffields,efields", [
+    (["SrcIP"], ["DstIP"]),
+    (["SrcIP", "SrcPort"], ["DstIP", "DstPort", "Protocol"]),
+    (["DstPort"], ["SrcIP"]),
+])
+def test_tuples_and_headers_parity(gpu, oracle, ffields, efields):
+    from go2netspectra_amd import PacketBatch, SuperSpread
+    rng = np.random.default_rng(len(ffields) * 10 + len(efields))
+    t = random_tuples(rng, 60_000, 4000, v6_frac=0.2, s=1.0)
+    seeds = np.array([0x1111, 0x2222, 0x3333], np.uint32)
+    batch = PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"])
+    kw = dict(flow_fields=ffields, elem_fields=efields, seeds=seeds, hll_master=HLL_MASTER, rng_seed=RNG_SEED)
+    ss = SuperSpread(2048, 3, 20, 64, 5, 0.5, 1.08, **kw)
+    ss.insert_tuples(batch)
+    ss.flush()
+    fk, ek = batch.keys(ffields), batch.keys(efields)
+    orc = oracle.SuperSpread(2048, 3, 20, 64, 5, 0.5, 1.08, fk.shape[1], ek.shape[1], seeds, HLL_MASTER, RNG_SEED)
+    orc.insert(fk, ek)
+    assert_same_ss(ss, orc)
+    # 64-byte frame records, with some records the parser drops
+    hdr = frames_from_tuples(t, rng, vlan_frac=0.3)
+    bad = rng.random(len(hdr)) < 0.02
+    hdr[bad, 12:14] = [0x08, 0x06]  # ARP: dropped, still advances the packet index
+    ss2 = SuperSpread(2048, 3, 20, 64, 5, 0.5, 1.08, **kw)
+    ss2.insert_headers(hdr, t["length"])
+    ss2.flush()
+    orc2 = oracle.SuperSpread(2048, 3, 20, 64, 5, 0.5, 1.08, fk.shape[1], ek.shape[1], seeds, HLL_MASTER,
+                              RNG_SEED)
+    done = orc2.insert_hdr64(hdr, t["length"], ffields, efields)
+    st = ss2.stats()
+    assert done == st["inserted"] and st["dropped"] == int(bad.sum())
+    assert st["packets"] == orc2.packets() == len(hdr)
+    assert_same_ss(ss2, orc2)
+
+
+def test_golden_stream_fixture(gpu):
+    """The committed oracle fixture (tests/golden/ss_stream.npz) through the engine."""
+    from go2netspectra_amd import SuperSpread
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "ss_stream.npz"))
+    w, d, thr, m, size, Kf, Ke = (int(x) for x in z["params"])
+    base, b = (float(x) for x in z["fparams"])
+    hm, rs = (int(x) for x in z["seeds64"])
+    ss = SuperSpread(w, d, thr, m, size, base, b, flow_bytes=Kf, elem_bytes=Ke, seeds=z["seeds"],
+                     hll_master=hm, rng_seed=rs)
+    ss.insert_keys(z["flows"], z["elems"])
+    ss.flush()
+    values, keys, regs, pbits = ss.export_state()
+    assert np.array_equal(values, z["values"]) and np.array_equal(keys, z["keys"])
+    assert np.array_equal(regs, z["regs"]) and np.array_equal(pbits.view(np.uint64), z["pbits"].view(np.uint64))
+    hh = ss.heavy_hitters()
+    assert [h.Count for h in hh.Count] == z["hh"].tolist()
+    assert [h.Flow for h in hh.Count] == [bytes(x).ljust(Kf, b"\0") for x in z["hh_flows"]]
+
+
+def test_synthetic_device_resident(gpu, oracle):
+    """C3 shape on device-resident synthetic headers: flow SrcIP, element DstIP."""
+    import torch
+    from go2netspectra_amd import SuperSpread, SyntheticTraffic
+    syn = SyntheticTraffic()
+    hdr, wl = syn.generate(1_000_000)
+    seeds = np.array([0xA1, 0xB2, 0xC3], np.uint32)
+    kw = dict(flow_fields=["SrcIP"], elem_fields=["DstIP"], seeds=seeds, hll_master=HLL_MASTER, rng_seed=RNG_SEED)
+    ss = SuperSpread(1 << 16, 3, 4096, 128, 5, 0.5, 1.08, **kw)
+    ss.insert_headers(hdr, wl)
+    ss.flush()
+    torch.cuda.synchronize()
+    orc = oracle.SuperSpread(1 << 16, 3, 4096, 128, 5, 0.5, 1.08, 16, 16, seeds, HLL_MASTER, RNG_SEED)
+    assert orc.insert_hdr64(hdr.cpu().numpy(), wl.cpu().numpy().view(np.uint32), ["SrcIP"], ["DstIP"]) == 1_000_000
+    assert_same_ss(ss, orc)
