@@ -81,6 +81,99 @@ def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0):
     }
 
 
+def cpu_baseline_ss(hdr_dev, wl_dev, seconds: float = 10.0):
+    """Sequential SuperSpread oracle on a bounded prefix of the same stream (rank 0)."""
+    from oracle import oracle as orc
+    n = min(int(wl_dev.shape[0]), 8_000_000)
+    hdr = hdr_dev[:n].cpu().numpy()
+    wl = wl_dev[:n].cpu().numpy().view(np.uint32)
+    ss = orc.SuperSpread(SS_W, SS_D, SS_THR, SS_M, 5, 0.5, 1.08, 16, 16, row_seeds(SS_D), SS_HLL, SS_RNG)
+    chunk, done, t0 = 500_000, 0, time.perf_counter()
+    while done < n and time.perf_counter() - t0 < seconds:
+        m = min(chunk, n - done)
+        ss.insert_hdr64(hdr[done:done + m], wl[done:done + m], ["SrcIP"], ["DstIP"])
+        done += m
+    rate = done / (time.perf_counter() - t0) / 1e6
+    return {"value": round(rate, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port",
+            "sample": f"first {done:,} packets of window 0; sequential C restatement of "
+                      f"super_spread.go (parse + encode + HLL + MV), 1 thread"}
+
+
+# configs[2] / SURVEY §8d C3: the reference's default SuperSpread task
+# (configs/config.yaml:112-122): flow [SrcIP], element [DstIP], d=2, w=32768,
+# m=128, size=5, base=0.5, b=1.08; per-source fan-out Zipf(1.1) over 2^20 dsts.
+SS_W, SS_D, SS_M, SS_THR, SS_FANOUT = 32768, 2, 128, 4096, 1 << 20
+SS_HLL, SS_RNG = 0x0123456789ABCDEF, 0x0DDBA11CAFEF00D5
+
+
+def bench_superspread(args, torch, dist, world, rank, local):
+    """configs[2]: SuperSpread over 100M-packet windows in HBM.  Every step is a
+    fresh window of the stream (packets [k*n, (k+1)*n)), generated on the device
+    between steps and excluded from the timed sum, so HLL encodes keep
+    happening as they would on live traffic (replaying one window would make
+    every later pass encode-free)."""
+    from go2netspectra_amd import SuperSpread, SyntheticTraffic
+    n = args.packets
+    syn = SyntheticTraffic(shard=rank, nshards=world, device=local, fanout=SS_FANOUT)
+    hdr = torch.empty((n, 64), dtype=torch.uint8, device=f"cuda:{local}")
+    wl = torch.empty((n,), dtype=torch.int32, device=f"cuda:{local}")
+    ss = SuperSpread(SS_W, SS_D, SS_THR, SS_M, 5, 0.5, 1.08, flow_fields=["SrcIP"], elem_fields=["DstIP"],
+                     seeds=row_seeds(SS_D), hll_master=SS_HLL, rng_seed=SS_RNG,
+                     batch_packets=args.batch or (8 << 20), device=local)
+    elapsed = 0.0
+    for k in range(args.warmup + args.steps):
+        syn.fill(hdr, wl, first=k * n)
+        if k == args.warmup:
+            ss.set_timing(True)
+            ss.stage_times(reset=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ss.insert_headers(hdr, wl)
+        ss.flush()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        if k >= args.warmup:
+            elapsed += time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    stages = ss.stage_times()
+    kern = {k: v for k, v in stages.items() if k in ("extract", "resolve", "encode", "apply")}
+    dom = max(kern, key=lambda k: kern[k][0])
+    dom_ms, dom_launches = kern[dom]
+    avg_ms = dom_ms / max(dom_launches, 1)
+    pkts_per_launch = n * args.steps / max(dom_launches, 1)
+    achieved = BYTES_PER_PKT * pkts_per_launch / (avg_ms * 1e-3) / 1e9
+    hh = ss.heavy_hitters()
+    line = {
+        "metric": "Mpackets/s SuperSpread update (device-resident, d=2 w=32768 m=128)",
+        "value": round(n * args.steps * world / elapsed / 1e6, 2), "unit": "Mpackets/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8/u32/f64",
+        "data": "synthetic (Zipf 1.1 sources over 2^20 5-tuples, per-packet Zipf 1.1 DstIP over 2^20, "
+                "on-device generator, fresh window per step)",
+        "config": {"workload": "configs[2]: SuperSpread flow=SrcIP elem=DstIP (default task geometry), "
+                               "100M headers in HBM per GPU per step, bit-exact registers/pbits/counters",
+                   "packets_per_step_per_gpu": n},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_per_packet": BYTES_PER_PKT, "kernel_avg_ms": round(avg_ms, 4)},
+        "stage_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()},
+        "heavy_hitters": len(hh.Count), "engine_counters": ss.counters(),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_ss(*syn.generate(8_000_000))
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,6 +182,8 @@ def main():
     ap.add_argument("--packets", type=int, default=PACKETS)
     ap.add_argument("--batch", type=int, default=0, help="device batch (packets); 0 = whole step")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--sketch", choices=["countmin", "superspread"], default="countmin",
+                    help="superspread = configs[2] (not the headline metric)")
     ap.add_argument("--host-input", action="store_true",
                     help="time inserts from host memory (PCIe-inclusive rate, for DESIGN.md)")
     args = ap.parse_args()
@@ -107,6 +202,8 @@ def main():
 
     from go2netspectra_amd import CountMin, SyntheticTraffic
 
+    if args.sketch == "superspread":
+        return bench_superspread(args, torch, dist, world, rank, local)
     n = args.packets
     syn = SyntheticTraffic(shard=rank, nshards=world, device=local)
     hdr, wl = syn.generate(n)

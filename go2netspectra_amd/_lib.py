@@ -27,7 +27,7 @@ EXPORTED = [
     "gns_cm_export_state", "gns_cm_stats", "gns_cm_counters", "gns_cm_set_timing", "gns_cm_stage_times", "gns_cm_stream",
     "gns_ss_create", "gns_ss_destroy", "gns_ss_insert_keys", "gns_ss_insert_tuples",
     "gns_ss_insert_headers", "gns_ss_flush", "gns_ss_query", "gns_ss_heavy_hitters", "gns_ss_reset",
-    "gns_ss_export_state", "gns_ss_stats", "gns_ss_set_timing", "gns_ss_stage_times",
+    "gns_ss_export_state", "gns_ss_stats", "gns_ss_counters", "gns_ss_set_timing", "gns_ss_stage_times",
     "gns_synth_create", "gns_synth_destroy", "gns_synth_fill", "gns_synth_flows",
     "gns_pack_pcap", "gns_last_error", "gns_version",
 ]
@@ -77,7 +77,7 @@ class SsParams(ct.Structure):
 class SynthParams(ct.Structure):
     _fields_ = [("flows", ct.c_uint32), ("zipf_s", ct.c_double), ("tuple_seed", ct.c_uint64),
                 ("rank_seed", ct.c_uint64), ("len_seed", ct.c_uint64), ("shard", ct.c_uint32),
-                ("nshards", ct.c_uint32), ("device", ct.c_int)]
+                ("nshards", ct.c_uint32), ("device", ct.c_int), ("fanout", ct.c_uint32)]
 
 
 _lib = None
@@ -119,6 +119,7 @@ def load() -> ct.CDLL:
         "gns_ss_flush": ([vp], i32), "gns_ss_query": ([vp, vp, u32, u64, vp], i32),
         "gns_ss_heavy_hitters": ([vp, vp, vp, vp], i32), "gns_ss_reset": ([vp], i32),
         "gns_ss_export_state": ([vp, vp, vp, vp, vp], i32), "gns_ss_stats": ([vp, vp], i32),
+        "gns_ss_counters": ([vp, vp], i32),
         "gns_ss_set_timing": ([vp, i32], i32), "gns_ss_stage_times": ([vp, vp, vp, i32], i32),
         "gns_synth_create": ([vp, vp], i32), "gns_synth_destroy": ([vp], i32),
         "gns_synth_fill": ([vp, vp, vp, u64, u64], i32), "gns_synth_flows": ([vp, vp], i32),

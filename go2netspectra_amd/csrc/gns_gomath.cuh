@@ -97,6 +97,39 @@ __host__ __device__ inline double go_pow_int(double x, double y) {
     return go_ldexp(a1, ae);
 }
 
+// deterministic log on (0, 1] (oracle: or_det_log)
+__host__ __device__ inline double gm_log(double x) {
+    const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+    const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01;
+    const double L3 = 2.857142874366239149e-01, L4 = 2.222219843214978396e-01;
+    const double L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01;
+    const double L7 = 1.479819860511658591e-01;
+    int ki;
+    double f1 = go_frexp(x, &ki);
+    if (f1 < 0.70710678118654752440) { f1 *= 2; ki--; }
+    const double f = f1 - 1;
+    const double k = (double)ki;
+    const double s = f / (2 + f);
+    const double s2 = s * s;
+    const double s4 = s2 * s2;
+    const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+    const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+    const double R = t1 + t2;
+    const double hfsq = 0.5 * f * f;
+    return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+// log(1 - p), 0 < p < 1 (oracle: or_det_log1m)
+__host__ __device__ inline double gm_log1m(double p) {
+    if (p < 1e-4) {
+        const double t = p * p;
+        double r = p + t * 0.5;
+        r = r + t * p * (1.0 / 3.0);
+        return -r;
+    }
+    return gm_log(1.0 - p);
+}
+
 #pragma clang fp contract(on)
 
 }  // namespace gns

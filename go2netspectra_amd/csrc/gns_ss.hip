@@ -31,7 +31,6 @@ namespace gns {
 
 constexpr int kSsNW = 20;             // merged key words (flow ‖ elem <= 74 bytes)
 constexpr uint32_t kSsPktBits = 27;   // packet index bits in the sort keys (batch <= 2^27)
-constexpr uint32_t kSsDrawCap = 1u << 24;
 constexpr int kSsThreads = 256;
 constexpr uint32_t kSsChunk = 16384;
 
@@ -50,7 +49,6 @@ struct SsExtractArgs {
     InputDesc in;
     uint64_t n;
     KeyPlanN kpf, kpm;
-    int modef, modem;
     SsGeom g;
     DictDev D;
     uint32_t epoch;
@@ -58,23 +56,28 @@ struct SsExtractArgs {
     uint32_t *flowid;
     uint64_t *pend;
     uint32_t *pend_cnt, *pend_total;
-    uint64_t *ckey;     // candidates: (cell*m + reg) << 27 | packet
+    uint64_t *ckey;     // candidates: (cell*m + reg) << 27 | packet, block regions of chunk*d
     uint32_t *cval;     // lz
-    uint32_t *ccount;
-    uint32_t ccap;
+    uint32_t *ccount;   // total candidates
+    uint32_t *cblk;     // [2*nblk]: per-block count, per-block output base
     unsigned long long *stats;  // 0 inserted, 1 dropped, 2 unsupported, 3 dict full, 4 cand overflow, 5 encodes
 };
 
-template <int NW>
-__device__ __forceinline__ void make_key_rt(int mode, uint32_t K, const uint8_t *s_src,
-                                            const uint32_t (&tw)[10], uint32_t (&kw)[NW]) {
-    if (mode == PLAN_SLICE0) make_key_m<PLAN_SLICE0, NW>(K, s_src, tw, kw);
-    else if (mode == PLAN_SLICE4) make_key_m<PLAN_SLICE4, NW>(K, s_src, tw, kw);
-    else make_key_m<PLAN_GENERIC, NW>(K, s_src, tw, kw);
+// one wave-aggregated atomic for every lane that wants a slot (call convergently)
+__device__ __forceinline__ uint32_t wave_alloc(uint32_t *ctr, bool want) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return 0;
+    const uint32_t lane = __lane_id();
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
 }
 
-// flow key (kwf) and merged key flow‖elem (kwm) of packet p
-template <int KIND>
+// flow key (kwf) and merged key flow‖elem (kwm) of packet p.  MF/MM: plan
+// modes of the flow and merged layouts (SLICE0 for SrcIP / SrcIP‖DstIP).
+template <int KIND, int MF, int MM>
 __device__ __forceinline__ int ss_keys(const SsExtractArgs &a, const uint8_t *s_srcf, const uint8_t *s_srcm,
                                        uint64_t p, uint32_t (&kwf)[GNS_KWMAX], uint32_t (&kwm)[kSsNW]) {
     if constexpr (KIND == IN_KEYS) {
@@ -99,27 +102,29 @@ __device__ __forceinline__ int ss_keys(const SsExtractArgs &a, const uint8_t *s_
         uint32_t tw[10];
         const int st = load_tuple<KIND>(a.in, p, tw);
         if (st != PARSE_OK) return st;
-        make_key_rt<GNS_KWMAX>(a.modef, a.g.Kf, s_srcf, tw, kwf);
-        make_key_rt<kSsNW>(a.modem, a.g.Km, s_srcm, tw, kwm);
+        make_key_m<MF, GNS_KWMAX>(a.g.Kf, s_srcf, tw, kwf);
+        make_key_m<MM, kSsNW>(a.g.Km, s_srcm, tw, kwm);
         return PARSE_OK;
     }
 }
 
 // S1: keys, flow id, per-row HLL encode test against the batch-entry registers
-template <int KIND>
+template <int KIND, int MF, int MM>
 __global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
     __shared__ uint8_t s_srcf[80], s_srcm[80];
-    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
+    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_cc;
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
     for (uint32_t j = tid; j < 80; j += kSsThreads) { s_srcf[j] = a.kpf.src[j]; s_srcm[j] = a.kpm.src[j]; }
-    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; }
+    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; s_cc = 0; }
     __syncthreads();
     const uint64_t beg = (uint64_t)blk * kSsChunk;
     const uint64_t end = min(a.n, beg + kSsChunk);
+    uint64_t *rkey = a.ckey + beg * a.g.d;  // this block's candidate region (never overflows)
+    uint32_t *rval = a.cval + beg * a.g.d;
     uint32_t n_ok = 0;
     for (uint64_t p = beg + tid; p < end; p += kSsThreads) {
         uint32_t kwf[GNS_KWMAX], kwm[kSsNW];
-        const int st = ss_keys<KIND>(a, s_srcf, s_srcm, p, kwf, kwm);
+        const int st = ss_keys<KIND, MF, MM>(a, s_srcf, s_srcm, p, kwf, kwm);
         if (st != PARSE_OK) {
             a.flowid[p] = GNS_ID_NONE;
             atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
@@ -154,14 +159,11 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
             if (lz > a.g.maxv) lz = a.g.maxv;
             const uint32_t idx = mm3_chain<kSsNW>(mkm, a.g.Km, s1) % a.g.m;  // :87-88
             const uint64_t seg = cell * a.g.m + idx;
-            if (lz > a.regs[seg]) {  // can encode only if above the batch-entry register
-                const uint32_t q = atomicAdd(a.ccount, 1u);
-                if (q < a.ccap) {
-                    a.ckey[q] = seg << kSsPktBits | (p & ((1ull << kSsPktBits) - 1));
-                    a.cval[q] = lz;
-                } else {
-                    atomicAdd(&a.stats[4], 1ull);
-                }
+            const bool want = lz > a.regs[seg];  // can encode only if above the batch-entry register
+            const uint32_t q = wave_alloc(&s_cc, want);
+            if (want) {
+                rkey[q] = seg << kSsPktBits | (p & ((1ull << kSsPktBits) - 1));
+                rval[q] = lz;
             }
         }
     }
@@ -169,6 +171,9 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
     __syncthreads();
     if (tid == 0) {
         a.pend_cnt[blk] = s_pend;
+        a.cblk[blk] = s_cc;
+        a.cblk[gridDim.x + blk] = s_cc ? atomicAdd(a.ccount, s_cc) : 0u;
+        if (s_cc) atomicAdd(&a.stats[4], (unsigned long long)s_cc);
         if (s_pend) atomicAdd(a.pend_total, s_pend);
         if (s_ok) atomicAdd(&a.stats[0], (unsigned long long)s_ok);
         if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
@@ -185,7 +190,7 @@ struct SsResolveArgs {
     uint32_t *cnt_out, *total_out;
 };
 
-template <int KIND>
+template <int KIND, int MF, int MM>
 __global__ __launch_bounds__(kSsThreads) void k_ss_resolve(SsResolveArgs r) {
     __shared__ uint8_t s_srcf[80], s_srcm[80];
     __shared__ uint32_t s_cnt, s_full;
@@ -200,7 +205,7 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_resolve(SsResolveArgs r) {
         const uint64_t v = r.pend_in[beg + i];
         const uint64_t p = beg + (v >> 32);
         uint32_t kwf[GNS_KWMAX], kwm[kSsNW];
-        (void)ss_keys<KIND>(a, s_srcf, s_srcm, p, kwf, kwm);
+        (void)ss_keys<KIND, MF, MM>(a, s_srcf, s_srcm, p, kwf, kwm);
         uint32_t out;
         const int res = dict_find_or_claim(a.D, kwf, (uint32_t)v, a.epoch, &out);
         if (res == DICT_FOUND) a.flowid[p] = out;
@@ -212,6 +217,18 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_resolve(SsResolveArgs r) {
         r.cnt_out[blk] = s_cnt;
         if (s_cnt) atomicAdd(r.total_out, s_cnt);
         if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+    }
+}
+
+// S1b: block regions -> one dense candidate array (sort input)
+__global__ __launch_bounds__(256) void k_ss_compact(const uint64_t *rkey, const uint32_t *rval, const uint32_t *cblk,
+                                                    uint32_t d, uint64_t *okey, uint32_t *oval) {
+    const uint32_t blk = blockIdx.x;
+    const uint32_t cnt = cblk[blk], base = cblk[gridDim.x + blk];
+    const uint64_t r = (uint64_t)blk * kSsChunk * d;
+    for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+        okey[base + i] = rkey[r + i];
+        oval[base + i] = rval[r + i];
     }
 }
 
@@ -286,17 +303,28 @@ __global__ __launch_bounds__(256) void k_ss_apply(SsApplyArgs a) {
         if (ss_uniform(a.g.rng_seed, pkt, row, 0) >= pCU) continue;          // :201-204
         int64_t vv = (cv < 9223372036854775808.0) ? (int64_t)cv : INT64_MIN;  // :206, amd64 semantics
         const uint32_t f = a.flowid[p];
-        uint32_t draw = 1, draws = 0;
+        uint32_t draw = 1;
         while (vv > 0) {                                                    // :207-233
-            if (val == 0 || key == f) {  // every remaining iteration increments
+            if (val == 0 || key == f) {  // every remaining iteration increments (:211-220)
                 if (val == 0) key = f;
                 val = (uint32_t)((uint64_t)val + (uint64_t)vv);
                 break;
             }
-            vv--;
-            if (draws++ >= kSsDrawCap) break;
             const double ppp = go_pow_int(a.g.b, -(double)val);              // :222
-            if (ss_uniform(a.g.rng_seed, pkt, row, draw++) < ppp) val = val - 1;  // :223-227
+            if (!(ppp > 0)) break;  // underflow: no later iteration can decrement
+            if (ppp >= 1) {         // b <= 1: every iteration decrements
+                const int64_t dec = (int64_t)val < vv ? (int64_t)val : vv;
+                val -= (uint32_t)dec;
+                vv -= dec;
+                continue;
+            }
+            // declared generator: failed iterations before the next decrement
+            // (:223-227) as one geometric waiting time
+            const double u = ss_uniform(a.g.rng_seed, pkt, row, draw++);
+            const double q = gm_log(1.0 - u) / gm_log1m(ppp);
+            if (!(q < (double)vv)) break;
+            vv -= (int64_t)floor(q) + 1;
+            val -= 1;
         }
     }
     a.pbits[cell] = pb;
@@ -369,6 +397,7 @@ struct gns_ss {
     uint64_t dict_slots = 0;
     uint32_t epoch = 0;
     uint64_t pkt = 0;     // records inserted since create (RNG packet index)
+    uint64_t n_encodes = 0, n_batches = 0;
     uint64_t bmax = 0;
     uint32_t nblk_max = 0;
     uint32_t *flowid = nullptr;
@@ -379,6 +408,7 @@ struct gns_ss {
     uint64_t *ckey = nullptr, *ckey_s = nullptr, *skey = nullptr, *skey_s = nullptr;
     uint32_t *cval = nullptr, *cval_s = nullptr, *cmax = nullptr, *sval = nullptr, *sval_s = nullptr;
     uint32_t *counts = nullptr;  // [0] candidates, [1] successes
+    uint32_t *cblk = nullptr;
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
     unsigned long long *stats = nullptr;
@@ -400,7 +430,7 @@ void ss_free_all(gns_ss *ss) {
     dfree(ss->flowid); dfree(ss->pend[0]); dfree(ss->pend[1]); dfree(ss->pcnt[0]); dfree(ss->pcnt[1]);
     dfree(ss->ptotal); dfree(ss->ckey); dfree(ss->ckey_s); dfree(ss->skey); dfree(ss->skey_s);
     dfree(ss->cval); dfree(ss->cval_s); dfree(ss->cmax); dfree(ss->sval); dfree(ss->sval_s);
-    dfree(ss->counts); dfree(ss->tmp); dfree(ss->stats); dfree(ss->stage);
+    dfree(ss->counts); dfree(ss->cblk); dfree(ss->tmp); dfree(ss->stats); dfree(ss->stage);
     if (ss->h_pin) (void)hipHostFree(ss->h_pin);
     ss->timer.destroy();
     if (ss->stream) (void)hipStreamDestroy(ss->stream);
@@ -433,7 +463,7 @@ size_t ss_tmp_need(gns_ss *ss, uint64_t n) {
     return std::max(a, b) + 256;
 }
 
-template <int KIND>
+template <int KIND, int MF, int MM>
 int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     if (n == 0) return GNS_OK;
     hipStream_t s = ss->stream;
@@ -443,13 +473,13 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     GNS_HIP(hipMemsetAsync(ss->counts, 0, 8, s));
     if (++ss->epoch == 0) ss->epoch = 1;
     SsExtractArgs x{};
-    x.in = in; x.n = n; x.kpf = ss->kpf; x.kpm = ss->kpm; x.modef = plan_mode(ss->kpf); x.modem = plan_mode(ss->kpm);
+    x.in = in; x.n = n; x.kpf = ss->kpf; x.kpm = ss->kpm;
     x.g = ss->g; x.D = ss->D; x.epoch = ss->epoch; x.regs = ss->regs; x.flowid = ss->flowid;
     x.pend = ss->pend[0]; x.pend_cnt = ss->pcnt[0]; x.pend_total = ss->ptotal;
-    x.ckey = ss->ckey; x.cval = ss->cval; x.ccount = ss->counts; x.ccap = (uint32_t)ss->ccap; x.stats = ss->stats;
+    x.ckey = ss->ckey; x.cval = ss->cval; x.ccount = ss->counts; x.cblk = ss->cblk; x.stats = ss->stats;
     {
         ScopedStage st(ss->timer, 0);
-        hipLaunchKernelGGL(k_ss_extract<KIND>, dim3(nblk), dim3(kSsThreads), 0, s, x);
+        hipLaunchKernelGGL((k_ss_extract<KIND, MF, MM>), dim3(nblk), dim3(kSsThreads), 0, s, x);
         GNS_HIP(hipGetLastError());
     }
     int cur = 0;
@@ -458,7 +488,6 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         GNS_HIP(hipMemcpyAsync(ss->h_pin + 2, ss->stats + 3, 16, hipMemcpyDeviceToHost, s));
         GNS_HIP(hipStreamSynchronize(s));
         if (ss->h_pin[2] | ss->h_pin[3]) { set_error("flow dictionary full; raise max flows"); return GNS_E_FULL; }
-        if (ss->h_pin[4] | ss->h_pin[5]) { set_error("candidate buffer overflow"); return GNS_E_RANGE; }
         if (ss->h_pin[0] == 0) break;
         if (round > 64) { set_error("dictionary resolve did not converge"); return GNS_E_FULL; }
         GNS_HIP(hipMemsetAsync(ss->ptotal + (cur ^ 1), 0, 4, s));
@@ -468,7 +497,7 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         r.pend_in = ss->pend[cur]; r.cnt_in = ss->pcnt[cur];
         r.pend_out = ss->pend[cur ^ 1]; r.cnt_out = ss->pcnt[cur ^ 1]; r.total_out = ss->ptotal + (cur ^ 1);
         ScopedStage st(ss->timer, 1);
-        hipLaunchKernelGGL(k_ss_resolve<KIND>, dim3(nblk), dim3(kSsThreads), 0, s, r);
+        hipLaunchKernelGGL((k_ss_resolve<KIND, MF, MM>), dim3(nblk), dim3(kSsThreads), 0, s, r);
         GNS_HIP(hipGetLastError());
         cur ^= 1;
     }
@@ -479,21 +508,25 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         const unsigned bits = std::min(64u, kSsPktBits + ceil_log2((uint64_t)ss->g.d * ss->g.w * ss->g.m) + 1);
         {
             ScopedStage st(ss->timer, 2);
+            hipLaunchKernelGGL(k_ss_compact, dim3(nblk), dim3(256), 0, s, ss->ckey, ss->cval, ss->cblk, ss->g.d,
+                               ss->ckey_s, ss->cval_s);
+            GNS_HIP(hipGetLastError());
             size_t tb = ss->tmp_bytes;
-            if (rocprim::radix_sort_pairs(ss->tmp, tb, ss->ckey, ss->ckey_s, ss->cval, ss->cval_s, (size_t)nc, 0u,
+            if (rocprim::radix_sort_pairs(ss->tmp, tb, ss->ckey_s, ss->ckey, ss->cval_s, ss->cval, (size_t)nc, 0u,
                                           bits, s) != hipSuccess) { set_error("candidate sort failed"); return GNS_E_HIP; }
-            auto kit = rocprim::make_transform_iterator(ss->ckey_s, SegKey());
+            auto kit = rocprim::make_transform_iterator(ss->ckey, SegKey());
             tb = ss->tmp_bytes;
-            if (rocprim::inclusive_scan_by_key(ss->tmp, tb, kit, ss->cval_s, ss->cmax, (size_t)nc,
+            if (rocprim::inclusive_scan_by_key(ss->tmp, tb, kit, ss->cval, ss->cmax, (size_t)nc,
                                                rocprim::maximum<uint32_t>(), rocprim::equal_to<uint64_t>(),
                                                s) != hipSuccess) { set_error("segmented max failed"); return GNS_E_HIP; }
-            SsSuccArgs a{ss->ckey_s, ss->cval_s, ss->cmax, nc, ss->regs, ss->g.m, ss->skey, ss->sval, ss->counts + 1};
+            SsSuccArgs a{ss->ckey, ss->cval, ss->cmax, nc, ss->regs, ss->g.m, ss->skey, ss->sval, ss->counts + 1};
             hipLaunchKernelGGL(k_ss_success, dim3((nc + 255) / 256), dim3(256), 0, s, a);
             GNS_HIP(hipGetLastError());
         }
         GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->counts + 1, 4, hipMemcpyDeviceToHost, s));
         GNS_HIP(hipStreamSynchronize(s));
         const uint32_t ns = ss->h_pin[0];
+        ss->n_encodes += ns;
         if (ns > 0) {
             ScopedStage st(ss->timer, 3);
             const unsigned bits2 = std::min(64u, kSsPktBits + ceil_log2((uint64_t)ss->g.d * ss->g.w) + 1);
@@ -507,6 +540,7 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         }
     }
     ss->pkt += n;  // every record advances the RNG packet index
+    ss->n_batches++;
     return GNS_OK;
 }
 
@@ -563,7 +597,13 @@ int ss_insert(gns_ss *ss, InputDesc in, uint64_t n, gns_mem where) {
                 d.sizes = reinterpret_cast<const uint32_t *>(p);
             }
         }
-        GNS_TRY(ss_run_batch<KIND>(ss, d, m));
+        if constexpr (KIND == IN_KEYS) {
+            GNS_TRY((ss_run_batch<KIND, PLAN_GENERIC, PLAN_GENERIC>(ss, d, m)));
+        } else if (plan_mode(ss->kpf) == PLAN_SLICE0 && plan_mode(ss->kpm) == PLAN_SLICE0) {
+            GNS_TRY((ss_run_batch<KIND, PLAN_SLICE0, PLAN_SLICE0>(ss, d, m)));
+        } else {
+            GNS_TRY((ss_run_batch<KIND, PLAN_GENERIC, PLAN_GENERIC>(ss, d, m)));
+        }
     }
     return GNS_OK;
 }
@@ -649,7 +689,7 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
             (rc = dalloc_t(&ss->skey, ss->ccap)) || (rc = dalloc_t(&ss->skey_s, ss->ccap)) ||
             (rc = dalloc_t(&ss->cval, ss->ccap)) || (rc = dalloc_t(&ss->cval_s, ss->ccap)) ||
             (rc = dalloc_t(&ss->cmax, ss->ccap)) || (rc = dalloc_t(&ss->sval, ss->ccap)) ||
-            (rc = dalloc_t(&ss->sval_s, ss->ccap)) || (rc = dalloc_t(&ss->counts, 4)) ||
+            (rc = dalloc_t(&ss->sval_s, ss->ccap)) || (rc = dalloc_t(&ss->counts, 4)) || (rc = dalloc_t(&ss->cblk, 2ull * ss->nblk_max)) ||
             (rc = dalloc_t(&ss->stats, 8)))
             break;
         ss->tmp_bytes = ss_tmp_need(ss, ss->ccap);
@@ -849,6 +889,17 @@ int gns_ss_stats(gns_ss *ss, uint64_t stats[4]) {
     unsigned long long h[8];
     GNS_HIP(hipMemcpy(h, ss->stats, sizeof(h), hipMemcpyDeviceToHost));
     stats[0] = h[0]; stats[1] = h[1]; stats[2] = h[2]; stats[3] = ss->pkt;
+    return GNS_OK;
+}
+
+int gns_ss_counters(gns_ss *ss, uint64_t out[8]) {
+    if (!ss || !out) return GNS_E_ARG;
+    GNS_TRY(ss_set_dev(ss));
+    GNS_HIP(hipStreamSynchronize(ss->stream));
+    unsigned long long h[8];
+    GNS_HIP(hipMemcpy(h, ss->stats, sizeof(h), hipMemcpyDeviceToHost));
+    out[0] = h[0]; out[1] = h[1]; out[2] = h[2]; out[3] = h[3]; out[4] = h[4];
+    out[5] = ss->n_encodes; out[6] = ss->pkt; out[7] = ss->n_batches;
     return GNS_OK;
 }
 

@@ -57,7 +57,19 @@ struct SynthDev {
     const double *cdf;                   // inclusive CDF over shard flows (rank order)
     uint32_t nf;
     uint64_t rank_key, len_key;
+    const double *dcdf;                  // fan-out mode: CDF over destinations (nd > 0)
+    uint32_t nd;
+    uint64_t dst_key;
 };
+
+__device__ __forceinline__ uint32_t cdf_search(const double *cdf, uint32_t n, double u) {
+    uint32_t lo = 0, hi = n - 1;  // first j with cdf[j] > u
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cdf[mid] > u) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
 
 __global__ __launch_bounds__(256) void k_synth(SynthDev s, uint32_t *hdr, uint32_t *wirelen,
                                                uint64_t first, uint64_t n) {
@@ -65,14 +77,15 @@ __global__ __launch_bounds__(256) void k_synth(SynthDev s, uint32_t *hdr, uint32
     if (i >= n) return;
     const uint64_t pk = first + i;
     const double u = (double)(mix64_d(s.rank_key + pk * 0x9E3779B97F4A7C15ull) >> 11) * 0x1.0p-53;
-    uint32_t lo = 0, hi = s.nf - 1;  // first j with cdf[j] > u
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s.cdf[mid] > u) hi = mid; else lo = mid + 1;
-    }
-    const uint32_t f = lo;
+    const uint32_t f = cdf_search(s.cdf, s.nf, u);
     const uint32_t len = 64u + (uint32_t)(mix64_d(s.len_key + pk * 0x9E3779B97F4A7C15ull) % 1455u);
-    const uint32_t src = s.src[f], dst = s.dst[f], ports = s.ports[f];
+    const uint32_t src = s.src[f], ports = s.ports[f];
+    uint32_t dst = s.dst[f];
+    if (s.nd) {  // per-packet destination: Zipf rank -> hashed address
+        const uint64_t dk = mix64_d(s.dst_key + pk * 0x9E3779B97F4A7C15ull);
+        const uint32_t r = cdf_search(s.dcdf, s.nd, (double)(dk >> 11) * 0x1.0p-53);
+        dst = (uint32_t)mix64_d(0xD57D57ull + r);
+    }
     const uint32_t proto = s.proto[f];
     uint8_t b[64];
 #pragma unroll
@@ -119,7 +132,7 @@ struct gns_synth {
     SynthDev dev{};
     uint32_t *src = nullptr, *dst = nullptr, *ports = nullptr;
     uint8_t *proto = nullptr;
-    double *cdf = nullptr;
+    double *cdf = nullptr, *dcdf = nullptr;
 };
 
 extern "C" {
@@ -205,15 +218,31 @@ int gns_synth_create(const gns_synth_params *p, gns_synth **out) {
         gns_synth_destroy(sy);
         return GNS_E_HIP;
     }
+    uint32_t nd = p->fanout;
+    if (nd) {
+        std::vector<double> dc(nd);
+        double dacc = 0;
+        for (uint32_t i = 0; i < nd; i++) dacc += std::pow((double)(i + 1), -s);
+        double drun = 0;
+        for (uint32_t i = 0; i < nd; i++) { drun += std::pow((double)(i + 1), -s); dc[i] = drun / dacc; }
+        dc[nd - 1] = 1.0;
+        if ((rc = dalloc_t(&sy->dcdf, nd)) != GNS_OK) { gns_synth_destroy(sy); return rc; }
+        if (hipMemcpy(sy->dcdf, dc.data(), nd * 8, hipMemcpyHostToDevice) != hipSuccess) {
+            set_error("synth upload failed");
+            gns_synth_destroy(sy);
+            return GNS_E_HIP;
+        }
+    }
     sy->dev = SynthDev{sy->src, sy->dst, sy->ports, sy->proto, sy->cdf, nf,
-                       rseed + (uint64_t)shard * 0xD1B54A32D192ED03ull, lseed + (uint64_t)shard * 0x8CB92BA72F3D8DD7ull};
+                       rseed + (uint64_t)shard * 0xD1B54A32D192ED03ull, lseed + (uint64_t)shard * 0x8CB92BA72F3D8DD7ull,
+                       sy->dcdf, nd, rseed ^ 0x7F4A7C159E3779B9ull};
     *out = sy;
     return GNS_OK;
 }
 
 int gns_synth_destroy(gns_synth *s) {
     if (!s) return GNS_OK;
-    dfree(s->src); dfree(s->dst); dfree(s->ports); dfree(s->proto); dfree(s->cdf);
+    dfree(s->src); dfree(s->dst); dfree(s->ports); dfree(s->proto); dfree(s->cdf); dfree(s->dcdf);
     delete s;
     return GNS_OK;
 }

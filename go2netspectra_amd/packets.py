@@ -140,9 +140,11 @@ class SyntheticTraffic:
 
     def __init__(self, flows: int = 1 << 20, zipf_s: float = 1.1, shard: int = 0, nshards: int = 1,
                  device: int = 0, tuple_seed: int = 0x5EED0001, rank_seed: int = 0x5EED0002,
-                 len_seed: int = 0x5EED0003):
+                 len_seed: int = 0x5EED0003, fanout: int = 0):
+        """fanout > 0: every packet's DstIP is drawn Zipf(zipf_s) over `fanout`
+        destinations (per-source fan-out, the SuperSpread C3 stream)."""
         self._L = _lib.load()
-        p = _lib.SynthParams(flows, zipf_s, tuple_seed, rank_seed, len_seed, shard, nshards, device)
+        p = _lib.SynthParams(flows, zipf_s, tuple_seed, rank_seed, len_seed, shard, nshards, device, fanout)
         h = ct.c_void_p()
         check(self._L.gns_synth_create(ct.byref(p), ct.byref(h)))
         self._h = h

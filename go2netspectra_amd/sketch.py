@@ -352,6 +352,12 @@ class SuperSpread:
         check(self._L.gns_ss_stats(self._h, s))
         return {"inserted": s[0], "dropped": s[1], "unsupported": s[2], "packets": s[3]}
 
+    def counters(self) -> dict:
+        s = (ct.c_uint64 * 8)()
+        check(self._L.gns_ss_counters(self._h, s))
+        names = ["inserted", "dropped", "unsupported", "dict_full", "candidates", "encodes", "records", "batches"]
+        return {k: int(s[i]) for i, k in enumerate(names)}
+
     def set_timing(self, on: bool = True) -> None:
         check(self._L.gns_ss_set_timing(self._h, 1 if on else 0))
 

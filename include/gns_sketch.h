@@ -170,6 +170,9 @@ int gns_ss_reset(gns_ss *ss);
 /* values[d*w], keys[d*w*flow_bytes], regs[d*w*m] (u8), pbits[d*w] */
 int gns_ss_export_state(gns_ss *ss, uint32_t *values, uint8_t *keys, uint8_t *regs, double *pbits);
 int gns_ss_stats(gns_ss *ss, uint64_t stats[4]);
+/* out[8]: inserted, dropped, unsupported, dictionary full, HLL candidates
+ * (lz above the batch-entry register), HLL encodes, records, device batches */
+int gns_ss_counters(gns_ss *ss, uint64_t out[8]);
 int gns_ss_set_timing(gns_ss *ss, int on);
 int gns_ss_stage_times(gns_ss *ss, double ms[8], uint64_t launches[8], int reset);
 
@@ -185,6 +188,8 @@ typedef struct gns_synth_params {
     uint64_t len_seed;     /* default 0x5EED0003 */
     uint32_t shard, nshards; /* keep only flows whose src slot hashes to `shard` */
     int device;
+    uint32_t fanout;       /* > 0: each packet's DstIP is drawn Zipf(zipf_s) over `fanout`
+                              destinations instead of the flow's own (SuperSpread C3 shape) */
 } gns_synth_params;
 int gns_synth_create(const gns_synth_params *p, gns_synth **out);
 int gns_synth_destroy(gns_synth *s);

@@ -541,7 +541,71 @@ double or_go_pow(double x, double y) {
 /* ------------------------------------------------------------------------- */
 /* super_spread.go                                                            */
 /* ------------------------------------------------------------------------- */
-#define OR_SS_DRAW_CAP (1u << 24) /* cap on non-owner draws per packet-row */
+/* Deterministic natural log for x in (0, 1]: the fdlibm reduction and
+ * polynomial (as in Go's math.Log), plain IEEE double operations only, so the
+ * device (gns_gomath.cuh gm_log) rounds identically. */
+double or_det_log(double x) {
+    const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+    const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01;
+    const double L3 = 2.857142874366239149e-01, L4 = 2.222219843214978396e-01;
+    const double L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01;
+    const double L7 = 1.479819860511658591e-01;
+    int ki;
+    double f1 = frexp(x, &ki);
+    if (f1 < 0.70710678118654752440) { f1 *= 2; ki--; }
+    double f = f1 - 1;
+    double k = (double)ki;
+    double s = f / (2 + f);
+    double s2 = s * s;
+    double s4 = s2 * s2;
+    double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+    double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+    double R = t1 + t2;
+    double hfsq = 0.5 * f * f;
+    return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+/* log(1 - p) for 0 < p < 1 (series below 1e-4). */
+double or_det_log1m(double p) {
+    if (p < 1e-4) {
+        double t = p * p;
+        double r = p + t * 0.5;
+        r = r + t * p * (1.0 / 3.0);
+        return -r;
+    }
+    return or_det_log(1.0 - p);
+}
+
+/* super_spread.go:207-233 for one (packet, row) after sampling passed.
+ * Owner (or empty) counter: every remaining iteration increments (:211-220).
+ * Foreign counter: iteration t decrements with probability b^-val (:222-227);
+ * the declared generator draws the number of failed iterations before the
+ * next decrement as a geometric waiting time (one uniform per decrement,
+ * draw = 1, 2, ...), the same law as one uniform per iteration. */
+static void ss_mv(uint32_t *val, uint8_t *key, const uint8_t *flow, uint32_t K, int64_t vv, double b,
+                  uint64_t rng_seed, uint64_t pkt, uint32_t row) {
+    uint32_t draw = 1;
+    while (vv > 0) {
+        if (*val == 0 || memcmp(key, flow, K) == 0) {
+            if (*val == 0) memcpy(key, flow, K);
+            *val = (uint32_t)((uint64_t)*val + (uint64_t)vv);
+            return;
+        }
+        double ppp = or_go_pow(b, -(double)*val); /* :222 */
+        if (!(ppp > 0)) return;                   /* underflow: no decrement can happen */
+        if (ppp >= 1) {                           /* b <= 1: every iteration decrements */
+            int64_t k = (int64_t)*val < vv ? (int64_t)*val : vv;
+            *val -= (uint32_t)k;
+            vv -= k;
+            continue;
+        }
+        double u = or_ss_uniform(rng_seed, pkt, row, draw++);
+        double q = or_det_log(1.0 - u) / or_det_log1m(ppp); /* failures before the decrement */
+        if (!(q < (double)vv)) return;
+        vv -= (int64_t)floor(q) + 1;
+        *val -= 1;
+    }
+}
 
 struct or_ss {
     uint32_t d, w, thr, m, size, maxv, Kf, Ke;
@@ -626,22 +690,7 @@ void or_ss_insert(or_ss *ss, const uint8_t *flow, const uint8_t *elem) {
         double cv = ceil(inv);
         /* :206 int(math.Ceil(1.0/tempP)); amd64 maps out-of-range to MinInt64 */
         int64_t tempVV = (cv < 9223372036854775808.0) ? (int64_t)cv : INT64_MIN;
-        uint32_t *val = &ss->values[cell];
-        uint8_t *key = ss->keys + cell * ss->Kf;
-        uint32_t draw = 1, draws = 0;
-        while (tempVV > 0) { /* :207-233 */
-            if (*val == 0 || memcmp(key, flow, ss->Kf) == 0) {
-                /* every remaining iteration takes the +1 branch (:211-220) */
-                if (*val == 0) memcpy(key, flow, ss->Kf);
-                *val = (uint32_t)((uint64_t)*val + (uint64_t)tempVV);
-                tempVV = 0;
-                break;
-            }
-            tempVV--;
-            if (draws++ >= OR_SS_DRAW_CAP) { tempVV = 0; break; }
-            double ppp = or_go_pow(ss->b, -(double)*val); /* :222 */
-            if (or_ss_uniform(ss->rng_seed, pkt, i, draw++) < ppp) *val = *val - 1; /* :223-227 */
-        }
+        ss_mv(&ss->values[cell], ss->keys + cell * ss->Kf, flow, ss->Kf, tempVV, ss->b, ss->rng_seed, pkt, i);
     }
 }
 

@@ -112,6 +112,8 @@ uint64_t or_mix64(uint64_t x);
 double or_ss_uniform(uint64_t rng_seed, uint64_t pkt, uint32_t row, uint32_t draw);
 void or_ss_hll_seeds(uint64_t hll_master, uint64_t cell, uint32_t *s0, uint32_t *s1);
 double or_go_pow(double x, double y);
+double or_det_log(double x);    /* deterministic log, x in (0, 1] */
+double or_det_log1m(double p);  /* log(1 - p), 0 < p < 1 */
 double or_go_ldexp(double frac, int e);
 
 /* splitmix64 stream (BASELINE/SURVEY §8d seeds) */

@@ -78,6 +78,10 @@ def lib():
     L.or_ss_packets.argtypes = [ct.c_void_p]
     L.or_mix64.restype = ct.c_uint64
     L.or_mix64.argtypes = [ct.c_uint64]
+    L.or_det_log.restype = ct.c_double
+    L.or_det_log.argtypes = [ct.c_double]
+    L.or_det_log1m.restype = ct.c_double
+    L.or_det_log1m.argtypes = [ct.c_double]
     L.or_ss_uniform.restype = ct.c_double
     L.or_ss_uniform.argtypes = [ct.c_uint64, ct.c_uint64, ct.c_uint32, ct.c_uint32]
     L.or_go_pow.restype = ct.c_double

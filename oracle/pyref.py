@@ -192,10 +192,39 @@ def go_pow_int(x: float, y: float) -> float:
         return math.inf
 
 
+def det_log(x: float) -> float:
+    """Deterministic log on (0, 1] (fdlibm reduction + polynomial, as Go's math.Log)."""
+    Ln2Hi, Ln2Lo = 6.93147180369123816490e-01, 1.90821492927058770002e-10
+    L1, L2, L3 = 6.666666666666735130e-01, 3.999999999940941908e-01, 2.857142874366239149e-01
+    L4, L5, L6 = 2.222219843214978396e-01, 1.818357216161805012e-01, 1.531383769920937332e-01
+    L7 = 1.479819860511658591e-01
+    f1, ki = math.frexp(x)
+    if f1 < 0.70710678118654752440:
+        f1 *= 2
+        ki -= 1
+    f = f1 - 1
+    k = float(ki)
+    s = f / (2 + f)
+    s2 = s * s
+    s4 = s2 * s2
+    t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)))
+    t2 = s4 * (L2 + s4 * (L4 + s4 * L6))
+    R = t1 + t2
+    hfsq = 0.5 * f * f
+    return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f)
+
+
+def det_log1m(p: float) -> float:
+    if p < 1e-4:
+        t = p * p
+        r = p + t * 0.5
+        r = r + t * p * (1.0 / 3.0)
+        return -r
+    return det_log(1.0 - p)
+
+
 class SuperSpreadSeq:
     """super_spread.go with injected HLL seeds and the declared generator."""
-
-    DRAW_CAP = 1 << 24
 
     def __init__(self, width, depth, threshold, m, size, base, b, kf, ke, seeds, hll_master, rng_seed):
         self.w = width or (1 << 20)
@@ -247,22 +276,32 @@ class SuperSpreadSeq:
             if ss_uniform(self.rs, pkt, i, 0) >= pcu:
                 continue
             vv = int(cv) if cv < 2.0 ** 63 else -(1 << 63)
-            draw, draws = 1, 0
-            while vv > 0:
-                if self.values[cell] == 0 or self.keys[cell] == flow:
-                    if self.values[cell] == 0:
-                        self.keys[cell] = flow
-                    self.values[cell] = (self.values[cell] + vv) & M32
-                    break
-                vv -= 1
-                if draws >= self.DRAW_CAP:
-                    break
-                draws += 1
-                ppp = go_pow_int(self.b, -float(self.values[cell]))
-                u = ss_uniform(self.rs, pkt, i, draw)
-                draw += 1
-                if u < ppp:
-                    self.values[cell] -= 1
+            self._mv(cell, flow, vv, pkt, i)
+
+    def _mv(self, cell, flow, vv, pkt, row):
+        """super_spread.go:207-233; foreign decrements as geometric waiting times."""
+        draw = 1
+        while vv > 0:
+            if self.values[cell] == 0 or self.keys[cell] == flow:
+                if self.values[cell] == 0:
+                    self.keys[cell] = flow
+                self.values[cell] = (self.values[cell] + vv) & M32
+                return
+            ppp = go_pow_int(self.b, -float(self.values[cell]))
+            if not ppp > 0:
+                return
+            if ppp >= 1:
+                k = min(self.values[cell], vv)
+                self.values[cell] -= k
+                vv -= k
+                continue
+            u = ss_uniform(self.rs, pkt, row, draw)
+            draw += 1
+            q = det_log(1.0 - u) / det_log1m(ppp)
+            if not q < float(vv):
+                return
+            vv -= int(math.floor(q)) + 1
+            self.values[cell] -= 1
 
     def estimate(self, flow: bytes) -> int:
         est = 0

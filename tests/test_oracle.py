@@ -132,3 +132,21 @@ def test_golden_streams_reproduced(oracle):
     values, keys, regs, pbits = ss.export()
     assert np.array_equal(values, s["values"]) and np.array_equal(regs, s["regs"])
     assert np.array_equal(pbits, s["pbits"]) and np.array_equal(keys, s["keys"])
+
+
+def test_det_log_c_python_and_accuracy(oracle):
+    """The deterministic log behind the declared geometric waiting times:
+    C and Python round identically, and both stay within 2 ulp of libm."""
+    from oracle import pyref
+    import math
+    rng = np.random.default_rng(17)
+    xs = np.concatenate([rng.random(3000), 1.0 - rng.random(500) * 1e-9, [1.0, 0.5, 2.0 ** -53, 0.70710678118654752]])
+    xs = xs[xs > 0]
+    for x in xs:
+        c = oracle.lib().or_det_log(float(x))
+        assert c == pyref.det_log(float(x))
+        assert abs(c - math.log(x)) <= 2 * math.ulp(math.log(x)) + 1e-300
+    for p in np.concatenate([rng.random(1000) * 1e-3, rng.random(1000), [1e-300, 1e-17, 1e-4, 0.999999]]):
+        c = oracle.lib().or_det_log1m(float(p))
+        assert c == pyref.det_log1m(float(p))
+        assert abs(c - math.log1p(-p)) <= 1e-12 * abs(math.log1p(-p))

@@ -159,17 +159,57 @@ def test_golden_stream_fixture(gpu):
 
 
 def test_synthetic_device_resident(gpu, oracle):
-    """C3 shape on device-resident synthetic headers: flow SrcIP, element DstIP."""
+    """C3 on device-resident synthetic headers: default task geometry
+    (configs/config.yaml:112-122: flow SrcIP, element DstIP, d=2, w=32768),
+    per-source fan-out stream, two consecutive windows."""
     import torch
     from go2netspectra_amd import SuperSpread, SyntheticTraffic
-    syn = SyntheticTraffic()
-    hdr, wl = syn.generate(1_000_000)
-    seeds = np.array([0xA1, 0xB2, 0xC3], np.uint32)
+    syn = SyntheticTraffic(fanout=1 << 20)
+    seeds = np.array([0xA1, 0xB2], np.uint32)
     kw = dict(flow_fields=["SrcIP"], elem_fields=["DstIP"], seeds=seeds, hll_master=HLL_MASTER, rng_seed=RNG_SEED)
-    ss = SuperSpread(1 << 16, 3, 4096, 128, 5, 0.5, 1.08, **kw)
-    ss.insert_headers(hdr, wl)
+    ss = SuperSpread(32768, 2, 4096, 128, 5, 0.5, 1.08, **kw)
+    orc = oracle.SuperSpread(32768, 2, 4096, 128, 5, 0.5, 1.08, 16, 16, seeds, HLL_MASTER, RNG_SEED)
+    for k in range(2):
+        hdr, wl = syn.generate(1_000_000, first=k * 1_000_000)
+        ss.insert_headers(hdr, wl)
+        ss.flush()
+        torch.cuda.synchronize()
+        got = orc.insert_hdr64(hdr.cpu().numpy(), wl.cpu().numpy().view(np.uint32), ["SrcIP"], ["DstIP"])
+        assert got == 1_000_000
+        assert_same_ss(ss, orc)
+    assert [(h.Flow, h.Count) for h in ss.heavy_hitters().Count] == orc.heavy()
+
+
+def test_superspreader_accuracy(gpu, oracle):
+    """Statistical check in the shape of ss_test.go:18-136 (per-flow spread error,
+    superspreader precision/recall vs exact distinct sets; threshold 750,
+    w=2^13, d=2, m=128).  The GPU result is also bit-exact against the oracle,
+    so the accuracy reported is the reference algorithm's own."""
+    rng = np.random.default_rng(21)
+    n, nsrc, ndst = 1_500_000, 20_000, 400_000
+    src = rng.integers(0, 256, (nsrc, 16), dtype=np.uint8)
+    src[:, 4:] = 0
+    dst = rng.integers(0, 256, (ndst, 16), dtype=np.uint8)
+    dst[:, 4:] = 0
+    si = zipf_index(rng, n, nsrc, 1.1)
+    di = rng.integers(0, ndst, n)
+    fl, el = np.ascontiguousarray(src[si]), np.ascontiguousarray(dst[di])
+    ss, orc = make_pair(oracle, 1 << 13, 2, 128, 5, 16, 16, thr=750)
+    ss.insert_keys(fl, el)
     ss.flush()
-    torch.cuda.synchronize()
-    orc = oracle.SuperSpread(1 << 16, 3, 4096, 128, 5, 0.5, 1.08, 16, 16, seeds, HLL_MASTER, RNG_SEED)
-    assert orc.insert_hdr64(hdr.cpu().numpy(), wl.cpu().numpy().view(np.uint32), ["SrcIP"], ["DstIP"]) == 1_000_000
+    orc.insert(fl, el)
     assert_same_ss(ss, orc)
+    pairs = np.unique(si.astype(np.int64) * ndst + di)
+    truth = np.bincount(pairs // ndst, minlength=nsrc)
+    est = ss.query_many(src).astype(np.int64)
+    seen = truth > 0
+    are = float(np.mean(np.abs(est[seen] - truth[seen]) / truth[seen]))
+    true_ss = {bytes(src[i]) for i in np.nonzero(truth >= 750)[0]}
+    det = {h.Flow for h in ss.heavy_hitters().Count}
+    tp = len(true_ss & det)
+    prec = tp / max(1, len(det))
+    rec = tp / max(1, len(true_ss))
+    print(f"superspreaders: true={len(true_ss)} detected={len(det)} precision={prec:.3f} recall={rec:.3f} "
+          f"ARE={are:.3f}")
+    assert len(true_ss) > 10
+    assert rec >= 0.8 and prec >= 0.8
