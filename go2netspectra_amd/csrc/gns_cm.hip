@@ -27,12 +27,29 @@
 
 namespace gns {
 
-constexpr uint32_t kTileBitsMax = 12;
+#ifndef GNS_TILE_BITS
+#define GNS_TILE_BITS 12
+#endif
+#ifndef GNS_AP_THREADS
+#define GNS_AP_THREADS 1024
+#endif
+#ifndef GNS_AP_ITEMS
+#define GNS_AP_ITEMS 8
+#endif
+constexpr uint32_t kTileBitsMax = GNS_TILE_BITS;
 constexpr uint32_t kTileMax = 1u << kTileBitsMax;   // buckets per LDS tile
 constexpr uint32_t kMaxTilesPerRow = 1024;
-constexpr uint32_t kSizeEsc = 0xFFFFFu;             // 20-bit size field escape
+// Update entry: lo = flow id (or kOvfFlag | overflow slot), hi = size << 16 | low,
+// low = bucket within the (row, bin) range or the hot slot.  Sizes >= kSizeEsc
+// take the overflow side table (and an exact replay); below it the per-chunk
+// sums of K4 (kApChunk = 2^13 updates) stay under 2^32, so the packed
+// own/foreign 32-bit halves of accS never carry.
+constexpr uint32_t kEntShift = 16;
+constexpr uint32_t kLowMask = (1u << kEntShift) - 1u;
+constexpr uint32_t kSizeEsc = 0xFFFFu;
 constexpr uint32_t kOvfFlag = 0x80000000u;
-constexpr uint32_t kOvfCap = 1u << 20;
+constexpr uint32_t kOvfCap = 1u << 22;
+constexpr uint32_t kMaxBinsAll = 4096;               // d * bins per row (k_order, K3 LDS)
 constexpr int kExThreads = 256;
 constexpr uint32_t kChunk = 16384;                  // packets per K1/K3 block
 #ifndef GNS_SC_THREADS
@@ -42,9 +59,11 @@ constexpr int kScThreads = GNS_SC_THREADS;          // K3 block
 constexpr int kScWaves = kScThreads / 64;
 constexpr int kScItems = 16;
 constexpr uint32_t kScRound = kScThreads * kScItems; // 8192 updates staged in LDS per round
-constexpr int kApThreads = 1024;
-constexpr int kApItems = 8;
-constexpr uint32_t kApChunk = kApThreads * kApItems; // 4096 updates per K4 step
+constexpr int kApThreads = GNS_AP_THREADS;
+constexpr int kApWaves = kApThreads / 64;
+constexpr int kApItems = GNS_AP_ITEMS;
+constexpr uint32_t kApChunk = kApThreads * kApItems; // 8192 updates per K4 step
+static_assert((uint64_t)kApChunk * (kSizeEsc - 1) < (1ull << 32), "K4 per-chunk size sums must fit 32 bits");
 constexpr uint32_t kScanSeg = 4096;
 constexpr uint32_t kHot = 64;                       // designated hot buckets per row
 constexpr uint32_t kHotTab = 512;                   // LDS hash slots per row (load <= 1/8)
@@ -52,7 +71,8 @@ constexpr uint32_t kHotMinBits = 11;                // designate only buckets wi
 
 struct CmGeom {
     uint32_t w, d, wmask, pow2;
-    uint32_t tile_bits, ntiles, nbins, nbits;  // nbits = ceil_log2(ntiles + kHot)
+    uint32_t tile_bits, ntiles, nbins, nbits;  // nbits = ceil_log2(ntiles + kHot); ntiles = bins per row
+    uint32_t bin_bits, sub_bits;               // bin = 2^sub_bits LDS tiles of 2^tile_bits buckets
     uint32_t nbins_all;                        // nbins + d*kHot (hot bins follow the tile bins)
     uint32_t seeds[8];
 };
@@ -189,7 +209,7 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
                 const int h = hot_lookup(s_tab + rr * kHotTab, b);
                 // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
                 a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
-                binid = h >= 0 ? a.g.nbins + rr * kHot + (uint32_t)h : rr * a.g.ntiles + (b >> a.g.tile_bits);
+                binid = h >= 0 ? a.g.nbins + rr * kHot + (uint32_t)h : rr * a.g.ntiles + (b >> a.g.bin_bits);
             }
             // heavy bins: one LDS add for the wave's majority bin
             const uint32_t b0 = __builtin_amdgcn_readfirstlane(binid);
@@ -399,7 +419,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
     uint16_t *s_bin = reinterpret_cast<uint16_t *>(s_ent + kScRound);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t blk = blockIdx.x;
-    const uint32_t tmask = (1u << a.g.tile_bits) - 1u;
+    const uint32_t tmask = (1u << a.g.bin_bits) - 1u;
     const uint64_t beg = (uint64_t)blk * kChunk;
     const uint64_t end = min(a.n, beg + kChunk);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -441,7 +461,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                     const uint32_t b = bs[i];
                     const bool hot = (b >> 31) != 0;
                     const uint32_t h = b & 0x7FFFFFFFu;
-                    t = hot ? a.g.ntiles + h : (b >> a.g.tile_bits);
+                    t = hot ? a.g.ntiles + h : (b >> a.g.bin_bits);
                     const uint32_t low = hot ? r * kHot + h : (b & tmask);
                     const uint32_t sz = szs[i];
                     uint32_t lo = ids[i], sf = sz;
@@ -456,7 +476,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                         }
                         sf = kSizeEsc;
                     }
-                    e = (uint64_t)((sf << 12) | low) << 32 | lo;
+                    e = (uint64_t)((sf << kEntShift) | low) << 32 | lo;
                 }
                 uint64_t peers = __ballot(valid);
                 for (uint32_t bit = 0; bit < a.g.nbits; bit++) {
@@ -557,6 +577,7 @@ __global__ __launch_bounds__(1024) void k_order(const uint32_t *offsets, uint32_
 struct ApplyArgs {
     unsigned long long *stats;  // [5] replayed updates, [6] chunks, [7] chunks with a replay
     const uint64_t *entries;
+    uint64_t *entries2;         // super-bin sub-partition scratch (sub_bits > 0)
     const uint32_t *offsets;
     uint32_t nblk, nbins;
     const uint32_t *total;
@@ -574,23 +595,24 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
-__global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
-    __shared__ uint32_t sC[kTileMax], sFc[kTileMax], sS[kTileMax], sFs[kTileMax];
-    __shared__ unsigned long long accN[kTileMax];  // n | n_oth_c<<21 | n_oth_s<<42 | force<<63
-    __shared__ unsigned long long accS[kTileMax];  // sum_own | sum_oth<<32 ; replay owner words
-    __shared__ uint16_t s_list[kApChunk];
-    __shared__ uint32_t s_wc[kApItems * 16];
-    __shared__ uint32_t s_any, s_nlist;
+struct ApplyLds {
+    uint32_t sC[kTileMax], sFc[kTileMax], sS[kTileMax], sFs[kTileMax];
+    unsigned long long accN[kTileMax];  // n | n_oth_c<<21 | n_oth_s<<42 | force<<63
+    unsigned long long accS[kTileMax];  // sum_own | sum_oth<<32 ; replay owner words
+    uint16_t s_list[kApChunk];
+    uint32_t s_wc[kApItems * kApWaves];
+    uint32_t s_any, s_nlist;
+};
+
+// Updates ent[beg, end) (stream order) of one LDS tile: buckets cbase .. cbase+tn-1.
+__device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, const uint64_t *ent, uint32_t beg,
+                                           uint32_t end, uint64_t cbase, uint32_t tn) {
+    uint32_t *sC = L.sC, *sFc = L.sFc, *sS = L.sS, *sFs = L.sFs;
+    unsigned long long *accN = L.accN, *accS = L.accS;
+    uint16_t *s_list = L.s_list;
+    uint32_t *s_wc = L.s_wc;
+    uint32_t &s_any = L.s_any, &s_nlist = L.s_nlist;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const CmGeom &g = a.g;
-    const uint32_t bin = a.order ? a.order[blockIdx.x] : blockIdx.x;
-    const uint32_t beg = a.offsets[(uint64_t)bin * a.nblk];
-    const uint32_t end = (bin + 1 < g.nbins_all) ? a.offsets[(uint64_t)(bin + 1) * a.nblk] : *a.total;
-    if (beg >= end) return;
-    const uint32_t r = bin / g.ntiles, t = bin % g.ntiles;
-    const uint32_t tbase = t << g.tile_bits;
-    const uint32_t tn = min(1u << g.tile_bits, g.w - tbase);
-    const uint64_t cbase = (uint64_t)r * g.w + tbase;
     for (uint32_t i = tid; i < tn; i += kApThreads) {
         sC[i] = a.C[cbase + i]; sFc[i] = a.Fc[cbase + i];
         sS[i] = a.S[cbase + i]; sFs[i] = a.Fs[cbase + i];
@@ -602,11 +624,18 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
 #pragma unroll
     for (int j = 0; j < kApItems; j++) {  // first chunk
         const uint32_t q = beg + j * kApThreads + tid;
-        e[j] = q < end ? a.entries[q] : 0ull;
+        e[j] = q < end ? ent[q] : 0ull;
     }
+#ifdef GNS_K4_PROF
+    uint64_t pt[4] = {0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
+#define K4_MARK(i) do { if (tid == 0) { const uint64_t tn_ = __builtin_amdgcn_s_memtime(); pt[i] += tn_ - tprev; tprev = tn_; } } while (0)
+#else
+#define K4_MARK(i) do { } while (0)
+#endif
     for (uint32_t cb = beg; cb < end; cb += kApChunk) {
         if (tid == 0) { s_any = 0; atomicAdd(&a.stats[6], 1ull); }
         __syncthreads();
+        K4_MARK(3);
         bool v[kApItems];
         // --- classify against the chunk-entry state, aggregate per bucket ---
 #pragma unroll
@@ -619,7 +648,7 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
             const bool ovf = (lo & kOvfFlag) != 0;
             uint64_t incN = 0, incS = 0;
             if (v[j] && !ovf) {
-                const uint32_t s = hi >> 12;
+                const uint32_t s = hi >> kEntShift;
                 const bool oc = lo != sFc[b], os = lo != sFs[b];
                 incN = 1ull | (uint64_t)oc << 21 | (uint64_t)os << 42;
                 incS = os ? (uint64_t)s << 32 : (uint64_t)s;
@@ -652,9 +681,10 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
 #pragma unroll
         for (int j = 0; j < kApItems; j++) {
             const uint32_t q = cb + kApChunk + j * kApThreads + tid;
-            en[j] = q < end ? a.entries[q] : 0ull;
+            en[j] = q < end ? ent[q] : 0ull;
         }
         __syncthreads();
+        K4_MARK(0);
         // --- per bucket: exact aggregate update or mark for replay ---
         for (uint32_t i = tid; i < tn; i += kApThreads) {
             const uint64_t an = accN[i];
@@ -688,6 +718,7 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
             if (rep) s_any = 1;
         }
         __syncthreads();
+        K4_MARK(1);
         if (s_any) {
             // --- stable compaction of the updates that need replay ---
             bool need[kApItems];
@@ -697,26 +728,34 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
                 const uint32_t b = (uint32_t)(e[j] >> 32) & (kTileMax - 1u);
                 need[j] = v[j] && accN[b] != 0;
                 bal[j] = __ballot(need[j]);
-                if (lane == 0) s_wc[j * 16 + wave] = __popcll(bal[j]);
+                if (lane == 0) s_wc[j * kApWaves + wave] = __popcll(bal[j]);
             }
             __syncthreads();
-            if (wave == 0) {  // exclusive scan of the kApItems*16 wave counts, (item, wave) order
-                constexpr uint32_t PER = kApItems * 16 / 64;
+            if (wave == 0) {  // exclusive scan of the kApItems*kApWaves wave counts, (item, wave) order
+                constexpr uint32_t NC = kApItems * kApWaves;
+                constexpr uint32_t PER = (NC + 63) / 64;
                 uint32_t x[PER], sum = 0;
 #pragma unroll
-                for (uint32_t q = 0; q < PER; q++) { x[q] = s_wc[lane * PER + q]; sum += x[q]; }
+                for (uint32_t q = 0; q < PER; q++) {
+                    x[q] = lane * PER + q < NC ? s_wc[lane * PER + q] : 0u;
+                    sum += x[q];
+                }
                 const uint32_t inc = wave_incl_scan(sum);
                 uint32_t run = inc - sum;
 #pragma unroll
-                for (uint32_t q = 0; q < PER; q++) { s_wc[lane * PER + q] = run; run += x[q]; }
+                for (uint32_t q = 0; q < PER; q++) {
+                    if (lane * PER + q < NC) s_wc[lane * PER + q] = run;
+                    run += x[q];
+                }
                 if (lane == 63) s_nlist = inc;
             }
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < kApItems; j++)
-                if (need[j]) s_list[s_wc[j * 16 + wave] + __popcll(bal[j] & lt_mask)] = (uint16_t)(j * kApThreads + tid);
+                if (need[j]) s_list[s_wc[j * kApWaves + wave] + __popcll(bal[j] & lt_mask)] = (uint16_t)(j * kApThreads + tid);
             __syncthreads();
             const uint32_t nlist = s_nlist;
+            K4_MARK(2);
             if (tid == 0) { atomicAdd(&a.stats[5], (unsigned long long)nlist); atomicAdd(&a.stats[7], 1ull); }
             // --- sequential replay (count_min.go:180-235), in order.  Buckets are
             //     partitioned over the 16 waves (b % 16); each wave walks the
@@ -728,16 +767,16 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
                 bool pending = false;
                 uint32_t b = 0, k = 0, s = 0, rf = 0;
                 if (i < nlist) {
-                    const uint64_t ee = a.entries[cb + s_list[i]];
+                    const uint64_t ee = ent[cb + s_list[i]];
                     b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
-                    pending = (b & 15u) == wave;
+                    pending = b % kApWaves == wave;
                     if (pending) {
                         const uint32_t lo = (uint32_t)ee, hi = (uint32_t)(ee >> 32);
                         if (lo & kOvfFlag) {
                             const uint64_t ov = a.ovf[lo & ~kOvfFlag];
                             k = (uint32_t)ov; s = (uint32_t)(ov >> 32);
                         } else {
-                            k = lo; s = hi >> 12;
+                            k = lo; s = hi >> kEntShift;
                         }
                         rf = (uint32_t)accN[b];
                     }
@@ -770,8 +809,8 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
             for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
                 const uint32_t i = g0 + lane;
                 if (i < nlist) {
-                    const uint32_t b = (uint32_t)(a.entries[cb + s_list[i]] >> 32) & (kTileMax - 1u);
-                    if ((b & 15u) == wave) accN[b] = 0;
+                    const uint32_t b = (uint32_t)(ent[cb + s_list[i]] >> 32) & (kTileMax - 1u);
+                    if (b % kApWaves == wave) accN[b] = 0;
                 }
             }
         }
@@ -779,9 +818,91 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
 #pragma unroll
         for (int j = 0; j < kApItems; j++) e[j] = en[j];
     }
+#ifdef GNS_K4_PROF
+    if (tid == 0) for (int i = 0; i < 4; i++) atomicAdd(&a.stats[8 + i], (unsigned long long)pt[i]);
+#endif
     for (uint32_t i = tid; i < tn; i += kApThreads) {
         a.C[cbase + i] = sC[i]; a.Fc[cbase + i] = sFc[i];
         a.S[cbase + i] = sS[i]; a.Fs[cbase + i] = sFs[i];
+    }
+}
+
+// Super-bin (2^sub_bits tiles, C5-size widths): stable partition of the bin's
+// updates by tile into ent2[beg, end); L.s_soff[t] = start of tile t (relative).
+struct SubLds {
+    uint32_t cnt[kApWaves][16];
+    uint32_t base[16];
+    uint32_t soff[17];
+};
+
+__device__ __forceinline__ void sub_partition(const uint64_t *ent, uint64_t *ent2, uint32_t beg, uint32_t end,
+                                              uint32_t tile_bits, uint32_t sub_bits, SubLds &P) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t nsub = 1u << sub_bits;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    if (tid < 16) P.base[tid] = 0;
+    for (uint32_t i = tid; i < kApWaves * 16; i += kApThreads) (&P.cnt[0][0])[i] = 0;
+    __syncthreads();
+    for (uint32_t q = beg + tid; q < end; q += kApThreads)
+        atomicAdd(&P.base[((uint32_t)(ent[q] >> 32) & kLowMask) >> tile_bits], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (uint32_t t = 0; t < nsub; t++) { P.soff[t] = run; const uint32_t c = P.base[t]; P.base[t] = run; run += c; }
+        P.soff[nsub] = run;
+    }
+    __syncthreads();
+    for (uint32_t q0 = beg; q0 < end; q0 += kApThreads) {
+        const uint32_t q = q0 + tid;
+        const bool valid = q < end;
+        const uint64_t e = valid ? ent[q] : 0ull;
+        const uint32_t sub = valid ? (((uint32_t)(e >> 32) & kLowMask) >> tile_bits) : 0u;
+        uint64_t peers = __ballot(valid);
+        for (uint32_t bit = 0; bit < sub_bits; bit++) {
+            const uint64_t m = __ballot(valid && ((sub >> bit) & 1u));
+            peers &= ((sub >> bit) & 1u) ? m : ~m;
+        }
+        const uint32_t before = __popcll(peers & lt_mask);
+        if (valid && before == 0) P.cnt[wave][sub] = __popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pre = 0;
+            for (uint32_t w2 = 0; w2 < wave; w2++) pre += P.cnt[w2][sub];
+            ent2[beg + P.base[sub] + pre + before] = e;
+        }
+        __syncthreads();
+        if (tid < nsub) {
+            uint32_t tot = 0;
+            for (uint32_t w2 = 0; w2 < (uint32_t)kApWaves; w2++) tot += P.cnt[w2][tid];
+            P.base[tid] += tot;
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < kApWaves * 16; i += kApThreads) (&P.cnt[0][0])[i] = 0;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
+    __shared__ ApplyLds L;
+    __shared__ SubLds P;
+    const CmGeom &g = a.g;
+    const uint32_t bin = a.order ? a.order[blockIdx.x] : blockIdx.x;
+    const uint32_t beg = a.offsets[(uint64_t)bin * a.nblk];
+    const uint32_t end = (bin + 1 < g.nbins_all) ? a.offsets[(uint64_t)(bin + 1) * a.nblk] : *a.total;
+    if (beg >= end) return;
+    const uint32_t r = bin / g.ntiles, t = bin % g.ntiles;
+    const uint32_t bbase = t << g.bin_bits;
+    if (g.sub_bits == 0) {
+        apply_tile(a, L, a.entries, beg, end, (uint64_t)r * g.w + bbase, min(1u << g.tile_bits, g.w - bbase));
+        return;
+    }
+    sub_partition(a.entries, a.entries2, beg, end, g.tile_bits, g.sub_bits, P);
+    for (uint32_t st = 0; st < (1u << g.sub_bits); st++) {
+        const uint32_t tbase = bbase + (st << g.tile_bits);
+        const uint32_t sb = beg + P.soff[st], se = beg + P.soff[st + 1];
+        if (tbase >= g.w || sb >= se) continue;
+        apply_tile(a, L, a.entries2, sb, se, (uint64_t)r * g.w + tbase, min(1u << g.tile_bits, g.w - tbase));
+        __syncthreads();
     }
 }
 
@@ -891,7 +1012,7 @@ __device__ __forceinline__ void decode_entry(const uint64_t *ovf, uint64_t e, ui
         const uint64_t ov = ovf[lo & ~kOvfFlag];
         k = (uint32_t)ov; s = (uint32_t)(ov >> 32);
     } else {
-        k = lo; s = hi >> 12;
+        k = lo; s = hi >> kEntShift;
     }
 }
 
@@ -1172,7 +1293,7 @@ struct gns_cm {
     uint32_t *pcnt[2] = {nullptr, nullptr};
     uint32_t *ptotal = nullptr;        // [2]
     uint32_t *hist = nullptr, *part = nullptr, *total = nullptr, *order = nullptr;
-    uint64_t *entries = nullptr;
+    uint64_t *entries = nullptr, *entries2 = nullptr;
     uint64_t *ovf = nullptr;
     uint32_t *ovf_cnt = nullptr;
     unsigned long long *stats = nullptr;  // [8]
@@ -1210,7 +1331,7 @@ int cm_free_all(gns_cm *cm) {
     dfree(cm->keyid); dfree(cm->idx);
     dfree(cm->pend[0]); dfree(cm->pend[1]); dfree(cm->pcnt[0]); dfree(cm->pcnt[1]);
     dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
-    dfree(cm->entries); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats); dfree(cm->stage);
+    dfree(cm->entries); dfree(cm->entries2); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats); dfree(cm->stage);
     dfree(cm->hot_ids); dfree(cm->segtot); dfree(cm->hflag); dfree(cm->hhist); dfree(cm->hthr); dfree(cm->hcnt);
     if (cm->h_pin) (void)hipHostFree(cm->h_pin);
     cm->timer.destroy();
@@ -1307,7 +1428,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
                                cm->total, cm->order);
         ApplyArgs a{};
         a.stats = cm->stats;
-        a.entries = cm->entries; a.offsets = cm->hist; a.nblk = nblk; a.nbins = g.nbins;
+        a.entries = cm->entries; a.entries2 = cm->entries2; a.offsets = cm->hist; a.nblk = nblk; a.nbins = g.nbins;
         a.total = cm->total; a.order = ordered ? cm->order : nullptr; a.ovf = cm->ovf; a.g = g;
         a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs;
         ScopedStage st(cm->timer, 4);
@@ -1435,13 +1556,20 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         uint32_t tb = kTileBitsMax;
         while (tb > 8 && (uint64_t)g.d * ((g.w + (1u << tb) - 1) >> tb) < 1024) tb--;
         g.tile_bits = tb;
-        g.ntiles = (g.w + (1u << tb) - 1) >> tb;
-        if (g.ntiles > kMaxTilesPerRow) {
-            set_error("width %u needs %u tiles per row (max %u): widths above 2^22 not yet supported",
-                      g.w, g.ntiles, kMaxTilesPerRow);
+        // bins of 2^sub_bits tiles keep the per-row bin count (K1/K3 LDS, the
+        // block histograms) and d * bins bounded for wide rows (C5: w = 2^24)
+        uint32_t sb = 0;
+        auto bins_at = [&](uint32_t bits) { return (uint32_t)(((uint64_t)g.w + (1ull << bits) - 1) >> bits); };
+        while (bins_at(tb + sb) > kMaxTilesPerRow || (uint64_t)g.d * bins_at(tb + sb) > kMaxBinsAll) sb++;
+        if (tb + sb > kEntShift || sb > 4) {
+            set_error("width %u with depth %u is too wide (max %u buckets per row at this depth)", g.w, g.d,
+                      (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, (uint64_t)std::min(kMaxTilesPerRow, kMaxBinsAll / g.d) << kEntShift));
             rc = GNS_E_RANGE;
             break;
         }
+        g.sub_bits = sb;
+        g.bin_bits = tb + sb;
+        g.ntiles = bins_at(g.bin_bits);
         g.nbins = g.d * g.ntiles;
         g.nbins_all = g.nbins + g.d * kHot;
         g.nbits = ceil_log2(g.ntiles + kHot);
@@ -1470,6 +1598,9 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         cm->bmax = p->batch_packets ? p->batch_packets : (16ull << 20);
         cm->bmax = ((cm->bmax + kChunk - 1) / kChunk) * kChunk;
         if (cm->bmax > (1ull << 31)) { set_error("batch_packets too large"); rc = GNS_E_ARG; break; }
+        // update positions are u32: d * batch < 2^32
+        const uint64_t bcap = ((0xFFFFFFFFull / g.d) / kChunk) * kChunk;
+        if (cm->bmax > bcap) cm->bmax = bcap;
         cm->nblk_max = (uint32_t)(cm->bmax / kChunk);
         const uint64_t nseg = ((uint64_t)g.nbins_all * cm->nblk_max + kScanSeg - 1) / kScanSeg;
         if ((rc = dalloc_t(&cm->keyid, cm->bmax)) || (rc = dalloc_t(&cm->idx, cm->bmax * g.d)) ||
@@ -1478,15 +1609,16 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (rc = dalloc_t(&cm->ptotal, 2)) || (rc = dalloc_t(&cm->hist, (uint64_t)g.nbins_all * cm->nblk_max)) ||
             (rc = dalloc_t(&cm->part, nseg + 1)) || (rc = dalloc_t(&cm->total, 1)) ||
             (rc = dalloc_t(&cm->order, g.nbins)) || (rc = dalloc_t(&cm->entries, cm->bmax * g.d)) ||
+            (g.sub_bits && (rc = dalloc_t(&cm->entries2, cm->bmax * g.d))) ||
             (rc = dalloc_t(&cm->ovf, kOvfCap)) || (rc = dalloc_t(&cm->ovf_cnt, 1)) ||
-            (rc = dalloc_t(&cm->stats, 8)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
+            (rc = dalloc_t(&cm->stats, 16)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
             (rc = dalloc_t(&cm->segtot, (size_t)g.d * kHot * kHotSegs * 2)) || (rc = dalloc_t(&cm->hflag, g.d * kHot)) ||
             (rc = dalloc_t(&cm->hhist, g.d * 33)) || (rc = dalloc_t(&cm->hthr, 8)) || (rc = dalloc_t(&cm->hcnt, 8)))
             break;
         if (hipHostMalloc(reinterpret_cast<void **>(&cm->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
         }
-        if (hipMemsetAsync(cm->stats, 0, 64, cm->stream) != hipSuccess) { rc = GNS_E_HIP; break; }
+        if (hipMemsetAsync(cm->stats, 0, 128, cm->stream) != hipSuccess) { rc = GNS_E_HIP; break; }
         if ((rc = cm_reset_state(cm)) != GNS_OK) break;
         if (hipStreamSynchronize(cm->stream) != hipSuccess) { set_error("sync failed"); rc = GNS_E_HIP; break; }
     } while (0);
@@ -1546,7 +1678,7 @@ int gns_cm_flush(gns_cm *cm) {
     cm->timer.collect();
     GNS_HIP(hipMemcpy(cm->h_pin, cm->stats + 4, 8, hipMemcpyDeviceToHost));
     if (cm->h_pin[0] | cm->h_pin[1]) {
-        set_error("more than %u packets of size >= 2^20-1 in one batch", kOvfCap);
+        set_error("more than %u packets of size >= 2^19-1 in one batch", kOvfCap);
         return GNS_E_RANGE;
     }
     return GNS_OK;
@@ -1716,9 +1848,14 @@ int gns_cm_counters(gns_cm *cm, uint64_t out[8]) {
     if (!cm || !out) return GNS_E_ARG;
     GNS_TRY(set_dev(cm));
     GNS_HIP(hipStreamSynchronize(cm->stream));
-    unsigned long long h[8];
+    unsigned long long h[16];
     GNS_HIP(hipMemcpy(h, cm->stats, sizeof(h), hipMemcpyDeviceToHost));
+#ifdef GNS_K4_PROF  // profiling build: K4 phase cycles (classify, decide, compact, replay), chunks, ...
+    for (int i = 0; i < 4; i++) out[i] = h[8 + i];
+    for (int i = 4; i < 8; i++) out[i] = h[i + 1];
+#else
     for (int i = 0; i < 8; i++) out[i] = h[i];
+#endif
     return GNS_OK;
 }
 

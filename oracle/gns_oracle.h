@@ -119,6 +119,23 @@ double or_go_ldexp(double frac, int e);
 /* splitmix64 stream (BASELINE/SURVEY §8d seeds) */
 uint64_t or_splitmix64_next(uint64_t *state);
 
+/* ---- exact aggregator, internal/engine/impl/exact/task.go (gns_oracle_exact.c) ---- */
+typedef struct or_ex or_ex;
+or_ex *or_ex_new(const uint8_t *fields, uint32_t nfields);
+void or_ex_free(or_ex *ex);
+void or_ex_reset(or_ex *ex);
+void or_ex_insert(or_ex *ex, const or_tuple *t, int64_t ts, uint64_t length);
+void or_ex_insert_tuples(or_ex *ex, const uint8_t *src16, const uint8_t *dst16, const uint16_t *sport,
+                         const uint16_t *dport, const uint8_t *proto, const uint8_t *ipver,
+                         const uint32_t *length, const int64_t *ts, uint64_t n);
+uint64_t or_ex_insert_hdr64(or_ex *ex, const uint8_t *hdr, const uint32_t *wirelen, const int64_t *ts,
+                            uint64_t n);
+uint64_t or_ex_query(const or_ex *ex, const uint8_t *flow);
+uint64_t or_ex_count(const or_ex *ex);
+uint64_t or_ex_export(const or_ex *ex, char *keys_out, uint64_t keys_cap, int64_t *start, int64_t *end,
+                      uint64_t *pkts, uint64_t *bytes);
+int or_parse_hdr64_len(const uint8_t *rec, uint32_t wirelen, or_tuple *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -217,3 +217,47 @@ aggregator:
         o.insert_hdr64(hdr, t["length"], fields)
         assert [(h.Flow, h.Count) for h in snaps[task].Count] == o.heavy("count")
         assert [(h.Flow, h.Size) for h in snaps[task].Size] == o.heavy("size")
+
+
+def test_large_sizes_mixed_owner(gpu, oracle):
+    """Sizes just below and above the 2^19-1 escape, one bucket shared by an owner
+    and a foreign flow: the per-chunk size sums must not carry between halves."""
+    rng = np.random.default_rng(77)
+    cm, orc = make_pair(oracle, 1, 1, 8, st=1, ct=1)
+    n = 200_000
+    flows = rng.integers(0, 256, (2, 8), dtype=np.uint8)
+    idx = (rng.random(n) < 0.02).astype(np.int64)
+    keys = np.ascontiguousarray(flows[idx])
+    sizes = np.where(idx == 0, (1 << 19) - 2, rng.integers(0, 1 << 19, n)).astype(np.uint32)
+    sizes[::97] = (1 << 19) - 1
+    sizes[::89] = (1 << 20) - 2
+    for part in np.array_split(np.arange(n), 4):
+        cm.insert_keys(keys[part], sizes[part])
+        orc.insert_keys(keys[part], sizes[part])
+    cm.flush()
+    assert_same_state(cm, orc)
+
+
+@pytest.mark.parametrize("w,d,K,nflows,n", [
+    (1 << 24, 8, 4, 1 << 16, 2_000_000),   # C5 geometry: bins of 16 LDS tiles
+    (1 << 22, 8, 8, 1 << 15, 1_000_000),   # d * tiles > 4096: bins of 2 tiles
+    (5_000_000, 3, 13, 50_000, 1_000_000),  # non power-of-two wide row
+])
+def test_wide_rows_parity(gpu, oracle, w, d, K, nflows, n):
+    """Widths beyond 1024 LDS tiles per row: K3 bins hold 2^sub_bits tiles and K4
+    partitions each bin by tile before the in-order tile pass."""
+    rng = np.random.default_rng(w % 1000 + d)
+    cm, orc = make_pair(oracle, w, d, K, st=1 << 16, ct=100, max_flows=1 << 20)
+    keys, flows, _ = zipf_keys(rng, n, nflows, K)
+    sizes = sizes_u32(rng, n)
+    sizes[::1001] = 70_000  # overflow side table
+    half = n // 2
+    for sl in (slice(0, half), slice(half, n)):
+        cm.insert_keys(keys[sl], sizes[sl])
+        orc.insert_keys(keys[sl], sizes[sl])
+    cm.flush()
+    assert_same_state(cm, orc)
+    q = cm.query_many(flows[:2000])
+    assert np.array_equal(q, np.array([orc.query(bytes(f)) for f in flows[:2000]], np.uint64))
+    hh = cm.heavy_hitters()
+    assert [(h.Flow, h.Count) for h in hh.Count] == orc.heavy("count")
