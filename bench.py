@@ -46,15 +46,15 @@ def row_seeds(d):
     return np.array(out, np.uint32)
 
 
-def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0):
+def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, depth: int = DEPTH):
     """Timed CPU restatements on a bounded prefix of the same stream (rank 0)."""
     from oracle import oracle as orc
     n = min(int(wl_dev.shape[0]), 24_000_000)
     hdr = hdr_dev[:n].cpu().numpy()
     wl = wl_dev[:n].cpu().numpy().view(np.uint32)
-    seeds = row_seeds(DEPTH)
+    seeds = row_seeds(depth)
     # (1) sequential oracle, 1 thread
-    cm = orc.CountMin(WIDTH, DEPTH, 1 << 20, 1000, 37, seeds)
+    cm = orc.CountMin(width, depth, 1 << 20, 1000, 37, seeds)
     chunk, done, t0 = 1_000_000, 0, time.perf_counter()
     while done < n and time.perf_counter() - t0 < seconds:
         m = min(chunk, n - done)
@@ -65,7 +65,7 @@ def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0):
     del cm
     # (2) restatement of the Go worker pool (shared sketch, CAS loops, shared cursor)
     threads = int(os.environ.get("GNS_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    cm = orc.CountMin(WIDTH, DEPTH, 1 << 20, 1000, 37, seeds)
+    cm = orc.CountMin(width, depth, 1 << 20, 1000, 37, seeds)
     done, t0 = 0, time.perf_counter()
     chunk = 4_000_000
     while done < n and time.perf_counter() - t0 < seconds / 2:
@@ -182,6 +182,8 @@ def main():
     ap.add_argument("--packets", type=int, default=PACKETS)
     ap.add_argument("--batch", type=int, default=0, help="device batch (packets); 0 = whole step")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--width", type=int, default=WIDTH, help="Count-Min width (2^24 = configs[4] geometry)")
+    ap.add_argument("--depth", type=int, default=DEPTH, help="Count-Min depth (8 = configs[4] geometry)")
     ap.add_argument("--sketch", choices=["countmin", "superspread"], default="countmin",
                     help="superspread = configs[2] (not the headline metric)")
     ap.add_argument("--host-input", action="store_true",
@@ -208,7 +210,7 @@ def main():
     syn = SyntheticTraffic(shard=rank, nshards=world, device=local)
     hdr, wl = syn.generate(n)
     batch = args.batch or n
-    cm = CountMin(WIDTH, DEPTH, 1 << 20, 1000, flow_fields=FIELDS, seeds=row_seeds(DEPTH),
+    cm = CountMin(args.width, args.depth, 1 << 20, 1000, flow_fields=FIELDS, seeds=row_seeds(args.depth),
                   max_flows=1 << 21, batch_packets=batch, device=local)
     torch.cuda.synchronize()
 
@@ -285,11 +287,17 @@ def main():
         "heavy_hitters": {"count": len(hh.Count), "size": len(hh.Size or [])},
         "engine_counters": counters,
     }
+    if (args.width, args.depth) != (WIDTH, DEPTH):
+        wl2 = f"2^{args.width.bit_length() - 1}" if args.width & (args.width - 1) == 0 else str(args.width)
+        line["metric"] = f"Mpackets/s CMS update (device-resident, d={args.depth} w={wl2})"
+        line["config"]["workload"] = (f"Count-Min d={args.depth} w={wl2} (configs[4] geometry when d=8 w=2^24), "
+                                      f"100M Zipf(1.1) 5-tuple headers in HBM per GPU, bit-exact counters")
+        line["note"] = "not the headline metric (BASELINE.json metric is d=4 w=2^20)"
     if args.host_input:
         line["metric"] = "Mpackets/s CMS update, HOST-resident input (PCIe H2D inclusive), d=4 w=2^20"
         line["note"] = "not the headline metric: inputs start in pinned host memory"
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(hdr, wl)
+        line["cpu_baseline"] = cpu_baseline(hdr, wl, width=args.width, depth=args.depth)
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:

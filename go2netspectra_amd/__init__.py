@@ -2,11 +2,13 @@
 
 Drop-in for the reference's per-packet sketch path (internal/engine/impl/sketch):
 header parse -> flow-key encode -> d seeded MurmurHash3 -> fingerprinted
-Count-Min / SuperSpread bucket updates, executed by hand-written gfx950 HIP
-kernels behind the C ABI in include/gns_sketch.h (libgns_sketch.so).
+Count-Min / SuperSpread bucket updates, plus the exact per-flow aggregator
+(internal/engine/impl/exact), executed by hand-written gfx950 HIP kernels
+behind the C ABI in include/gns_sketch.h (libgns_sketch.so).
 """
 from ._lib import GnsError, build, load
-from .config import Config, SketchTaskDef, load_config, parse_config
+from .config import Config, ExactTaskDef, SketchTaskDef, load_config, parse_config
+from .exact import ExactAggregator, ExactTask, NewExact, SnapshotData
 from .factory import Manager, TaskGroup, create, register_aggregator
 from .packets import HeaderBatch, PacketBatch, SyntheticTraffic, ip_slot, read_pcap, write_pcap
 from .sketch import CountMin, HeavyCount, HeavyRecord, HeavySize, SuperSpread
@@ -16,5 +18,6 @@ __all__ = [
     "GnsError", "build", "load", "Config", "SketchTaskDef", "load_config", "parse_config", "Manager",
     "TaskGroup", "create", "register_aggregator", "HeaderBatch", "PacketBatch", "SyntheticTraffic",
     "ip_slot", "read_pcap", "write_pcap", "CountMin", "HeavyCount", "HeavyRecord", "HeavySize",
-    "SuperSpread", "New", "SketchTask", "decode_flow",
+    "SuperSpread", "New", "SketchTask", "decode_flow", "ExactTaskDef", "ExactAggregator", "ExactTask",
+    "NewExact", "SnapshotData",
 ]

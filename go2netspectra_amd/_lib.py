@@ -29,7 +29,10 @@ EXPORTED = [
     "gns_ss_insert_headers", "gns_ss_flush", "gns_ss_query", "gns_ss_heavy_hitters", "gns_ss_reset",
     "gns_ss_export_state", "gns_ss_stats", "gns_ss_counters", "gns_ss_set_timing", "gns_ss_stage_times",
     "gns_synth_create", "gns_synth_destroy", "gns_synth_fill", "gns_synth_flows",
-    "gns_pack_pcap", "gns_last_error", "gns_version",
+    "gns_ex_create", "gns_ex_destroy", "gns_ex_insert_tuples", "gns_ex_insert_headers", "gns_ex_flush",
+    "gns_ex_query", "gns_ex_snapshot", "gns_ex_reset", "gns_ex_counters", "gns_ex_set_timing",
+    "gns_ex_stage_times",
+    "gns_pack_pcap", "gns_pack_pcap_ts", "gns_last_error", "gns_version",
 ]
 
 
@@ -72,6 +75,10 @@ class SsParams(ct.Structure):
                 ("flow", Layout), ("elem", Layout), ("flow_bytes", ct.c_uint32),
                 ("elem_bytes", ct.c_uint32), ("seeds", ct.c_void_p), ("hll_master", ct.c_uint64),
                 ("rng_seed", ct.c_uint64), ("batch_packets", ct.c_uint64), ("device", ct.c_int)]
+
+
+class ExParams(ct.Structure):
+    _fields_ = [("key", Layout), ("max_flows", ct.c_uint64), ("batch_packets", ct.c_uint64), ("device", ct.c_int)]
 
 
 class SynthParams(ct.Structure):
@@ -123,7 +130,15 @@ def load() -> ct.CDLL:
         "gns_ss_set_timing": ([vp, i32], i32), "gns_ss_stage_times": ([vp, vp, vp, i32], i32),
         "gns_synth_create": ([vp, vp], i32), "gns_synth_destroy": ([vp], i32),
         "gns_synth_fill": ([vp, vp, vp, u64, u64], i32), "gns_synth_flows": ([vp, vp], i32),
+        "gns_ex_create": ([vp, vp], i32), "gns_ex_destroy": ([vp], i32),
+        "gns_ex_insert_tuples": ([vp, vp, vp, vp, u64, i32], i32),
+        "gns_ex_insert_headers": ([vp, vp, vp, vp, u64, i32], i32),
+        "gns_ex_flush": ([vp], i32), "gns_ex_query": ([vp, vp, u32, u64, vp], i32),
+        "gns_ex_snapshot": ([vp, vp, vp, vp, vp, vp, vp], i32), "gns_ex_reset": ([vp], i32),
+        "gns_ex_counters": ([vp, vp], i32), "gns_ex_set_timing": ([vp, i32], i32),
+        "gns_ex_stage_times": ([vp, vp, vp, i32], i32),
         "gns_pack_pcap": ([ct.c_char_p, vp, vp, u64, vp], ct.c_int64),
+        "gns_pack_pcap_ts": ([ct.c_char_p, vp, vp, vp, u64, vp], ct.c_int64),
         "gns_last_error": ([], ct.c_char_p), "gns_version": ([], ct.c_char_p),
     }
     for name, (args, res) in sig.items():

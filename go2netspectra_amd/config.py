@@ -51,6 +51,24 @@ class SketchTaskDef:
 
 
 @dataclass
+class ExactTaskDef:  # config.go:42-47
+    Name: str = ""
+    NumShards: int = 0
+    KeyFields: List[str] = field(default_factory=list)
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "ExactTaskDef":
+        d = d or {}
+        return cls(str(d.get("name", "") or ""), int(d.get("num_shards", 0) or 0), list(d.get("key_fields", []) or []))
+
+
+@dataclass
+class ExactAggregatorConfig:  # config.go:49-53
+    Tasks: List[ExactTaskDef] = field(default_factory=list)
+    Writers: List[dict] = field(default_factory=list)
+
+
+@dataclass
 class SketchAggregatorConfig:
     Tasks: List[SketchTaskDef] = field(default_factory=list)
     Writers: List[dict] = field(default_factory=list)  # writers are out of scope; kept verbatim
@@ -63,6 +81,7 @@ class AggregatorConfig:
     NumWorkers: int = 1
     SizeOfPacketChannel: int = 10000
     Sketch: SketchAggregatorConfig = field(default_factory=SketchAggregatorConfig)
+    Exact: ExactAggregatorConfig = field(default_factory=ExactAggregatorConfig)
 
 
 @dataclass
@@ -76,6 +95,7 @@ def parse_config(text: str) -> Config:
     doc = yaml.safe_load(os.path.expandvars(text)) or {}
     agg = doc.get("aggregator", {}) or {}
     sk = agg.get("sketch", {}) or {}
+    ex = agg.get("exact", {}) or {}
     cfg = Config(raw=doc)
     cfg.Aggregator = AggregatorConfig(
         Types=list(agg.get("types", []) or []),
@@ -84,7 +104,10 @@ def parse_config(text: str) -> Config:
         SizeOfPacketChannel=int(agg.get("size_of_packet_channel", 10000) or 10000),
         Sketch=SketchAggregatorConfig(
             Tasks=[SketchTaskDef.from_dict(t) for t in (sk.get("tasks", []) or [])],
-            Writers=list(sk.get("writers", []) or [])))
+            Writers=list(sk.get("writers", []) or [])),
+        Exact=ExactAggregatorConfig(
+            Tasks=[ExactTaskDef.from_dict(t) for t in (ex.get("tasks", []) or [])],
+            Writers=list(ex.get("writers", []) or [])))
     return cfg
 
 

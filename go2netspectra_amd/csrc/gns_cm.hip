@@ -588,6 +588,10 @@ struct ApplyArgs {
 };
 
 constexpr uint64_t kM21 = (1ull << 21) - 1;
+#ifndef GNS_REP_CAP
+#define GNS_REP_CAP 1536
+#endif
+constexpr uint32_t kRepCap = GNS_REP_CAP;
 
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
@@ -600,6 +604,7 @@ struct ApplyLds {
     unsigned long long accN[kTileMax];  // n | n_oth_c<<21 | n_oth_s<<42 | force<<63
     unsigned long long accS[kTileMax];  // sum_own | sum_oth<<32 ; replay owner words
     uint16_t s_list[kApChunk];
+    uint64_t s_rep[kRepCap];            // the first kRepCap replay entries themselves (no global re-read)
     uint32_t s_wc[kApItems * kApWaves];
     uint32_t s_any, s_nlist;
 };
@@ -752,7 +757,11 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < kApItems; j++)
-                if (need[j]) s_list[s_wc[j * kApWaves + wave] + __popcll(bal[j] & lt_mask)] = (uint16_t)(j * kApThreads + tid);
+                if (need[j]) {
+                    const uint32_t pos = s_wc[j * kApWaves + wave] + __popcll(bal[j] & lt_mask);
+                    s_list[pos] = (uint16_t)(j * kApThreads + tid);
+                    if (pos < kRepCap) L.s_rep[pos] = e[j];
+                }
             __syncthreads();
             const uint32_t nlist = s_nlist;
             K4_MARK(2);
@@ -767,7 +776,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                 bool pending = false;
                 uint32_t b = 0, k = 0, s = 0, rf = 0;
                 if (i < nlist) {
-                    const uint64_t ee = ent[cb + s_list[i]];
+                    const uint64_t ee = i < kRepCap ? L.s_rep[i] : ent[cb + s_list[i]];
                     b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
                     pending = b % kApWaves == wave;
                     if (pending) {
@@ -809,7 +818,8 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
                 const uint32_t i = g0 + lane;
                 if (i < nlist) {
-                    const uint32_t b = (uint32_t)(ent[cb + s_list[i]] >> 32) & (kTileMax - 1u);
+                    const uint64_t ee = i < kRepCap ? L.s_rep[i] : ent[cb + s_list[i]];
+                    const uint32_t b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
                     if (b % kApWaves == wave) accN[b] = 0;
                 }
             }

@@ -158,7 +158,8 @@ __device__ __forceinline__ int parse_l3(const uint32_t (&w)[16], uint32_t type, 
     }
 }
 
-// 64-byte record -> canonical tuple words. Returns PARSE_*.
+// 64-byte record -> canonical tuple words (bytes 0..36 = src16, dst16, sport,
+// dport BE, proto; byte 39 = IP version 4/6).  Returns PARSE_*.
 __device__ __forceinline__ int parse_record(const uint32_t (&w)[16], uint32_t wirelen,
                                             uint32_t (&tw)[10]) {
 #pragma unroll
@@ -169,6 +170,7 @@ __device__ __forceinline__ int parse_record(const uint32_t (&w)[16], uint32_t wi
         tw[0] = w[4]; tw[1] = w[5]; tw[2] = w[6];  tw[3] = w[7];
         tw[4] = w[8]; tw[5] = w[9]; tw[6] = w[10]; tw[7] = w[11];
         set_ports(tw, rec_be16<48>(w), rec_be16<50>(w), rec_byte<52>(w));
+        tw[9] |= rec_byte<15>(w) << 24;  // IP version (byte 39, outside every key plan)
         return PARSE_OK;
     }
     // gopacket Dot1Q: up to two tags (4 bytes = one word each) before the ethertype
@@ -190,7 +192,9 @@ __device__ __forceinline__ int parse_record(const uint32_t (&w)[16], uint32_t wi
         const uint32_t a2 = (i >= 3 && i + 2 < 16) ? w[i + 2 < 16 ? i + 2 : 15] : w[i];
         ws[i] = nv == 0 ? w[i] : (nv == 1 ? a1 : a2);
     }
-    return parse_l3(ws, type, wirelen, nv, tw);
+    const int st = parse_l3(ws, type, wirelen, nv, tw);
+    tw[9] |= (type == 0x86DDu ? 6u : 4u) << 24;  // IP version (byte 39, outside every key plan)
+    return st;
 }
 
 // byte idx (0..36) of the canonical tuple; 255 (or >= 40) -> 0

@@ -1,0 +1,677 @@
+// gns_exact.hip -- MI355X engine for Go2NetSpectra's exact aggregator
+// (internal/engine/impl/exact/task.go): per-flow PacketCount, ByteCount,
+// StartTime (first packet) and EndTime (last packet, in stream order).
+//
+// Keys: the reference keys flows by the STRING strings.Join(fields, "-")
+// with IPs printed by net.IP.String() (generateKeyAndFields, task.go:330-366).
+// Two IPs print the same exactly when their 16-byte forms (To16) are equal:
+// IPv4 (4-byte) and IPv4-mapped IPv6 both print as a dotted quad, every other
+// IPv6 prints its 16 bytes.  The engine therefore keys flows by the key bytes
+// of the sketch layout (task.go:265-300) with every IP field in To16 form, in
+// the flow dictionary of gns_keys.cuh (full key bytes, exact compare).
+//
+// Counters are additive; only StartTime/EndTime depend on order.  They are the
+// timestamps of the flow's first and last packet in stream order, found with
+// atomicMin/atomicMax on the global packet index and resolved by a second
+// pass that lets the packet holding that index write its timestamp.
+//
+//   X1  k_ex_extract   parse -> To16 tuple -> key -> flow id (dictionary)
+//   X1b k_ex_resolve   re-probe packets parked on a same-launch claim
+//   X2  k_ex_aggregate per 16K-packet block: LDS hash aggregation of
+//                      (count, bytes, first, last) per flow id, one set of
+//                      global atomics per distinct flow per block
+//   X3  k_ex_times     first/last packets write StartTime/EndTime
+#include <algorithm>
+#include <vector>
+
+#include "gns_common.hpp"
+
+namespace gns {
+
+constexpr int kXThreads = 256;
+constexpr uint32_t kXChunk = 16384;
+constexpr uint32_t kXTab = 2048;   // LDS aggregation slots per block
+constexpr uint32_t kXProbe = 16;
+
+struct ExIn {
+    InputDesc in;
+    const uint8_t *ipver;  // IN_TUPLE: 4 / 6 per packet (NULL -> 4)
+    const int64_t *ts;
+};
+
+// IPv4 (4-byte net.IP, left-aligned in its slot) -> ::ffff:a.b.c.d, the form
+// in which it compares equal to the same address arriving IPv4-mapped.
+__device__ __forceinline__ void to16(uint32_t (&tw)[10], uint32_t ver) {
+    if (ver == 4u) {
+        tw[3] = tw[0]; tw[0] = 0u; tw[1] = 0u; tw[2] = 0xFFFF0000u;
+        tw[7] = tw[4]; tw[4] = 0u; tw[5] = 0u; tw[6] = 0xFFFF0000u;
+    }
+}
+
+template <int KIND, int MODE>
+__device__ __forceinline__ int ex_key(const ExIn &x, uint32_t K, const uint8_t *s_src, uint64_t p,
+                                      uint32_t (&kw)[GNS_KWMAX]) {
+    uint32_t tw[10];
+    const int st = load_tuple<KIND>(x.in, p, tw);
+    if (st != PARSE_OK) return st;
+    uint32_t ver;
+    if constexpr (KIND == IN_HDR) ver = tw[9] >> 24;
+    else ver = x.ipver ? x.ipver[p] : 4u;
+    to16(tw, ver);
+    tw[9] &= 0xFFu;
+    make_key_m<MODE, GNS_KWMAX>(K, s_src, tw, kw);
+    return PARSE_OK;
+}
+
+struct ExArgs {
+    ExIn x;
+    uint64_t n;
+    KeyPlanN kp;
+    DictDev D;
+    uint32_t epoch;
+    uint32_t *keyid;
+    uint64_t *pend;
+    uint32_t *pend_cnt, *pend_total;
+    unsigned long long *stats;  // 0 inserted, 1 dropped, 2 unsupported, 3 dict full
+};
+
+template <int KIND, int MODE>
+__global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
+    __shared__ uint8_t s_src[80];
+    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
+    const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    stage_plan<MODE>(a.kp, s_src);
+    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; }
+    __syncthreads();
+    const uint32_t K = a.kp.K;
+    const uint64_t beg = (uint64_t)blk * kXChunk;
+    const uint64_t end = min(a.n, beg + kXChunk);
+    uint32_t n_ok = 0;
+    for (uint64_t p = beg + tid; p < end; p += kXThreads) {
+        uint32_t kw[GNS_KWMAX];
+        const int st = ex_key<KIND, MODE>(a.x, K, s_src, p, kw);
+        if (st != PARSE_OK) {
+            a.keyid[p] = GNS_ID_NONE;
+            atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
+            continue;
+        }
+        uint32_t out;
+        const int r = dict_find_or_claim(a.D, kw, mm3_n<GNS_KWMAX>(kw, K, a.D.seed) & a.D.mask, a.epoch, &out);
+        if (r == DICT_FULL) {
+            a.keyid[p] = GNS_ID_NONE;
+            atomicAdd(&s_full, 1u);
+            continue;
+        }
+        n_ok++;
+        if (r == DICT_FOUND) {
+            a.keyid[p] = out;
+        } else {
+            a.keyid[p] = GNS_ID_NONE;
+            a.pend[beg + atomicAdd(&s_pend, 1u)] = (uint64_t)(p - beg) << 32 | out;
+        }
+    }
+    atomicAdd(&s_ok, n_ok);
+    __syncthreads();
+    if (tid == 0) {
+        a.pend_cnt[blk] = s_pend;
+        if (s_pend) atomicAdd(a.pend_total, s_pend);
+        if (s_ok) atomicAdd(&a.stats[0], (unsigned long long)s_ok);
+        if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
+        if (s_unsup) atomicAdd(&a.stats[2], (unsigned long long)s_unsup);
+        if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+    }
+}
+
+struct ExResolveArgs {
+    ExArgs x;
+    const uint64_t *pend_in;
+    const uint32_t *cnt_in;
+    uint64_t *pend_out;
+    uint32_t *cnt_out, *total_out;
+};
+
+template <int KIND, int MODE>
+__global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
+    __shared__ uint8_t s_src[80];
+    __shared__ uint32_t s_cnt, s_full;
+    const ExArgs &a = r.x;
+    const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    stage_plan<MODE>(a.kp, s_src);
+    if (tid == 0) { s_cnt = 0; s_full = 0; }
+    __syncthreads();
+    const uint32_t cnt = r.cnt_in[blk];
+    const uint64_t beg = (uint64_t)blk * kXChunk;
+    for (uint32_t i = tid; i < cnt; i += kXThreads) {
+        const uint64_t v = r.pend_in[beg + i];
+        const uint64_t p = beg + (v >> 32);
+        uint32_t kw[GNS_KWMAX];
+        (void)ex_key<KIND, MODE>(a.x, a.kp.K, s_src, p, kw);
+        uint32_t out;
+        const int res = dict_find_or_claim(a.D, kw, (uint32_t)v, a.epoch, &out);
+        if (res == DICT_FOUND) a.keyid[p] = out;
+        else if (res == DICT_PENDING) r.pend_out[beg + atomicAdd(&s_cnt, 1u)] = (v & 0xFFFFFFFF00000000ull) | out;
+        else atomicAdd(&s_full, 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        r.cnt_out[blk] = s_cnt;
+        if (s_cnt) atomicAdd(r.total_out, s_cnt);
+        if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+    }
+}
+
+struct FlowState {
+    unsigned long long *pkts, *bytes, *first, *last;
+    long long *start, *end;
+};
+
+struct ExAggArgs {
+    const uint32_t *keyid;
+    const uint32_t *len;
+    uint64_t n, pkt_base;
+    FlowState f;
+};
+
+// X2: per block, LDS hash aggregation keyed by flow id (Zipf: the heavy flows
+// collapse to one set of global atomics per block); flows that do not find a
+// slot within kXProbe probes go straight to global atomics.
+__global__ __launch_bounds__(kXThreads) void k_ex_aggregate(ExAggArgs a) {
+    __shared__ uint32_t s_key[kXTab], s_cnt[kXTab], s_mn[kXTab], s_mx[kXTab];
+    __shared__ unsigned long long s_bytes[kXTab];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < kXTab; i += kXThreads) {
+        s_key[i] = GNS_ID_NONE; s_cnt[i] = 0; s_bytes[i] = 0; s_mn[i] = 0xFFFFFFFFu; s_mx[i] = 0;
+    }
+    __syncthreads();
+    const uint64_t beg = (uint64_t)blockIdx.x * kXChunk;
+    const uint64_t end = min(a.n, beg + kXChunk);
+    for (uint64_t p = beg + tid; p < end; p += kXThreads) {
+        const uint32_t id = a.keyid[p];
+        if (id == GNS_ID_NONE) continue;
+        const uint32_t ln = a.len[p];
+        const uint32_t li = (uint32_t)(p - beg);
+        uint32_t slot = (id * 0x9E3779B1u) >> (32 - 11);
+        bool done = false;
+        for (uint32_t k = 0; k < kXProbe; k++) {
+            uint32_t cur = s_key[slot];
+            if (cur == GNS_ID_NONE) {
+                const uint32_t prev = atomicCAS(&s_key[slot], GNS_ID_NONE, id);
+                cur = prev == GNS_ID_NONE ? id : prev;
+            }
+            if (cur == id) {
+                atomicAdd(&s_cnt[slot], 1u);
+                atomicAdd(&s_bytes[slot], (unsigned long long)ln);
+                atomicMin(&s_mn[slot], li);
+                atomicMax(&s_mx[slot], li);
+                done = true;
+                break;
+            }
+            slot = (slot + 1) & (kXTab - 1);
+        }
+        if (!done) {
+            const unsigned long long g = a.pkt_base + p;
+            atomicAdd(&a.f.pkts[id], 1ull);
+            atomicAdd(&a.f.bytes[id], (unsigned long long)ln);
+            atomicMin(&a.f.first[id], g);
+            atomicMax(&a.f.last[id], g);
+        }
+    }
+    __syncthreads();
+    const unsigned long long gb = a.pkt_base + beg;
+    for (uint32_t i = tid; i < kXTab; i += kXThreads) {
+        const uint32_t id = s_key[i];
+        if (id == GNS_ID_NONE) continue;
+        atomicAdd(&a.f.pkts[id], (unsigned long long)s_cnt[i]);
+        atomicAdd(&a.f.bytes[id], s_bytes[i]);
+        atomicMin(&a.f.first[id], gb + s_mn[i]);
+        atomicMax(&a.f.last[id], gb + s_mx[i]);
+    }
+}
+
+// X3: the packet that is its flow's first (last) writes StartTime (EndTime).
+__global__ __launch_bounds__(256) void k_ex_times(const uint32_t *keyid, const int64_t *ts, uint64_t n,
+                                                  uint64_t pkt_base, FlowState f) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t id = keyid[p];
+    if (id == GNS_ID_NONE) return;
+    const unsigned long long g = pkt_base + p;
+    if (f.first[id] == g) f.start[id] = ts[p];
+    if (f.last[id] == g) f.end[id] = ts[p];
+}
+
+__global__ __launch_bounds__(256) void k_ex_query(const uint8_t *flows, uint32_t stride, uint64_t n, uint32_t K,
+                                                  DictDev D, FlowState f, uint64_t *out) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    uint32_t kw[GNS_KWMAX];
+    load_key_bytes<GNS_KWMAX>(flows + p * stride, K, false, kw);
+    const uint32_t id = dict_lookup(D, kw);
+    out[p] = id == GNS_ID_NONE ? 0ull : (uint64_t)(f.pkts[id] << 32 | f.bytes[id]);  // task.go:323
+}
+
+// occupied dictionary slots -> ids (snapshot)
+__global__ __launch_bounds__(256) void k_ex_list(DictDev D, uint64_t slots, uint32_t *ids, uint32_t *count) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool occ = s < slots && D.rec[s * D.RW] != 0u;
+    const uint64_t m = __ballot(occ);
+    if (m == 0) return;
+    const uint32_t lane = __lane_id();
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (occ) ids[base + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)s;
+}
+
+__global__ __launch_bounds__(256) void k_ex_gather(const uint32_t *ids, uint64_t n, DictDev D, FlowState f,
+                                                   uint8_t *keys, long long *start, long long *end,
+                                                   unsigned long long *pkts, unsigned long long *bytes) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t id = ids[p];
+    uint32_t r[12];
+    load_record(D, id, r);
+    for (uint32_t j = 0; j < D.K; j++) keys[p * D.K + j] = (uint8_t)(r[1 + (j >> 2)] >> (8 * (j & 3)));
+    start[p] = f.start[id]; end[p] = f.end[id]; pkts[p] = f.pkts[id]; bytes[p] = f.bytes[id];
+}
+
+__global__ __launch_bounds__(256) void k_ex_init(FlowState f, uint64_t slots) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= slots) return;
+    f.pkts[s] = 0; f.bytes[s] = 0; f.first[s] = ~0ull; f.last[s] = 0; f.start[s] = 0; f.end[s] = 0;
+}
+
+}  // namespace gns
+
+using namespace gns;
+
+struct gns_ex {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    KeyPlanN kp{};
+    uint32_t K = 0;
+    DictDev D{};
+    uint64_t slots = 0;
+    FlowState f{};
+    uint32_t epoch = 0;
+    uint64_t pkt = 0, batches = 0;
+    uint64_t bmax = 0;
+    uint32_t nblk_max = 0;
+    uint32_t *keyid = nullptr;
+    uint64_t *pend[2] = {nullptr, nullptr};
+    uint32_t *pcnt[2] = {nullptr, nullptr};
+    uint32_t *ptotal = nullptr;
+    unsigned long long *stats = nullptr;
+    uint32_t *h_pin = nullptr;
+    uint8_t *stage = nullptr;
+    size_t stage_bytes = 0;
+    StageTimer timer;
+};
+
+namespace {
+
+int ex_set_dev(gns_ex *ex) {
+    GNS_HIP(hipSetDevice(ex->device));
+    return GNS_OK;
+}
+
+void ex_free_all(gns_ex *ex) {
+    dfree(ex->D.rec); dfree(ex->f.pkts); dfree(ex->f.bytes); dfree(ex->f.first); dfree(ex->f.last);
+    dfree(ex->f.start); dfree(ex->f.end); dfree(ex->keyid); dfree(ex->pend[0]); dfree(ex->pend[1]);
+    dfree(ex->pcnt[0]); dfree(ex->pcnt[1]); dfree(ex->ptotal); dfree(ex->stats); dfree(ex->stage);
+    if (ex->h_pin) (void)hipHostFree(ex->h_pin);
+    ex->timer.destroy();
+    if (ex->stream) (void)hipStreamDestroy(ex->stream);
+}
+
+int ex_clear(gns_ex *ex) {
+    GNS_HIP(hipMemsetAsync(ex->D.rec, 0, ex->slots * ex->D.RW * 4, ex->stream));
+    hipLaunchKernelGGL(k_ex_init, dim3((unsigned)((ex->slots + 255) / 256)), dim3(256), 0, ex->stream, ex->f,
+                       ex->slots);
+    GNS_HIP(hipGetLastError());
+    return GNS_OK;
+}
+
+template <int KIND, int MODE>
+int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
+    if (n == 0) return GNS_OK;
+    hipStream_t s = ex->stream;
+    const uint32_t nblk = (uint32_t)((n + kXChunk - 1) / kXChunk);
+    ScopedStage total_stage(ex->timer, 5);
+    GNS_HIP(hipMemsetAsync(ex->ptotal, 0, 8, s));
+    if (++ex->epoch == 0) ex->epoch = 1;
+    ExArgs x{};
+    x.x = xin; x.n = n; x.kp = ex->kp; x.D = ex->D; x.epoch = ex->epoch; x.keyid = ex->keyid;
+    x.pend = ex->pend[0]; x.pend_cnt = ex->pcnt[0]; x.pend_total = ex->ptotal; x.stats = ex->stats;
+    {
+        ScopedStage st(ex->timer, 0);
+        hipLaunchKernelGGL((k_ex_extract<KIND, MODE>), dim3(nblk), dim3(kXThreads), 0, s, x);
+        GNS_HIP(hipGetLastError());
+    }
+    int cur = 0;
+    for (int round = 0;; round++) {
+        GNS_HIP(hipMemcpyAsync(ex->h_pin, ex->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
+        GNS_HIP(hipMemcpyAsync(ex->h_pin + 2, ex->stats + 3, 8, hipMemcpyDeviceToHost, s));
+        GNS_HIP(hipStreamSynchronize(s));
+        if (ex->h_pin[2] | ex->h_pin[3]) { set_error("flow dictionary full; raise max_flows"); return GNS_E_FULL; }
+        if (ex->h_pin[0] == 0) break;
+        if (round > 64) { set_error("dictionary resolve did not converge"); return GNS_E_FULL; }
+        GNS_HIP(hipMemsetAsync(ex->ptotal + (cur ^ 1), 0, 4, s));
+        if (++ex->epoch == 0) ex->epoch = 1;
+        ExResolveArgs r{};
+        r.x = x; r.x.epoch = ex->epoch;
+        r.pend_in = ex->pend[cur]; r.cnt_in = ex->pcnt[cur];
+        r.pend_out = ex->pend[cur ^ 1]; r.cnt_out = ex->pcnt[cur ^ 1]; r.total_out = ex->ptotal + (cur ^ 1);
+        ScopedStage st(ex->timer, 1);
+        hipLaunchKernelGGL((k_ex_resolve<KIND, MODE>), dim3(nblk), dim3(kXThreads), 0, s, r);
+        GNS_HIP(hipGetLastError());
+        cur ^= 1;
+    }
+    {
+        ScopedStage st(ex->timer, 2);
+        ExAggArgs g{ex->keyid, xin.in.sizes, n, ex->pkt, ex->f};
+        hipLaunchKernelGGL(k_ex_aggregate, dim3(nblk), dim3(kXThreads), 0, s, g);
+        GNS_HIP(hipGetLastError());
+    }
+    {
+        ScopedStage st(ex->timer, 3);
+        hipLaunchKernelGGL(k_ex_times, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ex->keyid, xin.ts, n,
+                           ex->pkt, ex->f);
+        GNS_HIP(hipGetLastError());
+    }
+    ex->pkt += n;
+    ex->batches++;
+    return GNS_OK;
+}
+
+template <int KIND>
+int ex_dispatch(gns_ex *ex, const ExIn &x, uint64_t n) {
+    switch (plan_mode(ex->kp)) {
+    case PLAN_SLICE0: return ex_run_batch<KIND, PLAN_SLICE0>(ex, x, n);
+    case PLAN_SLICE4: return ex_run_batch<KIND, PLAN_SLICE4>(ex, x, n);
+    default: return ex_run_batch<KIND, PLAN_GENERIC>(ex, x, n);
+    }
+}
+
+template <int KIND>
+int ex_insert(gns_ex *ex, const ExIn &x0, uint64_t n, gns_mem where) {
+    GNS_TRY(ex_set_dev(ex));
+    for (uint64_t off = 0; off < n; off += ex->bmax) {
+        const uint64_t m = std::min<uint64_t>(ex->bmax, n - off);
+        ExIn x = x0;
+        InputDesc &d = x.in;
+        const InputDesc &in = x0.in;
+        if (where == GNS_MEM_DEVICE) {
+            if (d.hdr) d.hdr += off * 16;
+            if (d.src16) d.src16 += off * 16;
+            if (d.dst16) d.dst16 += off * 16;
+            if (d.sport) d.sport += off;
+            if (d.dport) d.dport += off;
+            if (d.proto) d.proto += off;
+            if (d.sizes) d.sizes += off;
+            if (x.ipver) x.ipver += off;
+            x.ts += off;
+        } else {
+            const void *src[9] = {in.hdr ? (const void *)(in.hdr + off * 16) : nullptr,
+                                  in.src16 ? (const void *)(in.src16 + off * 16) : nullptr,
+                                  in.dst16 ? (const void *)(in.dst16 + off * 16) : nullptr,
+                                  in.sport ? (const void *)(in.sport + off) : nullptr,
+                                  in.dport ? (const void *)(in.dport + off) : nullptr,
+                                  in.proto ? (const void *)(in.proto + off) : nullptr,
+                                  in.sizes ? (const void *)(in.sizes + off) : nullptr,
+                                  x0.ipver ? (const void *)(x0.ipver + off) : nullptr,
+                                  (const void *)(x0.ts + off)};
+            const size_t bytes[9] = {in.hdr ? m * 64 : 0, in.src16 ? m * 16 : 0, in.dst16 ? m * 16 : 0,
+                                     in.sport ? m * 2 : 0, in.dport ? m * 2 : 0, in.proto ? m : 0,
+                                     in.sizes ? m * 4 : 0, x0.ipver ? m : 0, m * 8};
+            size_t tot = 0;
+            for (int i = 0; i < 9; i++) tot += (bytes[i] + 15) & ~size_t(15);
+            if (ex->stage_bytes < tot) {
+                dfree(ex->stage);
+                ex->stage = nullptr;
+                ex->stage_bytes = 0;
+                GNS_TRY(dalloc(reinterpret_cast<void **>(&ex->stage), tot));
+                ex->stage_bytes = tot;
+            }
+            uint8_t *p = ex->stage;
+            const void **dst[9] = {(const void **)&d.hdr, (const void **)&d.src16, (const void **)&d.dst16,
+                                   (const void **)&d.sport, (const void **)&d.dport, (const void **)&d.proto,
+                                   (const void **)&d.sizes, (const void **)&x.ipver, (const void **)&x.ts};
+            for (int i = 0; i < 9; i++) {
+                if (!bytes[i]) continue;
+                GNS_HIP(hipMemcpyAsync(p, src[i], bytes[i], hipMemcpyHostToDevice, ex->stream));
+                *dst[i] = p;
+                p += (bytes[i] + 15) & ~size_t(15);
+            }
+        }
+        GNS_TRY(ex_dispatch<KIND>(ex, x, m));
+    }
+    return GNS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gns_ex_create(const gns_ex_params *p, gns_ex **out) {
+    if (!p || !out) { set_error("null argument"); return GNS_E_ARG; }
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device available");
+        return GNS_E_NODEV;
+    }
+    if (p->device < 0 || p->device >= ndev) { set_error("device %d out of range", p->device); return GNS_E_ARG; }
+    gns_ex *ex = new gns_ex();
+    ex->device = p->device;
+    int rc = GNS_OK;
+    do {
+        if ((rc = ex_set_dev(ex)) != GNS_OK) break;
+        if (p->key.n_fields == 0) { set_error("exact task needs key_fields"); rc = GNS_E_ARG; break; }
+        for (uint32_t i = 0; i < p->key.n_fields; i++)
+            if (p->key.fields[i] < GNS_F_SRCIP || p->key.fields[i] > GNS_F_PROTO) {
+                set_error("unknown key field id %u (task.go:363 rejects it)", p->key.fields[i]);
+                rc = GNS_E_ARG;
+            }
+        if (rc) break;
+        if ((rc = make_plan(p->key, 0, &ex->kp)) != GNS_OK) break;
+        ex->K = ex->kp.K;
+        if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) {
+            set_error("hipStreamCreate failed"); rc = GNS_E_HIP; break;
+        }
+        ex->timer.stream = ex->stream;
+        const uint64_t mf = p->max_flows ? p->max_flows : (4ull << 20);
+        uint64_t slots = 1;
+        while (slots < 2 * mf) slots <<= 1;
+        if (slots > (1ull << 30)) { set_error("max_flows too large"); rc = GNS_E_ARG; break; }
+        ex->slots = slots;
+        ex->D.mask = (uint32_t)(slots - 1);
+        ex->D.K = ex->K;
+        ex->D.RW = ((1 + (ex->K + 3) / 4) + 3) & ~3u;
+        ex->D.seed = 0x5BD1E995u;
+        ex->bmax = p->batch_packets ? p->batch_packets : (16ull << 20);
+        ex->bmax = std::min<uint64_t>(((ex->bmax + kXChunk - 1) / kXChunk) * kXChunk, 1ull << 31);
+        ex->nblk_max = (uint32_t)(ex->bmax / kXChunk);
+        if ((rc = dalloc_t(&ex->D.rec, slots * ex->D.RW)) || (rc = dalloc_t(&ex->f.pkts, slots)) ||
+            (rc = dalloc_t(&ex->f.bytes, slots)) || (rc = dalloc_t(&ex->f.first, slots)) ||
+            (rc = dalloc_t(&ex->f.last, slots)) || (rc = dalloc_t(&ex->f.start, slots)) ||
+            (rc = dalloc_t(&ex->f.end, slots)) || (rc = dalloc_t(&ex->keyid, ex->bmax)) ||
+            (rc = dalloc_t(&ex->pend[0], ex->bmax)) || (rc = dalloc_t(&ex->pend[1], ex->bmax)) ||
+            (rc = dalloc_t(&ex->pcnt[0], ex->nblk_max)) || (rc = dalloc_t(&ex->pcnt[1], ex->nblk_max)) ||
+            (rc = dalloc_t(&ex->ptotal, 2)) || (rc = dalloc_t(&ex->stats, 8)))
+            break;
+        if (hipHostMalloc(reinterpret_cast<void **>(&ex->h_pin), 64, 0) != hipSuccess) {
+            set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
+        }
+        if (hipMemsetAsync(ex->stats, 0, 64, ex->stream) != hipSuccess) { rc = GNS_E_HIP; break; }
+        if ((rc = ex_clear(ex)) != GNS_OK) break;
+        if (hipStreamSynchronize(ex->stream) != hipSuccess) { rc = GNS_E_HIP; break; }
+    } while (0);
+    if (rc != GNS_OK) {
+        ex_free_all(ex);
+        delete ex;
+        return rc;
+    }
+    *out = ex;
+    return GNS_OK;
+}
+
+int gns_ex_destroy(gns_ex *ex) {
+    if (!ex) return GNS_OK;
+    (void)hipSetDevice(ex->device);
+    if (ex->stream) (void)hipStreamSynchronize(ex->stream);
+    ex_free_all(ex);
+    delete ex;
+    return GNS_OK;
+}
+
+int gns_ex_insert_tuples(gns_ex *ex, const gns_tuples *t, const uint8_t *ipver, const int64_t *ts_ns,
+                         uint64_t n, gns_mem where) {
+    if (!ex || !t) { set_error("null argument"); return GNS_E_ARG; }
+    if (n && (!t->src16 || !t->dst16 || !t->sport || !t->dport || !t->proto || !t->length || !ts_ns)) {
+        set_error("null tuple array"); return GNS_E_ARG;
+    }
+    ExIn x{};
+    x.in.src16 = t->src16; x.in.dst16 = t->dst16; x.in.sport = t->sport; x.in.dport = t->dport;
+    x.in.proto = t->proto; x.in.sizes = t->length;
+    x.ipver = ipver; x.ts = ts_ns;
+    return ex_insert<IN_TUPLE>(ex, x, n, where);
+}
+
+int gns_ex_insert_headers(gns_ex *ex, const uint8_t *hdr, const uint32_t *wirelen, const int64_t *ts_ns,
+                          uint64_t n, gns_mem where) {
+    if (!ex || (n && (!hdr || !wirelen || !ts_ns))) { set_error("null argument"); return GNS_E_ARG; }
+    ExIn x{};
+    x.in.hdr = reinterpret_cast<const uint32_t *>(hdr);
+    x.in.sizes = wirelen;
+    x.ts = ts_ns;
+    return ex_insert<IN_HDR>(ex, x, n, where);
+}
+
+int gns_ex_flush(gns_ex *ex) {
+    if (!ex) return GNS_E_ARG;
+    GNS_TRY(ex_set_dev(ex));
+    GNS_HIP(hipStreamSynchronize(ex->stream));
+    ex->timer.collect();
+    return GNS_OK;
+}
+
+int gns_ex_query(gns_ex *ex, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out) {
+    if (!ex || (n && (!flows || !out))) { set_error("null argument"); return GNS_E_ARG; }
+    if (n == 0) return GNS_OK;
+    if (stride < ex->K) { set_error("stride < key bytes"); return GNS_E_ARG; }
+    GNS_TRY(ex_set_dev(ex));
+    uint8_t *dk = nullptr;
+    uint64_t *dout = nullptr;
+    GNS_TRY(dalloc(reinterpret_cast<void **>(&dk), n * stride));
+    int rc = dalloc(reinterpret_cast<void **>(&dout), n * 8);
+    if (rc) { dfree(dk); return rc; }
+    hipError_t e = hipMemcpyAsync(dk, flows, n * stride, hipMemcpyHostToDevice, ex->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_ex_query, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ex->stream, dk, stride, n,
+                           ex->K, ex->D, ex->f, dout);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, ex->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ex->stream);
+    dfree(dk);
+    dfree(dout);
+    if (e != hipSuccess) { set_error("exact query: %s", hipGetErrorString(e)); return GNS_E_HIP; }
+    return GNS_OK;
+}
+
+int gns_ex_snapshot(gns_ex *ex, uint8_t *keys, int64_t *start_ns, int64_t *end_ns, uint64_t *pkts,
+                    uint64_t *bytes, uint64_t *n_io) {
+    if (!ex || !n_io) { set_error("null argument"); return GNS_E_ARG; }
+    GNS_TRY(ex_set_dev(ex));
+    hipStream_t s = ex->stream;
+    uint32_t *ids = nullptr, *cnt = nullptr;
+    GNS_TRY(dalloc(reinterpret_cast<void **>(&cnt), 16));
+    int rc = dalloc(reinterpret_cast<void **>(&ids), ex->slots * 4);
+    if (rc) { dfree(cnt); return rc; }
+    uint32_t nf = 0;
+    hipError_t e = hipMemsetAsync(cnt, 0, 4, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_ex_list, dim3((unsigned)((ex->slots + 255) / 256)), dim3(256), 0, s, ex->D, ex->slots,
+                           ids, cnt);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&nf, cnt, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    const uint64_t cap = *n_io;
+    *n_io = nf;
+    const uint64_t m = std::min<uint64_t>(cap, nf);
+    if (e == hipSuccess && m > 0 && (keys || start_ns || end_ns || pkts || bytes)) {
+        // slot order (deterministic)
+        std::vector<uint32_t> h(nf);
+        e = hipMemcpy(h.data(), ids, (size_t)nf * 4, hipMemcpyDeviceToHost);
+        std::sort(h.begin(), h.end());
+        if (e == hipSuccess) e = hipMemcpy(ids, h.data(), (size_t)m * 4, hipMemcpyHostToDevice);
+        uint8_t *dk = nullptr;
+        long long *ds = nullptr, *de = nullptr;
+        unsigned long long *dp = nullptr, *db = nullptr;
+        const size_t kb = (size_t)m * std::max<uint32_t>(ex->K, 1);
+        if (e == hipSuccess && (dalloc(reinterpret_cast<void **>(&dk), kb) || dalloc_t(&ds, m) || dalloc_t(&de, m) ||
+                                dalloc_t(&dp, m) || dalloc_t(&db, m)))
+            e = hipErrorOutOfMemory;
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_ex_gather, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, ids, m, ex->D, ex->f,
+                               dk, ds, de, dp, db);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess && keys) e = hipMemcpyAsync(keys, dk, (size_t)m * ex->K, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && start_ns) e = hipMemcpyAsync(start_ns, ds, m * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && end_ns) e = hipMemcpyAsync(end_ns, de, m * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && pkts) e = hipMemcpyAsync(pkts, dp, m * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && bytes) e = hipMemcpyAsync(bytes, db, m * 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        dfree(dk); dfree(ds); dfree(de); dfree(dp); dfree(db);
+    }
+    dfree(ids);
+    dfree(cnt);
+    if (e != hipSuccess) { set_error("exact snapshot: %s", hipGetErrorString(e)); return GNS_E_HIP; }
+    return GNS_OK;
+}
+
+int gns_ex_reset(gns_ex *ex) {
+    if (!ex) return GNS_E_ARG;
+    GNS_TRY(ex_set_dev(ex));
+    GNS_TRY(ex_clear(ex));
+    GNS_HIP(hipStreamSynchronize(ex->stream));
+    return GNS_OK;
+}
+
+int gns_ex_counters(gns_ex *ex, uint64_t out[8]) {
+    if (!ex || !out) return GNS_E_ARG;
+    GNS_TRY(ex_set_dev(ex));
+    GNS_HIP(hipStreamSynchronize(ex->stream));
+    unsigned long long h[8];
+    GNS_HIP(hipMemcpy(h, ex->stats, sizeof(h), hipMemcpyDeviceToHost));
+    uint64_t nf = 0;
+    GNS_TRY(gns_ex_snapshot(ex, nullptr, nullptr, nullptr, nullptr, nullptr, &nf));
+    out[0] = h[0]; out[1] = h[1]; out[2] = h[2]; out[3] = h[3];
+    out[4] = nf; out[5] = ex->pkt; out[6] = ex->batches; out[7] = 0;
+    return GNS_OK;
+}
+
+int gns_ex_set_timing(gns_ex *ex, int on) {
+    if (!ex) return GNS_E_ARG;
+    ex->timer.on = on != 0;
+    return GNS_OK;
+}
+
+int gns_ex_stage_times(gns_ex *ex, double ms[8], uint64_t launches[8], int reset) {
+    if (!ex) return GNS_E_ARG;
+    GNS_TRY(ex_set_dev(ex));
+    ex->timer.collect();
+    for (int i = 0; i < 8; i++) {
+        if (ms) ms[i] = ex->timer.ms[i];
+        if (launches) launches[i] = ex->timer.launches[i];
+    }
+    if (reset) for (int i = 0; i < 8; i++) { ex->timer.ms[i] = 0; ex->timer.launches[i] = 0; }
+    return GNS_OK;
+}
+
+}  // extern "C"

@@ -20,8 +20,10 @@ inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 }  // namespace
 
-extern "C" int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirelen, uint64_t cap,
-                                 uint64_t *total) {
+// ts_ns: capture timestamps in ns (gopacket's pcap handle opens files with
+// nanosecond precision: usec files scale by 1000, nsec files as recorded).
+extern "C" int64_t gns_pack_pcap_ts(const char *path, uint8_t *hdr, uint32_t *wirelen, int64_t *ts_ns,
+                                    uint64_t cap, uint64_t *total) {
     using gns::set_error;
     if (!path) { set_error("null path"); return GNS_E_ARG; }
     FILE *f = fopen(path, "rb");
@@ -33,6 +35,7 @@ extern "C" int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirel
     uint32_t magic;
     memcpy(&magic, gh, 4);
     bool swap = false;
+    const bool nsec = magic == 0xa1b23c4du || magic == 0x4d3cb2a1u;
     if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du) swap = false;
     else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u) swap = true;
     else { fclose(f); set_error("%s: not a classic pcap file (magic %08x)", path, magic); return GNS_E_ARG; }
@@ -51,10 +54,12 @@ extern "C" int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirel
         const size_t got = fread(rh, 1, 16, f);
         if (got == 0) break;
         if (got != 16) break;  // truncated trailer: gopacket stops too
-        uint32_t incl, orig;
+        uint32_t incl, orig, tsec, tfrac;
+        memcpy(&tsec, rh, 4);
+        memcpy(&tfrac, rh + 4, 4);
         memcpy(&incl, rh + 8, 4);
         memcpy(&orig, rh + 12, 4);
-        if (swap) { incl = bswap32(incl); orig = bswap32(orig); }
+        if (swap) { incl = bswap32(incl); orig = bswap32(orig); tsec = bswap32(tsec); tfrac = bswap32(tfrac); }
         if (incl > pkt.size()) pkt.resize(incl);
         if (fread(pkt.data(), 1, incl, f) != incl) break;
         if (written < cap && hdr && wirelen) {
@@ -63,6 +68,7 @@ extern "C" int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirel
             memcpy(r, pkt.data(), c);
             if (c < 64) memset(r + c, 0, 64 - c);
             wirelen[written] = orig;
+            if (ts_ns) ts_ns[written] = (int64_t)(int32_t)tsec * 1000000000ll + (int64_t)tfrac * (nsec ? 1 : 1000);
             written++;
         }
         n++;
@@ -70,4 +76,9 @@ extern "C" int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirel
     fclose(f);
     if (total) *total = n;
     return (int64_t)written;
+}
+
+extern "C" int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirelen, uint64_t cap,
+                                 uint64_t *total) {
+    return gns_pack_pcap_ts(path, hdr, wirelen, nullptr, cap, total);
 }

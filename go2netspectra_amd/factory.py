@@ -49,7 +49,15 @@ def _sketch_factory(cfg: Config, **task_kw) -> TaskGroup:  # sketch/task.go:21-6
     return TaskGroup(Tasks=[SketchTask(t, **task_kw) for t in cfg.Aggregator.Sketch.Tasks], Writers=[])
 
 
+def _exact_factory(cfg: Config, device: int = 0, max_flows: int = 0, batch_packets: int = 0,
+                   **_sketch_only) -> TaskGroup:  # exact/task.go:20-64
+    from .exact import ExactTask
+    return TaskGroup(Tasks=[ExactTask(t.Name, t.KeyFields, t.NumShards, device=device, max_flows=max_flows,
+                                      batch_packets=batch_packets) for t in cfg.Aggregator.Exact.Tasks], Writers=[])
+
+
 register_aggregator("sketch", _sketch_factory)
+register_aggregator("exact", _exact_factory)
 RegisterAggregator = register_aggregator
 Create = create
 
@@ -73,7 +81,7 @@ class Manager:
             t.process_packets(batch)
 
     def snapshot(self) -> Dict[str, object]:
-        """takeSnapshotForWriter without writers: name -> HeavyRecord."""
+        """takeSnapshotForWriter without writers: name -> HeavyRecord (sketch) / SnapshotData (exact)."""
         return {t.name(): t.snapshot() for t in self.tasks()}
 
     def reset_all(self) -> None:  # resetAllTasks, manager.go:179-193

@@ -34,6 +34,15 @@ def ip_slot(ip) -> bytes:
     return ip + bytes(16 - len(ip))
 
 
+def ip_version(ip) -> int:
+    """4 for a 4-byte net.IP (IPv4 layer), 6 for a 16-byte one."""
+    if isinstance(ip, str):
+        return ipaddress.ip_address(ip).version
+    if isinstance(ip, (ipaddress.IPv4Address, ipaddress.IPv6Address)):
+        return ip.version
+    return 4 if len(bytes(ip)) == 4 else 6
+
+
 @dataclass
 class PacketBatch:
     src16: "np.ndarray"   # [n,16] uint8
@@ -42,21 +51,28 @@ class PacketBatch:
     dport: "np.ndarray"   # [n] uint16
     proto: "np.ndarray"   # [n] uint8
     length: "np.ndarray"  # [n] uint32 (uint32(PacketInfo.Length), task.go:168)
+    ipver: Optional["np.ndarray"] = None  # [n] uint8 4/6: len(net.IP) 4 or 16 (exact keys)
+    ts: Optional["np.ndarray"] = None     # [n] int64 PacketInfo.Timestamp.UnixNano()
 
     def __len__(self) -> int:
         return int(self.length.shape[0])
 
     @classmethod
     def from_packets(cls, packets) -> "PacketBatch":
-        """packets: iterable of (src, dst, sport, dport, proto, length)."""
+        """packets: iterable of (src, dst, sport, dport, proto, length[, ts_ns]).  The IP
+        version of each packet is that of its source address (net.IP length 4 or 16)."""
         rows = list(packets)
         n = len(rows)
         b = cls(np.zeros((n, 16), np.uint8), np.zeros((n, 16), np.uint8), np.zeros(n, np.uint16),
-                np.zeros(n, np.uint16), np.zeros(n, np.uint8), np.zeros(n, np.uint32))
-        for i, (s, d, sp, dp, pr, ln) in enumerate(rows):
+                np.zeros(n, np.uint16), np.zeros(n, np.uint8), np.zeros(n, np.uint32),
+                np.zeros(n, np.uint8), np.zeros(n, np.int64))
+        for i, row in enumerate(rows):
+            s, d, sp, dp, pr, ln = row[:6]
             b.src16[i] = np.frombuffer(ip_slot(s), np.uint8)
             b.dst16[i] = np.frombuffer(ip_slot(d), np.uint8)
             b.sport[i], b.dport[i], b.proto[i], b.length[i] = sp, dp, pr, ln & 0xFFFFFFFF
+            b.ipver[i] = ip_version(s)
+            b.ts[i] = row[6] if len(row) > 6 else i
         return b
 
     def to(self, device):
@@ -64,7 +80,9 @@ class PacketBatch:
         import torch
         f = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
         return PacketBatch(f(self.src16), f(self.dst16), f(self.sport.view(np.int16)),
-                           f(self.dport.view(np.int16)), f(self.proto), f(self.length.view(np.int32)))
+                           f(self.dport.view(np.int16)), f(self.proto), f(self.length.view(np.int32)),
+                           None if self.ipver is None else f(self.ipver),
+                           None if self.ts is None else f(self.ts))
 
     def c_struct(self):
         arrs = [self.src16, self.dst16, self.sport, self.dport, self.proto, self.length]
@@ -101,6 +119,7 @@ class PacketBatch:
 class HeaderBatch:
     hdr: "np.ndarray"      # [n,64] uint8
     wirelen: "np.ndarray"  # [n] uint32
+    ts: Optional["np.ndarray"] = None  # [n] int64 capture timestamps (ns)
 
     def __len__(self) -> int:
         return int(self.wirelen.shape[0])
@@ -117,21 +136,24 @@ def read_pcap(path: str, limit: Optional[int] = None) -> HeaderBatch:
         limit = total.value
     hdr = np.zeros((limit, 64), np.uint8)
     wl = np.zeros(limit, np.uint32)
-    r = L.gns_pack_pcap(os.fsencode(path), hdr.ctypes.data, wl.ctypes.data, limit, ct.byref(total))
+    ts = np.zeros(limit, np.int64)
+    r = L.gns_pack_pcap_ts(os.fsencode(path), hdr.ctypes.data, wl.ctypes.data, ts.ctypes.data, limit,
+                           ct.byref(total))
     if r < 0:
         check(int(r))
-    return HeaderBatch(hdr[:r], wl[:r])
+    return HeaderBatch(hdr[:r], wl[:r], ts[:r])
 
 
-def write_pcap(path: str, frames, wirelens=None, snaplen: int = 65536) -> None:
-    """Classic little-endian pcap writer (tests / tools)."""
+def write_pcap(path: str, frames, wirelens=None, snaplen: int = 65536, ts_ns=None) -> None:
+    """Classic little-endian microsecond pcap writer (tests / tools)."""
     import struct
     with open(path, "wb") as f:
         f.write(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, snaplen, 1))
         for i, fr in enumerate(frames):
             fr = bytes(fr)
             wl = len(fr) if wirelens is None else int(wirelens[i])
-            f.write(struct.pack("<IIII", i, 0, len(fr), wl))
+            sec, usec = (i, 0) if ts_ns is None else divmod(int(ts_ns[i]) // 1000, 1_000_000)
+            f.write(struct.pack("<IIII", sec, usec, len(fr), wl))
             f.write(fr)
 
 

@@ -206,6 +206,53 @@ int gns_synth_flows(gns_synth *s, uint32_t *n_flows);
 int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirelen, uint64_t cap,
                       uint64_t *total);
 
+/* as gns_pack_pcap, plus ts_ns[n] = capture timestamp in ns (PacketInfo.Timestamp,
+ * parser.go:30-33; gopacket opens captures with nanosecond precision) */
+int64_t gns_pack_pcap_ts(const char *path, uint8_t *hdr, uint32_t *wirelen, int64_t *ts_ns, uint64_t cap,
+                         uint64_t *total);
+
+/* ------------------------------------------------------------------ */
+/* Exact aggregator (internal/engine/impl/exact/task.go)               */
+/* ------------------------------------------------------------------ */
+/* Replaces exact.New (task.go:83-103), Task.ProcessPacket (:124-149),
+ * Task.Query (:298-326), Task.Snapshot (:153-191) and Task.Reset (:194-210).
+ * Flows are keyed like the reference's string key strings.Join(fields, "-")
+ * with IPs printed by net.IP.String(): the engine stores each IP field as its
+ * 16-byte form (IPv4 and IPv4-mapped IPv6 -> ::ffff:a.b.c.d, other IPv6 as
+ * is), which is equal exactly when the printed strings are equal. */
+typedef struct gns_ex gns_ex;
+typedef struct gns_ex_params {
+    gns_layout key;          /* key_fields (task.go:330-366) */
+    uint64_t max_flows;      /* distinct flows per measurement period (default 4M) */
+    uint64_t batch_packets;  /* device batch (default 16M) */
+    int device;
+} gns_ex_params;
+int gns_ex_create(const gns_ex_params *p, gns_ex **out);
+int gns_ex_destroy(gns_ex *ex);
+/* ProcessPacket over PacketInfo batches.  ipver[n]: 4 (net.IP of 4 bytes, IPv4
+ * left-aligned in the 16-byte slots) or 6 (16-byte net.IP); ts_ns[n] =
+ * PacketInfo.Timestamp.UnixNano(); t->length = ByteCount increment. */
+int gns_ex_insert_tuples(gns_ex *ex, const gns_tuples *t, const uint8_t *ipver, const int64_t *ts_ns,
+                         uint64_t n, gns_mem where);
+/* fused parse of 64-byte records (as gns_cm_insert_headers) + timestamps */
+int gns_ex_insert_headers(gns_ex *ex, const uint8_t *hdr, const uint32_t *wirelen, const int64_t *ts_ns,
+                          uint64_t n, gns_mem where);
+int gns_ex_flush(gns_ex *ex);
+/* out[i] = PacketCount << 32 | ByteCount (task.go:323); IP fields of the
+ * encoded flow are read as 16-byte net.IPs, as the reference does; 0 if absent */
+int gns_ex_query(gns_ex *ex, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out);
+/* Snapshot: *n_io = capacity in, number of flows out.  keys[n*key_bytes] in the
+ * canonical 16-byte-IP layout; start/end = first/last packet timestamps
+ * (stream order), pkts/bytes = PacketCount/ByteCount.  Any pointer may be NULL. */
+int gns_ex_snapshot(gns_ex *ex, uint8_t *keys, int64_t *start_ns, int64_t *end_ns, uint64_t *pkts,
+                    uint64_t *bytes, uint64_t *n_io);
+int gns_ex_reset(gns_ex *ex);
+/* out[8]: inserted, dropped, unsupported, dictionary full, flows, records, batches, 0 */
+int gns_ex_counters(gns_ex *ex, uint64_t out[8]);
+int gns_ex_set_timing(gns_ex *ex, int on);
+/* stages: 0 extract, 1 resolve, 2 aggregate, 3 timestamps, 5 total */
+int gns_ex_stage_times(gns_ex *ex, double ms[8], uint64_t launches[8], int reset);
+
 const char *gns_last_error(void);
 const char *gns_version(void);
 

@@ -136,3 +136,179 @@ func (c *CountMin) Reset() { C.gns_cm_reset(c.h) }
 func (c *CountMin) Close() { C.gns_cm_destroy(c.h) }
 
 var _ statistic.Sketch = (*CountMin)(nil)
+
+// SuperSpread mirrors statistic.SuperSpread (super_spread.go) on one GPU.
+type SuperSpread struct {
+	h        *C.gns_ss
+	flowSize int
+}
+
+// NewSuperSpread replaces statistic.NewSuperSpread (super_spread.go:129-149). Seeds, the
+// HLL master seed and the declared generator's seed are injected (DESIGN.md §2).
+func NewSuperSpread(width, depth, threshold, m, size uint32, base, b float64, flowFields, elemFields []string,
+	seeds []uint32, hllMaster, rngSeed uint64, device int) (*SuperSpread, error) {
+	var p C.gns_ss_params
+	p.width, p.depth, p.threshold, p.m, p.size = C.uint32_t(width), C.uint32_t(depth), C.uint32_t(threshold),
+		C.uint32_t(m), C.uint32_t(size)
+	p.base, p.b = C.double(base), C.double(b)
+	p.flow.n_fields = C.uint32_t(len(flowFields))
+	for i, f := range flowFields {
+		p.flow.fields[i] = fieldIDs[f]
+	}
+	p.elem.n_fields = C.uint32_t(len(elemFields))
+	for i, f := range elemFields {
+		p.elem.fields[i] = fieldIDs[f]
+	}
+	if len(seeds) > 0 {
+		p.seeds = (*C.uint32_t)(unsafe.Pointer(&seeds[0]))
+	}
+	p.hll_master, p.rng_seed, p.device = C.uint64_t(hllMaster), C.uint64_t(rngSeed), C.int(device)
+	var h *C.gns_ss
+	if err := lastErr(C.gns_ss_create(&p, &h)); err != nil {
+		return nil, err
+	}
+	fs := 0
+	for _, f := range flowFields {
+		fs += map[string]int{"SrcIP": 16, "DstIP": 16, "SrcPort": 2, "DstPort": 2, "Protocol": 1}[f]
+	}
+	return &SuperSpread{h: h, flowSize: fs}, nil
+}
+
+// InsertTuples: PacketInfo batch (task.go:156-169 for a whole batch).
+func (s *SuperSpread) InsertTuples(src16, dst16 []byte, sport, dport []uint16, proto []uint8, length []uint32) error {
+	n := len(length)
+	if n == 0 {
+		return nil
+	}
+	t := C.gns_tuples{
+		src16: (*C.uint8_t)(unsafe.Pointer(&src16[0])), dst16: (*C.uint8_t)(unsafe.Pointer(&dst16[0])),
+		sport: (*C.uint16_t)(unsafe.Pointer(&sport[0])), dport: (*C.uint16_t)(unsafe.Pointer(&dport[0])),
+		proto: (*C.uint8_t)(unsafe.Pointer(&proto[0])), length: (*C.uint32_t)(unsafe.Pointer(&length[0])),
+	}
+	return lastErr(C.gns_ss_insert_tuples(s.h, &t, C.uint64_t(n), C.GNS_MEM_HOST))
+}
+
+// Insert implements statistic.Sketch for one packet (prefer InsertTuples).
+func (s *SuperSpread) Insert(flow, elem []byte, size uint32) {
+	if len(flow) == 0 {
+		return
+	}
+	var e *C.uint8_t
+	if len(elem) > 0 {
+		e = (*C.uint8_t)(unsafe.Pointer(&elem[0]))
+	}
+	C.gns_ss_insert_keys(s.h, (*C.uint8_t)(unsafe.Pointer(&flow[0])), C.uint32_t(len(flow)), e,
+		C.uint32_t(len(elem)), 1, C.GNS_MEM_HOST)
+}
+
+// Query implements statistic.Sketch (super_spread.go:238-249).
+func (s *SuperSpread) Query(flow []byte) uint64 {
+	if len(flow) != s.flowSize || len(flow) == 0 {
+		return 1
+	}
+	var out C.uint64_t
+	if C.gns_ss_query(s.h, (*C.uint8_t)(unsafe.Pointer(&flow[0])), C.uint32_t(len(flow)), 1, &out) != C.GNS_OK {
+		return 1
+	}
+	return uint64(out)
+}
+
+// HeavyHitters implements statistic.Sketch (super_spread.go:254-294): Size is nil.
+func (s *SuperSpread) HeavyHitters() statistic.HeavyRecord {
+	var n C.uint64_t
+	if C.gns_ss_heavy_hitters(s.h, nil, nil, &n) != C.GNS_OK {
+		return statistic.HeavyRecord{Count: []statistic.HeavyCount{}}
+	}
+	K := s.flowSize
+	fl := make([]byte, int(n)*K+1)
+	v := make([]uint32, int(n)+1)
+	C.gns_ss_heavy_hitters(s.h, (*C.uint8_t)(unsafe.Pointer(&fl[0])), (*C.uint32_t)(unsafe.Pointer(&v[0])), &n)
+	rec := statistic.HeavyRecord{Count: make([]statistic.HeavyCount, 0, int(n))}
+	for i := 0; i < int(n); i++ {
+		rec.Count = append(rec.Count, statistic.HeavyCount{Flow: append([]byte(nil), fl[i*K:(i+1)*K]...), Count: v[i]})
+	}
+	return rec
+}
+
+// Reset implements statistic.Sketch (super_spread.go:297-311).
+func (s *SuperSpread) Reset() { C.gns_ss_reset(s.h) }
+
+// Close releases the device sketch.
+func (s *SuperSpread) Close() { C.gns_ss_destroy(s.h) }
+
+var _ statistic.Sketch = (*SuperSpread)(nil)
+
+// Exact is the device state of one exact task (internal/engine/impl/exact/task.go).
+type Exact struct {
+	h        *C.gns_ex
+	keyBytes int
+}
+
+// NewExact replaces exact.New's flow map (task.go:83-103).
+func NewExact(keyFields []string, maxFlows uint64, device int) (*Exact, error) {
+	var p C.gns_ex_params
+	p.key.n_fields = C.uint32_t(len(keyFields))
+	kb := 0
+	for i, f := range keyFields {
+		p.key.fields[i] = fieldIDs[f]
+		kb += map[string]int{"SrcIP": 16, "DstIP": 16, "SrcPort": 2, "DstPort": 2, "Protocol": 1}[f]
+	}
+	p.max_flows, p.device = C.uint64_t(maxFlows), C.int(device)
+	var h *C.gns_ex
+	if err := lastErr(C.gns_ex_create(&p, &h)); err != nil {
+		return nil, err
+	}
+	return &Exact{h: h, keyBytes: kb}, nil
+}
+
+// InsertTuples is ProcessPacket (task.go:124-149) for a batch; ipver[i] = len(IP) == 4 ? 4 : 6.
+func (e *Exact) InsertTuples(src16, dst16 []byte, sport, dport []uint16, proto []uint8, length []uint32,
+	ipver []uint8, tsNano []int64) error {
+	n := len(length)
+	if n == 0 {
+		return nil
+	}
+	t := C.gns_tuples{
+		src16: (*C.uint8_t)(unsafe.Pointer(&src16[0])), dst16: (*C.uint8_t)(unsafe.Pointer(&dst16[0])),
+		sport: (*C.uint16_t)(unsafe.Pointer(&sport[0])), dport: (*C.uint16_t)(unsafe.Pointer(&dport[0])),
+		proto: (*C.uint8_t)(unsafe.Pointer(&proto[0])), length: (*C.uint32_t)(unsafe.Pointer(&length[0])),
+	}
+	return lastErr(C.gns_ex_insert_tuples(e.h, &t, (*C.uint8_t)(unsafe.Pointer(&ipver[0])),
+		(*C.int64_t)(unsafe.Pointer(&tsNano[0])), C.uint64_t(n), C.GNS_MEM_HOST))
+}
+
+// Query is exact.Task.Query (task.go:298-326).
+func (e *Exact) Query(flow []byte) uint64 {
+	if len(flow) != e.keyBytes || len(flow) == 0 {
+		return 0
+	}
+	var out C.uint64_t
+	if C.gns_ex_query(e.h, (*C.uint8_t)(unsafe.Pointer(&flow[0])), C.uint32_t(len(flow)), 1, &out) != C.GNS_OK {
+		return 0
+	}
+	return uint64(out)
+}
+
+// Flows returns the snapshot arrays; the task rebuilds statistic.Flow (Key string via
+// net.IP(key[i:i+16]).String(), Fields, StartTime = time.Unix(0, start[i]), ...).
+func (e *Exact) Flows() (keys []byte, start, end []int64, pkts, bytes []uint64, err error) {
+	var n C.uint64_t
+	if err = lastErr(C.gns_ex_snapshot(e.h, nil, nil, nil, nil, nil, &n)); err != nil {
+		return
+	}
+	m := int(n)
+	keys = make([]byte, m*e.keyBytes+1)
+	start, end = make([]int64, m+1), make([]int64, m+1)
+	pkts, bytes = make([]uint64, m+1), make([]uint64, m+1)
+	err = lastErr(C.gns_ex_snapshot(e.h, (*C.uint8_t)(unsafe.Pointer(&keys[0])), (*C.int64_t)(unsafe.Pointer(&start[0])),
+		(*C.int64_t)(unsafe.Pointer(&end[0])), (*C.uint64_t)(unsafe.Pointer(&pkts[0])),
+		(*C.uint64_t)(unsafe.Pointer(&bytes[0])), &n))
+	m = int(n)
+	return keys[:m*e.keyBytes], start[:m], end[:m], pkts[:m], bytes[:m], err
+}
+
+// Reset is exact.Task.Reset (task.go:194-210).
+func (e *Exact) Reset() { C.gns_ex_reset(e.h) }
+
+// Close releases the device state.
+func (e *Exact) Close() { C.gns_ex_destroy(e.h) }

@@ -82,6 +82,19 @@ def lib():
     L.or_det_log.argtypes = [ct.c_double]
     L.or_det_log1m.restype = ct.c_double
     L.or_det_log1m.argtypes = [ct.c_double]
+    L.or_ex_new.restype = ct.c_void_p
+    L.or_ex_new.argtypes = [ct.c_void_p, ct.c_uint32]
+    L.or_ex_free.argtypes = [ct.c_void_p]
+    L.or_ex_reset.argtypes = [ct.c_void_p]
+    L.or_ex_insert_tuples.argtypes = [ct.c_void_p] + [ct.c_void_p] * 8 + [ct.c_uint64]
+    L.or_ex_insert_hdr64.restype = ct.c_uint64
+    L.or_ex_insert_hdr64.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_uint64]
+    L.or_ex_query.restype = ct.c_uint64
+    L.or_ex_query.argtypes = [ct.c_void_p, ct.c_void_p]
+    L.or_ex_count.restype = ct.c_uint64
+    L.or_ex_count.argtypes = [ct.c_void_p]
+    L.or_ex_export.restype = ct.c_uint64
+    L.or_ex_export.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_uint64] + [ct.c_void_p] * 4
     L.or_ss_uniform.restype = ct.c_double
     L.or_ss_uniform.argtypes = [ct.c_uint64, ct.c_uint64, ct.c_uint32, ct.c_uint32]
     L.or_go_pow.restype = ct.c_double
@@ -235,3 +248,49 @@ class SuperSpread:
 
     def reset(self):
         self.L.or_ss_reset(self.h)
+
+
+class Exact:
+    """Sequential exact aggregator (exact/task.go) with Go-formatted string keys."""
+
+    def __init__(self, fields):
+        self.L = lib()
+        f = field_ids(fields)
+        self.fields = list(fields)
+        self.h = self.L.or_ex_new(_p(f), len(fields))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.or_ex_free(self.h)
+            self.h = None
+
+    def insert_tuples(self, src16, dst16, sport, dport, proto, ipver, length, ts):
+        arrs = [np.ascontiguousarray(src16, np.uint8), np.ascontiguousarray(dst16, np.uint8),
+                np.ascontiguousarray(sport, np.uint16), np.ascontiguousarray(dport, np.uint16),
+                np.ascontiguousarray(proto, np.uint8), np.ascontiguousarray(ipver, np.uint8),
+                np.ascontiguousarray(length, np.uint32), np.ascontiguousarray(ts, np.int64)]
+        self.L.or_ex_insert_tuples(self.h, *[_p(a) for a in arrs], len(arrs[-1]))
+
+    def insert_hdr64(self, hdr, wirelen, ts) -> int:
+        hdr = np.ascontiguousarray(hdr, np.uint8)
+        wirelen = np.ascontiguousarray(wirelen, np.uint32)
+        ts = np.ascontiguousarray(ts, np.int64)
+        return self.L.or_ex_insert_hdr64(self.h, _p(hdr), _p(wirelen), _p(ts), len(wirelen))
+
+    def query(self, flow: bytes) -> int:
+        buf = (ct.c_uint8 * max(1, len(flow))).from_buffer_copy(flow or b"\0")
+        return self.L.or_ex_query(self.h, buf)
+
+    def reset(self):
+        self.L.or_ex_reset(self.h)
+
+    def export(self):
+        """{key string: (start_ns, end_ns, packets, bytes)}"""
+        n = self.L.or_ex_count(self.h)
+        cap = max(1, n) * 128
+        keys = ct.create_string_buffer(cap)
+        st, en = np.zeros(max(n, 1), np.int64), np.zeros(max(n, 1), np.int64)
+        pk, by = np.zeros(max(n, 1), np.uint64), np.zeros(max(n, 1), np.uint64)
+        self.L.or_ex_export(self.h, keys, cap, _p(st), _p(en), _p(pk), _p(by))
+        names = keys.value.decode().split("\n")[:n]
+        return {k: (int(st[i]), int(en[i]), int(pk[i]), int(by[i])) for i, k in enumerate(names)}

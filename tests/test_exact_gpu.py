@@ -1,0 +1,155 @@
+"""Exact aggregator parity on the GPU: every flow's Go key string, StartTime,
+EndTime, PacketCount and ByteCount from the engine (C ABI gns_ex_*) equal the
+sequential C restatement of exact/task.go, which keys flows by the Go-formatted
+string itself."""
+import numpy as np
+import pytest
+
+from helpers import frames_from_tuples, random_tuples
+
+pytestmark = pytest.mark.gpu
+
+FIVE = ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"]
+
+
+def gpu_flows(task):
+    return {f.Key: (f.StartTime, f.EndTime, f.PacketCount, f.ByteCount) for f in task.flows()}
+
+
+def tricky_tuples(rng, n, nflows):
+    """IPv4 flows, the same flows arriving IPv4-mapped over IPv6 (same key string),
+    and IPv6 addresses whose 16-byte slot equals an IPv4 slot (different string)."""
+    t = random_tuples(rng, n, nflows, v6_frac=0.3, s=1.05)
+    v6 = t["v6"].copy()
+    ipver = np.where(v6, 6, 4).astype(np.uint8)
+    sel = rng.random(n) < 0.15  # re-send some IPv4 packets as IPv4-mapped IPv6
+    m = sel & ~v6
+    for a in ("src16", "dst16"):
+        x = t[a]
+        x[m, 12:16] = x[m, 0:4]
+        x[m, 0:10] = 0
+        x[m, 10:12] = 0xFF
+    ipver[m] = 6
+    alias = (rng.random(n) < 0.05) & ~v6 & ~m  # IPv4 slot bytes, but a 16-byte IPv6 net.IP
+    ipver[alias] = 6
+    return t, ipver
+
+
+def test_tuples_parity(gpu, oracle):
+    from go2netspectra_amd import ExactTask, PacketBatch
+    rng = np.random.default_rng(1)
+    n = 300_000
+    t, ipver = tricky_tuples(rng, n, 20_000)
+    ts = rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)  # not monotonic: order is stream order
+    b = PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"], ipver, ts)
+    task = ExactTask("per_five_tuple", FIVE, 128, batch_packets=65536)
+    for part in np.array_split(np.arange(n), 3):
+        task.process_packets(PacketBatch(*(None if a is None else a[part] for a in
+                                           (b.src16, b.dst16, b.sport, b.dport, b.proto, b.length, b.ipver, b.ts))))
+    task.flush()
+    orc = oracle.Exact(FIVE)
+    orc.insert_tuples(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], ipver, t["length"], ts)
+    want = orc.export()
+    got = gpu_flows(task)
+    assert len(got) == len(want)
+    assert got == want
+    snap = task.snapshot()
+    assert snap.TaskName == "per_five_tuple" and len(snap.Shards) == 128
+    assert sum(len(s.Flows) for s in snap.Shards) == len(want)
+
+
+@pytest.mark.parametrize("fields", [["SrcIP"], ["DstPort", "Protocol"], ["DstIP", "SrcIP", "SrcPort"]])
+def test_headers_parity_and_reset(gpu, oracle, fields):
+    from go2netspectra_amd import ExactTask, HeaderBatch
+    rng = np.random.default_rng(len(fields))
+    t = random_tuples(rng, 80_000, 3000, v6_frac=0.25)
+    hdr = frames_from_tuples(t, rng, vlan_frac=0.3)
+    hdr[rng.random(len(hdr)) < 0.02, 12:14] = [0x08, 0x06]  # ARP: dropped (parser.go:48-49)
+    ts = np.cumsum(rng.integers(0, 5000, len(hdr))).astype(np.int64)
+    task = ExactTask("x", fields)
+    task.process_packets(HeaderBatch(hdr, t["length"], ts))
+    task.flush()
+    orc = oracle.Exact(fields)
+    done = orc.insert_hdr64(hdr, t["length"], ts)
+    assert task.agg.counters()["inserted"] == done
+    assert gpu_flows(task) == orc.export()
+    task.reset()
+    orc.reset()
+    task.process_packets(HeaderBatch(hdr[:5000], t["length"][:5000], ts[:5000] + 7))
+    orc.insert_hdr64(hdr[:5000], t["length"][:5000], ts[:5000] + 7)
+    task.flush()
+    assert gpu_flows(task) == orc.export()
+
+
+def test_query(gpu, oracle):
+    """Query reads IP fields as 16-byte net.IPs (task.go:298-326): an IPv4 flow is found
+    through its IPv4-mapped form, not through the left-aligned sketch slot."""
+    from go2netspectra_amd import ExactTask, PacketBatch
+    rng = np.random.default_rng(3)
+    n = 50_000
+    t, ipver = tricky_tuples(rng, n, 2000)
+    ts = np.arange(n, dtype=np.int64)
+    task = ExactTask("q", FIVE)
+    task.process_packets(PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"],
+                                     ipver, ts))
+    task.flush()
+    orc = oracle.Exact(FIVE)
+    orc.insert_tuples(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], ipver, t["length"], ts)
+    keys = PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"]).keys(FIVE)[:3000]
+    mapped = keys.copy()
+    v4 = ipver[:3000] == 4
+    for off in (0, 16):
+        mapped[v4, off + 12:off + 16] = keys[v4, off:off + 4]
+        mapped[v4, off:off + 10] = 0
+        mapped[v4, off + 10:off + 12] = 0xFF
+    for q in (keys, mapped):
+        got = task.agg.query_many(q)
+        want = np.array([orc.query(bytes(k)) for k in q], np.uint64)
+        assert np.array_equal(got, want)
+    assert (task.agg.query_many(mapped[v4]) > 0).all()
+    assert task.query(bytes(mapped[0])) == orc.query(bytes(mapped[0]))
+
+
+def test_synthetic_device_resident(gpu, oracle):
+    import torch
+    from go2netspectra_amd import ExactTask, HeaderBatch, SyntheticTraffic
+    syn = SyntheticTraffic()
+    hdr, wl = syn.generate(2_000_000)
+    ts = torch.arange(2_000_000, dtype=torch.int64, device="cuda") * 1000 + 1_700_000_000_000_000_000
+    task = ExactTask("per_five_tuple", FIVE, max_flows=1 << 21)
+    task.process_packets(HeaderBatch(hdr, wl, ts))
+    task.flush()
+    torch.cuda.synchronize()
+    orc = oracle.Exact(FIVE)
+    assert orc.insert_hdr64(hdr.cpu().numpy(), wl.cpu().numpy().view(np.uint32), ts.cpu().numpy()) == 2_000_000
+    assert gpu_flows(task) == orc.export()
+
+
+def test_manager_exact_group(gpu, oracle):
+    from go2netspectra_amd import HeaderBatch, Manager, parse_config
+    cfg = parse_config("""
+aggregator:
+  types: ["exact"]
+  exact:
+    tasks:
+      - name: "per_five_tuple"
+        key_fields: ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"]
+        num_shards: 128
+""")
+    rng = np.random.default_rng(9)
+    t = random_tuples(rng, 20_000, 500)
+    hdr = frames_from_tuples(t)
+    ts = np.arange(20_000, dtype=np.int64)
+    mgr = Manager(cfg)
+    mgr.start()
+    mgr.process(HeaderBatch(hdr, t["length"], ts))
+    snaps = mgr.stop()
+    orc = oracle.Exact(FIVE)
+    orc.insert_hdr64(hdr, t["length"], ts)
+    got = {k: (f.StartTime, f.EndTime, f.PacketCount, f.ByteCount)
+           for s in snaps["per_five_tuple"].Shards for k, f in s.Flows.items()}
+    assert got == orc.export()
+    task = mgr.tasks()[0]
+    msg = task.alerter_msg([{"name": "r", "task_name": "per_five_tuple", "metric": "total_packets",
+                             "operator": ">", "threshold": 100}])
+    assert "Observed Value:</b> <code>20000 packets" in msg

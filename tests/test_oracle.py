@@ -150,3 +150,48 @@ def test_det_log_c_python_and_accuracy(oracle):
         c = oracle.lib().or_det_log1m(float(p))
         assert c == pyref.det_log1m(float(p))
         assert abs(c - math.log1p(-p)) <= 1e-12 * abs(math.log1p(-p))
+
+
+def _ipv6_zero_runs(rng, n):
+    """IPv6 slots with random runs of zero groups (RFC 5952 '::' selection cases)."""
+    out = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    for i in range(n):
+        g = rng.integers(0, 8)
+        ln = rng.integers(0, 9 - g)
+        out[i, 2 * g:2 * (g + ln)] = 0
+        if rng.random() < 0.2:
+            out[i, :10] = 0
+            out[i, 10:12] = 0xFF  # IPv4-mapped: prints dotted
+        if rng.random() < 0.1:
+            out[i, 2:4] = 0
+    return out
+
+
+def test_exact_key_strings_c_vs_python(oracle):
+    """Go key strings (net.IP.String + strings.Join) from the C exact oracle equal the
+    host's rebuild from canonical bytes (go2netspectra_amd.exact.key_string)."""
+    from go2netspectra_amd.exact import key_string
+    rng = np.random.default_rng(5)
+    n = 3000
+    src = _ipv6_zero_runs(rng, n)
+    dst = _ipv6_zero_runs(rng, n)
+    v4 = rng.random(n) < 0.3
+    src[v4, 4:] = 0
+    dst[v4, 4:] = 0
+    sport = rng.integers(0, 65536, n).astype(np.uint16)
+    dport = rng.integers(0, 65536, n).astype(np.uint16)
+    proto = rng.integers(0, 256, n).astype(np.uint8)
+    ipver = np.where(v4, 4, 6).astype(np.uint8)
+    fields = ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"]
+    ex = oracle.Exact(fields)
+    ex.insert_tuples(src, dst, sport, dport, proto, ipver, np.ones(n, np.uint32), np.arange(n))
+    got = set(ex.export())
+    want = set()
+    for i in range(n):
+        s16, d16 = bytes(src[i]), bytes(dst[i])
+        if v4[i]:  # To16 of a 4-byte net.IP
+            s16 = bytes(10) + b"\xff\xff" + s16[:4]
+            d16 = bytes(10) + b"\xff\xff" + d16[:4]
+        key = s16 + d16 + int(sport[i]).to_bytes(2, "big") + int(dport[i]).to_bytes(2, "big") + bytes([proto[i]])
+        want.add(key_string(key, fields)[0])
+    assert got == want
