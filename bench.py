@@ -174,6 +174,84 @@ def bench_superspread(args, torch, dist, world, rank, local):
         dist.destroy_process_group()
 
 
+def cpu_baseline_exact(hdr_dev, wl_dev, ts_dev, seconds: float = 10.0):
+    from oracle import oracle as orc
+    n = min(int(wl_dev.shape[0]), 4_000_000)
+    hdr = hdr_dev[:n].cpu().numpy()
+    wl = wl_dev[:n].cpu().numpy().view(np.uint32)
+    ts = ts_dev[:n].cpu().numpy()
+    ex = orc.Exact(FIELDS)
+    chunk, done, t0 = 250_000, 0, time.perf_counter()
+    while done < n and time.perf_counter() - t0 < seconds:
+        m = min(chunk, n - done)
+        ex.insert_hdr64(hdr[done:done + m], wl[done:done + m], ts[done:done + m])
+        done += m
+    rate = done / (time.perf_counter() - t0) / 1e6
+    return {"value": round(rate, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port",
+            "sample": f"first {done:,} packets; sequential C restatement of exact/task.go (parse, Go key "
+                      f"string, hash map), 1 thread"}
+
+
+def bench_exact(args, torch, dist, world, rank, local):
+    """Exact aggregator (per 5-tuple) over 100M device-resident headers per step."""
+    from go2netspectra_amd import ExactTask, HeaderBatch, SyntheticTraffic
+    n = args.packets
+    syn = SyntheticTraffic(shard=rank, nshards=world, device=local)
+    hdr, wl = syn.generate(n)
+    ts = torch.arange(n, dtype=torch.int64, device=f"cuda:{local}") * 100 + 1_700_000_000_000_000_000
+    task = ExactTask("per_five_tuple", FIELDS, 128, device=local, max_flows=1 << 21,
+                     batch_packets=args.batch or n)
+    batch = HeaderBatch(hdr, wl, ts)
+    for _ in range(args.warmup):
+        task.process_packets(batch)
+        task.flush()
+    task.agg.set_timing(True)
+    task.agg.stage_times(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        task.process_packets(batch)
+    task.flush()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    stages = task.agg.stage_times()
+    kern = {k: v for k, v in stages.items() if k in ("extract", "resolve", "aggregate", "timestamps")}
+    dom = max(kern, key=lambda k: kern[k][0])
+    dom_ms, dom_launches = kern[dom]
+    avg_ms = dom_ms / max(dom_launches, 1)
+    bpp = {"extract": BYTES_PER_PKT, "aggregate": 8, "timestamps": 12, "resolve": BYTES_PER_PKT}[dom]
+    achieved = bpp * (n * args.steps / max(dom_launches, 1)) / (avg_ms * 1e-3) / 1e9
+    line = {
+        "metric": "Mpackets/s exact per-5-tuple aggregation (device-resident)",
+        "value": round(n * args.steps * world / elapsed / 1e6, 2), "unit": "Mpackets/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (Zipf 1.1 over 2^20 5-tuples, on-device generator, ts = 100 ns apart)",
+        "config": {"workload": "exact aggregator, key = 5-tuple, 100M headers in HBM per GPU, exact "
+                               "per-flow packets/bytes/start/end", "packets_per_step_per_gpu": n},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_per_packet": bpp, "kernel_avg_ms": round(avg_ms, 4)},
+        "stage_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()},
+        "engine_counters": task.agg.counters(),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_exact(hdr, wl, ts)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -184,8 +262,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--width", type=int, default=WIDTH, help="Count-Min width (2^24 = configs[4] geometry)")
     ap.add_argument("--depth", type=int, default=DEPTH, help="Count-Min depth (8 = configs[4] geometry)")
-    ap.add_argument("--sketch", choices=["countmin", "superspread"], default="countmin",
-                    help="superspread = configs[2] (not the headline metric)")
+    ap.add_argument("--sketch", choices=["countmin", "superspread", "exact"], default="countmin",
+                    help="superspread = configs[2]; exact = the exact aggregator (neither is the headline metric)")
     ap.add_argument("--host-input", action="store_true",
                     help="time inserts from host memory (PCIe-inclusive rate, for DESIGN.md)")
     args = ap.parse_args()
@@ -206,6 +284,8 @@ def main():
 
     if args.sketch == "superspread":
         return bench_superspread(args, torch, dist, world, rank, local)
+    if args.sketch == "exact":
+        return bench_exact(args, torch, dist, world, rank, local)
     n = args.packets
     syn = SyntheticTraffic(shard=rank, nshards=world, device=local)
     hdr, wl = syn.generate(n)

@@ -32,7 +32,7 @@ EXPORTED = [
     "gns_ex_create", "gns_ex_destroy", "gns_ex_insert_tuples", "gns_ex_insert_headers", "gns_ex_flush",
     "gns_ex_query", "gns_ex_snapshot", "gns_ex_reset", "gns_ex_counters", "gns_ex_set_timing",
     "gns_ex_stage_times",
-    "gns_pack_pcap", "gns_pack_pcap_ts", "gns_last_error", "gns_version",
+    "gns_thrift_decode", "gns_pack_pcap", "gns_pack_pcap_ts", "gns_last_error", "gns_version",
 ]
 
 
@@ -137,6 +137,7 @@ def load() -> ct.CDLL:
         "gns_ex_snapshot": ([vp, vp, vp, vp, vp, vp, vp], i32), "gns_ex_reset": ([vp], i32),
         "gns_ex_counters": ([vp, vp], i32), "gns_ex_set_timing": ([vp, i32], i32),
         "gns_ex_stage_times": ([vp, vp, vp, i32], i32),
+        "gns_thrift_decode": ([vp, u64, vp, u64, vp, vp, vp, vp, i32, i32], i32),
         "gns_pack_pcap": ([ct.c_char_p, vp, vp, u64, vp], ct.c_int64),
         "gns_pack_pcap_ts": ([ct.c_char_p, vp, vp, vp, u64, vp], ct.c_int64),
         "gns_last_error": ([], ct.c_char_p), "gns_version": ([], ct.c_char_p),

@@ -159,7 +159,8 @@ __device__ __forceinline__ int parse_l3(const uint32_t (&w)[16], uint32_t type, 
 }
 
 // 64-byte record -> canonical tuple words (bytes 0..36 = src16, dst16, sport,
-// dport BE, proto; byte 39 = IP version 4/6).  Returns PARSE_*.
+// dport BE, proto; byte 39 / 38 = IP version of the source / destination:
+// 4 or 6, 0 for a net.IP of another length).  Returns PARSE_*.
 __device__ __forceinline__ int parse_record(const uint32_t (&w)[16], uint32_t wirelen,
                                             uint32_t (&tw)[10]) {
 #pragma unroll
@@ -170,7 +171,10 @@ __device__ __forceinline__ int parse_record(const uint32_t (&w)[16], uint32_t wi
         tw[0] = w[4]; tw[1] = w[5]; tw[2] = w[6];  tw[3] = w[7];
         tw[4] = w[8]; tw[5] = w[9]; tw[6] = w[10]; tw[7] = w[11];
         set_ports(tw, rec_be16<48>(w), rec_be16<50>(w), rec_byte<52>(w));
-        tw[9] |= rec_byte<15>(w) << 24;  // IP version (byte 39, outside every key plan)
+        // IP versions: byte 39 = source, byte 38 = destination (record byte 53; 0 -> same
+        // as the source).  Bytes 37..39 lie outside every key plan.
+        const uint32_t sv = rec_byte<15>(w), dv0 = rec_byte<53>(w);
+        tw[9] |= sv << 24 | (dv0 ? dv0 : sv) << 16;
         return PARSE_OK;
     }
     // gopacket Dot1Q: up to two tags (4 bytes = one word each) before the ethertype
@@ -193,7 +197,8 @@ __device__ __forceinline__ int parse_record(const uint32_t (&w)[16], uint32_t wi
         ws[i] = nv == 0 ? w[i] : (nv == 1 ? a1 : a2);
     }
     const int st = parse_l3(ws, type, wirelen, nv, tw);
-    tw[9] |= (type == 0x86DDu ? 6u : 4u) << 24;  // IP version (byte 39, outside every key plan)
+    const uint32_t ver = type == 0x86DDu ? 6u : 4u;  // IP version of both addresses (bytes 38, 39)
+    tw[9] |= ver << 24 | ver << 16;
     return st;
 }
 

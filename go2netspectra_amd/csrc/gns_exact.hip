@@ -41,11 +41,9 @@ struct ExIn {
 
 // IPv4 (4-byte net.IP, left-aligned in its slot) -> ::ffff:a.b.c.d, the form
 // in which it compares equal to the same address arriving IPv4-mapped.
-__device__ __forceinline__ void to16(uint32_t (&tw)[10], uint32_t ver) {
-    if (ver == 4u) {
-        tw[3] = tw[0]; tw[0] = 0u; tw[1] = 0u; tw[2] = 0xFFFF0000u;
-        tw[7] = tw[4]; tw[4] = 0u; tw[5] = 0u; tw[6] = 0xFFFF0000u;
-    }
+__device__ __forceinline__ void to16(uint32_t (&tw)[10], uint32_t sver, uint32_t dver) {
+    if (sver == 4u) { tw[3] = tw[0]; tw[0] = 0u; tw[1] = 0u; tw[2] = 0xFFFF0000u; }
+    if (dver == 4u) { tw[7] = tw[4]; tw[4] = 0u; tw[5] = 0u; tw[6] = 0xFFFF0000u; }
 }
 
 template <int KIND, int MODE>
@@ -54,10 +52,13 @@ __device__ __forceinline__ int ex_key(const ExIn &x, uint32_t K, const uint8_t *
     uint32_t tw[10];
     const int st = load_tuple<KIND>(x.in, p, tw);
     if (st != PARSE_OK) return st;
-    uint32_t ver;
-    if constexpr (KIND == IN_HDR) ver = tw[9] >> 24;
-    else ver = x.ipver ? x.ipver[p] : 4u;
-    to16(tw, ver);
+    uint32_t sv, dv;
+    if constexpr (KIND == IN_HDR) { sv = tw[9] >> 24; dv = (tw[9] >> 16) & 0xFFu; }
+    else { sv = dv = x.ipver ? x.ipver[p] : 4u; }
+    // a net.IP of neither 4 nor 16 bytes prints as "?<hex>" / "<nil>" (net/ip.go):
+    // outside the canonical form, counted as unsupported
+    if (sv == 0u || dv == 0u) return PARSE_UNSUPPORTED;
+    to16(tw, sv, dv);
     tw[9] &= 0xFFu;
     make_key_m<MODE, GNS_KWMAX>(K, s_src, tw, kw);
     return PARSE_OK;

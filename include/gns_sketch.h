@@ -211,6 +211,18 @@ int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirelen, uint64_
 int64_t gns_pack_pcap_ts(const char *path, uint8_t *hdr, uint32_t *wirelen, int64_t *ts_ns, uint64_t cap,
                          uint64_t *total);
 
+/* Thrift live path: decode n binary-protocol PacketInfo messages
+ * (api/thrift/v1/traffic.thrift; packetcodec.go:97-108 UnmarshalPacketInfo over
+ * apache/thrift v0.22.0) laid out back to back in buf, message i =
+ * buf[offsets[i], offsets[i+1]), into DEVICE buffers hdr_out[n*64] (pre-parsed
+ * 0x88B5 records), wirelen_out[n] = uint32(Length), ts_out[n] =
+ * TimestampUnixNano.  A message the reference rejects becomes a record the
+ * parser drops (*n_bad counts them).  buf/offsets live in `where`.  The records
+ * feed gns_{cm,ss,ex}_insert_headers unchanged. */
+int gns_thrift_decode(const uint8_t *buf, uint64_t buf_bytes, const uint64_t *offsets, uint64_t n,
+                      uint8_t *hdr_out, uint32_t *wirelen_out, int64_t *ts_out, uint64_t *n_bad,
+                      gns_mem where, int device);
+
 /* ------------------------------------------------------------------ */
 /* Exact aggregator (internal/engine/impl/exact/task.go)               */
 /* ------------------------------------------------------------------ */

@@ -74,6 +74,7 @@ int or_parse_hdr64_len(const uint8_t *r, uint32_t wirelen, or_tuple *t) {
     if (type == 0x88B5) { /* pre-parsed record written by the host packer */
         if (r[14] != 1) return OR_PARSE_UNSUPPORTED;
         t->ipver = r[15];
+        t->dst_ipver = r[53] ? r[53] : r[15];
         memcpy(t->src, r + 16, 16);
         memcpy(t->dst, r + 32, 16);
         t->sport = be16(r + 48);
@@ -96,6 +97,7 @@ int or_parse_hdr64_len(const uint8_t *r, uint32_t wirelen, or_tuple *t) {
         if (ihl > 5) return OR_PARSE_UNSUPPORTED; /* options: host packer */
         if (tot < 20 || l2len < 20) return OR_PARSE_DROP;
         t->ipver = 4;
+        t->dst_ipver = 4;
         t->proto = ip[9];                        /* parser.go:42 */
         memcpy(t->src, ip + 12, 4);               /* parser.go:40-41; task.go:281-286 */
         memcpy(t->dst, ip + 16, 4);
@@ -134,6 +136,7 @@ int or_parse_hdr64_len(const uint8_t *r, uint32_t wirelen, or_tuple *t) {
         uint32_t nh = ip[6];
         if (plen == 0) return OR_PARSE_UNSUPPORTED; /* jumbogram / TSO */
         t->ipver = 6;
+        t->dst_ipver = 6;
         t->proto = (uint8_t)nh; /* parser.go:47: first NextHeader */
         memcpy(t->src, ip + 8, 16);
         memcpy(t->dst, ip + 24, 16);

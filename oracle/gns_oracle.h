@@ -43,7 +43,8 @@ typedef struct or_tuple {
     uint8_t dst[16];
     uint16_t sport, dport;
     uint8_t proto;
-    uint8_t ipver; /* 4 or 6; informational */
+    uint8_t ipver;     /* source net.IP: 4 (4 bytes) or 6 (16 bytes); 0 other (Thrift path) */
+    uint8_t dst_ipver; /* destination, same coding */
 } or_tuple;
 
 enum { OR_PARSE_OK = 0, OR_PARSE_DROP = 1, OR_PARSE_UNSUPPORTED = 2 };
@@ -135,6 +136,13 @@ uint64_t or_ex_count(const or_ex *ex);
 uint64_t or_ex_export(const or_ex *ex, char *keys_out, uint64_t keys_cap, int64_t *start, int64_t *end,
                       uint64_t *pkts, uint64_t *bytes);
 int or_parse_hdr64_len(const uint8_t *rec, uint32_t wirelen, or_tuple *out);
+
+/* ---- Thrift PacketInfo decode, packetcodec.go:97-108 (gns_oracle_thrift.c) ---- */
+int or_thrift_decode_one(const uint8_t *msg, uint64_t len, or_tuple *t, uint8_t *dst_ver, int64_t *length,
+                         int64_t *ts);
+uint64_t or_thrift_decode(const uint8_t *buf, const uint64_t *offsets, uint64_t n, uint8_t *ok, uint8_t *src16,
+                          uint8_t *dst16, uint16_t *sport, uint16_t *dport, uint8_t *proto, uint8_t *sver,
+                          uint8_t *dver, int64_t *length, int64_t *ts);
 
 #ifdef __cplusplus
 }

@@ -129,7 +129,7 @@ static void ex_key_tuple(const or_ex *ex, const or_tuple *t, char *out) {
         if (i) out[o++] = '-';
         switch (ex->fields[i]) {
         case OR_F_SRCIP: o += go_ip_string(t->src, t->ipver == 4 ? 4 : 16, out + o); break;
-        case OR_F_DSTIP: o += go_ip_string(t->dst, t->ipver == 4 ? 4 : 16, out + o); break;
+        case OR_F_DSTIP: o += go_ip_string(t->dst, t->dst_ipver == 4 ? 4 : 16, out + o); break;
         case OR_F_SRCPORT: o += sprintf(out + o, "%u", t->sport); break;
         case OR_F_DSTPORT: o += sprintf(out + o, "%u", t->dport); break;
         case OR_F_PROTO: o += sprintf(out + o, "%u", t->proto); break;
@@ -159,7 +159,7 @@ void or_ex_insert_tuples(or_ex *ex, const uint8_t *src16, const uint8_t *dst16, 
         or_tuple t;
         memcpy(t.src, src16 + 16 * p, 16);
         memcpy(t.dst, dst16 + 16 * p, 16);
-        t.sport = sport[p]; t.dport = dport[p]; t.proto = proto[p]; t.ipver = ipver[p];
+        t.sport = sport[p]; t.dport = dport[p]; t.proto = proto[p]; t.ipver = t.dst_ipver = ipver[p];
         or_ex_insert(ex, &t, ts[p], length[p]);
     }
 }
@@ -171,6 +171,7 @@ uint64_t or_ex_insert_hdr64(or_ex *ex, const uint8_t *hdr, const uint32_t *wirel
     for (uint64_t p = 0; p < n; p++) {
         or_tuple t;
         if (or_parse_hdr64_len(hdr + 64 * p, wirelen[p], &t) != OR_PARSE_OK) continue;
+        if (t.ipver == 0 || t.dst_ipver == 0) continue; /* "?hex" keys: outside this build's scope */
         or_ex_insert(ex, &t, ts[p], wirelen[p]);
         done++;
     }

@@ -95,6 +95,8 @@ def lib():
     L.or_ex_count.argtypes = [ct.c_void_p]
     L.or_ex_export.restype = ct.c_uint64
     L.or_ex_export.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_uint64] + [ct.c_void_p] * 4
+    L.or_thrift_decode.restype = ct.c_uint64
+    L.or_thrift_decode.argtypes = [ct.c_void_p] * 2 + [ct.c_uint64] + [ct.c_void_p] * 10
     L.or_ss_uniform.restype = ct.c_double
     L.or_ss_uniform.argtypes = [ct.c_uint64, ct.c_uint64, ct.c_uint32, ct.c_uint32]
     L.or_go_pow.restype = ct.c_double
@@ -114,7 +116,7 @@ def mm3(data: bytes, seed: int) -> int:
 
 class TupleRec(ct.Structure):
     _fields_ = [("src", ct.c_uint8 * 16), ("dst", ct.c_uint8 * 16), ("sport", ct.c_uint16),
-                ("dport", ct.c_uint16), ("proto", ct.c_uint8), ("ipver", ct.c_uint8)]
+                ("dport", ct.c_uint16), ("proto", ct.c_uint8), ("ipver", ct.c_uint8), ("dst_ipver", ct.c_uint8)]
 
 
 def parse_hdr64(rec: bytes, wirelen: int):
@@ -294,3 +296,18 @@ class Exact:
         self.L.or_ex_export(self.h, keys, cap, _p(st), _p(en), _p(pk), _p(by))
         names = keys.value.decode().split("\n")[:n]
         return {k: (int(st[i]), int(en[i]), int(pk[i]), int(by[i])) for i, k in enumerate(names)}
+
+
+def thrift_decode(buf: bytes, offsets: np.ndarray) -> dict:
+    """Sequential restatement of UnmarshalPacketInfo over a message batch."""
+    L = lib()
+    n = len(offsets) - 1
+    b = np.frombuffer(bytes(buf) or b"\0", np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    out = dict(ok=np.zeros(n, np.uint8), src16=np.zeros((n, 16), np.uint8), dst16=np.zeros((n, 16), np.uint8),
+               sport=np.zeros(n, np.uint16), dport=np.zeros(n, np.uint16), proto=np.zeros(n, np.uint8),
+               sver=np.zeros(n, np.uint8), dver=np.zeros(n, np.uint8), length=np.zeros(n, np.int64),
+               ts=np.zeros(n, np.int64))
+    keys = ["ok", "src16", "dst16", "sport", "dport", "proto", "sver", "dver", "length", "ts"]
+    L.or_thrift_decode(_p(b), _p(offsets), n, *[_p(out[k]) for k in keys])
+    return out

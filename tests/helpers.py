@@ -95,3 +95,217 @@ def frames_from_tuples(t, rng=None, vlan_frac=0.0):
                                        t["proto"][i], int(t["length"][i]), v6=bool(t["v6"][i]), vlans=vl),
                                np.uint8)
     return hdr
+
+
+# ---------------------------------------------------------------------------
+# Thrift PacketInfo messages (traffic.thrift) for the live-path tests: a third,
+# pure-Python restatement of the decode (generated readers + lib/go Skip) and a
+# generator of valid, reordered, padded and broken messages.
+# ---------------------------------------------------------------------------
+def py_thrift_decode(msg: bytes):
+    """-> None if rejected, else (ts, src bytes, dst bytes, sport, dport, proto, length)."""
+    class Bad(Exception):
+        pass
+
+    pos = [0]
+
+    def take(k):
+        if k < 0 or len(msg) - pos[0] < k:
+            raise Bad()
+        b = msg[pos[0]:pos[0] + k]
+        pos[0] += k
+        return b
+
+    def i8():
+        return take(1)[0]
+
+    def i16():
+        return struct.unpack(">H", take(2))[0]
+
+    def i32():
+        return struct.unpack(">i", take(4))[0]
+
+    def i64():
+        return struct.unpack(">q", take(8))[0]
+
+    def binary():
+        n = i32()
+        if n < 0:
+            raise Bad()
+        return take(n)
+
+    def skip(t, depth):
+        if depth <= 0:
+            raise Bad()
+        if t in (2, 3):
+            take(1)
+        elif t == 6:
+            take(2)
+        elif t == 8:
+            take(4)
+        elif t in (4, 10):
+            take(8)
+        elif t == 16:
+            take(16)
+        elif t == 11:
+            binary()
+        elif t == 12:
+            while True:
+                ft = i8()
+                if ft == 0:
+                    return
+                i16()
+                skip(ft, depth - 1)
+        elif t == 13:
+            kt, vt, n = i8(), i8(), i32()
+            if n < 0:
+                raise Bad()
+            for _ in range(n):
+                skip(kt, depth - 1)
+                skip(vt, depth - 1)
+        elif t in (14, 15):
+            et, n = i8(), i32()
+            if n < 0:
+                raise Bad()
+            for _ in range(n):
+                skip(et, depth - 1)
+        else:
+            raise Bad()
+
+    def five_tuple():
+        got, v = set(), {}
+        while True:
+            t = i8()
+            if t == 0:
+                break
+            fid = i16()
+            if fid in (1, 2) and t == 11:
+                v[fid] = binary()
+            elif fid in (3, 4, 5) and t == 8:
+                v[fid] = i32()
+            else:
+                skip(t, 64)
+                continue
+            got.add(fid)
+        if got != {1, 2, 3, 4, 5}:
+            raise Bad()
+        return v
+
+    try:
+        top, ft = {}, None
+        while True:
+            t = i8()
+            if t == 0:
+                break
+            fid = i16()
+            if fid in (1, 3) and t == 10:
+                top[fid] = i64()
+            elif fid == 2 and t == 12:
+                ft = five_tuple()
+                top[2] = True
+            else:
+                skip(t, 64)
+        if set(top) != {1, 2, 3}:
+            return None
+        return (top[1], ft[1], ft[2], ft[3] & 0xFFFF, ft[4] & 0xFFFF, ft[5] & 0xFF, top[3])
+    except Bad:
+        return None
+
+
+def _junk_value(rng, depth=0):
+    """(wire type, encoded value) of a random skippable value."""
+    t = int(rng.choice([2, 3, 4, 6, 8, 10, 11, 12, 13, 14, 15, 16]))
+    if depth > 3 and t in (12, 13, 14, 15):
+        t = 8
+    if t in (2, 3):
+        return t, bytes([int(rng.integers(0, 256))])
+    if t == 6:
+        return t, struct.pack(">h", int(rng.integers(-30000, 30000)))
+    if t == 8:
+        return t, struct.pack(">i", int(rng.integers(-2**31, 2**31)))
+    if t in (4, 10):
+        return t, bytes(rng.integers(0, 256, 8, dtype=np.uint8))
+    if t == 16:
+        return t, bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+    if t == 11:
+        b = bytes(rng.integers(0, 256, int(rng.integers(0, 12)), dtype=np.uint8))
+        return t, struct.pack(">i", len(b)) + b
+    if t == 12:
+        body = b""
+        for _ in range(int(rng.integers(0, 3))):
+            ft, fv = _junk_value(rng, depth + 1)
+            body += bytes([ft]) + struct.pack(">h", int(rng.integers(1, 100))) + fv
+        return t, body + b"\x00"
+    if t == 13:
+        n = int(rng.integers(0, 3))
+        kt, _ = _junk_value(rng, depth + 1)
+        vt, _ = _junk_value(rng, depth + 1)
+        body = b""
+        for _ in range(n):
+            body += _junk_of(rng, kt, depth + 1) + _junk_of(rng, vt, depth + 1)
+        return t, bytes([kt, vt]) + struct.pack(">i", n) + body
+    n = int(rng.integers(0, 3))
+    et, _ = _junk_value(rng, depth + 1)
+    return t, bytes([et]) + struct.pack(">i", n) + b"".join(_junk_of(rng, et, depth + 1) for _ in range(n))
+
+
+def _junk_of(rng, t, depth):
+    for _ in range(100):
+        tt, v = _junk_value(rng, depth)
+        if tt == t:
+            return v
+    return {2: b"\x01", 3: b"\x01", 6: b"\x00\x01", 8: b"\x00" * 4, 4: b"\x00" * 8, 10: b"\x00" * 8,
+            16: b"\x00" * 16, 11: b"\x00" * 4, 12: b"\x00", 13: b"\x08\x08\x00\x00\x00\x00",
+            14: b"\x08\x00\x00\x00\x00", 15: b"\x08\x00\x00\x00\x00"}[t]
+
+
+def thrift_messages(rng, n, nflows=500, bad_frac=0.1, v6_frac=0.3):
+    """Valid PacketInfo messages (canonical, reordered, padded with unknown
+    fields, duplicated fields, odd IP lengths) and broken ones (truncated,
+    missing fields, wrong types, negative sizes, junk)."""
+    from go2netspectra_amd.thrift import marshal_packet_info
+    flows = []
+    for _ in range(nflows):
+        v6 = rng.random() < v6_frac
+        ln = 16 if v6 else 4
+        if rng.random() < 0.02:
+            ln = int(rng.integers(0, 20))
+        s = bytes(rng.integers(0, 256, ln, dtype=np.uint8))
+        d = bytes(rng.integers(0, 256, 16 if v6 else 4, dtype=np.uint8))
+        flows.append((s, d, int(rng.integers(-70000, 70000)), int(rng.integers(0, 65536)), int(rng.integers(0, 300))))
+    msgs = []
+    for i in range(n):
+        s, d, sp, dp, pr = flows[int(zipf_index(rng, 1, nflows)[0])]
+        ts = int(rng.integers(-2**62, 2**62))
+        ln = int(rng.integers(0, 2**33)) if rng.random() < 0.05 else int(rng.integers(40, 1600))
+        m = marshal_packet_info(ts, s, d, sp, dp, pr, ln)
+        u = rng.random()
+        if u < 0.15:  # reorder top-level fields and add unknown ones
+            f1 = b"\x0a\x00\x01" + struct.pack(">q", ts)
+            f3 = b"\x0a\x00\x03" + struct.pack(">q", ln)
+            f2 = m[11:-(11 + 1)]
+            parts = [f1, f2, f3]
+            rng.shuffle(parts)
+            jt, jv = _junk_value(rng)
+            parts.insert(int(rng.integers(0, 4)), bytes([jt]) + struct.pack(">h", int(rng.integers(4, 50))) + jv)
+            m = b"".join(parts) + b"\x00"
+        elif u < 0.2:  # known id with the wrong type (skipped), then the real field
+            jt, jv = _junk_value(rng)
+            if jt != 10:
+                m = bytes([jt]) + b"\x00\x01" + jv + m
+        elif u < 0.23:  # trailing bytes after STOP are ignored
+            m = m + bytes(rng.integers(0, 256, 5, dtype=np.uint8))
+        if rng.random() < bad_frac:
+            kind = int(rng.integers(0, 5))
+            if kind == 0:
+                m = m[: int(rng.integers(0, len(m)))]
+            elif kind == 1:
+                m = m[3 + 8:]  # drop the timestamp field
+            elif kind == 2:
+                m = b"\x0b\x00\x09" + struct.pack(">i", -1) + m  # negative binary size
+            elif kind == 3:
+                m = b"\x11\x00\x07" + m  # unknown wire type 17
+            else:
+                m = bytes(rng.integers(0, 256, int(rng.integers(1, 80)), dtype=np.uint8))
+        msgs.append(m)
+    return msgs

@@ -195,3 +195,49 @@ def test_exact_key_strings_c_vs_python(oracle):
         key = s16 + d16 + int(sport[i]).to_bytes(2, "big") + int(dport[i]).to_bytes(2, "big") + bytes([proto[i]])
         want.add(key_string(key, fields)[0])
     assert got == want
+
+
+def test_thrift_golden_vectors(oracle):
+    """packetcodec_test.go: the legacy protobuf payload (:123) is rejected; the
+    round-trip values (:13-98, net.ParseIP -> 16-byte forms) decode back."""
+    from go2netspectra_amd.thrift import marshal_packet_info, pack_messages
+    import ipaddress
+    legacy = bytes.fromhex("0a060880e2cfaa0612140a04c000020a1204c633641418bb0320fb412806188001")
+    m1 = marshal_packet_info(1700000000 * 10**9 + 123, bytes(10) + b"\xff\xff" + ipaddress.ip_address("192.0.2.10").packed,
+                             ipaddress.ip_address("2001:db8::1").packed, 443, 8080, 17, 128)
+    m2 = marshal_packet_info(1700000010 * 10**9 + 456, bytes(10) + b"\xff\xff" + bytes([198, 51, 100, 1]),
+                             ipaddress.ip_address("2001:db8::2").packed, 53000, 8443, 6, 256)
+    buf, offs = pack_messages([legacy, m1, m2, b"", b"\x00"])
+    out = oracle.thrift_decode(buf, offs)
+    assert out["ok"].tolist() == [0, 1, 1, 0, 0]  # b"" (EOF) and a bare STOP (missing fields) fail
+    assert bytes(out["dst16"][1]) == ipaddress.ip_address("2001:db8::1").packed
+    assert out["sport"][1] == 443 and out["dport"][1] == 8080 and out["proto"][1] == 17
+    assert out["length"][1] == 128 and out["ts"][1] == 1700000000 * 10**9 + 123
+    assert out["sver"][1] == 6 and out["dver"][2] == 6
+    assert out["sport"][2] == 53000 and out["length"][2] == 256
+    # the canonical 4-byte-IP message is 70 bytes (SURVEY §8 f3)
+    assert len(marshal_packet_info(0, b"\1\2\3\4", b"\5\6\7\10", 1, 2, 6, 60)) == 70
+
+
+def test_thrift_decode_c_vs_python(oracle):
+    """C restatement (recursive Skip) == pure-Python restatement on fuzzed messages."""
+    from go2netspectra_amd.thrift import pack_messages
+    from helpers import py_thrift_decode, thrift_messages
+    rng = np.random.default_rng(11)
+    msgs = thrift_messages(rng, 4000, bad_frac=0.2)
+    buf, offs = pack_messages(msgs)
+    out = oracle.thrift_decode(buf, offs)
+    nok = 0
+    for i, m in enumerate(msgs):
+        want = py_thrift_decode(m)
+        assert bool(out["ok"][i]) == (want is not None), (i, m.hex())
+        if want is None:
+            continue
+        nok += 1
+        ts, s, d, sp, dp, pr, ln = want
+        assert out["ts"][i] == ts and out["length"][i] == ln
+        assert bytes(out["src16"][i]) == (s[:16] + bytes(16))[:16]
+        assert bytes(out["dst16"][i]) == (d[:16] + bytes(16))[:16]
+        assert (out["sport"][i], out["dport"][i], out["proto"][i]) == (sp, dp, pr)
+        assert out["sver"][i] == {4: 4, 16: 6}.get(len(s), 0)
+    assert 2500 < nok < 3900
