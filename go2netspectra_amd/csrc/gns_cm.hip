@@ -599,6 +599,77 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
+// ---------------------------------------------------------------------------
+// Exact wave-parallel sequence for ONE bucket (count_min.go:180-235): 64
+// updates per step; a prefix sum gives the counter before every update, the
+// first update that would leave the linear regime (an "event": fingerprint
+// take-over, counter wrap) is applied explicitly and the scan restarts after
+// it.  Steps per 64 updates = events + 1.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t t = __shfl_up(v, o, 64);
+        if (lane >= (uint32_t)o) v += t;
+    }
+    return v;
+}
+
+// count half; F, C wave-uniform
+__device__ __forceinline__ void count_seq64(bool valid, uint32_t k, uint32_t &F, uint32_t &C) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t start = 0;
+    for (;;) {
+        const bool act = valid && lane >= start;
+        const bool own = k == F;
+        const int64_t dlt = act ? (own ? 1 : -1) : 0;
+        const int64_t P = wave_incl_scan64(dlt);
+        const int64_t Cb = (int64_t)C + P - dlt;
+        const bool ev = act && ((!own && Cb <= 1) || (own && Cb >= 0xFFFFFFFFll));
+        const uint64_t m = __ballot(ev);
+        if (!m) {
+            C = (uint32_t)((int64_t)C + __shfl(P, 63, 64));
+            return;
+        }
+        const uint32_t t = (uint32_t)__ffsll((long long)m) - 1;
+        const int64_t cbt = __shfl(Cb, t, 64);
+        const uint32_t kt = __shfl(k, t, 64);
+        const bool ownt = kt == F;
+        if (ownt) { C = 0; }                        // C+1 wraps to 0 (u32), F kept
+        else if (cbt == 0) { C = 1; F = kt; }       // :214-218
+        else { C = 0; F = kt; }                     // :226-231 reaches 0, F := flow
+        start = t + 1;
+        if (start >= 64) return;
+    }
+}
+
+// size half; F, S wave-uniform
+__device__ __forceinline__ void size_seq64(bool valid, uint32_t k, uint32_t s, uint32_t &F, uint32_t &S) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t start = 0;
+    for (;;) {
+        const bool act = valid && lane >= start;
+        const bool own = k == F;
+        const int64_t dlt = act ? (own ? (int64_t)s : -(int64_t)s) : 0;
+        const int64_t W = wave_incl_scan64(dlt);
+        const int64_t Sb = (int64_t)S + W - dlt;
+        const bool ev = act && ((!own && (Sb == 0 || (int64_t)s > Sb)) || (own && Sb + (int64_t)s > 0xFFFFFFFFll));
+        const uint64_t m = __ballot(ev);
+        if (!m) {
+            S = (uint32_t)((int64_t)S + __shfl(W, 63, 64));
+            return;
+        }
+        const uint32_t t = (uint32_t)__ffsll((long long)m) - 1;
+        const int64_t sbt = __shfl(Sb, t, 64);
+        const uint32_t kt = __shfl(k, t, 64), st = __shfl(s, t, 64);
+        if (kt == F) { S = (uint32_t)((uint64_t)sbt + st); }   // u32 wrap, F kept
+        else { S = st; F = kt; }                               // :184-188 / :196-200
+        start = t + 1;
+        if (start >= 64) return;
+    }
+}
+
 struct ApplyLds {
     uint32_t sC[kTileMax], sFc[kTileMax], sS[kTileMax], sFs[kTileMax];
     unsigned long long accN[kTileMax];  // n | n_oth_c<<21 | n_oth_s<<42 | force<<63
@@ -790,6 +861,29 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                         rf = (uint32_t)accN[b];
                     }
                 }
+                // a bucket with many updates in this group (a contested bucket that
+                // failed the linear check): wave-parallel sequence, 64 updates per step
+                for (;;) {
+                    const uint64_t pm = __ballot(pending);
+                    if (!pm) break;
+                    const uint32_t lead = (uint32_t)__ffsll((long long)pm) - 1;
+                    const uint32_t b0 = __shfl(b, lead, 64);
+                    const bool mine = pending && b == b0;
+                    const uint64_t m0 = __ballot(mine);
+                    if (__popcll(m0) < 8) break;
+                    const uint32_t rf0 = __shfl(rf, lead, 64);
+                    if (rf0 & 2u) {
+                        uint32_t F = sFs[b0], S = sS[b0];
+                        size_seq64(mine, k, s, F, S);
+                        if (lane == lead) { sS[b0] = S; sFs[b0] = F; }
+                    }
+                    if (rf0 & 1u) {
+                        uint32_t F = sFc[b0], C = sC[b0];
+                        count_seq64(mine, k, F, C);
+                        if (lane == lead) { sC[b0] = C; sFc[b0] = F; }
+                    }
+                    if (mine) pending = false;
+                }
                 while (__ballot(pending)) {
                     if (pending) atomicMax(&own[b], 64u - lane);
                     const bool win = pending && own[b] == 64u - lane;
@@ -913,77 +1007,6 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
         if (tbase >= g.w || sb >= se) continue;
         apply_tile(a, L, a.entries2, sb, se, (uint64_t)r * g.w + tbase, min(1u << g.tile_bits, g.w - tbase));
         __syncthreads();
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Exact wave-parallel sequence for ONE bucket (count_min.go:180-235): 64
-// updates per step; a prefix sum gives the counter before every update, the
-// first update that would leave the linear regime (an "event": fingerprint
-// take-over, counter wrap) is applied explicitly and the scan restarts after
-// it.  Steps per 64 updates = events + 1.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) {
-    const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int64_t t = __shfl_up(v, o, 64);
-        if (lane >= (uint32_t)o) v += t;
-    }
-    return v;
-}
-
-// count half; F, C wave-uniform
-__device__ __forceinline__ void count_seq64(bool valid, uint32_t k, uint32_t &F, uint32_t &C) {
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t start = 0;
-    for (;;) {
-        const bool act = valid && lane >= start;
-        const bool own = k == F;
-        const int64_t dlt = act ? (own ? 1 : -1) : 0;
-        const int64_t P = wave_incl_scan64(dlt);
-        const int64_t Cb = (int64_t)C + P - dlt;
-        const bool ev = act && ((!own && Cb <= 1) || (own && Cb >= 0xFFFFFFFFll));
-        const uint64_t m = __ballot(ev);
-        if (!m) {
-            C = (uint32_t)((int64_t)C + __shfl(P, 63, 64));
-            return;
-        }
-        const uint32_t t = (uint32_t)__ffsll((long long)m) - 1;
-        const int64_t cbt = __shfl(Cb, t, 64);
-        const uint32_t kt = __shfl(k, t, 64);
-        const bool ownt = kt == F;
-        if (ownt) { C = 0; }                        // C+1 wraps to 0 (u32), F kept
-        else if (cbt == 0) { C = 1; F = kt; }       // :214-218
-        else { C = 0; F = kt; }                     // :226-231 reaches 0, F := flow
-        start = t + 1;
-        if (start >= 64) return;
-    }
-}
-
-// size half; F, S wave-uniform
-__device__ __forceinline__ void size_seq64(bool valid, uint32_t k, uint32_t s, uint32_t &F, uint32_t &S) {
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t start = 0;
-    for (;;) {
-        const bool act = valid && lane >= start;
-        const bool own = k == F;
-        const int64_t dlt = act ? (own ? (int64_t)s : -(int64_t)s) : 0;
-        const int64_t W = wave_incl_scan64(dlt);
-        const int64_t Sb = (int64_t)S + W - dlt;
-        const bool ev = act && ((!own && (Sb == 0 || (int64_t)s > Sb)) || (own && Sb + (int64_t)s > 0xFFFFFFFFll));
-        const uint64_t m = __ballot(ev);
-        if (!m) {
-            S = (uint32_t)((int64_t)S + __shfl(W, 63, 64));
-            return;
-        }
-        const uint32_t t = (uint32_t)__ffsll((long long)m) - 1;
-        const int64_t sbt = __shfl(Sb, t, 64);
-        const uint32_t kt = __shfl(k, t, 64), st = __shfl(s, t, 64);
-        if (kt == F) { S = (uint32_t)((uint64_t)sbt + st); }   // u32 wrap, F kept
-        else { S = st; F = kt; }                               // :184-188 / :196-200
-        start = t + 1;
-        if (start >= 64) return;
     }
 }
 
@@ -1601,7 +1624,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         cm->dict_slots = slots;
         cm->D.mask = (uint32_t)(slots - 1);
         cm->D.K = cm->K;
-        cm->D.RW = ((1 + (cm->K + 3) / 4) + 3) & ~3u;
+        cm->D.RW = dict_record_words(cm->K);
         cm->D.seed = 0x2545F491u;
         if ((rc = dalloc_t(&cm->D.rec, slots * cm->D.RW)) != GNS_OK) break;
         // batch buffers

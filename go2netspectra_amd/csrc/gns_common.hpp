@@ -76,6 +76,17 @@ struct ScopedStage {
 // splitmix64 row seeds used when the caller passes none.
 void default_seeds(uint32_t *out, uint32_t n);
 
+// Dictionary record words {tag, key words}: a power of two (4, 8 or 16 words)
+// so that no record straddles a 64-byte line (one line per probe).
+inline uint32_t dict_record_words(uint32_t K) {
+    const uint32_t w = 1 + (K + 3) / 4;
+#ifdef GNS_DICT_PACKED
+    return (w + 3) & ~3u;
+#else
+    return w <= 4 ? 4u : (w <= 8 ? 8u : 16u);
+#endif
+}
+
 inline uint32_t ceil_log2(uint64_t x) {
     uint32_t b = 0;
     while ((1ull << b) < x) b++;

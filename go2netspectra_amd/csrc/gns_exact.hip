@@ -490,7 +490,7 @@ int gns_ex_create(const gns_ex_params *p, gns_ex **out) {
         ex->slots = slots;
         ex->D.mask = (uint32_t)(slots - 1);
         ex->D.K = ex->K;
-        ex->D.RW = ((1 + (ex->K + 3) / 4) + 3) & ~3u;
+        ex->D.RW = dict_record_words(ex->K);
         ex->D.seed = 0x5BD1E995u;
         ex->bmax = p->batch_packets ? p->batch_packets : (16ull << 20);
         ex->bmax = std::min<uint64_t>(((ex->bmax + kXChunk - 1) / kXChunk) * kXChunk, 1ull << 31);

@@ -179,7 +179,7 @@ __device__ __forceinline__ void stage_plan(const KeyPlanN &kp, uint8_t *s_src) {
 struct DictDev {
     uint32_t *rec;     // slots * RW words
     uint32_t mask;     // slots - 1
-    uint32_t RW;       // record words (multiple of 4, <= 12)
+    uint32_t RW;       // record words: 4, 8 or 16 (a record never straddles a 64-byte line)
     uint32_t seed;     // slot hash seed
     uint32_t K;        // key bytes
 };

@@ -675,7 +675,7 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
         ss->dict_slots = slots;
         ss->D.mask = (uint32_t)(slots - 1);
         ss->D.K = g.Kf;
-        ss->D.RW = ((1 + (g.Kf + 3) / 4) + 3) & ~3u;
+        ss->D.RW = dict_record_words(g.Kf);
         ss->D.seed = 0x2545F491u;
         if ((rc = dalloc_t(&ss->D.rec, slots * ss->D.RW)) != GNS_OK) break;
         ss->bmax = p->batch_packets ? p->batch_packets : (8ull << 20);

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs -> per-kernel HBM traffic.
+
+usage: pmc_traffic.py FETCH_CSV WRITE_CSV [out.json]
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC_EA0_RDREQ/WRREQ x 64 B).
+MI355X_MICROARCH.md (HBM section): on gfx950 FETCH_SIZE reports half of the
+bytes of wide coalesced streaming reads, so reads are doubled.  The median
+over each kernel's dispatches is taken (cold-start dispatches excluded by
+the median).  Output keys are bench.py stage names.
+"""
+import collections
+import csv
+import json
+import statistics
+import sys
+
+STAGE = {"k_extract": "extract", "k_resolve": "resolve", "k_scatter": "scatter", "k_apply": "apply",
+         "k_hot_sum": "hot_sum", "k_hot_verify": "hot_verify", "k_scan_down": "scan", "k_synth": "synth"}
+
+
+def load(path):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1].strip()
+        d[name].append(float(r["Counter_Value"]) * 1024.0)
+    return d
+
+
+def main():
+    fetch, write = load(sys.argv[1]), load(sys.argv[2])
+    out = {}
+    for k in sorted(set(fetch) | set(write)):
+        f = statistics.median(fetch.get(k, [0.0])) * 2.0
+        w = statistics.median(write.get(k, [0.0]))
+        rec = {"fetch_bytes_x2": round(f), "write_bytes": round(w), "bytes": round(f + w),
+               "dispatches": len(fetch.get(k, []))}
+        out[STAGE.get(k, k)] = rec
+        print(f"{k:24s} read {f / 1e9:8.3f} GB  write {w / 1e9:8.3f} GB  per dispatch")
+    if len(sys.argv) > 3:
+        json.dump(out, open(sys.argv[3], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
