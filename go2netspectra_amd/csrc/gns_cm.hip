@@ -68,6 +68,7 @@ constexpr uint32_t kScanSeg = 4096;
 constexpr uint32_t kHot = 64;                       // designated hot buckets per row
 constexpr uint32_t kHotTab = 512;                   // LDS hash slots per row (load <= 1/8)
 constexpr uint32_t kHotMinBits = 11;                // designate only buckets with C >= 1024
+constexpr uint32_t kPendingId = 0xFFFFFFFEu;        // K1: flow not yet committed (equals no fingerprint)
 
 struct CmGeom {
     uint32_t w, d, wmask, pow2;
@@ -114,8 +115,27 @@ __device__ __forceinline__ int hot_lookup(const uint32_t *tabrow, uint32_t b) {
     }
 }
 
+__device__ __forceinline__ uint32_t ceil_log2_dev(uint32_t x) { return x <= 1 ? 0u : 32u - __clz(x - 1u); }
+
 __device__ __forceinline__ uint32_t row_index(const CmGeom &g, uint32_t h) {
     return g.pow2 ? (h & g.wmask) : (h % g.w);  // count_min.go:177 `% t.w`
+}
+
+// Per (hot slot, K1 block) summary of the block's updates to a designated
+// bucket, relative to the batch-entry fingerprints (count_min.go:180-235):
+// n updates, nfc / nfs of them foreign to the count / size owner, os / fs the
+// owner / foreign size sums, smax the largest foreign size.  k_hot_decide
+// turns them into the bucket's exact batch result without any per-update
+// entry (hot updates are never scattered).
+struct HotSum {
+    uint32_t n, nfc, nfs, smax;
+    unsigned long long os, fs;
+};
+
+// k_extract dynamic LDS: u64 os[S], fs[S] | u32 hist[nbins_all] | tab[d*kHotTab] |
+// u32 hFc[S], hFs[S], nfc[S], nfs[S], smax[S]   (S = d*kHot hot slots)
+__host__ __device__ inline size_t extract_lds_bytes(uint32_t nbins_all, uint32_t d) {
+    return (size_t)d * kHot * 16 + ((size_t)nbins_all + d * kHotTab) * 4 + (size_t)d * kHot * 20;
 }
 
 // Counter words of stats[]: 0 inserted, 1 dropped, 2 unsupported, 3 dict-full, 4 ovf-full
@@ -134,6 +154,8 @@ struct ExtractArgs {
     uint32_t *hist;      // [nbins_all][nblk]
     uint32_t nblk;
     const uint32_t *hot_ids;  // [d][kHot]
+    const uint32_t *Fc, *Fs;  // batch-entry fingerprints (hot slots' owners)
+    HotSum *hsum;             // [d*kHot][nblk]
     unsigned long long *stats;
 };
 
@@ -153,17 +175,36 @@ __device__ __forceinline__ int packet_key(const InputDesc &in, uint32_t K, const
 }
 
 // K1: parse/encode, dictionary, row hashes, block histogram.
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 template <int KIND, int MODE>
 __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
-    extern __shared__ uint32_t s_hist[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t xsm[];
     __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
     __shared__ uint8_t s_src[80];
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    const uint32_t NS = a.g.d * kHot;
+    unsigned long long *s_os = reinterpret_cast<unsigned long long *>(xsm);
+    unsigned long long *s_fs = s_os + NS;
+    uint32_t *s_hist = reinterpret_cast<uint32_t *>(s_fs + NS);
+    uint32_t *s_tab = s_hist + a.g.nbins_all;
+    uint32_t *s_hFc = s_tab + a.g.d * kHotTab;
+    uint32_t *s_hFs = s_hFc + NS, *s_nfc = s_hFs + NS, *s_nfs = s_nfc + NS, *s_smax = s_nfs + NS;
     stage_plan<MODE>(a.kp, s_src);
     const uint32_t K = a.kp.K;
-    uint32_t *s_tab = s_hist + a.g.nbins_all;
     build_hot_tab(a.hot_ids, 0, a.g.d, s_tab);
     for (uint32_t i = tid; i < a.g.nbins_all; i += kExThreads) s_hist[i] = 0;
+    for (uint32_t i = tid; i < NS; i += kExThreads) {
+        const uint32_t id = a.hot_ids[i];
+        const uint64_t cell = (uint64_t)(i / kHot) * a.g.w + id;
+        s_hFc[i] = id != GNS_ID_NONE ? a.Fc[cell] : GNS_ID_NONE;
+        s_hFs[i] = id != GNS_ID_NONE ? a.Fs[cell] : GNS_ID_NONE;
+        s_nfc[i] = 0; s_nfs[i] = 0; s_smax[i] = 0; s_os[i] = 0; s_fs[i] = 0;
+    }
     if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; }
     __syncthreads();
     const uint64_t beg = (uint64_t)blk * kChunk;
@@ -183,6 +224,7 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
         }
         uint32_t mk[GNS_KWMAX];
         mm3_premix<GNS_KWMAX>(kw, K, mk);
+        uint32_t kid = kPendingId;  // flow id when already committed (pending: foreign to every owner)
         if (ok) {
             uint32_t out;
             const uint32_t slot0 = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
@@ -193,20 +235,23 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
                 ok = false;
             } else if (r == DICT_FOUND) {
                 a.keyid[p] = out;
+                kid = out;
             } else {
                 a.keyid[p] = GNS_ID_NONE;  // set by k_resolve
                 const uint32_t q = atomicAdd(&s_pend, 1u);
                 a.pend[beg + q] = (uint64_t)(p - beg) << 32 | out;
             }
         }
+        const uint32_t sz = ok ? a.in.sizes[p] : 0u;
         n_ok += ok ? 1u : 0u;
 #pragma unroll
         for (uint32_t rr = 0; rr < 8; rr++) {
             if (rr >= a.g.d) break;
             uint32_t binid = 0xFFFFFFFFu;
+            int h = -1;
             if (ok) {
                 const uint32_t b = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, K, a.g.seeds[rr]));
-                const int h = hot_lookup(s_tab + rr * kHotTab, b);
+                h = hot_lookup(s_tab + rr * kHotTab, b);
                 // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
                 a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
                 binid = h >= 0 ? a.g.nbins + rr * kHot + (uint32_t)h : rr * a.g.ntiles + (b >> a.g.bin_bits);
@@ -215,18 +260,42 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
             const uint32_t b0 = __builtin_amdgcn_readfirstlane(binid);
             const uint64_t mm = __ballot(binid == b0 && b0 != 0xFFFFFFFFu);
             const uint32_t cnt = __popcll(mm);
-            if (cnt >= 4) {
-                if (binid == b0 && (uint32_t)__ffsll((long long)mm) - 1 == (threadIdx.x & 63u))
-                    atomicAdd(&s_hist[b0], cnt);
-                if (binid != 0xFFFFFFFFu && binid != b0) atomicAdd(&s_hist[binid], 1u);
-            } else if (binid != 0xFFFFFFFFu) {
-                atomicAdd(&s_hist[binid], 1u);
+            const bool agg = cnt >= 4;  // wave-uniform
+            const bool inmaj = agg && binid == b0;
+            const bool leader = inmaj && (uint32_t)__ffsll((long long)mm) - 1 == (threadIdx.x & 63u);
+            if (leader) atomicAdd(&s_hist[b0], cnt);
+            if (binid != 0xFFFFFFFFu && !inmaj) atomicAdd(&s_hist[binid], 1u);
+            // designated bucket: summary against the batch-entry owners
+            uint64_t ownv = 0;
+            if (h >= 0) {
+                const uint32_t slot = rr * kHot + (uint32_t)h;
+                if (kid != s_hFc[slot]) atomicAdd(&s_nfc[slot], 1u);
+                if (kid != s_hFs[slot]) {
+                    atomicAdd(&s_nfs[slot], 1u);
+                    atomicAdd(&s_fs[slot], (unsigned long long)sz);
+                    atomicMax(&s_smax[slot], sz);
+                } else {
+                    ownv = sz;
+                }
+            }
+            if (agg && b0 >= a.g.nbins && b0 != 0xFFFFFFFFu) {  // wave-uniform: majority bin is hot
+                const uint64_t tot = wave_sum64(inmaj ? ownv : 0ull);
+                if (leader && tot) atomicAdd(&s_os[b0 - a.g.nbins], (unsigned long long)tot);
+                if (!inmaj && ownv) atomicAdd(&s_os[binid - a.g.nbins], (unsigned long long)ownv);
+            } else if (ownv) {
+                atomicAdd(&s_os[binid - a.g.nbins], (unsigned long long)ownv);
             }
         }
     }
     atomicAdd(&s_ok, n_ok);
     __syncthreads();
     for (uint32_t i = tid; i < a.g.nbins_all; i += kExThreads) a.hist[(uint64_t)i * a.nblk + blk] = s_hist[i];
+    for (uint32_t i = tid; i < NS; i += kExThreads) {
+        HotSum hs;
+        hs.n = s_hist[a.g.nbins + i]; hs.nfc = s_nfc[i]; hs.nfs = s_nfs[i]; hs.smax = s_smax[i];
+        hs.os = s_os[i]; hs.fs = s_fs[i];
+        a.hsum[(uint64_t)i * a.nblk + blk] = hs;
+    }
     if (tid == 0) {
         a.pend_cnt[blk] = s_pend;
         if (s_pend) atomicAdd(a.pend_total, s_pend);
@@ -377,6 +446,12 @@ struct ScatterArgs {
     uint32_t *ovf_cnt;
     const uint32_t *hot_ids;
     unsigned long long *stats;
+    // hot_mode 0: tile bins only (designated buckets are summarized by K1);
+    // 1: only the hot slots flagged for the exact fallback (hflag2 & 3), and
+    // only when *hany (the whole grid exits otherwise).
+    uint32_t hot_mode;
+    const uint32_t *hflag2;
+    const uint32_t *hany;
 };
 
 // block (NW waves) exclusive scan; *total = sum
@@ -424,6 +499,8 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
     const uint64_t end = min(a.n, beg + kChunk);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     constexpr uint32_t TPT = (1536 + kScThreads - 1) / kScThreads;  // local bins per thread (LB <= 1536)
+    if (a.hot_mode && *a.hany == 0) return;
+    const uint32_t nbits = a.hot_mode ? a.g.nbits : ceil_log2_dev(a.g.ntiles);
     for (uint32_t i = tid; i < d * LB; i += kScThreads) {
         const uint32_t r = i / LB, t = i % LB;
         const uint64_t gb = t < a.g.ntiles ? (uint64_t)(r * a.g.ntiles + t)
@@ -454,7 +531,12 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
             // phase 1: stable per-wave ranks; wave w owns packets [rb + w*64*kScItems, ...), order (slot, lane)
 #pragma unroll
             for (int i = 0; i < kScItems; i++) {
-                const bool valid = ids[i] != GNS_ID_NONE;
+                bool valid = ids[i] != GNS_ID_NONE;
+                {
+                    const bool hot = (bs[i] >> 31) != 0;
+                    if (a.hot_mode) valid = valid && hot && (a.hflag2[r * kHot + (bs[i] & 0x7FFFFFFFu)] & 3u) != 0;
+                    else valid = valid && !hot;
+                }
                 uint32_t t = 0;
                 uint64_t e = 0;
                 if (valid) {
@@ -479,7 +561,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                     e = (uint64_t)((sf << kEntShift) | low) << 32 | lo;
                 }
                 uint64_t peers = __ballot(valid);
-                for (uint32_t bit = 0; bit < a.g.nbits; bit++) {
+                for (uint32_t bit = 0; bit < nbits; bit++) {
                     const uint64_t m = __ballot(valid && ((t >> bit) & 1u));
                     peers &= ((t >> bit) & 1u) ? m : ~m;
                 }
@@ -592,12 +674,6 @@ constexpr uint64_t kM21 = (1ull << 21) - 1;
 #define GNS_REP_CAP 1536
 #endif
 constexpr uint32_t kRepCap = GNS_REP_CAP;
-
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
 
 // ---------------------------------------------------------------------------
 // Exact wave-parallel sequence for ONE bucket (count_min.go:180-235): 64
@@ -1011,6 +1087,7 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
 }
 
 constexpr uint32_t kHotSegs = 64;   // segments per hot bin (blocks working on one bucket)
+constexpr uint32_t kChkCap = 4096;  // (slot, K1 block) exact size checks per batch
 
 struct HotArgs {
     const uint64_t *entries;
@@ -1023,6 +1100,16 @@ struct HotArgs {
     uint32_t *C, *Fc, *S, *Fs;
     long long *segtot;  // [d*kHot][kHotSegs][2]: count walk, size walk of each segment
     uint32_t *hflag;    // [d*kHot]: bit0/bit1 = count/size half saw an event (needs replay)
+    // summary path (k_hot_decide / k_hot_blockcheck / k_hot_commit)
+    const HotSum *hsum;     // [d*kHot][nblk]
+    uint32_t *hflag2;       // [d*kHot]: bit0/bit1 = count/size half goes to the exact entry path
+    uint32_t *hany;         // any hflag2 bit set in this batch
+    uint32_t *hres;         // [d*kHot][2]: linear-regime C, S at batch end
+    uint4 *chk;             // (slot, K1 block, walk lo, walk hi) blocks needing the exact size check
+    uint32_t *nchk;
+    uint32_t chk_cap;
+    const uint32_t *keyid, *idx, *sizes;
+    uint64_t n;
 };
 
 __device__ __forceinline__ void hot_bin_range(const HotArgs &a, uint32_t hb, uint32_t &beg, uint32_t &end) {
@@ -1065,6 +1152,7 @@ __device__ __forceinline__ void block_sum2(long long &x, long long &y, long long
 __global__ __launch_bounds__(256) void k_hot_sum(HotArgs a) {
     __shared__ long long sh[8];
     const uint32_t hb = blockIdx.y, sidx = blockIdx.x;
+    if (*a.hany == 0 || (a.hflag2[hb] & 3u) == 0) return;
     const uint32_t id = a.hot_ids[hb];
     if (id == GNS_ID_NONE) return;
     uint32_t beg, end, sb, se;
@@ -1094,6 +1182,7 @@ __global__ __launch_bounds__(256) void k_hot_verify(HotArgs a) {
     __shared__ long long sh_w[2][4];
     const uint32_t hb = blockIdx.y, sidx = blockIdx.x, tid = threadIdx.x;
     const uint32_t lane = tid & 63u, wave = tid >> 6;
+    if (*a.hany == 0 || (a.hflag2[hb] & 3u) == 0) return;
     const uint32_t id = a.hot_ids[hb];
     if (id == GNS_ID_NONE) return;
     uint32_t beg, end, sb, se;
@@ -1153,6 +1242,9 @@ __global__ __launch_bounds__(256) void k_hot_verify(HotArgs a) {
 __global__ __launch_bounds__(512) void k_hot_apply(HotArgs a) {
     const uint32_t hb = threadIdx.x;
     if (hb >= a.g.d * kHot) return;
+    if (*a.hany == 0) return;
+    const uint32_t f2 = a.hflag2[hb] & 3u;
+    if (!f2) return;
     const uint32_t id = a.hot_ids[hb];
     if (id == GNS_ID_NONE) return;
     uint32_t beg, end;
@@ -1165,14 +1257,15 @@ __global__ __launch_bounds__(512) void k_hot_apply(HotArgs a) {
     }
     const uint64_t cell = (uint64_t)(hb / kHot) * a.g.w + id;
     const uint32_t f = a.hflag[hb];
-    if (!(f & 1u)) a.C[cell] = (uint32_t)((long long)a.C[cell] + tc);
-    if (!(f & 2u)) a.S[cell] = (uint32_t)((long long)a.S[cell] + ts);
+    if ((f2 & 1u) && !(f & 1u)) a.C[cell] = (uint32_t)((long long)a.C[cell] + tc);
+    if ((f2 & 2u) && !(f & 2u)) a.S[cell] = (uint32_t)((long long)a.S[cell] + ts);
 }
 
 // Exact in-order replay of one hot bin (cold start / ownership change).
 __global__ __launch_bounds__(64) void k_hot_fallback(HotArgs a) {
     const uint32_t i = blockIdx.x, lane = threadIdx.x;
-    const uint32_t rep = a.hflag[i];
+    if (*a.hany == 0) return;
+    const uint32_t rep = a.hflag[i] & a.hflag2[i] & 3u;
     if (!rep) return;
     const uint32_t id = a.hot_ids[i];
     const uint64_t cell = (uint64_t)(i / kHot) * a.g.w + id;
@@ -1191,6 +1284,148 @@ __global__ __launch_bounds__(64) void k_hot_fallback(HotArgs a) {
         if (rep & 1u) { a.C[cell] = C; a.Fc[cell] = Fc; }
         if (rep & 2u) { a.S[cell] = S; a.Fs[cell] = Fs; }
     }
+}
+
+// ---------------------------------------------------------------------------
+// Summary path for designated buckets.  K1 left one HotSum per (slot, K1
+// block).  The count half is linear (owner fixed, C' = C + n_own - n_foreign)
+// when C > n_foreign over the batch: every foreign update then finds C >= 2
+// (count_min.go:226-231 never reaches 0) -- and no u32 wrap.  The size half
+// is linear when every foreign update finds S >= max(s, 1) (:184-200 never
+// replace), where S is the running walk W = S0 + sum(own) - sum(foreign) taken
+// mod 2^32 (owner adds wrap exactly like the walk, :190-193).  Per K1 block j
+// the walk stays in [W_j - fs_j, W_j + os_j]; if that interval lies inside one
+// 2^32 period with low part >= max(smax_j, 1) the block is safe; otherwise
+// k_hot_blockcheck replays the block's walk exactly.  Anything that fails goes
+// to the exact entry path (K3 hot mode + k_hot_sum/verify/apply/fallback).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hot_decide(HotArgs a) {
+    __shared__ long long sh_w[4];
+    __shared__ unsigned long long sh_r[3][4];
+    __shared__ uint32_t s_fail;
+    const uint32_t slot = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t id = a.hot_ids[slot];
+    if (id == GNS_ID_NONE) return;
+    if (tid == 0) s_fail = 0;
+    const uint64_t cell = (uint64_t)(slot / kHot) * a.g.w + id;
+    const uint32_t C0 = a.C[cell], S0 = a.S[cell];
+    const HotSum *hs = a.hsum + (uint64_t)slot * a.nblk;
+    long long run = S0;
+    unsigned long long N = 0, NFC = 0, NFS = 0;
+    __syncthreads();
+    for (uint32_t j0 = 0; j0 < a.nblk; j0 += 256) {
+        const uint32_t j = j0 + tid;
+        HotSum h{};
+        if (j < a.nblk) h = hs[j];
+        const long long dlt = (long long)h.os - (long long)h.fs;
+        const long long inc = wave_incl_scan64(dlt);
+        if (lane == 63) sh_w[wave] = inc;
+        __syncthreads();
+        long long base = 0, tot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 4; w++) {
+            if (w < wave) base += sh_w[w];
+            tot += sh_w[w];
+        }
+        __syncthreads();
+        const long long W = run + base + inc - dlt;  // walk before block j
+        if (h.nfs) {
+            const long long L = W - (long long)h.fs, U = W + (long long)h.os;
+            const uint32_t m = h.smax > 1u ? h.smax : 1u;
+            const bool safe = L >= 0 && (L >> 32) == (U >> 32) && (uint32_t)L >= m;
+            if (!safe) {
+                const uint32_t q = atomicAdd(a.nchk, 1u);
+                if (q < a.chk_cap) a.chk[q] = make_uint4(slot, j, (uint32_t)W, (uint32_t)((unsigned long long)W >> 32));
+                else s_fail = 1;
+            }
+        }
+        run += tot;
+        N += h.n; NFC += h.nfc; NFS += h.nfs;
+    }
+    N = wave_sum64(N); NFC = wave_sum64(NFC); NFS = wave_sum64(NFS);
+    if (lane == 0) { sh_r[0][wave] = N; sh_r[1][wave] = NFC; sh_r[2][wave] = NFS; }
+    __syncthreads();
+    if (tid == 0) {
+        N = sh_r[0][0] + sh_r[0][1] + sh_r[0][2] + sh_r[0][3];
+        NFC = sh_r[1][0] + sh_r[1][1] + sh_r[1][2] + sh_r[1][3];
+        NFS = sh_r[2][0] + sh_r[2][1] + sh_r[2][2] + sh_r[2][3];
+        uint32_t f = 0;
+        // count half
+        if ((unsigned long long)C0 > NFC && (unsigned long long)C0 + (N - NFC) < (1ull << 32))
+            a.hres[slot * 2] = (uint32_t)((unsigned long long)C0 + N - 2 * NFC);
+        else
+            f |= 1u;
+        // size half: all-own is plain u32 addition; otherwise per-block checks
+        if (NFS && (S0 == 0 || s_fail)) f |= 2u;
+        a.hres[slot * 2 + 1] = (uint32_t)(unsigned long long)run;
+        if (f) { atomicOr(&a.hflag2[slot], f); atomicOr(a.hany, 1u); }
+    }
+}
+
+// Exact walk of one K1 block's updates to one designated bucket (size half).
+__global__ __launch_bounds__(256) void k_hot_blockcheck(HotArgs a) {
+    __shared__ long long sh_w[4];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    if (q >= min(*a.nchk, a.chk_cap)) return;
+    const uint4 c = a.chk[q];
+    const uint32_t slot = c.x, blk = c.y;
+    const uint32_t r = slot / kHot, code = 0x80000000u | (slot % kHot);
+    const uint32_t Fs0 = a.Fs[(uint64_t)r * a.g.w + a.hot_ids[slot]];
+    long long run = (long long)((unsigned long long)c.z | (unsigned long long)c.w << 32);
+    const uint64_t beg = (uint64_t)blk * kChunk, end = min(a.n, beg + kChunk);
+    const uint32_t *idxr = a.idx + (uint64_t)r * a.n;
+    bool ev = false;
+    for (uint64_t q0 = beg; q0 < end; q0 += 1024) {  // 4 consecutive packets per thread
+        long long dl[4], tl = 0;
+        bool fo[4];
+        uint32_t sv[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint64_t p = q0 + tid * 4 + i;
+            dl[i] = 0; fo[i] = false; sv[i] = 0;
+            if (p < end && idxr[p] == code && a.keyid[p] != GNS_ID_NONE) {
+                const uint32_t s = a.sizes[p];
+                const bool own = a.keyid[p] == Fs0;
+                dl[i] = own ? (long long)s : -(long long)s;
+                fo[i] = !own;
+                sv[i] = s;
+            }
+            tl += dl[i];
+        }
+        const long long inc = wave_incl_scan64(tl);
+        if (lane == 63) sh_w[wave] = inc;
+        __syncthreads();
+        long long base = 0, tot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 4; w++) {
+            if (w < wave) base += sh_w[w];
+            tot += sh_w[w];
+        }
+        __syncthreads();
+        long long wb = run + base + inc - tl;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if (fo[i]) {
+                const uint32_t Sb = (uint32_t)(unsigned long long)wb;
+                if (wb < 0 || Sb == 0u || sv[i] > Sb) ev = true;
+            }
+            wb += dl[i];
+        }
+        run += tot;
+    }
+    if (__ballot(ev) && lane == 0) { atomicOr(&a.hflag2[slot], 2u); atomicOr(a.hany, 1u); }
+}
+
+// Commit the linear results of the halves that stay on the summary path.
+__global__ __launch_bounds__(512) void k_hot_commit(HotArgs a) {
+    const uint32_t slot = threadIdx.x;
+    if (slot >= a.g.d * kHot) return;
+    const uint32_t id = a.hot_ids[slot];
+    if (id == GNS_ID_NONE) return;
+    const uint64_t cell = (uint64_t)(slot / kHot) * a.g.w + id;
+    const uint32_t f = a.hflag2[slot];
+    if (!(f & 1u)) a.C[cell] = a.hres[slot * 2];
+    if (!(f & 2u)) a.S[cell] = a.hres[slot * 2 + 1];
 }
 
 // Designation for the next batch: per row, the buckets whose counter bit
@@ -1333,6 +1568,10 @@ struct gns_cm {
     uint32_t *hot_ids = nullptr;          // [d][kHot] designated buckets for the next batch
     long long *segtot = nullptr;          // [d*kHot][kHotSegs][2]
     uint32_t *hflag = nullptr, *hhist = nullptr, *hthr = nullptr, *hcnt = nullptr;
+    HotSum *hsum = nullptr;               // [d*kHot][nblk_max]
+    uint32_t *hflag2 = nullptr;           // [d*kHot + 2]: flags, then hany, nchk
+    uint32_t *hres = nullptr;             // [d*kHot][2]
+    uint4 *chk = nullptr;                 // [kChkCap]
     bool warm = false;                    // a batch has run since create/reset
     uint32_t *h_pin = nullptr;            // pinned host mirror of small counters
     // staging for host inputs
@@ -1366,6 +1605,7 @@ int cm_free_all(gns_cm *cm) {
     dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
     dfree(cm->entries); dfree(cm->entries2); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats); dfree(cm->stage);
     dfree(cm->hot_ids); dfree(cm->segtot); dfree(cm->hflag); dfree(cm->hhist); dfree(cm->hthr); dfree(cm->hcnt);
+    dfree(cm->hsum); dfree(cm->hflag2); dfree(cm->hres); dfree(cm->chk);
     if (cm->h_pin) (void)hipHostFree(cm->h_pin);
     cm->timer.destroy();
     if (cm->stream) (void)hipStreamDestroy(cm->stream);
@@ -1395,16 +1635,18 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
     ScopedStage total_stage(cm->timer, 5);
     // K1
     GNS_HIP(hipMemsetAsync(cm->ptotal, 0, 8, s));
+    GNS_HIP(hipMemsetAsync(cm->hflag2, 0, ((size_t)g.d * kHot + 2) * 4, s));
     if (++cm->epoch == 0) cm->epoch = 1;
     {
         ExtractArgs a{};
         a.in = in; a.n = n; a.kp = cm->kp; a.g = g; a.D = cm->D; a.epoch = cm->epoch;
         a.keyid = cm->keyid; a.idx = cm->idx; a.pend = cm->pend[0]; a.pend_cnt = cm->pcnt[0];
         a.pend_total = cm->ptotal; a.hist = cm->hist; a.nblk = nblk; a.hot_ids = cm->hot_ids;
+        a.Fc = cm->Fc; a.Fs = cm->Fs; a.hsum = cm->hsum;
         a.stats = cm->stats;
         ScopedStage st(cm->timer, 0);
         hipLaunchKernelGGL((k_extract<KIND, MODE>), dim3(nblk), dim3(kExThreads),
-                           (g.nbins_all + g.d * kHotTab) * 4, s, a);
+                           extract_lds_bytes(g.nbins_all, g.d), s, a);
         GNS_HIP(hipGetLastError());
     }
     // K1b: resolve parked packets until none remain
@@ -1449,6 +1691,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.n = n; a.g = g; a.keyid = cm->keyid; a.idx = cm->idx; a.sizes = in.sizes;
         a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
         a.ovf_cnt = cm->ovf_cnt; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
+        a.hot_mode = 0; a.hflag2 = cm->hflag2; a.hany = cm->hflag2 + g.d * kHot;
         ScopedStage st(cm->timer, 3);
         hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
         GNS_HIP(hipGetLastError());
@@ -1474,8 +1717,24 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         h.entries = cm->entries; h.offsets = cm->hist; h.nblk = nblk; h.total = cm->total; h.ovf = cm->ovf;
         h.hot_ids = cm->hot_ids; h.g = g; h.C = cm->C; h.Fc = cm->Fc; h.S = cm->S; h.Fs = cm->Fs;
         h.segtot = cm->segtot; h.hflag = cm->hflag;
+        h.hsum = cm->hsum; h.hflag2 = cm->hflag2; h.hany = cm->hflag2 + g.d * kHot; h.nchk = h.hany + 1;
+        h.hres = cm->hres; h.chk = cm->chk; h.chk_cap = kChkCap;
+        h.keyid = cm->keyid; h.idx = cm->idx; h.sizes = in.sizes; h.n = n;
         ScopedStage st(cm->timer, 6);
         GNS_HIP(hipMemsetAsync(cm->hflag, 0, (size_t)g.d * kHot * 4, s));
+        // summary path: decide, exact block checks, commit
+        hipLaunchKernelGGL(k_hot_decide, dim3(g.d * kHot), dim3(256), 0, s, h);
+        hipLaunchKernelGGL(k_hot_blockcheck, dim3(kChkCap), dim3(256), 0, s, h);
+        hipLaunchKernelGGL(k_hot_commit, dim3(1), dim3(512), 0, s, h);
+        // exact entry path for flagged halves (device-side early exit when none)
+        {
+            ScatterArgs a{};
+            a.n = n; a.g = g; a.keyid = cm->keyid; a.idx = cm->idx; a.sizes = in.sizes;
+            a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
+            a.ovf_cnt = cm->ovf_cnt; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
+            a.hot_mode = 1; a.hflag2 = cm->hflag2; a.hany = h.hany;
+            hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
+        }
         hipLaunchKernelGGL(k_hot_sum, dim3(kHotSegs, g.d * kHot), dim3(256), 0, s, h);
         hipLaunchKernelGGL(k_hot_verify, dim3(kHotSegs, g.d * kHot), dim3(256), 0, s, h);
         hipLaunchKernelGGL(k_hot_apply, dim3(1), dim3(512), 0, s, h);
@@ -1646,7 +1905,10 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (rc = dalloc_t(&cm->ovf, kOvfCap)) || (rc = dalloc_t(&cm->ovf_cnt, 1)) ||
             (rc = dalloc_t(&cm->stats, 16)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
             (rc = dalloc_t(&cm->segtot, (size_t)g.d * kHot * kHotSegs * 2)) || (rc = dalloc_t(&cm->hflag, g.d * kHot)) ||
-            (rc = dalloc_t(&cm->hhist, g.d * 33)) || (rc = dalloc_t(&cm->hthr, 8)) || (rc = dalloc_t(&cm->hcnt, 8)))
+            (rc = dalloc_t(&cm->hhist, g.d * 33)) || (rc = dalloc_t(&cm->hthr, 8)) || (rc = dalloc_t(&cm->hcnt, 8)) ||
+            (rc = dalloc_t(&cm->hsum, (uint64_t)g.d * kHot * cm->nblk_max)) ||
+            (rc = dalloc_t(&cm->hflag2, g.d * kHot + 2)) || (rc = dalloc_t(&cm->hres, g.d * kHot * 2)) ||
+            (rc = dalloc_t(&cm->chk, kChkCap)))
             break;
         if (hipHostMalloc(reinterpret_cast<void **>(&cm->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
