@@ -65,7 +65,7 @@ constexpr int kApItems = GNS_AP_ITEMS;
 constexpr uint32_t kApChunk = kApThreads * kApItems; // 8192 updates per K4 step
 static_assert((uint64_t)kApChunk * (kSizeEsc - 1) < (1ull << 32), "K4 per-chunk size sums must fit 32 bits");
 constexpr uint32_t kScanSeg = 4096;
-constexpr uint32_t kHot = 64;                       // designated hot buckets per row
+constexpr uint32_t kHot = 64;                       // designated hot buckets per row (slot fits 6 bits)
 constexpr uint32_t kHotTab = 512;                   // LDS hash slots per row (load <= 1/8)
 constexpr uint32_t kHotMinBits = 11;                // designate only buckets with C >= 1024
 constexpr uint32_t kPendingId = 0xFFFFFFFEu;        // K1: flow not yet committed (equals no fingerprint)
@@ -85,34 +85,22 @@ struct CmGeom {
 // parallel instead of one workgroup walking it.  Designation only moves work;
 // exactness comes from the verify/fallback steps (k_hot_verify, k_hot_fallback).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t hot_hash(uint32_t b) { return (b * 0x9E3779B1u) >> 23; }  // 0..511
-
-// LDS table rows [r0, r0+nrows): value = bucket<<7 | h, empty = ~0
-__device__ __forceinline__ void build_hot_tab(const uint32_t *hot_ids, uint32_t r0, uint32_t nrows,
-                                              uint32_t *tab) {
-    for (uint32_t i = threadIdx.x; i < nrows * kHotTab; i += blockDim.x) tab[i] = 0xFFFFFFFFu;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nrows * kHot; i += blockDim.x) {
-        const uint32_t r = i / kHot, h = i % kHot;
-        const uint32_t id = hot_ids[(r0 + r) * kHot + h];
-        if (id == GNS_ID_NONE) continue;
-        uint32_t slot = hot_hash(id);
-        for (;;) {
-            if (atomicCAS(&tab[r * kHotTab + slot], 0xFFFFFFFFu, id << 7 | h) == 0xFFFFFFFFu) break;
-            slot = (slot + 1) & (kHotTab - 1);
-        }
-    }
-    __syncthreads();
-}
+// Per-row lookup table of the designated buckets, built once per batch by
+// k_hot_table (deterministic, single thread per row) and copied to LDS by K1:
+// 128 groups of 4 entries (one 16-byte LDS read per lookup, no probing);
+// entry = bucket << 6 | hot slot, empty = ~0.  A bucket whose group is full is
+// simply not designated (designation only moves work).
+static_assert(kHotTab / 4 == 128 && kHot <= 64, "hot_group() yields 7 bits; table entries hold a 6-bit slot");
+__device__ __forceinline__ uint32_t hot_group(uint32_t b) { return (b * 0x9E3779B1u) >> 25; }  // 0..127
 
 __device__ __forceinline__ int hot_lookup(const uint32_t *tabrow, uint32_t b) {
-    uint32_t slot = hot_hash(b);
-    for (;;) {
-        const uint32_t v = tabrow[slot];
-        if (v == 0xFFFFFFFFu) return -1;
-        if ((v >> 7) == b) return (int)(v & 127u);
-        slot = (slot + 1) & (kHotTab - 1);
-    }
+    const uint4 e = *reinterpret_cast<const uint4 *>(tabrow + hot_group(b) * 4);
+    int h = -1;
+    h = (e.w >> 6) == b ? (int)(e.w & 63u) : h;
+    h = (e.z >> 6) == b ? (int)(e.z & 63u) : h;
+    h = (e.y >> 6) == b ? (int)(e.y & 63u) : h;
+    h = (e.x >> 6) == b ? (int)(e.x & 63u) : h;
+    return h;
 }
 
 __device__ __forceinline__ uint32_t ceil_log2_dev(uint32_t x) { return x <= 1 ? 0u : 32u - __clz(x - 1u); }
@@ -132,7 +120,7 @@ struct HotSum {
     unsigned long long os, fs;
 };
 
-// k_extract dynamic LDS: u64 os[S], fs[S] | u32 hist[nbins_all] | tab[d*kHotTab] |
+// k_extract dynamic LDS: u64 os[S], fs[S] | u32 tab[d*kHotTab] | hist[nbins_all] |
 // u32 hFc[S], hFs[S], nfc[S], nfs[S], smax[S]   (S = d*kHot hot slots)
 __host__ __device__ inline size_t extract_lds_bytes(uint32_t nbins_all, uint32_t d) {
     return (size_t)d * kHot * 16 + ((size_t)nbins_all + d * kHotTab) * 4 + (size_t)d * kHot * 20;
@@ -154,6 +142,7 @@ struct ExtractArgs {
     uint32_t *hist;      // [nbins_all][nblk]
     uint32_t nblk;
     const uint32_t *hot_ids;  // [d][kHot]
+    const uint32_t *hot_tab;  // [d][kHotTab] lookup groups (k_hot_table)
     const uint32_t *Fc, *Fs;  // batch-entry fingerprints (hot slots' owners)
     HotSum *hsum;             // [d*kHot][nblk]
     unsigned long long *stats;
@@ -174,14 +163,64 @@ __device__ __forceinline__ int packet_key(const InputDesc &in, uint32_t K, const
     }
 }
 
-// K1: parse/encode, dictionary, row hashes, block histogram.
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+enum { CM_FOUND = 0, CM_PENDING = 1, CM_FULL = 2, CM_CLAIMED = 3 };
+
+// Dictionary probe for the Count-Min engine: like dict_find_or_claim, but
+// loads whole 64-byte records (r[] holds the found record, bucket cache
+// included) and reports CM_CLAIMED when this lane inserted the key (the
+// caller then writes the bucket words).  K is a compile-time constant in the
+// specialized kernels.
+__device__ __forceinline__ int cm_find_or_claim(const DictDev &D, const uint32_t (&kw)[GNS_KWMAX], uint32_t K,
+                                                uint32_t slot, uint32_t epoch, uint32_t *out,
+                                                uint32_t (&r)[16]) {
+    const uint32_t nkw = (K + 3) >> 2;
+    for (int probe = 0; probe < GNS_DICT_MAX_PROBE; probe++) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(D.rec + (size_t)slot * D.RW);
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+        for (int i = 0; i < 4; i++) {
+            const uint4 v = (4u * i < D.RW) ? q[i] : make_uint4(0, 0, 0, 0);
+            r[4 * i] = v.x; r[4 * i + 1] = v.y; r[4 * i + 2] = v.z; r[4 * i + 3] = v.w;
+        }
+        uint32_t tag = r[0];
+        if (tag == 0) {
+            uint32_t *tp = D.rec + (size_t)slot * D.RW;
+            const uint32_t old = atomicCAS(tp, 0u, epoch);
+            if (old == 0) {
+#pragma unroll
+                for (int i = 0; i < GNS_KWMAX; i++)
+                    if ((uint32_t)i < nkw) tp[1 + i] = kw[i];
+                *out = slot;
+                return CM_CLAIMED;
+            }
+            tag = old;
+            if (tag != epoch) {  // committed earlier: need its key words
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const uint4 v = (4u * i < D.RW) ? q[i] : make_uint4(0, 0, 0, 0);
+                    r[4 * i] = v.x; r[4 * i + 1] = v.y; r[4 * i + 2] = v.z; r[4 * i + 3] = v.w;
+                }
+            }
+        }
+        if (tag == epoch) { *out = slot; return CM_PENDING; }
+        bool eq = true;
+#pragma unroll
+        for (int i = 0; i < GNS_KWMAX; i++)
+            if ((uint32_t)i < nkw) eq = eq && (r[1 + i] == kw[i]);
+        if (eq) { *out = slot; return CM_FOUND; }
+        slot = (slot + 1u) & D.mask;
+    }
+    return CM_FULL;
 }
 
-template <int KIND, int MODE>
+// Whole-wave sums through the device library's DPP reductions (row_shl /
+// wave_shl / row_mirror, no LDS round trips).  Call with all 64 lanes active.
+extern "C" __device__ unsigned long long __ockl_wfred_add_u64(unsigned long long);
+extern "C" __device__ unsigned __ockl_wfred_add_u32(unsigned);
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) { return __ockl_wfred_add_u64(v); }
+
+// K1: parse/encode, dictionary, row buckets, block histogram, hot summaries.
+// KB = key bytes when known at compile time (16 / 37), 0 = runtime a.kp.K.
+template <int KIND, int MODE, int KB>
 __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xsm[];
     __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
@@ -190,13 +229,14 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
     const uint32_t NS = a.g.d * kHot;
     unsigned long long *s_os = reinterpret_cast<unsigned long long *>(xsm);
     unsigned long long *s_fs = s_os + NS;
-    uint32_t *s_hist = reinterpret_cast<uint32_t *>(s_fs + NS);
-    uint32_t *s_tab = s_hist + a.g.nbins_all;
-    uint32_t *s_hFc = s_tab + a.g.d * kHotTab;
+    uint32_t *s_tab = reinterpret_cast<uint32_t *>(s_fs + NS);  // 16-byte aligned groups
+    uint32_t *s_hist = s_tab + a.g.d * kHotTab;
+    uint32_t *s_hFc = s_hist + a.g.nbins_all;
     uint32_t *s_hFs = s_hFc + NS, *s_nfc = s_hFs + NS, *s_nfs = s_nfc + NS, *s_smax = s_nfs + NS;
     stage_plan<MODE>(a.kp, s_src);
-    const uint32_t K = a.kp.K;
-    build_hot_tab(a.hot_ids, 0, a.g.d, s_tab);
+    const uint32_t K = KB ? (uint32_t)KB : a.kp.K;
+    const uint32_t d = a.g.d;
+    for (uint32_t i = tid; i < d * kHotTab; i += kExThreads) s_tab[i] = a.hot_tab[i];
     for (uint32_t i = tid; i < a.g.nbins_all; i += kExThreads) s_hist[i] = 0;
     for (uint32_t i = tid; i < NS; i += kExThreads) {
         const uint32_t id = a.hot_ids[i];
@@ -209,6 +249,7 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
     __syncthreads();
     const uint64_t beg = (uint64_t)blk * kChunk;
     const uint64_t end = min(a.n, beg + kChunk);
+    const bool bw = a.D.bw != 0;
     uint32_t n_ok = 0;
     for (uint64_t p0 = beg; p0 < end; p0 += kExThreads) {  // wave-uniform trip count
         const uint64_t p = p0 + tid;
@@ -225,32 +266,52 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
         uint32_t mk[GNS_KWMAX];
         mm3_premix<GNS_KWMAX>(kw, K, mk);
         uint32_t kid = kPendingId;  // flow id when already committed (pending: foreign to every owner)
+        uint32_t rec[16];
+        int res = CM_FULL;
+        uint32_t out = 0;
         if (ok) {
-            uint32_t out;
             const uint32_t slot0 = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
-            const int r = dict_find_or_claim(a.D, kw, slot0, a.epoch, &out);
-            if (r == DICT_FULL) {
+            res = cm_find_or_claim(a.D, kw, K, slot0, a.epoch, &out, rec);
+            if (res == CM_FULL) {
                 a.keyid[p] = GNS_ID_NONE;
                 atomicAdd(&s_full, 1u);
                 ok = false;
-            } else if (r == DICT_FOUND) {
-                a.keyid[p] = out;
-                kid = out;
-            } else {
+            } else if (res == CM_PENDING) {
                 a.keyid[p] = GNS_ID_NONE;  // set by k_resolve
                 const uint32_t q = atomicAdd(&s_pend, 1u);
                 a.pend[beg + q] = (uint64_t)(p - beg) << 32 | out;
+            } else {
+                a.keyid[p] = out;
+                kid = out;
             }
+        }
+        // row buckets: from the record's cache (rows 0..3 of a committed flow), else hashed
+        uint32_t bk[8];
+        const bool cached = bw && res == CM_FOUND;
+#pragma unroll
+        for (uint32_t rr = 0; rr < 8; rr++) bk[rr] = (rr < 4 && cached) ? rec[12 + rr] : 0u;
+        if (__ballot(ok && !cached) || d > 4) {
+#pragma unroll
+            for (uint32_t rr = 0; rr < 8; rr++) {
+                if (rr >= d) break;
+                if (ok && (!cached || rr >= 4)) bk[rr] = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, K, a.g.seeds[rr]));
+            }
+        }
+        if (bw && res == CM_CLAIMED) {  // publish the bucket cache with the key (visible next launch)
+            uint32_t *tp = a.D.rec + (size_t)out * a.D.RW;
+#pragma unroll
+            for (uint32_t rr = 0; rr < 4; rr++)
+                if (rr < d) tp[12 + rr] = bk[rr];
         }
         const uint32_t sz = ok ? a.in.sizes[p] : 0u;
         n_ok += ok ? 1u : 0u;
 #pragma unroll
         for (uint32_t rr = 0; rr < 8; rr++) {
-            if (rr >= a.g.d) break;
+            if (rr >= d) break;
             uint32_t binid = 0xFFFFFFFFu;
             int h = -1;
             if (ok) {
-                const uint32_t b = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, K, a.g.seeds[rr]));
+                const uint32_t b = bk[rr];
                 h = hot_lookup(s_tab + rr * kHotTab, b);
                 // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
                 a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
@@ -319,6 +380,7 @@ struct ResolveArgs {
     uint32_t *cnt_out;
     uint32_t *total_out;
     unsigned long long *stats;
+    CmGeom g;
 };
 
 // K1b: packets parked on a slot claimed in the previous launch.
@@ -337,11 +399,18 @@ __global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
         const uint64_t p = beg + (v >> 32);
         uint32_t kw[GNS_KWMAX];
         (void)packet_key<KIND, MODE>(a.in, a.kp.K, s_src, p, kw);
-        uint32_t out;
-        const int r = dict_find_or_claim(a.D, kw, (uint32_t)v, a.epoch, &out);
-        if (r == DICT_FOUND) {
+        uint32_t out, rec[16];
+        const int r = cm_find_or_claim(a.D, kw, a.kp.K, (uint32_t)v, a.epoch, &out, rec);
+        if (r == CM_FOUND || r == CM_CLAIMED) {
             a.keyid[p] = out;
-        } else if (r == DICT_PENDING) {
+            if (r == CM_CLAIMED && a.D.bw) {  // bucket cache, as in k_extract
+                uint32_t mk[GNS_KWMAX];
+                mm3_premix<GNS_KWMAX>(kw, a.kp.K, mk);
+                uint32_t *tp = a.D.rec + (size_t)out * a.D.RW;
+                for (uint32_t rr = 0; rr < 4 && rr < a.g.d; rr++)
+                    tp[12 + rr] = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, a.kp.K, a.g.seeds[rr]));
+            }
+        } else if (r == CM_PENDING) {
             const uint32_t q = atomicAdd(&s_cnt, 1u);
             a.pend_out[beg + q] = (v & 0xFFFFFFFF00000000ull) | out;
         } else {
@@ -359,15 +428,9 @@ __global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
 // ---------------------------------------------------------------------------
 // K2: exclusive scan (three phases) of hist[nbins*nblk] in place.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o, 64);
-        if (lane >= (uint32_t)o) v += t;
-    }
-    return v;
-}
+extern "C" __device__ unsigned __ockl_wfscan_add_u32(unsigned, bool);
+// DPP inclusive scan over the whole wave (call with all 64 lanes active)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) { return __ockl_wfscan_add_u32(v, true); }
 
 // block (256 threads) exclusive scan; returns exclusive prefix, *total = sum
 __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *s_w, uint32_t *total) {
@@ -682,15 +745,9 @@ constexpr uint32_t kRepCap = GNS_REP_CAP;
 // take-over, counter wrap) is applied explicitly and the scan restarts after
 // it.  Steps per 64 updates = events + 1.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) {
-    const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int64_t t = __shfl_up(v, o, 64);
-        if (lane >= (uint32_t)o) v += t;
-    }
-    return v;
-}
+extern "C" __device__ long __ockl_wfscan_add_i64(long, bool);
+// DPP inclusive scan over the whole wave (call with all 64 lanes active)
+__device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) { return __ockl_wfscan_add_i64(v, true); }
 
 // count half; F, C wave-uniform
 __device__ __forceinline__ void count_seq64(bool valid, uint32_t k, uint32_t &F, uint32_t &C) {
@@ -1474,6 +1531,24 @@ __global__ __launch_bounds__(256) void k_hot_collect(const uint32_t *C, CmGeom g
     }
 }
 
+// Lookup groups of the designated buckets (one thread per row, deterministic);
+// a bucket whose group is full is dropped from the designation.
+__global__ void k_hot_table(CmGeom g, uint32_t *hot_ids, uint32_t *hot_tab) {
+    const uint32_t r = threadIdx.x;
+    if (r >= g.d) return;
+    uint32_t *tab = hot_tab + r * kHotTab;
+    for (uint32_t i = 0; i < kHotTab; i++) tab[i] = 0xFFFFFFFFu;
+    for (uint32_t h = 0; h < kHot; h++) {
+        const uint32_t b = hot_ids[r * kHot + h];
+        if (b == GNS_ID_NONE) continue;
+        uint32_t *grp = tab + hot_group(b) * 4;
+        uint32_t j = 0;
+        while (j < 4 && grp[j] != 0xFFFFFFFFu) j++;
+        if (j < 4) grp[j] = b << 6 | h;
+        else hot_ids[r * kHot + h] = GNS_ID_NONE;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Query (count_min.go:240-254), export, heavy-hitter candidates
 // ---------------------------------------------------------------------------
@@ -1566,6 +1641,7 @@ struct gns_cm {
     uint32_t *ovf_cnt = nullptr;
     unsigned long long *stats = nullptr;  // [8]
     uint32_t *hot_ids = nullptr;          // [d][kHot] designated buckets for the next batch
+    uint32_t *hot_tab = nullptr;          // [d][kHotTab] their lookup groups
     long long *segtot = nullptr;          // [d*kHot][kHotSegs][2]
     uint32_t *hflag = nullptr, *hhist = nullptr, *hthr = nullptr, *hcnt = nullptr;
     HotSum *hsum = nullptr;               // [d*kHot][nblk_max]
@@ -1605,7 +1681,7 @@ int cm_free_all(gns_cm *cm) {
     dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
     dfree(cm->entries); dfree(cm->entries2); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats); dfree(cm->stage);
     dfree(cm->hot_ids); dfree(cm->segtot); dfree(cm->hflag); dfree(cm->hhist); dfree(cm->hthr); dfree(cm->hcnt);
-    dfree(cm->hsum); dfree(cm->hflag2); dfree(cm->hres); dfree(cm->chk);
+    dfree(cm->hsum); dfree(cm->hflag2); dfree(cm->hres); dfree(cm->chk); dfree(cm->hot_tab);
     if (cm->h_pin) (void)hipHostFree(cm->h_pin);
     cm->timer.destroy();
     if (cm->stream) (void)hipStreamDestroy(cm->stream);
@@ -1620,6 +1696,7 @@ int cm_reset_state(gns_cm *cm) {
     GNS_HIP(hipMemsetAsync(cm->Fs, 0xFF, cells * 4, cm->stream));
     GNS_HIP(hipMemsetAsync(cm->D.rec, 0, cm->dict_slots * cm->D.RW * 4, cm->stream));
     GNS_HIP(hipMemsetAsync(cm->hot_ids, 0xFF, (size_t)cm->g.d * kHot * 4, cm->stream));
+    GNS_HIP(hipMemsetAsync(cm->hot_tab, 0xFF, (size_t)cm->g.d * kHotTab * 4, cm->stream));
     GNS_HIP(hipMemsetAsync(cm->hhist, 0, (size_t)cm->g.d * 33 * 4, cm->stream));
     cm->warm = false;
     return GNS_OK;
@@ -1642,11 +1719,16 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.in = in; a.n = n; a.kp = cm->kp; a.g = g; a.D = cm->D; a.epoch = cm->epoch;
         a.keyid = cm->keyid; a.idx = cm->idx; a.pend = cm->pend[0]; a.pend_cnt = cm->pcnt[0];
         a.pend_total = cm->ptotal; a.hist = cm->hist; a.nblk = nblk; a.hot_ids = cm->hot_ids;
-        a.Fc = cm->Fc; a.Fs = cm->Fs; a.hsum = cm->hsum;
+        a.Fc = cm->Fc; a.Fs = cm->Fs; a.hsum = cm->hsum; a.hot_tab = cm->hot_tab;
         a.stats = cm->stats;
         ScopedStage st(cm->timer, 0);
-        hipLaunchKernelGGL((k_extract<KIND, MODE>), dim3(nblk), dim3(kExThreads),
-                           extract_lds_bytes(g.nbins_all, g.d), s, a);
+        const size_t lds = extract_lds_bytes(g.nbins_all, g.d);
+        if (cm->K == 37)
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 37>), dim3(nblk), dim3(kExThreads), lds, s, a);
+        else if (cm->K == 16)
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 16>), dim3(nblk), dim3(kExThreads), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 0>), dim3(nblk), dim3(kExThreads), lds, s, a);
         GNS_HIP(hipGetLastError());
     }
     // K1b: resolve parked packets until none remain
@@ -1668,7 +1750,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.in = in; a.n = n; a.kp = cm->kp; a.D = cm->D; a.epoch = cm->epoch; a.keyid = cm->keyid;
         a.pend_in = cm->pend[cur]; a.cnt_in = cm->pcnt[cur];
         a.pend_out = cm->pend[cur ^ 1]; a.cnt_out = cm->pcnt[cur ^ 1]; a.total_out = cm->ptotal + (cur ^ 1);
-        a.stats = cm->stats;
+        a.stats = cm->stats; a.g = g;
         ScopedStage st(cm->timer, 1);
         hipLaunchKernelGGL((k_resolve<KIND, MODE>), dim3(nblk), dim3(kExThreads), 0, s, a);
         GNS_HIP(hipGetLastError());
@@ -1749,6 +1831,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         hipLaunchKernelGGL(k_hot_hist, dim3(grid), dim3(256), 0, s, cm->C, g, cm->hhist);
         hipLaunchKernelGGL(k_hot_pick, dim3(1), dim3(512), 0, s, cm->hhist, g, cm->hthr, cm->hcnt, cm->hot_ids);
         hipLaunchKernelGGL(k_hot_collect, dim3(grid), dim3(256), 0, s, cm->C, g, cm->hthr, cm->hcnt, cm->hot_ids);
+        hipLaunchKernelGGL(k_hot_table, dim3(1), dim3(64), 0, s, g, cm->hot_ids, cm->hot_tab);
         GNS_HIP(hipGetLastError());
     }
     cm->warm = true;
@@ -1843,6 +1926,9 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         if (g.d > 8) { set_error("depth %u > 8 not supported", g.d); rc = GNS_E_ARG; break; }
         if ((rc = make_plan(p->flow, p->key_bytes, &cm->kp)) != GNS_OK) break;
         cm->K = cm->kp.K;
+        if (g.w >= (1u << 26)) {  // designated-bucket table entries hold bucket << 6
+            set_error("width %u >= 2^26 is not supported", g.w); rc = GNS_E_RANGE; break;
+        }
         g.pow2 = (g.w & (g.w - 1)) == 0;
         g.wmask = g.pow2 ? g.w - 1 : 0;
         uint32_t tb = kTileBitsMax;
@@ -1883,7 +1969,8 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         cm->dict_slots = slots;
         cm->D.mask = (uint32_t)(slots - 1);
         cm->D.K = cm->K;
-        cm->D.RW = dict_record_words(cm->K);
+        cm->D.RW = dict_record_words_cm(cm->K);
+        cm->D.bw = cm->D.RW == 16 && 1 + (cm->K + 3) / 4 <= 12 ? 1u : 0u;
         cm->D.seed = 0x2545F491u;
         if ((rc = dalloc_t(&cm->D.rec, slots * cm->D.RW)) != GNS_OK) break;
         // batch buffers
@@ -1908,7 +1995,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (rc = dalloc_t(&cm->hhist, g.d * 33)) || (rc = dalloc_t(&cm->hthr, 8)) || (rc = dalloc_t(&cm->hcnt, 8)) ||
             (rc = dalloc_t(&cm->hsum, (uint64_t)g.d * kHot * cm->nblk_max)) ||
             (rc = dalloc_t(&cm->hflag2, g.d * kHot + 2)) || (rc = dalloc_t(&cm->hres, g.d * kHot * 2)) ||
-            (rc = dalloc_t(&cm->chk, kChkCap)))
+            (rc = dalloc_t(&cm->chk, kChkCap)) || (rc = dalloc_t(&cm->hot_tab, (size_t)g.d * kHotTab)))
             break;
         if (hipHostMalloc(reinterpret_cast<void **>(&cm->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;

@@ -87,6 +87,14 @@ inline uint32_t dict_record_words(uint32_t K) {
 #endif
 }
 
+// Count-Min records: 16 words whenever the key leaves words 12..15 free, which
+// then cache the flow's bucket indices of rows 0..3 (written by the claimer),
+// so a packet of a known flow needs no per-row MurmurHash3.
+inline uint32_t dict_record_words_cm(uint32_t K) {
+    const uint32_t w = 1 + (K + 3) / 4;
+    return (K > 12 && w <= 12) ? 16u : dict_record_words(K);
+}
+
 inline uint32_t ceil_log2(uint64_t x) {
     uint32_t b = 0;
     while ((1ull << b) < x) b++;

@@ -202,6 +202,45 @@ __device__ __forceinline__ int parse_record(const uint32_t (&w)[16], uint32_t wi
     return st;
 }
 
+// Branch-free fast path for the dominant record shape: untagged Ethernet II,
+// IPv4 with IHL 5, not a fragment, TCP (data offset inside the datagram) or
+// UDP (no tunnel port).  Returns true and fills tw exactly as parse_record
+// would; false means "use parse_record" (tw is then garbage).
+__device__ __forceinline__ bool parse_fast_ipv4(const uint32_t (&w)[16], uint32_t wirelen, uint32_t (&tw)[10]) {
+    constexpr int OFF = 14;
+    const uint32_t type = rec_be16<12>(w);
+    const uint32_t ihl = rec_byte<OFF>(w) & 15u;
+    const uint32_t l2len = wirelen > 14u ? wirelen - 14u : 0u;
+    uint32_t tot = rec_be16<OFF + 2>(w);
+    tot = tot == 0 ? l2len : tot;
+    const uint32_t proto = rec_byte<OFF + 9>(w);
+    const uint32_t frag = rec_be16<OFF + 6>(w);
+    const uint32_t avail = (tot < l2len ? tot : l2len) - 20u;  // wraps when < 20: rejected below
+    const uint32_t doff = rec_byte<OFF + 32>(w) >> 4;
+    const uint32_t sp = rec_be16<OFF + 20>(w), dp = rec_be16<OFF + 22>(w);
+    const bool tcp = proto == 6u && avail >= 20u && doff >= 5u && doff * 4u <= avail;
+    const bool udp = proto == 17u && avail >= 8u && !udp_tunnel_port(sp) && !udp_tunnel_port(dp);
+    const bool ok = type == 0x0800u && ihl == 5u && (frag & 0x3FFFu) == 0 && tot >= 20u && l2len >= 20u &&
+                    (tcp || udp);
+    tw[0] = rec_u32<OFF + 12>(w); tw[1] = 0; tw[2] = 0; tw[3] = 0;
+    tw[4] = rec_u32<OFF + 16>(w); tw[5] = 0; tw[6] = 0; tw[7] = 0;
+    set_ports(tw, sp, dp, proto);
+    tw[9] |= 4u << 24 | 4u << 16;
+    return ok;
+}
+
+// parse_record with the fast path first; the general decoder runs only when
+// some active lane of the wave needs it.
+__device__ __forceinline__ int parse_record_fast(const uint32_t (&w)[16], uint32_t wirelen, bool valid,
+                                                 uint32_t (&tw)[10]) {
+    const bool fast = parse_fast_ipv4(w, wirelen, tw);
+    int st = PARSE_OK;
+    if (__ballot(valid && !fast)) {
+        if (valid && !fast) st = parse_record(w, wirelen, tw);
+    }
+    return st;
+}
+
 // byte idx (0..36) of the canonical tuple; 255 (or >= 40) -> 0
 __device__ __forceinline__ uint32_t tuple_byte(const uint32_t (&tw)[10], uint32_t idx) {
     uint32_t w = 0;

@@ -115,7 +115,7 @@ __device__ __forceinline__ int load_tuple(const InputDesc &in, uint64_t p, uint3
             uint4 v = r[i];
             w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
         }
-        return parse_record(w, in.sizes[p], tw);
+        return parse_record_fast(w, in.sizes[p], true, tw);
     } else {
         const uint4 s = *reinterpret_cast<const uint4 *>(in.src16 + p * 16);
         const uint4 d = *reinterpret_cast<const uint4 *>(in.dst16 + p * 16);
@@ -182,6 +182,7 @@ struct DictDev {
     uint32_t RW;       // record words: 4, 8 or 16 (a record never straddles a 64-byte line)
     uint32_t seed;     // slot hash seed
     uint32_t K;        // key bytes
+    uint32_t bw;       // Count-Min: words 12..15 cache the flow's row 0..3 buckets
 };
 
 enum { DICT_FOUND = 0, DICT_PENDING = 1, DICT_FULL = 2, DICT_ABSENT = 3 };
