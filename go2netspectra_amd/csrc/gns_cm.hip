@@ -251,12 +251,41 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
     const uint64_t end = min(a.n, beg + kChunk);
     const bool bw = a.D.bw != 0;
     uint32_t n_ok = 0;
+    // header records: the next iteration's record is loaded while this one's
+    // dictionary probe is in flight (two memory latencies overlap, not add)
+    uint4 hv[4];
+    uint32_t hsz = 0;
+    if constexpr (KIND == IN_HDR) {
+        const uint64_t pc = min(beg + tid, end - 1);
+        const uint4 *r = reinterpret_cast<const uint4 *>(a.in.hdr + pc * 16);
+#pragma unroll
+        for (int i = 0; i < 4; i++) hv[i] = r[i];
+        hsz = a.in.sizes[pc];
+    }
     for (uint64_t p0 = beg; p0 < end; p0 += kExThreads) {  // wave-uniform trip count
         const uint64_t p = p0 + tid;
         bool ok = p < end;
         uint32_t kw[GNS_KWMAX];
+        uint32_t cw[16], csz = 0;
+        if constexpr (KIND == IN_HDR) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) { cw[4 * i] = hv[i].x; cw[4 * i + 1] = hv[i].y; cw[4 * i + 2] = hv[i].z; cw[4 * i + 3] = hv[i].w; }
+            csz = hsz;
+            const uint64_t pc = min(p + kExThreads, end - 1);
+            const uint4 *r = reinterpret_cast<const uint4 *>(a.in.hdr + pc * 16);
+#pragma unroll
+            for (int i = 0; i < 4; i++) hv[i] = r[i];
+            hsz = a.in.sizes[pc];
+        }
         if (ok) {
-            const int st = packet_key<KIND, MODE>(a.in, K, s_src, p, kw);
+            int st;
+            if constexpr (KIND == IN_HDR) {
+                uint32_t tw[10];
+                st = parse_record_fast(cw, csz, true, tw);
+                if (st == PARSE_OK) make_key_m<MODE, GNS_KWMAX>(K, s_src, tw, kw);
+            } else {
+                st = packet_key<KIND, MODE>(a.in, K, s_src, p, kw);
+            }
             if (st != PARSE_OK) {
                 a.keyid[p] = GNS_ID_NONE;
                 atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
@@ -303,7 +332,9 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
             for (uint32_t rr = 0; rr < 4; rr++)
                 if (rr < d) tp[12 + rr] = bk[rr];
         }
-        const uint32_t sz = ok ? a.in.sizes[p] : 0u;
+        uint32_t sz = 0;
+        if constexpr (KIND == IN_HDR) sz = ok ? csz : 0u;
+        else sz = ok ? a.in.sizes[p] : 0u;
         n_ok += ok ? 1u : 0u;
 #pragma unroll
         for (uint32_t rr = 0; rr < 8; rr++) {
@@ -571,6 +602,14 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
         s_goff[i] = a.offsets[gb * a.nblk + blk];
     }
     for (uint32_t t = tid; t < kScWaves * LB; t += kScThreads) s_cnt[t] = 0;
+    // bin codes of the next (round, row) step are loaded one step ahead, so
+    // their latency hides behind the current step's LDS phases
+    uint32_t bsn[kScItems];
+#pragma unroll
+    for (int i = 0; i < kScItems; i++) {
+        const uint64_t p = beg + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
+        bsn[i] = a.idx[p < end ? p : end - 1];
+    }
     for (uint64_t rb = beg; rb < end; rb += kScRound) {
         // flow ids and sizes once per round (clamped loads, one latency)
         uint32_t ids[kScItems], szs[kScItems];
@@ -585,9 +624,17 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
             __syncthreads();
             uint32_t bs[kScItems];
 #pragma unroll
-            for (int i = 0; i < kScItems; i++) {
-                const uint64_t p = rb + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
-                bs[i] = a.idx[(uint64_t)r * a.n + (p < end ? p : end - 1)];
+            for (int i = 0; i < kScItems; i++) bs[i] = bsn[i];
+            {
+                const uint32_t nr = r + 1 < d ? r + 1 : 0u;
+                const uint64_t nrb = r + 1 < d ? rb : rb + kScRound;
+                if (nrb < end) {
+#pragma unroll
+                    for (int i = 0; i < kScItems; i++) {
+                        const uint64_t p = nrb + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
+                        bsn[i] = a.idx[(uint64_t)nr * a.n + (p < end ? p : end - 1)];
+                    }
+                }
             }
             uint64_t ent[kScItems];
             uint32_t bin[kScItems], rank[kScItems];
@@ -732,7 +779,11 @@ struct ApplyArgs {
     uint32_t *C, *Fc, *S, *Fs;
 };
 
-constexpr uint64_t kM21 = (1ull << 21) - 1;
+// accN per bucket and chunk: n [0,14) | n_foreign_count [14,28) | n_foreign_size
+// [28,42) | force (size escape) bit 42
+constexpr uint64_t kM14 = (1ull << 14) - 1;
+constexpr uint32_t kAccForce = 42;
+static_assert(kApChunk < (1u << 14), "accN field widths");
 #ifndef GNS_REP_CAP
 #define GNS_REP_CAP 1536
 #endif
@@ -813,6 +864,16 @@ struct ApplyLds {
     uint32_t s_any, s_nlist;
 };
 
+__device__ __forceinline__ void decode_entry(const uint64_t *ovf, uint64_t e, uint32_t &k, uint32_t &s) {
+    const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+    if (lo & kOvfFlag) {
+        const uint64_t ov = ovf[lo & ~kOvfFlag];
+        k = (uint32_t)ov; s = (uint32_t)(ov >> 32);
+    } else {
+        k = lo; s = hi >> kEntShift;
+    }
+}
+
 // Updates ent[beg, end) (stream order) of one LDS tile: buckets cbase .. cbase+tn-1.
 __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, const uint64_t *ent, uint32_t beg,
                                            uint32_t end, uint64_t cbase, uint32_t tn) {
@@ -859,7 +920,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             if (v[j] && !ovf) {
                 const uint32_t s = hi >> kEntShift;
                 const bool oc = lo != sFc[b], os = lo != sFs[b];
-                incN = 1ull | (uint64_t)oc << 21 | (uint64_t)os << 42;
+                incN = 1ull | (uint64_t)oc << 14 | (uint64_t)os << 28;
                 incS = os ? (uint64_t)s << 32 : (uint64_t)s;
             }
             // heavy bins: most lanes of a wave hit one bucket -> one LDS atomic
@@ -883,7 +944,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             }
             if (v[j] && ovf) {  // size >= 2^20-1: always replayed
                 atomicAdd(&accN[b], 1ull);
-                atomicOr(&accN[b], 1ull << 63);
+                atomicOr(&accN[b], 1ull << kAccForce);
             }
         }
         // prefetch the next chunk while this one is decided / replayed
@@ -898,10 +959,10 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
         for (uint32_t i = tid; i < tn; i += kApThreads) {
             const uint64_t an = accN[i];
             if (!an) continue;
-            const uint32_t n = (uint32_t)(an & kM21);
-            const uint32_t noc = (uint32_t)((an >> 21) & kM21);
-            const uint32_t nos = (uint32_t)((an >> 42) & kM21);
-            const bool force = (an >> 63) != 0;
+            const uint32_t n = (uint32_t)(an & kM14);
+            const uint32_t noc = (uint32_t)((an >> 14) & kM14);
+            const uint32_t nos = (uint32_t)((an >> 28) & kM14);
+            const bool force = ((an >> kAccForce) & 1u) != 0;
             const uint64_t as = accS[i];
             const uint32_t so = (uint32_t)as, sx = (uint32_t)(as >> 32);
             uint32_t rep = 0;
@@ -1183,15 +1244,6 @@ __device__ __forceinline__ void hot_seg_range(uint32_t beg, uint32_t end, uint32
     se = min(end, sb + per);
 }
 
-__device__ __forceinline__ void decode_entry(const uint64_t *ovf, uint64_t e, uint32_t &k, uint32_t &s) {
-    const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
-    if (lo & kOvfFlag) {
-        const uint64_t ov = ovf[lo & ~kOvfFlag];
-        k = (uint32_t)ov; s = (uint32_t)(ov >> 32);
-    } else {
-        k = lo; s = hi >> kEntShift;
-    }
-}
 
 // block (256) reduction of two int64
 __device__ __forceinline__ void block_sum2(long long &x, long long &y, long long *sh /*8*/) {
