@@ -5,14 +5,14 @@ usage: pmc_traffic.py FETCH_CSV WRITE_CSV [out.json]
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC_EA0_RDREQ/WRREQ x 64 B).
 MI355X_MICROARCH.md (HBM section): on gfx950 FETCH_SIZE reports half of the
-bytes of wide coalesced streaming reads, so reads are doubled.  The median
-over each kernel's dispatches is taken (cold-start dispatches excluded by
-the median).  Output keys are bench.py stage names.
+bytes of wide coalesced streaming reads, so reads are doubled.  The largest
+dispatch of each kernel is taken: the bench's full 100M-packet batches (the
+cold-start batch and the early-exit launches of the hot fallback path are
+smaller).  Output keys are bench.py stage names.
 """
 import collections
 import csv
 import json
-import statistics
 import sys
 
 STAGE = {"k_extract": "extract", "k_resolve": "resolve", "k_scatter": "scatter", "k_apply": "apply",
@@ -31,8 +31,8 @@ def main():
     fetch, write = load(sys.argv[1]), load(sys.argv[2])
     out = {}
     for k in sorted(set(fetch) | set(write)):
-        f = statistics.median(fetch.get(k, [0.0])) * 2.0
-        w = statistics.median(write.get(k, [0.0]))
+        f = max(fetch.get(k, [0.0])) * 2.0
+        w = max(write.get(k, [0.0]))
         rec = {"fetch_bytes_x2": round(f), "write_bytes": round(w), "bytes": round(f + w),
                "dispatches": len(fetch.get(k, []))}
         out[STAGE.get(k, k)] = rec
