@@ -53,12 +53,15 @@ constexpr uint32_t kMaxBinsAll = 4096;               // d * bins per row (k_orde
 constexpr int kExThreads = 256;
 constexpr uint32_t kChunk = 16384;                  // packets per K1/K3 block
 #ifndef GNS_SC_THREADS
-#define GNS_SC_THREADS 256
+#define GNS_SC_THREADS 512
 #endif
 constexpr int kScThreads = GNS_SC_THREADS;          // K3 block
 constexpr int kScWaves = kScThreads / 64;
-constexpr int kScItems = 16;
-constexpr uint32_t kScRound = kScThreads * kScItems; // 8192 updates staged in LDS per round
+#ifndef GNS_SC_ITEMS
+#define GNS_SC_ITEMS 8
+#endif
+constexpr int kScItems = GNS_SC_ITEMS;
+constexpr uint32_t kScRound = kScThreads * kScItems; // 4096 updates staged in LDS per round
 constexpr int kApThreads = GNS_AP_THREADS;
 constexpr int kApWaves = kApThreads / 64;
 constexpr int kApItems = GNS_AP_ITEMS;
@@ -567,10 +570,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, u
     return base + inc - v;
 }
 
-// LDS layout of k_scatter (dynamic): s_cnt[kScWaves][LB], s_rstart[LB], s_goff[d][LB],
-// s_ent[kScRound] (u64), s_bin[kScRound] (u16)
+// LDS layout of k_scatter (dynamic): s_cnt[kScWaves][LB], s_rstart[LB], s_dbase[LB],
+// s_goff[d][LB], s_ent[kScRound] (u64), s_bin[kScRound] (u16)
 __host__ __device__ inline size_t scatter_lds_head(uint32_t LB, uint32_t d) {
-    return ((size_t)(kScWaves + 1 + d) * LB * 4 + 15) / 16 * 16;
+    return ((size_t)(kScWaves + 2 + d) * LB * 4 + 15) / 16 * 16;
 }
 __host__ __device__ inline size_t scatter_lds_bytes(uint32_t LB, uint32_t d) {
     return scatter_lds_head(LB, d) + (size_t)kScRound * 8 + (size_t)kScRound * 2;
@@ -583,7 +586,8 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
     const uint32_t d = a.g.d;
     uint32_t *s_cnt = reinterpret_cast<uint32_t *>(smem);
     uint32_t *s_rstart = s_cnt + kScWaves * LB;
-    uint32_t *s_goff = s_rstart + LB;  // [d][LB]
+    uint32_t *s_dbase = s_rstart + LB;  // [LB] global index of staged slot 0 of each bin
+    uint32_t *s_goff = s_dbase + LB;    // [d][LB]
     uint64_t *s_ent = reinterpret_cast<uint64_t *>(smem + scatter_lds_head(LB, d));
     uint16_t *s_bin = reinterpret_cast<uint16_t *>(s_ent + kScRound);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -637,7 +641,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                 }
             }
             uint64_t ent[kScItems];
-            uint32_t bin[kScItems], rank[kScItems];
+            uint32_t bin[kScItems], rank[kScItems];  // bin 0xFFFF = no update
             // phase 1: stable per-wave ranks; wave w owns packets [rb + w*64*kScItems, ...), order (slot, lane)
 #pragma unroll
             for (int i = 0; i < kScItems; i++) {
@@ -675,14 +679,14 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                     const uint64_t m = __ballot(valid && ((t >> bit) & 1u));
                     peers &= ((t >> bit) & 1u) ? m : ~m;
                 }
+                const uint32_t before = __popcll(peers & lt_mask);
                 uint32_t rk = 0;
                 if (valid) {
-                    const uint32_t before = __popcll(peers & lt_mask);
                     rk = s_cnt[wave * LB + t] + before;
                     if (before == 0) s_cnt[wave * LB + t] += __popcll(peers);
                 }
                 ent[i] = e;
-                bin[i] = valid ? t : 0xFFFFFFFFu;
+                bin[i] = valid ? t : 0xFFFFu;
                 rank[i] = rk;
             }
             __syncthreads();
@@ -694,28 +698,29 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                 const uint32_t t = tid * TPT + j;
                 uint32_t c = 0;
                 if (t < LB) {
-                    for (uint32_t w = 0; w < (uint32_t)kScWaves; w++) {
-                        const uint32_t x = s_cnt[w * LB + t];
-                        s_cnt[w * LB + t] = c;
-                        c += x;
-                    }
+                    uint32_t x[kScWaves];
+#pragma unroll
+                    for (uint32_t w = 0; w < (uint32_t)kScWaves; w++) x[w] = s_cnt[w * LB + t];
+#pragma unroll
+                    for (uint32_t w = 0; w < (uint32_t)kScWaves; w++) { s_cnt[w * LB + t] = c; c += x[w]; }
                 }
                 tot[j] = c;
                 lsum += c;
             }
             uint32_t rtotal;
             uint32_t run = block_excl_scan<kScWaves>(lsum, s_w, &rtotal);
+            uint32_t *goff = s_goff + r * LB;
 #pragma unroll
             for (uint32_t j = 0; j < TPT; j++) {
                 const uint32_t t = tid * TPT + j;
-                if (t < LB) s_rstart[t] = run;
+                if (t < LB) { s_rstart[t] = run; s_dbase[t] = goff[t] - run; }
                 run += tot[j];
             }
             __syncthreads();
             // phase 3: stage in bin order
 #pragma unroll
             for (int i = 0; i < kScItems; i++) {
-                if (bin[i] != 0xFFFFFFFFu) {
+                if (bin[i] != 0xFFFFu) {
                     const uint32_t t = bin[i];
                     const uint32_t l = s_rstart[t] + s_cnt[wave * LB + t] + rank[i];
                     s_ent[l] = ent[i];
@@ -724,11 +729,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
             }
             __syncthreads();
             // phase 4: contiguous runs per bin to global
-            uint32_t *goff = s_goff + r * LB;
-            for (uint32_t s2 = tid; s2 < rtotal; s2 += kScThreads) {
-                const uint32_t t = s_bin[s2];
-                a.entries[goff[t] + (s2 - s_rstart[t])] = s_ent[s2];
-            }
+            for (uint32_t s2 = tid; s2 < rtotal; s2 += kScThreads) a.entries[s_dbase[s_bin[s2]] + s2] = s_ent[s2];
             __syncthreads();
 #pragma unroll
             for (uint32_t j = 0; j < TPT; j++) {
