@@ -264,6 +264,8 @@ def main():
     ap.add_argument("--depth", type=int, default=DEPTH, help="Count-Min depth (8 = configs[4] geometry)")
     ap.add_argument("--sketch", choices=["countmin", "superspread", "exact"], default="countmin",
                     help="superspread = configs[2]; exact = the exact aggregator (neither is the headline metric)")
+    ap.add_argument("--flows", type=int, default=1 << 20,
+                    help="distinct flows of the synthetic stream (experiments; the headline uses 2^20)")
     ap.add_argument("--host-input", action="store_true",
                     help="time inserts from host memory (PCIe-inclusive rate, for DESIGN.md)")
     args = ap.parse_args()
@@ -287,7 +289,7 @@ def main():
     if args.sketch == "exact":
         return bench_exact(args, torch, dist, world, rank, local)
     n = args.packets
-    syn = SyntheticTraffic(shard=rank, nshards=world, device=local)
+    syn = SyntheticTraffic(flows=args.flows, shard=rank, nshards=world, device=local)
     hdr, wl = syn.generate(n)
     batch = args.batch or n
     cm = CountMin(args.width, args.depth, 1 << 20, 1000, flow_fields=FIELDS, seeds=row_seeds(args.depth),
@@ -373,6 +375,9 @@ def main():
         line["config"]["workload"] = (f"Count-Min d={args.depth} w={wl2} (configs[4] geometry when d=8 w=2^24), "
                                       f"100M Zipf(1.1) 5-tuple headers in HBM per GPU, bit-exact counters")
         line["note"] = "not the headline metric (BASELINE.json metric is d=4 w=2^20)"
+    if args.flows != 1 << 20:
+        line["config"]["flows"] = args.flows
+        line["note"] = "not the headline metric (BASELINE.json stream has 2^20 flows)"
     if args.host_input:
         line["metric"] = "Mpackets/s CMS update, HOST-resident input (PCIe H2D inclusive), d=4 w=2^20"
         line["note"] = "not the headline metric: inputs start in pinned host memory"

@@ -274,11 +274,6 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; i++) { cw[4 * i] = hv[i].x; cw[4 * i + 1] = hv[i].y; cw[4 * i + 2] = hv[i].z; cw[4 * i + 3] = hv[i].w; }
             csz = hsz;
-            const uint64_t pc = min(p + kExThreads, end - 1);
-            const uint4 *r = reinterpret_cast<const uint4 *>(a.in.hdr + pc * 16);
-#pragma unroll
-            for (int i = 0; i < 4; i++) hv[i] = r[i];
-            hsz = a.in.sizes[pc];
         }
         if (ok) {
             int st;
@@ -301,9 +296,35 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
         uint32_t rec[16];
         int res = CM_FULL;
         uint32_t out = 0;
+        // first dictionary probe issued BEFORE the next record's prefetch: the
+        // probe's wait then leaves the prefetch in flight (vmcnt counts in order)
+        const uint32_t slot0 = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
+        uint4 r4[4];
         if (ok) {
-            const uint32_t slot0 = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
-            res = cm_find_or_claim(a.D, kw, K, slot0, a.epoch, &out, rec);
+            const uint4 *q = reinterpret_cast<const uint4 *>(a.D.rec + (size_t)slot0 * a.D.RW);
+#pragma unroll
+            for (int i = 0; i < 4; i++) r4[i] = (4u * i < a.D.RW) ? q[i] : make_uint4(0, 0, 0, 0);
+        }
+        if constexpr (KIND == IN_HDR) {
+            const uint64_t pc = min(p + kExThreads, end - 1);
+            const uint4 *r = reinterpret_cast<const uint4 *>(a.in.hdr + pc * 16);
+#pragma unroll
+            for (int i = 0; i < 4; i++) hv[i] = r[i];
+            hsz = a.in.sizes[pc];
+        }
+        if (ok) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                rec[4 * i] = r4[i].x; rec[4 * i + 1] = r4[i].y; rec[4 * i + 2] = r4[i].z; rec[4 * i + 3] = r4[i].w;
+            }
+            const uint32_t tag = rec[0];
+            bool eq = tag != 0 && tag != a.epoch;
+#pragma unroll
+            for (int i = 0; i < GNS_KWMAX; i++)
+                if ((uint32_t)i < ((K + 3) >> 2)) eq = eq && (rec[1 + i] == kw[i]);
+            if (tag == a.epoch) { res = CM_PENDING; out = slot0; }
+            else if (eq) { res = CM_FOUND; out = slot0; }
+            else res = cm_find_or_claim(a.D, kw, K, tag == 0 ? slot0 : ((slot0 + 1u) & a.D.mask), a.epoch, &out, rec);
             if (res == CM_FULL) {
                 a.keyid[p] = GNS_ID_NONE;
                 atomicAdd(&s_full, 1u);
