@@ -77,9 +77,10 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t *ctr, bool want) {
 
 // flow key (kwf) and merged key flow‖elem (kwm) of packet p.  MF/MM: plan
 // modes of the flow and merged layouts (SLICE0 for SrcIP / SrcIP‖DstIP).
-template <int KIND, int MF, int MM>
+template <int KIND, int MF, int MM, int KF = 0, int KM = 0>
 __device__ __forceinline__ int ss_keys(const SsExtractArgs &a, const uint8_t *s_srcf, const uint8_t *s_srcm,
                                        uint64_t p, uint32_t (&kwf)[GNS_KWMAX], uint32_t (&kwm)[kSsNW]) {
+    const uint32_t Kf = KF ? (uint32_t)KF : a.g.Kf, Km = KM ? (uint32_t)KM : a.g.Km;
     if constexpr (KIND == IN_KEYS) {
         const uint8_t *f = a.in.keys + p * a.in.stride;
         const uint8_t *e = a.in.keys2 + p * a.in.stride2;
@@ -102,15 +103,20 @@ __device__ __forceinline__ int ss_keys(const SsExtractArgs &a, const uint8_t *s_
         uint32_t tw[10];
         const int st = load_tuple<KIND>(a.in, p, tw);
         if (st != PARSE_OK) return st;
-        make_key_m<MF, GNS_KWMAX>(a.g.Kf, s_srcf, tw, kwf);
-        make_key_m<MM, kSsNW>(a.g.Km, s_srcm, tw, kwm);
+        make_key_m<MF, GNS_KWMAX>(Kf, s_srcf, tw, kwf);
+        make_key_m<MM, kSsNW>(Km, s_srcm, tw, kwm);
         return PARSE_OK;
     }
 }
 
 // S1: keys, flow id, per-row HLL encode test against the batch-entry registers
-template <int KIND, int MF, int MM>
+// KF/KM: flow / merged key bytes when known at compile time (16/32 for the
+// default task SrcIP / SrcIP|DstIP), 0 = runtime.
+template <int KIND, int MF, int MM, int KF, int KM>
 __global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
+    const uint32_t Kf = KF ? (uint32_t)KF : a.g.Kf, Km = KM ? (uint32_t)KM : a.g.Km;
+    const uint32_t mmask = a.g.m - 1u;
+    const bool mpow2 = (a.g.m & mmask) == 0;
     __shared__ uint8_t s_srcf[80], s_srcm[80];
     __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_cc;
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
@@ -124,17 +130,17 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
     uint32_t n_ok = 0;
     for (uint64_t p = beg + tid; p < end; p += kSsThreads) {
         uint32_t kwf[GNS_KWMAX], kwm[kSsNW];
-        const int st = ss_keys<KIND, MF, MM>(a, s_srcf, s_srcm, p, kwf, kwm);
+        const int st = ss_keys<KIND, MF, MM, KF, KM>(a, s_srcf, s_srcm, p, kwf, kwm);
         if (st != PARSE_OK) {
             a.flowid[p] = GNS_ID_NONE;
             atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
             continue;
         }
         uint32_t mkf[GNS_KWMAX], mkm[kSsNW];
-        mm3_premix<GNS_KWMAX>(kwf, a.g.Kf, mkf);
-        mm3_premix<kSsNW>(kwm, a.g.Km, mkm);
+        mm3_premix<GNS_KWMAX>(kwf, Kf, mkf);
+        mm3_premix<kSsNW>(kwm, Km, mkm);
         uint32_t out;
-        const int r = dict_find_or_claim(a.D, kwf, mm3_chain<GNS_KWMAX>(mkf, a.g.Kf, a.D.seed) & a.D.mask,
+        const int r = dict_find_or_claim(a.D, kwf, mm3_chain<GNS_KWMAX>(mkf, Kf, a.D.seed) & a.D.mask,
                                          a.epoch, &out);
         if (r == DICT_FULL) {
             a.flowid[p] = GNS_ID_NONE;
@@ -150,14 +156,15 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
         }
         n_ok++;
         for (uint32_t rr = 0; rr < a.g.d; rr++) {
-            const uint32_t j = ss_row_index(a.g, mm3_chain<GNS_KWMAX>(mkf, a.g.Kf, a.g.seeds[rr]));
+            const uint32_t j = ss_row_index(a.g, mm3_chain<GNS_KWMAX>(mkf, Kf, a.g.seeds[rr]));
             const uint64_t cell = (uint64_t)rr * a.g.w + j;
             uint32_t s0, s1;
             ss_hll_seeds(a.g.hll_master, cell, s0, s1);
-            const uint32_t h0 = mm3_chain<kSsNW>(mkm, a.g.Km, s0);  // geometricHash :66-70
+            const uint32_t h0 = mm3_chain<kSsNW>(mkm, Km, s0);  // geometricHash :66-70
             uint32_t lz = (h0 ? (uint32_t)__clz(h0) : 32u) + 1u;
             if (lz > a.g.maxv) lz = a.g.maxv;
-            const uint32_t idx = mm3_chain<kSsNW>(mkm, a.g.Km, s1) % a.g.m;  // :87-88
+            const uint32_t h1 = mm3_chain<kSsNW>(mkm, Km, s1);
+            const uint32_t idx = mpow2 ? (h1 & mmask) : h1 % a.g.m;  // :87-88
             const uint64_t seg = cell * a.g.m + idx;
             const bool want = lz > a.regs[seg];  // can encode only if above the batch-entry register
             const uint32_t q = wave_alloc(&s_cc, want);
@@ -479,7 +486,10 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     x.ckey = ss->ckey; x.cval = ss->cval; x.ccount = ss->counts; x.cblk = ss->cblk; x.stats = ss->stats;
     {
         ScopedStage st(ss->timer, 0);
-        hipLaunchKernelGGL((k_ss_extract<KIND, MF, MM>), dim3(nblk), dim3(kSsThreads), 0, s, x);
+        if (ss->g.Kf == 16 && ss->g.Km == 32)
+            hipLaunchKernelGGL((k_ss_extract<KIND, MF, MM, 16, 32>), dim3(nblk), dim3(kSsThreads), 0, s, x);
+        else
+            hipLaunchKernelGGL((k_ss_extract<KIND, MF, MM, 0, 0>), dim3(nblk), dim3(kSsThreads), 0, s, x);
         GNS_HIP(hipGetLastError());
     }
     int cur = 0;
