@@ -30,8 +30,15 @@ namespace gns {
 
 constexpr int kXThreads = 256;
 constexpr uint32_t kXChunk = 16384;
-constexpr uint32_t kXTab = 2048;   // LDS aggregation slots per block
-constexpr uint32_t kXProbe = 16;
+#ifndef GNS_XTAB_BITS
+#define GNS_XTAB_BITS 11
+#endif
+#ifndef GNS_XPROBE
+#define GNS_XPROBE 16
+#endif
+constexpr uint32_t kXTabBits = GNS_XTAB_BITS;
+constexpr uint32_t kXTab = 1u << kXTabBits;   // LDS aggregation slots per block
+constexpr uint32_t kXProbe = GNS_XPROBE;
 
 struct ExIn {
     InputDesc in;
@@ -176,46 +183,82 @@ struct ExAggArgs {
 // X2: per block, LDS hash aggregation keyed by flow id (Zipf: the heavy flows
 // collapse to one set of global atomics per block); flows that do not find a
 // slot within kXProbe probes go straight to global atomics.
+extern "C" __device__ unsigned long long __ockl_wfred_add_u64(unsigned long long);
+
+// first/last packet index of a flow: first only decreases and last only
+// increases, so a value read earlier that already beats the candidate proves
+// the atomic would not change anything (most flows were seen before).
+__device__ __forceinline__ void ex_first_last(const FlowState &f, uint32_t id, unsigned long long fst,
+                                              unsigned long long lst) {
+    if (__atomic_load_n(&f.first[id], __ATOMIC_RELAXED) > fst) atomicMin(&f.first[id], fst);
+    if (__atomic_load_n(&f.last[id], __ATOMIC_RELAXED) < lst) atomicMax(&f.last[id], lst);
+}
+
+// one (count, bytes, first, last) contribution of flow id into the block table
+// (or straight to the global arrays when its probe window is full)
+__device__ __forceinline__ void ex_agg_insert(const ExAggArgs &a, uint32_t *s_key, uint32_t *s_cnt, uint32_t *s_mn,
+                                              uint32_t *s_mx, unsigned long long *s_bytes, uint64_t beg,
+                                              uint32_t id, uint32_t cnt, unsigned long long bytes, uint32_t mn,
+                                              uint32_t mx) {
+    uint32_t slot = (id * 0x9E3779B1u) >> (32 - kXTabBits);
+    for (uint32_t k = 0; k < kXProbe; k++) {
+        uint32_t cur = s_key[slot];
+        if (cur == GNS_ID_NONE) {
+            const uint32_t prev = atomicCAS(&s_key[slot], GNS_ID_NONE, id);
+            cur = prev == GNS_ID_NONE ? id : prev;
+        }
+        if (cur == id) {
+            atomicAdd(&s_cnt[slot], cnt);
+            atomicAdd(&s_bytes[slot], bytes);
+            atomicMin(&s_mn[slot], mn);
+            atomicMax(&s_mx[slot], mx);
+            return;
+        }
+        slot = (slot + 1) & (kXTab - 1);
+    }
+    const unsigned long long g = a.pkt_base + beg;
+    atomicAdd(&a.f.pkts[id], (unsigned long long)cnt);
+    atomicAdd(&a.f.bytes[id], bytes);
+    ex_first_last(a.f, id, g + mn, g + mx);
+}
+
+// X2: per block, LDS hash aggregation keyed by flow id.  Zipf traffic puts
+// many lanes of a wave on one heavy flow: that group is reduced in registers
+// (count = popcount, bytes = DPP wave sum, first/last = lowest/highest lane)
+// and enters the table once; flows that do not find a slot within kXProbe
+// probes go straight to global atomics.
 __global__ __launch_bounds__(kXThreads) void k_ex_aggregate(ExAggArgs a) {
     __shared__ uint32_t s_key[kXTab], s_cnt[kXTab], s_mn[kXTab], s_mx[kXTab];
     __shared__ unsigned long long s_bytes[kXTab];
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
     for (uint32_t i = tid; i < kXTab; i += kXThreads) {
         s_key[i] = GNS_ID_NONE; s_cnt[i] = 0; s_bytes[i] = 0; s_mn[i] = 0xFFFFFFFFu; s_mx[i] = 0;
     }
     __syncthreads();
     const uint64_t beg = (uint64_t)blockIdx.x * kXChunk;
     const uint64_t end = min(a.n, beg + kXChunk);
-    for (uint64_t p = beg + tid; p < end; p += kXThreads) {
-        const uint32_t id = a.keyid[p];
-        if (id == GNS_ID_NONE) continue;
-        const uint32_t ln = a.len[p];
+    for (uint64_t p0 = beg; p0 < end; p0 += kXThreads) {  // wave-uniform trip count
+        const uint64_t p = p0 + tid;
+        const uint32_t id = p < end ? a.keyid[p] : GNS_ID_NONE;
+        const uint32_t ln = p < end ? a.len[p] : 0u;
         const uint32_t li = (uint32_t)(p - beg);
-        uint32_t slot = (id * 0x9E3779B1u) >> (32 - 11);
-        bool done = false;
-        for (uint32_t k = 0; k < kXProbe; k++) {
-            uint32_t cur = s_key[slot];
-            if (cur == GNS_ID_NONE) {
-                const uint32_t prev = atomicCAS(&s_key[slot], GNS_ID_NONE, id);
-                cur = prev == GNS_ID_NONE ? id : prev;
+        const uint64_t valid = __ballot(id != GNS_ID_NONE);
+        bool mine = id != GNS_ID_NONE;
+        if (valid) {
+            const uint32_t b0 = __builtin_amdgcn_readlane(id, __ffsll((unsigned long long)valid) - 1);
+            const uint64_t mm = __ballot(id == b0);
+            if (__popcll(mm) >= 8) {  // wave-uniform
+                const unsigned long long sb = __ockl_wfred_add_u64(id == b0 ? (unsigned long long)ln : 0ull);
+                const uint32_t first = (uint32_t)__ffsll((unsigned long long)mm) - 1u;
+                const uint32_t last = 63u - (uint32_t)__clzll((long long)mm);
+                const uint32_t lbase = li - lane;
+                if (lane == first)
+                    ex_agg_insert(a, s_key, s_cnt, s_mn, s_mx, s_bytes, beg, b0, (uint32_t)__popcll(mm), sb,
+                                  lbase + first, lbase + last);
+                mine = mine && id != b0;
             }
-            if (cur == id) {
-                atomicAdd(&s_cnt[slot], 1u);
-                atomicAdd(&s_bytes[slot], (unsigned long long)ln);
-                atomicMin(&s_mn[slot], li);
-                atomicMax(&s_mx[slot], li);
-                done = true;
-                break;
-            }
-            slot = (slot + 1) & (kXTab - 1);
         }
-        if (!done) {
-            const unsigned long long g = a.pkt_base + p;
-            atomicAdd(&a.f.pkts[id], 1ull);
-            atomicAdd(&a.f.bytes[id], (unsigned long long)ln);
-            atomicMin(&a.f.first[id], g);
-            atomicMax(&a.f.last[id], g);
-        }
+        if (mine) ex_agg_insert(a, s_key, s_cnt, s_mn, s_mx, s_bytes, beg, id, 1u, ln, li, li);
     }
     __syncthreads();
     const unsigned long long gb = a.pkt_base + beg;
@@ -224,8 +267,7 @@ __global__ __launch_bounds__(kXThreads) void k_ex_aggregate(ExAggArgs a) {
         if (id == GNS_ID_NONE) continue;
         atomicAdd(&a.f.pkts[id], (unsigned long long)s_cnt[i]);
         atomicAdd(&a.f.bytes[id], s_bytes[i]);
-        atomicMin(&a.f.first[id], gb + s_mn[i]);
-        atomicMax(&a.f.last[id], gb + s_mx[i]);
+        ex_first_last(a.f, id, gb + s_mn[i], gb + s_mx[i]);
     }
 }
 
