@@ -20,6 +20,7 @@
 //                   order-free aggregate fast path where provably exact,
 //                   sequential replay for the buckets where it is not.
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -600,7 +601,18 @@ __host__ __device__ inline size_t scatter_lds_bytes(uint32_t LB, uint32_t d) {
     return scatter_lds_head(LB, d) + (size_t)kScRound * 8 + (size_t)kScRound * 2;
 }
 
+#ifdef GNS_K3_PROF
+#define K3_MARK(i) do { if (threadIdx.x == 0) { const uint64_t tn_ = __builtin_amdgcn_s_memtime(); k3t[i] += tn_ - k3prev; k3prev = tn_; } } while (0)
+#else
+#define K3_MARK(i) do { } while (0)
+#endif
+// RANK 1: stable per-wave ranks from returning LDS adds; 0: ballot multisplit
+// (used when the lane-order probe fails on this device).
+template <int RANK>
 __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
+#ifdef GNS_K3_PROF
+    uint64_t k3t[5] = {0, 0, 0, 0, 0}, k3prev = __builtin_amdgcn_s_memtime();
+#endif
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t s_w[kScWaves];
     const uint32_t LB = a.g.ntiles + kHot;  // local bins of a row: tiles, then its hot buckets
@@ -663,6 +675,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
             }
             uint64_t ent[kScItems];
             uint32_t bin[kScItems], rank[kScItems];  // bin 0xFFFF = no update
+            K3_MARK(0);
             // phase 1: stable per-wave ranks; wave w owns packets [rb + w*64*kScItems, ...), order (slot, lane)
 #pragma unroll
             for (int i = 0; i < kScItems; i++) {
@@ -695,22 +708,29 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                     }
                     e = (uint64_t)((sf << kEntShift) | low) << 32 | lo;
                 }
-                uint64_t peers = __ballot(valid);
-                for (uint32_t bit = 0; bit < nbits; bit++) {
-                    const uint64_t m = __ballot(valid && ((t >> bit) & 1u));
-                    peers &= ((t >> bit) & 1u) ? m : ~m;
-                }
-                const uint32_t before = __popcll(peers & lt_mask);
                 uint32_t rk = 0;
-                if (valid) {
-                    rk = s_cnt[wave * LB + t] + before;
-                    if (before == 0) s_cnt[wave * LB + t] += __popcll(peers);
+                if constexpr (RANK == 1) {
+                    // returning LDS adds: same-address lanes of one instruction are
+                    // served in lane order (verified at create by k_lds_order_probe)
+                    if (valid) rk = atomicAdd(&s_cnt[wave * LB + t], 1u);
+                } else {
+                    uint64_t peers = __ballot(valid);
+                    for (uint32_t bit = 0; bit < nbits; bit++) {
+                        const uint64_t m = __ballot(valid && ((t >> bit) & 1u));
+                        peers &= ((t >> bit) & 1u) ? m : ~m;
+                    }
+                    const uint32_t before = __popcll(peers & lt_mask);
+                    if (valid) {
+                        rk = s_cnt[wave * LB + t] + before;
+                        if (before == 0) s_cnt[wave * LB + t] += __popcll(peers);
+                    }
                 }
                 ent[i] = e;
                 bin[i] = valid ? t : 0xFFFFu;
                 rank[i] = rk;
             }
             __syncthreads();
+            K3_MARK(1);
             // phase 2: per bin, exclusive prefix over waves; block scan over bins
             uint32_t tot[TPT];
             uint32_t lsum = 0;
@@ -738,6 +758,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                 run += tot[j];
             }
             __syncthreads();
+            K3_MARK(2);
             // phase 3: stage in bin order
 #pragma unroll
             for (int i = 0; i < kScItems; i++) {
@@ -749,6 +770,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                 }
             }
             __syncthreads();
+            K3_MARK(3);
             // phase 4: contiguous runs per bin to global
             for (uint32_t s2 = tid; s2 < rtotal; s2 += kScThreads) a.entries[s_dbase[s_bin[s2]] + s2] = s_ent[s2];
             __syncthreads();
@@ -760,8 +782,31 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                     for (uint32_t w = 0; w < (uint32_t)kScWaves; w++) s_cnt[w * LB + t] = 0;
                 }
             }
+            K3_MARK(4);
         }
     }
+#ifdef GNS_K3_PROF
+    if (threadIdx.x == 0 && !a.hot_mode) for (int i = 0; i < 5; i++) atomicAdd(&a.stats[11 + i], (unsigned long long)k3t[i]);
+#endif
+}
+
+// Does a returning LDS add serve the same-address lanes of one wave
+// instruction in lane order?  (K3's RANK 1 relies on it; measured on gfx950:
+// tools/lds_order.hip, 0 of 1.3e10 same-address lane pairs out of order.)
+__global__ __launch_bounds__(256) void k_lds_order_probe(uint32_t *viol, int iters) {
+    __shared__ uint32_t s[4][64], s_old[4][64], s_ad[4][64];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t x = (blockIdx.x * 256 + threadIdx.x) * 0x9E3779B1u + 12345u, v = 0;
+    for (int it = 0; it < iters; it++) {
+        s[w][lane] = 0;
+        x = x * 1664525u + 1013904223u;
+        const uint32_t ad = (x >> 16) % (1u + (uint32_t)it % 16u);
+        const uint32_t old = atomicAdd(&s[w][ad], 1u);
+        s_old[w][lane] = old;
+        s_ad[w][lane] = ad;
+        for (uint32_t j = 0; j < lane; j++) v += (s_ad[w][j] == ad && s_old[w][j] >= old) ? 1u : 0u;
+    }
+    if (v) atomicAdd(viol, v);
 }
 
 // Order bins by size (largest first) so the heavy bins start first.
@@ -1723,6 +1768,7 @@ struct gns_cm {
     uint32_t *hres = nullptr;             // [d*kHot][2]
     uint4 *chk = nullptr;                 // [kChkCap]
     bool warm = false;                    // a batch has run since create/reset
+    bool lds_ordered = false;             // k_lds_order_probe passed: K3 ranks by LDS adds
     uint32_t *h_pin = nullptr;            // pinned host mirror of small counters
     // staging for host inputs
     uint8_t *stage = nullptr;
@@ -1849,7 +1895,10 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.ovf_cnt = cm->ovf_cnt; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
         a.hot_mode = 0; a.hflag2 = cm->hflag2; a.hany = cm->hflag2 + g.d * kHot;
         ScopedStage st(cm->timer, 3);
-        hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
+        if (cm->lds_ordered)
+            hipLaunchKernelGGL(k_scatter<1>, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
+        else
+            hipLaunchKernelGGL(k_scatter<0>, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
         GNS_HIP(hipGetLastError());
     }
     // K4
@@ -1889,7 +1938,10 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
             a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
             a.ovf_cnt = cm->ovf_cnt; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
             a.hot_mode = 1; a.hflag2 = cm->hflag2; a.hany = h.hany;
-            hipLaunchKernelGGL(k_scatter, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
+            if (cm->lds_ordered)
+                hipLaunchKernelGGL(k_scatter<1>, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
+            else
+                hipLaunchKernelGGL(k_scatter<0>, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
         }
         hipLaunchKernelGGL(k_hot_sum, dim3(kHotSegs, g.d * kHot), dim3(256), 0, s, h);
         hipLaunchKernelGGL(k_hot_verify, dim3(kHotSegs, g.d * kHot), dim3(256), 0, s, h);
@@ -2076,6 +2128,22 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         }
         if (hipMemsetAsync(cm->stats, 0, 128, cm->stream) != hipSuccess) { rc = GNS_E_HIP; break; }
         if ((rc = cm_reset_state(cm)) != GNS_OK) break;
+        {   // lane-order probe for K3's ranking (GNS_K3_RANK=0 forces the ballot multisplit)
+            const char *env = getenv("GNS_K3_RANK");
+            uint32_t *viol = nullptr;
+            if ((rc = dalloc_t(&viol, 1)) != GNS_OK) break;
+            hipError_t e = hipMemsetAsync(viol, 0, 4, cm->stream);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(k_lds_order_probe, dim3(256), dim3(256), 0, cm->stream, viol, 64);
+                e = hipGetLastError();
+            }
+            uint32_t hv = 1;
+            if (e == hipSuccess) e = hipMemcpyAsync(&hv, viol, 4, hipMemcpyDeviceToHost, cm->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(cm->stream);
+            dfree(viol);
+            if (e != hipSuccess) { set_error("lds order probe: %s", hipGetErrorString(e)); rc = GNS_E_HIP; break; }
+            cm->lds_ordered = hv == 0 && !(env && env[0] == '0');
+        }
         if (hipStreamSynchronize(cm->stream) != hipSuccess) { set_error("sync failed"); rc = GNS_E_HIP; break; }
     } while (0);
     if (rc != GNS_OK) {
@@ -2306,6 +2374,11 @@ int gns_cm_counters(gns_cm *cm, uint64_t out[8]) {
     GNS_HIP(hipStreamSynchronize(cm->stream));
     unsigned long long h[16];
     GNS_HIP(hipMemcpy(h, cm->stats, sizeof(h), hipMemcpyDeviceToHost));
+#ifdef GNS_K3_PROF  // profiling build: K3 phase cycles (loads, rank, scan, stage, write)
+    for (int i = 0; i < 5; i++) out[i] = h[11 + i];
+    for (int i = 5; i < 8; i++) out[i] = h[i];
+    return GNS_OK;
+#endif
 #ifdef GNS_K4_PROF  // profiling build: K4 phase cycles (classify, decide, compact, replay), chunks, ...
     for (int i = 0; i < 4; i++) out[i] = h[8 + i];
     for (int i = 4; i < 8; i++) out[i] = h[i + 1];
