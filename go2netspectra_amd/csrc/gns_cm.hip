@@ -2134,7 +2134,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             if ((rc = dalloc_t(&viol, 1)) != GNS_OK) break;
             hipError_t e = hipMemsetAsync(viol, 0, 4, cm->stream);
             if (e == hipSuccess) {
-                hipLaunchKernelGGL(k_lds_order_probe, dim3(256), dim3(256), 0, cm->stream, viol, 64);
+                hipLaunchKernelGGL(k_lds_order_probe, dim3(64), dim3(256), 0, cm->stream, viol, 32);
                 e = hipGetLastError();
             }
             uint32_t hv = 1;
