@@ -261,3 +261,21 @@ def test_wide_rows_parity(gpu, oracle, w, d, K, nflows, n):
     assert np.array_equal(q, np.array([orc.query(bytes(f)) for f in flows[:2000]], np.uint64))
     hh = cm.heavy_hitters()
     assert [(h.Flow, h.Count) for h in hh.Count] == orc.heavy("count")
+
+
+@pytest.mark.parametrize("w,d,K,nflows,n", [
+    (65536, 4, 37, 50_000, 1_000_000),
+    (256, 2, 16, 2000, 100_000),
+])
+def test_ballot_rank_fallback_parity(gpu, oracle, monkeypatch, w, d, K, nflows, n):
+    """K3's ballot multisplit (used when the LDS lane-order probe fails; forced
+    here with GNS_K3_RANK=0) gives the same bit-exact state."""
+    monkeypatch.setenv("GNS_K3_RANK", "0")
+    rng = np.random.default_rng(w + 3 * d)
+    cm, orc = make_pair(oracle, w, d, K, batch_packets=n // 3)
+    keys, _, _ = zipf_keys(rng, n, nflows, K)
+    sizes = sizes_u32(rng, n)
+    cm.insert_keys(keys, sizes)
+    cm.flush()
+    orc.insert_keys(keys, sizes)
+    assert_same_state(cm, orc)
