@@ -224,8 +224,12 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) { return __ockl_wfred
 
 // K1: parse/encode, dictionary, row buckets, block histogram, hot summaries.
 // KB = key bytes when known at compile time (16 / 37), 0 = runtime a.kp.K.
-template <int KIND, int MODE, int KB>
-__global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
+// DD = depth when known at compile time (4: the rows loops unroll exactly), 0 = runtime
+#ifndef GNS_EX_MINW
+#define GNS_EX_MINW 5
+#endif
+template <int KIND, int MODE, int KB, int DD>
+__global__ __launch_bounds__(kExThreads, GNS_EX_MINW) void k_extract(ExtractArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xsm[];
     __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
     __shared__ uint8_t s_src[80];
@@ -239,7 +243,8 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
     uint32_t *s_hFs = s_hFc + NS, *s_nfc = s_hFs + NS, *s_nfs = s_nfc + NS, *s_smax = s_nfs + NS;
     stage_plan<MODE>(a.kp, s_src);
     const uint32_t K = KB ? (uint32_t)KB : a.kp.K;
-    const uint32_t d = a.g.d;
+    const uint32_t d = DD ? (uint32_t)DD : a.g.d;
+    constexpr uint32_t RMAX = DD ? (uint32_t)DD : 8u;
     for (uint32_t i = tid; i < d * kHotTab; i += kExThreads) s_tab[i] = a.hot_tab[i];
     for (uint32_t i = tid; i < a.g.nbins_all; i += kExThreads) s_hist[i] = 0;
     for (uint32_t i = tid; i < NS; i += kExThreads) {
@@ -291,15 +296,18 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
                 ok = false;
             }
         }
-        uint32_t mk[GNS_KWMAX];
-        mm3_premix<GNS_KWMAX>(kw, K, mk);
+        uint32_t slot0;
+        {   // the premixed key dies here; the rare rehash below recomputes it
+            uint32_t mk[GNS_KWMAX];
+            mm3_premix<GNS_KWMAX>(kw, K, mk);
+            slot0 = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
+        }
         uint32_t kid = kPendingId;  // flow id when already committed (pending: foreign to every owner)
         uint32_t rec[16];
         int res = CM_FULL;
         uint32_t out = 0;
         // first dictionary probe issued BEFORE the next record's prefetch: the
         // probe's wait then leaves the prefetch in flight (vmcnt counts in order)
-        const uint32_t slot0 = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
         uint4 r4[4];
         if (ok) {
             const uint4 *q = reinterpret_cast<const uint4 *>(a.D.rec + (size_t)slot0 * a.D.RW);
@@ -340,13 +348,15 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
             }
         }
         // row buckets: from the record's cache (rows 0..3 of a committed flow), else hashed
-        uint32_t bk[8];
+        uint32_t bk[RMAX];
         const bool cached = bw && res == CM_FOUND;
 #pragma unroll
-        for (uint32_t rr = 0; rr < 8; rr++) bk[rr] = (rr < 4 && cached) ? rec[12 + rr] : 0u;
-        if (__ballot(ok && !cached) || d > 4) {
+        for (uint32_t rr = 0; rr < RMAX; rr++) bk[rr] = (rr < 4 && cached) ? rec[12 + rr] : 0u;
+        if (__ballot(ok && !cached) || (RMAX > 4 && d > 4)) {
+            uint32_t mk[GNS_KWMAX];
+            mm3_premix<GNS_KWMAX>(kw, K, mk);
 #pragma unroll
-            for (uint32_t rr = 0; rr < 8; rr++) {
+            for (uint32_t rr = 0; rr < RMAX; rr++) {
                 if (rr >= d) break;
                 if (ok && (!cached || rr >= 4)) bk[rr] = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, K, a.g.seeds[rr]));
             }
@@ -362,7 +372,7 @@ __global__ __launch_bounds__(kExThreads) void k_extract(ExtractArgs a) {
         else sz = ok ? a.in.sizes[p] : 0u;
         n_ok += ok ? 1u : 0u;
 #pragma unroll
-        for (uint32_t rr = 0; rr < 8; rr++) {
+        for (uint32_t rr = 0; rr < RMAX; rr++) {
             if (rr >= d) break;
             uint32_t binid = 0xFFFFFFFFu;
             int h = -1;
@@ -1843,12 +1853,16 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.stats = cm->stats;
         ScopedStage st(cm->timer, 0);
         const size_t lds = extract_lds_bytes(g.nbins_all, g.d);
-        if (cm->K == 37)
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 37>), dim3(nblk), dim3(kExThreads), lds, s, a);
+        if (cm->K == 37 && g.d == 4)
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 4>), dim3(nblk), dim3(kExThreads), lds, s, a);
+        else if (cm->K == 37)
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 0>), dim3(nblk), dim3(kExThreads), lds, s, a);
+        else if (cm->K == 16 && g.d == 4)
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 16, 4>), dim3(nblk), dim3(kExThreads), lds, s, a);
         else if (cm->K == 16)
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 16>), dim3(nblk), dim3(kExThreads), lds, s, a);
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 16, 0>), dim3(nblk), dim3(kExThreads), lds, s, a);
         else
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 0>), dim3(nblk), dim3(kExThreads), lds, s, a);
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 0, 0>), dim3(nblk), dim3(kExThreads), lds, s, a);
         GNS_HIP(hipGetLastError());
     }
     // K1b: resolve parked packets until none remain
