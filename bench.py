@@ -266,8 +266,10 @@ def main():
                     help="superspread = configs[2]; exact = the exact aggregator (neither is the headline metric)")
     ap.add_argument("--flows", type=int, default=1 << 20,
                     help="distinct flows of the synthetic stream (experiments; the headline uses 2^20)")
-    ap.add_argument("--host-input", action="store_true",
-                    help="time inserts from host memory (PCIe-inclusive rate, for DESIGN.md)")
+    ap.add_argument("--host-input", nargs="?", const="headers", choices=["headers", "tuples"], default=None,
+                    help="time inserts from pinned host memory plus the per-window D2H of counters and heavy "
+                         "hitters (PCIe-inclusive rate, for DESIGN.md): 64-B header records or 41-B PacketInfo "
+                         "tuples (the live path's pre-parsed form)")
     args = ap.parse_args()
 
     import torch
@@ -300,15 +302,45 @@ def main():
         if world > 1:
             dist.barrier()
 
-    src_hdr, src_wl = hdr, wl
+    src_hdr, src_wl, tuples = hdr, wl, None
+    window_out = None
     if args.host_input:  # pinned host copies; the engine stages them H2D per device batch
-        src_hdr = torch.empty(hdr.shape, dtype=hdr.dtype, pin_memory=True)
-        src_wl = torch.empty(wl.shape, dtype=wl.dtype, pin_memory=True)
-        src_hdr.copy_(hdr)
-        src_wl.copy_(wl)
-        src_hdr, src_wl = src_hdr.numpy(), src_wl.numpy().view(np.uint32)
+        def pinned(a):
+            t = torch.empty(a.shape, dtype=a.dtype, pin_memory=True)
+            t.copy_(a)
+            return t
+        if args.host_input == "tuples":  # PacketInfo SoA (src16, dst16, ports, proto, length) = 41 B/packet
+            from go2netspectra_amd.packets import PacketBatch
+            h = hdr.view(torch.int32).view(torch.uint8)
+            src16 = torch.zeros((n, 16), dtype=torch.uint8, device=hdr.device)
+            dst16 = torch.zeros((n, 16), dtype=torch.uint8, device=hdr.device)
+            src16[:, :4] = h[:, 26:30]
+            dst16[:, :4] = h[:, 30:34]
+            sport = (h[:, 34].to(torch.int32) << 8 | h[:, 35].to(torch.int32)).to(torch.int16)
+            dport = (h[:, 36].to(torch.int32) << 8 | h[:, 37].to(torch.int32)).to(torch.int16)
+            tuples = PacketBatch(pinned(src16).numpy(), pinned(dst16).numpy(), pinned(sport).numpy().view(np.uint16),
+                                 pinned(dport).numpy().view(np.uint16), pinned(h[:, 23].contiguous()).numpy(),
+                                 pinned(wl).numpy().view(np.uint32))
+            del src16, dst16, sport, dport
+        else:
+            src_hdr, src_wl = pinned(hdr).numpy(), pinned(wl).numpy().view(np.uint32)
+        cnt_C = np.empty(args.depth * args.width, np.uint32)
+        cnt_S = np.empty(args.depth * args.width, np.uint32)
+
+        def window_out():  # per-window outputs back to the host: counter rows + heavy hitters (Snapshot)
+            cm.export_counters(cnt_C, cnt_S)
+            return cm.heavy_hitters_arrays()
+
+    def step():
+        if tuples is not None:
+            cm.insert_tuples(tuples)
+        else:
+            cm.insert_headers(src_hdr, src_wl)
+        if window_out is not None:
+            window_out()
+
     for _ in range(args.warmup):
-        cm.insert_headers(src_hdr, src_wl)
+        step()
         cm.flush()
     cm.set_timing(True)
     cm.stage_times(reset=True)
@@ -316,7 +348,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        cm.insert_headers(src_hdr, src_wl)
+        step()
     cm.flush()
     torch.cuda.synchronize()
     barrier()
@@ -379,8 +411,10 @@ def main():
         line["config"]["flows"] = args.flows
         line["note"] = "not the headline metric (BASELINE.json stream has 2^20 flows)"
     if args.host_input:
-        line["metric"] = "Mpackets/s CMS update, HOST-resident input (PCIe H2D inclusive), d=4 w=2^20"
-        line["note"] = "not the headline metric: inputs start in pinned host memory"
+        line["metric"] = ("Mpackets/s CMS update, HOST-resident input (PCIe H2D of %s + per-window D2H of "
+                          "counter rows and heavy hitters), d=4 w=2^20" % args.host_input)
+        line["note"] = "not the headline metric: inputs start in pinned host memory, outputs end in host memory"
+        line["config"]["host_input"] = args.host_input
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(hdr, wl, width=args.width, depth=args.depth)
     elif rank == 0:

@@ -171,6 +171,22 @@ class CountMin:
             return 0  # bytes.Equal against FS-byte fingerprints never matches
         return int(self.query_many(np.frombuffer(bytes(flow), np.uint8).reshape(1, -1))[0])
 
+    def heavy_hitters_arrays(self):
+        """HeavyHitters as arrays (count flows [n,K], counts, size flows, sizes): the
+        snapshot handed to a writer without building per-flow Python objects."""
+        nc, ns = ct.c_uint64(0), ct.c_uint64(0)
+        check(self._L.gns_cm_heavy_hitters(self._h, None, None, ct.byref(nc), None, None, ct.byref(ns)))
+        K = max(self.key_bytes, 1)
+        cf = np.zeros((max(nc.value, 1), K), np.uint8)
+        cv = np.zeros(max(nc.value, 1), np.uint32)
+        sf = np.zeros((max(ns.value, 1), K), np.uint8)
+        sv = np.zeros(max(ns.value, 1), np.uint32)
+        nc2, ns2 = ct.c_uint64(nc.value), ct.c_uint64(ns.value)
+        check(self._L.gns_cm_heavy_hitters(self._h, cf.ctypes.data, cv.ctypes.data, ct.byref(nc2),
+                                           sf.ctypes.data, sv.ctypes.data, ct.byref(ns2)))
+        m, q = min(nc.value, nc2.value), min(ns.value, ns2.value)
+        return cf[:m], cv[:m], sf[:q], sv[:q]
+
     def heavy_hitters(self) -> HeavyRecord:
         nc, ns = ct.c_uint64(0), ct.c_uint64(0)
         check(self._L.gns_cm_heavy_hitters(self._h, None, None, ct.byref(nc), None, None, ct.byref(ns)))
@@ -197,6 +213,14 @@ class CountMin:
     Reset = reset
 
     # --- parity / observability ---
+    def export_counters(self, C=None, S=None):
+        """Counter rows only (C, S as u32 [d*w]) to host memory: the per-window D2H."""
+        n = self.depth * self.width
+        C = np.empty(n, np.uint32) if C is None else C
+        S = np.empty(n, np.uint32) if S is None else S
+        check(self._L.gns_cm_export_state(self._h, C.ctypes.data, S.ctypes.data, None, None))
+        return C, S
+
     def export_state(self):
         n = self.depth * self.width
         K = max(self.key_bytes, 1)
