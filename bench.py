@@ -46,7 +46,7 @@ def row_seeds(d):
     return np.array(out, np.uint32)
 
 
-def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, depth: int = DEPTH):
+def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, depth: int = DEPTH, fields=FIELDS):
     """Timed CPU restatements on a bounded prefix of the same stream (rank 0)."""
     from oracle import oracle as orc
     n = min(int(wl_dev.shape[0]), 24_000_000)
@@ -54,23 +54,24 @@ def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, dept
     wl = wl_dev[:n].cpu().numpy().view(np.uint32)
     seeds = row_seeds(depth)
     # (1) sequential oracle, 1 thread
-    cm = orc.CountMin(width, depth, 1 << 20, 1000, 37, seeds)
+    K = 37 if len(fields) == 5 else 16
+    cm = orc.CountMin(width, depth, 1 << 20, 1000, K, seeds)
     chunk, done, t0 = 1_000_000, 0, time.perf_counter()
     while done < n and time.perf_counter() - t0 < seconds:
         m = min(chunk, n - done)
-        cm.insert_hdr64(hdr[done:done + m], wl[done:done + m], FIELDS)
+        cm.insert_hdr64(hdr[done:done + m], wl[done:done + m], fields)
         done += m
     seq_rate = done / (time.perf_counter() - t0) / 1e6
     seq_n = done
     del cm
     # (2) restatement of the Go worker pool (shared sketch, CAS loops, shared cursor)
     threads = int(os.environ.get("GNS_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    cm = orc.CountMin(width, depth, 1 << 20, 1000, 37, seeds)
+    cm = orc.CountMin(width, depth, 1 << 20, 1000, K, seeds)
     done, t0 = 0, time.perf_counter()
     chunk = 4_000_000
     while done < n and time.perf_counter() - t0 < seconds / 2:
         m = min(chunk, n - done)
-        cm.insert_hdr64_pool(hdr[done:done + m], wl[done:done + m], FIELDS, threads)
+        cm.insert_hdr64_pool(hdr[done:done + m], wl[done:done + m], fields, threads)
         done += m
     pool_rate = done / (time.perf_counter() - t0) / 1e6
     return {
@@ -264,6 +265,8 @@ def main():
     ap.add_argument("--depth", type=int, default=DEPTH, help="Count-Min depth (8 = configs[4] geometry)")
     ap.add_argument("--sketch", choices=["countmin", "superspread", "exact"], default="countmin",
                     help="superspread = configs[2]; exact = the exact aggregator (neither is the headline metric)")
+    ap.add_argument("--key", choices=["5tuple", "srcip"], default="5tuple",
+                    help="flow key: full 5-tuple (37 B, primary) or [SrcIP] (16 B, the default task layout)")
     ap.add_argument("--flows", type=int, default=1 << 20,
                     help="distinct flows of the synthetic stream (experiments; the headline uses 2^20)")
     ap.add_argument("--host-input", nargs="?", const="headers", choices=["headers", "tuples"], default=None,
@@ -294,7 +297,8 @@ def main():
     syn = SyntheticTraffic(flows=args.flows, shard=rank, nshards=world, device=local)
     hdr, wl = syn.generate(n)
     batch = args.batch or n
-    cm = CountMin(args.width, args.depth, 1 << 20, 1000, flow_fields=FIELDS, seeds=row_seeds(args.depth),
+    fields = FIELDS if args.key == "5tuple" else ["SrcIP"]
+    cm = CountMin(args.width, args.depth, 1 << 20, 1000, flow_fields=fields, seeds=row_seeds(args.depth),
                   max_flows=1 << 21, batch_packets=batch, device=local)
     torch.cuda.synchronize()
 
@@ -407,6 +411,9 @@ def main():
         line["config"]["workload"] = (f"Count-Min d={args.depth} w={wl2} (configs[4] geometry when d=8 w=2^24), "
                                       f"100M Zipf(1.1) 5-tuple headers in HBM per GPU, bit-exact counters")
         line["note"] = "not the headline metric (BASELINE.json metric is d=4 w=2^20)"
+    if args.key != "5tuple":
+        line["config"]["key"] = "[SrcIP] (16 B)"
+        line["note"] = "secondary key layout (SURVEY §8d); the headline uses the 5-tuple key"
     if args.flows != 1 << 20:
         line["config"]["flows"] = args.flows
         line["note"] = "not the headline metric (BASELINE.json stream has 2^20 flows)"
@@ -416,7 +423,7 @@ def main():
         line["note"] = "not the headline metric: inputs start in pinned host memory, outputs end in host memory"
         line["config"]["host_input"] = args.host_input
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(hdr, wl, width=args.width, depth=args.depth)
+        line["cpu_baseline"] = cpu_baseline(hdr, wl, width=args.width, depth=args.depth, fields=fields)
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:
