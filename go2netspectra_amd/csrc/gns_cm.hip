@@ -69,8 +69,16 @@ constexpr int kApItems = GNS_AP_ITEMS;
 constexpr uint32_t kApChunk = kApThreads * kApItems; // 8192 updates per K4 step
 static_assert((uint64_t)kApChunk * (kSizeEsc - 1) < (1ull << 32), "K4 per-chunk size sums must fit 32 bits");
 constexpr uint32_t kScanSeg = 4096;
-constexpr uint32_t kHot = 64;                       // designated hot buckets per row (slot fits 6 bits)
-constexpr uint32_t kHotTab = 512;                   // LDS hash slots per row (load <= 1/8)
+#ifndef GNS_HOT_BITS
+#define GNS_HOT_BITS 7
+#endif
+constexpr uint32_t kHotBits = GNS_HOT_BITS;           // designated hot buckets per row = 2^kHotBits
+constexpr uint32_t kHot = 1u << kHotBits;
+#ifndef GNS_HOT_TAB_MUL
+#define GNS_HOT_TAB_MUL 4
+#endif
+constexpr uint32_t kHotTab = kHot * GNS_HOT_TAB_MUL;  // lookup slots per row (load <= 1/GNS_HOT_TAB_MUL)
+constexpr uint32_t kHotGroupBits = kHotBits + (GNS_HOT_TAB_MUL == 8 ? 1 : 0);  // 4-entry groups = kHotTab / 4
 constexpr uint32_t kHotMinBits = 11;                // designate only buckets with C >= 1024
 constexpr uint32_t kPendingId = 0xFFFFFFFEu;        // K1: flow not yet committed (equals no fingerprint)
 
@@ -92,18 +100,18 @@ struct CmGeom {
 // Per-row lookup table of the designated buckets, built once per batch by
 // k_hot_table (deterministic, single thread per row) and copied to LDS by K1:
 // 128 groups of 4 entries (one 16-byte LDS read per lookup, no probing);
-// entry = bucket << 6 | hot slot, empty = ~0.  A bucket whose group is full is
+// entry = bucket << kHotBits | hot slot, empty = ~0.  A bucket whose group is full is
 // simply not designated (designation only moves work).
-static_assert(kHotTab / 4 == 128 && kHot <= 64, "hot_group() yields 7 bits; table entries hold a 6-bit slot");
-__device__ __forceinline__ uint32_t hot_group(uint32_t b) { return (b * 0x9E3779B1u) >> 25; }  // 0..127
+static_assert(kHotTab / 4 == (1u << kHotGroupBits), "hot_group() yields kHotGroupBits bits");
+__device__ __forceinline__ uint32_t hot_group(uint32_t b) { return (b * 0x9E3779B1u) >> (32 - kHotGroupBits); }
 
 __device__ __forceinline__ int hot_lookup(const uint32_t *tabrow, uint32_t b) {
     const uint4 e = *reinterpret_cast<const uint4 *>(tabrow + hot_group(b) * 4);
     int h = -1;
-    h = (e.w >> 6) == b ? (int)(e.w & 63u) : h;
-    h = (e.z >> 6) == b ? (int)(e.z & 63u) : h;
-    h = (e.y >> 6) == b ? (int)(e.y & 63u) : h;
-    h = (e.x >> 6) == b ? (int)(e.x & 63u) : h;
+    h = (e.w >> kHotBits) == b ? (int)(e.w & (kHot - 1u)) : h;
+    h = (e.z >> kHotBits) == b ? (int)(e.z & (kHot - 1u)) : h;
+    h = (e.y >> kHotBits) == b ? (int)(e.y & (kHot - 1u)) : h;
+    h = (e.x >> kHotBits) == b ? (int)(e.x & (kHot - 1u)) : h;
     return h;
 }
 
@@ -226,7 +234,7 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) { return __ockl_wfred
 // KB = key bytes when known at compile time (16 / 37), 0 = runtime a.kp.K.
 // DD = depth when known at compile time (4: the rows loops unroll exactly), 0 = runtime
 #ifndef GNS_EX_MINW
-#define GNS_EX_MINW 5
+#define GNS_EX_MINW 4
 #endif
 template <int KIND, int MODE, int KB, int DD>
 __global__ __launch_bounds__(kExThreads, GNS_EX_MINW) void k_extract(ExtractArgs a) {
@@ -1426,7 +1434,7 @@ __global__ __launch_bounds__(256) void k_hot_verify(HotArgs a) {
 // H3: apply the verified halves; flagged halves keep the batch-entry state
 // for the in-order fallback.
 __global__ __launch_bounds__(512) void k_hot_apply(HotArgs a) {
-    const uint32_t hb = threadIdx.x;
+    const uint32_t hb = blockIdx.x * 512 + threadIdx.x;
     if (hb >= a.g.d * kHot) return;
     if (*a.hany == 0) return;
     const uint32_t f2 = a.hflag2[hb] & 3u;
@@ -1604,7 +1612,7 @@ __global__ __launch_bounds__(256) void k_hot_blockcheck(HotArgs a) {
 
 // Commit the linear results of the halves that stay on the summary path.
 __global__ __launch_bounds__(512) void k_hot_commit(HotArgs a) {
-    const uint32_t slot = threadIdx.x;
+    const uint32_t slot = blockIdx.x * 512 + threadIdx.x;
     if (slot >= a.g.d * kHot) return;
     const uint32_t id = a.hot_ids[slot];
     if (id == GNS_ID_NONE) return;
@@ -1616,33 +1624,41 @@ __global__ __launch_bounds__(512) void k_hot_commit(HotArgs a) {
 
 // Designation for the next batch: per row, the buckets whose counter bit
 // length is in the top band holding at most kHot buckets (and >= 2^(kHotMinBits-1)).
-__global__ __launch_bounds__(256) void k_hot_hist(const uint32_t *C, CmGeom g, uint32_t *hh /*[d][33]*/) {
-    __shared__ uint32_t s[8 * 33];
-    for (uint32_t i = threadIdx.x; i < g.d * 33; i += 256) s[i] = 0;
+// Designation key: bit length and the 3 bits below the leading one (a
+// monotone 1/8-octave log scale), so the band picked by k_hot_pick holds
+// close to kHot buckets.
+constexpr uint32_t kHotKeys = 33 * 8;
+__device__ __forceinline__ uint32_t hot_key(uint32_t v) {
+    const uint32_t bits = v ? 32u - __clz(v) : 0u;
+    return bits >= 4 ? bits * 8u + ((v >> (bits - 4u)) & 7u) : bits * 8u;
+}
+
+__global__ __launch_bounds__(256) void k_hot_hist(const uint32_t *C, CmGeom g, uint32_t *hh /*[d][kHotKeys]*/) {
+    __shared__ uint32_t s[8 * kHotKeys];
+    for (uint32_t i = threadIdx.x; i < g.d * kHotKeys; i += 256) s[i] = 0;
     __syncthreads();
     const uint64_t cells = (uint64_t)g.d * g.w;
     for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += (uint64_t)gridDim.x * 256) {
         const uint32_t v = C[c];
-        const uint32_t bits = v ? 32u - __clz(v) : 0u;
-        if (bits >= kHotMinBits) atomicAdd(&s[(c / g.w) * 33 + bits], 1u);
+        if (v >= (1u << (kHotMinBits - 1))) atomicAdd(&s[(c / g.w) * kHotKeys + hot_key(v)], 1u);
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < g.d * 33; i += 256) if (s[i]) atomicAdd(&hh[i], s[i]);
+    for (uint32_t i = threadIdx.x; i < g.d * kHotKeys; i += 256) if (s[i]) atomicAdd(&hh[i], s[i]);
 }
 
 __global__ void k_hot_pick(uint32_t *hh, CmGeom g, uint32_t *thr, uint32_t *hcnt, uint32_t *hot_ids) {
     const uint32_t r = threadIdx.x;
     for (uint32_t i = threadIdx.x; i < g.d * kHot; i += blockDim.x) hot_ids[i] = GNS_ID_NONE;
     if (r < g.d) {
-        uint32_t cum = 0, t = 33;
-        for (int b = 32; b >= (int)kHotMinBits; b--) {
-            cum += hh[r * 33 + b];
+        uint32_t cum = 0, t = kHotKeys;
+        for (int k = (int)kHotKeys - 1; k >= (int)(kHotMinBits * 8); k--) {
+            cum += hh[r * kHotKeys + k];
             if (cum > kHot) break;
-            t = (uint32_t)b;
+            t = (uint32_t)k;
         }
         thr[r] = t;
         hcnt[r] = 0;
-        for (int b = 0; b < 33; b++) hh[r * 33 + b] = 0;
+        for (uint32_t k = 0; k < kHotKeys; k++) hh[r * kHotKeys + k] = 0;
     }
 }
 
@@ -1652,8 +1668,7 @@ __global__ __launch_bounds__(256) void k_hot_collect(const uint32_t *C, CmGeom g
     for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += (uint64_t)gridDim.x * 256) {
         const uint32_t v = C[c];
         const uint32_t r = (uint32_t)(c / g.w);
-        const uint32_t bits = v ? 32u - __clz(v) : 0u;
-        if (bits >= thr[r] && bits >= kHotMinBits) {
+        if (v >= (1u << (kHotMinBits - 1)) && hot_key(v) >= thr[r]) {
             const uint32_t q = atomicAdd(&hcnt[r], 1u);
             if (q < kHot) hot_ids[r * kHot + q] = (uint32_t)(c - (uint64_t)r * g.w);
         }
@@ -1673,7 +1688,7 @@ __global__ void k_hot_table(CmGeom g, uint32_t *hot_ids, uint32_t *hot_tab) {
         uint32_t *grp = tab + hot_group(b) * 4;
         uint32_t j = 0;
         while (j < 4 && grp[j] != 0xFFFFFFFFu) j++;
-        if (j < 4) grp[j] = b << 6 | h;
+        if (j < 4) grp[j] = b << kHotBits | h;
         else hot_ids[r * kHot + h] = GNS_ID_NONE;
     }
 }
@@ -1827,7 +1842,7 @@ int cm_reset_state(gns_cm *cm) {
     GNS_HIP(hipMemsetAsync(cm->D.rec, 0, cm->dict_slots * cm->D.RW * 4, cm->stream));
     GNS_HIP(hipMemsetAsync(cm->hot_ids, 0xFF, (size_t)cm->g.d * kHot * 4, cm->stream));
     GNS_HIP(hipMemsetAsync(cm->hot_tab, 0xFF, (size_t)cm->g.d * kHotTab * 4, cm->stream));
-    GNS_HIP(hipMemsetAsync(cm->hhist, 0, (size_t)cm->g.d * 33 * 4, cm->stream));
+    GNS_HIP(hipMemsetAsync(cm->hhist, 0, (size_t)cm->g.d * kHotKeys * 4, cm->stream));
     cm->warm = false;
     return GNS_OK;
 }
@@ -1944,7 +1959,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         // summary path: decide, exact block checks, commit
         hipLaunchKernelGGL(k_hot_decide, dim3(g.d * kHot), dim3(256), 0, s, h);
         hipLaunchKernelGGL(k_hot_blockcheck, dim3(kChkCap), dim3(256), 0, s, h);
-        hipLaunchKernelGGL(k_hot_commit, dim3(1), dim3(512), 0, s, h);
+        hipLaunchKernelGGL(k_hot_commit, dim3((g.d * kHot + 511) / 512), dim3(512), 0, s, h);
         // exact entry path for flagged halves (device-side early exit when none)
         {
             ScatterArgs a{};
@@ -1959,7 +1974,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         }
         hipLaunchKernelGGL(k_hot_sum, dim3(kHotSegs, g.d * kHot), dim3(256), 0, s, h);
         hipLaunchKernelGGL(k_hot_verify, dim3(kHotSegs, g.d * kHot), dim3(256), 0, s, h);
-        hipLaunchKernelGGL(k_hot_apply, dim3(1), dim3(512), 0, s, h);
+        hipLaunchKernelGGL(k_hot_apply, dim3((g.d * kHot + 511) / 512), dim3(512), 0, s, h);
         hipLaunchKernelGGL(k_hot_fallback, dim3(g.d * kHot), dim3(64), 0, s, h);
         GNS_HIP(hipGetLastError());
     }
@@ -2066,8 +2081,8 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         if (g.d > 8) { set_error("depth %u > 8 not supported", g.d); rc = GNS_E_ARG; break; }
         if ((rc = make_plan(p->flow, p->key_bytes, &cm->kp)) != GNS_OK) break;
         cm->K = cm->kp.K;
-        if (g.w >= (1u << 26)) {  // designated-bucket table entries hold bucket << 6
-            set_error("width %u >= 2^26 is not supported", g.w); rc = GNS_E_RANGE; break;
+        if (g.w >= (1u << (32 - kHotBits))) {  // designated-bucket table entries hold bucket << kHotBits
+            set_error("width %u >= 2^%u is not supported", g.w, 32 - kHotBits); rc = GNS_E_RANGE; break;
         }
         g.pow2 = (g.w & (g.w - 1)) == 0;
         g.wmask = g.pow2 ? g.w - 1 : 0;
@@ -2132,7 +2147,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (rc = dalloc_t(&cm->ovf, kOvfCap)) || (rc = dalloc_t(&cm->ovf_cnt, 1)) ||
             (rc = dalloc_t(&cm->stats, 16)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
             (rc = dalloc_t(&cm->segtot, (size_t)g.d * kHot * kHotSegs * 2)) || (rc = dalloc_t(&cm->hflag, g.d * kHot)) ||
-            (rc = dalloc_t(&cm->hhist, g.d * 33)) || (rc = dalloc_t(&cm->hthr, 8)) || (rc = dalloc_t(&cm->hcnt, 8)) ||
+            (rc = dalloc_t(&cm->hhist, g.d * kHotKeys)) || (rc = dalloc_t(&cm->hthr, 8)) || (rc = dalloc_t(&cm->hcnt, 8)) ||
             (rc = dalloc_t(&cm->hsum, (uint64_t)g.d * kHot * cm->nblk_max)) ||
             (rc = dalloc_t(&cm->hflag2, g.d * kHot + 2)) || (rc = dalloc_t(&cm->hres, g.d * kHot * 2)) ||
             (rc = dalloc_t(&cm->chk, kChkCap)) || (rc = dalloc_t(&cm->hot_tab, (size_t)g.d * kHotTab)))
