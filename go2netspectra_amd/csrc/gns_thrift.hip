@@ -24,18 +24,51 @@ __global__ __launch_bounds__(256) void k_thrift_decode(const uint8_t *buf, uint6
     ThriftPacket pk{};
     bool ok = o0 <= o1 && o1 <= buf_bytes && o1 - o0 <= 0xFFFFFFFFull;
     const uint8_t *msg = buf + (ok ? o0 : 0);
-    if (ok) ok = thrift_packet_info(msg, (uint32_t)(o1 - o0), pk);
     uint8_t b[64];
 #pragma unroll
     for (int i = 0; i < 64; i++) b[i] = 0;
+    // Fast path: the 70-byte message MarshalPacketInfo writes for an IPv4
+    // PacketInfo (fields in id order, 4-byte IPs).  Aligned word loads +
+    // v_alignbyte realignment; every header byte of the layout is checked, so
+    // a message takes this path only if the full decoder would read exactly
+    // these fields from it (anything else falls through to thrift_packet_info).
+    bool fast = ok && o1 - o0 == 70 && (o0 & ~3ull) + 76 <= ((buf_bytes + 15) & ~15ull);
+    if (fast) {
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(buf + (o0 & ~3ull));
+        const uint32_t sh = (uint32_t)(o0 & 3u);
+        uint32_t w[19], m[18];
+#pragma unroll
+        for (int i = 0; i < 19; i++) w[i] = wp[i];
+#pragma unroll
+        for (int i = 0; i < 18; i++) m[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+        auto B = [&](int k) -> uint32_t { return (m[k >> 2] >> (8 * (k & 3))) & 0xFFu; };
+        auto be32 = [&](int k) -> uint32_t { return B(k) << 24 | B(k + 1) << 16 | B(k + 2) << 8 | B(k + 3); };
+        const uint32_t hdrs = (B(0) ^ 0x0A) | B(1) | (B(2) ^ 1) | (B(11) ^ 0x0C) | B(12) | (B(13) ^ 2) |
+                              (B(14) ^ 0x0B) | B(15) | (B(16) ^ 1) | (be32(17) ^ 4) |
+                              (B(25) ^ 0x0B) | B(26) | (B(27) ^ 2) | (be32(28) ^ 4) |
+                              (B(36) ^ 8) | B(37) | (B(38) ^ 3) | (B(43) ^ 8) | B(44) | (B(45) ^ 4) |
+                              (B(50) ^ 8) | B(51) | (B(52) ^ 5) | B(57) | (B(58) ^ 0x0A) | B(59) | (B(60) ^ 3) | B(69);
+        fast = hdrs == 0;
+        if (fast) {
+            pk.ts = (int64_t)((uint64_t)be32(3) << 32 | be32(7));
+            pk.length = (int64_t)((uint64_t)be32(61) << 32 | be32(65));
+            pk.src_len = 4; pk.dst_len = 4;
+            pk.sport = (int32_t)be32(39); pk.dport = (int32_t)be32(46); pk.proto = (int32_t)be32(53);
+#pragma unroll
+            for (int i = 0; i < 4; i++) { b[16 + i] = (uint8_t)B(21 + i); b[32 + i] = (uint8_t)B(32 + i); }
+        }
+    }
+    if (ok && !fast) ok = thrift_packet_info(msg, (uint32_t)(o1 - o0), pk);
     if (ok) {
         b[12] = 0x88; b[13] = 0xB5; b[14] = 1;
         b[15] = (uint8_t)ip_code(pk.src_len);
         b[53] = (uint8_t)ip_code(pk.dst_len);
         // EncodeFlow copies min(len, 16) bytes of each net.IP into its slot (task.go:281-286)
-        const uint32_t ls = min(pk.src_len, 16u), ld = min(pk.dst_len, 16u);
-        for (uint32_t i = 0; i < ls; i++) b[16 + i] = msg[pk.src_off + i];
-        for (uint32_t i = 0; i < ld; i++) b[32 + i] = msg[pk.dst_off + i];
+        if (!fast) {
+            const uint32_t ls = min(pk.src_len, 16u), ld = min(pk.dst_len, 16u);
+            for (uint32_t i = 0; i < ls; i++) b[16 + i] = msg[pk.src_off + i];
+            for (uint32_t i = 0; i < ld; i++) b[32 + i] = msg[pk.dst_off + i];
+        }
         const uint32_t sp = (uint16_t)pk.sport, dp = (uint16_t)pk.dport;  // uint16(int32), packetcodec.go:90-91
         b[48] = (uint8_t)(sp >> 8); b[49] = (uint8_t)sp;
         b[50] = (uint8_t)(dp >> 8); b[51] = (uint8_t)dp;
