@@ -365,6 +365,8 @@ def main():
     ap.add_argument("--depth", type=int, default=DEPTH, help="Count-Min depth (8 = configs[4] geometry)")
     ap.add_argument("--sketch", choices=["countmin", "superspread", "exact", "thrift"], default="countmin",
                     help="superspread = configs[2]; exact = the exact aggregator (neither is the headline metric)")
+    ap.add_argument("--max-flows", type=int, default=1 << 21,
+                    help="flow dictionary capacity (slots = next power of two >= 2x)")
     ap.add_argument("--key", choices=["5tuple", "srcip"], default="5tuple",
                     help="flow key: full 5-tuple (37 B, primary) or [SrcIP] (16 B, the default task layout)")
     ap.add_argument("--flows", type=int, default=1 << 20,
@@ -401,7 +403,7 @@ def main():
     batch = args.batch or n
     fields = FIELDS if args.key == "5tuple" else ["SrcIP"]
     cm = CountMin(args.width, args.depth, 1 << 20, 1000, flow_fields=fields, seeds=row_seeds(args.depth),
-                  max_flows=1 << 21, batch_packets=batch, device=local)
+                  max_flows=args.max_flows, batch_packets=batch, device=local)
     torch.cuda.synchronize()
 
     def barrier():

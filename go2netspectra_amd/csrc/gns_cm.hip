@@ -230,6 +230,118 @@ extern "C" __device__ unsigned long long __ockl_wfred_add_u64(unsigned long long
 extern "C" __device__ unsigned __ockl_wfred_add_u32(unsigned);
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) { return __ockl_wfred_add_u64(v); }
 
+// K1 second half for one packet: resolve the first dictionary probe (r4,
+// issued earlier by the caller), publish/hash the row buckets, bin codes,
+// block histogram and designated-bucket summaries.
+struct K1Lds {
+    uint32_t *s_tab, *s_hist, *s_hFc, *s_hFs, *s_nfc, *s_nfs, *s_smax, *s_pend, *s_full;
+    unsigned long long *s_os, *s_fs;
+};
+
+template <int RMAX>
+__device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S, uint32_t K, uint32_t d, bool bw,
+                                           uint64_t p, uint64_t beg, bool ok, const uint32_t (&kw)[GNS_KWMAX],
+                                           uint32_t slot0, const uint4 (&r4)[4], uint32_t sz, uint32_t &n_ok) {
+    uint32_t *s_tab = S.s_tab, *s_hist = S.s_hist, *s_hFc = S.s_hFc, *s_hFs = S.s_hFs, *s_nfc = S.s_nfc;
+    uint32_t *s_nfs = S.s_nfs, *s_smax = S.s_smax;
+    unsigned long long *s_os = S.s_os, *s_fs = S.s_fs;
+    uint32_t &s_pend = *S.s_pend, &s_full = *S.s_full;
+    uint32_t kid = kPendingId;  // flow id when already committed (pending: foreign to every owner)
+    uint32_t rec[16];
+    int res = CM_FULL;
+    uint32_t out = 0;
+    if (ok) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            rec[4 * i] = r4[i].x; rec[4 * i + 1] = r4[i].y; rec[4 * i + 2] = r4[i].z; rec[4 * i + 3] = r4[i].w;
+        }
+        const uint32_t tag = rec[0];
+        bool eq = tag != 0 && tag != a.epoch;
+#pragma unroll
+        for (int i = 0; i < GNS_KWMAX; i++)
+            if ((uint32_t)i < ((K + 3) >> 2)) eq = eq && (rec[1 + i] == kw[i]);
+        if (tag == a.epoch) { res = CM_PENDING; out = slot0; }
+        else if (eq) { res = CM_FOUND; out = slot0; }
+        else res = cm_find_or_claim(a.D, kw, K, tag == 0 ? slot0 : ((slot0 + 1u) & a.D.mask), a.epoch, &out, rec);
+        if (res == CM_FULL) {
+            a.keyid[p] = GNS_ID_NONE;
+            atomicAdd(&s_full, 1u);
+            ok = false;
+        } else if (res == CM_PENDING) {
+            a.keyid[p] = GNS_ID_NONE;  // set by k_resolve
+            const uint32_t q = atomicAdd(&s_pend, 1u);
+            a.pend[beg + q] = (uint64_t)(p - beg) << 32 | out;
+        } else {
+            a.keyid[p] = out;
+            kid = out;
+        }
+    }
+    // row buckets: from the record's cache (rows 0..3 of a committed flow), else hashed
+    uint32_t bk[RMAX];
+    const bool cached = bw && res == CM_FOUND;
+#pragma unroll
+    for (uint32_t rr = 0; rr < RMAX; rr++) bk[rr] = (rr < 4 && cached) ? rec[12 + rr] : 0u;
+    if (__ballot(ok && !cached) || (RMAX > 4 && d > 4)) {
+        uint32_t mk[GNS_KWMAX];
+        mm3_premix<GNS_KWMAX>(kw, K, mk);
+#pragma unroll
+        for (uint32_t rr = 0; rr < RMAX; rr++) {
+            if (rr >= d) break;
+            if (ok && (!cached || rr >= 4)) bk[rr] = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, K, a.g.seeds[rr]));
+        }
+    }
+    if (bw && res == CM_CLAIMED) {  // publish the bucket cache with the key (visible next launch)
+        uint32_t *tp = a.D.rec + (size_t)out * a.D.RW;
+#pragma unroll
+        for (uint32_t rr = 0; rr < 4; rr++)
+            if (rr < d) tp[12 + rr] = bk[rr];
+    }
+    if (!ok) sz = 0;
+    n_ok += ok ? 1u : 0u;
+#pragma unroll
+    for (uint32_t rr = 0; rr < RMAX; rr++) {
+        if (rr >= d) break;
+        uint32_t binid = 0xFFFFFFFFu;
+        int h = -1;
+        if (ok) {
+            const uint32_t b = bk[rr];
+            h = hot_lookup(s_tab + rr * kHotTab, b);
+            // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
+            a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
+            binid = h >= 0 ? a.g.nbins + rr * kHot + (uint32_t)h : rr * a.g.ntiles + (b >> a.g.bin_bits);
+        }
+        // heavy bins: one LDS add for the wave's majority bin
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(binid);
+        const uint64_t mm = __ballot(binid == b0 && b0 != 0xFFFFFFFFu);
+        const uint32_t cnt = __popcll(mm);
+        const bool agg = cnt >= 4;  // wave-uniform
+        const bool inmaj = agg && binid == b0;
+        const bool leader = inmaj && (uint32_t)__ffsll((long long)mm) - 1 == (threadIdx.x & 63u);
+        if (leader) atomicAdd(&s_hist[b0], cnt);
+        if (binid != 0xFFFFFFFFu && !inmaj) atomicAdd(&s_hist[binid], 1u);
+        // designated bucket: summary against the batch-entry owners
+        uint64_t ownv = 0;
+        if (h >= 0) {
+            const uint32_t slot = rr * kHot + (uint32_t)h;
+            if (kid != s_hFc[slot]) atomicAdd(&s_nfc[slot], 1u);
+            if (kid != s_hFs[slot]) {
+                atomicAdd(&s_nfs[slot], 1u);
+                atomicAdd(&s_fs[slot], (unsigned long long)sz);
+                atomicMax(&s_smax[slot], sz);
+            } else {
+                ownv = sz;
+            }
+        }
+        if (agg && b0 >= a.g.nbins && b0 != 0xFFFFFFFFu) {  // wave-uniform: majority bin is hot
+            const uint64_t tot = wave_sum64(inmaj ? ownv : 0ull);
+            if (leader && tot) atomicAdd(&s_os[b0 - a.g.nbins], (unsigned long long)tot);
+            if (!inmaj && ownv) atomicAdd(&s_os[binid - a.g.nbins], (unsigned long long)ownv);
+        } else if (ownv) {
+            atomicAdd(&s_os[binid - a.g.nbins], (unsigned long long)ownv);
+        }
+    }
+}
+
 // K1: parse/encode, dictionary, row buckets, block histogram, hot summaries.
 // KB = key bytes when known at compile time (16 / 37), 0 = runtime a.kp.K.
 // DD = depth when known at compile time (4: the rows loops unroll exactly), 0 = runtime
@@ -268,158 +380,93 @@ __global__ __launch_bounds__(kExThreads, GNS_EX_MINW) void k_extract(ExtractArgs
     const uint64_t end = min(a.n, beg + kChunk);
     const bool bw = a.D.bw != 0;
     uint32_t n_ok = 0;
-    // header records: the next iteration's record is loaded while this one's
-    // dictionary probe is in flight (two memory latencies overlap, not add)
-    uint4 hv[4];
-    uint32_t hsz = 0;
+    const K1Lds S{s_tab, s_hist, s_hFc, s_hFs, s_nfc, s_nfs, s_smax, &s_pend, &s_full, s_os, s_fs};
     if constexpr (KIND == IN_HDR) {
-        const uint64_t pc = min(beg + tid, end - 1);
-        const uint4 *r = reinterpret_cast<const uint4 *>(a.in.hdr + pc * 16);
-#pragma unroll
-        for (int i = 0; i < 4; i++) hv[i] = r[i];
-        hsz = a.in.sizes[pc];
-    }
-    for (uint64_t p0 = beg; p0 < end; p0 += kExThreads) {  // wave-uniform trip count
-        const uint64_t p = p0 + tid;
-        bool ok = p < end;
-        uint32_t kw[GNS_KWMAX];
-        uint32_t cw[16], csz = 0;
-        if constexpr (KIND == IN_HDR) {
-#pragma unroll
-            for (int i = 0; i < 4; i++) { cw[4 * i] = hv[i].x; cw[4 * i + 1] = hv[i].y; cw[4 * i + 2] = hv[i].z; cw[4 * i + 3] = hv[i].w; }
-            csz = hsz;
-        }
-        if (ok) {
-            int st;
-            if constexpr (KIND == IN_HDR) {
-                uint32_t tw[10];
-                st = parse_record_fast(cw, csz, true, tw);
-                if (st == PARSE_OK) make_key_m<MODE, GNS_KWMAX>(K, s_src, tw, kw);
-            } else {
-                st = packet_key<KIND, MODE>(a.in, K, s_src, p, kw);
-            }
-            if (st != PARSE_OK) {
-                a.keyid[p] = GNS_ID_NONE;
-                atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
-                ok = false;
-            }
-        }
-        uint32_t slot0;
-        {   // the premixed key dies here; the rare rehash below recomputes it
-            uint32_t mk[GNS_KWMAX];
-            mm3_premix<GNS_KWMAX>(kw, K, mk);
-            slot0 = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
-        }
-        uint32_t kid = kPendingId;  // flow id when already committed (pending: foreign to every owner)
-        uint32_t rec[16];
-        int res = CM_FULL;
-        uint32_t out = 0;
-        // first dictionary probe issued BEFORE the next record's prefetch: the
-        // probe's wait then leaves the prefetch in flight (vmcnt counts in order)
-        uint4 r4[4];
-        if (ok) {
-            const uint4 *q = reinterpret_cast<const uint4 *>(a.D.rec + (size_t)slot0 * a.D.RW);
-#pragma unroll
-            for (int i = 0; i < 4; i++) r4[i] = (4u * i < a.D.RW) ? q[i] : make_uint4(0, 0, 0, 0);
-        }
-        if constexpr (KIND == IN_HDR) {
-            const uint64_t pc = min(p + kExThreads, end - 1);
+        // Two-stage software pipeline over the block's packets: iteration k
+        // parses packet k+1 and issues its dictionary probe (and the header
+        // prefetch of packet k+2), then consumes packet k, whose probe was
+        // issued one iteration earlier.  Probe and header latencies hide behind
+        // a whole iteration of work instead of stalling it.
+        uint4 hv[4];
+        uint32_t hsz;
+        auto load_hdr = [&](uint64_t q) {
+            const uint64_t pc = min(q, end - 1);
             const uint4 *r = reinterpret_cast<const uint4 *>(a.in.hdr + pc * 16);
 #pragma unroll
             for (int i = 0; i < 4; i++) hv[i] = r[i];
             hsz = a.in.sizes[pc];
-        }
-        if (ok) {
+        };
+        // stage B of packet q: parse the prefetched record, key, slot, issue the probe
+        auto stage_b = [&](uint64_t q, bool &okq, uint32_t (&kwq)[GNS_KWMAX], uint32_t &slotq, uint4 (&r4q)[4],
+                           uint32_t &szq) {
+            okq = q < end;
+            uint32_t cw[16];
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                rec[4 * i] = r4[i].x; rec[4 * i + 1] = r4[i].y; rec[4 * i + 2] = r4[i].z; rec[4 * i + 3] = r4[i].w;
-            }
-            const uint32_t tag = rec[0];
-            bool eq = tag != 0 && tag != a.epoch;
-#pragma unroll
-            for (int i = 0; i < GNS_KWMAX; i++)
-                if ((uint32_t)i < ((K + 3) >> 2)) eq = eq && (rec[1 + i] == kw[i]);
-            if (tag == a.epoch) { res = CM_PENDING; out = slot0; }
-            else if (eq) { res = CM_FOUND; out = slot0; }
-            else res = cm_find_or_claim(a.D, kw, K, tag == 0 ? slot0 : ((slot0 + 1u) & a.D.mask), a.epoch, &out, rec);
-            if (res == CM_FULL) {
-                a.keyid[p] = GNS_ID_NONE;
-                atomicAdd(&s_full, 1u);
-                ok = false;
-            } else if (res == CM_PENDING) {
-                a.keyid[p] = GNS_ID_NONE;  // set by k_resolve
-                const uint32_t q = atomicAdd(&s_pend, 1u);
-                a.pend[beg + q] = (uint64_t)(p - beg) << 32 | out;
-            } else {
-                a.keyid[p] = out;
-                kid = out;
-            }
-        }
-        // row buckets: from the record's cache (rows 0..3 of a committed flow), else hashed
-        uint32_t bk[RMAX];
-        const bool cached = bw && res == CM_FOUND;
-#pragma unroll
-        for (uint32_t rr = 0; rr < RMAX; rr++) bk[rr] = (rr < 4 && cached) ? rec[12 + rr] : 0u;
-        if (__ballot(ok && !cached) || (RMAX > 4 && d > 4)) {
-            uint32_t mk[GNS_KWMAX];
-            mm3_premix<GNS_KWMAX>(kw, K, mk);
-#pragma unroll
-            for (uint32_t rr = 0; rr < RMAX; rr++) {
-                if (rr >= d) break;
-                if (ok && (!cached || rr >= 4)) bk[rr] = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, K, a.g.seeds[rr]));
-            }
-        }
-        if (bw && res == CM_CLAIMED) {  // publish the bucket cache with the key (visible next launch)
-            uint32_t *tp = a.D.rec + (size_t)out * a.D.RW;
-#pragma unroll
-            for (uint32_t rr = 0; rr < 4; rr++)
-                if (rr < d) tp[12 + rr] = bk[rr];
-        }
-        uint32_t sz = 0;
-        if constexpr (KIND == IN_HDR) sz = ok ? csz : 0u;
-        else sz = ok ? a.in.sizes[p] : 0u;
-        n_ok += ok ? 1u : 0u;
-#pragma unroll
-        for (uint32_t rr = 0; rr < RMAX; rr++) {
-            if (rr >= d) break;
-            uint32_t binid = 0xFFFFFFFFu;
-            int h = -1;
-            if (ok) {
-                const uint32_t b = bk[rr];
-                h = hot_lookup(s_tab + rr * kHotTab, b);
-                // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
-                a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
-                binid = h >= 0 ? a.g.nbins + rr * kHot + (uint32_t)h : rr * a.g.ntiles + (b >> a.g.bin_bits);
-            }
-            // heavy bins: one LDS add for the wave's majority bin
-            const uint32_t b0 = __builtin_amdgcn_readfirstlane(binid);
-            const uint64_t mm = __ballot(binid == b0 && b0 != 0xFFFFFFFFu);
-            const uint32_t cnt = __popcll(mm);
-            const bool agg = cnt >= 4;  // wave-uniform
-            const bool inmaj = agg && binid == b0;
-            const bool leader = inmaj && (uint32_t)__ffsll((long long)mm) - 1 == (threadIdx.x & 63u);
-            if (leader) atomicAdd(&s_hist[b0], cnt);
-            if (binid != 0xFFFFFFFFu && !inmaj) atomicAdd(&s_hist[binid], 1u);
-            // designated bucket: summary against the batch-entry owners
-            uint64_t ownv = 0;
-            if (h >= 0) {
-                const uint32_t slot = rr * kHot + (uint32_t)h;
-                if (kid != s_hFc[slot]) atomicAdd(&s_nfc[slot], 1u);
-                if (kid != s_hFs[slot]) {
-                    atomicAdd(&s_nfs[slot], 1u);
-                    atomicAdd(&s_fs[slot], (unsigned long long)sz);
-                    atomicMax(&s_smax[slot], sz);
-                } else {
-                    ownv = sz;
+            for (int i = 0; i < 4; i++) { cw[4 * i] = hv[i].x; cw[4 * i + 1] = hv[i].y; cw[4 * i + 2] = hv[i].z; cw[4 * i + 3] = hv[i].w; }
+            szq = hsz;
+            load_hdr(q + kExThreads);
+            if (okq) {
+                uint32_t tw[10];
+                const int st = parse_record_fast(cw, szq, true, tw);
+                if (st == PARSE_OK) make_key_m<MODE, GNS_KWMAX>(K, s_src, tw, kwq);
+                else {
+                    a.keyid[q] = GNS_ID_NONE;
+                    atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
+                    okq = false;
                 }
             }
-            if (agg && b0 >= a.g.nbins && b0 != 0xFFFFFFFFu) {  // wave-uniform: majority bin is hot
-                const uint64_t tot = wave_sum64(inmaj ? ownv : 0ull);
-                if (leader && tot) atomicAdd(&s_os[b0 - a.g.nbins], (unsigned long long)tot);
-                if (!inmaj && ownv) atomicAdd(&s_os[binid - a.g.nbins], (unsigned long long)ownv);
-            } else if (ownv) {
-                atomicAdd(&s_os[binid - a.g.nbins], (unsigned long long)ownv);
+            uint32_t mk[GNS_KWMAX];
+            mm3_premix<GNS_KWMAX>(kwq, K, mk);
+            slotq = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
+            if (okq) {
+                const uint4 *rq = reinterpret_cast<const uint4 *>(a.D.rec + (size_t)slotq * a.D.RW);
+#pragma unroll
+                for (int i = 0; i < 4; i++) r4q[i] = (4u * i < a.D.RW) ? rq[i] : make_uint4(0, 0, 0, 0);
             }
+        };
+        load_hdr(beg + tid);
+        bool okc;
+        uint32_t kwc[GNS_KWMAX], slotc, szc;
+        uint4 r4c[4];
+        stage_b(beg + tid, okc, kwc, slotc, r4c, szc);
+        for (uint64_t p0 = beg; p0 < end; p0 += kExThreads) {  // wave-uniform trip count
+            bool okn = false;
+            uint32_t kwn[GNS_KWMAX], slotn = 0, szn = 0;
+            uint4 r4n[4];
+            if (p0 + kExThreads < end) stage_b(p0 + kExThreads + tid, okn, kwn, slotn, r4n, szn);
+            k1_consume<RMAX>(a, S, K, d, bw, p0 + tid, beg, okc, kwc, slotc, r4c, szc, n_ok);
+            okc = okn; slotc = slotn; szc = szn;
+#pragma unroll
+            for (int i = 0; i < GNS_KWMAX; i++) kwc[i] = kwn[i];
+#pragma unroll
+            for (int i = 0; i < 4; i++) r4c[i] = r4n[i];
+        }
+    } else {
+        for (uint64_t p0 = beg; p0 < end; p0 += kExThreads) {  // wave-uniform trip count
+            const uint64_t p = p0 + tid;
+            bool ok = p < end;
+            uint32_t kw[GNS_KWMAX];
+            if (ok) {
+                const int st = packet_key<KIND, MODE>(a.in, K, s_src, p, kw);
+                if (st != PARSE_OK) {
+                    a.keyid[p] = GNS_ID_NONE;
+                    atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
+                    ok = false;
+                }
+            }
+            uint32_t slot0;
+            {
+                uint32_t mk[GNS_KWMAX];
+                mm3_premix<GNS_KWMAX>(kw, K, mk);
+                slot0 = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
+            }
+            uint4 r4[4];
+            if (ok) {
+                const uint4 *q = reinterpret_cast<const uint4 *>(a.D.rec + (size_t)slot0 * a.D.RW);
+#pragma unroll
+                for (int i = 0; i < 4; i++) r4[i] = (4u * i < a.D.RW) ? q[i] : make_uint4(0, 0, 0, 0);
+            }
+            k1_consume<RMAX>(a, S, K, d, bw, p, beg, ok, kw, slot0, r4, ok ? a.in.sizes[p] : 0u, n_ok);
         }
     }
     atomicAdd(&s_ok, n_ok);
