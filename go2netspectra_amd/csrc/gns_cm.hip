@@ -1006,6 +1006,63 @@ __device__ __forceinline__ void decode_entry(const uint64_t *ovf, uint64_t e, ui
     }
 }
 
+// Replay of one 64-item group (count_min.go:180-235): pending lanes hold
+// updates of this wave's buckets, in stream order by lane.  A bucket with >= 8
+// updates in the group runs the wave-parallel sequence; the rest resolve
+// same-bucket lanes lowest-lane-first.
+__device__ __forceinline__ void replay_group(ApplyLds &L, bool pending, uint32_t b, uint32_t k, uint32_t s,
+                                             uint32_t rf) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t *sC = L.sC, *sFc = L.sFc, *sS = L.sS, *sFs = L.sFs;
+    uint32_t *own = reinterpret_cast<uint32_t *>(L.accS);
+    // a bucket with many updates in this group (a contested bucket that
+    // failed the linear check): wave-parallel sequence, 64 updates per step
+    for (;;) {
+        const uint64_t pm = __ballot(pending);
+        if (!pm) break;
+        const uint32_t lead = (uint32_t)__ffsll((long long)pm) - 1;
+        const uint32_t b0 = __shfl(b, lead, 64);
+        const bool mine = pending && b == b0;
+        const uint64_t m0 = __ballot(mine);
+        if (__popcll(m0) < 8) break;
+        const uint32_t rf0 = __shfl(rf, lead, 64);
+        if (rf0 & 2u) {
+            uint32_t F = sFs[b0], S = sS[b0];
+            size_seq64(mine, k, s, F, S);
+            if (lane == lead) { sS[b0] = S; sFs[b0] = F; }
+        }
+        if (rf0 & 1u) {
+            uint32_t F = sFc[b0], C = sC[b0];
+            count_seq64(mine, k, F, C);
+            if (lane == lead) { sC[b0] = C; sFc[b0] = F; }
+        }
+        if (mine) pending = false;
+    }
+    while (__ballot(pending)) {
+        if (pending) atomicMax(&own[b], 64u - lane);
+        const bool win = pending && own[b] == 64u - lane;
+        if (win) {
+            if (rf & 2u) {  // size half, count_min.go:181-209
+                uint32_t S = sS[b], F = sFs[b];
+                if (S == 0) { S = s; F = k; }
+                else if (F == k) S = S + s;
+                else if (s > S) { S = s; F = k; }
+                else S = S - s;
+                sS[b] = S; sFs[b] = F;
+            }
+            if (rf & 1u) {  // count half, count_min.go:211-235
+                uint32_t C = sC[b], F = sFc[b];
+                if (C == 0) { C = 1; F = k; }
+                else if (F == k) C = C + 1;
+                else { C = C - 1; if (C == 0) F = k; }
+                sC[b] = C; sFc[b] = F;
+            }
+            own[b] = 0;
+            pending = false;
+        }
+    }
+}
+
 // Updates ent[beg, end) (stream order) of one LDS tile: buckets cbase .. cbase+tn-1.
 __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, const uint64_t *ent, uint32_t beg,
                                            uint32_t end, uint64_t cbase, uint32_t tn) {
@@ -1021,7 +1078,6 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
         accN[i] = 0; accS[i] = 0;
     }
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint32_t *own = reinterpret_cast<uint32_t *>(accS);  // replay: lowest-lane arbitration
     uint64_t e[kApItems], en[kApItems];
 #pragma unroll
     for (int j = 0; j < kApItems; j++) {  // first chunk
@@ -1168,6 +1224,42 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             //     list in order and applies its buckets' updates; lanes of one
             //     64-item group hitting distinct buckets run in parallel,
             //     same-bucket lanes in lane order (lowest lane wins a round).
+            // Each wave first gathers the list positions of its own buckets (stream
+            // order) into its slice of s_list, which is free once every replay entry
+            // sits in s_rep, then replays only those: ~nlist/16 items instead of a
+            // walk over the whole list.  A wave whose slice overflows walks the list.
+            constexpr uint32_t kWl = kApChunk / kApWaves;
+            uint32_t nmine = 0xFFFFFFFFu;
+            if (nlist <= kRepCap) {
+                uint16_t *wl = s_list + wave * kWl;
+                uint32_t c = 0;
+                for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
+                    const uint32_t i = g0 + lane;
+                    const bool mine = i < nlist && ((uint32_t)(L.s_rep[i] >> 32) & (kTileMax - 1u)) % kApWaves == wave;
+                    const uint64_t m = __ballot(mine);
+                    const uint32_t pos = c + __popcll(m & lt_mask);
+                    if (mine && pos < kWl) wl[pos] = (uint16_t)i;
+                    c += __popcll(m);
+                }
+                if (c <= kWl) nmine = c;
+            }
+            if (nmine != 0xFFFFFFFFu) {
+                const uint16_t *wl = s_list + wave * kWl;
+                for (uint32_t g0 = 0; g0 < nmine; g0 += 64) {
+                    const uint32_t j = g0 + lane;
+                    bool pending = j < nmine;
+                    uint32_t b = 0, k = 0, s = 0, rf = 0;
+                    if (pending) {
+                        const uint64_t ee = L.s_rep[wl[j]];
+                        b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
+                        decode_entry(a.ovf, ee, k, s);
+                        rf = (uint32_t)accN[b];
+                    }
+                    replay_group(L, pending, b, k, s, rf);
+                }
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t j = lane; j < nmine; j += 64) accN[(uint32_t)(L.s_rep[wl[j]] >> 32) & (kTileMax - 1u)] = 0;
+            } else {
             for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
                 const uint32_t i = g0 + lane;
                 bool pending = false;
@@ -1177,64 +1269,14 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                     b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
                     pending = b % kApWaves == wave;
                     if (pending) {
-                        const uint32_t lo = (uint32_t)ee, hi = (uint32_t)(ee >> 32);
-                        if (lo & kOvfFlag) {
-                            const uint64_t ov = a.ovf[lo & ~kOvfFlag];
-                            k = (uint32_t)ov; s = (uint32_t)(ov >> 32);
-                        } else {
-                            k = lo; s = hi >> kEntShift;
-                        }
+                        decode_entry(a.ovf, ee, k, s);
                         rf = (uint32_t)accN[b];
                     }
                 }
-                // a bucket with many updates in this group (a contested bucket that
-                // failed the linear check): wave-parallel sequence, 64 updates per step
-                for (;;) {
-                    const uint64_t pm = __ballot(pending);
-                    if (!pm) break;
-                    const uint32_t lead = (uint32_t)__ffsll((long long)pm) - 1;
-                    const uint32_t b0 = __shfl(b, lead, 64);
-                    const bool mine = pending && b == b0;
-                    const uint64_t m0 = __ballot(mine);
-                    if (__popcll(m0) < 8) break;
-                    const uint32_t rf0 = __shfl(rf, lead, 64);
-                    if (rf0 & 2u) {
-                        uint32_t F = sFs[b0], S = sS[b0];
-                        size_seq64(mine, k, s, F, S);
-                        if (lane == lead) { sS[b0] = S; sFs[b0] = F; }
-                    }
-                    if (rf0 & 1u) {
-                        uint32_t F = sFc[b0], C = sC[b0];
-                        count_seq64(mine, k, F, C);
-                        if (lane == lead) { sC[b0] = C; sFc[b0] = F; }
-                    }
-                    if (mine) pending = false;
-                }
-                while (__ballot(pending)) {
-                    if (pending) atomicMax(&own[b], 64u - lane);
-                    const bool win = pending && own[b] == 64u - lane;
-                    if (win) {
-                        if (rf & 2u) {  // size half, count_min.go:181-209
-                            uint32_t S = sS[b], F = sFs[b];
-                            if (S == 0) { S = s; F = k; }
-                            else if (F == k) S = S + s;
-                            else if (s > S) { S = s; F = k; }
-                            else S = S - s;
-                            sS[b] = S; sFs[b] = F;
-                        }
-                        if (rf & 1u) {  // count half, count_min.go:211-235
-                            uint32_t C = sC[b], F = sFc[b];
-                            if (C == 0) { C = 1; F = k; }
-                            else if (F == k) C = C + 1;
-                            else { C = C - 1; if (C == 0) F = k; }
-                            sC[b] = C; sFc[b] = F;
-                        }
-                        own[b] = 0;
-                        pending = false;
-                    }
-                }
+                replay_group(L, pending, b, k, s, rf);
             }
             // this wave's buckets are done: clear their replay flags
+            __builtin_amdgcn_wave_barrier();
             for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
                 const uint32_t i = g0 + lane;
                 if (i < nlist) {
@@ -1242,6 +1284,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                     const uint32_t b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
                     if (b % kApWaves == wave) accN[b] = 0;
                 }
+            }
             }
         }
         __syncthreads();
