@@ -674,7 +674,7 @@ __host__ __device__ inline size_t scatter_lds_bytes(uint32_t LB, uint32_t d) {
 // RANK 1: stable per-wave ranks from returning LDS adds; 0: ballot multisplit
 // (used when the lane-order probe fails on this device).
 template <int RANK>
-__global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
+__global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_scatter(ScatterArgs a) {
 #ifdef GNS_K3_PROF
     uint64_t k3t[5] = {0, 0, 0, 0, 0}, k3prev = __builtin_amdgcn_s_memtime();
 #endif
@@ -712,16 +712,23 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
         const uint64_t p = beg + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
         bsn[i] = a.idx[p < end ? p : end - 1];
     }
-    for (uint64_t rb = beg; rb < end; rb += kScRound) {
-        // flow ids and sizes once per round (clamped loads, one latency)
-        uint32_t ids[kScItems], szs[kScItems];
+    // flow ids and sizes once per round, loaded one round ahead (clamped loads)
+    uint32_t idsn[kScItems], szsn[kScItems];
+    auto load_ids = [&](uint64_t rb) {
 #pragma unroll
         for (int i = 0; i < kScItems; i++) {
             const uint64_t p = rb + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
             const uint64_t pc = p < end ? p : end - 1;
-            ids[i] = p < end ? a.keyid[pc] : GNS_ID_NONE;
-            szs[i] = a.sizes[pc];
+            idsn[i] = p < end ? a.keyid[pc] : GNS_ID_NONE;
+            szsn[i] = a.sizes[pc];
         }
+    };
+    load_ids(beg);
+    for (uint64_t rb = beg; rb < end; rb += kScRound) {
+        uint32_t ids[kScItems], szs[kScItems];
+#pragma unroll
+        for (int i = 0; i < kScItems; i++) { ids[i] = idsn[i]; szs[i] = szsn[i]; }
+        if (rb + kScRound < end) load_ids(rb + kScRound);
         for (uint32_t r = 0; r < d; r++) {
             __syncthreads();
             uint32_t bs[kScItems];
@@ -739,7 +746,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                 }
             }
             uint64_t ent[kScItems];
-            uint32_t bin[kScItems], rank[kScItems];  // bin 0xFFFF = no update
+            uint32_t br[kScItems];  // bin << 16 | rank within (wave, bin); bin 0xFFFF = no update
             K3_MARK(0);
             // phase 1: stable per-wave ranks; wave w owns packets [rb + w*64*kScItems, ...), order (slot, lane)
 #pragma unroll
@@ -791,8 +798,7 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
                     }
                 }
                 ent[i] = e;
-                bin[i] = valid ? t : 0xFFFFu;
-                rank[i] = rk;
+                br[i] = (valid ? t : 0xFFFFu) << 16 | rk;
             }
             __syncthreads();
             K3_MARK(1);
@@ -827,15 +833,19 @@ __global__ __launch_bounds__(kScThreads) void k_scatter(ScatterArgs a) {
             // phase 3: stage in bin order
 #pragma unroll
             for (int i = 0; i < kScItems; i++) {
-                if (bin[i] != 0xFFFFu) {
-                    const uint32_t t = bin[i];
-                    const uint32_t l = s_rstart[t] + s_cnt[wave * LB + t] + rank[i];
+                if ((br[i] >> 16) != 0xFFFFu) {
+                    const uint32_t t = br[i] >> 16;
+                    const uint32_t l = s_rstart[t] + s_cnt[wave * LB + t] + (br[i] & 0xFFFFu);
                     s_ent[l] = ent[i];
                     s_bin[l] = (uint16_t)t;
                 }
             }
             __syncthreads();
             K3_MARK(3);
+            // the next step's codes are needed now, before this step's stores: the
+            // wait after a loop of stores would drain them (vmcnt is one in-order counter)
+#pragma unroll
+            for (int i = 0; i < kScItems; i++) asm volatile("" ::"v"(bsn[i]));
             // phase 4: contiguous runs per bin to global
             for (uint32_t s2 = tid; s2 < rtotal; s2 += kScThreads) a.entries[s_dbase[s_bin[s2]] + s2] = s_ent[s2];
             __syncthreads();
@@ -916,6 +926,7 @@ struct ApplyArgs {
 constexpr uint64_t kM14 = (1ull << 14) - 1;
 constexpr uint32_t kAccForce = 42;
 static_assert(kApChunk < (1u << 14), "accN field widths");
+static_assert(kScRound <= 65536, "K3 packs ranks in 16 bits");
 #ifndef GNS_REP_CAP
 #define GNS_REP_CAP 1536
 #endif
@@ -1090,8 +1101,11 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
 #else
 #define K4_MARK(i) do { } while (0)
 #endif
+    // engine counters in registers (global atomics inside the loop would be
+    // drained by the next chunk's load waits)
+    uint32_t st_chunks = 0, st_rep = 0, st_crep = 0;
     for (uint32_t cb = beg; cb < end; cb += kApChunk) {
-        if (tid == 0) { s_any = 0; atomicAdd(&a.stats[6], 1ull); }
+        if (tid == 0) { s_any = 0; st_chunks++; }
         __syncthreads();
         K4_MARK(3);
         bool v[kApItems];
@@ -1218,7 +1232,8 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             __syncthreads();
             const uint32_t nlist = s_nlist;
             K4_MARK(2);
-            if (tid == 0) { atomicAdd(&a.stats[5], (unsigned long long)nlist); atomicAdd(&a.stats[7], 1ull); }
+            st_rep += nlist;
+            st_crep++;
             // --- sequential replay (count_min.go:180-235), in order.  Buckets are
             //     partitioned over the 16 waves (b % 16); each wave walks the
             //     list in order and applies its buckets' updates; lanes of one
@@ -1290,6 +1305,11 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < kApItems; j++) e[j] = en[j];
+    }
+    if (tid == 0) {
+        atomicAdd(&a.stats[5], (unsigned long long)st_rep);
+        atomicAdd(&a.stats[6], (unsigned long long)st_chunks);
+        if (st_crep) atomicAdd(&a.stats[7], (unsigned long long)st_crep);
     }
 #ifdef GNS_K4_PROF
     if (tid == 0) for (int i = 0; i < 4; i++) atomicAdd(&a.stats[8 + i], (unsigned long long)pt[i]);
