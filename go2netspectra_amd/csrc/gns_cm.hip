@@ -616,6 +616,11 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t *x, uint64_t N, cons
 // ---------------------------------------------------------------------------
 // K3: stable partition of row r's bucket updates into its tile bins.
 // Entry (u64): lo = flow id (or kOvfFlag|ovf slot), hi = size<<12 | bucket&(tile-1)
+// Per step (4096 packets, one row): stable rank of every update among the
+// wave's updates to the same bin (returning LDS adds), per-bin prefix over the
+// waves (= the global slot of each wave's run), then each update is stored
+// straight to its slot.  Two barriers per step; the counters are
+// double-buffered so the next step needs no barrier before counting.
 // ---------------------------------------------------------------------------
 struct ScatterArgs {
     uint64_t n;
@@ -638,32 +643,9 @@ struct ScatterArgs {
     const uint32_t *hany;
 };
 
-// block (NW waves) exclusive scan; *total = sum
-template <int NW>
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, uint32_t *total) {
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t inc = wave_incl_scan(v);
-    if (lane == 63) s_w[wave] = inc;
-    __syncthreads();
-    uint32_t base = 0, tot = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < NW; w++) {
-        const uint32_t x = s_w[w];
-        if (w < wave) base += x;
-        tot += x;
-    }
-    __syncthreads();
-    *total = tot;
-    return base + inc - v;
-}
-
-// LDS layout of k_scatter (dynamic): s_cnt[kScWaves][LB], s_rstart[LB], s_dbase[LB],
-// s_goff[d][LB], s_ent[kScRound] (u64), s_bin[kScRound] (u16)
-__host__ __device__ inline size_t scatter_lds_head(uint32_t LB, uint32_t d) {
-    return ((size_t)(kScWaves + 2 + d) * LB * 4 + 15) / 16 * 16;
-}
+// LDS layout of k_scatter (dynamic): s_cnt[2][kScWaves][LB] (double-buffered), s_goff[d][LB]
 __host__ __device__ inline size_t scatter_lds_bytes(uint32_t LB, uint32_t d) {
-    return scatter_lds_head(LB, d) + (size_t)kScRound * 8 + (size_t)kScRound * 2;
+    return (size_t)(2 * kScWaves + d) * LB * 4;
 }
 
 #ifdef GNS_K3_PROF
@@ -679,22 +661,17 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
     uint64_t k3t[5] = {0, 0, 0, 0, 0}, k3prev = __builtin_amdgcn_s_memtime();
 #endif
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ uint32_t s_w[kScWaves];
     const uint32_t LB = a.g.ntiles + kHot;  // local bins of a row: tiles, then its hot buckets
     const uint32_t d = a.g.d;
-    uint32_t *s_cnt = reinterpret_cast<uint32_t *>(smem);
-    uint32_t *s_rstart = s_cnt + kScWaves * LB;
-    uint32_t *s_dbase = s_rstart + LB;  // [LB] global index of staged slot 0 of each bin
-    uint32_t *s_goff = s_dbase + LB;    // [d][LB]
-    uint64_t *s_ent = reinterpret_cast<uint64_t *>(smem + scatter_lds_head(LB, d));
-    uint16_t *s_bin = reinterpret_cast<uint16_t *>(s_ent + kScRound);
+    uint32_t *s_cnt2 = reinterpret_cast<uint32_t *>(smem);  // [2][kScWaves][LB]
+    uint32_t *s_goff = s_cnt2 + 2 * kScWaves * LB;          // [d][LB]
+    uint32_t par = 0;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t blk = blockIdx.x;
     const uint32_t tmask = (1u << a.g.bin_bits) - 1u;
     const uint64_t beg = (uint64_t)blk * kChunk;
     const uint64_t end = min(a.n, beg + kChunk);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    constexpr uint32_t TPT = (1536 + kScThreads - 1) / kScThreads;  // local bins per thread (LB <= 1536)
     if (a.hot_mode && *a.hany == 0) return;
     const uint32_t nbits = a.hot_mode ? a.g.nbits : ceil_log2_dev(a.g.ntiles);
     for (uint32_t i = tid; i < d * LB; i += kScThreads) {
@@ -703,14 +680,27 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
                                            : (uint64_t)(a.g.nbins + r * kHot + (t - a.g.ntiles));
         s_goff[i] = a.offsets[gb * a.nblk + blk];
     }
-    for (uint32_t t = tid; t < kScWaves * LB; t += kScThreads) s_cnt[t] = 0;
-    // bin codes of the next (round, row) step are loaded one step ahead, so
-    // their latency hides behind the current step's LDS phases
+    for (uint32_t t = tid; t < 2 * kScWaves * LB; t += kScThreads) s_cnt2[t] = 0;
+    // bin codes of the next two (round, row) steps are in flight while a step
+    // runs (K3 is latency-bound: bytes in flight, not bandwidth)
     uint32_t bsn[kScItems];
 #pragma unroll
     for (int i = 0; i < kScItems; i++) {
         const uint64_t p = beg + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
         bsn[i] = a.idx[p < end ? p : end - 1];
+    }
+    // and the step after it (two steps in flight)
+    uint32_t bsn2[kScItems];
+    {
+        const uint32_t r1 = d > 1 ? 1u : 0u;
+        const uint64_t rb1 = d > 1 ? beg : beg + kScRound;
+        if (rb1 < end) {
+#pragma unroll
+            for (int i = 0; i < kScItems; i++) {
+                const uint64_t p = rb1 + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
+                bsn2[i] = a.idx[(uint64_t)r1 * a.n + (p < end ? p : end - 1)];
+            }
+        }
     }
     // flow ids and sizes once per round, loaded one round ahead (clamped loads)
     uint32_t idsn[kScItems], szsn[kScItems];
@@ -730,18 +720,28 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
         for (int i = 0; i < kScItems; i++) { ids[i] = idsn[i]; szs[i] = szsn[i]; }
         if (rb + kScRound < end) load_ids(rb + kScRound);
         for (uint32_t r = 0; r < d; r++) {
-            __syncthreads();
+            // no barrier needed here: this step's count buffer was cleared in the
+            // previous step's phase 2, which a barrier closed
+            uint32_t *s_cnt = s_cnt2 + par * kScWaves * LB;
+            uint32_t *s_cnto = s_cnt2 + (par ^ 1u) * kScWaves * LB;
+            par ^= 1u;
+            if (r == 0 && rb == beg) __syncthreads();  // s_goff / buffers initialised
             uint32_t bs[kScItems];
 #pragma unroll
             for (int i = 0; i < kScItems; i++) bs[i] = bsn[i];
             {
-                const uint32_t nr = r + 1 < d ? r + 1 : 0u;
-                const uint64_t nrb = r + 1 < d ? rb : rb + kScRound;
+                // (nrb, nr) = the step after the next one
+                const uint64_t rb1 = r + 1 < d ? rb : rb + kScRound;
+                const uint32_t r1 = r + 1 < d ? r + 1 : 0u;
+                const uint64_t nrb = r1 + 1 < d ? rb1 : rb1 + kScRound;
+                const uint32_t nr = r1 + 1 < d ? r1 + 1 : 0u;
+#pragma unroll
+                for (int i = 0; i < kScItems; i++) bsn[i] = bsn2[i];
                 if (nrb < end) {
 #pragma unroll
                     for (int i = 0; i < kScItems; i++) {
                         const uint64_t p = nrb + (uint64_t)wave * 64 * kScItems + (uint64_t)i * 64 + lane;
-                        bsn[i] = a.idx[(uint64_t)nr * a.n + (p < end ? p : end - 1)];
+                        bsn2[i] = a.idx[(uint64_t)nr * a.n + (p < end ? p : end - 1)];
                     }
                 }
             }
@@ -802,59 +802,30 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
             }
             __syncthreads();
             K3_MARK(1);
-            // phase 2: per bin, exclusive prefix over waves; block scan over bins
-            uint32_t tot[TPT];
-            uint32_t lsum = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < TPT; j++) {
-                const uint32_t t = tid * TPT + j;
-                uint32_t c = 0;
-                if (t < LB) {
+            // phase 2: per bin, global base of each wave's run; clear the other buffer
+            {
+                uint32_t *goff = s_goff + r * LB;
+                for (uint32_t t = tid; t < LB; t += kScThreads) {
                     uint32_t x[kScWaves];
 #pragma unroll
                     for (uint32_t w = 0; w < (uint32_t)kScWaves; w++) x[w] = s_cnt[w * LB + t];
+                    uint32_t c = goff[t];
 #pragma unroll
                     for (uint32_t w = 0; w < (uint32_t)kScWaves; w++) { s_cnt[w * LB + t] = c; c += x[w]; }
+                    goff[t] = c;
                 }
-                tot[j] = c;
-                lsum += c;
-            }
-            uint32_t rtotal;
-            uint32_t run = block_excl_scan<kScWaves>(lsum, s_w, &rtotal);
-            uint32_t *goff = s_goff + r * LB;
-#pragma unroll
-            for (uint32_t j = 0; j < TPT; j++) {
-                const uint32_t t = tid * TPT + j;
-                if (t < LB) { s_rstart[t] = run; s_dbase[t] = goff[t] - run; }
-                run += tot[j];
+                for (uint32_t t = tid; t < kScWaves * LB; t += kScThreads) s_cnto[t] = 0;
             }
             __syncthreads();
             K3_MARK(2);
-            // phase 3: stage in bin order
+#pragma unroll
+            for (int i = 0; i < kScItems; i++) asm volatile("" ::"v"(bsn[i]));
+            // phase 3: each update straight to its slot (runs per bin and wave are contiguous)
 #pragma unroll
             for (int i = 0; i < kScItems; i++) {
                 if ((br[i] >> 16) != 0xFFFFu) {
                     const uint32_t t = br[i] >> 16;
-                    const uint32_t l = s_rstart[t] + s_cnt[wave * LB + t] + (br[i] & 0xFFFFu);
-                    s_ent[l] = ent[i];
-                    s_bin[l] = (uint16_t)t;
-                }
-            }
-            __syncthreads();
-            K3_MARK(3);
-            // the next step's codes are needed now, before this step's stores: the
-            // wait after a loop of stores would drain them (vmcnt is one in-order counter)
-#pragma unroll
-            for (int i = 0; i < kScItems; i++) asm volatile("" ::"v"(bsn[i]));
-            // phase 4: contiguous runs per bin to global
-            for (uint32_t s2 = tid; s2 < rtotal; s2 += kScThreads) a.entries[s_dbase[s_bin[s2]] + s2] = s_ent[s2];
-            __syncthreads();
-#pragma unroll
-            for (uint32_t j = 0; j < TPT; j++) {
-                const uint32_t t = tid * TPT + j;
-                if (t < LB) {
-                    goff[t] += tot[j];
-                    for (uint32_t w = 0; w < (uint32_t)kScWaves; w++) s_cnt[w * LB + t] = 0;
+                    a.entries[s_cnt[wave * LB + t] + (br[i] & 0xFFFFu)] = ent[i];
                 }
             }
             K3_MARK(4);
