@@ -98,7 +98,7 @@ struct CmGeom {
 // exactness comes from the verify/fallback steps (k_hot_verify, k_hot_fallback).
 // ---------------------------------------------------------------------------
 // Per-row lookup table of the designated buckets, built once per batch by
-// k_hot_table (deterministic, single thread per row) and copied to LDS by K1:
+// k_hot_table (deterministic: as if inserted in hot-slot order) and copied to LDS by K1:
 // 128 groups of 4 entries (one 16-byte LDS read per lookup, no probing);
 // entry = bucket << kHotBits | hot slot, empty = ~0.  A bucket whose group is full is
 // simply not designated (designation only moves work).
@@ -575,8 +575,17 @@ __global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t *x, uint64_t
     __shared__ uint32_t s_w[4];
     const uint64_t base = (uint64_t)blockIdx.x * kScanSeg;
     uint32_t sum = 0;
-    for (uint32_t i = threadIdx.x; i < kScanSeg; i += 256)
-        if (base + i < N) sum += x[base + i];
+    if (base + kScanSeg <= N) {
+        const uint4 *x4 = reinterpret_cast<const uint4 *>(x + base);
+        uint4 v[kScanSeg / 1024];
+#pragma unroll
+        for (uint32_t j = 0; j < kScanSeg / 1024; j++) v[j] = x4[threadIdx.x + 256 * j];
+#pragma unroll
+        for (uint32_t j = 0; j < kScanSeg / 1024; j++) sum += v[j].x + v[j].y + v[j].z + v[j].w;
+    } else {
+        for (uint32_t i = threadIdx.x; i < kScanSeg; i += 256)
+            if (base + i < N) sum += x[base + i];
+    }
     uint32_t tot;
     (void)block_excl_scan256(sum, s_w, &tot);
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
@@ -602,15 +611,36 @@ __global__ __launch_bounds__(256) void k_scan_down(uint32_t *x, uint64_t N, cons
     const uint64_t base = (uint64_t)blockIdx.x * kScanSeg;
     constexpr uint32_t per = kScanSeg / 256;  // 16 contiguous per thread
     const uint64_t t0 = base + threadIdx.x * per;
+    static_assert(per == 16, "four 16-byte vectors per thread");
+    const bool full = t0 + per <= N;
     uint32_t v[per];
+    if (full) {
+        const uint4 *x4 = reinterpret_cast<const uint4 *>(x + t0);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint4 q = x4[j];
+            v[4 * j] = q.x; v[4 * j + 1] = q.y; v[4 * j + 2] = q.z; v[4 * j + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < per; i++) v[i] = (t0 + i < N) ? x[t0 + i] : 0u;
+    }
     uint32_t sum = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < per; i++) { v[i] = (t0 + i < N) ? x[t0 + i] : 0u; sum += v[i]; }
+    for (uint32_t i = 0; i < per; i++) sum += v[i];
     uint32_t tot;
     uint32_t run = block_excl_scan256(sum, s_w, &tot) + part[blockIdx.x];
 #pragma unroll
-    for (uint32_t i = 0; i < per; i++)
-        if (t0 + i < N) { x[t0 + i] = run; run += v[i]; }
+    for (uint32_t i = 0; i < per; i++) { const uint32_t e = v[i]; v[i] = run; run += e; }
+    if (full) {
+        uint4 *x4 = reinterpret_cast<uint4 *>(x + t0);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) x4[j] = make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < per; i++)
+            if (t0 + i < N) x[t0 + i] = v[i];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -858,22 +888,43 @@ __global__ __launch_bounds__(256) void k_lds_order_probe(uint32_t *viol, int ite
 // Order bins by size (largest first) so the heavy bins start first.
 __global__ __launch_bounds__(1024) void k_order(const uint32_t *offsets, uint32_t nblk, uint32_t nbins,
                                                 uint32_t nall, const uint32_t *total, uint32_t *order) {
-    __shared__ uint32_t s_sz[4096];
+    // K4 schedule: bins by decreasing size (1/8-octave classes; order within a
+    // class is arbitrary: it only balances the launch, results do not depend on it)
+    constexpr uint32_t NK = 33 * 8;
+    __shared__ uint32_t s_cnt[NK];
+    __shared__ uint16_t s_key[4096];
+    for (uint32_t k = threadIdx.x; k < NK; k += 1024) s_cnt[k] = 0;
+    __syncthreads();
     for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
         const uint32_t s0 = offsets[(uint64_t)b * nblk];
         const uint32_t s1 = (b + 1 < nall) ? offsets[(uint64_t)(b + 1) * nblk] : *total;
-        s_sz[b] = s1 - s0;
+        const uint32_t sz = s1 - s0;
+        const uint32_t lz = __clz(sz);
+        const uint32_t key = sz == 0 ? 0u : (32u - lz) * 8u + ((sz << lz) >> 28 & 7u);
+        s_key[b] = (uint16_t)key;
+        atomicAdd(&s_cnt[key], 1u);
     }
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
-        const uint32_t mine = s_sz[b];
-        uint32_t rank = 0;
-        for (uint32_t j = 0; j < nbins; j++) {
-            const uint32_t o = s_sz[j];
-            rank += (o > mine) || (o == mine && j < b);
+    if (threadIdx.x < 64) {  // descending exclusive scan of the class counts
+        constexpr uint32_t PER = (NK + 63) / 64;
+        const uint32_t lane = threadIdx.x;
+        uint32_t x[PER], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t k = lane * PER + q;  // k-th class from the top
+            x[q] = k < NK ? s_cnt[NK - 1 - k] : 0u;
+            sum += x[q];
         }
-        order[rank] = b;
+        uint32_t run = wave_incl_scan(sum) - sum;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t k = lane * PER + q;
+            if (k < NK) s_cnt[NK - 1 - k] = run;
+            run += x[q];
+        }
     }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbins; b += 1024) order[atomicAdd(&s_cnt[s_key[b]], 1u)] = b;
 }
 
 // ---------------------------------------------------------------------------
@@ -1426,10 +1477,13 @@ __device__ __forceinline__ void block_sum2(long long &x, long long &y, long long
 // H1: walk totals of every segment of every hot bin (owner = batch-entry fingerprint)
 __global__ __launch_bounds__(256) void k_hot_sum(HotArgs a) {
     __shared__ long long sh[8];
-    const uint32_t hb = blockIdx.y, sidx = blockIdx.x;
-    if (*a.hany == 0 || (a.hflag2[hb] & 3u) == 0) return;
+    if (*a.hany == 0) return;
+    // grid-stride over (slot, segment): a small grid exits fast in the common case
+    for (uint32_t wi = blockIdx.x; wi < a.g.d * kHot * kHotSegs; wi += gridDim.x) {
+    const uint32_t hb = wi / kHotSegs, sidx = wi % kHotSegs;
+    if ((a.hflag2[hb] & 3u) == 0) continue;
     const uint32_t id = a.hot_ids[hb];
-    if (id == GNS_ID_NONE) return;
+    if (id == GNS_ID_NONE) continue;
     uint32_t beg, end, sb, se;
     hot_bin_range(a, hb, beg, end);
     hot_seg_range(beg, end, sidx, sb, se);
@@ -1447,6 +1501,7 @@ __global__ __launch_bounds__(256) void k_hot_sum(HotArgs a) {
         a.segtot[((size_t)hb * kHotSegs + sidx) * 2] = wc;
         a.segtot[((size_t)hb * kHotSegs + sidx) * 2 + 1] = ws;
     }
+    }
 }
 
 // H2: exact check.  With no event the owner never changes and every counter
@@ -1455,15 +1510,18 @@ __global__ __launch_bounds__(256) void k_hot_sum(HotArgs a) {
 // would find C <= 1 (:226-231 take-over) or S == 0 / s > S (:184-200).
 __global__ __launch_bounds__(256) void k_hot_verify(HotArgs a) {
     __shared__ long long sh_w[2][4];
-    const uint32_t hb = blockIdx.y, sidx = blockIdx.x, tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u, wave = tid >> 6;
-    if (*a.hany == 0 || (a.hflag2[hb] & 3u) == 0) return;
+    if (*a.hany == 0) return;
+    for (uint32_t wi = blockIdx.x; wi < a.g.d * kHot * kHotSegs; wi += gridDim.x) {
+    const uint32_t hb = wi / kHotSegs, sidx = wi % kHotSegs;
+    if ((a.hflag2[hb] & 3u) == 0) continue;
     const uint32_t id = a.hot_ids[hb];
-    if (id == GNS_ID_NONE) return;
+    if (id == GNS_ID_NONE) continue;
     uint32_t beg, end, sb, se;
     hot_bin_range(a, hb, beg, end);
     hot_seg_range(beg, end, sidx, sb, se);
-    if (sb >= se) return;
+    if (sb >= se) continue;
     const uint64_t cell = (uint64_t)(hb / kHot) * a.g.w + id;
     const uint32_t F_c = a.Fc[cell], F_s = a.Fs[cell];
     long long run_c = a.C[cell], run_s = a.S[cell];
@@ -1510,6 +1568,7 @@ __global__ __launch_bounds__(256) void k_hot_verify(HotArgs a) {
     }
     const uint32_t any = (uint32_t)(__ballot(ev & 1u) != 0) | ((uint32_t)(__ballot(ev & 2u) != 0) << 1);
     if (lane == 0 && any) atomicOr(&a.hflag[hb], any);
+    }
 }
 
 // H3: apply the verified halves; flagged halves keep the batch-entry state
@@ -1728,18 +1787,20 @@ __global__ __launch_bounds__(256) void k_hot_hist(const uint32_t *C, CmGeom g, u
 }
 
 __global__ void k_hot_pick(uint32_t *hh, CmGeom g, uint32_t *thr, uint32_t *hcnt, uint32_t *hot_ids) {
-    const uint32_t r = threadIdx.x;
+    __shared__ uint32_t s_hh[8 * kHotKeys];
     for (uint32_t i = threadIdx.x; i < g.d * kHot; i += blockDim.x) hot_ids[i] = GNS_ID_NONE;
+    for (uint32_t i = threadIdx.x; i < g.d * kHotKeys; i += blockDim.x) { s_hh[i] = hh[i]; hh[i] = 0; }
+    __syncthreads();
+    const uint32_t r = threadIdx.x;
     if (r < g.d) {
         uint32_t cum = 0, t = kHotKeys;
         for (int k = (int)kHotKeys - 1; k >= (int)(kHotMinBits * 8); k--) {
-            cum += hh[r * kHotKeys + k];
+            cum += s_hh[r * kHotKeys + k];
             if (cum > kHot) break;
             t = (uint32_t)k;
         }
         thr[r] = t;
         hcnt[r] = 0;
-        for (uint32_t k = 0; k < kHotKeys; k++) hh[r * kHotKeys + k] = 0;
     }
 }
 
@@ -1758,19 +1819,26 @@ __global__ __launch_bounds__(256) void k_hot_collect(const uint32_t *C, CmGeom g
 
 // Lookup groups of the designated buckets (one thread per row, deterministic);
 // a bucket whose group is full is dropped from the designation.
-__global__ void k_hot_table(CmGeom g, uint32_t *hot_ids, uint32_t *hot_tab) {
-    const uint32_t r = threadIdx.x;
-    if (r >= g.d) return;
-    uint32_t *tab = hot_tab + r * kHotTab;
-    for (uint32_t i = 0; i < kHotTab; i++) tab[i] = 0xFFFFFFFFu;
-    for (uint32_t h = 0; h < kHot; h++) {
-        const uint32_t b = hot_ids[r * kHot + h];
+__global__ __launch_bounds__(1024) void k_hot_table(CmGeom g, uint32_t *hot_ids, uint32_t *hot_tab) {
+    // entry h of a row takes slot j of its group, j = number of earlier valid
+    // entries of the row in the same group (what inserting in h order gives);
+    // j >= 4: the group is full and the bucket is not designated
+    __shared__ uint32_t s_ids[8 * kHot];
+    const uint32_t NS = g.d * kHot;
+    for (uint32_t i = threadIdx.x; i < g.d * kHotTab; i += blockDim.x) hot_tab[i] = 0xFFFFFFFFu;
+    for (uint32_t i = threadIdx.x; i < NS; i += blockDim.x) s_ids[i] = hot_ids[i];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < NS; i += blockDim.x) {
+        const uint32_t r = i / kHot, h = i % kHot, b = s_ids[i];
         if (b == GNS_ID_NONE) continue;
-        uint32_t *grp = tab + hot_group(b) * 4;
+        const uint32_t grp = hot_group(b);
         uint32_t j = 0;
-        while (j < 4 && grp[j] != 0xFFFFFFFFu) j++;
-        if (j < 4) grp[j] = b << kHotBits | h;
-        else hot_ids[r * kHot + h] = GNS_ID_NONE;
+        for (uint32_t h2 = 0; h2 < h; h2++) {
+            const uint32_t b2 = s_ids[r * kHot + h2];
+            j += (b2 != GNS_ID_NONE && hot_group(b2) == grp) ? 1u : 0u;
+        }
+        if (j < 4) hot_tab[r * kHotTab + grp * 4 + j] = b << kHotBits | h;
+        else hot_ids[i] = GNS_ID_NONE;
     }
 }
 
@@ -2053,8 +2121,8 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
             else
                 hipLaunchKernelGGL(k_scatter<0>, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
         }
-        hipLaunchKernelGGL(k_hot_sum, dim3(kHotSegs, g.d * kHot), dim3(256), 0, s, h);
-        hipLaunchKernelGGL(k_hot_verify, dim3(kHotSegs, g.d * kHot), dim3(256), 0, s, h);
+        hipLaunchKernelGGL(k_hot_sum, dim3(1024), dim3(256), 0, s, h);
+        hipLaunchKernelGGL(k_hot_verify, dim3(1024), dim3(256), 0, s, h);
         hipLaunchKernelGGL(k_hot_apply, dim3((g.d * kHot + 511) / 512), dim3(512), 0, s, h);
         hipLaunchKernelGGL(k_hot_fallback, dim3(g.d * kHot), dim3(64), 0, s, h);
         GNS_HIP(hipGetLastError());
@@ -2064,10 +2132,11 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         ScopedStage st(cm->timer, 7);
         const uint64_t cells = (uint64_t)g.d * g.w;
         const unsigned grid = (unsigned)std::min<uint64_t>(2048, (cells + 255) / 256);
-        hipLaunchKernelGGL(k_hot_hist, dim3(grid), dim3(256), 0, s, cm->C, g, cm->hhist);
+        // few blocks for the histogram: its flush is one global atomic per (block, nonzero class)
+        hipLaunchKernelGGL(k_hot_hist, dim3(std::min(grid, 256u)), dim3(256), 0, s, cm->C, g, cm->hhist);
         hipLaunchKernelGGL(k_hot_pick, dim3(1), dim3(512), 0, s, cm->hhist, g, cm->hthr, cm->hcnt, cm->hot_ids);
         hipLaunchKernelGGL(k_hot_collect, dim3(grid), dim3(256), 0, s, cm->C, g, cm->hthr, cm->hcnt, cm->hot_ids);
-        hipLaunchKernelGGL(k_hot_table, dim3(1), dim3(64), 0, s, g, cm->hot_ids, cm->hot_tab);
+        hipLaunchKernelGGL(k_hot_table, dim3(1), dim3(1024), 0, s, g, cm->hot_ids, cm->hot_tab);
         GNS_HIP(hipGetLastError());
     }
     cm->warm = true;
