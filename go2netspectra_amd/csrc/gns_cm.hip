@@ -1147,22 +1147,9 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                 incN = 1ull | (uint64_t)oc << 14 | (uint64_t)os << 28;
                 incS = os ? (uint64_t)s << 32 : (uint64_t)s;
             }
-            // heavy bins: most lanes of a wave hit one bucket -> one LDS atomic
-            const uint32_t b0 = __builtin_amdgcn_readfirstlane(b);
-            const bool m0 = v[j] && !ovf && b == b0;
-            const uint64_t mm = __ballot(m0);
-            if (__popcll(mm) >= 16) {
-                const uint64_t sN = wave_sum64(m0 ? incN : 0ull);
-                const uint64_t sS_ = wave_sum64(m0 ? incS : 0ull);
-                if (lane == (uint32_t)__ffsll((long long)mm) - 1) {
-                    atomicAdd(&accN[b0], (unsigned long long)sN);
-                    atomicAdd(&accS[b0], (unsigned long long)sS_);
-                }
-                if (v[j] && !ovf && !m0) {
-                    atomicAdd(&accN[b], (unsigned long long)incN);
-                    atomicAdd(&accS[b], (unsigned long long)incS);
-                }
-            } else if (v[j] && !ovf) {
+            // (designated buckets never reach K4, so a wave's updates rarely share a
+            // bucket: plain per-lane LDS atomics beat a wave-majority pre-sum here)
+            if (v[j] && !ovf) {
                 atomicAdd(&accN[b], (unsigned long long)incN);
                 atomicAdd(&accS[b], (unsigned long long)incS);
             }
