@@ -66,7 +66,7 @@ class CmParams(ct.Structure):
     _fields_ = [("width", ct.c_uint32), ("depth", ct.c_uint32), ("size_threshold", ct.c_uint32),
                 ("count_threshold", ct.c_uint32), ("flow", Layout), ("key_bytes", ct.c_uint32),
                 ("seeds", ct.c_void_p), ("max_flows", ct.c_uint64), ("batch_packets", ct.c_uint64),
-                ("device", ct.c_int)]
+                ("device", ct.c_int), ("bucket_lo", ct.c_uint32), ("bucket_hi", ct.c_uint32)]
 
 
 class SsParams(ct.Structure):

@@ -87,6 +87,7 @@ struct CmGeom {
     uint32_t tile_bits, ntiles, nbins, nbits;  // nbits = ceil_log2(ntiles + kHot); ntiles = bins per row
     uint32_t bin_bits, sub_bits;               // bin = 2^sub_bits LDS tiles of 2^tile_bits buckets
     uint32_t nbins_all;                        // nbins + d*kHot (hot bins follow the tile bins)
+    uint32_t blo, bspan;                       // bucket-range slice [blo, blo + bspan) applied by K4 (whole row: 0, w)
     uint32_t seeds[8];
 };
 
@@ -1098,7 +1099,7 @@ __device__ __forceinline__ void replay_group(ApplyLds &L, bool pending, uint32_t
 
 // Updates ent[beg, end) (stream order) of one LDS tile: buckets cbase .. cbase+tn-1.
 __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, const uint64_t *ent, uint32_t beg,
-                                           uint32_t end, uint64_t cbase, uint32_t tn) {
+                                           uint32_t end, uint64_t cbase, uint32_t tn, uint32_t col0) {
     uint32_t *sC = L.sC, *sFc = L.sFc, *sS = L.sS, *sFs = L.sFs;
     unsigned long long *accN = L.accN, *accS = L.accS;
     uint16_t *s_list = L.s_list;
@@ -1135,10 +1136,11 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
 #pragma unroll
         for (int j = 0; j < kApItems; j++) {
             const uint32_t q = cb + j * kApThreads + tid;
-            v[j] = q < end;
             const uint32_t lo = (uint32_t)e[j];
             const uint32_t hi = (uint32_t)(e[j] >> 32);
             const uint32_t b = hi & (kTileMax - 1u);
+            // bucket-range slice (exact global mode): other handles own the rest of the row
+            v[j] = q < end && (col0 + b) - a.g.blo < a.g.bspan;
             const bool ovf = (lo & kOvfFlag) != 0;
             uint64_t incN = 0, incS = 0;
             if (v[j] && !ovf) {
@@ -1395,7 +1397,7 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
     const uint32_t r = bin / g.ntiles, t = bin % g.ntiles;
     const uint32_t bbase = t << g.bin_bits;
     if (g.sub_bits == 0) {
-        apply_tile(a, L, a.entries, beg, end, (uint64_t)r * g.w + bbase, min(1u << g.tile_bits, g.w - bbase));
+        apply_tile(a, L, a.entries, beg, end, (uint64_t)r * g.w + bbase, min(1u << g.tile_bits, g.w - bbase), bbase);
         return;
     }
     sub_partition(a.entries, a.entries2, beg, end, g.tile_bits, g.sub_bits, P);
@@ -1403,7 +1405,7 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
         const uint32_t tbase = bbase + (st << g.tile_bits);
         const uint32_t sb = beg + P.soff[st], se = beg + P.soff[st + 1];
         if (tbase >= g.w || sb >= se) continue;
-        apply_tile(a, L, a.entries2, sb, se, (uint64_t)r * g.w + tbase, min(1u << g.tile_bits, g.w - tbase));
+        apply_tile(a, L, a.entries2, sb, se, (uint64_t)r * g.w + tbase, min(1u << g.tile_bits, g.w - tbase), tbase);
         __syncthreads();
     }
 }
@@ -2220,6 +2222,14 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         cm->K = cm->kp.K;
         if (g.w >= (1u << (32 - kHotBits))) {  // designated-bucket table entries hold bucket << kHotBits
             set_error("width %u >= 2^%u is not supported", g.w, 32 - kHotBits); rc = GNS_E_RANGE; break;
+        }
+        if (p->bucket_lo == 0 && p->bucket_hi == 0) {
+            g.blo = 0; g.bspan = g.w;
+        } else if (p->bucket_lo < p->bucket_hi && p->bucket_hi <= g.w) {
+            g.blo = p->bucket_lo; g.bspan = p->bucket_hi - p->bucket_lo;
+        } else {
+            set_error("bucket range [%u, %u) is not inside [0, %u)", p->bucket_lo, p->bucket_hi, g.w);
+            rc = GNS_E_ARG; break;
         }
         g.pow2 = (g.w & (g.w - 1)) == 0;
         g.wmask = g.pow2 ? g.w - 1 : 0;

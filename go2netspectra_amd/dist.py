@@ -114,3 +114,74 @@ def allgather_heavy(hh: HeavyRecord, world: int) -> HeavyRecord:
     sz = _unpack(_allgather_rows(_pack([(h.Flow, h.Size) for h in hh.Size], K), world), K)
     merged_s = merge_heavy([sz])
     return HeavyRecord(Size=[HeavySize(f, v) for f, v in merged_s], Count=[HeavyCount(f, v) for f, v in merged_c])
+
+
+# ---------------------------------------------------------------------------
+# Exact global mode (SURVEY §8e "exact global alternative"): every GPU sees the
+# whole stream but applies only the updates that fall in its slice of bucket
+# columns [lo, hi) of every row (CountMin(bucket_range=...)).  Buckets are
+# independent (count_min.go:94-157 touches one bucket per row), so the slices
+# together are exactly the single-GPU sketch; the global state is an
+# all-gather of the slices.  Input is replicated, so this mode does not scale
+# throughput: it is the bit-exact correctness mode, flow sharding is the
+# scaling mode.
+# ---------------------------------------------------------------------------
+def bucket_slice(rank: int, world: int, width: int):
+    """[lo, hi) bucket columns owned by `rank` (contiguous, sizes differ by at most one)."""
+    return (rank * width // world, (rank + 1) * width // world)
+
+
+def assemble_slices(states, ranges, width: int, depth: int):
+    """Global (C, S, FPc, FPs) from per-slice exports (each a full-size export
+    whose columns outside its range are untouched)."""
+    C = np.zeros(depth * width, np.uint32)
+    S = np.zeros(depth * width, np.uint32)
+    K = states[0][2].shape[1]
+    Fc = np.zeros((depth * width, K), np.uint8)
+    Fs = np.zeros((depth * width, K), np.uint8)
+    for (c, s, fc, fs), (lo, hi) in zip(states, ranges):
+        for r in range(depth):
+            sl = slice(r * width + lo, r * width + hi)
+            C[sl], S[sl], Fc[sl], Fs[sl] = c[sl], s[sl], fc[sl], fs[sl]
+    return C, S, Fc, Fs
+
+
+def allgather_slices(state, rank: int, world: int, width: int, depth: int):
+    """All-gather of every rank's slice (RCCL on GPU, gloo on CPU) -> the global state."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    C, S, Fc, Fs = state
+    K = Fc.shape[1]
+    lo, hi = bucket_slice(rank, world, width)
+    cap = max(bucket_slice(q, world, width)[1] - bucket_slice(q, world, width)[0] for q in range(world))
+    # per row: C, S as 4 bytes each + the two fingerprints, padded to the widest slice
+    rowb = 8 + 2 * K
+    mine = np.zeros((depth, cap, rowb), np.uint8)
+    for r in range(depth):
+        sl = slice(r * width + lo, r * width + hi)
+        mine[r, : hi - lo, 0:4] = C[sl].view(np.uint8).reshape(-1, 4)
+        mine[r, : hi - lo, 4:8] = S[sl].view(np.uint8).reshape(-1, 4)
+        mine[r, : hi - lo, 8:8 + K] = Fc[sl]
+        mine[r, : hi - lo, 8 + K:] = Fs[sl]
+    t = torch.from_numpy(mine).to(dev)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    states, ranges = [], []
+    for q, part in enumerate(parts):
+        a = part.cpu().numpy()
+        qlo, qhi = bucket_slice(q, world, width)
+        c = np.zeros(depth * width, np.uint32)
+        s = np.zeros(depth * width, np.uint32)
+        fc = np.zeros((depth * width, K), np.uint8)
+        fs = np.zeros((depth * width, K), np.uint8)
+        for r in range(depth):
+            sl = slice(r * width + qlo, r * width + qhi)
+            n = qhi - qlo
+            c[sl] = np.ascontiguousarray(a[r, :n, 0:4]).view(np.uint32).reshape(-1)
+            s[sl] = np.ascontiguousarray(a[r, :n, 4:8]).view(np.uint32).reshape(-1)
+            fc[sl] = a[r, :n, 8:8 + K]
+            fs[sl] = a[r, :n, 8 + K:]
+        states.append((c, s, fc, fs))
+        ranges.append((qlo, qhi))
+    return assemble_slices(states, ranges, width, depth)

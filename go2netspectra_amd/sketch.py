@@ -89,7 +89,9 @@ class CountMin:
     def __init__(self, width: int = 0, depth: int = 0, size_threshold: int = 0,
                  count_threshold: int = 0, flow_fields: Optional[Sequence[str]] = None,
                  key_bytes: Optional[int] = None, seeds=None, max_flows: int = 0,
-                 batch_packets: int = 0, device: int = 0):
+                 batch_packets: int = 0, device: int = 0, bucket_range=None):
+        """bucket_range=(lo, hi): apply only the updates whose row bucket is in
+        [lo, hi) (SURVEY §8e exact global mode; dist.bucket_slice / dist.assemble_slices)."""
         self._L = _lib.load()
         self.flow_fields = list(flow_fields or [])
         kb = key_bytes if key_bytes is not None else _lib.layout_bytes(self.flow_fields)
@@ -100,9 +102,12 @@ class CountMin:
         p.key_bytes = kb
         self._seeds, p.seeds = _seeds_arg(seeds, depth or 3)
         p.max_flows, p.batch_packets, p.device = max_flows, batch_packets, device
+        if bucket_range is not None:
+            p.bucket_lo, p.bucket_hi = int(bucket_range[0]), int(bucket_range[1])
         h = ct.c_void_p()
         check(self._L.gns_cm_create(ct.byref(p), ct.byref(h)))
         self._h = h
+        self.bucket_range = tuple(bucket_range) if bucket_range is not None else None
         self.width = width or (1 << 20)
         self.depth = depth or 3
         self.size_threshold = size_threshold or 512 * 1024

@@ -94,6 +94,12 @@ typedef struct gns_cm_params {
                                                  (flow dictionary capacity); 0 -> 4M */
     uint64_t batch_packets;                   /* device batch size; 0 -> 16M packets */
     int device;                               /* HIP device ordinal */
+    uint32_t bucket_lo, bucket_hi;            /* bucket-range slice (SURVEY §8e exact global
+                                                 mode): only updates whose row bucket lies in
+                                                 [bucket_lo, bucket_hi) are applied, so G handles
+                                                 fed the same stream with disjoint ranges hold,
+                                                 between them, exactly the state of one handle.
+                                                 0, 0 -> the whole row */
 } gns_cm_params;
 
 int gns_cm_create(const gns_cm_params *p, gns_cm **out);

@@ -279,3 +279,39 @@ def test_ballot_rank_fallback_parity(gpu, oracle, monkeypatch, w, d, K, nflows, 
     cm.flush()
     orc.insert_keys(keys, sizes)
     assert_same_state(cm, orc)
+
+
+@pytest.mark.parametrize("K,batch", [(16, 0), (37, 40_000)])
+def test_bucket_range_slices_are_the_global_sketch(gpu, oracle, K, batch):
+    """SURVEY §8e exact global mode: G handles with disjoint bucket ranges, each
+    fed the whole stream, together hold exactly the single sketch (hot
+    designation, replay and multi-batch paths included)."""
+    from go2netspectra_amd import CountMin
+    from go2netspectra_amd.dist import assemble_slices, bucket_slice
+    w, d = 5000, 4
+    rng = np.random.default_rng(77 + K)
+    seeds = rng.integers(0, 2**32, d, dtype=np.uint64).astype(np.uint32)
+    keys, _, _ = zipf_keys(rng, 400_000, 20_000, K)
+    sizes = sizes_u32(rng, 400_000)
+    orc = oracle.CountMin(w, d, 1000, 10, K, seeds)
+    orc.insert_keys(keys, sizes)
+    world = 3
+    states, ranges = [], []
+    for r in range(world):
+        rg = bucket_slice(r, world, w)
+        cm = CountMin(w, d, 1000, 10, key_bytes=K, seeds=seeds, batch_packets=batch, bucket_range=rg)
+        cm.insert_keys(keys, sizes)
+        cm.flush()
+        states.append(cm.export_state())
+        ranges.append(rg)
+        cm.close()
+    got = assemble_slices(states, ranges, w, d)
+    for name, a, b in zip(("C", "S", "FPc", "FPs"), got, orc.export()):
+        assert np.array_equal(a, b), name
+
+
+def test_bucket_range_rejects_bad_ranges(gpu):
+    from go2netspectra_amd import CountMin
+    for rg in [(10, 10), (20, 10), (0, 5001)]:
+        with pytest.raises(Exception):
+            CountMin(5000, 2, 1000, 10, key_bytes=16, bucket_range=rg)

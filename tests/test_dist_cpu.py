@@ -86,3 +86,61 @@ def test_two_rank_shard_and_allgather():
     assert total == len(batch)
     assert got_c == merge_heavy(lists_c) and got_s == merge_heavy(lists_s)
     assert len(got_c) > 0
+
+
+# --- exact global mode: bucket-range slices, all-gathered -------
+W_EX, D_EX, K_EX = 600, 3, 16   # width not divisible by the world size: uneven slices
+
+
+def _full_state():
+    from oracle import oracle as orc
+    t = _stream(8_000)
+    import sys
+    sys.path.insert(0, ROOT)
+    from go2netspectra_amd.packets import PacketBatch
+    batch = PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"])
+    cm = orc.CountMin(W_EX, D_EX, 50_000, 40, K_EX, np.array([7, 8, 9], np.uint32))
+    cm.insert_keys(batch.keys(["SrcIP"]), batch.length)
+    return cm.export()
+
+
+def _slice_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from go2netspectra_amd.dist import allgather_slices, bucket_slice
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # stand-in for CountMin(bucket_range=slice): the full sketch's columns inside
+    # the slice, everything else untouched (zero)
+    C, S, Fc, Fs = _full_state()
+    lo, hi = bucket_slice(rank, world, W_EX)
+    keep = np.zeros(D_EX * W_EX, bool)
+    for r in range(D_EX):
+        keep[r * W_EX + lo: r * W_EX + hi] = True
+    mine = (np.where(keep, C, 0).astype(np.uint32), np.where(keep, S, 0).astype(np.uint32),
+            np.where(keep[:, None], Fc, 0).astype(np.uint8), np.where(keep[:, None], Fs, 0).astype(np.uint8))
+    g = allgather_slices(mine, rank, world, W_EX, D_EX)
+    if rank == 0:
+        q.put([a.copy() for a in g])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bucket_slices_allgather(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slice_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = _full_state()
+    for g, w in zip(got, want):
+        assert np.array_equal(g, w)
+    assert want[0].any()
