@@ -120,7 +120,7 @@ def bench_superspread(args, torch, dist, world, rank, local):
     wl = torch.empty((n,), dtype=torch.int32, device=f"cuda:{local}")
     ss = SuperSpread(SS_W, SS_D, SS_THR, SS_M, 5, 0.5, 1.08, flow_fields=["SrcIP"], elem_fields=["DstIP"],
                      seeds=row_seeds(SS_D), hll_master=SS_HLL, rng_seed=SS_RNG,
-                     batch_packets=args.batch or (8 << 20), device=local)
+                     batch_packets=args.batch or n, device=local)  # one device batch per step, as the CM bench
     elapsed = 0.0
     for k in range(args.warmup + args.steps):
         syn.fill(hdr, wl, first=k * n)

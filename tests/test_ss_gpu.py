@@ -213,3 +213,16 @@ def test_superspreader_accuracy(gpu, oracle):
           f"ARE={are:.3f}")
     assert len(true_ss) > 10
     assert rec >= 0.8 and prec >= 0.8
+
+
+def test_bench_geometry_one_large_batch(gpu, oracle):
+    """configs[2] geometry (default task: d=2, w=32768, m=128, size 5) with the
+    whole stream in ONE device batch, as bench.py runs it, vs the oracle."""
+    rng = np.random.default_rng(2024)
+    n = 3_000_000
+    ss, orc = make_pair(oracle, 32768, 2, 128, 5, 16, 16, thr=4096, batch_packets=n)
+    fl, el, _ = spread_stream(rng, n, 200_000, 16, 16, s=1.1, elem_pool=1 << 20)
+    ss.insert_keys(fl, el)
+    ss.flush()
+    orc.insert(fl, el)
+    assert_same_ss(ss, orc)
