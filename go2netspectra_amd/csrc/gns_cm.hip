@@ -52,7 +52,10 @@ constexpr uint32_t kOvfFlag = 0x80000000u;
 constexpr uint32_t kOvfCap = 1u << 22;
 constexpr uint32_t kMaxBinsAll = 4096;               // d * bins per row (k_order, K3 LDS)
 constexpr int kExThreads = 256;
-constexpr uint32_t kChunk = 16384;                  // packets per K1/K3 block
+#ifndef GNS_CHUNK
+#define GNS_CHUNK 16384
+#endif
+constexpr uint32_t kChunk = GNS_CHUNK;              // packets per K1/K3 block
 #ifndef GNS_SC_THREADS
 #define GNS_SC_THREADS 512
 #endif
