@@ -249,8 +249,10 @@ struct SsSuccArgs {
     const uint8_t *regs;
     uint32_t m;
     uint64_t *skey;  // (cell << 27) | packet
-    uint32_t *sval;  // reg | lz << 8 | old << 16
+    uint64_t *sval;  // flow id << 32 | reg | lz << 8 | old << 16 (the id rides along the sort,
+                     // so S5's sequential walk has no dependent flowid[] load)
     uint32_t *scount;
+    const uint32_t *flowid;
 };
 
 __global__ __launch_bounds__(256) void k_ss_success(SsSuccArgs a) {
@@ -265,51 +267,105 @@ __global__ __launch_bounds__(256) void k_ss_success(SsSuccArgs a) {
         const uint32_t q = atomicAdd(a.scount, 1u);
         const uint64_t cell = seg / a.m;
         const uint32_t reg = (uint32_t)(seg % a.m);
-        a.skey[q] = cell << kSsPktBits | (key & ((1ull << kSsPktBits) - 1));
-        a.sval[q] = reg | lz << 8 | old << 16;
+        const uint32_t p = (uint32_t)(key & ((1ull << kSsPktBits) - 1));
+        a.skey[q] = cell << kSsPktBits | p;
+        a.sval[q] = (uint64_t)a.flowid[p] << 32 | (reg | lz << 8 | old << 16);
     }
 }
 
-// S5: every cell's encodes in stream order (one lane per cell):
-// register write, pbits (:105-109), sampling (:200-204), MV loop (:206-233).
+// S5: every cell's encodes in stream order: register write, pbits (:105-109),
+// sampling (:200-204), MV loop (:206-233).  Split in three so the long
+// sequential walks (one lane per cell; a superspreader's cell holds thousands
+// of encodes) carry only the state that is really sequential:
+//   S5a (per cell)   pbits walk -> tempP of every encode (table lookups + 2 adds)
+//   S5b (per encode) sampling from tempP: repeat count vv, or 0 (skip)
+//   S5c (per cell)   MV loop over the sampled encodes (owner: one add)
+// Same operations in the same order as the single walk, so bit-identical.
 struct SsApplyArgs {
     const uint64_t *skey;
-    const uint32_t *sval;
+    const uint64_t *sval;  // flow id << 32 | reg | lz << 8 | old << 16
     uint32_t n;
     SsGeom g;
     uint64_t pkt_base;
-    const uint32_t *flowid;
     uint8_t *regs;
     double *pbits;
     uint32_t *values, *keys;
+    double *tp;    // [n] pbits before each encode (S5a -> S5b); then log(1 - first MV draw) (S5b -> S5c)
+    int64_t *rep;  // [n] MV repeat count, 0 = not sampled (S5b -> S5c)
 };
 
 #pragma clang fp contract(off)
-__global__ __launch_bounds__(256) void k_ss_apply(SsApplyArgs a) {
+__global__ __launch_bounds__(256) void k_ss_walk_pbits(SsApplyArgs a) {
+    __shared__ double s_t[256];  // go_pow_int(base, k) / m for every register value k
+    const double mD = (double)a.g.m;
+    s_t[threadIdx.x] = go_pow_int(a.g.base, (double)threadIdx.x) / mD;
+    __syncthreads();
+    const uint32_t k0 = blockIdx.x * 256 + threadIdx.x;
+    if (k0 >= a.n) return;
+    const uint64_t cell = a.skey[k0] >> kSsPktBits;
+    if (k0 > 0 && (a.skey[k0 - 1] >> kSsPktBits) == cell) return;  // not a segment head
+    double pb = a.pbits[cell];
+    uint64_t vc = a.sval[k0];
+    for (uint32_t k = k0;;) {
+        const uint32_t kn = k + 1;
+        const uint64_t kx = kn < a.n ? a.skey[kn] : ~0ull;
+        const uint64_t vx = kn < a.n ? a.sval[kn] : 0ull;
+        const uint32_t v = (uint32_t)vc;
+        const uint32_t reg = v & 0xFFu, lz = (v >> 8) & 0xFFu, old = (v >> 16) & 0xFFu;
+        a.regs[cell * a.g.m + reg] = (uint8_t)lz;
+        a.tp[k] = pb;                                    // tempP (:105)
+        pb = pb + (-s_t[old]);                           // :106
+        if (lz < a.g.maxv) pb = pb + s_t[lz];            // :107-109
+        if ((kx >> kSsPktBits) != cell) break;
+        k = kn; vc = vx;
+    }
+    a.pbits[cell] = pb;
+}
+
+__global__ __launch_bounds__(256) void k_ss_sample(SsApplyArgs a) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= a.n) return;
+    const double tempP = a.tp[k];
+    int64_t vv = 0;
+    if (tempP != -1.0) {                                                  // :196
+        const uint64_t key = a.skey[k];
+        const uint32_t row = (uint32_t)((key >> kSsPktBits) / a.g.w);
+        const double inv = 1.0 / tempP;
+        const double cv = ceil(inv);
+        const double pCU = inv / cv;                                      // :200
+        const uint64_t pkt = a.pkt_base + (key & ((1ull << kSsPktBits) - 1));
+        if (!(ss_uniform(a.g.rng_seed, pkt, row, 0) >= pCU)) {            // :201-204
+            vv = (cv < 9223372036854775808.0) ? (int64_t)cv : INT64_MIN;  // :206, amd64 semantics
+            // the MV loop's first draw does not depend on the cell state: its log here, in parallel
+            a.tp[k] = gm_log(1.0 - ss_uniform(a.g.rng_seed, pkt, row, 1));
+        }
+    }
+    a.rep[k] = vv;
+}
+
+__global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
     const uint32_t k0 = blockIdx.x * 256 + threadIdx.x;
     if (k0 >= a.n) return;
     const uint64_t cell = a.skey[k0] >> kSsPktBits;
     if (k0 > 0 && (a.skey[k0 - 1] >> kSsPktBits) == cell) return;  // not a segment head
     const uint32_t row = (uint32_t)(cell / a.g.w);
-    const double mD = (double)a.g.m;
-    double pb = a.pbits[cell];
     uint32_t val = a.values[cell], key = a.keys[cell];
-    for (uint32_t k = k0; k < a.n && (a.skey[k] >> kSsPktBits) == cell; k++) {
-        const uint64_t p = a.skey[k] & ((1ull << kSsPktBits) - 1);
-        const uint32_t v = a.sval[k];
-        const uint32_t reg = v & 0xFFu, lz = (v >> 8) & 0xFFu, old = (v >> 16) & 0xFFu;
-        a.regs[cell * a.g.m + reg] = (uint8_t)lz;
-        const double tempP = pb;                                            // :105
-        pb = pb + (-go_pow_int(a.g.base, (double)old) / mD);                // :106
-        if (lz < a.g.maxv) pb = pb + go_pow_int(a.g.base, (double)lz) / mD; // :107-109
-        if (tempP == -1.0) continue;                                        // :196
-        const double inv = 1.0 / tempP;
-        const double cv = ceil(inv);
-        const double pCU = inv / cv;                                        // :200
-        const uint64_t pkt = a.pkt_base + p;
-        if (ss_uniform(a.g.rng_seed, pkt, row, 0) >= pCU) continue;          // :201-204
-        int64_t vv = (cv < 9223372036854775808.0) ? (int64_t)cv : INT64_MIN;  // :206, amd64 semantics
-        const uint32_t f = a.flowid[p];
+    // b^-val and log1m(b^-val) depend only on val: kept for the next foreign
+    // encode while val does not change
+    uint32_t mval = 0xFFFFFFFFu;
+    double mppp = 0.0, ml1m = 0.0;
+    uint64_t kc = a.skey[k0], vc = a.sval[k0];
+    int64_t rc = a.rep[k0];
+    double lc = a.tp[k0];
+    for (uint32_t k = k0;;) {
+        const uint32_t kn = k + 1;  // the next encode's inputs load while this one runs
+        const uint64_t kx = kn < a.n ? a.skey[kn] : ~0ull;
+        const uint64_t vx = kn < a.n ? a.sval[kn] : 0ull;
+        const int64_t rx = kn < a.n ? a.rep[kn] : 0;
+        const double lx = kn < a.n ? a.tp[kn] : 0.0;
+        int64_t vv = rc;
+        const uint32_t f = (uint32_t)(vc >> 32);
+        const uint64_t pkt = a.pkt_base + (kc & ((1ull << kSsPktBits) - 1));
         uint32_t draw = 1;
         while (vv > 0) {                                                    // :207-233
             if (val == 0 || key == f) {  // every remaining iteration increments (:211-220)
@@ -317,7 +373,12 @@ __global__ __launch_bounds__(256) void k_ss_apply(SsApplyArgs a) {
                 val = (uint32_t)((uint64_t)val + (uint64_t)vv);
                 break;
             }
-            const double ppp = go_pow_int(a.g.b, -(double)val);              // :222
+            if (val != mval) {
+                mval = val;
+                mppp = go_pow_int(a.g.b, -(double)val);                         // :222
+                ml1m = (mppp > 0 && mppp < 1) ? gm_log1m(mppp) : 0.0;
+            }
+            const double ppp = mppp;
             if (!(ppp > 0)) break;  // underflow: no later iteration can decrement
             if (ppp >= 1) {         // b <= 1: every iteration decrements
                 const int64_t dec = (int64_t)val < vv ? (int64_t)val : vv;
@@ -326,15 +387,17 @@ __global__ __launch_bounds__(256) void k_ss_apply(SsApplyArgs a) {
                 continue;
             }
             // declared generator: failed iterations before the next decrement
-            // (:223-227) as one geometric waiting time
-            const double u = ss_uniform(a.g.rng_seed, pkt, row, draw++);
-            const double q = gm_log(1.0 - u) / gm_log1m(ppp);
+            // (:223-227) as one geometric waiting time; the first draw's log came from S5b
+            const double lu = draw == 1 ? lc : gm_log(1.0 - ss_uniform(a.g.rng_seed, pkt, row, draw));
+            draw++;
+            const double q = lu / ml1m;
             if (!(q < (double)vv)) break;
             vv -= (int64_t)floor(q) + 1;
             val -= 1;
         }
+        if ((kx >> kSsPktBits) != cell) break;
+        k = kn; kc = kx; vc = vx; rc = rx; lc = lx;
     }
-    a.pbits[cell] = pb;
     a.values[cell] = val;
     a.keys[cell] = key;
 }
@@ -413,7 +476,8 @@ struct gns_ss {
     uint32_t *ptotal = nullptr;
     uint64_t ccap = 0;
     uint64_t *ckey = nullptr, *ckey_s = nullptr, *skey = nullptr, *skey_s = nullptr;
-    uint32_t *cval = nullptr, *cval_s = nullptr, *cmax = nullptr, *sval = nullptr, *sval_s = nullptr;
+    uint32_t *cval = nullptr, *cval_s = nullptr, *cmax = nullptr;
+    uint64_t *sval = nullptr, *sval_s = nullptr;
     uint32_t *counts = nullptr;  // [0] candidates, [1] successes
     uint32_t *cblk = nullptr;
     void *tmp = nullptr;
@@ -466,8 +530,9 @@ size_t ss_tmp_need(gns_ss *ss, uint64_t n) {
     (void)rocprim::inclusive_scan_by_key(nullptr, b, kit, ss->cval_s, ss->cmax, (size_t)n,
                                          rocprim::maximum<uint32_t>(), rocprim::equal_to<uint64_t>(),
                                          ss->stream);
-    (void)c;
-    return std::max(a, b) + 256;
+    (void)rocprim::radix_sort_pairs(nullptr, c, ss->skey, ss->skey_s, ss->sval, ss->sval_s, (size_t)n, 0u,
+                                    std::min(64u, bits), ss->stream);
+    return std::max(std::max(a, b), c) + 256;
 }
 
 template <int KIND, int MF, int MM>
@@ -529,7 +594,8 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
             if (rocprim::inclusive_scan_by_key(ss->tmp, tb, kit, ss->cval, ss->cmax, (size_t)nc,
                                                rocprim::maximum<uint32_t>(), rocprim::equal_to<uint64_t>(),
                                                s) != hipSuccess) { set_error("segmented max failed"); return GNS_E_HIP; }
-            SsSuccArgs a{ss->ckey, ss->cval, ss->cmax, nc, ss->regs, ss->g.m, ss->skey, ss->sval, ss->counts + 1};
+            SsSuccArgs a{ss->ckey, ss->cval, ss->cmax, nc, ss->regs, ss->g.m, ss->skey, ss->sval, ss->counts + 1,
+                         ss->flowid};
             hipLaunchKernelGGL(k_ss_success, dim3((nc + 255) / 256), dim3(256), 0, s, a);
             GNS_HIP(hipGetLastError());
         }
@@ -543,9 +609,12 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
             size_t tb = ss->tmp_bytes;
             if (rocprim::radix_sort_pairs(ss->tmp, tb, ss->skey, ss->skey_s, ss->sval, ss->sval_s, (size_t)ns, 0u,
                                           bits2, s) != hipSuccess) { set_error("encode sort failed"); return GNS_E_HIP; }
-            SsApplyArgs a{ss->skey_s, ss->sval_s, ns, ss->g, ss->pkt, ss->flowid, ss->regs, ss->pbits,
-                          ss->values, ss->keys};
-            hipLaunchKernelGGL(k_ss_apply, dim3((ns + 255) / 256), dim3(256), 0, s, a);
+            // the sort's sources are free now: pbits-before and repeat counts go there
+            SsApplyArgs a{ss->skey_s, ss->sval_s, ns, ss->g, ss->pkt, ss->regs, ss->pbits, ss->values, ss->keys,
+                          reinterpret_cast<double *>(ss->skey), reinterpret_cast<int64_t *>(ss->sval)};
+            hipLaunchKernelGGL(k_ss_walk_pbits, dim3((ns + 255) / 256), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(k_ss_sample, dim3((ns + 255) / 256), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(k_ss_walk_mv, dim3((ns + 255) / 256), dim3(256), 0, s, a);
             GNS_HIP(hipGetLastError());
         }
     }
