@@ -292,7 +292,20 @@ struct SsApplyArgs {
     uint32_t *values, *keys;
     double *tp;    // [n] pbits before each encode (S5a -> S5b); then log(1 - first MV draw) (S5b -> S5c)
     int64_t *rep;  // [n] MV repeat count, 0 = not sampled (S5b -> S5c)
+    const uint32_t *heads;  // segment starts, [nh] count at heads[cells]
+    uint32_t cells;
 };
+
+// S5 segment starts (one per touched cell; order is irrelevant: cells are
+// independent), so the per-cell walks run on fully populated waves instead of
+// one sparse lane per 64 encodes.
+__global__ __launch_bounds__(256) void k_ss_heads(const uint64_t *skey, uint32_t n, uint32_t *heads,
+                                                  uint32_t cells) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    if (k == 0 || (skey[k - 1] >> kSsPktBits) != (skey[k] >> kSsPktBits))
+        heads[atomicAdd(&heads[cells], 1u)] = k;
+}
 
 #pragma clang fp contract(off)
 __global__ __launch_bounds__(256) void k_ss_walk_pbits(SsApplyArgs a) {
@@ -300,10 +313,10 @@ __global__ __launch_bounds__(256) void k_ss_walk_pbits(SsApplyArgs a) {
     const double mD = (double)a.g.m;
     s_t[threadIdx.x] = go_pow_int(a.g.base, (double)threadIdx.x) / mD;
     __syncthreads();
-    const uint32_t k0 = blockIdx.x * 256 + threadIdx.x;
-    if (k0 >= a.n) return;
+    const uint32_t hi = blockIdx.x * 256 + threadIdx.x;
+    if (hi >= a.heads[a.cells]) return;
+    const uint32_t k0 = a.heads[hi];
     const uint64_t cell = a.skey[k0] >> kSsPktBits;
-    if (k0 > 0 && (a.skey[k0 - 1] >> kSsPktBits) == cell) return;  // not a segment head
     double pb = a.pbits[cell];
     uint64_t vc = a.sval[k0];
     for (uint32_t k = k0;;) {
@@ -344,10 +357,10 @@ __global__ __launch_bounds__(256) void k_ss_sample(SsApplyArgs a) {
 }
 
 __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
-    const uint32_t k0 = blockIdx.x * 256 + threadIdx.x;
-    if (k0 >= a.n) return;
+    const uint32_t hi = blockIdx.x * 256 + threadIdx.x;
+    if (hi >= a.heads[a.cells]) return;
+    const uint32_t k0 = a.heads[hi];
     const uint64_t cell = a.skey[k0] >> kSsPktBits;
-    if (k0 > 0 && (a.skey[k0 - 1] >> kSsPktBits) == cell) return;  // not a segment head
     const uint32_t row = (uint32_t)(cell / a.g.w);
     uint32_t val = a.values[cell], key = a.keys[cell];
     // b^-val and log1m(b^-val) depend only on val: kept for the next foreign
@@ -479,6 +492,7 @@ struct gns_ss {
     uint32_t *cval = nullptr, *cval_s = nullptr, *cmax = nullptr;
     uint64_t *sval = nullptr, *sval_s = nullptr;
     uint32_t *counts = nullptr;  // [0] candidates, [1] successes
+    uint32_t *heads = nullptr;   // [cells + 1]: S5 segment starts (unordered), then their count
     uint32_t *cblk = nullptr;
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
@@ -501,7 +515,7 @@ void ss_free_all(gns_ss *ss) {
     dfree(ss->flowid); dfree(ss->pend[0]); dfree(ss->pend[1]); dfree(ss->pcnt[0]); dfree(ss->pcnt[1]);
     dfree(ss->ptotal); dfree(ss->ckey); dfree(ss->ckey_s); dfree(ss->skey); dfree(ss->skey_s);
     dfree(ss->cval); dfree(ss->cval_s); dfree(ss->cmax); dfree(ss->sval); dfree(ss->sval_s);
-    dfree(ss->counts); dfree(ss->cblk); dfree(ss->tmp); dfree(ss->stats); dfree(ss->stage);
+    dfree(ss->counts); dfree(ss->heads); dfree(ss->cblk); dfree(ss->tmp); dfree(ss->stats); dfree(ss->stage);
     if (ss->h_pin) (void)hipHostFree(ss->h_pin);
     ss->timer.destroy();
     if (ss->stream) (void)hipStreamDestroy(ss->stream);
@@ -610,11 +624,15 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
             if (rocprim::radix_sort_pairs(ss->tmp, tb, ss->skey, ss->skey_s, ss->sval, ss->sval_s, (size_t)ns, 0u,
                                           bits2, s) != hipSuccess) { set_error("encode sort failed"); return GNS_E_HIP; }
             // the sort's sources are free now: pbits-before and repeat counts go there
+            const uint32_t cells = ss->g.d * ss->g.w;
             SsApplyArgs a{ss->skey_s, ss->sval_s, ns, ss->g, ss->pkt, ss->regs, ss->pbits, ss->values, ss->keys,
-                          reinterpret_cast<double *>(ss->skey), reinterpret_cast<int64_t *>(ss->sval)};
-            hipLaunchKernelGGL(k_ss_walk_pbits, dim3((ns + 255) / 256), dim3(256), 0, s, a);
+                          reinterpret_cast<double *>(ss->skey), reinterpret_cast<int64_t *>(ss->sval), ss->heads, cells};
+            const uint32_t hgrid = (std::min<uint32_t>(ns, cells) + 255) / 256;  // segments <= touched cells
+            GNS_HIP(hipMemsetAsync(ss->heads + cells, 0, 4, s));
+            hipLaunchKernelGGL(k_ss_heads, dim3((ns + 255) / 256), dim3(256), 0, s, ss->skey_s, ns, ss->heads, cells);
+            hipLaunchKernelGGL(k_ss_walk_pbits, dim3(hgrid), dim3(256), 0, s, a);
             hipLaunchKernelGGL(k_ss_sample, dim3((ns + 255) / 256), dim3(256), 0, s, a);
-            hipLaunchKernelGGL(k_ss_walk_mv, dim3((ns + 255) / 256), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(k_ss_walk_mv, dim3(hgrid), dim3(256), 0, s, a);
             GNS_HIP(hipGetLastError());
         }
     }
@@ -746,7 +764,8 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
         ss->timer.stream = ss->stream;
         const uint64_t cells = (uint64_t)g.d * g.w;
         if ((rc = dalloc_t(&ss->regs, cells * g.m)) || (rc = dalloc_t(&ss->pbits, cells)) ||
-            (rc = dalloc_t(&ss->values, cells)) || (rc = dalloc_t(&ss->keys, cells)))
+            (rc = dalloc_t(&ss->values, cells)) || (rc = dalloc_t(&ss->keys, cells)) ||
+            (rc = dalloc_t(&ss->heads, cells + 1)))
             break;
         uint64_t slots = 1;
         const uint64_t mf = 4ull << 20;
