@@ -18,6 +18,7 @@
 //     sequential per cell: the successful encodes (at most maxValue per
 //     register per batch, sparse) are sorted by (cell, packet) and every cell
 //     is walked in stream order by one lane.
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -33,6 +34,7 @@ constexpr int kSsNW = 20;             // merged key words (flow ‖ elem <= 74 b
 constexpr uint32_t kSsPktBits = 27;   // packet index bits in the sort keys (batch <= 2^27)
 constexpr int kSsThreads = 256;
 constexpr uint32_t kSsChunk = 16384;
+constexpr uint32_t kSsIdChunk = 1024;  // S3b encodes per workgroup (4 per lane: many short-lived waves)
 
 struct SsGeom {
     uint32_t d, w, wmask, pow2, m, maxv, Kf, Km;
@@ -50,17 +52,12 @@ struct SsExtractArgs {
     uint64_t n;
     KeyPlanN kpf, kpm;
     SsGeom g;
-    DictDev D;
-    uint32_t epoch;
     const uint8_t *regs;
-    uint32_t *flowid;
-    uint64_t *pend;
-    uint32_t *pend_cnt, *pend_total;
     uint64_t *ckey;     // candidates: (cell*m + reg) << 27 | packet, block regions of chunk*d
     uint32_t *cval;     // lz
     uint32_t *ccount;   // total candidates
     uint32_t *cblk;     // [2*nblk]: per-block count, per-block output base
-    unsigned long long *stats;  // 0 inserted, 1 dropped, 2 unsupported, 3 dict full, 4 cand overflow, 5 encodes
+    unsigned long long *stats;  // 0 inserted, 1 dropped, 2 unsupported, 3 dict full, 4 candidates, 5 encodes
 };
 
 // one wave-aggregated atomic for every lane that wants a slot (call convergently)
@@ -118,10 +115,10 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
     const uint32_t mmask = a.g.m - 1u;
     const bool mpow2 = (a.g.m & mmask) == 0;
     __shared__ uint8_t s_srcf[80], s_srcm[80];
-    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_cc;
+    __shared__ uint32_t s_drop, s_unsup, s_ok, s_cc;
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
     for (uint32_t j = tid; j < 80; j += kSsThreads) { s_srcf[j] = a.kpf.src[j]; s_srcm[j] = a.kpm.src[j]; }
-    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; s_cc = 0; }
+    if (tid == 0) { s_drop = 0; s_unsup = 0; s_ok = 0; s_cc = 0; }
     __syncthreads();
     const uint64_t beg = (uint64_t)blk * kSsChunk;
     const uint64_t end = min(a.n, beg + kSsChunk);
@@ -132,28 +129,12 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
         uint32_t kwf[GNS_KWMAX], kwm[kSsNW];
         const int st = ss_keys<KIND, MF, MM, KF, KM>(a, s_srcf, s_srcm, p, kwf, kwm);
         if (st != PARSE_OK) {
-            a.flowid[p] = GNS_ID_NONE;
             atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
             continue;
         }
         uint32_t mkf[GNS_KWMAX], mkm[kSsNW];
         mm3_premix<GNS_KWMAX>(kwf, Kf, mkf);
         mm3_premix<kSsNW>(kwm, Km, mkm);
-        uint32_t out;
-        const int r = dict_find_or_claim(a.D, kwf, mm3_chain<GNS_KWMAX>(mkf, Kf, a.D.seed) & a.D.mask,
-                                         a.epoch, &out);
-        if (r == DICT_FULL) {
-            a.flowid[p] = GNS_ID_NONE;
-            atomicAdd(&s_full, 1u);
-            continue;
-        }
-        if (r == DICT_FOUND) {
-            a.flowid[p] = out;
-        } else {
-            a.flowid[p] = GNS_ID_NONE;
-            const uint32_t q = atomicAdd(&s_pend, 1u);
-            a.pend[beg + q] = (uint64_t)(p - beg) << 32 | out;
-        }
         n_ok++;
         for (uint32_t rr = 0; rr < a.g.d; rr++) {
             const uint32_t j = ss_row_index(a.g, mm3_chain<GNS_KWMAX>(mkf, Kf, a.g.seeds[rr]));
@@ -177,53 +158,183 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
     atomicAdd(&s_ok, n_ok);
     __syncthreads();
     if (tid == 0) {
-        a.pend_cnt[blk] = s_pend;
         a.cblk[blk] = s_cc;
         a.cblk[gridDim.x + blk] = s_cc ? atomicAdd(a.ccount, s_cc) : 0u;
         if (s_cc) atomicAdd(&a.stats[4], (unsigned long long)s_cc);
-        if (s_pend) atomicAdd(a.pend_total, s_pend);
         if (s_ok) atomicAdd(&a.stats[0], (unsigned long long)s_ok);
         if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
         if (s_unsup) atomicAdd(&a.stats[2], (unsigned long long)s_unsup);
-        if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
     }
 }
 
-struct SsResolveArgs {
-    SsExtractArgs x;
+// S1 for header records with compile-time key widths and depth (the default
+// task: SrcIP / SrcIP|DstIP, d=2): the same per-packet work as k_ss_extract,
+// as a two-stage software pipeline.  Iteration k parses packet k+1, hashes
+// its keys and issues its d batch-entry register reads (and prefetches the
+// record of packet k+2), then emits the candidates of packet k, whose register
+// reads were issued one iteration earlier.  Results are identical: candidates
+// carry (segment, packet) and are radix-sorted afterwards, so their order in
+// the block region does not matter.
+#ifndef GNS_SS_MINW
+#define GNS_SS_MINW 4
+#endif
+template <int MF, int MM, int KF, int KM, int DD>
+__global__ __launch_bounds__(kSsThreads, GNS_SS_MINW) void k_ss_extract_hdr(SsExtractArgs a) {
+    const uint32_t mmask = a.g.m - 1u;
+    const bool mpow2 = (a.g.m & mmask) == 0;
+    __shared__ uint8_t s_srcf[80], s_srcm[80];
+    __shared__ uint32_t s_drop, s_unsup, s_ok, s_cc;
+    const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    for (uint32_t j = tid; j < 80; j += kSsThreads) { s_srcf[j] = a.kpf.src[j]; s_srcm[j] = a.kpm.src[j]; }
+    if (tid == 0) { s_drop = 0; s_unsup = 0; s_ok = 0; s_cc = 0; }
+    __syncthreads();
+    const uint64_t beg = (uint64_t)blk * kSsChunk;
+    const uint64_t end = min(a.n, beg + kSsChunk);
+    uint64_t *rkey = a.ckey + beg * a.g.d;
+    uint32_t *rval = a.cval + beg * a.g.d;
+    uint32_t n_ok = 0;
+    uint4 hv[4];
+    uint32_t hsz;
+    auto load_hdr = [&](uint64_t q) {
+        const uint64_t pc = min(q, end - 1);
+        const uint4 *r = reinterpret_cast<const uint4 *>(a.in.hdr + pc * 16);
+#pragma unroll
+        for (int i = 0; i < 4; i++) hv[i] = r[i];
+        hsz = a.in.sizes[pc];
+    };
+    // stage B of packet q: parse, keys, row cells, register reads
+    auto stage_b = [&](uint64_t q, bool &okq, uint64_t (&segq)[DD], uint32_t (&lzq)[DD], uint32_t (&regq)[DD]) {
+        okq = q < end;
+        uint32_t cw[16];
+#pragma unroll
+        for (int i = 0; i < 4; i++) { cw[4 * i] = hv[i].x; cw[4 * i + 1] = hv[i].y; cw[4 * i + 2] = hv[i].z; cw[4 * i + 3] = hv[i].w; }
+        const uint32_t szq = hsz;
+        load_hdr(q + kSsThreads);
+        uint32_t kwf[GNS_KWMAX], kwm[kSsNW];
+#pragma unroll
+        for (int i = 0; i < GNS_KWMAX; i++) kwf[i] = 0;
+#pragma unroll
+        for (int i = 0; i < kSsNW; i++) kwm[i] = 0;
+        if (okq) {
+            uint32_t tw[10];
+            const int st = parse_record_fast(cw, szq, true, tw);
+            if (st == PARSE_OK) {
+                make_key_m<MF, GNS_KWMAX>(KF, s_srcf, tw, kwf);
+                make_key_m<MM, kSsNW>(KM, s_srcm, tw, kwm);
+            } else {
+                atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
+                okq = false;
+            }
+        }
+        uint32_t mkf[GNS_KWMAX], mkm[kSsNW];
+        mm3_premix<GNS_KWMAX>(kwf, KF, mkf);
+        mm3_premix<kSsNW>(kwm, KM, mkm);
+#pragma unroll
+        for (int rr = 0; rr < DD; rr++) {
+            const uint32_t j = ss_row_index(a.g, mm3_chain<GNS_KWMAX>(mkf, KF, a.g.seeds[rr]));
+            const uint64_t cell = (uint64_t)rr * a.g.w + j;
+            uint32_t s0, s1;
+            ss_hll_seeds(a.g.hll_master, cell, s0, s1);
+            const uint32_t h0 = mm3_chain<kSsNW>(mkm, KM, s0);  // geometricHash :66-70
+            uint32_t lz = (h0 ? (uint32_t)__clz(h0) : 32u) + 1u;
+            lzq[rr] = lz > a.g.maxv ? a.g.maxv : lz;
+            const uint32_t h1 = mm3_chain<kSsNW>(mkm, KM, s1);
+            const uint32_t idx = mpow2 ? (h1 & mmask) : h1 % a.g.m;  // :87-88
+            segq[rr] = cell * a.g.m + idx;
+            regq[rr] = okq ? (uint32_t)a.regs[segq[rr]] : 0xFFu;
+        }
+    };
+    load_hdr(beg + tid);
+    bool okc;
+    uint32_t lzc[DD], regc[DD];
+    uint64_t segc[DD];
+    stage_b(beg + tid, okc, segc, lzc, regc);
+    for (uint64_t p0 = beg; p0 < end; p0 += kSsThreads) {  // wave-uniform trip count
+        bool okn = false;
+        uint32_t lzn[DD], regn[DD];
+        uint64_t segn[DD];
+        if (p0 + kSsThreads < end) stage_b(p0 + kSsThreads + tid, okn, segn, lzn, regn);
+        const uint64_t p = p0 + tid;
+        if (okc) n_ok++;
+#pragma unroll
+        for (int rr = 0; rr < DD; rr++) {
+            const bool want = okc && lzc[rr] > regc[rr];  // can encode only if above the batch-entry register
+            const uint32_t q = wave_alloc(&s_cc, want);
+            if (want) {
+                rkey[q] = segc[rr] << kSsPktBits | (p & ((1ull << kSsPktBits) - 1));
+                rval[q] = lzc[rr];
+            }
+        }
+        okc = okn;
+#pragma unroll
+        for (int rr = 0; rr < DD; rr++) { segc[rr] = segn[rr]; lzc[rr] = lzn[rr]; regc[rr] = regn[rr]; }
+    }
+    atomicAdd(&s_ok, n_ok);
+    __syncthreads();
+    if (tid == 0) {
+        a.cblk[blk] = s_cc;
+        a.cblk[gridDim.x + blk] = s_cc ? atomicAdd(a.ccount, s_cc) : 0u;
+        if (s_cc) atomicAdd(&a.stats[4], (unsigned long long)s_cc);
+        if (s_ok) atomicAdd(&a.stats[0], (unsigned long long)s_ok);
+        if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
+        if (s_unsup) atomicAdd(&a.stats[2], (unsigned long long)s_unsup);
+    }
+}
+
+// S3b: flow ids for the successful encodes only (the MV loop's owner test and
+// the cell keys are the only consumers of flow identity, and only encodes
+// reach them).  Encode q's packet index is in skey[q]; its flow key is
+// re-derived from the input, looked up / claimed in the dictionary and the id
+// stored in sval[q]'s high word.  FIRST: encodes [blk*kSsIdChunk, +kSsIdChunk), probing
+// from the key's hash slot; otherwise the block's parked encodes
+// ((q - beg) << 32 | slot to resume at), from the previous launch.
+struct SsIdsArgs {
+    InputDesc in;
+    KeyPlanN kpf, kpm;
+    SsGeom g;
+    DictDev D;
+    uint32_t epoch, ns;
+    const uint64_t *skey;
+    uint64_t *sval;
     const uint64_t *pend_in;
     const uint32_t *cnt_in;
     uint64_t *pend_out;
     uint32_t *cnt_out, *total_out;
+    unsigned long long *stats;
 };
 
-template <int KIND, int MF, int MM>
-__global__ __launch_bounds__(kSsThreads) void k_ss_resolve(SsResolveArgs r) {
+template <int KIND, int MF, int MM, bool FIRST>
+__global__ __launch_bounds__(kSsThreads) void k_ss_ids(SsIdsArgs r) {
     __shared__ uint8_t s_srcf[80], s_srcm[80];
     __shared__ uint32_t s_cnt, s_full;
-    const SsExtractArgs &a = r.x;
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
-    for (uint32_t j = tid; j < 80; j += kSsThreads) { s_srcf[j] = a.kpf.src[j]; s_srcm[j] = a.kpm.src[j]; }
+    for (uint32_t j = tid; j < 80; j += kSsThreads) { s_srcf[j] = r.kpf.src[j]; s_srcm[j] = r.kpm.src[j]; }
     if (tid == 0) { s_cnt = 0; s_full = 0; }
     __syncthreads();
-    const uint32_t cnt = r.cnt_in[blk];
-    const uint64_t beg = (uint64_t)blk * kSsChunk;
+    const uint64_t beg = (uint64_t)blk * kSsIdChunk;
+    const uint32_t cnt = FIRST ? (uint32_t)min<uint64_t>(kSsIdChunk, r.ns - beg) : r.cnt_in[blk];
+    SsExtractArgs a{};
+    a.in = r.in; a.kpf = r.kpf; a.kpm = r.kpm; a.g = r.g;
     for (uint32_t i = tid; i < cnt; i += kSsThreads) {
-        const uint64_t v = r.pend_in[beg + i];
-        const uint64_t p = beg + (v >> 32);
+        uint64_t q;
+        uint32_t slot = 0;
+        if (FIRST) q = beg + i;
+        else { const uint64_t v = r.pend_in[beg + i]; q = beg + (v >> 32); slot = (uint32_t)v; }
+        const uint64_t p = r.skey[q] & ((1ull << kSsPktBits) - 1);
         uint32_t kwf[GNS_KWMAX], kwm[kSsNW];
-        (void)ss_keys<KIND, MF, MM>(a, s_srcf, s_srcm, p, kwf, kwm);
+        (void)ss_keys<KIND, MF, MM>(a, s_srcf, s_srcm, p, kwf, kwm);  // parsed OK in S1
+        if (FIRST) slot = mm3_n<GNS_KWMAX>(kwf, r.g.Kf, r.D.seed) & r.D.mask;
         uint32_t out;
-        const int res = dict_find_or_claim(a.D, kwf, (uint32_t)v, a.epoch, &out);
-        if (res == DICT_FOUND) a.flowid[p] = out;
-        else if (res == DICT_PENDING) r.pend_out[beg + atomicAdd(&s_cnt, 1u)] = (v & 0xFFFFFFFF00000000ull) | out;
+        const int res = dict_find_or_claim(r.D, kwf, slot, r.epoch, &out);
+        if (res == DICT_FOUND) r.sval[q] = (uint64_t)out << 32 | (r.sval[q] & 0xFFFFFFFFull);
+        else if (res == DICT_PENDING) r.pend_out[beg + atomicAdd(&s_cnt, 1u)] = (q - beg) << 32 | out;
         else atomicAdd(&s_full, 1u);
     }
     __syncthreads();
     if (tid == 0) {
         r.cnt_out[blk] = s_cnt;
         if (s_cnt) atomicAdd(r.total_out, s_cnt);
-        if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+        if (s_full) atomicAdd(&r.stats[3], (unsigned long long)s_full);
     }
 }
 
@@ -249,10 +360,9 @@ struct SsSuccArgs {
     const uint8_t *regs;
     uint32_t m;
     uint64_t *skey;  // (cell << 27) | packet
-    uint64_t *sval;  // flow id << 32 | reg | lz << 8 | old << 16 (the id rides along the sort,
-                     // so S5's sequential walk has no dependent flowid[] load)
+    uint64_t *sval;  // flow id << 32 | reg | lz << 8 | old << 16 (the id, filled in by S3b, rides
+                     // along the sort, so S5's sequential walk has no dependent id load)
     uint32_t *scount;
-    const uint32_t *flowid;
 };
 
 __global__ __launch_bounds__(256) void k_ss_success(SsSuccArgs a) {
@@ -269,7 +379,7 @@ __global__ __launch_bounds__(256) void k_ss_success(SsSuccArgs a) {
         const uint32_t reg = (uint32_t)(seg % a.m);
         const uint32_t p = (uint32_t)(key & ((1ull << kSsPktBits) - 1));
         a.skey[q] = cell << kSsPktBits | p;
-        a.sval[q] = (uint64_t)a.flowid[p] << 32 | (reg | lz << 8 | old << 16);
+        a.sval[q] = (uint64_t)GNS_ID_NONE << 32 | (reg | lz << 8 | old << 16);
     }
 }
 
@@ -480,11 +590,11 @@ struct gns_ss {
     uint64_t dict_slots = 0;
     uint32_t epoch = 0;
     uint64_t pkt = 0;     // records inserted since create (RNG packet index)
+    bool s1_pipe = true;
+    bool s1_nodict = false;  // pipelined S1 for header records (GNS_SS_PIPE=0: the plain loop)
     uint64_t n_encodes = 0, n_batches = 0;
     uint64_t bmax = 0;
     uint32_t nblk_max = 0;
-    uint32_t *flowid = nullptr;
-    uint64_t *pend[2] = {nullptr, nullptr};
     uint32_t *pcnt[2] = {nullptr, nullptr};
     uint32_t *ptotal = nullptr;
     uint64_t ccap = 0;
@@ -512,7 +622,7 @@ int ss_set_dev(gns_ss *ss) {
 
 void ss_free_all(gns_ss *ss) {
     dfree(ss->regs); dfree(ss->pbits); dfree(ss->values); dfree(ss->keys); dfree(ss->D.rec);
-    dfree(ss->flowid); dfree(ss->pend[0]); dfree(ss->pend[1]); dfree(ss->pcnt[0]); dfree(ss->pcnt[1]);
+    dfree(ss->pcnt[0]); dfree(ss->pcnt[1]);
     dfree(ss->ptotal); dfree(ss->ckey); dfree(ss->ckey_s); dfree(ss->skey); dfree(ss->skey_s);
     dfree(ss->cval); dfree(ss->cval_s); dfree(ss->cmax); dfree(ss->sval); dfree(ss->sval_s);
     dfree(ss->counts); dfree(ss->heads); dfree(ss->cblk); dfree(ss->tmp); dfree(ss->stats); dfree(ss->stage);
@@ -549,6 +659,45 @@ size_t ss_tmp_need(gns_ss *ss, uint64_t n) {
     return std::max(std::max(a, b), c) + 256;
 }
 
+// S3b driver: flow ids of the ns encodes (sval high words), with the
+// first-sight resolve rounds (a key claimed in this launch parks its other
+// encodes until the claim is committed).  The candidate buffers are free
+// after S3: ckey / ckey_s hold the parked lists.  Runs before any state is
+// written, so a full dictionary leaves the sketch unchanged.
+template <int KIND, int MF, int MM>
+int ss_encode_ids(gns_ss *ss, const InputDesc &in, uint32_t ns) {
+    hipStream_t s = ss->stream;
+    const uint32_t nb = (ns + kSsIdChunk - 1) / kSsIdChunk;
+    uint64_t *pend[2] = {ss->ckey, ss->ckey_s};
+    SsIdsArgs r{};
+    r.in = in; r.kpf = ss->kpf; r.kpm = ss->kpm; r.g = ss->g; r.D = ss->D; r.ns = ns;
+    r.skey = ss->skey; r.sval = ss->sval; r.stats = ss->stats;
+    ScopedStage st(ss->timer, 1);
+    GNS_HIP(hipMemsetAsync(ss->ptotal, 0, 8, s));
+    int cur = 0;
+    for (int round = 0;; round++) {
+        if (++ss->epoch == 0) ss->epoch = 1;
+        r.epoch = ss->epoch;
+        r.pend_in = pend[cur]; r.cnt_in = ss->pcnt[cur];
+        r.pend_out = pend[cur ^ 1]; r.cnt_out = ss->pcnt[cur ^ 1]; r.total_out = ss->ptotal + (cur ^ 1);
+        if (round == 0) {
+            r.pend_out = pend[0]; r.cnt_out = ss->pcnt[0]; r.total_out = ss->ptotal;
+            hipLaunchKernelGGL((k_ss_ids<KIND, MF, MM, true>), dim3(nb), dim3(kSsThreads), 0, s, r);
+        } else {
+            hipLaunchKernelGGL((k_ss_ids<KIND, MF, MM, false>), dim3(nb), dim3(kSsThreads), 0, s, r);
+            cur ^= 1;
+        }
+        GNS_HIP(hipGetLastError());
+        GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
+        GNS_HIP(hipMemcpyAsync(ss->h_pin + 2, ss->stats + 3, 8, hipMemcpyDeviceToHost, s));
+        GNS_HIP(hipStreamSynchronize(s));
+        if (ss->h_pin[2] | ss->h_pin[3]) { set_error("flow dictionary full; raise max flows"); return GNS_E_FULL; }
+        if (ss->h_pin[0] == 0) return GNS_OK;
+        if (round > 64) { set_error("dictionary resolve did not converge"); return GNS_E_FULL; }
+        GNS_HIP(hipMemsetAsync(ss->ptotal + (cur ^ 1), 0, 4, s));
+    }
+}
+
 template <int KIND, int MF, int MM>
 int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     if (n == 0) return GNS_OK;
@@ -560,35 +709,23 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     if (++ss->epoch == 0) ss->epoch = 1;
     SsExtractArgs x{};
     x.in = in; x.n = n; x.kpf = ss->kpf; x.kpm = ss->kpm;
-    x.g = ss->g; x.D = ss->D; x.epoch = ss->epoch; x.regs = ss->regs; x.flowid = ss->flowid;
-    x.pend = ss->pend[0]; x.pend_cnt = ss->pcnt[0]; x.pend_total = ss->ptotal;
+    x.g = ss->g; x.regs = ss->regs;
     x.ckey = ss->ckey; x.cval = ss->cval; x.ccount = ss->counts; x.cblk = ss->cblk; x.stats = ss->stats;
     {
         ScopedStage st(ss->timer, 0);
-        if (ss->g.Kf == 16 && ss->g.Km == 32)
+        bool piped = false;
+        if constexpr (KIND == IN_HDR && MF == PLAN_SLICE0 && MM == PLAN_SLICE0) {
+            if (ss->s1_pipe && ss->g.Kf == 16 && ss->g.Km == 32 && ss->g.d == 2) {
+                hipLaunchKernelGGL((k_ss_extract_hdr<MF, MM, 16, 32, 2>), dim3(nblk), dim3(kSsThreads), 0, s, x);
+                piped = true;
+            }
+        }
+        if (piped) {
+        } else if (ss->g.Kf == 16 && ss->g.Km == 32)
             hipLaunchKernelGGL((k_ss_extract<KIND, MF, MM, 16, 32>), dim3(nblk), dim3(kSsThreads), 0, s, x);
         else
             hipLaunchKernelGGL((k_ss_extract<KIND, MF, MM, 0, 0>), dim3(nblk), dim3(kSsThreads), 0, s, x);
         GNS_HIP(hipGetLastError());
-    }
-    int cur = 0;
-    for (int round = 0;; round++) {
-        GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
-        GNS_HIP(hipMemcpyAsync(ss->h_pin + 2, ss->stats + 3, 16, hipMemcpyDeviceToHost, s));
-        GNS_HIP(hipStreamSynchronize(s));
-        if (ss->h_pin[2] | ss->h_pin[3]) { set_error("flow dictionary full; raise max flows"); return GNS_E_FULL; }
-        if (ss->h_pin[0] == 0) break;
-        if (round > 64) { set_error("dictionary resolve did not converge"); return GNS_E_FULL; }
-        GNS_HIP(hipMemsetAsync(ss->ptotal + (cur ^ 1), 0, 4, s));
-        if (++ss->epoch == 0) ss->epoch = 1;
-        SsResolveArgs r{};
-        r.x = x; r.x.epoch = ss->epoch;
-        r.pend_in = ss->pend[cur]; r.cnt_in = ss->pcnt[cur];
-        r.pend_out = ss->pend[cur ^ 1]; r.cnt_out = ss->pcnt[cur ^ 1]; r.total_out = ss->ptotal + (cur ^ 1);
-        ScopedStage st(ss->timer, 1);
-        hipLaunchKernelGGL((k_ss_resolve<KIND, MF, MM>), dim3(nblk), dim3(kSsThreads), 0, s, r);
-        GNS_HIP(hipGetLastError());
-        cur ^= 1;
     }
     GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->counts, 4, hipMemcpyDeviceToHost, s));
     GNS_HIP(hipStreamSynchronize(s));
@@ -608,14 +745,14 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
             if (rocprim::inclusive_scan_by_key(ss->tmp, tb, kit, ss->cval, ss->cmax, (size_t)nc,
                                                rocprim::maximum<uint32_t>(), rocprim::equal_to<uint64_t>(),
                                                s) != hipSuccess) { set_error("segmented max failed"); return GNS_E_HIP; }
-            SsSuccArgs a{ss->ckey, ss->cval, ss->cmax, nc, ss->regs, ss->g.m, ss->skey, ss->sval, ss->counts + 1,
-                         ss->flowid};
+            SsSuccArgs a{ss->ckey, ss->cval, ss->cmax, nc, ss->regs, ss->g.m, ss->skey, ss->sval, ss->counts + 1};
             hipLaunchKernelGGL(k_ss_success, dim3((nc + 255) / 256), dim3(256), 0, s, a);
             GNS_HIP(hipGetLastError());
         }
         GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->counts + 1, 4, hipMemcpyDeviceToHost, s));
         GNS_HIP(hipStreamSynchronize(s));
         const uint32_t ns = ss->h_pin[0];
+        if (ns > 0) GNS_TRY((ss_encode_ids<KIND, MF, MM>(ss, in, ns)));
         ss->n_encodes += ns;
         if (ns > 0) {
             ScopedStage st(ss->timer, 3);
@@ -775,14 +912,18 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
         ss->D.K = g.Kf;
         ss->D.RW = dict_record_words(g.Kf);
         ss->D.seed = 0x2545F491u;
+        {
+            const char *env = getenv("GNS_SS_PIPE");
+            ss->s1_pipe = !(env && env[0] == '0');
+        }
         if ((rc = dalloc_t(&ss->D.rec, slots * ss->D.RW)) != GNS_OK) break;
         ss->bmax = p->batch_packets ? p->batch_packets : (8ull << 20);
         ss->bmax = std::min<uint64_t>(((ss->bmax + kSsChunk - 1) / kSsChunk) * kSsChunk, 1ull << kSsPktBits);
         ss->nblk_max = (uint32_t)(ss->bmax / kSsChunk);
         ss->ccap = ss->bmax * g.d;
-        if ((rc = dalloc_t(&ss->flowid, ss->bmax)) || (rc = dalloc_t(&ss->pend[0], ss->bmax)) ||
-            (rc = dalloc_t(&ss->pend[1], ss->bmax)) || (rc = dalloc_t(&ss->pcnt[0], ss->nblk_max)) ||
-            (rc = dalloc_t(&ss->pcnt[1], ss->nblk_max)) || (rc = dalloc_t(&ss->ptotal, 2)) ||
+        const uint64_t nblk_enc = (ss->ccap + kSsIdChunk - 1) / kSsIdChunk;  // S3b blocks over encodes
+        if ((rc = dalloc_t(&ss->pcnt[0], nblk_enc)) ||
+            (rc = dalloc_t(&ss->pcnt[1], nblk_enc)) || (rc = dalloc_t(&ss->ptotal, 2)) ||
             (rc = dalloc_t(&ss->ckey, ss->ccap)) || (rc = dalloc_t(&ss->ckey_s, ss->ccap)) ||
             (rc = dalloc_t(&ss->skey, ss->ccap)) || (rc = dalloc_t(&ss->skey_s, ss->ccap)) ||
             (rc = dalloc_t(&ss->cval, ss->ccap)) || (rc = dalloc_t(&ss->cval_s, ss->ccap)) ||

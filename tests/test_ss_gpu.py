@@ -139,6 +139,36 @@ def test_tuples_and_headers_parity(gpu, oracle, ffields, efields):
     assert_same_ss(ss2, orc2)
 
 
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_default_task_headers_both_s1_forms(gpu, oracle, monkeypatch, pipe):
+    """Default task (SrcIP / DstIP, d=2) on 64-byte records with VLAN tags,
+    dropped ARP records and a ragged last block: the pipelined S1
+    (k_ss_extract_hdr, GNS_SS_PIPE=1) and the plain loop (GNS_SS_PIPE=0) both
+    give the oracle's state, in one batch and in ragged smaller batches."""
+    from go2netspectra_amd import SuperSpread
+    monkeypatch.setenv("GNS_SS_PIPE", pipe)
+    rng = np.random.default_rng(77)
+    t = random_tuples(rng, 70_001, 3000, v6_frac=0.0, s=1.1)
+    hdr = frames_from_tuples(t, rng, vlan_frac=0.3)
+    bad = rng.random(len(hdr)) < 0.03
+    hdr[bad, 12:14] = [0x08, 0x06]
+    seeds = np.array([0xA1, 0xB2], np.uint32)
+    kw = dict(flow_fields=["SrcIP"], elem_fields=["DstIP"], seeds=seeds, hll_master=HLL_MASTER, rng_seed=RNG_SEED)
+    orc = oracle.SuperSpread(1024, 2, 20, 128, 5, 0.5, 1.08, 16, 16, seeds, HLL_MASTER, RNG_SEED)
+    assert orc.insert_hdr64(hdr, t["length"], ["SrcIP"], ["DstIP"]) == int((~bad).sum())
+    for batch in (None, 5000):
+        ss = SuperSpread(1024, 2, 20, 128, 5, 0.5, 1.08, **kw)
+        if batch is None:
+            ss.insert_headers(hdr, t["length"])
+        else:
+            for i in range(0, len(hdr), batch):
+                ss.insert_headers(hdr[i:i + batch], t["length"][i:i + batch])
+        ss.flush()
+        st = ss.stats()
+        assert st["dropped"] == int(bad.sum()) and st["packets"] == len(hdr)
+        assert_same_ss(ss, orc)
+
+
 def test_golden_stream_fixture(gpu):
     """The committed oracle fixture (tests/golden/ss_stream.npz) through the engine."""
     from go2netspectra_amd import SuperSpread
