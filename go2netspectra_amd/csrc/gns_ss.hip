@@ -365,22 +365,42 @@ struct SsSuccArgs {
     uint32_t *scount;
 };
 
+// kSsSuccItems candidates per lane; one global atomic per workgroup reserves
+// the encodes' slots (S4 sorts them, so their order here does not matter).
+constexpr uint32_t kSsSuccItems = 8;
 __global__ __launch_bounds__(256) void k_ss_success(SsSuccArgs a) {
-    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= a.n) return;
-    const uint64_t key = a.ckey[k];
-    const uint64_t seg = key >> kSsPktBits;
-    const uint32_t lz = a.cval[k];
-    uint32_t old = a.regs[seg];
-    if (k > 0 && (a.ckey[k - 1] >> kSsPktBits) == seg) old = max(old, a.cmax[k - 1]);
-    if (lz > old) {
-        const uint32_t q = atomicAdd(a.scount, 1u);
-        const uint64_t cell = seg / a.m;
-        const uint32_t reg = (uint32_t)(seg % a.m);
-        const uint32_t p = (uint32_t)(key & ((1ull << kSsPktBits) - 1));
-        a.skey[q] = cell << kSsPktBits | p;
-        a.sval[q] = (uint64_t)GNS_ID_NONE << 32 | (reg | lz << 8 | old << 16);
+    __shared__ uint32_t s_n, s_base;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    const uint32_t k0 = blockIdx.x * 256 * kSsSuccItems + threadIdx.x;
+    uint64_t ok[kSsSuccItems], ov[kSsSuccItems];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kSsSuccItems; i++) {
+        const uint32_t k = k0 + i * 256;
+        ok[i] = ~0ull;
+        if (k >= a.n) continue;
+        const uint64_t key = a.ckey[k];
+        const uint64_t seg = key >> kSsPktBits;
+        const uint32_t lz = a.cval[k];
+        uint32_t old = a.regs[seg];
+        if (k > 0 && (a.ckey[k - 1] >> kSsPktBits) == seg) old = max(old, a.cmax[k - 1]);
+        if (lz > old) {
+            const uint64_t cell = seg / a.m;
+            const uint32_t reg = (uint32_t)(seg % a.m);
+            ok[i] = cell << kSsPktBits | (key & ((1ull << kSsPktBits) - 1));
+            ov[i] = (uint64_t)GNS_ID_NONE << 32 | (reg | lz << 8 | old << 16);
+            cnt++;
+        }
     }
+    const uint32_t off = cnt ? atomicAdd(&s_n, cnt) : 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_n ? atomicAdd(a.scount, s_n) : 0u;
+    __syncthreads();
+    uint32_t q = s_base + off;
+#pragma unroll
+    for (uint32_t i = 0; i < kSsSuccItems; i++)
+        if (ok[i] != ~0ull) { a.skey[q] = ok[i]; a.sval[q] = ov[i]; q++; }
 }
 
 // S5: every cell's encodes in stream order: register write, pbits (:105-109),
@@ -409,12 +429,32 @@ struct SsApplyArgs {
 // S5 segment starts (one per touched cell; order is irrelevant: cells are
 // independent), so the per-cell walks run on fully populated waves instead of
 // one sparse lane per 64 encodes.
+// Each workgroup covers kSsHeadItems encodes per lane; the heads it finds take
+// one global atomic per workgroup (a per-head atomic on the one counter
+// serialized 65K times per batch).
+constexpr uint32_t kSsHeadItems = 8;
 __global__ __launch_bounds__(256) void k_ss_heads(const uint64_t *skey, uint32_t n, uint32_t *heads,
                                                   uint32_t cells) {
-    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= n) return;
-    if (k == 0 || (skey[k - 1] >> kSsPktBits) != (skey[k] >> kSsPktBits))
-        heads[atomicAdd(&heads[cells], 1u)] = k;
+    __shared__ uint32_t s_n, s_base;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    const uint32_t k0 = blockIdx.x * 256 * kSsHeadItems + threadIdx.x;
+    bool hd[kSsHeadItems];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kSsHeadItems; i++) {
+        const uint32_t k = k0 + i * 256;
+        hd[i] = k < n && (k == 0 || (skey[k - 1] >> kSsPktBits) != (skey[k] >> kSsPktBits));
+        cnt += hd[i];
+    }
+    const uint32_t off = cnt ? atomicAdd(&s_n, cnt) : 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_n ? atomicAdd(&heads[cells], s_n) : 0u;
+    __syncthreads();
+    uint32_t q = s_base + off;
+#pragma unroll
+    for (uint32_t i = 0; i < kSsHeadItems; i++)
+        if (hd[i]) heads[q++] = k0 + i * 256;
 }
 
 #pragma clang fp contract(off)
@@ -746,7 +786,7 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
                                                rocprim::maximum<uint32_t>(), rocprim::equal_to<uint64_t>(),
                                                s) != hipSuccess) { set_error("segmented max failed"); return GNS_E_HIP; }
             SsSuccArgs a{ss->ckey, ss->cval, ss->cmax, nc, ss->regs, ss->g.m, ss->skey, ss->sval, ss->counts + 1};
-            hipLaunchKernelGGL(k_ss_success, dim3((nc + 255) / 256), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(k_ss_success, dim3((nc + 256 * kSsSuccItems - 1) / (256 * kSsSuccItems)), dim3(256), 0, s, a);
             GNS_HIP(hipGetLastError());
         }
         GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->counts + 1, 4, hipMemcpyDeviceToHost, s));
@@ -766,7 +806,8 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
                           reinterpret_cast<double *>(ss->skey), reinterpret_cast<int64_t *>(ss->sval), ss->heads, cells};
             const uint32_t hgrid = (std::min<uint32_t>(ns, cells) + 255) / 256;  // segments <= touched cells
             GNS_HIP(hipMemsetAsync(ss->heads + cells, 0, 4, s));
-            hipLaunchKernelGGL(k_ss_heads, dim3((ns + 255) / 256), dim3(256), 0, s, ss->skey_s, ns, ss->heads, cells);
+            hipLaunchKernelGGL(k_ss_heads, dim3((ns + 256 * kSsHeadItems - 1) / (256 * kSsHeadItems)), dim3(256), 0, s,
+                               ss->skey_s, ns, ss->heads, cells);
             hipLaunchKernelGGL(k_ss_walk_pbits, dim3(hgrid), dim3(256), 0, s, a);
             hipLaunchKernelGGL(k_ss_sample, dim3((ns + 255) / 256), dim3(256), 0, s, a);
             hipLaunchKernelGGL(k_ss_walk_mv, dim3(hgrid), dim3(256), 0, s, a);
