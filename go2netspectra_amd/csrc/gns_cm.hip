@@ -1932,6 +1932,8 @@ struct gns_cm {
     KeyPlanN kp{};
     uint32_t K = 0, st = 0, ct = 0;
     uint32_t *C = nullptr, *S = nullptr, *Fc = nullptr, *Fs = nullptr;
+    uint64_t *hh_cand = nullptr;  // heavy-hitter candidates (allocated at the first query, kept)
+    uint32_t *hh_n = nullptr;
     DictDev D{};
     uint64_t dict_slots = 0;
     uint32_t epoch = 0;
@@ -1981,7 +1983,7 @@ int set_dev(gns_cm *cm) {
 }
 
 int cm_free_all(gns_cm *cm) {
-    dfree(cm->C); dfree(cm->S); dfree(cm->Fc); dfree(cm->Fs);
+    dfree(cm->C); dfree(cm->S); dfree(cm->Fc); dfree(cm->Fs); dfree(cm->hh_cand); dfree(cm->hh_n);
     dfree(cm->D.rec);
     dfree(cm->keyid); dfree(cm->idx);
     dfree(cm->pend[0]); dfree(cm->pend[1]); dfree(cm->pcnt[0]); dfree(cm->pcnt[1]);
@@ -2467,12 +2469,14 @@ int gns_cm_export_state(gns_cm *cm, uint32_t *C, uint32_t *S, uint8_t *FPc, uint
 static int cm_heavy_one(gns_cm *cm, const uint32_t *val, const uint32_t *fp, uint32_t thr,
                         uint8_t *flows, uint32_t *vals, uint64_t *n_io) {
     const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
-    uint64_t *cand = nullptr;
-    uint32_t *ncand = nullptr;
     const uint32_t cap = (uint32_t)std::min<uint64_t>(cells, 1ull << 26);
-    GNS_TRY(dalloc(reinterpret_cast<void **>(&cand), (uint64_t)cap * 8));
-    int rc = dalloc(reinterpret_cast<void **>(&ncand), 16);
-    if (rc) { dfree(cand); return rc; }
+    if (!cm->hh_cand) {
+        GNS_TRY(dalloc(reinterpret_cast<void **>(&cm->hh_cand), (uint64_t)cap * 8));
+        GNS_TRY(dalloc(reinterpret_cast<void **>(&cm->hh_n), 16));
+    }
+    uint64_t *cand = cm->hh_cand;
+    uint32_t *ncand = cm->hh_n;
+    int rc = GNS_OK;
     std::vector<uint64_t> h;
     uint32_t nc = 0;
     hipError_t e = hipMemsetAsync(ncand, 0, 4, cm->stream);
@@ -2488,8 +2492,6 @@ static int cm_heavy_one(gns_cm *cm, const uint32_t *val, const uint32_t *fp, uin
         h.resize(nc);
         e = hipMemcpy(h.data(), cand, (uint64_t)nc * 8, hipMemcpyDeviceToHost);
     }
-    dfree(cand);
-    dfree(ncand);
     if (e != hipSuccess) { set_error("heavy: %s", hipGetErrorString(e)); return GNS_E_HIP; }
     // dedupe by id keeping max value
     std::sort(h.begin(), h.end(), [](uint64_t a, uint64_t b) {
