@@ -728,6 +728,10 @@ int ss_encode_ids(gns_ss *ss, const InputDesc &in, uint32_t ns) {
             cur ^= 1;
         }
         GNS_HIP(hipGetLastError());
+        // a fresh window parks the repeat encodes of every new flow: queue the
+        // second round behind the first without a host round trip (an empty
+        // parked list makes it a no-op; ptotal[1] was zeroed above)
+        if (round == 0) continue;
         GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
         GNS_HIP(hipMemcpyAsync(ss->h_pin + 2, ss->stats + 3, 8, hipMemcpyDeviceToHost, s));
         GNS_HIP(hipStreamSynchronize(s));
