@@ -149,6 +149,13 @@ def bench_superspread(args, torch, dist, world, rank, local):
     avg_ms = dom_ms / max(dom_launches, 1)
     pkts_per_launch = n * args.steps / max(dom_launches, 1)
     achieved = BYTES_PER_PKT * pkts_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None  # PMC HBM bytes per launch of the dominant kernel (tools/pmc_ss.sh)
+    tfile = os.path.join(ROOT, "profiles", "traffic_ss_latest.json")
+    if os.path.exists(tfile):
+        try:
+            traffic = json.load(open(tfile)).get(dom)
+        except Exception:
+            traffic = None
     hh = ss.heavy_hitters()
     line = {
         "metric": "Mpackets/s SuperSpread update (device-resident, d=2 w=32768 m=128)",
@@ -161,7 +168,7 @@ def bench_superspread(args, torch, dist, world, rank, local):
                                "100M headers in HBM per GPU per step, bit-exact registers/pbits/counters",
                    "packets_per_step_per_gpu": n},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_packet": BYTES_PER_PKT, "kernel_avg_ms": round(avg_ms, 4)},
         "stage_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()},
         "heavy_hitters": len(hh.Count), "engine_counters": ss.counters(),
