@@ -162,6 +162,10 @@ typedef struct gns_ss_params {
     int device;
 } gns_ss_params;
 
+/* The SuperSpread flow dictionary (4M flows) holds the flows that ever encoded
+ * in the period (only they can own a cell, so only they can be named by a key,
+ * a query or a heavy hitter); inserts return GNS_E_FULL beyond it, with the
+ * batch not applied. */
 int gns_ss_create(const gns_ss_params *p, gns_ss **out);
 int gns_ss_destroy(gns_ss *ss);
 int gns_ss_insert_keys(gns_ss *ss, const uint8_t *flows, uint32_t fstride, const uint8_t *elems,
