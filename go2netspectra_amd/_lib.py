@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("GNS_LIB") or os.path.join(_HERE, "libgns_sketch.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 GNS_OK = 0
+GNS_E_ARG, GNS_E_HIP, GNS_E_OOM, GNS_E_FULL, GNS_E_RANGE, GNS_E_NODEV = -1, -2, -3, -4, -5, -6
 ERRORS = {-1: "GNS_E_ARG", -2: "GNS_E_HIP", -3: "GNS_E_OOM", -4: "GNS_E_FULL", -5: "GNS_E_RANGE",
           -6: "GNS_E_NODEV"}
 MEM_HOST, MEM_DEVICE = 0, 1
@@ -74,7 +75,8 @@ class SsParams(ct.Structure):
                 ("m", ct.c_uint32), ("size", ct.c_uint32), ("base", ct.c_double), ("b", ct.c_double),
                 ("flow", Layout), ("elem", Layout), ("flow_bytes", ct.c_uint32),
                 ("elem_bytes", ct.c_uint32), ("seeds", ct.c_void_p), ("hll_master", ct.c_uint64),
-                ("rng_seed", ct.c_uint64), ("batch_packets", ct.c_uint64), ("device", ct.c_int)]
+                ("rng_seed", ct.c_uint64), ("batch_packets", ct.c_uint64), ("max_flows", ct.c_uint64),
+                ("device", ct.c_int)]
 
 
 class ExParams(ct.Structure):

@@ -5,7 +5,7 @@
 // count_min.go fed the same packets in the same order by ONE worker with the
 // same row seeds.  Each bucket holds two independent
 // (fingerprint, counter) pairs whose update rules are ORDER-DEPENDENT
-// (count_min.go:180-235), so the engine never scatters with plain atomics.
+// (count_min.go:99-155), so the engine never scatters with plain atomics.
 //
 // Pipeline per device batch:
 //   K1 k_extract  : packet -> flow key (registers) -> flow id (exact dictionary)
@@ -122,11 +122,11 @@ __device__ __forceinline__ int hot_lookup(const uint32_t *tabrow, uint32_t b) {
 __device__ __forceinline__ uint32_t ceil_log2_dev(uint32_t x) { return x <= 1 ? 0u : 32u - __clz(x - 1u); }
 
 __device__ __forceinline__ uint32_t row_index(const CmGeom &g, uint32_t h) {
-    return g.pow2 ? (h & g.wmask) : (h % g.w);  // count_min.go:177 `% t.w`
+    return g.pow2 ? (h & g.wmask) : (h % g.w);  // count_min.go:96 `% t.w`
 }
 
 // Per (hot slot, K1 block) summary of the block's updates to a designated
-// bucket, relative to the batch-entry fingerprints (count_min.go:180-235):
+// bucket, relative to the batch-entry fingerprints (count_min.go:99-155):
 // n updates, nfc / nfs of them foreign to the count / size owner, os / fs the
 // owner / foreign size sums, smax the largest foreign size.  k_hot_decide
 // turns them into the bucket's exact batch result without any per-update
@@ -959,7 +959,7 @@ static_assert(kScRound <= 65536, "K3 packs ranks in 16 bits");
 constexpr uint32_t kRepCap = GNS_REP_CAP;
 
 // ---------------------------------------------------------------------------
-// Exact wave-parallel sequence for ONE bucket (count_min.go:180-235): 64
+// Exact wave-parallel sequence for ONE bucket (count_min.go:99-155): 64
 // updates per step; a prefix sum gives the counter before every update, the
 // first update that would leave the linear regime (an "event": fingerprint
 // take-over, counter wrap) is applied explicitly and the scan restarts after
@@ -1043,7 +1043,7 @@ __device__ __forceinline__ void decode_entry(const uint64_t *ovf, uint64_t e, ui
     }
 }
 
-// Replay of one 64-item group (count_min.go:180-235): pending lanes hold
+// Replay of one 64-item group (count_min.go:99-155): pending lanes hold
 // updates of this wave's buckets, in stream order by lane.  A bucket with >= 8
 // updates in the group runs the wave-parallel sequence; the rest resolve
 // same-bucket lanes lowest-lane-first.
@@ -1079,7 +1079,7 @@ __device__ __forceinline__ void replay_group(ApplyLds &L, bool pending, uint32_t
         if (pending) atomicMax(&own[b], 64u - lane);
         const bool win = pending && own[b] == 64u - lane;
         if (win) {
-            if (rf & 2u) {  // size half, count_min.go:181-209
+            if (rf & 2u) {  // size half, count_min.go:99-128
                 uint32_t S = sS[b], F = sFs[b];
                 if (S == 0) { S = s; F = k; }
                 else if (F == k) S = S + s;
@@ -1087,7 +1087,7 @@ __device__ __forceinline__ void replay_group(ApplyLds &L, bool pending, uint32_t
                 else S = S - s;
                 sS[b] = S; sFs[b] = F;
             }
-            if (rf & 1u) {  // count half, count_min.go:211-235
+            if (rf & 1u) {  // count half, count_min.go:130-155
                 uint32_t C = sC[b], F = sFc[b];
                 if (C == 0) { C = 1; F = k; }
                 else if (F == k) C = C + 1;
@@ -1248,7 +1248,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             K4_MARK(2);
             st_rep += nlist;
             st_crep++;
-            // --- sequential replay (count_min.go:180-235), in order.  Buckets are
+            // --- sequential replay (count_min.go:99-155), in order.  Buckets are
             //     partitioned over the 16 waves (b % 16); each wave walks the
             //     list in order and applies its buckets' updates; lanes of one
             //     64-item group hitting distinct buckets run in parallel,
@@ -1497,7 +1497,7 @@ __global__ __launch_bounds__(256) void k_hot_sum(HotArgs a) {
 }
 
 // H2: exact check.  With no event the owner never changes and every counter
-// follows u32 arithmetic on the running walk (count_min.go:190-193 owner adds
+// follows u32 arithmetic on the running walk (count_min.go:109-113 owner adds
 // wrap mod 2^32 exactly like the walk); an event is a foreign update that
 // would find C <= 1 (:226-231 take-over) or S == 0 / s > S (:184-200).
 __global__ __launch_bounds__(256) void k_hot_verify(HotArgs a) {
@@ -1616,7 +1616,7 @@ __global__ __launch_bounds__(64) void k_hot_fallback(HotArgs a) {
 // Summary path for designated buckets.  K1 left one HotSum per (slot, K1
 // block).  The count half is linear (owner fixed, C' = C + n_own - n_foreign)
 // when C > n_foreign over the batch: every foreign update then finds C >= 2
-// (count_min.go:226-231 never reaches 0) -- and no u32 wrap.  The size half
+// (count_min.go:145-150 never reaches 0) -- and no u32 wrap.  The size half
 // is linear when every foreign update finds S >= max(s, 1) (:184-200 never
 // replace), where S is the running walk W = S0 + sum(own) - sum(foreign) taken
 // mod 2^32 (owner adds wrap exactly like the walk, :190-193).  Per K1 block j
@@ -1835,7 +1835,7 @@ __global__ __launch_bounds__(1024) void k_hot_table(CmGeom g, uint32_t *hot_ids,
 }
 
 // ---------------------------------------------------------------------------
-// Query (count_min.go:240-254), export, heavy-hitter candidates
+// Query (count_min.go:160-174), export, heavy-hitter candidates
 // ---------------------------------------------------------------------------
 struct QueryArgs {
     const uint8_t *keys;
@@ -2007,6 +2007,9 @@ int cm_reset_state(gns_cm *cm) {
     GNS_HIP(hipMemsetAsync(cm->hot_ids, 0xFF, (size_t)cm->g.d * kHot * 4, cm->stream));
     GNS_HIP(hipMemsetAsync(cm->hot_tab, 0xFF, (size_t)cm->g.d * kHotTab * 4, cm->stream));
     GNS_HIP(hipMemsetAsync(cm->hhist, 0, (size_t)cm->g.d * kHotKeys * 4, cm->stream));
+    // the error words (3 dict-full, 4 ovf-full) belong to the period: a reset
+    // empties the dictionary, so the next period starts without them
+    GNS_HIP(hipMemsetAsync(cm->stats + 3, 0, 2 * sizeof(unsigned long long), cm->stream));
     cm->warm = false;
     return GNS_OK;
 }
@@ -2237,7 +2240,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
     int rc = GNS_OK;
     do {
         if ((rc = set_dev(cm)) != GNS_OK) break;
-        // count_min.go:128-140 defaults
+        // count_min.go:48-59 defaults
         CmGeom &g = cm->g;
         g.w = p->width ? p->width : (1u << 20);
         g.d = p->depth ? p->depth : 3u;
@@ -2463,16 +2466,21 @@ int gns_cm_export_state(gns_cm *cm, uint32_t *C, uint32_t *S, uint8_t *FPc, uint
     return GNS_OK;
 }
 
-// HeavyHitters (count_min.go:259-327): a flow's max over its buckets reaches the
+// HeavyHitters (count_min.go:178-247): a flow's max over its buckets reaches the
 // threshold iff one of its buckets does, so only cells >= threshold are
 // candidates; dedupe by fingerprint keeping the max; sort value desc.
 static int cm_heavy_one(gns_cm *cm, const uint32_t *val, const uint32_t *fp, uint32_t thr,
                         uint8_t *flows, uint32_t *vals, uint64_t *n_io) {
     const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
     const uint32_t cap = (uint32_t)std::min<uint64_t>(cells, 1ull << 26);
-    if (!cm->hh_cand) {
-        GNS_TRY(dalloc(reinterpret_cast<void **>(&cm->hh_cand), (uint64_t)cap * 8));
-        GNS_TRY(dalloc(reinterpret_cast<void **>(&cm->hh_n), 16));
+    if (!cm->hh_cand || !cm->hh_n) {  // both or neither: a failed second allocation leaves neither
+        dfree(cm->hh_cand); dfree(cm->hh_n);
+        cm->hh_cand = nullptr; cm->hh_n = nullptr;
+        uint64_t *c = nullptr;
+        uint32_t *nn = nullptr;
+        GNS_TRY(dalloc(reinterpret_cast<void **>(&c), (uint64_t)cap * 8));
+        if (int rc = dalloc(reinterpret_cast<void **>(&nn), 16)) { dfree(c); return rc; }
+        cm->hh_cand = c; cm->hh_n = nn;
     }
     uint64_t *cand = cm->hh_cand;
     uint32_t *ncand = cm->hh_n;

@@ -370,6 +370,7 @@ void ex_free_all(gns_ex *ex) {
 
 int ex_clear(gns_ex *ex) {
     GNS_HIP(hipMemsetAsync(ex->D.rec, 0, ex->slots * ex->D.RW * 4, ex->stream));
+    GNS_HIP(hipMemsetAsync(ex->stats + 3, 0, sizeof(unsigned long long), ex->stream));  // dict-full word
     hipLaunchKernelGGL(k_ex_init, dim3((unsigned)((ex->slots + 255) / 256)), dim3(256), 0, ex->stream, ex->f,
                        ex->slots);
     GNS_HIP(hipGetLastError());

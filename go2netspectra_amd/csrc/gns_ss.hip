@@ -628,6 +628,7 @@ struct gns_ss {
     uint32_t *values = nullptr, *keys = nullptr;
     DictDev D{};
     uint64_t dict_slots = 0;
+    uint64_t max_flows = 0;  // dictionary capacity (gns_ss_params.max_flows)
     uint32_t epoch = 0;
     uint64_t pkt = 0;     // records inserted since create (RNG packet index)
     bool s1_pipe = true;
@@ -677,6 +678,7 @@ int ss_reset_state(gns_ss *ss, bool init) {
     GNS_HIP(hipMemsetAsync(ss->values, 0, cells * 4, ss->stream));
     GNS_HIP(hipMemsetAsync(ss->keys, 0xFF, cells * 4, ss->stream));
     GNS_HIP(hipMemsetAsync(ss->D.rec, 0, ss->dict_slots * ss->D.RW * 4, ss->stream));
+    GNS_HIP(hipMemsetAsync(ss->stats + 3, 0, sizeof(unsigned long long), ss->stream));  // dict-full word
     if (init) {  // pbits starts at 1.0 (:44); Reset leaves it untouched (:297-311)
         std::vector<double> ones(cells, 1.0);
         GNS_HIP(hipMemcpyAsync(ss->pbits, ones.data(), cells * 8, hipMemcpyHostToDevice, ss->stream));
@@ -735,7 +737,11 @@ int ss_encode_ids(gns_ss *ss, const InputDesc &in, uint32_t ns) {
         GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
         GNS_HIP(hipMemcpyAsync(ss->h_pin + 2, ss->stats + 3, 8, hipMemcpyDeviceToHost, s));
         GNS_HIP(hipStreamSynchronize(s));
-        if (ss->h_pin[2] | ss->h_pin[3]) { set_error("flow dictionary full; raise max flows"); return GNS_E_FULL; }
+        if (ss->h_pin[2] | ss->h_pin[3]) {
+            set_error("flow dictionary full (max_flows %llu, %llu slots); raise max_flows",
+                      (unsigned long long)ss->max_flows, (unsigned long long)ss->dict_slots);
+            return GNS_E_FULL;
+        }
         if (ss->h_pin[0] == 0) return GNS_OK;
         if (round > 64) { set_error("dictionary resolve did not converge"); return GNS_E_FULL; }
         GNS_HIP(hipMemsetAsync(ss->ptotal + (cur ^ 1), 0, 4, s));
@@ -950,7 +956,9 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
             (rc = dalloc_t(&ss->heads, cells + 1)))
             break;
         uint64_t slots = 1;
-        const uint64_t mf = 4ull << 20;
+        const uint64_t mf = p->max_flows ? p->max_flows : (4ull << 20);
+        if (mf > (1ull << 30)) { set_error("max_flows > 2^30"); rc = GNS_E_ARG; break; }
+        ss->max_flows = mf;
         while (slots < 2 * mf) slots <<= 1;
         ss->dict_slots = slots;
         ss->D.mask = (uint32_t)(slots - 1);

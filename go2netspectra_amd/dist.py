@@ -1,7 +1,7 @@
 """Multi-GPU sharding of the sketch path (one process per GPU, torch.distributed).
 
 Count-Min buckets are (fingerprint, counter) pairs under order-dependent
-majority-vote rules (count_min.go:180-235): they are NOT additive, so summing
+majority-vote rules (count_min.go:99-155): they are NOT additive, so summing
 counter rows across GPUs (all-reduce) would not produce the sketch of the
 union stream.  The path therefore shards by flow: packets are routed to the
 GPU that owns their SrcIP (every flow of a source lands on one GPU, SURVEY.md

@@ -83,8 +83,8 @@ def _seeds_arg(seeds, depth):
 class CountMin:
     """Fingerprinted majority-vote "CountMin" of count_min.go on one GPU.
 
-    Defaults mirror NewCountMin (count_min.go:128-140).  Row seeds are injected
-    (the reference draws them from math/rand/v2, count_min.go:142-145)."""
+    Defaults mirror NewCountMin (count_min.go:48-59).  Row seeds are injected
+    (the reference draws them from math/rand/v2, count_min.go:61-64)."""
 
     def __init__(self, width: int = 0, depth: int = 0, size_threshold: int = 0,
                  count_threshold: int = 0, flow_fields: Optional[Sequence[str]] = None,
@@ -157,7 +157,7 @@ class CountMin:
 
     # --- statistic.Sketch ---
     def insert(self, flow: bytes, elem: bytes = b"", size: int = 0) -> None:
-        """Insert(flow, elem, size); elem is unused by CountMin (count_min.go:175)."""
+        """Insert(flow, elem, size); elem is unused by CountMin (count_min.go:94)."""
         k = np.frombuffer(bytes(flow), dtype=np.uint8).reshape(1, -1)
         self.insert_keys(k, np.array([size], dtype=np.uint32))
 
@@ -171,7 +171,7 @@ class CountMin:
         return out
 
     def query(self, flow: bytes) -> int:
-        """Query(flow) = count<<32 | size (count_min.go:240-254)."""
+        """Query(flow) = count<<32 | size (count_min.go:160-174)."""
         if len(flow) != self.key_bytes:
             return 0  # bytes.Equal against FS-byte fingerprints never matches
         return int(self.query_many(np.frombuffer(bytes(flow), np.uint8).reshape(1, -1))[0])
@@ -271,7 +271,8 @@ class SuperSpread:
                  base: float = 0.0, b: float = 0.0, flow_fields: Optional[Sequence[str]] = None,
                  elem_fields: Optional[Sequence[str]] = None, flow_bytes: Optional[int] = None,
                  elem_bytes: Optional[int] = None, seeds=None, hll_master: int = 0x1234ABCD5678EF01,
-                 rng_seed: int = 0x0DDBA11CAFEF00D5, batch_packets: int = 0, device: int = 0):
+                 rng_seed: int = 0x0DDBA11CAFEF00D5, batch_packets: int = 0, device: int = 0,
+                 max_flows: int = 0):
         self._L = _lib.load()
         self.flow_fields = list(flow_fields or [])
         self.elem_fields = list(elem_fields or [])
@@ -284,6 +285,7 @@ class SuperSpread:
         p.flow_bytes, p.elem_bytes = fb, eb
         self._seeds, p.seeds = _seeds_arg(seeds, depth or 3)
         p.hll_master, p.rng_seed, p.batch_packets, p.device = hll_master, rng_seed, batch_packets, device
+        p.max_flows = max_flows
         h = ct.c_void_p()
         check(self._L.gns_ss_create(ct.byref(p), ct.byref(h)))
         self._h = h

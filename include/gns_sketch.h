@@ -10,13 +10,13 @@
  *       -> gns_cm_insert_tuples / gns_ss_insert_tuples       (EncodeFlow fused on device)
  *   pcap.Reader.ReadPackets + ParsePacketInto  pkg/pcap/reader.go:35-49, internal/protocol/parser.go:23-67
  *       -> gns_cm_insert_headers / gns_ss_insert_headers     (64-byte records, parse fused)
- *   statistic.Sketch.Query(flow)               sketch.go:7; count_min.go:240-254; super_spread.go:238-249
+ *   statistic.Sketch.Query(flow)               sketch.go:7; count_min.go:160-174; super_spread.go:238-249
  *       -> gns_cm_query / gns_ss_query
- *   statistic.Sketch.HeavyHitters()            sketch.go:8; count_min.go:259-327; super_spread.go:254-294
+ *   statistic.Sketch.HeavyHitters()            sketch.go:8; count_min.go:178-247; super_spread.go:254-294
  *       -> gns_cm_heavy_hitters / gns_ss_heavy_hitters
- *   statistic.Sketch.Reset()                   sketch.go:9; count_min.go:330-346; super_spread.go:297-311
+ *   statistic.Sketch.Reset()                   sketch.go:9; count_min.go:249-265; super_spread.go:297-311
  *       -> gns_cm_reset / gns_ss_reset
- *   statistic.NewCountMin / NewSuperSpread     count_min.go:128-172; super_spread.go:127-179
+ *   statistic.NewCountMin / NewSuperSpread     count_min.go:47-90; super_spread.go:127-179
  *       -> gns_cm_create / gns_ss_create (seeds injected, see below)
  *
  * Rules:
@@ -32,6 +32,13 @@
  *   - Flow keys are the reference EncodeFlow bytes (task.go:279-300): IP slots
  *     of 16 bytes with IPv4 left-aligned and zero padded, ports big-endian,
  *     protocol one byte; key_bytes <= 37 (task.go:74).
+ *   - GNS_E_FULL ends the measurement period for the handle: the failing
+ *     device batch is not applied (earlier device batches of the same call
+ *     are) and every later insert returns GNS_E_FULL, until gns_*_reset()
+ *     empties the sketch and its flow dictionary (the reference's period
+ *     reset, manager.go:179-193).  Count-Min's GNS_E_RANGE (from flush: too
+ *     many oversize packets in one device batch) is sticky the same way; the
+ *     sketch is not exact after it.
  */
 #ifndef GNS_SKETCH_H
 #define GNS_SKETCH_H
@@ -82,12 +89,12 @@ typedef struct gns_tuples {
 typedef struct gns_cm gns_cm;
 
 typedef struct gns_cm_params {
-    uint32_t width, depth;                    /* 0 -> 2^20 / 3 (count_min.go:128-134) */
-    uint32_t size_threshold, count_threshold; /* 0 -> 512 KiB / 512 (count_min.go:135-140) */
+    uint32_t width, depth;                    /* 0 -> 2^20 / 3 (count_min.go:48-53) */
+    uint32_t size_threshold, count_threshold; /* 0 -> 512 KiB / 512 (count_min.go:54-59) */
     gns_layout flow;                          /* flow key layout (for tuples/headers input) */
     uint32_t key_bytes;                       /* FS; must equal the layout's byte size when
                                                  n_fields > 0; used alone for keys input */
-    const uint32_t *seeds;                    /* depth row seeds (count_min.go:142-145 draws
+    const uint32_t *seeds;                    /* depth row seeds (count_min.go:61-64 draws
                                                  them with rand.Uint32; here injected).
                                                  NULL -> splitmix64(0x9747B28C) stream */
     uint64_t max_flows;                       /* distinct flows per measurement period
@@ -116,9 +123,9 @@ int gns_cm_insert_tuples(gns_cm *cm, const gns_tuples *t, uint64_t n, gns_mem wh
 int gns_cm_insert_headers(gns_cm *cm, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
                           gns_mem where);
 int gns_cm_flush(gns_cm *cm);
-/* out[i] = count<<32 | size, count_min.go:240-254 */
+/* out[i] = count<<32 | size, count_min.go:160-174 */
 int gns_cm_query(gns_cm *cm, const uint8_t *keys, uint32_t stride, uint64_t n, uint64_t *out);
-/* HeavyHitters, count_min.go:259-327.  Lists are sorted value-descending with
+/* HeavyHitters, count_min.go:178-247.  Lists are sorted value-descending with
  * ties broken by flow bytes ascending (the reference leaves ties unordered).
  * On input *n_count / *n_size hold the capacities (entries); on output the
  * full list lengths (call again with larger buffers if they exceed the
@@ -159,13 +166,17 @@ typedef struct gns_ss_params {
     uint64_t hll_master;               /* derives each GeneralHLL's seeds[0..1] */
     uint64_t rng_seed;                 /* keys the declared generator replacing rand.Float64 */
     uint64_t batch_packets;
+    uint64_t max_flows;                /* flow dictionary capacity; 0 -> 4M (2^22) */
     int device;
 } gns_ss_params;
 
-/* The SuperSpread flow dictionary (4M flows) holds the flows that ever encoded
+/* The SuperSpread flow dictionary (max_flows) holds the flows that ever encoded
  * in the period (only they can own a cell, so only they can be named by a key,
- * a query or a heavy hitter); inserts return GNS_E_FULL beyond it, with the
- * batch not applied. */
+ * a query or a heavy hitter).  An insert that would exceed it returns
+ * GNS_E_FULL naming max_flows; the device batch (<= batch_packets records) in
+ * which it happened is not applied, earlier device batches of the same call
+ * are.  gns_ss_counters() out[6] (records) tells how far the stream got, and
+ * gns_ss_reset starts a new period with an empty dictionary. */
 int gns_ss_create(const gns_ss_params *p, gns_ss **out);
 int gns_ss_destroy(gns_ss *ss);
 int gns_ss_insert_keys(gns_ss *ss, const uint8_t *flows, uint32_t fstride, const uint8_t *elems,

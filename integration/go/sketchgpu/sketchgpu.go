@@ -22,6 +22,7 @@ import "C"
 
 import (
 	"errors"
+	"log"
 	"unsafe"
 
 	"Go2NetSpectra/internal/engine/impl/sketch/statistic"
@@ -40,9 +41,20 @@ func lastErr(rc C.int) error {
 type CountMin struct {
 	h        *C.gns_cm
 	keyBytes int
+	err      error // first insert failure of the period (Insert has no error return)
 }
 
-// NewCountMin replaces statistic.NewCountMin (count_min.go:128-172); seeds are injected.
+// sticky keeps the first failure of a measurement period and logs it the way
+// the reference logs a dropped packet (task.go:162-166).  GNS_E_FULL is sticky
+// in the engine too: every later insert fails until Reset.
+func sticky(dst *error, err error) {
+	if err != nil && *dst == nil {
+		*dst = err
+		log.Printf("sketchgpu: insert failed, packets are dropped until Reset: %v", err)
+	}
+}
+
+// NewCountMin replaces statistic.NewCountMin (count_min.go:47-90); seeds are injected.
 func NewCountMin(width, depth, st, ct uint32, flowFields []string, keyBytes uint32, seeds []uint32,
 	maxFlows uint64, device int) (*CountMin, error) {
 	var p C.gns_cm_params
@@ -67,8 +79,14 @@ func NewCountMin(width, depth, st, ct uint32, flowFields []string, keyBytes uint
 
 // Insert implements statistic.Sketch for one packet (a batch of one; prefer InsertBatch).
 func (c *CountMin) Insert(flow, elem []byte, size uint32) {
-	_ = c.InsertBatch(flow, uint32(len(flow)), []uint32{size})
+	if len(flow) == 0 {
+		return
+	}
+	sticky(&c.err, c.InsertBatch(flow, uint32(len(flow)), []uint32{size}))
 }
+
+// Err reports the first insert failure since the last Reset (nil if none).
+func (c *CountMin) Err() error { return c.err }
 
 // InsertBatch: keys is n*stride bytes, sizes n entries, applied in order.
 func (c *CountMin) InsertBatch(keys []byte, stride uint32, sizes []uint32) error {
@@ -93,7 +111,7 @@ func (c *CountMin) InsertTuples(src16, dst16 []byte, sport, dport []uint16, prot
 	return lastErr(C.gns_cm_insert_tuples(c.h, &t, C.uint64_t(n), C.GNS_MEM_HOST))
 }
 
-// Query implements statistic.Sketch (count_min.go:240-254).
+// Query implements statistic.Sketch (count_min.go:160-174).
 func (c *CountMin) Query(flow []byte) uint64 {
 	if len(flow) != c.keyBytes || len(flow) == 0 {
 		return 0
@@ -105,7 +123,7 @@ func (c *CountMin) Query(flow []byte) uint64 {
 	return uint64(out)
 }
 
-// HeavyHitters implements statistic.Sketch (count_min.go:259-327).
+// HeavyHitters implements statistic.Sketch (count_min.go:178-247).
 func (c *CountMin) HeavyHitters() statistic.HeavyRecord {
 	var nc, ns C.uint64_t
 	if C.gns_cm_heavy_hitters(c.h, nil, nil, &nc, nil, nil, &ns) != C.GNS_OK {
@@ -129,8 +147,11 @@ func (c *CountMin) HeavyHitters() statistic.HeavyRecord {
 	return rec
 }
 
-// Reset implements statistic.Sketch (count_min.go:330-346).
-func (c *CountMin) Reset() { C.gns_cm_reset(c.h) }
+// Reset implements statistic.Sketch (count_min.go:249-265).
+func (c *CountMin) Reset() {
+	C.gns_cm_reset(c.h)
+	c.err = nil
+}
 
 // Close releases the device sketch.
 func (c *CountMin) Close() { C.gns_cm_destroy(c.h) }
@@ -141,12 +162,13 @@ var _ statistic.Sketch = (*CountMin)(nil)
 type SuperSpread struct {
 	h        *C.gns_ss
 	flowSize int
+	err      error // first insert failure of the period
 }
 
 // NewSuperSpread replaces statistic.NewSuperSpread (super_spread.go:129-149). Seeds, the
 // HLL master seed and the declared generator's seed are injected (DESIGN.md §2).
 func NewSuperSpread(width, depth, threshold, m, size uint32, base, b float64, flowFields, elemFields []string,
-	seeds []uint32, hllMaster, rngSeed uint64, device int) (*SuperSpread, error) {
+	seeds []uint32, hllMaster, rngSeed, maxFlows uint64, device int) (*SuperSpread, error) {
 	var p C.gns_ss_params
 	p.width, p.depth, p.threshold, p.m, p.size = C.uint32_t(width), C.uint32_t(depth), C.uint32_t(threshold),
 		C.uint32_t(m), C.uint32_t(size)
@@ -163,6 +185,7 @@ func NewSuperSpread(width, depth, threshold, m, size uint32, base, b float64, fl
 		p.seeds = (*C.uint32_t)(unsafe.Pointer(&seeds[0]))
 	}
 	p.hll_master, p.rng_seed, p.device = C.uint64_t(hllMaster), C.uint64_t(rngSeed), C.int(device)
+	p.max_flows = C.uint64_t(maxFlows) // 0 -> 4M
 	var h *C.gns_ss
 	if err := lastErr(C.gns_ss_create(&p, &h)); err != nil {
 		return nil, err
@@ -197,9 +220,12 @@ func (s *SuperSpread) Insert(flow, elem []byte, size uint32) {
 	if len(elem) > 0 {
 		e = (*C.uint8_t)(unsafe.Pointer(&elem[0]))
 	}
-	C.gns_ss_insert_keys(s.h, (*C.uint8_t)(unsafe.Pointer(&flow[0])), C.uint32_t(len(flow)), e,
-		C.uint32_t(len(elem)), 1, C.GNS_MEM_HOST)
+	sticky(&s.err, lastErr(C.gns_ss_insert_keys(s.h, (*C.uint8_t)(unsafe.Pointer(&flow[0])),
+		C.uint32_t(len(flow)), e, C.uint32_t(len(elem)), 1, C.GNS_MEM_HOST)))
 }
+
+// Err reports the first insert failure since the last Reset (nil if none).
+func (s *SuperSpread) Err() error { return s.err }
 
 // Query implements statistic.Sketch (super_spread.go:238-249).
 func (s *SuperSpread) Query(flow []byte) uint64 {
@@ -231,7 +257,10 @@ func (s *SuperSpread) HeavyHitters() statistic.HeavyRecord {
 }
 
 // Reset implements statistic.Sketch (super_spread.go:297-311).
-func (s *SuperSpread) Reset() { C.gns_ss_reset(s.h) }
+func (s *SuperSpread) Reset() {
+	C.gns_ss_reset(s.h)
+	s.err = nil
+}
 
 // Close releases the device sketch.
 func (s *SuperSpread) Close() { C.gns_ss_destroy(s.h) }

@@ -225,7 +225,7 @@ or_cm *or_cm_new(uint32_t width, uint32_t depth, uint32_t st, uint32_t ct, uint3
     or_cm *cm = (or_cm *)calloc(1, sizeof(or_cm));
     cm->w = width; cm->d = depth; cm->st = st; cm->ct = ct; cm->K = K;
     cm->seed = (uint32_t *)malloc(sizeof(uint32_t) * depth);
-    for (uint32_t i = 0; i < depth; i++) cm->seed[i] = seeds[i]; /* injected (count_min.go:142-145) */
+    for (uint32_t i = 0; i < depth; i++) cm->seed[i] = seeds[i]; /* injected (count_min.go:61-64) */
     size_t cells = (size_t)depth * width;
     cm->C = (uint32_t *)calloc(cells, 4);
     cm->S = (uint32_t *)calloc(cells, 4);
@@ -243,7 +243,7 @@ void or_cm_params(const or_cm *cm, uint32_t *w, uint32_t *d, uint32_t *st, uint3
     *w = cm->w; *d = cm->d; *st = cm->st; *ct = cm->ct;
 }
 
-/* count_min.go:175-238, one worker (no CAS races). */
+/* count_min.go:94-157, one worker (no CAS races). */
 void or_cm_insert(or_cm *cm, const uint8_t *key, uint32_t size) {
     const uint32_t K = cm->K;
     for (uint32_t i = 0; i < cm->d; i++) {
@@ -300,7 +300,7 @@ static void cas_insert(or_cm *cm, const uint8_t *key, uint32_t size) {
         size_t cell = (size_t)i * cm->w + or_mm3(key, K, cm->seed[i]) % cm->w;
         uint32_t *Sp = &cm->S[cell], *Cp = &cm->C[cell];
         uint8_t *fs = cm->FPs + cell * K, *fc = cm->FPc + cell * K;
-        for (;;) { /* count_min.go:181-209 */
+        for (;;) { /* count_min.go:99-128 */
             uint32_t cur = __atomic_load_n(Sp, __ATOMIC_SEQ_CST);
             if (cur == 0) {
                 if (__atomic_compare_exchange_n(Sp, &cur, size, 0, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {
@@ -316,7 +316,7 @@ static void cas_insert(or_cm *cm, const uint8_t *key, uint32_t size) {
                 if (__atomic_compare_exchange_n(Sp, &cur, cur - size, 0, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) break;
             }
         }
-        for (;;) { /* count_min.go:211-235 */
+        for (;;) { /* count_min.go:130-155 */
             uint32_t cur = __atomic_load_n(Cp, __ATOMIC_SEQ_CST);
             if (cur == 0) {
                 if (__atomic_compare_exchange_n(Cp, &cur, 1, 0, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {
@@ -367,7 +367,7 @@ uint64_t or_cm_insert_hdr64_pool(or_cm *cm, const uint8_t *hdr, const uint32_t *
     return done;
 }
 
-/* count_min.go:240-254 */
+/* count_min.go:160-174 */
 uint64_t or_cm_query(const or_cm *cm, const uint8_t *key) {
     uint32_t sz = 0, ct = 0;
     for (uint32_t i = 0; i < cm->d; i++) {
@@ -412,7 +412,7 @@ static int hh_cmp_val(const void *a, const void *b) {
 static pthread_mutex_t hh_mu = PTHREAD_MUTEX_INITIALIZER;
 
 /* dedupe by fingerprint keeping the max, keep >= thr, sort value desc
- * (count_min.go:259-327); ties ordered by flow bytes (canonical). */
+ * (count_min.go:178-247); ties ordered by flow bytes (canonical). */
 static uint32_t hh_finish(hh_item *it, size_t n, uint32_t K, uint32_t thr, uint8_t *flows,
                           uint32_t *vals, uint32_t cap) {
     pthread_mutex_lock(&hh_mu);

@@ -4,7 +4,7 @@
   mm3_kat.json      public MurmurHash3_x86_32 known answers (SMHasher
                     verification value and published vectors) -- the external
                     pin of hash.go:13-53.
-  cm_traces.json    hand-derived single-bucket traces of count_min.go:180-235
+  cm_traces.json    hand-derived single-bucket traces of count_min.go:99-155
                     (w=1, d=1: every update hits the same bucket, so the
                     expected states follow from reading the Go code; they are
                     written out literally below, not computed).
@@ -47,7 +47,7 @@ SMHASHER_VERIFICATION = 0xB0F57EE3
 
 # Hand-derived traces.  Keys are 4-byte strings; size in bytes.  After every
 # update the expected bucket state (C, FPc, S, FPs) is listed, following
-# count_min.go:181-235 line by line.
+# count_min.go:99-155 line by line.
 A, B, Cc = "aaaa", "bbbb", "cccc"
 CM_TRACES = [
     {"name": "takeover_on_empty_then_majority",

@@ -68,7 +68,7 @@ def test_many_calls_and_reset(gpu, oracle):
 
 
 def test_sizes_wrap_and_overflow(gpu, oracle):
-    """sizes >= 2^20-1 take the overflow path; u32 wrap of S (count_min.go:191)."""
+    """sizes >= 2^20-1 take the overflow path; u32 wrap of S (count_min.go:110)."""
     rng = np.random.default_rng(9)
     cm, orc = make_pair(oracle, 128, 2, 8)
     keys, _, _ = zipf_keys(rng, 50_000, 40, 8, s=1.5)
@@ -315,3 +315,27 @@ def test_bucket_range_rejects_bad_ranges(gpu):
     for rg in [(10, 10), (20, 10), (0, 5001)]:
         with pytest.raises(Exception):
             CountMin(5000, 2, 1000, 10, key_bytes=16, bucket_range=rg)
+
+
+def test_full_dictionary_is_cleared_by_reset(gpu, oracle):
+    """GNS_E_FULL holds for the period (sticky) and reset starts a clean one:
+    after an overflow and a reset, inserts succeed and match the oracle."""
+    from go2netspectra_amd._lib import GNS_E_FULL, GnsError
+    rng = np.random.default_rng(17)
+    cm, orc = make_pair(oracle, 1024, 3, 16, max_flows=64)
+    keys, _, _ = zipf_keys(rng, 20_000, 5000, 16, s=0.5)
+    with pytest.raises(GnsError) as e:
+        cm.insert_keys(keys, sizes_u32(rng, 20_000))
+    assert e.value.code == GNS_E_FULL and "max_flows" in str(e.value)
+    small, _, _ = zipf_keys(rng, 1000, 20, 16)
+    with pytest.raises(GnsError):
+        cm.insert_keys(small, sizes_u32(rng, 1000))  # still the same period
+    cm.reset()
+    orc.reset()
+    for _ in range(3):
+        small, _, _ = zipf_keys(rng, 5000, 40, 16)
+        sizes = sizes_u32(rng, 5000)
+        cm.insert_keys(small, sizes)
+        orc.insert_keys(small, sizes)
+    cm.flush()
+    assert_same_state(cm, orc)

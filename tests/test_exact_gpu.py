@@ -153,3 +153,27 @@ aggregator:
     msg = task.alerter_msg([{"name": "r", "task_name": "per_five_tuple", "metric": "total_packets",
                              "operator": ">", "threshold": 100}])
     assert "Observed Value:</b> <code>20000 packets" in msg
+
+
+def test_full_dictionary_is_cleared_by_reset(gpu, oracle):
+    """GNS_E_FULL holds for the period; reset starts a clean one that matches the oracle."""
+    from go2netspectra_amd import ExactTask, HeaderBatch
+    from go2netspectra_amd._lib import GNS_E_FULL, GnsError
+    rng = np.random.default_rng(29)
+    task = ExactTask("tiny", FIVE, max_flows=32)
+    t = random_tuples(rng, 20_000, 3000, s=0.5)
+    hdr = frames_from_tuples(t, rng)
+    ts = np.arange(len(hdr), dtype=np.int64)
+    with pytest.raises(GnsError) as e:
+        task.process_packets(HeaderBatch(hdr, t["length"], ts))
+        task.flush()
+    assert e.value.code == GNS_E_FULL
+    task.reset()
+    orc = oracle.Exact(FIVE)
+    t2 = random_tuples(rng, 5000, 20)
+    hdr2 = frames_from_tuples(t2, rng)
+    ts2 = np.arange(len(hdr2), dtype=np.int64) + 99
+    task.process_packets(HeaderBatch(hdr2, t2["length"], ts2))
+    task.flush()
+    orc.insert_hdr64(hdr2, t2["length"], ts2)
+    assert gpu_flows(task) == orc.export()
