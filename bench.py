@@ -360,6 +360,121 @@ def bench_thrift(args, torch, dist, world, rank, local):
         dist.destroy_process_group()
 
 
+def bench_hybrid(args, torch, dist, world, rank, local):
+    """configs[4]: hybrid exact + sketch.  Each step (one window of 100M packets per
+    GPU) goes through BOTH the exact per-5-tuple aggregator and a Count-Min of the
+    configs[4] geometry (d=8, w=2^24); at every window boundary the sketch's
+    snapshot view is refreshed and a reader thread extracts the device-side
+    heavy-hitter lists (count and size) and answers a batch of point queries
+    from it while the next window is being ingested (queries concurrent with
+    ingest).  value = packets ingested by both paths / time; the reader's work
+    is inside the timed region (it is joined before the closing barrier)."""
+    import threading
+    from go2netspectra_amd import CountMin, ExactTask, HeaderBatch, SyntheticTraffic
+    n = args.packets
+    W, D = 1 << 24, 8
+    syn = SyntheticTraffic(shard=rank, nshards=world, device=local)
+    hdr, wl = syn.generate(n)
+    ts = torch.arange(n, dtype=torch.int64, device=f"cuda:{local}") * 100 + 1_700_000_000_000_000_000
+    batch = HeaderBatch(hdr, wl, ts)
+    ex = ExactTask("per_five_tuple", FIELDS, 128, device=local, max_flows=1 << 21, batch_packets=args.batch or n)
+    cm = CountMin(W, D, 1 << 20, 1000, flow_fields=FIELDS, seeds=row_seeds(D), max_flows=1 << 21,
+                  batch_packets=args.batch or n, device=local)
+    view = cm.view()
+    # point-query keys: the 5-tuple keys of 2^16 packets of the stream (host copy, made once)
+    h = hdr[: 1 << 16].view(torch.uint8).cpu().numpy()
+    qkeys = np.zeros((h.shape[0], 37), np.uint8)
+    qkeys[:, 0:4], qkeys[:, 16:20], qkeys[:, 32:36], qkeys[:, 36] = h[:, 26:30], h[:, 30:34], h[:, 34:38], h[:, 23]
+
+    # the two ingest paths run on their own streams from two host threads (each
+    # engine synchronizes its own stream at batch boundaries)
+    def ex_step():
+        ex.process_packets(batch)
+        ex.flush()
+
+    def step():
+        te = threading.Thread(target=ex_step)
+        te.start()
+        cm.insert_headers(hdr, wl)
+        te.join()
+
+    for _ in range(args.warmup):
+        step()
+    ex.flush()
+    cm.flush()
+    cm.set_timing(True)
+    cm.stage_times(reset=True)
+    windows = []
+    lock = threading.Condition()
+    pending = [0]
+    stop = [False]
+    lat = []
+
+    def reader():
+        while True:
+            with lock:
+                while pending[0] == 0 and not stop[0]:
+                    lock.wait()
+                if pending[0] == 0 and stop[0]:
+                    return
+                pending[0] = 0
+            t0 = time.perf_counter()
+            cf, cv, sf, sv = view.heavy_hitters_arrays()
+            q = view.query_many(qkeys)
+            lat.append(time.perf_counter() - t0)
+            windows.append((len(cv), len(sv), int((q >> np.uint64(32)).max()) if len(q) else 0))
+
+    th = threading.Thread(target=reader)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    th.start()
+    for _ in range(args.steps):
+        step()
+        view.refresh()               # window boundary: snapshot for the reader
+        with lock:
+            pending[0] += 1
+            lock.notify()
+    ex.flush()
+    cm.flush()
+    with lock:
+        stop[0] = True
+        lock.notify()
+    th.join()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    stages = cm.stage_times()
+    line = {
+        "metric": "Mpackets/s hybrid exact + CMS d=8 w=2^24 ingest with concurrent heavy-hitter queries",
+        "value": round(n * args.steps * world / elapsed / 1e6, 2), "unit": "Mpackets/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32/u64",
+        "data": "synthetic (Zipf 1.1 over 2^20 5-tuples, 64-B records, on-device generator)",
+        "config": {"workload": "configs[4]: exact per-5-tuple aggregator + Count-Min d=8 w=2^24 on the same "
+                               "100M-packet window per GPU; per window a snapshot view, device-side heavy-hitter "
+                               "extraction and 65,536 point queries on a reader thread concurrent with ingest",
+                   "packets_per_step_per_gpu": n, "windows_queried": len(windows)},
+        "queries": {"windows": len(windows), "latency_ms_avg": round(1e3 * sum(lat) / max(len(lat), 1), 3),
+                    "latency_ms_max": round(1e3 * max(lat), 3) if lat else None,
+                    "last_window_heavy_hitters": {"count": windows[-1][0], "size": windows[-1][1]} if windows else None},
+        "stage_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()},
+        "note": "not the headline metric",
+    }
+    view.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -370,8 +485,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--width", type=int, default=WIDTH, help="Count-Min width (2^24 = configs[4] geometry)")
     ap.add_argument("--depth", type=int, default=DEPTH, help="Count-Min depth (8 = configs[4] geometry)")
-    ap.add_argument("--sketch", choices=["countmin", "superspread", "exact", "thrift"], default="countmin",
-                    help="superspread = configs[2]; exact = the exact aggregator (neither is the headline metric)")
+    ap.add_argument("--sketch", choices=["countmin", "superspread", "exact", "thrift", "hybrid"], default="countmin",
+                    help="superspread = configs[2]; hybrid = configs[4]; exact = the exact aggregator "
+                         "(none of them is the headline metric)")
     ap.add_argument("--max-flows", type=int, default=1 << 21,
                     help="flow dictionary capacity (slots = next power of two >= 2x)")
     ap.add_argument("--key", choices=["5tuple", "srcip"], default="5tuple",
@@ -404,6 +520,8 @@ def main():
         return bench_exact(args, torch, dist, world, rank, local)
     if args.sketch == "thrift":
         return bench_thrift(args, torch, dist, world, rank, local)
+    if args.sketch == "hybrid":
+        return bench_hybrid(args, torch, dist, world, rank, local)
     n = args.packets
     syn = SyntheticTraffic(flows=args.flows, shard=rank, nshards=world, device=local)
     hdr, wl = syn.generate(n)

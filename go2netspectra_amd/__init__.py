@@ -11,13 +11,13 @@ from .config import Config, ExactTaskDef, SketchTaskDef, load_config, parse_conf
 from .exact import ExactAggregator, ExactTask, NewExact, SnapshotData
 from .factory import Manager, TaskGroup, create, register_aggregator
 from .packets import HeaderBatch, PacketBatch, SyntheticTraffic, ip_slot, read_pcap, write_pcap
-from .sketch import CountMin, HeavyCount, HeavyRecord, HeavySize, SuperSpread
+from .sketch import CountMin, CountMinView, HeavyCount, HeavyRecord, HeavySize, SuperSpread
 from .task import New, SketchTask, decode_flow
 
 __all__ = [
     "GnsError", "build", "load", "Config", "SketchTaskDef", "load_config", "parse_config", "Manager",
     "TaskGroup", "create", "register_aggregator", "HeaderBatch", "PacketBatch", "SyntheticTraffic",
-    "ip_slot", "read_pcap", "write_pcap", "CountMin", "HeavyCount", "HeavyRecord", "HeavySize",
+    "ip_slot", "read_pcap", "write_pcap", "CountMin", "CountMinView", "HeavyCount", "HeavyRecord", "HeavySize",
     "SuperSpread", "New", "SketchTask", "decode_flow", "ExactTaskDef", "ExactAggregator", "ExactTask",
     "NewExact", "SnapshotData",
 ]

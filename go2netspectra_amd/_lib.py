@@ -26,6 +26,8 @@ EXPORTED = [
     "gns_cm_create", "gns_cm_destroy", "gns_cm_insert_keys", "gns_cm_insert_tuples",
     "gns_cm_insert_headers", "gns_cm_flush", "gns_cm_query", "gns_cm_heavy_hitters", "gns_cm_reset",
     "gns_cm_export_state", "gns_cm_stats", "gns_cm_counters", "gns_cm_set_timing", "gns_cm_stage_times", "gns_cm_stream",
+    "gns_cm_view_create", "gns_cm_view_destroy", "gns_cm_view_refresh", "gns_cm_view_heavy_hitters",
+    "gns_cm_view_query",
     "gns_ss_create", "gns_ss_destroy", "gns_ss_insert_keys", "gns_ss_insert_tuples",
     "gns_ss_insert_headers", "gns_ss_flush", "gns_ss_query", "gns_ss_heavy_hitters", "gns_ss_reset",
     "gns_ss_export_state", "gns_ss_stats", "gns_ss_counters", "gns_ss_set_timing", "gns_ss_stage_times",
@@ -121,6 +123,9 @@ def load() -> ct.CDLL:
         "gns_cm_counters": ([vp, vp], i32),
         "gns_cm_set_timing": ([vp, i32], i32), "gns_cm_stage_times": ([vp, vp, vp, i32], i32),
         "gns_cm_stream": ([vp], vp),
+        "gns_cm_view_create": ([vp, vp], i32), "gns_cm_view_destroy": ([vp], i32),
+        "gns_cm_view_refresh": ([vp], i32), "gns_cm_view_heavy_hitters": ([vp, vp, vp, vp, vp, vp, vp], i32),
+        "gns_cm_view_query": ([vp, vp, u32, u64, vp], i32),
         "gns_ss_create": ([vp, vp], i32), "gns_ss_destroy": ([vp], i32),
         "gns_ss_insert_keys": ([vp, vp, u32, vp, u32, u64, i32], i32),
         "gns_ss_insert_tuples": ([vp, vp, u64, i32], i32),

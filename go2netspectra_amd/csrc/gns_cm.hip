@@ -15,11 +15,13 @@
 //   K2 k_scan*    : exclusive scan of the histograms -> stable bin offsets.
 //   K3 k_scatter  : stable partition of 8-byte bucket updates into (row, tile)
 //                   bins (LDS-staged so every bin receives contiguous runs).
-//   K4 k_apply    : one workgroup per bin; the tile's bucket state lives in
+//   K4 k_apply    : persistent, one workgroup per CU taking bins from a work
+//                   counter (largest first); the tile's bucket state lives in
 //                   LDS; updates are applied chunk by chunk in stream order:
 //                   order-free aggregate fast path where provably exact,
 //                   sequential replay for the buckets where it is not.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -51,7 +53,11 @@ constexpr uint32_t kSizeEsc = 0xFFFFu;
 constexpr uint32_t kOvfFlag = 0x80000000u;
 constexpr uint32_t kOvfCap = 1u << 22;
 constexpr uint32_t kMaxBinsAll = 4096;               // d * bins per row (k_order, K3 LDS)
-constexpr int kExThreads = 256;
+#ifndef GNS_EX_THREADS
+#define GNS_EX_THREADS 256
+#endif
+constexpr int kExThreads = GNS_EX_THREADS;
+constexpr size_t kExLdsSmall = 40 * 1024;             // K1 LDS above this: 1024-thread blocks
 #ifndef GNS_CHUNK
 #define GNS_CHUNK 16384
 #endif
@@ -352,8 +358,11 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 #ifndef GNS_EX_MINW
 #define GNS_EX_MINW 4
 #endif
-template <int KIND, int MODE, int KB, int DD>
-__global__ __launch_bounds__(kExThreads, GNS_EX_MINW) void k_extract(ExtractArgs a) {
+// NT = threads per block: 256 (four blocks per CU) when the block's LDS fits four
+// times in a CU, else 1024 (one block of 16 waves: wide or deep sketches, whose
+// histogram and hot-slot tables take more than a quarter of the LDS).
+template <int KIND, int MODE, int KB, int DD, int NT>
+__global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : 1) void k_extract(ExtractArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xsm[];
     __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
     __shared__ uint8_t s_src[80];
@@ -369,9 +378,9 @@ __global__ __launch_bounds__(kExThreads, GNS_EX_MINW) void k_extract(ExtractArgs
     const uint32_t K = KB ? (uint32_t)KB : a.kp.K;
     const uint32_t d = DD ? (uint32_t)DD : a.g.d;
     constexpr uint32_t RMAX = DD ? (uint32_t)DD : 8u;
-    for (uint32_t i = tid; i < d * kHotTab; i += kExThreads) s_tab[i] = a.hot_tab[i];
-    for (uint32_t i = tid; i < a.g.nbins_all; i += kExThreads) s_hist[i] = 0;
-    for (uint32_t i = tid; i < NS; i += kExThreads) {
+    for (uint32_t i = tid; i < d * kHotTab; i += NT) s_tab[i] = a.hot_tab[i];
+    for (uint32_t i = tid; i < a.g.nbins_all; i += NT) s_hist[i] = 0;
+    for (uint32_t i = tid; i < NS; i += NT) {
         const uint32_t id = a.hot_ids[i];
         const uint64_t cell = (uint64_t)(i / kHot) * a.g.w + id;
         s_hFc[i] = id != GNS_ID_NONE ? a.Fc[cell] : GNS_ID_NONE;
@@ -408,7 +417,7 @@ __global__ __launch_bounds__(kExThreads, GNS_EX_MINW) void k_extract(ExtractArgs
 #pragma unroll
             for (int i = 0; i < 4; i++) { cw[4 * i] = hv[i].x; cw[4 * i + 1] = hv[i].y; cw[4 * i + 2] = hv[i].z; cw[4 * i + 3] = hv[i].w; }
             szq = hsz;
-            load_hdr(q + kExThreads);
+            load_hdr(q + NT);
             if (okq) {
                 uint32_t tw[10];
                 const int st = parse_record_fast(cw, szq, true, tw);
@@ -433,11 +442,11 @@ __global__ __launch_bounds__(kExThreads, GNS_EX_MINW) void k_extract(ExtractArgs
         uint32_t kwc[GNS_KWMAX], slotc, szc;
         uint4 r4c[4];
         stage_b(beg + tid, okc, kwc, slotc, r4c, szc);
-        for (uint64_t p0 = beg; p0 < end; p0 += kExThreads) {  // wave-uniform trip count
+        for (uint64_t p0 = beg; p0 < end; p0 += NT) {  // wave-uniform trip count
             bool okn = false;
             uint32_t kwn[GNS_KWMAX], slotn = 0, szn = 0;
             uint4 r4n[4];
-            if (p0 + kExThreads < end) stage_b(p0 + kExThreads + tid, okn, kwn, slotn, r4n, szn);
+            if (p0 + NT < end) stage_b(p0 + NT + tid, okn, kwn, slotn, r4n, szn);
             k1_consume<RMAX>(a, S, K, d, bw, p0 + tid, beg, okc, kwc, slotc, r4c, szc, n_ok);
             okc = okn; slotc = slotn; szc = szn;
 #pragma unroll
@@ -446,7 +455,7 @@ __global__ __launch_bounds__(kExThreads, GNS_EX_MINW) void k_extract(ExtractArgs
             for (int i = 0; i < 4; i++) r4c[i] = r4n[i];
         }
     } else {
-        for (uint64_t p0 = beg; p0 < end; p0 += kExThreads) {  // wave-uniform trip count
+        for (uint64_t p0 = beg; p0 < end; p0 += NT) {  // wave-uniform trip count
             const uint64_t p = p0 + tid;
             bool ok = p < end;
             uint32_t kw[GNS_KWMAX];
@@ -475,8 +484,8 @@ __global__ __launch_bounds__(kExThreads, GNS_EX_MINW) void k_extract(ExtractArgs
     }
     atomicAdd(&s_ok, n_ok);
     __syncthreads();
-    for (uint32_t i = tid; i < a.g.nbins_all; i += kExThreads) a.hist[(uint64_t)i * a.nblk + blk] = s_hist[i];
-    for (uint32_t i = tid; i < NS; i += kExThreads) {
+    for (uint32_t i = tid; i < a.g.nbins_all; i += NT) a.hist[(uint64_t)i * a.nblk + blk] = s_hist[i];
+    for (uint32_t i = tid; i < NS; i += NT) {
         HotSum hs;
         hs.n = s_hist[a.g.nbins + i]; hs.nfc = s_nfc[i]; hs.nfs = s_nfs[i]; hs.smax = s_smax[i];
         hs.os = s_os[i]; hs.fs = s_fs[i];
@@ -945,6 +954,7 @@ struct ApplyArgs {
     const uint64_t *ovf;
     CmGeom g;
     uint32_t *C, *Fc, *S, *Fs;
+    uint32_t *work;             // persistent-schedule counter (zeroed before the launch)
 };
 
 // accN per bucket and chunk: n [0,14) | n_foreign_count [14,28) | n_foreign_size
@@ -1100,20 +1110,68 @@ __device__ __forceinline__ void replay_group(ApplyLds &L, bool pending, uint32_t
     }
 }
 
+// A tile's bucket state in registers (kTileMax / kApThreads buckets per thread):
+// the next tile is loaded while the current one is stored, so a workgroup's
+// tile loads and stores overlap instead of alternating.
+constexpr uint32_t kTilePer = kTileMax / kApThreads;
+static_assert(kTileMax % kApThreads == 0, "tile = whole items per thread");
+constexpr uint64_t kNoTile = ~0ull;
+struct TilePre {
+    uint32_t c[kTilePer], fc[kTilePer], s[kTilePer], fs[kTilePer];
+    uint64_t cbase;
+};
+
+__device__ __forceinline__ void tile_fetch(const ApplyArgs &a, TilePre &pre, uint64_t cbase, uint32_t tn) {
+    pre.cbase = cbase;
+#pragma unroll
+    for (uint32_t m = 0; m < kTilePer; m++) {
+        // unconditional (clamped) loads: every register is written on every path, so
+        // the old values die at the tile fill and no wait precedes the loads
+        const uint32_t i = min(threadIdx.x + m * kApThreads, tn - 1u);
+        pre.c[m] = a.C[cbase + i]; pre.fc[m] = a.Fc[cbase + i];
+        pre.s[m] = a.S[cbase + i]; pre.fs[m] = a.Fs[cbase + i];
+    }
+}
+
+__device__ __forceinline__ void tile_none(TilePre &pre) {
+    pre.cbase = kNoTile;
+#pragma unroll
+    for (uint32_t m = 0; m < kTilePer; m++) { pre.c[m] = 0; pre.fc[m] = 0; pre.s[m] = 0; pre.fs[m] = 0; }
+}
+
 // Updates ent[beg, end) (stream order) of one LDS tile: buckets cbase .. cbase+tn-1.
+// pre holds this tile's state if it was prefetched (pre.cbase == cbase); on
+// return it holds the state of the tile at next_cbase (kNoTile: none), loaded
+// after this tile's stores were issued.
 __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, const uint64_t *ent, uint32_t beg,
-                                           uint32_t end, uint64_t cbase, uint32_t tn, uint32_t col0) {
+                                           uint32_t end, uint64_t cbase, uint32_t tn, uint32_t col0,
+                                           TilePre &pre, uint64_t next_cbase, uint32_t next_tn) {
     uint32_t *sC = L.sC, *sFc = L.sFc, *sS = L.sS, *sFs = L.sFs;
     unsigned long long *accN = L.accN, *accS = L.accS;
     uint16_t *s_list = L.s_list;
     uint32_t *s_wc = L.s_wc;
     uint32_t &s_any = L.s_any, &s_nlist = L.s_nlist;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    for (uint32_t i = tid; i < tn; i += kApThreads) {
-        sC[i] = a.C[cbase + i]; sFc[i] = a.Fc[cbase + i];
-        sS[i] = a.S[cbase + i]; sFs[i] = a.Fs[cbase + i];
-        accN[i] = 0; accS[i] = 0;
+#ifdef GNS_K4_PROF
+    // phase cycles: 0 classify, 1 decide, 2 compact, 3 replay + loop, 4 tile load, 5 tile store
+    uint64_t pt[6] = {0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
+#define K4_MARK(i) do { if (tid == 0) { const uint64_t tn_ = __builtin_amdgcn_s_memtime(); pt[i] += tn_ - tprev; tprev = tn_; } } while (0)
+#else
+#define K4_MARK(i) do { } while (0)
+#endif
+    if (pre.cbase != cbase) tile_fetch(a, pre, cbase, tn);
+#pragma unroll
+    for (uint32_t m = 0; m < kTilePer; m++) {
+        const uint32_t i = tid + m * kApThreads;
+        if (i < tn) {
+            sC[i] = pre.c[m]; sFc[i] = pre.fc[m]; sS[i] = pre.s[m]; sFs[i] = pre.fs[m];
+            accN[i] = 0; accS[i] = 0;
+        }
     }
+#ifdef GNS_K4_PROF
+    __syncthreads();
+    K4_MARK(4);
+#endif
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint64_t e[kApItems], en[kApItems];
 #pragma unroll
@@ -1121,12 +1179,6 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
         const uint32_t q = beg + j * kApThreads + tid;
         e[j] = q < end ? ent[q] : 0ull;
     }
-#ifdef GNS_K4_PROF
-    uint64_t pt[4] = {0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
-#define K4_MARK(i) do { if (tid == 0) { const uint64_t tn_ = __builtin_amdgcn_s_memtime(); pt[i] += tn_ - tprev; tprev = tn_; } } while (0)
-#else
-#define K4_MARK(i) do { } while (0)
-#endif
     // engine counters in registers (global atomics inside the loop would be
     // drained by the next chunk's load waits)
     uint32_t st_chunks = 0, st_rep = 0, st_crep = 0;
@@ -1320,38 +1372,86 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
 #pragma unroll
         for (int j = 0; j < kApItems; j++) e[j] = en[j];
     }
+    // next tile's loads first, then this tile's stores: both are in flight together
+    if (next_cbase != kNoTile) tile_fetch(a, pre, next_cbase, next_tn);
+    else tile_none(pre);
+    for (uint32_t i = tid; i < tn; i += kApThreads) {
+        a.C[cbase + i] = sC[i]; a.Fc[cbase + i] = sFc[i];
+        a.S[cbase + i] = sS[i]; a.Fs[cbase + i] = sFs[i];
+    }
     if (tid == 0) {
         atomicAdd(&a.stats[5], (unsigned long long)st_rep);
         atomicAdd(&a.stats[6], (unsigned long long)st_chunks);
         if (st_crep) atomicAdd(&a.stats[7], (unsigned long long)st_crep);
     }
 #ifdef GNS_K4_PROF
-    if (tid == 0) for (int i = 0; i < 4; i++) atomicAdd(&a.stats[8 + i], (unsigned long long)pt[i]);
+    __syncthreads();
+    K4_MARK(5);
+    if (tid == 0) for (int i = 0; i < 6; i++) atomicAdd(&a.stats[8 + i], (unsigned long long)pt[i]);
 #endif
-    for (uint32_t i = tid; i < tn; i += kApThreads) {
-        a.C[cbase + i] = sC[i]; a.Fc[cbase + i] = sFc[i];
-        a.S[cbase + i] = sS[i]; a.Fs[cbase + i] = sFs[i];
-    }
 }
 
 // Super-bin (2^sub_bits tiles, C5-size widths): stable partition of the bin's
-// updates by tile into ent2[beg, end); L.s_soff[t] = start of tile t (relative).
+// updates by tile into ent2[beg, end); P.soff[t] = start of tile t (relative).
 struct SubLds {
-    uint32_t cnt[kApWaves][16];
     uint32_t base[16];
     uint32_t soff[17];
 };
+constexpr uint32_t kSubPairs = kApItems * kApWaves;  // (item, wave) groups of a round, in stream order
 
+// Two passes over the bin: per-tile totals (ballots), then rounds of kApChunk
+// updates in (item, wave, lane) = stream order: each (item, wave) group's
+// count per tile, one scan per tile over the groups, direct stores.  Two
+// barriers per round; cnt = 2 * kSubPairs * 16 words of LDS scratch (double
+// buffered), which the caller lends from the tile accumulators.
 __device__ __forceinline__ void sub_partition(const uint64_t *ent, uint64_t *ent2, uint32_t beg, uint32_t end,
-                                              uint32_t tile_bits, uint32_t sub_bits, SubLds &P) {
+                                              uint32_t tile_bits, uint32_t sub_bits, SubLds &P, uint32_t *cnt) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t nsub = 1u << sub_bits;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     if (tid < 16) P.base[tid] = 0;
-    for (uint32_t i = tid; i < kApWaves * 16; i += kApThreads) (&P.cnt[0][0])[i] = 0;
     __syncthreads();
-    for (uint32_t q = beg + tid; q < end; q += kApThreads)
-        atomicAdd(&P.base[((uint32_t)(ent[q] >> 32) & kLowMask) >> tile_bits], 1u);
+    {
+        // pass 1: per-tile totals; 8 entries per thread per step (16-byte loads,
+        // order does not matter here), counted in registers, one wave sum per tile
+        uint32_t c[16];
+#pragma unroll
+        for (uint32_t t = 0; t < 16; t++) c[t] = 0;
+        const uint32_t a0 = (beg + 1u) & ~1u;  // 16-byte aligned start (entries are 8 B)
+        if (a0 > beg && tid == 0) {
+            const uint32_t sb0 = ((uint32_t)(ent[beg] >> 32) & kLowMask) >> tile_bits;
+#pragma unroll
+            for (uint32_t t = 0; t < 16; t++) c[t] += sb0 == t ? 1u : 0u;
+        }
+        for (uint32_t q0 = a0 + tid * 8; q0 < end; q0 += kApThreads * 8) {
+            uint64_t v[8];
+            if (q0 + 8 <= end) {
+                const uint4 *p4 = reinterpret_cast<const uint4 *>(ent + q0);
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const uint4 x = p4[i];
+                    v[2 * i] = (uint64_t)x.y << 32 | x.x;
+                    v[2 * i + 1] = (uint64_t)x.w << 32 | x.z;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; i++) v[i] = q0 + i < end ? ent[q0 + i] : ~0ull;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const uint32_t sb = v[i] == ~0ull ? 0xFFu : (((uint32_t)(v[i] >> 32) & kLowMask) >> tile_bits);
+#pragma unroll
+                for (uint32_t t = 0; t < 16; t++) c[t] += (t < nsub && sb == t) ? 1u : 0u;
+            }
+        }
+#pragma unroll
+        for (uint32_t t = 0; t < 16; t++) {
+            if (t < nsub) {  // wave-uniform
+                const uint32_t tot = __ockl_wfred_add_u32(c[t]);
+                if (lane == 0 && tot) atomicAdd(&P.base[t], tot);
+            }
+        }
+    }
     __syncthreads();
     if (tid == 0) {
         uint32_t run = 0;
@@ -1359,57 +1459,135 @@ __device__ __forceinline__ void sub_partition(const uint64_t *ent, uint64_t *ent
         P.soff[nsub] = run;
     }
     __syncthreads();
-    for (uint32_t q0 = beg; q0 < end; q0 += kApThreads) {
-        const uint32_t q = q0 + tid;
-        const bool valid = q < end;
-        const uint64_t e = valid ? ent[q] : 0ull;
-        const uint32_t sub = valid ? (((uint32_t)(e >> 32) & kLowMask) >> tile_bits) : 0u;
-        uint64_t peers = __ballot(valid);
-        for (uint32_t bit = 0; bit < sub_bits; bit++) {
-            const uint64_t m = __ballot(valid && ((sub >> bit) & 1u));
-            peers &= ((sub >> bit) & 1u) ? m : ~m;
+    uint32_t par = 0;
+    for (uint32_t rb = beg; rb < end; rb += kApChunk) {
+        uint32_t *cb = cnt + par * (kSubPairs * 16);
+        par ^= 1u;
+        uint64_t e[kApItems];
+        uint32_t sub[kApItems], before[kApItems];
+#pragma unroll
+        for (int j = 0; j < kApItems; j++) {
+            const uint32_t q = rb + j * kApThreads + tid;
+            const bool valid = q < end;
+            e[j] = valid ? ent[q] : 0ull;
+            sub[j] = valid ? (((uint32_t)(e[j] >> 32) & kLowMask) >> tile_bits) : 0xFFu;
+            uint64_t peers = __ballot(valid);
+            for (uint32_t bit = 0; bit < sub_bits; bit++) {
+                const uint64_t m = __ballot(valid && ((sub[j] >> bit) & 1u));
+                peers &= ((sub[j] >> bit) & 1u) ? m : ~m;
+            }
+            before[j] = __popcll(peers & lt_mask);
+            // this wave's slots of group (j, wave): zeroed, then the first lane of
+            // each tile's peers writes the count (one wave: LDS ops stay in order)
+            if (lane < 16) cb[(j * kApWaves + wave) * 16 + lane] = 0;
+            if (valid && before[j] == 0) cb[(j * kApWaves + wave) * 16 + sub[j]] = (uint32_t)__popcll(peers);
         }
-        const uint32_t before = __popcll(peers & lt_mask);
-        if (valid && before == 0) P.cnt[wave][sub] = __popcll(peers);
         __syncthreads();
-        if (valid) {
-            uint32_t pre = 0;
-            for (uint32_t w2 = 0; w2 < wave; w2++) pre += P.cnt[w2][sub];
-            ent2[beg + P.base[sub] + pre + before] = e;
+        if (wave < nsub) {  // wave t: exclusive scan of tile t's group counts -> absolute slots
+            static_assert(kSubPairs == 128, "two groups per lane");
+            const uint32_t t = wave;
+            const uint32_t x0 = cb[(2 * lane) * 16 + t], x1 = cb[(2 * lane + 1) * 16 + t];
+            const uint32_t b0 = P.base[t];
+            const uint32_t inc = wave_incl_scan(x0 + x1);
+            const uint32_t ex = b0 + inc - (x0 + x1);
+            cb[(2 * lane) * 16 + t] = ex;
+            cb[(2 * lane + 1) * 16 + t] = ex + x0;
+            if (lane == 63) P.base[t] = b0 + inc;
         }
         __syncthreads();
-        if (tid < nsub) {
-            uint32_t tot = 0;
-            for (uint32_t w2 = 0; w2 < (uint32_t)kApWaves; w2++) tot += P.cnt[w2][tid];
-            P.base[tid] += tot;
-        }
-        __syncthreads();
-        for (uint32_t i = tid; i < kApWaves * 16; i += kApThreads) (&P.cnt[0][0])[i] = 0;
-        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kApItems; j++)
+            if (sub[j] != 0xFFu) ent2[beg + cb[(j * kApWaves + wave) * 16 + sub[j]] + before[j]] = e[j];
     }
+    __syncthreads();
+}
+
+// Persistent: each workgroup takes bins from the size-ordered schedule through
+// a work counter, one bin ahead, so the next tile's state can be loaded while
+// the current tile is stored.
+struct ApplyTile {
+    uint32_t beg, end;  // update range in the bin (super-bin: sub-partitioned later)
+    uint32_t r, bbase;  // row, first bucket of the bin
+    bool valid;
+};
+
+__device__ __forceinline__ ApplyTile apply_bin(const ApplyArgs &a, uint32_t k) {
+    ApplyTile t{};
+    t.valid = false;
+    if (k >= a.g.nbins) return t;
+    const uint32_t bin = a.order ? a.order[k] : k;
+    t.beg = a.offsets[(uint64_t)bin * a.nblk];
+    t.end = (bin + 1 < a.g.nbins_all) ? a.offsets[(uint64_t)(bin + 1) * a.nblk] : *a.total;
+    t.r = bin / a.g.ntiles;
+    t.bbase = (bin % a.g.ntiles) << a.g.bin_bits;
+    t.valid = true;
+    return t;
 }
 
 __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
     __shared__ ApplyLds L;
     __shared__ SubLds P;
+    __shared__ uint32_t s_k;
     const CmGeom &g = a.g;
-    const uint32_t bin = a.order ? a.order[blockIdx.x] : blockIdx.x;
-    const uint32_t beg = a.offsets[(uint64_t)bin * a.nblk];
-    const uint32_t end = (bin + 1 < g.nbins_all) ? a.offsets[(uint64_t)(bin + 1) * a.nblk] : *a.total;
-    if (beg >= end) return;
-    const uint32_t r = bin / g.ntiles, t = bin % g.ntiles;
-    const uint32_t bbase = t << g.bin_bits;
-    if (g.sub_bits == 0) {
-        apply_tile(a, L, a.entries, beg, end, (uint64_t)r * g.w + bbase, min(1u << g.tile_bits, g.w - bbase), bbase);
-        return;
-    }
-    sub_partition(a.entries, a.entries2, beg, end, g.tile_bits, g.sub_bits, P);
-    for (uint32_t st = 0; st < (1u << g.sub_bits); st++) {
-        const uint32_t tbase = bbase + (st << g.tile_bits);
-        const uint32_t sb = beg + P.soff[st], se = beg + P.soff[st + 1];
-        if (tbase >= g.w || sb >= se) continue;
-        apply_tile(a, L, a.entries2, sb, se, (uint64_t)r * g.w + tbase, min(1u << g.tile_bits, g.w - tbase), tbase);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t tw = 1u << g.tile_bits;
+    TilePre pre;
+    tile_none(pre);
+    if (tid == 0) s_k = atomicAdd(a.work, 1u);
+    __syncthreads();
+    uint32_t k = s_k;
+    __syncthreads();
+    while (k < g.nbins) {
+        if (tid == 0) s_k = atomicAdd(a.work, 1u);  // the bin after this one
+        const ApplyTile cur = apply_bin(a, k);
         __syncthreads();
+        const uint32_t kn = s_k;
+        const ApplyTile nxt = apply_bin(a, kn);
+        // first tile of the next bin (its state is prefetched; a super-bin's first
+        // tile may turn out empty, which only wastes that prefetch)
+        uint64_t nb_cbase = kNoTile;
+        uint32_t nb_tn = 0;
+        if (nxt.valid && nxt.beg < nxt.end && nxt.bbase < g.w) {
+            nb_cbase = (uint64_t)nxt.r * g.w + nxt.bbase;
+            nb_tn = min(tw, g.w - nxt.bbase);
+        }
+        if (cur.beg < cur.end) {
+            if (g.sub_bits == 0) {
+                apply_tile(a, L, a.entries, cur.beg, cur.end, (uint64_t)cur.r * g.w + cur.bbase,
+                           min(tw, g.w - cur.bbase), cur.bbase, pre, nb_cbase, nb_tn);
+            } else {
+#ifdef GNS_K4_PROF
+                const uint64_t t_sp = __builtin_amdgcn_s_memtime();
+#endif
+                sub_partition(a.entries, a.entries2, cur.beg, cur.end, g.tile_bits, g.sub_bits, P,
+                              reinterpret_cast<uint32_t *>(L.accN));
+#ifdef GNS_K4_PROF
+                if (tid == 0) atomicAdd(&a.stats[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_sp));
+#endif
+                const uint32_t nsub = 1u << g.sub_bits;
+                for (uint32_t st = 0; st < nsub; st++) {
+                    const uint32_t tbase = cur.bbase + (st << g.tile_bits);
+                    const uint32_t sb = cur.beg + P.soff[st], se = cur.beg + P.soff[st + 1];
+                    if (tbase >= g.w || sb >= se) continue;
+                    // next tile: the next non-empty tile of this bin, else the next bin's first
+                    uint64_t ncb = nb_cbase;
+                    uint32_t ntn = nb_tn;
+                    for (uint32_t s2 = st + 1; s2 < nsub; s2++) {
+                        const uint32_t tb2 = cur.bbase + (s2 << g.tile_bits);
+                        if (tb2 < g.w && P.soff[s2] < P.soff[s2 + 1]) {
+                            ncb = (uint64_t)cur.r * g.w + tb2;
+                            ntn = min(tw, g.w - tb2);
+                            break;
+                        }
+                    }
+                    apply_tile(a, L, a.entries2, sb, se, (uint64_t)cur.r * g.w + tbase, min(tw, g.w - tbase), tbase,
+                               pre, ncb, ntn);
+                    __syncthreads();
+                }
+            }
+        }
+        __syncthreads();
+        k = kn;
     }
 }
 
@@ -1769,10 +1947,26 @@ __global__ __launch_bounds__(256) void k_hot_hist(const uint32_t *C, CmGeom g, u
     __shared__ uint32_t s[8 * kHotKeys];
     for (uint32_t i = threadIdx.x; i < g.d * kHotKeys; i += 256) s[i] = 0;
     __syncthreads();
-    const uint64_t cells = (uint64_t)g.d * g.w;
-    for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += (uint64_t)gridDim.x * 256) {
-        const uint32_t v = C[c];
-        if (v >= (1u << (kHotMinBits - 1))) atomicAdd(&s[(c / g.w) * kHotKeys + hot_key(v)], 1u);
+    // row by row (no per-cell division), 16-byte loads when the row is whole words of 4
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint32_t r = 0; r < g.d; r++) {
+        const uint32_t *Cr = C + (uint64_t)r * g.w;
+        uint32_t *sr = s + r * kHotKeys;
+        if ((g.w & 3u) == 0) {
+            const uint4 *C4 = reinterpret_cast<const uint4 *>(Cr);
+            for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < g.w / 4; c += stride) {
+                const uint4 v = C4[c];
+                if (v.x >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v.x)], 1u);
+                if (v.y >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v.y)], 1u);
+                if (v.z >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v.z)], 1u);
+                if (v.w >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v.w)], 1u);
+            }
+        } else {
+            for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < g.w; c += stride) {
+                const uint32_t v = Cr[c];
+                if (v >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v)], 1u);
+            }
+        }
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < g.d * kHotKeys; i += 256) if (s[i]) atomicAdd(&hh[i], s[i]);
@@ -1798,13 +1992,24 @@ __global__ void k_hot_pick(uint32_t *hh, CmGeom g, uint32_t *thr, uint32_t *hcnt
 
 __global__ __launch_bounds__(256) void k_hot_collect(const uint32_t *C, CmGeom g, const uint32_t *thr,
                                                       uint32_t *hcnt, uint32_t *hot_ids) {
-    const uint64_t cells = (uint64_t)g.d * g.w;
-    for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < cells; c += (uint64_t)gridDim.x * 256) {
-        const uint32_t v = C[c];
-        const uint32_t r = (uint32_t)(c / g.w);
-        if (v >= (1u << (kHotMinBits - 1)) && hot_key(v) >= thr[r]) {
-            const uint32_t q = atomicAdd(&hcnt[r], 1u);
-            if (q < kHot) hot_ids[r * kHot + q] = (uint32_t)(c - (uint64_t)r * g.w);
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint32_t r = 0; r < g.d; r++) {
+        const uint32_t *Cr = C + (uint64_t)r * g.w;
+        const uint32_t t = thr[r];
+        auto take = [&](uint32_t v, uint64_t c) {
+            if (v >= (1u << (kHotMinBits - 1)) && hot_key(v) >= t) {
+                const uint32_t q = atomicAdd(&hcnt[r], 1u);
+                if (q < kHot) hot_ids[r * kHot + q] = (uint32_t)c;
+            }
+        };
+        if ((g.w & 3u) == 0) {
+            const uint4 *C4 = reinterpret_cast<const uint4 *>(Cr);
+            for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < g.w / 4; c += stride) {
+                const uint4 v = C4[c];
+                take(v.x, 4 * c); take(v.y, 4 * c + 1); take(v.z, 4 * c + 2); take(v.w, 4 * c + 3);
+            }
+        } else {
+            for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < g.w; c += stride) take(Cr[c], c);
         }
     }
 }
@@ -1925,6 +2130,39 @@ __global__ void k_fill_u32(uint32_t *p, uint64_t n, uint32_t v) {
 // ===========================================================================
 using namespace gns;
 
+// Grow-only device buffers of the read side (heavy hitters, queries, id -> key
+// bytes): no allocation or free -- hipFree synchronizes the device -- once
+// warm, so a snapshot view can query while the handle ingests.
+struct CmScratch {
+    uint64_t *cand = nullptr;
+    uint32_t *ncand = nullptr;
+    uint32_t cap = 0;
+    uint32_t *ids = nullptr;
+    uint64_t ids_n = 0;
+    uint8_t *bytes = nullptr;
+    uint64_t bytes_n = 0;
+    uint8_t *qkeys = nullptr;
+    uint64_t qkeys_n = 0;
+    uint64_t *qout = nullptr;
+    uint64_t qout_n = 0;
+    void free_all() {
+        dfree(cand); dfree(ncand); dfree(ids); dfree(bytes); dfree(qkeys); dfree(qout);
+        cand = nullptr; ncand = nullptr; ids = nullptr; bytes = nullptr; qkeys = nullptr; qout = nullptr;
+        cap = 0; ids_n = bytes_n = qkeys_n = qout_n = 0;
+    }
+};
+
+template <typename T>
+static int grow_buf(T **p, uint64_t &have, uint64_t need) {
+    if (need <= have && *p) return GNS_OK;
+    dfree(*p);
+    *p = nullptr;
+    have = 0;
+    GNS_TRY(dalloc(reinterpret_cast<void **>(p), std::max<uint64_t>(need, 1) * sizeof(T)));
+    have = need;
+    return GNS_OK;
+}
+
 struct gns_cm {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1932,8 +2170,8 @@ struct gns_cm {
     KeyPlanN kp{};
     uint32_t K = 0, st = 0, ct = 0;
     uint32_t *C = nullptr, *S = nullptr, *Fc = nullptr, *Fs = nullptr;
-    uint64_t *hh_cand = nullptr;  // heavy-hitter candidates (allocated at the first query, kept)
-    uint32_t *hh_n = nullptr;
+    CmScratch rd;                 // read-side buffers of the handle's own queries (grow-only)
+    std::atomic<uint32_t> period{0};  // bumped by reset: snapshot views taken before it are stale
     DictDev D{};
     uint64_t dict_slots = 0;
     uint32_t epoch = 0;
@@ -1954,6 +2192,8 @@ struct gns_cm {
     uint32_t *hflag = nullptr, *hhist = nullptr, *hthr = nullptr, *hcnt = nullptr;
     HotSum *hsum = nullptr;               // [d*kHot][nblk_max]
     uint32_t *hflag2 = nullptr;           // [d*kHot + 2]: flags, then hany, nchk
+    uint32_t *work = nullptr;             // K4 schedule counter
+    uint32_t ncu = 256;                   // compute units (K4 persistent grid)
     uint32_t *hres = nullptr;             // [d*kHot][2]
     uint4 *chk = nullptr;                 // [kChkCap]
     bool warm = false;                    // a batch has run since create/reset
@@ -1983,12 +2223,13 @@ int set_dev(gns_cm *cm) {
 }
 
 int cm_free_all(gns_cm *cm) {
-    dfree(cm->C); dfree(cm->S); dfree(cm->Fc); dfree(cm->Fs); dfree(cm->hh_cand); dfree(cm->hh_n);
+    dfree(cm->C); dfree(cm->S); dfree(cm->Fc); dfree(cm->Fs); cm->rd.free_all();
     dfree(cm->D.rec);
     dfree(cm->keyid); dfree(cm->idx);
     dfree(cm->pend[0]); dfree(cm->pend[1]); dfree(cm->pcnt[0]); dfree(cm->pcnt[1]);
     dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
     dfree(cm->entries); dfree(cm->entries2); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats); dfree(cm->stage);
+    dfree(cm->work);
     dfree(cm->hot_ids); dfree(cm->segtot); dfree(cm->hflag); dfree(cm->hhist); dfree(cm->hthr); dfree(cm->hcnt);
     dfree(cm->hsum); dfree(cm->hflag2); dfree(cm->hres); dfree(cm->chk); dfree(cm->hot_tab);
     if (cm->h_pin) (void)hipHostFree(cm->h_pin);
@@ -2035,16 +2276,23 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.stats = cm->stats;
         ScopedStage st(cm->timer, 0);
         const size_t lds = extract_lds_bytes(g.nbins_all, g.d);
-        if (cm->K == 37 && g.d == 4)
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 4>), dim3(nblk), dim3(kExThreads), lds, s, a);
+        if (lds > kExLdsSmall) {  // deep / wide sketch: one 1024-thread block per CU
+            if (cm->K == 37)
+                hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 0, 1024>), dim3(nblk), dim3(1024), lds, s, a);
+            else if (cm->K == 16)
+                hipLaunchKernelGGL((k_extract<KIND, MODE, 16, 0, 1024>), dim3(nblk), dim3(1024), lds, s, a);
+            else
+                hipLaunchKernelGGL((k_extract<KIND, MODE, 0, 0, 1024>), dim3(nblk), dim3(1024), lds, s, a);
+        } else if (cm->K == 37 && g.d == 4)
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 4, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
         else if (cm->K == 37)
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 0>), dim3(nblk), dim3(kExThreads), lds, s, a);
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 0, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
         else if (cm->K == 16 && g.d == 4)
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 16, 4>), dim3(nblk), dim3(kExThreads), lds, s, a);
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 16, 4, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
         else if (cm->K == 16)
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 16, 0>), dim3(nblk), dim3(kExThreads), lds, s, a);
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 16, 0, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
         else
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 0, 0>), dim3(nblk), dim3(kExThreads), lds, s, a);
+            hipLaunchKernelGGL((k_extract<KIND, MODE, 0, 0, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
         GNS_HIP(hipGetLastError());
     }
     // K1b: resolve parked packets until none remain
@@ -2107,9 +2355,11 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.stats = cm->stats;
         a.entries = cm->entries; a.entries2 = cm->entries2; a.offsets = cm->hist; a.nblk = nblk; a.nbins = g.nbins;
         a.total = cm->total; a.order = ordered ? cm->order : nullptr; a.ovf = cm->ovf; a.g = g;
-        a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs;
+        a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs; a.work = cm->work;
+        GNS_HIP(hipMemsetAsync(cm->work, 0, 4, s));
         ScopedStage st(cm->timer, 4);
-        hipLaunchKernelGGL(k_apply, dim3(g.nbins), dim3(kApThreads), 0, s, a);
+        // persistent: one workgroup per CU (the tile LDS fills a CU), bins from the schedule counter
+        hipLaunchKernelGGL(k_apply, dim3(std::min(g.nbins, cm->ncu)), dim3(kApThreads), 0, s, a);
         GNS_HIP(hipGetLastError());
     }
     // hot bins: chip-wide aggregate, exact decide, in-order fallback
@@ -2148,10 +2398,9 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
     // designate the next batch's hot buckets from the counters
     {
         ScopedStage st(cm->timer, 7);
-        const uint64_t cells = (uint64_t)g.d * g.w;
-        const unsigned grid = (unsigned)std::min<uint64_t>(2048, (cells + 255) / 256);
+        const unsigned grid = (unsigned)std::min<uint64_t>(2048, ((uint64_t)g.w / 4 + 255) / 256 + 1);
         // few blocks for the histogram: its flush is one global atomic per (block, nonzero class)
-        hipLaunchKernelGGL(k_hot_hist, dim3(std::min(grid, 256u)), dim3(256), 0, s, cm->C, g, cm->hhist);
+        hipLaunchKernelGGL(k_hot_hist, dim3(std::min(grid, 512u)), dim3(256), 0, s, cm->C, g, cm->hhist);
         hipLaunchKernelGGL(k_hot_pick, dim3(1), dim3(512), 0, s, cm->hhist, g, cm->hthr, cm->hcnt, cm->hot_ids);
         hipLaunchKernelGGL(k_hot_collect, dim3(grid), dim3(256), 0, s, cm->C, g, cm->hthr, cm->hcnt, cm->hot_ids);
         hipLaunchKernelGGL(k_hot_table, dim3(1), dim3(1024), 0, s, g, cm->hot_ids, cm->hot_tab);
@@ -2288,6 +2537,11 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             set_error("hipStreamCreate failed"); rc = GNS_E_HIP; break;
         }
         cm->timer.stream = cm->stream;
+        {
+            int ncu = 0;
+            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cm->device) == hipSuccess && ncu > 0)
+                cm->ncu = (uint32_t)ncu;
+        }
         const uint64_t cells = (uint64_t)g.d * g.w;
         if ((rc = dalloc_t(&cm->C, cells)) || (rc = dalloc_t(&cm->S, cells)) ||
             (rc = dalloc_t(&cm->Fc, cells)) || (rc = dalloc_t(&cm->Fs, cells)))
@@ -2321,7 +2575,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (rc = dalloc_t(&cm->order, g.nbins)) || (rc = dalloc_t(&cm->entries, cm->bmax * g.d)) ||
             (g.sub_bits && (rc = dalloc_t(&cm->entries2, cm->bmax * g.d))) ||
             (rc = dalloc_t(&cm->ovf, kOvfCap)) || (rc = dalloc_t(&cm->ovf_cnt, 1)) ||
-            (rc = dalloc_t(&cm->stats, 16)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
+            (rc = dalloc_t(&cm->stats, 16)) || (rc = dalloc_t(&cm->work, 4)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
             (rc = dalloc_t(&cm->segtot, (size_t)g.d * kHot * kHotSegs * 2)) || (rc = dalloc_t(&cm->hflag, g.d * kHot)) ||
             (rc = dalloc_t(&cm->hhist, g.d * kHotKeys)) || (rc = dalloc_t(&cm->hthr, 8)) || (rc = dalloc_t(&cm->hcnt, 8)) ||
             (rc = dalloc_t(&cm->hsum, (uint64_t)g.d * kHot * cm->nblk_max)) ||
@@ -2413,43 +2667,54 @@ int gns_cm_flush(gns_cm *cm) {
     return GNS_OK;
 }
 
+}  // extern "C"
+
+// Query (count_min.go:160-174) of host keys against state (C, Fc, S, Fs) on stream st.
+static int cm_query_impl(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_t *C, const uint32_t *Fc,
+                         const uint32_t *S, const uint32_t *Fs, const uint8_t *keys, uint32_t stride, uint64_t n,
+                         uint64_t *out) {
+    GNS_TRY(grow_buf(&sc.qkeys, sc.qkeys_n, n * stride));
+    GNS_TRY(grow_buf(&sc.qout, sc.qout_n, n));
+    QueryArgs a{};
+    a.keys = sc.qkeys; a.stride = stride; a.aligned = (stride % 4 == 0 && stride >= ((cm->K + 3) & ~3u));
+    a.n = n; a.K = cm->K; a.g = cm->g; a.D = cm->D;
+    a.C = C; a.Fc = Fc; a.S = S; a.Fs = Fs; a.out = sc.qout;
+    hipError_t e = hipMemcpyAsync(sc.qkeys, keys, n * stride, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_query, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out, sc.qout, n * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { set_error("query: %s", hipGetErrorString(e)); return GNS_E_HIP; }
+    return GNS_OK;
+}
+
+extern "C" {
+
 int gns_cm_query(gns_cm *cm, const uint8_t *keys, uint32_t stride, uint64_t n, uint64_t *out) {
     if (!cm || (n && (!keys || !out))) { set_error("null argument"); return GNS_E_ARG; }
     if (n == 0) return GNS_OK;
     if (stride < cm->K) { set_error("stride < key_bytes"); return GNS_E_ARG; }
     GNS_TRY(set_dev(cm));
-    uint8_t *dk = nullptr;
-    uint64_t *dout = nullptr;
-    GNS_TRY(dalloc(reinterpret_cast<void **>(&dk), n * stride));
-    int rc = dalloc(reinterpret_cast<void **>(&dout), n * 8);
-    if (rc != GNS_OK) { dfree(dk); return rc; }
-    QueryArgs a{};
-    a.keys = dk; a.stride = stride; a.aligned = (stride % 4 == 0 && stride >= ((cm->K + 3) & ~3u));
-    a.n = n; a.K = cm->K; a.g = cm->g; a.D = cm->D;
-    a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs; a.out = dout;
-    hipError_t e = hipMemcpyAsync(dk, keys, n * stride, hipMemcpyHostToDevice, cm->stream);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_query, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, cm->stream, a);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, cm->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(cm->stream);
-    dfree(dk);
-    dfree(dout);
-    if (e != hipSuccess) { set_error("query: %s", hipGetErrorString(e)); return GNS_E_HIP; }
-    return GNS_OK;
+    return cm_query_impl(cm, cm->stream, cm->rd, cm->C, cm->Fc, cm->S, cm->Fs, keys, stride, n, out);
 }
 
-static int cm_ids_to_host_bytes(gns_cm *cm, const uint32_t *d_ids, uint64_t n, uint8_t *host) {
+// ids -> key bytes on stream `st`: through the grow-only scratch when small
+// (heavy-hitter lists), a temporary buffer for whole-state exports.
+static int cm_ids_to_host_bytes(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_t *d_ids, uint64_t n,
+                                uint8_t *host) {
     if (n == 0 || cm->K == 0) return GNS_OK;
+    const uint64_t nb = n * cm->K;
+    const bool tmp = nb > (64ull << 20);
     uint8_t *d = nullptr;
-    GNS_TRY(dalloc(reinterpret_cast<void **>(&d), n * cm->K));
-    hipLaunchKernelGGL(k_ids_to_bytes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, cm->stream,
-                       d_ids, n, cm->D, d);
+    if (tmp) GNS_TRY(dalloc(reinterpret_cast<void **>(&d), nb));
+    else { GNS_TRY(grow_buf(&sc.bytes, sc.bytes_n, nb)); d = sc.bytes; }
+    hipLaunchKernelGGL(k_ids_to_bytes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_ids, n, cm->D, d);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(host, d, n * cm->K, hipMemcpyDeviceToHost, cm->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(cm->stream);
-    dfree(d);
+    if (e == hipSuccess) e = hipMemcpyAsync(host, d, nb, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (tmp) dfree(d);
     if (e != hipSuccess) { set_error("ids_to_bytes: %s", hipGetErrorString(e)); return GNS_E_HIP; }
     return GNS_OK;
 }
@@ -2461,44 +2726,45 @@ int gns_cm_export_state(gns_cm *cm, uint32_t *C, uint32_t *S, uint8_t *FPc, uint
     const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
     if (C) GNS_HIP(hipMemcpy(C, cm->C, cells * 4, hipMemcpyDeviceToHost));
     if (S) GNS_HIP(hipMemcpy(S, cm->S, cells * 4, hipMemcpyDeviceToHost));
-    if (FPc) GNS_TRY(cm_ids_to_host_bytes(cm, cm->Fc, cells, FPc));
-    if (FPs) GNS_TRY(cm_ids_to_host_bytes(cm, cm->Fs, cells, FPs));
+    if (FPc) GNS_TRY(cm_ids_to_host_bytes(cm, cm->stream, cm->rd, cm->Fc, cells, FPc));
+    if (FPs) GNS_TRY(cm_ids_to_host_bytes(cm, cm->stream, cm->rd, cm->Fs, cells, FPs));
     return GNS_OK;
 }
 
 // HeavyHitters (count_min.go:178-247): a flow's max over its buckets reaches the
 // threshold iff one of its buckets does, so only cells >= threshold are
 // candidates; dedupe by fingerprint keeping the max; sort value desc.
-static int cm_heavy_one(gns_cm *cm, const uint32_t *val, const uint32_t *fp, uint32_t thr,
-                        uint8_t *flows, uint32_t *vals, uint64_t *n_io) {
+static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_t *val, const uint32_t *fp,
+                        uint32_t thr, uint8_t *flows, uint32_t *vals, uint64_t *n_io) {
     const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
     const uint32_t cap = (uint32_t)std::min<uint64_t>(cells, 1ull << 26);
-    if (!cm->hh_cand || !cm->hh_n) {  // both or neither: a failed second allocation leaves neither
-        dfree(cm->hh_cand); dfree(cm->hh_n);
-        cm->hh_cand = nullptr; cm->hh_n = nullptr;
+    if (!sc.cand || !sc.ncand) {  // both or neither: a failed second allocation leaves neither
+        dfree(sc.cand); dfree(sc.ncand);
+        sc.cand = nullptr; sc.ncand = nullptr;
         uint64_t *c = nullptr;
         uint32_t *nn = nullptr;
         GNS_TRY(dalloc(reinterpret_cast<void **>(&c), (uint64_t)cap * 8));
         if (int rc = dalloc(reinterpret_cast<void **>(&nn), 16)) { dfree(c); return rc; }
-        cm->hh_cand = c; cm->hh_n = nn;
+        sc.cand = c; sc.ncand = nn; sc.cap = cap;
     }
-    uint64_t *cand = cm->hh_cand;
-    uint32_t *ncand = cm->hh_n;
+    uint64_t *cand = sc.cand;
+    uint32_t *ncand = sc.ncand;
     int rc = GNS_OK;
     std::vector<uint64_t> h;
     uint32_t nc = 0;
-    hipError_t e = hipMemsetAsync(ncand, 0, 4, cm->stream);
+    hipError_t e = hipMemsetAsync(ncand, 0, 4, st);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_hh_candidates, dim3((unsigned)((cells + 256 * kHhItems - 1) / (256 * kHhItems))), dim3(256), 0, cm->stream,
+        hipLaunchKernelGGL(k_hh_candidates, dim3((unsigned)((cells + 256 * kHhItems - 1) / (256 * kHhItems))), dim3(256), 0, st,
                            val, fp, cells, thr, cand, ncand, cap);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(&nc, ncand, 4, hipMemcpyDeviceToHost, cm->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(cm->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&nc, ncand, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess && nc) {
         nc = std::min(nc, cap);
         h.resize(nc);
-        e = hipMemcpy(h.data(), cand, (uint64_t)nc * 8, hipMemcpyDeviceToHost);
+        e = hipMemcpyAsync(h.data(), cand, (uint64_t)nc * 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
     }
     if (e != hipSuccess) { set_error("heavy: %s", hipGetErrorString(e)); return GNS_E_HIP; }
     // dedupe by id keeping max value
@@ -2515,11 +2781,10 @@ static int cm_heavy_one(gns_cm *cm, const uint32_t *val, const uint32_t *fp, uin
     for (size_t i = 0; i < u.size(); i++) ids[i] = (uint32_t)u[i];
     std::vector<uint8_t> kb(u.size() * (K ? K : 1));
     if (!u.empty() && K) {
-        uint32_t *dids = nullptr;
-        GNS_TRY(dalloc(reinterpret_cast<void **>(&dids), ids.size() * 4));
-        e = hipMemcpy(dids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice);
-        rc = e == hipSuccess ? cm_ids_to_host_bytes(cm, dids, ids.size(), kb.data()) : GNS_E_HIP;
-        dfree(dids);
+        GNS_TRY(grow_buf(&sc.ids, sc.ids_n, ids.size()));
+        e = hipMemcpyAsync(sc.ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) { set_error("heavy: %s", hipGetErrorString(e)); return GNS_E_HIP; }
+        rc = cm_ids_to_host_bytes(cm, st, sc, sc.ids, ids.size(), kb.data());
         if (rc) return rc;
     }
     std::vector<uint32_t> perm(u.size());
@@ -2543,15 +2808,118 @@ int gns_cm_heavy_hitters(gns_cm *cm, uint8_t *count_flows, uint32_t *counts, uin
     if (!cm || !n_count || !n_size) { set_error("null argument"); return GNS_E_ARG; }
     GNS_TRY(set_dev(cm));
     GNS_HIP(hipStreamSynchronize(cm->stream));
-    GNS_TRY(cm_heavy_one(cm, cm->C, cm->Fc, cm->ct, count_flows, counts, n_count));
-    GNS_TRY(cm_heavy_one(cm, cm->S, cm->Fs, cm->st, size_flows, sizes, n_size));
+    GNS_TRY(cm_heavy_one(cm, cm->stream, cm->rd, cm->C, cm->Fc, cm->ct, count_flows, counts, n_count));
+    GNS_TRY(cm_heavy_one(cm, cm->stream, cm->rd, cm->S, cm->Fs, cm->st, size_flows, sizes, n_size));
     return GNS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Snapshot views: heavy hitters and queries concurrent with ingest
+// (BASELINE configs[4]; the reference's snapshotter reads the live buckets
+// while workers insert, manager.go:139-159 -- here the read side sees a
+// consistent state taken at a point of the insert stream instead).
+// ---------------------------------------------------------------------------
+struct gns_cm_view {
+    gns_cm *cm = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ready = nullptr;
+    uint32_t *C = nullptr, *S = nullptr, *Fc = nullptr, *Fs = nullptr;
+    CmScratch rd;
+    std::mutex mu;          // refresh vs queries: a refresh waits for the query in progress
+    uint32_t period = ~0u;  // handle period of the snapshot (~0: never refreshed)
+};
+
+static void view_free(gns_cm_view *v) {
+    dfree(v->C); dfree(v->S); dfree(v->Fc); dfree(v->Fs);
+    v->rd.free_all();
+    if (v->ready) (void)hipEventDestroy(v->ready);
+    if (v->stream) (void)hipStreamDestroy(v->stream);
+}
+
+int gns_cm_view_create(gns_cm *cm, gns_cm_view **out) {
+    if (!cm || !out) { set_error("null argument"); return GNS_E_ARG; }
+    *out = nullptr;
+    GNS_TRY(set_dev(cm));
+    gns_cm_view *v = new gns_cm_view();
+    v->cm = cm;
+    const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
+    int rc = GNS_OK;
+    do {
+        if ((rc = dalloc_t(&v->C, cells)) || (rc = dalloc_t(&v->S, cells)) || (rc = dalloc_t(&v->Fc, cells)) ||
+            (rc = dalloc_t(&v->Fs, cells)))
+            break;
+        if (hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&v->ready, hipEventDisableTiming) != hipSuccess) {
+            set_error("view stream/event"); rc = GNS_E_HIP; break;
+        }
+    } while (0);
+    if (rc) { view_free(v); delete v; return rc; }
+    *out = v;
+    return GNS_OK;
+}
+
+int gns_cm_view_destroy(gns_cm_view *v) {
+    if (!v) return GNS_OK;
+    (void)hipSetDevice(v->cm->device);
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (v->stream) (void)hipStreamSynchronize(v->stream);
+    view_free(v);
+    delete v;
+    return GNS_OK;
+}
+
+int gns_cm_view_refresh(gns_cm_view *v) {
+    if (!v) { set_error("null argument"); return GNS_E_ARG; }
+    gns_cm *cm = v->cm;
+    GNS_TRY(set_dev(cm));
+    std::lock_guard<std::mutex> lk(v->mu);  // no view query is reading the snapshot
+    const uint64_t bytes = (uint64_t)cm->g.d * cm->g.w * 4;
+    // copies on the handle's stream: the snapshot is the state after every insert
+    // issued so far and before any later one; the view's stream waits for it
+    GNS_HIP(hipMemcpyAsync(v->C, cm->C, bytes, hipMemcpyDeviceToDevice, cm->stream));
+    GNS_HIP(hipMemcpyAsync(v->S, cm->S, bytes, hipMemcpyDeviceToDevice, cm->stream));
+    GNS_HIP(hipMemcpyAsync(v->Fc, cm->Fc, bytes, hipMemcpyDeviceToDevice, cm->stream));
+    GNS_HIP(hipMemcpyAsync(v->Fs, cm->Fs, bytes, hipMemcpyDeviceToDevice, cm->stream));
+    GNS_HIP(hipEventRecord(v->ready, cm->stream));
+    GNS_HIP(hipStreamWaitEvent(v->stream, v->ready, 0));
+    v->period = cm->period.load();
+    return GNS_OK;
+}
+
+static int view_check(gns_cm_view *v) {
+    if (v->period == ~0u) { set_error("view never refreshed"); return GNS_E_ARG; }
+    if (v->period != v->cm->period.load()) { set_error("view is stale: the handle was reset; refresh it"); return GNS_E_ARG; }
+    return GNS_OK;
+}
+
+int gns_cm_view_heavy_hitters(gns_cm_view *v, uint8_t *count_flows, uint32_t *counts, uint64_t *n_count,
+                              uint8_t *size_flows, uint32_t *sizes, uint64_t *n_size) {
+    if (!v || !n_count || !n_size) { set_error("null argument"); return GNS_E_ARG; }
+    gns_cm *cm = v->cm;
+    GNS_TRY(set_dev(cm));
+    std::lock_guard<std::mutex> lk(v->mu);
+    GNS_TRY(view_check(v));
+    GNS_TRY(cm_heavy_one(cm, v->stream, v->rd, v->C, v->Fc, cm->ct, count_flows, counts, n_count));
+    GNS_TRY(cm_heavy_one(cm, v->stream, v->rd, v->S, v->Fs, cm->st, size_flows, sizes, n_size));
+    return GNS_OK;
+}
+
+int gns_cm_view_query(gns_cm_view *v, const uint8_t *keys, uint32_t stride, uint64_t n, uint64_t *out) {
+    if (!v || (n && (!keys || !out))) { set_error("null argument"); return GNS_E_ARG; }
+    if (n == 0) return GNS_OK;
+    gns_cm *cm = v->cm;
+    if (stride < cm->K) { set_error("stride < key_bytes"); return GNS_E_ARG; }
+    GNS_TRY(set_dev(cm));
+    std::lock_guard<std::mutex> lk(v->mu);
+    GNS_TRY(view_check(v));
+    return cm_query_impl(cm, v->stream, v->rd, v->C, v->Fc, v->S, v->Fs, keys, stride, n, out);
 }
 
 int gns_cm_reset(gns_cm *cm) {
     if (!cm) return GNS_E_ARG;
     GNS_TRY(set_dev(cm));
     GNS_TRY(cm_reset_state(cm));
+    cm->period.fetch_add(1);
     GNS_HIP(hipStreamSynchronize(cm->stream));
     return GNS_OK;
 }
@@ -2589,9 +2957,10 @@ int gns_cm_counters(gns_cm *cm, uint64_t out[8]) {
     for (int i = 5; i < 8; i++) out[i] = h[i];
     return GNS_OK;
 #endif
-#ifdef GNS_K4_PROF  // profiling build: K4 phase cycles (classify, decide, compact, replay), chunks, ...
-    for (int i = 0; i < 4; i++) out[i] = h[8 + i];
-    for (int i = 4; i < 8; i++) out[i] = h[i + 1];
+#ifdef GNS_K4_PROF  // profiling build: K4 phase cycles (classify, decide, compact, replay, tile load,
+                    // tile store, sub-partition), chunks
+    for (int i = 0; i < 7; i++) out[i] = h[8 + i];
+    out[7] = h[6];
 #else
     for (int i = 0; i < 8; i++) out[i] = h[i];
 #endif

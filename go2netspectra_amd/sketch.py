@@ -80,6 +80,74 @@ def _seeds_arg(seeds, depth):
     return arr, arr.ctypes.data
 
 
+def _cm_heavy_arrays(fn, h, key_bytes):
+    """Two-call protocol of gns_cm_heavy_hitters / gns_cm_view_heavy_hitters: sizes, then lists."""
+    nc, ns = ct.c_uint64(0), ct.c_uint64(0)
+    check(fn(h, None, None, ct.byref(nc), None, None, ct.byref(ns)))
+    K = max(key_bytes, 1)
+    cf = np.zeros((max(nc.value, 1), K), np.uint8)
+    cv = np.zeros(max(nc.value, 1), np.uint32)
+    sf = np.zeros((max(ns.value, 1), K), np.uint8)
+    sv = np.zeros(max(ns.value, 1), np.uint32)
+    nc2, ns2 = ct.c_uint64(nc.value), ct.c_uint64(ns.value)
+    check(fn(h, cf.ctypes.data, cv.ctypes.data, ct.byref(nc2), sf.ctypes.data, sv.ctypes.data, ct.byref(ns2)))
+    m, q = min(nc.value, nc2.value), min(ns.value, ns2.value)
+    return cf[:m], cv[:m], sf[:q], sv[:q]
+
+
+def _cm_heavy_record(arrays, key_bytes) -> "HeavyRecord":
+    cf, cv, sf, sv = arrays
+    kb = key_bytes
+    return HeavyRecord(Size=[HeavySize(bytes(sf[i, :kb]), int(sv[i])) for i in range(len(sv))],
+                       Count=[HeavyCount(bytes(cf[i, :kb]), int(cv[i])) for i in range(len(cv))])
+
+
+class CountMinView:
+    """Snapshot of a CountMin taken at a point of its insert stream (refresh()),
+    queried from any thread while the handle keeps inserting: the read side of
+    BASELINE configs[4] ("queries concurrent with ingest").  The reference's
+    snapshotter reads live buckets under concurrent inserts (manager.go:139-159);
+    a view answers exactly what the handle would have answered at the refresh."""
+
+    def __init__(self, cm: "CountMin"):
+        self._L = cm._L
+        self._cm = cm
+        self.key_bytes = cm.key_bytes
+        h = ct.c_void_p()
+        check(self._L.gns_cm_view_create(cm._h, ct.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.gns_cm_view_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def refresh(self) -> None:
+        """Ingest side: snapshot the state after every insert issued so far (asynchronous)."""
+        check(self._L.gns_cm_view_refresh(self._h))
+
+    def heavy_hitters_arrays(self):
+        return _cm_heavy_arrays(self._L.gns_cm_view_heavy_hitters, self._h, self.key_bytes)
+
+    def heavy_hitters(self) -> "HeavyRecord":
+        return _cm_heavy_record(self.heavy_hitters_arrays(), self.key_bytes)
+
+    def query_many(self, keys) -> np.ndarray:
+        keys = _host(keys, np.uint8)
+        n = keys.shape[0]
+        out = np.zeros(n, dtype=np.uint64)
+        if n:
+            keys = keys.reshape(n, -1)
+            check(self._L.gns_cm_view_query(self._h, keys.ctypes.data, keys.shape[1], n, out.ctypes.data))
+        return out
+
+
 class CountMin:
     """Fingerprinted majority-vote "CountMin" of count_min.go on one GPU.
 
@@ -179,34 +247,15 @@ class CountMin:
     def heavy_hitters_arrays(self):
         """HeavyHitters as arrays (count flows [n,K], counts, size flows, sizes): the
         snapshot handed to a writer without building per-flow Python objects."""
-        nc, ns = ct.c_uint64(0), ct.c_uint64(0)
-        check(self._L.gns_cm_heavy_hitters(self._h, None, None, ct.byref(nc), None, None, ct.byref(ns)))
-        K = max(self.key_bytes, 1)
-        cf = np.zeros((max(nc.value, 1), K), np.uint8)
-        cv = np.zeros(max(nc.value, 1), np.uint32)
-        sf = np.zeros((max(ns.value, 1), K), np.uint8)
-        sv = np.zeros(max(ns.value, 1), np.uint32)
-        nc2, ns2 = ct.c_uint64(nc.value), ct.c_uint64(ns.value)
-        check(self._L.gns_cm_heavy_hitters(self._h, cf.ctypes.data, cv.ctypes.data, ct.byref(nc2),
-                                           sf.ctypes.data, sv.ctypes.data, ct.byref(ns2)))
-        m, q = min(nc.value, nc2.value), min(ns.value, ns2.value)
-        return cf[:m], cv[:m], sf[:q], sv[:q]
+        return _cm_heavy_arrays(self._L.gns_cm_heavy_hitters, self._h, self.key_bytes)
 
     def heavy_hitters(self) -> HeavyRecord:
-        nc, ns = ct.c_uint64(0), ct.c_uint64(0)
-        check(self._L.gns_cm_heavy_hitters(self._h, None, None, ct.byref(nc), None, None, ct.byref(ns)))
-        K = max(self.key_bytes, 1)
-        cf = np.zeros((max(nc.value, 1), K), np.uint8)
-        cv = np.zeros(max(nc.value, 1), np.uint32)
-        sf = np.zeros((max(ns.value, 1), K), np.uint8)
-        sv = np.zeros(max(ns.value, 1), np.uint32)
-        nc2, ns2 = ct.c_uint64(nc.value), ct.c_uint64(ns.value)
-        check(self._L.gns_cm_heavy_hitters(self._h, cf.ctypes.data, cv.ctypes.data, ct.byref(nc2),
-                                           sf.ctypes.data, sv.ctypes.data, ct.byref(ns2)))
-        kb = self.key_bytes
-        return HeavyRecord(
-            Size=[HeavySize(bytes(sf[i, :kb]), int(sv[i])) for i in range(min(ns.value, ns2.value))],
-            Count=[HeavyCount(bytes(cf[i, :kb]), int(cv[i])) for i in range(min(nc.value, nc2.value))])
+        return _cm_heavy_record(self.heavy_hitters_arrays(), self.key_bytes)
+
+    def view(self) -> "CountMinView":
+        """A snapshot view whose heavy hitters / queries run concurrently with
+        this handle's inserts (gns_cm_view_*); refresh() it at window boundaries."""
+        return CountMinView(self)
 
     def reset(self) -> None:
         check(self._L.gns_cm_reset(self._h))

@@ -151,6 +151,28 @@ int gns_cm_set_timing(gns_cm *cm, int on);
 int gns_cm_stage_times(gns_cm *cm, double ms[8], uint64_t launches[8], int reset);
 void *gns_cm_stream(gns_cm *cm); /* hipStream_t the handle launches on */
 
+/* Snapshot view: heavy hitters and queries CONCURRENT with ingest (BASELINE
+ * configs[4]; the reference's snapshotter and alerter call Task.Snapshot ->
+ * HeavyHitters while the workers insert, manager.go:139-159, task.go:177).
+ *   - gns_cm_view_refresh is an ingest-side call (serialized with the handle's
+ *     other calls): it copies the bucket state, in insert order, at the current
+ *     end of the insert stream (a window boundary), asynchronously on the
+ *     handle's stream.
+ *   - gns_cm_view_heavy_hitters / gns_cm_view_query may run on any other
+ *     thread while the handle keeps inserting; they run on the view's own
+ *     stream and see exactly the state at the last refresh (same results as
+ *     gns_cm_heavy_hitters / gns_cm_query called at that point).
+ *   - A refresh waits for a view call in progress; after gns_cm_reset the view
+ *     answers GNS_E_ARG until it is refreshed.  Destroy views before their handle.
+ * Memory: 16 bytes per bucket (depth*width) for the snapshot. */
+typedef struct gns_cm_view gns_cm_view;
+int gns_cm_view_create(gns_cm *cm, gns_cm_view **out);
+int gns_cm_view_destroy(gns_cm_view *v);
+int gns_cm_view_refresh(gns_cm_view *v);
+int gns_cm_view_heavy_hitters(gns_cm_view *v, uint8_t *count_flows, uint32_t *counts, uint64_t *n_count,
+                              uint8_t *size_flows, uint32_t *sizes, uint64_t *n_size);
+int gns_cm_view_query(gns_cm_view *v, const uint8_t *keys, uint32_t stride, uint64_t n, uint64_t *out);
+
 /* ------------------------------------------------------------------ */
 /* SuperSpread (super_spread.go)                                      */
 /* ------------------------------------------------------------------ */

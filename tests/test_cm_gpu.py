@@ -339,3 +339,58 @@ def test_full_dictionary_is_cleared_by_reset(gpu, oracle):
         orc.insert_keys(small, sizes)
     cm.flush()
     assert_same_state(cm, orc)
+
+
+def test_view_answers_the_state_at_refresh_while_ingesting(gpu, oracle):
+    """configs[4] read side: heavy hitters and queries of a snapshot view run on
+    another thread while the handle keeps inserting, and equal the oracle at the
+    refresh point (count_min.go:160-247), not at whatever the ingest reached."""
+    import threading
+    from go2netspectra_amd import GnsError
+    rng = np.random.default_rng(21)
+    cm, orc = make_pair(oracle, 8192, 4, 16, st=20_000, ct=50)
+    keys, flows, _ = zipf_keys(rng, 600_000, 30_000, 16)
+    sizes = sizes_u32(rng, 600_000)
+    a, b = 200_000, 600_000
+    cm.insert_keys(keys[:a], sizes[:a])
+    orc.insert_keys(keys[:a], sizes[:a])
+    want_q = np.array([orc.query(bytes(f)) for f in flows[:3000]], dtype=np.uint64)
+    want_c, want_s = orc.heavy("count"), orc.heavy("size")
+    view = cm.view()
+    with pytest.raises(GnsError):
+        view.heavy_hitters()          # never refreshed
+    view.refresh()                    # state after packets [0, a)
+    results, errors = [], []
+
+    def reader():
+        try:
+            for _ in range(6):
+                hh = view.heavy_hitters()
+                results.append(([(h.Flow, h.Count) for h in hh.Count], [(h.Flow, h.Size) for h in hh.Size],
+                                view.query_many(flows[:3000])))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    t = threading.Thread(target=reader)
+    t.start()
+    for lo in range(a, b, 50_000):   # ingest continues while the reader runs
+        cm.insert_keys(keys[lo:lo + 50_000], sizes[lo:lo + 50_000])
+    t.join()
+    assert not errors, errors
+    assert len(results) == 6
+    for c, s, q in results:
+        assert c == want_c and s == want_s
+        assert np.array_equal(q, want_q)
+    orc.insert_keys(keys[a:b], sizes[a:b])
+    view.refresh()                    # now the whole stream
+    hh = view.heavy_hitters()
+    assert [(h.Flow, h.Count) for h in hh.Count] == orc.heavy("count")
+    assert [(h.Flow, h.Size) for h in hh.Size] == orc.heavy("size")
+    cm.flush()
+    assert_same_state(cm, orc)
+    cm.reset()
+    with pytest.raises(GnsError):
+        view.query_many(flows[:10])   # stale after reset until refreshed
+    view.refresh()
+    assert not view.query_many(flows[:10]).any()
+    view.close()
