@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "gns_common.hpp"
+#include <rocprim/rocprim.hpp>
 
 namespace gns {
 
@@ -77,7 +78,6 @@ constexpr int kApWaves = kApThreads / 64;
 constexpr int kApItems = GNS_AP_ITEMS;
 constexpr uint32_t kApChunk = kApThreads * kApItems; // 8192 updates per K4 step
 static_assert((uint64_t)kApChunk * (kSizeEsc - 1) < (1ull << 32), "K4 per-chunk size sums must fit 32 bits");
-constexpr uint32_t kScanSeg = 4096;
 #ifndef GNS_HOT_BITS
 #define GNS_HOT_BITS 7
 #endif
@@ -161,7 +161,7 @@ struct ExtractArgs {
     uint64_t *pend;      // per-block regions of kChunk
     uint32_t *pend_cnt;  // [nblk]
     uint32_t *pend_total;
-    uint32_t *hist;      // [nbins_all][nblk]
+    uint32_t *hist;      // [nblk][nbins_all] (block-major)
     uint32_t nblk;
     const uint32_t *hot_ids;  // [d][kHot]
     const uint32_t *hot_tab;  // [d][kHotTab] lookup groups (k_hot_table)
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : 1) void k_extract(Ext
     }
     atomicAdd(&s_ok, n_ok);
     __syncthreads();
-    for (uint32_t i = tid; i < a.g.nbins_all; i += NT) a.hist[(uint64_t)i * a.nblk + blk] = s_hist[i];
+    for (uint32_t i = tid; i < a.g.nbins_all; i += NT) a.hist[(uint64_t)blk * a.g.nbins_all + i] = s_hist[i];
     for (uint32_t i = tid; i < NS; i += NT) {
         HotSum hs;
         hs.n = s_hist[a.g.nbins + i]; hs.nfc = s_nfc[i]; hs.nfs = s_nfs[i]; hs.smax = s_smax[i];
@@ -560,99 +560,86 @@ __global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// K2: exclusive scan (three phases) of hist[nbins*nblk] in place.
+// K2: exclusive scan of the per-block bin histograms (block-major), in place.
 // ---------------------------------------------------------------------------
 extern "C" __device__ unsigned __ockl_wfscan_add_u32(unsigned, bool);
 // DPP inclusive scan over the whole wave (call with all 64 lanes active)
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) { return __ockl_wfscan_add_u32(v, true); }
 
-// block (256 threads) exclusive scan; returns exclusive prefix, *total = sum
-__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *s_w, uint32_t *total) {
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t inc = wave_incl_scan(v);
+// K2 over the block-major histogram hist[blk][bin] (K1 flushes one contiguous
+// row per block, K3 loads one): offsets[blk][bin] = (updates of all bins
+// before `bin`) + (updates of `bin` in blocks before `blk`), in place.  Blocks
+// are taken in groups of kTGrp: group sums, a per-bin scan over the groups,
+// a scan over the bins, then each group's run.  Threads of a wave hold
+// consecutive bins, so every pass reads whole rows.
+constexpr uint32_t kTGrp = 32;
+
+__global__ __launch_bounds__(256) void k_tscan_part(const uint32_t *hist, uint32_t nblk, uint32_t nbins,
+                                                    uint32_t *part) {
+    const uint32_t bin = blockIdx.x * 256 + threadIdx.x, g = blockIdx.y;
+    if (bin >= nbins) return;
+    const uint32_t b0 = g * kTGrp, b1 = min(nblk, b0 + kTGrp);
+    uint32_t sum = 0;
+#pragma unroll 8
+    for (uint32_t b = b0; b < b1; b++) sum += hist[(uint64_t)b * nbins + bin];
+    part[(uint64_t)g * nbins + bin] = sum;
+}
+
+__global__ __launch_bounds__(256) void k_tscan_mid(uint32_t *part, uint32_t ngrp, uint32_t nbins, uint32_t *tot) {
+    const uint32_t bin = blockIdx.x * 256 + threadIdx.x;
+    if (bin >= nbins) return;
+    uint32_t run = 0;
+    for (uint32_t g = 0; g < ngrp; g++) {
+        const uint32_t v = part[(uint64_t)g * nbins + bin];
+        part[(uint64_t)g * nbins + bin] = run;
+        run += v;
+    }
+    tot[bin] = run;
+}
+
+// exclusive scan of the bin totals (nbins <= 8 * 1024), one 1024-thread block
+__global__ __launch_bounds__(1024) void k_tscan_bins(uint32_t *tot, uint32_t nbins, uint32_t *total) {
+    __shared__ uint32_t s_w[16];
+    constexpr uint32_t PER = 8;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    uint32_t v[PER], sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < PER; i++) {
+        const uint32_t b = tid * PER + i;
+        v[i] = b < nbins ? tot[b] : 0u;
+        sum += v[i];
+    }
+    const uint32_t inc = wave_incl_scan(sum);
     if (lane == 63) s_w[wave] = inc;
     __syncthreads();
-    uint32_t base = 0, tot = 0;
+    uint32_t base = 0, all = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < 4; w++) {
+    for (uint32_t w = 0; w < 16; w++) {
         const uint32_t x = s_w[w];
         if (w < wave) base += x;
-        tot += x;
+        all += x;
     }
-    __syncthreads();
-    *total = tot;
-    return base + inc - v;
+    uint32_t run = base + inc - sum;
+#pragma unroll
+    for (uint32_t i = 0; i < PER; i++) {
+        const uint32_t b = tid * PER + i;
+        if (b < nbins) tot[b] = run;
+        run += v[i];
+    }
+    if (tid == 0) *total = all;
 }
 
-__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t *x, uint64_t N, uint32_t *part) {
-    __shared__ uint32_t s_w[4];
-    const uint64_t base = (uint64_t)blockIdx.x * kScanSeg;
-    uint32_t sum = 0;
-    if (base + kScanSeg <= N) {
-        const uint4 *x4 = reinterpret_cast<const uint4 *>(x + base);
-        uint4 v[kScanSeg / 1024];
-#pragma unroll
-        for (uint32_t j = 0; j < kScanSeg / 1024; j++) v[j] = x4[threadIdx.x + 256 * j];
-#pragma unroll
-        for (uint32_t j = 0; j < kScanSeg / 1024; j++) sum += v[j].x + v[j].y + v[j].z + v[j].w;
-    } else {
-        for (uint32_t i = threadIdx.x; i < kScanSeg; i += 256)
-            if (base + i < N) sum += x[base + i];
-    }
-    uint32_t tot;
-    (void)block_excl_scan256(sum, s_w, &tot);
-    if (threadIdx.x == 0) part[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(256) void k_scan_parts(uint32_t *part, uint32_t nseg, uint32_t *total) {
-    __shared__ uint32_t s_w[4];
-    // each thread scans a contiguous run of ceil(nseg/256) parts
-    const uint32_t per = (nseg + 255) / 256;
-    const uint32_t b0 = threadIdx.x * per;
-    uint32_t sum = 0;
-    for (uint32_t i = 0; i < per; i++)
-        if (b0 + i < nseg) sum += part[b0 + i];
-    uint32_t tot;
-    uint32_t run = block_excl_scan256(sum, s_w, &tot);
-    for (uint32_t i = 0; i < per; i++)
-        if (b0 + i < nseg) { const uint32_t v = part[b0 + i]; part[b0 + i] = run; run += v; }
-    if (threadIdx.x == 0) *total = tot;
-}
-
-__global__ __launch_bounds__(256) void k_scan_down(uint32_t *x, uint64_t N, const uint32_t *part) {
-    __shared__ uint32_t s_w[4];
-    const uint64_t base = (uint64_t)blockIdx.x * kScanSeg;
-    constexpr uint32_t per = kScanSeg / 256;  // 16 contiguous per thread
-    const uint64_t t0 = base + threadIdx.x * per;
-    static_assert(per == 16, "four 16-byte vectors per thread");
-    const bool full = t0 + per <= N;
-    uint32_t v[per];
-    if (full) {
-        const uint4 *x4 = reinterpret_cast<const uint4 *>(x + t0);
-#pragma unroll
-        for (uint32_t j = 0; j < 4; j++) {
-            const uint4 q = x4[j];
-            v[4 * j] = q.x; v[4 * j + 1] = q.y; v[4 * j + 2] = q.z; v[4 * j + 3] = q.w;
-        }
-    } else {
-#pragma unroll
-        for (uint32_t i = 0; i < per; i++) v[i] = (t0 + i < N) ? x[t0 + i] : 0u;
-    }
-    uint32_t sum = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < per; i++) sum += v[i];
-    uint32_t tot;
-    uint32_t run = block_excl_scan256(sum, s_w, &tot) + part[blockIdx.x];
-#pragma unroll
-    for (uint32_t i = 0; i < per; i++) { const uint32_t e = v[i]; v[i] = run; run += e; }
-    if (full) {
-        uint4 *x4 = reinterpret_cast<uint4 *>(x + t0);
-#pragma unroll
-        for (uint32_t j = 0; j < 4; j++) x4[j] = make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
-    } else {
-#pragma unroll
-        for (uint32_t i = 0; i < per; i++)
-            if (t0 + i < N) x[t0 + i] = v[i];
+__global__ __launch_bounds__(256) void k_tscan_down(uint32_t *hist, uint32_t nblk, uint32_t nbins,
+                                                    const uint32_t *part, const uint32_t *tot) {
+    const uint32_t bin = blockIdx.x * 256 + threadIdx.x, g = blockIdx.y;
+    if (bin >= nbins) return;
+    const uint32_t b0 = g * kTGrp, b1 = min(nblk, b0 + kTGrp);
+    uint32_t run = tot[bin] + part[(uint64_t)g * nbins + bin];
+    for (uint32_t b = b0; b < b1; b++) {
+        const uint64_t i = (uint64_t)b * nbins + bin;
+        const uint32_t v = hist[i];
+        hist[i] = run;
+        run += v;
     }
 }
 
@@ -721,7 +708,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
         const uint32_t r = i / LB, t = i % LB;
         const uint64_t gb = t < a.g.ntiles ? (uint64_t)(r * a.g.ntiles + t)
                                            : (uint64_t)(a.g.nbins + r * kHot + (t - a.g.ntiles));
-        s_goff[i] = a.offsets[gb * a.nblk + blk];
+        s_goff[i] = a.offsets[(uint64_t)blk * a.g.nbins_all + gb];
     }
     for (uint32_t t = tid; t < 2 * kScWaves * LB; t += kScThreads) s_cnt2[t] = 0;
     // bin codes of the next two (round, row) steps are in flight while a step
@@ -909,8 +896,8 @@ __global__ __launch_bounds__(1024) void k_order(const uint32_t *offsets, uint32_
     for (uint32_t k = threadIdx.x; k < NK; k += 1024) s_cnt[k] = 0;
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
-        const uint32_t s0 = offsets[(uint64_t)b * nblk];
-        const uint32_t s1 = (b + 1 < nall) ? offsets[(uint64_t)(b + 1) * nblk] : *total;
+        const uint32_t s0 = offsets[b];  // block 0's row: the start of every bin
+        const uint32_t s1 = (b + 1 < nall) ? offsets[b + 1] : *total;
         const uint32_t sz = s1 - s0;
         const uint32_t lz = __clz(sz);
         const uint32_t key = sz == 0 ? 0u : (32u - lz) * 8u + ((sz << lz) >> 28 & 7u);
@@ -1516,8 +1503,8 @@ __device__ __forceinline__ ApplyTile apply_bin(const ApplyArgs &a, uint32_t k) {
     t.valid = false;
     if (k >= a.g.nbins) return t;
     const uint32_t bin = a.order ? a.order[k] : k;
-    t.beg = a.offsets[(uint64_t)bin * a.nblk];
-    t.end = (bin + 1 < a.g.nbins_all) ? a.offsets[(uint64_t)(bin + 1) * a.nblk] : *a.total;
+    t.beg = a.offsets[bin];
+    t.end = (bin + 1 < a.g.nbins_all) ? a.offsets[bin + 1] : *a.total;
     t.r = bin / a.g.ntiles;
     t.bbase = (bin % a.g.ntiles) << a.g.bin_bits;
     t.valid = true;
@@ -1619,8 +1606,8 @@ struct HotArgs {
 
 __device__ __forceinline__ void hot_bin_range(const HotArgs &a, uint32_t hb, uint32_t &beg, uint32_t &end) {
     const uint32_t bin = a.g.nbins + hb;
-    beg = a.offsets[(uint64_t)bin * a.nblk];
-    end = (bin + 1 < a.g.nbins_all) ? a.offsets[(uint64_t)(bin + 1) * a.nblk] : *a.total;
+    beg = a.offsets[bin];
+    end = (bin + 1 < a.g.nbins_all) ? a.offsets[bin + 1] : *a.total;
 }
 
 __device__ __forceinline__ void hot_seg_range(uint32_t beg, uint32_t end, uint32_t sidx, uint32_t &sb,
@@ -2090,6 +2077,37 @@ __global__ __launch_bounds__(256) void k_ids_to_bytes(const uint32_t *ids, uint6
 // candidate: 0.59 ms per call at the bench geometry).  Order is irrelevant:
 // the host dedupes and sorts.
 constexpr uint32_t kHhItems = 8;
+// Device-side heavy-hitter list (count_min.go:178-247 HeavyHitters): candidates
+// (cells >= threshold) -> sort by (flow id, value desc) -> first entry per flow
+// (the flow's max over its buckets) -> sort by (value desc, first key bytes).
+__global__ __launch_bounds__(256) void k_hh_key(uint64_t *cand, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t c = cand[i];  // value << 32 | id
+    cand[i] = (uint64_t)(uint32_t)c << 32 | (uint32_t)~(uint32_t)(c >> 32);
+}
+
+__global__ __launch_bounds__(256) void k_hh_unique(const uint64_t *s, uint32_t n, uint32_t *uid, uint32_t *uval,
+                                                   uint32_t *nu) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t id = (uint32_t)(s[i] >> 32);
+    if (i > 0 && (uint32_t)(s[i - 1] >> 32) == id) return;
+    const uint32_t j = atomicAdd(nu, 1u);
+    uid[j] = id;
+    uval[j] = ~(uint32_t)s[i];
+}
+
+__global__ __launch_bounds__(256) void k_hh_order_key(const uint32_t *uval, const uint8_t *ub, uint32_t K,
+                                                      uint32_t n, uint64_t *key, uint32_t *idx) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    uint32_t be = 0;
+    for (uint32_t b = 0; b < 4; b++) be = be << 8 | (b < K ? ub[(uint64_t)j * K + b] : 0u);
+    key[j] = (uint64_t)(~uval[j]) << 32 | be;
+    idx[j] = j;
+}
+
 __global__ __launch_bounds__(256) void k_hh_candidates(const uint32_t *val, const uint32_t *fp,
                                                        uint64_t cells, uint32_t thr,
                                                        uint64_t *cand, uint32_t *ncand, uint32_t cap) {
@@ -2145,10 +2163,20 @@ struct CmScratch {
     uint64_t qkeys_n = 0;
     uint64_t *qout = nullptr;
     uint64_t qout_n = 0;
+    // device heavy-hitter sort: sorted candidates, unique (id, value), order keys / indices, rocPRIM temp
+    uint64_t *k64a = nullptr, *k64b = nullptr;
+    uint64_t k64a_n = 0, k64b_n = 0;
+    uint32_t *u32a = nullptr, *u32b = nullptr, *u32c = nullptr, *u32d = nullptr;
+    uint64_t u32a_n = 0, u32b_n = 0, u32c_n = 0, u32d_n = 0;
+    uint8_t *tmp = nullptr;
+    uint64_t tmp_n = 0;
     void free_all() {
         dfree(cand); dfree(ncand); dfree(ids); dfree(bytes); dfree(qkeys); dfree(qout);
+        dfree(k64a); dfree(k64b); dfree(u32a); dfree(u32b); dfree(u32c); dfree(u32d); dfree(tmp);
         cand = nullptr; ncand = nullptr; ids = nullptr; bytes = nullptr; qkeys = nullptr; qout = nullptr;
+        k64a = k64b = nullptr; u32a = u32b = u32c = u32d = nullptr; tmp = nullptr;
         cap = 0; ids_n = bytes_n = qkeys_n = qout_n = 0;
+        k64a_n = k64b_n = u32a_n = u32b_n = u32c_n = u32d_n = tmp_n = 0;
     }
 };
 
@@ -2321,13 +2349,15 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         cur ^= 1;
     }
     // K2
-    const uint64_t N = (uint64_t)g.nbins_all * nblk;
-    const uint32_t nseg = (uint32_t)((N + kScanSeg - 1) / kScanSeg);
     {
         ScopedStage st(cm->timer, 2);
-        hipLaunchKernelGGL(k_scan_reduce, dim3(nseg), dim3(256), 0, s, cm->hist, N, cm->part);
-        hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(256), 0, s, cm->part, nseg, cm->total);
-        hipLaunchKernelGGL(k_scan_down, dim3(nseg), dim3(256), 0, s, cm->hist, N, cm->part);
+        const uint32_t ngrp = (nblk + kTGrp - 1) / kTGrp;
+        const dim3 g2((g.nbins_all + 255) / 256, ngrp);
+        uint32_t *tot = cm->part + (size_t)ngrp * g.nbins_all;
+        hipLaunchKernelGGL(k_tscan_part, g2, dim3(256), 0, s, cm->hist, nblk, g.nbins_all, cm->part);
+        hipLaunchKernelGGL(k_tscan_mid, dim3((g.nbins_all + 255) / 256), dim3(256), 0, s, cm->part, ngrp, g.nbins_all, tot);
+        hipLaunchKernelGGL(k_tscan_bins, dim3(1), dim3(1024), 0, s, tot, g.nbins_all, cm->total);
+        hipLaunchKernelGGL(k_tscan_down, g2, dim3(256), 0, s, cm->hist, nblk, g.nbins_all, cm->part, tot);
         GNS_HIP(hipGetLastError());
     }
     // K3
@@ -2566,12 +2596,13 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         const uint64_t bcap = ((0xFFFFFFFFull / g.d) / kChunk) * kChunk;
         if (cm->bmax > bcap) cm->bmax = bcap;
         cm->nblk_max = (uint32_t)(cm->bmax / kChunk);
-        const uint64_t nseg = ((uint64_t)g.nbins_all * cm->nblk_max + kScanSeg - 1) / kScanSeg;
+        // K2 scratch: group sums [ngrp][nbins_all] + bin totals [nbins_all]
+        const uint64_t nscan = ((uint64_t)(cm->nblk_max + kTGrp - 1) / kTGrp + 2) * g.nbins_all;
         if ((rc = dalloc_t(&cm->keyid, cm->bmax)) || (rc = dalloc_t(&cm->idx, cm->bmax * g.d)) ||
             (rc = dalloc_t(&cm->pend[0], cm->bmax)) || (rc = dalloc_t(&cm->pend[1], cm->bmax)) ||
             (rc = dalloc_t(&cm->pcnt[0], cm->nblk_max)) || (rc = dalloc_t(&cm->pcnt[1], cm->nblk_max)) ||
             (rc = dalloc_t(&cm->ptotal, 2)) || (rc = dalloc_t(&cm->hist, (uint64_t)g.nbins_all * cm->nblk_max)) ||
-            (rc = dalloc_t(&cm->part, nseg + 1)) || (rc = dalloc_t(&cm->total, 1)) ||
+            (rc = dalloc_t(&cm->part, nscan)) || (rc = dalloc_t(&cm->total, 1)) ||
             (rc = dalloc_t(&cm->order, g.nbins)) || (rc = dalloc_t(&cm->entries, cm->bmax * g.d)) ||
             (g.sub_bits && (rc = dalloc_t(&cm->entries2, cm->bmax * g.d))) ||
             (rc = dalloc_t(&cm->ovf, kOvfCap)) || (rc = dalloc_t(&cm->ovf_cnt, 1)) ||
@@ -2749,8 +2780,6 @@ static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_
     }
     uint64_t *cand = sc.cand;
     uint32_t *ncand = sc.ncand;
-    int rc = GNS_OK;
-    std::vector<uint64_t> h;
     uint32_t nc = 0;
     hipError_t e = hipMemsetAsync(ncand, 0, 4, st);
     if (e == hipSuccess) {
@@ -2760,44 +2789,77 @@ static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_
     }
     if (e == hipSuccess) e = hipMemcpyAsync(&nc, ncand, 4, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e == hipSuccess && nc) {
-        nc = std::min(nc, cap);
-        h.resize(nc);
-        e = hipMemcpyAsync(h.data(), cand, (uint64_t)nc * 8, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-    }
     if (e != hipSuccess) { set_error("heavy: %s", hipGetErrorString(e)); return GNS_E_HIP; }
-    // dedupe by id keeping max value
-    std::sort(h.begin(), h.end(), [](uint64_t a, uint64_t b) {
-        const uint32_t ia = (uint32_t)a, ib = (uint32_t)b;
-        return ia != ib ? ia < ib : (a >> 32) > (b >> 32);
-    });
-    std::vector<uint64_t> u;
-    for (size_t i = 0; i < h.size(); i++)
-        if (i == 0 || (uint32_t)h[i] != (uint32_t)h[i - 1]) u.push_back(h[i]);
-    // fetch key bytes for the unique ids
-    const uint32_t K = cm->K;
-    std::vector<uint32_t> ids(u.size());
-    for (size_t i = 0; i < u.size(); i++) ids[i] = (uint32_t)u[i];
-    std::vector<uint8_t> kb(u.size() * (K ? K : 1));
-    if (!u.empty() && K) {
-        GNS_TRY(grow_buf(&sc.ids, sc.ids_n, ids.size()));
-        e = hipMemcpyAsync(sc.ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st);
-        if (e != hipSuccess) { set_error("heavy: %s", hipGetErrorString(e)); return GNS_E_HIP; }
-        rc = cm_ids_to_host_bytes(cm, st, sc, sc.ids, ids.size(), kb.data());
-        if (rc) return rc;
+    if (nc > cap) {
+        set_error("heavy hitters: %u buckets reach the threshold %u (more than %u candidates)", nc, thr, cap);
+        return GNS_E_RANGE;
     }
-    std::vector<uint32_t> perm(u.size());
-    for (size_t i = 0; i < perm.size(); i++) perm[i] = (uint32_t)i;
-    std::sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) {
-        const uint32_t vx = (uint32_t)(u[x] >> 32), vy = (uint32_t)(u[y] >> 32);
-        if (vx != vy) return vx > vy;
-        return memcmp(&kb[(size_t)x * K], &kb[(size_t)y * K], K) < 0;
-    });
+    const uint32_t K = cm->K;
+    // on the device: dedupe by flow keeping the max, then order by value desc
+    uint32_t nu = 0;
+    std::vector<uint32_t> order, uval;
+    std::vector<uint64_t> okey;
+    std::vector<uint8_t> kb;
+    if (nc) {
+        const unsigned g = (nc + 255) / 256;
+        GNS_TRY(grow_buf(&sc.k64a, sc.k64a_n, nc));
+        GNS_TRY(grow_buf(&sc.u32a, sc.u32a_n, nc));
+        GNS_TRY(grow_buf(&sc.u32b, sc.u32b_n, nc + 1));
+        hipLaunchKernelGGL(k_hh_key, dim3(g), dim3(256), 0, st, cand, nc);
+        size_t tb = 0;
+        if (rocprim::radix_sort_keys(nullptr, tb, cand, sc.k64a, (size_t)nc, 0u, 64u, st) != hipSuccess) {
+            set_error("heavy: radix sort size"); return GNS_E_HIP;
+        }
+        GNS_TRY(grow_buf(&sc.tmp, sc.tmp_n, tb));
+        if (rocprim::radix_sort_keys(sc.tmp, tb, cand, sc.k64a, (size_t)nc, 0u, 64u, st) != hipSuccess) {
+            set_error("heavy: radix sort"); return GNS_E_HIP;
+        }
+        uint32_t *d_nu = sc.u32b + nc;
+        GNS_HIP(hipMemsetAsync(d_nu, 0, 4, st));
+        hipLaunchKernelGGL(k_hh_unique, dim3(g), dim3(256), 0, st, sc.k64a, nc, sc.u32a, sc.u32b, d_nu);
+        GNS_HIP(hipMemcpyAsync(&nu, d_nu, 4, hipMemcpyDeviceToHost, st));
+        GNS_HIP(hipStreamSynchronize(st));
+    }
+    if (nu) {
+        const unsigned g = (nu + 255) / 256;
+        const uint32_t Kb = K ? K : 1;
+        GNS_TRY(grow_buf(&sc.bytes, sc.bytes_n, (uint64_t)nu * Kb));
+        GNS_TRY(grow_buf(&sc.k64b, sc.k64b_n, (uint64_t)nu * 2));
+        GNS_TRY(grow_buf(&sc.u32c, sc.u32c_n, (uint64_t)nu * 2));
+        if (K) hipLaunchKernelGGL(k_ids_to_bytes, dim3(g), dim3(256), 0, st, sc.u32a, (uint64_t)nu, cm->D, sc.bytes);
+        hipLaunchKernelGGL(k_hh_order_key, dim3(g), dim3(256), 0, st, sc.u32b, sc.bytes, K, nu, sc.k64b, sc.u32c);
+        size_t tb = 0;
+        uint64_t *ko = sc.k64b + nu;
+        uint32_t *io = sc.u32c + nu;
+        if (rocprim::radix_sort_pairs(nullptr, tb, sc.k64b, ko, sc.u32c, io, (size_t)nu, 0u, 64u, st) != hipSuccess) {
+            set_error("heavy: radix sort size"); return GNS_E_HIP;
+        }
+        GNS_TRY(grow_buf(&sc.tmp, sc.tmp_n, tb));
+        if (rocprim::radix_sort_pairs(sc.tmp, tb, sc.k64b, ko, sc.u32c, io, (size_t)nu, 0u, 64u, st) != hipSuccess) {
+            set_error("heavy: radix sort"); return GNS_E_HIP;
+        }
+        order.resize(nu); uval.resize(nu); okey.resize(nu); kb.resize((size_t)nu * Kb);
+        GNS_HIP(hipMemcpyAsync(order.data(), io, (uint64_t)nu * 4, hipMemcpyDeviceToHost, st));
+        GNS_HIP(hipMemcpyAsync(okey.data(), ko, (uint64_t)nu * 8, hipMemcpyDeviceToHost, st));
+        GNS_HIP(hipMemcpyAsync(uval.data(), sc.u32b, (uint64_t)nu * 4, hipMemcpyDeviceToHost, st));
+        if (K) GNS_HIP(hipMemcpyAsync(kb.data(), sc.bytes, (uint64_t)nu * K, hipMemcpyDeviceToHost, st));
+        GNS_HIP(hipStreamSynchronize(st));
+        // ties beyond the first four key bytes: order each run of equal sort keys by the full bytes
+        for (uint32_t i = 0; i < nu;) {
+            uint32_t j = i + 1;
+            while (j < nu && okey[j] == okey[i]) j++;
+            if (j - i > 1 && K > 4)
+                std::sort(order.begin() + i, order.begin() + j, [&](uint32_t x, uint32_t y) {
+                    return memcmp(&kb[(size_t)x * K], &kb[(size_t)y * K], K) < 0;
+                });
+            i = j;
+        }
+    }
+    std::vector<uint32_t> &perm = order;
     const uint64_t capn = *n_io;
     for (size_t i = 0; i < perm.size() && i < capn; i++) {
         if (flows && K) memcpy(flows + i * K, &kb[(size_t)perm[i] * K], K);
-        if (vals) vals[i] = (uint32_t)(u[perm[i]] >> 32);
+        if (vals) vals[i] = uval[perm[i]];
     }
     *n_io = perm.size();
     return GNS_OK;
@@ -2848,7 +2910,11 @@ int gns_cm_view_create(gns_cm *cm, gns_cm_view **out) {
         if ((rc = dalloc_t(&v->C, cells)) || (rc = dalloc_t(&v->S, cells)) || (rc = dalloc_t(&v->Fc, cells)) ||
             (rc = dalloc_t(&v->Fs, cells)))
             break;
-        if (hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess ||
+        // high priority: the read side's small launches are dispatched ahead of the
+        // ingest pipeline's queued workgroups (query latency under load)
+        int lo_pri = 0, hi_pri = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
+        if (hipStreamCreateWithPriority(&v->stream, hipStreamNonBlocking, hi_pri) != hipSuccess ||
             hipEventCreateWithFlags(&v->ready, hipEventDisableTiming) != hipSuccess) {
             set_error("view stream/event"); rc = GNS_E_HIP; break;
         }

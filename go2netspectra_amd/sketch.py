@@ -80,19 +80,25 @@ def _seeds_arg(seeds, depth):
     return arr, arr.ctypes.data
 
 
-def _cm_heavy_arrays(fn, h, key_bytes):
-    """Two-call protocol of gns_cm_heavy_hitters / gns_cm_view_heavy_hitters: sizes, then lists."""
-    nc, ns = ct.c_uint64(0), ct.c_uint64(0)
-    check(fn(h, None, None, ct.byref(nc), None, None, ct.byref(ns)))
+def _cm_heavy_arrays(fn, h, key_bytes, hint=None):
+    """gns_cm_heavy_hitters / gns_cm_view_heavy_hitters into buffers of the capacity
+    `hint` ([count, size], updated in place); a list longer than its buffer is
+    fetched again with the full length the first call reported."""
     K = max(key_bytes, 1)
-    cf = np.zeros((max(nc.value, 1), K), np.uint8)
-    cv = np.zeros(max(nc.value, 1), np.uint32)
-    sf = np.zeros((max(ns.value, 1), K), np.uint8)
-    sv = np.zeros(max(ns.value, 1), np.uint32)
-    nc2, ns2 = ct.c_uint64(nc.value), ct.c_uint64(ns.value)
-    check(fn(h, cf.ctypes.data, cv.ctypes.data, ct.byref(nc2), sf.ctypes.data, sv.ctypes.data, ct.byref(ns2)))
-    m, q = min(nc.value, nc2.value), min(ns.value, ns2.value)
-    return cf[:m], cv[:m], sf[:q], sv[:q]
+    hint = hint if hint is not None else [0, 0]
+    while True:
+        cc, cs = max(hint[0], 1), max(hint[1], 1)
+        cf = np.zeros((cc, K), np.uint8)
+        cv = np.zeros(cc, np.uint32)
+        sf = np.zeros((cs, K), np.uint8)
+        sv = np.zeros(cs, np.uint32)
+        nc, ns = ct.c_uint64(cc), ct.c_uint64(cs)
+        check(fn(h, cf.ctypes.data, cv.ctypes.data, ct.byref(nc), sf.ctypes.data, sv.ctypes.data, ct.byref(ns)))
+        if nc.value <= cc and ns.value <= cs:
+            # next call: room for some growth, so a window usually needs one call
+            hint[0], hint[1] = nc.value + nc.value // 4 + 16, ns.value + ns.value // 4 + 16
+            return cf[:nc.value], cv[:nc.value], sf[:ns.value], sv[:ns.value]
+        hint[0], hint[1] = max(hint[0], nc.value), max(hint[1], ns.value)
 
 
 def _cm_heavy_record(arrays, key_bytes) -> "HeavyRecord":
@@ -113,6 +119,7 @@ class CountMinView:
         self._L = cm._L
         self._cm = cm
         self.key_bytes = cm.key_bytes
+        self._hh_hint = [0, 0]
         h = ct.c_void_p()
         check(self._L.gns_cm_view_create(cm._h, ct.byref(h)))
         self._h = h
@@ -133,7 +140,7 @@ class CountMinView:
         check(self._L.gns_cm_view_refresh(self._h))
 
     def heavy_hitters_arrays(self):
-        return _cm_heavy_arrays(self._L.gns_cm_view_heavy_hitters, self._h, self.key_bytes)
+        return _cm_heavy_arrays(self._L.gns_cm_view_heavy_hitters, self._h, self.key_bytes, self._hh_hint)
 
     def heavy_hitters(self) -> "HeavyRecord":
         return _cm_heavy_record(self.heavy_hitters_arrays(), self.key_bytes)
@@ -182,6 +189,7 @@ class CountMin:
         self.count_threshold = count_threshold or 512
         self.key_bytes = kb
         self.device = device
+        self._hh_hint = [0, 0]
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -247,7 +255,7 @@ class CountMin:
     def heavy_hitters_arrays(self):
         """HeavyHitters as arrays (count flows [n,K], counts, size flows, sizes): the
         snapshot handed to a writer without building per-flow Python objects."""
-        return _cm_heavy_arrays(self._L.gns_cm_heavy_hitters, self._h, self.key_bytes)
+        return _cm_heavy_arrays(self._L.gns_cm_heavy_hitters, self._h, self.key_bytes, self._hh_hint)
 
     def heavy_hitters(self) -> HeavyRecord:
         return _cm_heavy_record(self.heavy_hitters_arrays(), self.key_bytes)
