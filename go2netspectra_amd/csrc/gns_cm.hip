@@ -589,10 +589,15 @@ __global__ __launch_bounds__(256) void k_tscan_mid(uint32_t *part, uint32_t ngrp
     const uint32_t bin = blockIdx.x * 256 + threadIdx.x;
     if (bin >= nbins) return;
     uint32_t run = 0;
-    for (uint32_t g = 0; g < ngrp; g++) {
-        const uint32_t v = part[(uint64_t)g * nbins + bin];
-        part[(uint64_t)g * nbins + bin] = run;
-        run += v;
+    for (uint32_t g0 = 0; g0 < ngrp; g0 += 16) {  // 16 loads in flight, then the scan
+        uint32_t v[16];
+#pragma unroll
+        for (uint32_t j = 0; j < 16; j++) v[j] = g0 + j < ngrp ? part[(uint64_t)(g0 + j) * nbins + bin] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 16; j++) {
+            if (g0 + j < ngrp) part[(uint64_t)(g0 + j) * nbins + bin] = run;
+            run += v[j];
+        }
     }
     tot[bin] = run;
 }

@@ -20,7 +20,7 @@ import statistics
 import sys
 
 STAGE = {"k_extract": "extract", "k_resolve": "resolve", "k_scatter": "scatter", "k_apply": "apply",
-         "k_hot_sum": "hot_sum", "k_hot_verify": "hot_verify", "k_scan_down": "scan", "k_synth": "synth",
+         "k_hot_sum": "hot_sum", "k_hot_verify": "hot_verify", "k_tscan_down": "scan", "k_synth": "synth",
          "k_ss_extract_hdr": "extract", "k_ss_extract": "extract", "k_ss_walk_mv": "walk_mv"}
 
 
