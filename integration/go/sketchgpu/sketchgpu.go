@@ -158,6 +158,66 @@ func (c *CountMin) Close() { C.gns_cm_destroy(c.h) }
 
 var _ statistic.Sketch = (*CountMin)(nil)
 
+// View is a snapshot of a CountMin for the snapshotter / alerter goroutines
+// (manager.go:139-159 call Snapshot while the workers insert): the worker that
+// owns the CountMin calls Refresh at a window boundary, and any other goroutine
+// may call HeavyHitters / Query on the view meanwhile (gns_cm_view_*).
+type View struct {
+	v        *C.gns_cm_view
+	keyBytes int
+}
+
+// NewView allocates the snapshot (16 bytes per bucket).
+func (c *CountMin) NewView() (*View, error) {
+	var v *C.gns_cm_view
+	if err := lastErr(C.gns_cm_view_create(c.h, &v)); err != nil {
+		return nil, err
+	}
+	return &View{v: v, keyBytes: c.keyBytes}, nil
+}
+
+// Refresh snapshots the buckets after every insert issued so far (owner goroutine only).
+func (w *View) Refresh() error { return lastErr(C.gns_cm_view_refresh(w.v)) }
+
+// HeavyHitters is CountMin.HeavyHitters at the last Refresh, safe during inserts.
+func (w *View) HeavyHitters() statistic.HeavyRecord {
+	var nc, ns C.uint64_t
+	if C.gns_cm_view_heavy_hitters(w.v, nil, nil, &nc, nil, nil, &ns) != C.GNS_OK {
+		return statistic.HeavyRecord{Size: []statistic.HeavySize{}, Count: []statistic.HeavyCount{}}
+	}
+	K := w.keyBytes
+	cf := make([]byte, int(nc)*K+1)
+	cv := make([]uint32, int(nc)+1)
+	sf := make([]byte, int(ns)*K+1)
+	sv := make([]uint32, int(ns)+1)
+	C.gns_cm_view_heavy_hitters(w.v, (*C.uint8_t)(unsafe.Pointer(&cf[0])), (*C.uint32_t)(unsafe.Pointer(&cv[0])), &nc,
+		(*C.uint8_t)(unsafe.Pointer(&sf[0])), (*C.uint32_t)(unsafe.Pointer(&sv[0])), &ns)
+	rec := statistic.HeavyRecord{Size: make([]statistic.HeavySize, 0, int(ns)),
+		Count: make([]statistic.HeavyCount, 0, int(nc))}
+	for i := 0; i < int(ns); i++ {
+		rec.Size = append(rec.Size, statistic.HeavySize{Flow: append([]byte(nil), sf[i*K:(i+1)*K]...), Size: sv[i]})
+	}
+	for i := 0; i < int(nc); i++ {
+		rec.Count = append(rec.Count, statistic.HeavyCount{Flow: append([]byte(nil), cf[i*K:(i+1)*K]...), Count: cv[i]})
+	}
+	return rec
+}
+
+// Query is CountMin.Query at the last Refresh, safe during inserts.
+func (w *View) Query(flow []byte) uint64 {
+	if len(flow) != w.keyBytes || len(flow) == 0 {
+		return 0
+	}
+	var out C.uint64_t
+	if C.gns_cm_view_query(w.v, (*C.uint8_t)(unsafe.Pointer(&flow[0])), C.uint32_t(len(flow)), 1, &out) != C.GNS_OK {
+		return 0
+	}
+	return uint64(out)
+}
+
+// Close releases the snapshot (before the CountMin it views).
+func (w *View) Close() { C.gns_cm_view_destroy(w.v) }
+
 // SuperSpread mirrors statistic.SuperSpread (super_spread.go) on one GPU.
 type SuperSpread struct {
 	h        *C.gns_ss
