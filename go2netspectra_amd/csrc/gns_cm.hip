@@ -678,9 +678,10 @@ struct ScatterArgs {
     const uint32_t *hany;
 };
 
-// LDS layout of k_scatter (dynamic): s_cnt[2][kScWaves][LB] (double-buffered), s_goff[d][LB]
+// LDS layout of k_scatter (dynamic): s_cnt[2][kScWaves][LB] (double-buffered), s_goff[d][LB],
+// s_dummy[kScThreads] (rank adds of lanes without an update)
 __host__ __device__ inline size_t scatter_lds_bytes(uint32_t LB, uint32_t d) {
-    return (size_t)(2 * kScWaves + d) * LB * 4;
+    return (size_t)(2 * kScWaves + d) * LB * 4 + kScThreads * 4;
 }
 
 #ifdef GNS_K3_PROF
@@ -700,6 +701,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
     const uint32_t d = a.g.d;
     uint32_t *s_cnt2 = reinterpret_cast<uint32_t *>(smem);  // [2][kScWaves][LB]
     uint32_t *s_goff = s_cnt2 + 2 * kScWaves * LB;          // [d][LB]
+    uint32_t *s_dummy = s_goff + d * LB;                    // [kScThreads]
     uint32_t par = 0;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t blk = blockIdx.x;
@@ -817,9 +819,9 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 }
                 uint32_t rk = 0;
                 if constexpr (RANK == 1) {
-                    // returning LDS adds: same-address lanes of one instruction are
-                    // served in lane order (verified at create by k_lds_order_probe)
-                    if (valid) rk = atomicAdd(&s_cnt[wave * LB + t], 1u);
+                    // returning LDS adds (issued after this loop, all items under one
+                    // wait): same-address lanes of one instruction are served in lane
+                    // order (verified at create by k_lds_order_probe)
                 } else {
                     uint64_t peers = __ballot(valid);
                     for (uint32_t bit = 0; bit < nbits; bit++) {
@@ -834,6 +836,19 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 }
                 ent[i] = e;
                 br[i] = (valid ? t : 0xFFFFu) << 16 | rk;
+            }
+            if constexpr (RANK == 1) {
+                // every lane adds (0 to its own dummy word without an update): no
+                // divergence around the returning adds, one wait for all of them
+                uint32_t rks[kScItems];
+#pragma unroll
+                for (int i = 0; i < kScItems; i++) {
+                    const uint32_t t = br[i] >> 16;
+                    uint32_t *ad = t != 0xFFFFu ? &s_cnt[wave * LB + t] : &s_dummy[tid];
+                    rks[i] = atomicAdd(ad, t != 0xFFFFu ? 1u : 0u);
+                }
+#pragma unroll
+                for (int i = 0; i < kScItems; i++) br[i] |= rks[i];
             }
             __syncthreads();
             K3_MARK(1);
@@ -868,6 +883,202 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
     }
 #ifdef GNS_K3_PROF
     if (threadIdx.x == 0 && !a.hot_mode) for (int i = 0; i < 5; i++) atomicAdd(&a.stats[11 + i], (unsigned long long)k3t[i]);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// K3s: the same stable partition, staged.  A 1024-thread block takes its K1
+// block (16384 packets) in sub-passes of 8192 packets and, per row, ranks the
+// cold updates like K3 (returning LDS adds per (wave, bin), waves owning
+// contiguous packet ranges), lays them out bin by bin in LDS, and copies the
+// bins out as contiguous runs (~15 updates per bin and sub-pass at the bench
+// geometry).  Scattered 8-byte stores cost 2-3x the time of runs of >= 16
+// (tools/membench3.hip); the output is identical to K3's.  Rows of at most
+// kStBins bins (the bench geometry has 256); wider rows use K3.
+// ---------------------------------------------------------------------------
+#ifndef GNS_ST_THREADS
+#define GNS_ST_THREADS 1024
+#endif
+#ifndef GNS_ST_SUB
+#define GNS_ST_SUB 8192
+#endif
+constexpr int kStThreads = GNS_ST_THREADS;
+constexpr int kStWaves = kStThreads / 64;
+constexpr uint32_t kStSub = GNS_ST_SUB;               // packets per sub-pass
+constexpr int kStItems = kStSub / kStThreads;         // per thread
+constexpr uint32_t kStBins = 256;                     // bins per row handled here
+static_assert(kChunk % kStSub == 0, "whole sub-passes per K1 block");
+static_assert(kStSub / kStWaves == kStItems * 64, "a wave owns kStItems x 64 consecutive packets of a sub-pass");
+
+struct StLds {
+    uint64_t stage[kStSub];
+    uint16_t sbin[kStSub];
+    uint32_t cnt[2][kStWaves][kStBins];
+    uint32_t lstart[kStBins], gpos[kStBins];
+    uint32_t goff[8][kStBins];
+    uint32_t wsum[4];
+    uint32_t dummy[kStThreads];  // rank adds of lanes without an update
+};
+
+__global__ __launch_bounds__(kStThreads) void k_scatter_st(ScatterArgs a) {
+    __shared__ StLds L;
+#ifdef GNS_K3_PROF
+    uint64_t k3t[5] = {0, 0, 0, 0, 0}, k3prev = __builtin_amdgcn_s_memtime();
+#endif
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t blk = blockIdx.x, d = a.g.d, nt = a.g.ntiles;
+    const uint32_t tmask = (1u << a.g.bin_bits) - 1u;
+    const uint64_t beg = (uint64_t)blk * kChunk;
+    const uint64_t end = min(a.n, beg + kChunk);
+    for (uint32_t i = tid; i < d * kStBins; i += kStThreads) {
+        const uint32_t r = i / kStBins, t = i % kStBins;
+        L.goff[r][t] = t < nt ? a.offsets[(uint64_t)blk * a.g.nbins_all + r * nt + t] : 0u;
+    }
+    for (uint32_t i = tid; i < 2 * kStWaves * kStBins; i += kStThreads) (&L.cnt[0][0][0])[i] = 0;
+    // packet of item j in a sub-pass: wave-contiguous, (j, lane) order inside the wave
+    auto pkt = [&](uint64_t sp, int j) { return sp + (uint64_t)wave * (kStSub / kStWaves) + (uint64_t)j * 64 + lane; };
+    uint32_t ids[kStItems], szs[kStItems], cds[kStItems];
+    uint32_t ncd[kStItems], nids[kStItems], nszs[kStItems];
+    auto load_ids = [&](uint64_t sp, uint32_t (&di)[kStItems], uint32_t (&ds)[kStItems]) {
+#pragma unroll
+        for (int j = 0; j < kStItems; j++) {
+            const uint64_t p = pkt(sp, j);
+            const uint64_t pc = p < end ? p : end - 1;
+            di[j] = p < end ? a.keyid[pc] : GNS_ID_NONE;
+            ds[j] = a.sizes[pc];
+        }
+    };
+    auto load_codes = [&](uint64_t sp, uint32_t r, uint32_t (&c)[kStItems]) {
+#pragma unroll
+        for (int j = 0; j < kStItems; j++) {
+            const uint64_t p = pkt(sp, j);
+            c[j] = a.idx[(uint64_t)r * a.n + (p < end ? p : end - 1)];
+        }
+    };
+    load_ids(beg, ids, szs);
+    load_codes(beg, 0, cds);
+    uint32_t par = 0;
+    __syncthreads();
+    for (uint64_t sp = beg; sp < end; sp += kStSub) {
+        for (uint32_t r = 0; r < d; r++) {
+            uint32_t (&cnt)[kStWaves][kStBins] = L.cnt[par];
+            K3_MARK(4);  // loop
+            // phase A: entries and stable ranks within (wave, bin)
+            uint64_t ent[kStItems];
+            uint32_t tb[kStItems];  // bin << 16 | rank, 0xFFFF bin = no update
+#pragma unroll
+            for (int j = 0; j < kStItems; j++) {
+                const uint32_t b = cds[j];
+                const bool valid = ids[j] != GNS_ID_NONE && (b >> 31) == 0;
+                uint32_t t = 0xFFFFu, rk = 0;
+                uint64_t e = 0;
+                if (valid) {
+                    t = b >> a.g.bin_bits;
+                    const uint32_t low = b & tmask, sz = szs[j];
+                    uint32_t lo = ids[j], sf = sz;
+                    if (sz >= kSizeEsc) {
+                        const uint32_t q = atomicAdd(a.ovf_cnt, 1u);
+                        if (q < kOvfCap) {
+                            a.ovf[q] = (uint64_t)sz << 32 | ids[j];
+                            lo = kOvfFlag | q;
+                        } else {
+                            atomicAdd(&a.stats[4], 1ull);
+                            lo = kOvfFlag | (kOvfCap - 1);
+                        }
+                        sf = kSizeEsc;
+                    }
+                    e = (uint64_t)((sf << kEntShift) | low) << 32 | lo;
+                }
+                ent[j] = e;
+                tb[j] = t << 16 | rk;
+            }
+            // ranks: every lane adds (a lane without an update adds 0 to its own dummy
+            // word), so the eight returning adds issue back to back under one wait;
+            // same-address lanes are served in lane order
+            {
+                uint32_t rks[kStItems];
+#pragma unroll
+                for (int j = 0; j < kStItems; j++) {
+                    const uint32_t t = tb[j] >> 16;
+                    uint32_t *ad = t != 0xFFFFu ? &cnt[wave][t] : &L.dummy[tid];
+                    rks[j] = atomicAdd(ad, t != 0xFFFFu ? 1u : 0u);
+                }
+#pragma unroll
+                for (int j = 0; j < kStItems; j++) tb[j] |= rks[j];
+            }
+            // the next step's codes (and ids / sizes at a sub-pass boundary) load during C and D
+            const uint32_t r1 = r + 1 < d ? r + 1 : 0u;
+            const uint64_t sp1 = r + 1 < d ? sp : sp + kStSub;
+            if (sp1 < end) {
+                load_codes(sp1, r1, ncd);
+                if (r1 == 0) load_ids(sp1, nids, nszs);
+            }
+            __syncthreads();
+            K3_MARK(0);
+            // phase C: per bin, prefix over the waves and the bin's total; scan of the totals
+            uint32_t total = 0, incl = 0;
+            if (tid < kStBins) {
+                const uint32_t t = tid;
+                uint32_t run = 0;
+                if (t < nt) {
+#pragma unroll
+                    for (int w = 0; w < kStWaves; w++) {
+                        const uint32_t x = cnt[w][t];
+                        cnt[w][t] = run;
+                        run += x;
+                    }
+                }
+                total = run;
+                incl = wave_incl_scan(total);
+                if (lane == 63) L.wsum[wave] = incl;
+            }
+            __syncthreads();
+            if (tid < kStBins) {
+                uint32_t base = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < 4; w++) base += w < wave ? L.wsum[w] : 0u;
+                const uint32_t t = tid;
+                L.lstart[t] = base + incl - total;
+                L.gpos[t] = L.goff[r][t];
+                L.goff[r][t] += total;
+            }
+            __syncthreads();
+            K3_MARK(1);
+            // phase D: updates into the bin-ordered stage
+#pragma unroll
+            for (int j = 0; j < kStItems; j++) {
+                const uint32_t t = tb[j] >> 16;
+                if (t != 0xFFFFu) {
+                    const uint32_t pos = L.lstart[t] + cnt[wave][t] + (tb[j] & 0xFFFFu);
+                    L.stage[pos] = ent[j];
+                    L.sbin[pos] = (uint16_t)t;
+                }
+            }
+            __syncthreads();
+            K3_MARK(2);
+            // phase E: take the next step's inputs first (the wait for them lands here,
+            // before this step's stores are issued, not after them), then the bins out
+            // as contiguous runs; clear this step's counters
+            if (sp1 < end) {
+#pragma unroll
+                for (int j = 0; j < kStItems; j++) cds[j] = ncd[j];
+                if (r1 == 0) {
+#pragma unroll
+                    for (int j = 0; j < kStItems; j++) { ids[j] = nids[j]; szs[j] = nszs[j]; }
+                }
+            }
+            const uint32_t ntot = L.wsum[0] + L.wsum[1] + L.wsum[2] + L.wsum[3];
+            for (uint32_t i = tid; i < ntot; i += kStThreads) {
+                const uint32_t t = L.sbin[i];
+                a.entries[L.gpos[t] + (i - L.lstart[t])] = L.stage[i];
+            }
+            for (uint32_t i = tid; i < kStWaves * kStBins; i += kStThreads) (&cnt[0][0])[i] = 0;
+            par ^= 1u;
+            K3_MARK(3);
+        }
+    }
+#ifdef GNS_K3_PROF
+    if (threadIdx.x == 0) for (int i = 0; i < 5; i++) atomicAdd(&a.stats[11 + i], (unsigned long long)k3t[i]);
 #endif
 }
 
@@ -2231,6 +2442,7 @@ struct gns_cm {
     uint4 *chk = nullptr;                 // [kChkCap]
     bool warm = false;                    // a batch has run since create/reset
     bool lds_ordered = false;             // k_lds_order_probe passed: K3 ranks by LDS adds
+    bool k3_staged = true;                // K3s (LDS-staged runs) where the geometry allows; GNS_K3_STAGED=0: K3
     uint32_t *h_pin = nullptr;            // pinned host mirror of small counters
     // staging for host inputs
     uint8_t *stage = nullptr;
@@ -2374,7 +2586,9 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.ovf_cnt = cm->ovf_cnt; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
         a.hot_mode = 0; a.hflag2 = cm->hflag2; a.hany = cm->hflag2 + g.d * kHot;
         ScopedStage st(cm->timer, 3);
-        if (cm->lds_ordered)
+        if (cm->lds_ordered && cm->k3_staged && g.ntiles <= kStBins && g.d <= 8)
+            hipLaunchKernelGGL(k_scatter_st, dim3(nblk), dim3(kStThreads), 0, s, a);
+        else if (cm->lds_ordered)
             hipLaunchKernelGGL(k_scatter<1>, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
         else
             hipLaunchKernelGGL(k_scatter<0>, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
@@ -2638,6 +2852,8 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             dfree(viol);
             if (e != hipSuccess) { set_error("lds order probe: %s", hipGetErrorString(e)); rc = GNS_E_HIP; break; }
             cm->lds_ordered = hv == 0 && !(env && env[0] == '0');
+            const char *es = getenv("GNS_K3_STAGED");
+            cm->k3_staged = !(es && es[0] == '0');
         }
         if (hipStreamSynchronize(cm->stream) != hipSuccess) { set_error("sync failed"); rc = GNS_E_HIP; break; }
     } while (0);
