@@ -19,7 +19,7 @@ import json
 import statistics
 import sys
 
-STAGE = {"k_extract": "extract", "k_resolve": "resolve", "k_scatter": "scatter", "k_apply": "apply",
+STAGE = {"k_extract": "extract", "k_resolve": "resolve", "k_scatter": "scatter", "k_scatter_st": "scatter", "k_apply": "apply",
          "k_hot_sum": "hot_sum", "k_hot_verify": "hot_verify", "k_tscan_down": "scan", "k_synth": "synth",
          "k_ss_extract_hdr": "extract", "k_ss_extract": "extract", "k_ss_walk_mv": "walk_mv"}
 
