@@ -207,8 +207,9 @@ class CountMin:
         """Sketch.Insert for a batch: keys[n, stride] uint8 (first key_bytes used)."""
         where = _where(keys, sizes)
         if where == _lib.MEM_HOST:
-            keys = _host(keys, np.uint8).reshape(len(sizes), -1)
             sizes = _host(sizes, np.uint32)
+            keys = (_host(keys, np.uint8).reshape(len(sizes), -1) if len(sizes)
+                    else np.zeros((0, max(self.key_bytes, 1)), np.uint8))  # empty batch
         n = int(sizes.shape[0])
         stride = int(keys.shape[1]) if n else max(self.key_bytes, 1)
         check(self._L.gns_cm_insert_keys(self._h, _ptr(keys), stride, _ptr(sizes), n, where))
@@ -365,8 +366,12 @@ class SuperSpread:
     def insert_keys(self, flows, elems) -> None:
         where = _where(flows, elems)
         if where == _lib.MEM_HOST:
-            flows = _host(flows, np.uint8).reshape(len(flows), -1)
-            elems = _host(elems, np.uint8).reshape(len(elems), -1)
+            if len(flows) == 0:  # empty batch (numpy cannot infer -1 of a size-0 reshape)
+                flows = np.zeros((0, max(self.flow_bytes, 1)), np.uint8)
+                elems = np.zeros((0, max(self.elem_bytes, 1)), np.uint8)
+            else:
+                flows = _host(flows, np.uint8).reshape(len(flows), -1)
+                elems = _host(elems, np.uint8).reshape(len(elems), -1)
         n = int(flows.shape[0])
         fs = int(flows.shape[1]) if n else max(self.flow_bytes, 1)
         es = int(elems.shape[1]) if n else max(self.elem_bytes, 1)
