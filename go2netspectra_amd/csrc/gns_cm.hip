@@ -894,34 +894,38 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
 // bins out as contiguous runs (~15 updates per bin and sub-pass at the bench
 // geometry).  Scattered 8-byte stores cost 2-3x the time of runs of >= 16
 // (tools/membench3.hip); the output is identical to K3's.  Rows of at most
-// kStBins bins (the bench geometry has 256); wider rows use K3.
+// 512 bins (the bench geometry has 256, configs[5] 512); wider rows use K3.
 // ---------------------------------------------------------------------------
-#ifndef GNS_ST_THREADS
-#define GNS_ST_THREADS 1024
-#endif
 #ifndef GNS_ST_SUB
 #define GNS_ST_SUB 8192
 #endif
-constexpr int kStThreads = GNS_ST_THREADS;
-constexpr int kStWaves = kStThreads / 64;
 constexpr uint32_t kStSub = GNS_ST_SUB;               // packets per sub-pass
-constexpr int kStItems = kStSub / kStThreads;         // per thread
-constexpr uint32_t kStBins = 256;                     // bins per row handled here
 static_assert(kChunk % kStSub == 0, "whole sub-passes per K1 block");
-static_assert(kStSub / kStWaves == kStItems * 64, "a wave owns kStItems x 64 consecutive packets of a sub-pass");
 
+// NT threads, rows of at most BINS bins: <1024, 256> (the bench geometry) and
+// <512, 512> (the wide/deep configs[5] geometry, 16 packets per thread, one
+// 134 KB block per CU)
+template <int NT, int BINS>
 struct StLds {
+    static constexpr int kWaves = NT / 64;
     uint64_t stage[kStSub];
     uint16_t sbin[kStSub];
-    uint32_t cnt[2][kStWaves][kStBins];
-    uint32_t lstart[kStBins], gpos[kStBins];
-    uint32_t goff[8][kStBins];
-    uint32_t wsum[4];
-    uint32_t dummy[kStThreads];  // rank adds of lanes without an update
+    uint32_t cnt[2][kWaves][BINS];
+    uint32_t lstart[BINS], gpos[BINS];
+    uint32_t goff[8][BINS];
+    uint32_t wsum[BINS / 64];
+    uint32_t dummy[NT];  // rank adds of lanes without an update
 };
 
-__global__ __launch_bounds__(kStThreads) void k_scatter_st(ScatterArgs a) {
-    __shared__ StLds L;
+template <int NT, int BINS>
+__global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
+    constexpr int kStThreads = NT;
+    constexpr int kStWaves = NT / 64;
+    constexpr int kStItems = kStSub / NT;
+    constexpr uint32_t kStBins = BINS;
+    static_assert(kStSub / kStWaves == kStItems * 64, "a wave owns kStItems x 64 consecutive packets of a sub-pass");
+    static_assert(BINS <= NT && BINS % 64 == 0, "one thread per bin in the bin scan");
+    __shared__ StLds<NT, BINS> L;
 #ifdef GNS_K3_PROF
     uint64_t k3t[5] = {0, 0, 0, 0, 0}, k3prev = __builtin_amdgcn_s_memtime();
 #endif
@@ -1036,7 +1040,7 @@ __global__ __launch_bounds__(kStThreads) void k_scatter_st(ScatterArgs a) {
             if (tid < kStBins) {
                 uint32_t base = 0;
 #pragma unroll
-                for (uint32_t w = 0; w < 4; w++) base += w < wave ? L.wsum[w] : 0u;
+                for (uint32_t w = 0; w < kStBins / 64; w++) base += w < wave ? L.wsum[w] : 0u;
                 const uint32_t t = tid;
                 L.lstart[t] = base + incl - total;
                 L.gpos[t] = L.goff[r][t];
@@ -1067,7 +1071,9 @@ __global__ __launch_bounds__(kStThreads) void k_scatter_st(ScatterArgs a) {
                     for (int j = 0; j < kStItems; j++) { ids[j] = nids[j]; szs[j] = nszs[j]; }
                 }
             }
-            const uint32_t ntot = L.wsum[0] + L.wsum[1] + L.wsum[2] + L.wsum[3];
+            uint32_t ntot = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < kStBins / 64; w++) ntot += L.wsum[w];
             for (uint32_t i = tid; i < ntot; i += kStThreads) {
                 const uint32_t t = L.sbin[i];
                 a.entries[L.gpos[t] + (i - L.lstart[t])] = L.stage[i];
@@ -2586,8 +2592,10 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.ovf_cnt = cm->ovf_cnt; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
         a.hot_mode = 0; a.hflag2 = cm->hflag2; a.hany = cm->hflag2 + g.d * kHot;
         ScopedStage st(cm->timer, 3);
-        if (cm->lds_ordered && cm->k3_staged && g.ntiles <= kStBins && g.d <= 8)
-            hipLaunchKernelGGL(k_scatter_st, dim3(nblk), dim3(kStThreads), 0, s, a);
+        if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 256 && g.d <= 8)
+            hipLaunchKernelGGL((k_scatter_st<1024, 256>), dim3(nblk), dim3(1024), 0, s, a);
+        else if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 512 && g.d <= 8)
+            hipLaunchKernelGGL((k_scatter_st<512, 512>), dim3(nblk), dim3(512), 0, s, a);
         else if (cm->lds_ordered)
             hipLaunchKernelGGL(k_scatter<1>, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
         else
