@@ -638,7 +638,10 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_packet": BYTES_PER_PKT, "kernel_avg_ms": round(avg_ms, 4),
-                     "pipeline_frac": round(BYTES_PER_PKT * n * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4)},
+                     "pipeline_frac": round(BYTES_PER_PKT * n * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4),
+                     # SURVEY §8d convention B: + one 32-B counter sector read + written per row
+                     "pipeline_frac_b": round((BYTES_PER_PKT + args.depth * 64) * n * args.steps / elapsed / 1e9
+                                              / HBM_PEAK_GBS, 4)},
         "stage_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()},
         "heavy_hitters": {"count": len(hh.Count), "size": len(hh.Size or [])},
         "engine_counters": counters,

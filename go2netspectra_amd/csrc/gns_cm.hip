@@ -317,7 +317,9 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
             const uint32_t b = bk[rr];
             h = hot_lookup(s_tab + rr * kHotTab, b);
             // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
+#ifndef GNS_ABL_NOIDX
             a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
+#endif
             binid = h >= 0 ? a.g.nbins + rr * kHot + (uint32_t)h : rr * a.g.ntiles + (b >> a.g.bin_bits);
         }
         // heavy bins: one LDS add for the wave's majority bin
@@ -2840,6 +2842,9 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (rc = dalloc_t(&cm->hflag2, g.d * kHot + 2)) || (rc = dalloc_t(&cm->hres, g.d * kHot * 2)) ||
             (rc = dalloc_t(&cm->chk, kChkCap)) || (rc = dalloc_t(&cm->hot_tab, (size_t)g.d * kHotTab)))
             break;
+#ifdef GNS_ABL_NOIDX
+        if (hipMemset(cm->idx, 0, (size_t)cm->bmax * g.d * 4) != hipSuccess) { rc = GNS_E_HIP; break; }
+#endif
         if (hipHostMalloc(reinterpret_cast<void **>(&cm->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
         }
