@@ -1245,7 +1245,9 @@ __device__ __forceinline__ void size_seq64(bool valid, uint32_t k, uint32_t s, u
 }
 
 struct ApplyLds {
-    uint32_t sC[kTileMax], sFc[kTileMax], sS[kTileMax], sFs[kTileMax];
+    // bucket state, halves paired: sCS = {C, S}, sF = {Fc, Fs} (classify reads both
+    // fingerprints, decide both counters: one 8-byte LDS access each)
+    uint2 sCS[kTileMax], sF[kTileMax];
     unsigned long long accN[kTileMax];  // n | n_oth_c<<21 | n_oth_s<<42 | force<<63
     unsigned long long accS[kTileMax];  // sum_own | sum_oth<<32 ; replay owner words
     uint16_t s_list[kApChunk];
@@ -1271,7 +1273,6 @@ __device__ __forceinline__ void decode_entry(const uint64_t *ovf, uint64_t e, ui
 __device__ __forceinline__ void replay_group(ApplyLds &L, bool pending, uint32_t b, uint32_t k, uint32_t s,
                                              uint32_t rf) {
     const uint32_t lane = threadIdx.x & 63u;
-    uint32_t *sC = L.sC, *sFc = L.sFc, *sS = L.sS, *sFs = L.sFs;
     uint32_t *own = reinterpret_cast<uint32_t *>(L.accS);
     // a bucket with many updates in this group (a contested bucket that
     // failed the linear check): wave-parallel sequence, 64 updates per step
@@ -1285,14 +1286,14 @@ __device__ __forceinline__ void replay_group(ApplyLds &L, bool pending, uint32_t
         if (__popcll(m0) < 8) break;
         const uint32_t rf0 = __shfl(rf, lead, 64);
         if (rf0 & 2u) {
-            uint32_t F = sFs[b0], S = sS[b0];
+            uint32_t F = L.sF[b0].y, S = L.sCS[b0].y;
             size_seq64(mine, k, s, F, S);
-            if (lane == lead) { sS[b0] = S; sFs[b0] = F; }
+            if (lane == lead) { L.sCS[b0].y = S; L.sF[b0].y = F; }
         }
         if (rf0 & 1u) {
-            uint32_t F = sFc[b0], C = sC[b0];
+            uint32_t F = L.sF[b0].x, C = L.sCS[b0].x;
             count_seq64(mine, k, F, C);
-            if (lane == lead) { sC[b0] = C; sFc[b0] = F; }
+            if (lane == lead) { L.sCS[b0].x = C; L.sF[b0].x = F; }
         }
         if (mine) pending = false;
     }
@@ -1300,21 +1301,25 @@ __device__ __forceinline__ void replay_group(ApplyLds &L, bool pending, uint32_t
         if (pending) atomicMax(&own[b], 64u - lane);
         const bool win = pending && own[b] == 64u - lane;
         if (win) {
+            // (bucket b belongs to this wave and one lane wins it per round: the
+            // whole pair is read and written back)
+            uint2 cs = L.sCS[b], f = L.sF[b];
             if (rf & 2u) {  // size half, count_min.go:99-128
-                uint32_t S = sS[b], F = sFs[b];
+                uint32_t S = cs.y, F = f.y;
                 if (S == 0) { S = s; F = k; }
                 else if (F == k) S = S + s;
                 else if (s > S) { S = s; F = k; }
                 else S = S - s;
-                sS[b] = S; sFs[b] = F;
+                cs.y = S; f.y = F;
             }
             if (rf & 1u) {  // count half, count_min.go:130-155
-                uint32_t C = sC[b], F = sFc[b];
+                uint32_t C = cs.x, F = f.x;
                 if (C == 0) { C = 1; F = k; }
                 else if (F == k) C = C + 1;
                 else { C = C - 1; if (C == 0) F = k; }
-                sC[b] = C; sFc[b] = F;
+                cs.x = C; f.x = F;
             }
+            L.sCS[b] = cs; L.sF[b] = f;
             own[b] = 0;
             pending = false;
         }
@@ -1357,15 +1362,15 @@ __device__ __forceinline__ void tile_none(TilePre &pre) {
 __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, const uint64_t *ent, uint32_t beg,
                                            uint32_t end, uint64_t cbase, uint32_t tn, uint32_t col0,
                                            TilePre &pre, uint64_t next_cbase, uint32_t next_tn) {
-    uint32_t *sC = L.sC, *sFc = L.sFc, *sS = L.sS, *sFs = L.sFs;
     unsigned long long *accN = L.accN, *accS = L.accS;
     uint16_t *s_list = L.s_list;
     uint32_t *s_wc = L.s_wc;
     uint32_t &s_any = L.s_any, &s_nlist = L.s_nlist;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
 #ifdef GNS_K4_PROF
-    // phase cycles: 0 classify, 1 decide, 2 compact, 3 replay + loop, 4 tile load, 5 tile store
-    uint64_t pt[6] = {0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
+    // phase cycles: 0 classify, 1 decide, 2 compact, 3 replay clear + loop top, 4 replay gather,
+    // 5 tile load + store, 6 replay groups
+    uint64_t pt[7] = {0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
 #define K4_MARK(i) do { if (tid == 0) { const uint64_t tn_ = __builtin_amdgcn_s_memtime(); pt[i] += tn_ - tprev; tprev = tn_; } } while (0)
 #else
 #define K4_MARK(i) do { } while (0)
@@ -1375,13 +1380,13 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
     for (uint32_t m = 0; m < kTilePer; m++) {
         const uint32_t i = tid + m * kApThreads;
         if (i < tn) {
-            sC[i] = pre.c[m]; sFc[i] = pre.fc[m]; sS[i] = pre.s[m]; sFs[i] = pre.fs[m];
+            L.sCS[i] = make_uint2(pre.c[m], pre.s[m]); L.sF[i] = make_uint2(pre.fc[m], pre.fs[m]);
             accN[i] = 0; accS[i] = 0;
         }
     }
 #ifdef GNS_K4_PROF
     __syncthreads();
-    K4_MARK(4);
+    K4_MARK(5);
 #endif
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint64_t e[kApItems], en[kApItems];
@@ -1411,7 +1416,8 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             uint64_t incN = 0, incS = 0;
             if (v[j] && !ovf) {
                 const uint32_t s = hi >> kEntShift;
-                const bool oc = lo != sFc[b], os = lo != sFs[b];
+                const uint2 f = L.sF[b];
+                const bool oc = lo != f.x, os = lo != f.y;
                 incN = 1ull | (uint64_t)oc << 14 | (uint64_t)os << 28;
                 incS = os ? (uint64_t)s << 32 : (uint64_t)s;
             }
@@ -1448,17 +1454,19 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             if (!force) {
                 // count half: C > n_oth keeps C >= 2 before every foreign packet
                 // (count_min.go:145-151 never reaches 0) and no wrap.
-                const uint32_t C = sC[i];
+                uint2 cs = L.sCS[i];
+                const uint32_t C = cs.x;
                 const uint32_t nown = n - noc;
-                if (C > noc && (uint64_t)C + nown < (1ull << 32)) sC[i] = C + nown - noc;
+                if (C > noc && (uint64_t)C + nown < (1ull << 32)) cs.x = C + nown - noc;
                 else rep |= 1u;
                 // size half: all-own is pure addition (:109-114, u32 wrap ok);
                 // otherwise S > sum_oth keeps S > s before every foreign packet
                 // (:115-125 never replaces) and no wrap.
-                const uint32_t S = sS[i];
-                if (nos == 0) sS[i] = S + so;
-                else if (S > sx && (uint64_t)S + so < (1ull << 32)) sS[i] = S + so - sx;
+                const uint32_t S = cs.y;
+                if (nos == 0) cs.y = S + so;
+                else if (S > sx && (uint64_t)S + so < (1ull << 32)) cs.y = S + so - sx;
                 else rep |= 2u;
+                L.sCS[i] = cs;
             } else {
                 rep = 3u;
             }
@@ -1535,6 +1543,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                 }
                 if (c <= kWl) nmine = c;
             }
+            K4_MARK(4);
             if (nmine != 0xFFFFFFFFu) {
                 const uint16_t *wl = s_list + wave * kWl;
                 for (uint32_t g0 = 0; g0 < nmine; g0 += 64) {
@@ -1549,6 +1558,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                     }
                     replay_group(L, pending, b, k, s, rf);
                 }
+                K4_MARK(6);
                 __builtin_amdgcn_wave_barrier();
                 for (uint32_t j = lane; j < nmine; j += 64) accN[(uint32_t)(L.s_rep[wl[j]] >> 32) & (kTileMax - 1u)] = 0;
             } else {
@@ -1587,8 +1597,9 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
     if (next_cbase != kNoTile) tile_fetch(a, pre, next_cbase, next_tn);
     else tile_none(pre);
     for (uint32_t i = tid; i < tn; i += kApThreads) {
-        a.C[cbase + i] = sC[i]; a.Fc[cbase + i] = sFc[i];
-        a.S[cbase + i] = sS[i]; a.Fs[cbase + i] = sFs[i];
+        const uint2 cs = L.sCS[i], f = L.sF[i];
+        a.C[cbase + i] = cs.x; a.Fc[cbase + i] = f.x;
+        a.S[cbase + i] = cs.y; a.Fs[cbase + i] = f.y;
     }
     if (tid == 0) {
         atomicAdd(&a.stats[5], (unsigned long long)st_rep);
@@ -1599,6 +1610,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
     __syncthreads();
     K4_MARK(5);
     if (tid == 0) for (int i = 0; i < 6; i++) atomicAdd(&a.stats[8 + i], (unsigned long long)pt[i]);
+    if (tid == 0) atomicAdd(&a.stats[15], (unsigned long long)pt[6]);
 #endif
 }
 
@@ -3260,7 +3272,7 @@ int gns_cm_counters(gns_cm *cm, uint64_t out[8]) {
 #ifdef GNS_K4_PROF  // profiling build: K4 phase cycles (classify, decide, compact, replay, tile load,
                     // tile store, sub-partition), chunks
     for (int i = 0; i < 7; i++) out[i] = h[8 + i];
-    out[7] = h[6];
+    out[7] = h[15];  // replay groups (out[6]: sub-partition)
 #else
     for (int i = 0; i < 8; i++) out[i] = h[i];
 #endif
