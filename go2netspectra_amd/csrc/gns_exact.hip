@@ -10,35 +10,30 @@
 // of the sketch layout (task.go:265-300) with every IP field in To16 form, in
 // the flow dictionary of gns_keys.cuh (full key bytes, exact compare).
 //
-// Counters are additive; only StartTime/EndTime depend on order.  They are the
-// timestamps of the flow's first and last packet in stream order, found with
-// atomicMin/atomicMax on the global packet index and resolved by a second
-// pass that lets the packet holding that index write its timestamp.
+// Counters are additive; only StartTime/EndTime depend on order: the
+// timestamps of the flow's first and last packet in stream order.
 //
 //   X1  k_ex_extract   parse -> To16 tuple -> key -> flow id (dictionary)
 //   X1b k_ex_resolve   re-probe packets parked on a same-launch claim
-//   X2  k_ex_aggregate per 16K-packet block: LDS hash aggregation of
-//                      (count, bytes, first, last) per flow id, one set of
-//                      global atomics per distinct flow per block
-//   X3  k_ex_times     first/last packets write StartTime/EndTime
+//   X2  radix sort of X1's (flow id, packet index << 32 | wire length) pairs
+//       by flow id (rocPRIM; stable, so each flow's packets stay in stream order)
+//   X3  k_ex_runs      over the sorted pairs: the first / last packet of each
+//                      flow's run writes StartTime (a new flow) / EndTime, the
+//                      counters take one atomic add per run piece
+// A Zipf batch touches a flow in many places; per-block LDS aggregation left
+// the tail flows (about a third of the packets) to global atomics, three per
+// packet; after the sort a flow is one contiguous run.
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "gns_common.hpp"
+#include <rocprim/rocprim.hpp>
 
 namespace gns {
 
 constexpr int kXThreads = 256;
 constexpr uint32_t kXChunk = 16384;
-#ifndef GNS_XTAB_BITS
-#define GNS_XTAB_BITS 11
-#endif
-#ifndef GNS_XPROBE
-#define GNS_XPROBE 16
-#endif
-constexpr uint32_t kXTabBits = GNS_XTAB_BITS;
-constexpr uint32_t kXTab = 1u << kXTabBits;   // LDS aggregation slots per block
-constexpr uint32_t kXProbe = GNS_XPROBE;
 
 struct ExIn {
     InputDesc in;
@@ -77,7 +72,9 @@ struct ExArgs {
     KeyPlanN kp;
     DictDev D;
     uint32_t epoch;
-    uint32_t *keyid;
+    uint32_t *skey;      // X2 sort keys: flow id, none_key for a packet without one
+    uint64_t *sval;      // X2 sort values: packet index << 32 | wire length
+    uint32_t none_key;
     uint64_t *pend;
     uint32_t *pend_cnt, *pend_total;
     unsigned long long *stats;  // 0 inserted, 1 dropped, 2 unsupported, 3 dict full
@@ -97,24 +94,25 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
     uint32_t n_ok = 0;
     for (uint64_t p = beg + tid; p < end; p += kXThreads) {
         uint32_t kw[GNS_KWMAX];
+        a.sval[p] = p << 32 | a.x.in.sizes[p];
         const int st = ex_key<KIND, MODE>(a.x, K, s_src, p, kw);
         if (st != PARSE_OK) {
-            a.keyid[p] = GNS_ID_NONE;
+            a.skey[p] = a.none_key;
             atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
             continue;
         }
         uint32_t out;
         const int r = dict_find_or_claim(a.D, kw, mm3_n<GNS_KWMAX>(kw, K, a.D.seed) & a.D.mask, a.epoch, &out);
         if (r == DICT_FULL) {
-            a.keyid[p] = GNS_ID_NONE;
+            a.skey[p] = a.none_key;
             atomicAdd(&s_full, 1u);
             continue;
         }
         n_ok++;
         if (r == DICT_FOUND) {
-            a.keyid[p] = out;
+            a.skey[p] = out;
         } else {
-            a.keyid[p] = GNS_ID_NONE;
+            a.skey[p] = a.none_key;
             a.pend[beg + atomicAdd(&s_pend, 1u)] = (uint64_t)(p - beg) << 32 | out;
         }
     }
@@ -156,7 +154,7 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
         (void)ex_key<KIND, MODE>(a.x, a.kp.K, s_src, p, kw);
         uint32_t out;
         const int res = dict_find_or_claim(a.D, kw, (uint32_t)v, a.epoch, &out);
-        if (res == DICT_FOUND) a.keyid[p] = out;
+        if (res == DICT_FOUND) a.skey[p] = out;
         else if (res == DICT_PENDING) r.pend_out[beg + atomicAdd(&s_cnt, 1u)] = (v & 0xFFFFFFFF00000000ull) | out;
         else atomicAdd(&s_full, 1u);
     }
@@ -168,119 +166,105 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
     }
 }
 
+// per-flow state, one array per field (first/last: global packet index, ~0 / 0 = none
+// yet; start/end: StartTime / EndTime in ns).  (One 64-byte record per flow measured
+// slower: the two counter atomics of a run then hit one line.)
 struct FlowState {
     unsigned long long *pkts, *bytes, *first, *last;
     long long *start, *end;
 };
 
-struct ExAggArgs {
-    const uint32_t *keyid;
-    const uint32_t *len;
-    uint64_t n, pkt_base;
-    FlowState f;
-};
-
-// X2: per block, LDS hash aggregation keyed by flow id (Zipf: the heavy flows
-// collapse to one set of global atomics per block); flows that do not find a
-// slot within kXProbe probes go straight to global atomics.
+// X3 over the sorted pairs: thread t takes kRunItems consecutive packets.  A
+// packet that starts its flow's run (the flow's first packet of the batch, the
+// sort being stable) sets StartTime when the flow is new; the one that ends it
+// sets EndTime; counters go to the flow with one atomic add per (thread, run)
+// piece, or per wave when the whole wave lies inside one run (a heavy flow).
+// task.go:154-212 per packet: PacketCount++, ByteCount += Length, StartTime on
+// the first packet, EndTime on every packet.
+#ifndef GNS_RUN_ITEMS
+#define GNS_RUN_ITEMS 16
+#endif
+constexpr int kRunItems = GNS_RUN_ITEMS;
 extern "C" __device__ unsigned long long __ockl_wfred_add_u64(unsigned long long);
-
-// first/last packet index of a flow: first only decreases and last only
-// increases, so a value read earlier that already beats the candidate proves
-// the atomic would not change anything (most flows were seen before).
-__device__ __forceinline__ void ex_first_last(const FlowState &f, uint32_t id, unsigned long long fst,
-                                              unsigned long long lst) {
-    if (__atomic_load_n(&f.first[id], __ATOMIC_RELAXED) > fst) atomicMin(&f.first[id], fst);
-    if (__atomic_load_n(&f.last[id], __ATOMIC_RELAXED) < lst) atomicMax(&f.last[id], lst);
-}
-
-// one (count, bytes, first, last) contribution of flow id into the block table
-// (or straight to the global arrays when its probe window is full)
-__device__ __forceinline__ void ex_agg_insert(const ExAggArgs &a, uint32_t *s_key, uint32_t *s_cnt, uint32_t *s_mn,
-                                              uint32_t *s_mx, unsigned long long *s_bytes, uint64_t beg,
-                                              uint32_t id, uint32_t cnt, unsigned long long bytes, uint32_t mn,
-                                              uint32_t mx) {
-    uint32_t slot = (id * 0x9E3779B1u) >> (32 - kXTabBits);
-    for (uint32_t k = 0; k < kXProbe; k++) {
-        uint32_t cur = s_key[slot];
-        if (cur == GNS_ID_NONE) {
-            const uint32_t prev = atomicCAS(&s_key[slot], GNS_ID_NONE, id);
-            cur = prev == GNS_ID_NONE ? id : prev;
+__global__ __launch_bounds__(256) void k_ex_runs(const uint32_t *skey, const uint64_t *sval, uint64_t n,
+                                                 uint32_t none_key, const int64_t *ts, uint64_t pkt_base,
+                                                 FlowState f) {
+    const uint64_t b0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kRunItems;
+    if (b0 >= n) return;  // whole waves past the end exit together (n is rounded per wave below)
+    uint32_t k[kRunItems];
+    uint64_t v[kRunItems];
+#pragma unroll
+    for (int j = 0; j < kRunItems; j++) {
+        const uint64_t i = b0 + j;
+        k[j] = i < n ? skey[i] : none_key;
+        v[j] = i < n ? sval[i] : 0ull;
+    }
+    const uint32_t prev = b0 > 0 ? skey[b0 - 1] : ~0u;
+    const uint32_t next = b0 + kRunItems < n ? skey[b0 + kRunItems] : ~0u;
+    // a heavy flow covering the whole wave: one add per wave
+    const uint32_t kw = __builtin_amdgcn_readfirstlane(k[0]);
+    const bool inner = k[0] == kw && k[kRunItems - 1] == kw && prev == kw && next == kw;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (__ballot(true) == ~0ull && __ballot(inner) == ~0ull) {
+        uint64_t by = 0;
+#pragma unroll
+        for (int j = 0; j < kRunItems; j++) by += (uint32_t)v[j];
+        const unsigned long long tot = __ockl_wfred_add_u64(by);
+        if (lane == 0 && kw != none_key) {
+            atomicAdd(&f.pkts[kw], (unsigned long long)(64 * kRunItems));
+            atomicAdd(&f.bytes[kw], tot);
         }
-        if (cur == id) {
-            atomicAdd(&s_cnt[slot], cnt);
-            atomicAdd(&s_bytes[slot], bytes);
-            atomicMin(&s_mn[slot], mn);
-            atomicMax(&s_mx[slot], mx);
-            return;
+        return;
+    }
+    // pieces of runs (a run split over threads adds once per piece); the run's first
+    // packet sets StartTime when the flow is new, its last one EndTime.  The loads
+    // the walk depends on (a head's stored first-packet index, the timestamps of
+    // run heads and tails) are issued up front, all in flight together, instead of
+    // one dependent round trip per run.
+    unsigned long long fst[kRunItems];
+    long long tsv[kRunItems];
+#pragma unroll
+    for (int j = 0; j < kRunItems; j++) {
+        const bool valid = k[j] != none_key;
+        const bool head = valid && (j == 0 ? prev : k[j - 1]) != k[j];
+        const bool tail = valid && (j == kRunItems - 1 ? next : k[j + 1]) != k[j];
+        fst[j] = head ? f.first[k[j]] : 0ull;
+        tsv[j] = head || tail ? ts[(uint32_t)(v[j] >> 32)] : 0ll;
+    }
+    uint32_t cur = k[0], cnt = 0, pl = 0;
+    unsigned long long by = 0;
+    long long tl_ts = 0;
+#pragma unroll
+    for (int j = 0; j < kRunItems; j++) {
+        const uint32_t id = k[j];
+        if (id == none_key) break;  // invalid packets sort last
+        const uint32_t pidx = (uint32_t)(v[j] >> 32);
+        if (id != cur) {  // a piece ends at its run's last packet
+            atomicAdd(&f.pkts[cur], (unsigned long long)cnt);
+            atomicAdd(&f.bytes[cur], by);
+            f.last[cur] = pkt_base + pl;
+            f.end[cur] = tl_ts;
+            cur = id; cnt = 0; by = 0;
         }
-        slot = (slot + 1) & (kXTab - 1);
-    }
-    const unsigned long long g = a.pkt_base + beg;
-    atomicAdd(&a.f.pkts[id], (unsigned long long)cnt);
-    atomicAdd(&a.f.bytes[id], bytes);
-    ex_first_last(a.f, id, g + mn, g + mx);
-}
-
-// X2: per block, LDS hash aggregation keyed by flow id.  Zipf traffic puts
-// many lanes of a wave on one heavy flow: that group is reduced in registers
-// (count = popcount, bytes = DPP wave sum, first/last = lowest/highest lane)
-// and enters the table once; flows that do not find a slot within kXProbe
-// probes go straight to global atomics.
-__global__ __launch_bounds__(kXThreads) void k_ex_aggregate(ExAggArgs a) {
-    __shared__ uint32_t s_key[kXTab], s_cnt[kXTab], s_mn[kXTab], s_mx[kXTab];
-    __shared__ unsigned long long s_bytes[kXTab];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    for (uint32_t i = tid; i < kXTab; i += kXThreads) {
-        s_key[i] = GNS_ID_NONE; s_cnt[i] = 0; s_bytes[i] = 0; s_mn[i] = 0xFFFFFFFFu; s_mx[i] = 0;
-    }
-    __syncthreads();
-    const uint64_t beg = (uint64_t)blockIdx.x * kXChunk;
-    const uint64_t end = min(a.n, beg + kXChunk);
-    for (uint64_t p0 = beg; p0 < end; p0 += kXThreads) {  // wave-uniform trip count
-        const uint64_t p = p0 + tid;
-        const uint32_t id = p < end ? a.keyid[p] : GNS_ID_NONE;
-        const uint32_t ln = p < end ? a.len[p] : 0u;
-        const uint32_t li = (uint32_t)(p - beg);
-        const uint64_t valid = __ballot(id != GNS_ID_NONE);
-        bool mine = id != GNS_ID_NONE;
-        if (valid) {
-            const uint32_t b0 = __builtin_amdgcn_readlane(id, __ffsll((unsigned long long)valid) - 1);
-            const uint64_t mm = __ballot(id == b0);
-            if (__popcll(mm) >= 8) {  // wave-uniform
-                const unsigned long long sb = __ockl_wfred_add_u64(id == b0 ? (unsigned long long)ln : 0ull);
-                const uint32_t first = (uint32_t)__ffsll((unsigned long long)mm) - 1u;
-                const uint32_t last = 63u - (uint32_t)__clzll((long long)mm);
-                const uint32_t lbase = li - lane;
-                if (lane == first)
-                    ex_agg_insert(a, s_key, s_cnt, s_mn, s_mx, s_bytes, beg, b0, (uint32_t)__popcll(mm), sb,
-                                  lbase + first, lbase + last);
-                mine = mine && id != b0;
-            }
+        if (fst[j] == ~0ull) {  // head of a new flow's run: its first packet ever (batches in order)
+            f.first[id] = pkt_base + pidx;
+            f.start[id] = tsv[j];
         }
-        if (mine) ex_agg_insert(a, s_key, s_cnt, s_mn, s_mx, s_bytes, beg, id, 1u, ln, li, li);
+        cnt++;
+        by += (uint32_t)v[j];
+        pl = pidx;
+        tl_ts = tsv[j];
     }
-    __syncthreads();
-    const unsigned long long gb = a.pkt_base + beg;
-    for (uint32_t i = tid; i < kXTab; i += kXThreads) {
-        const uint32_t id = s_key[i];
-        if (id == GNS_ID_NONE) continue;
-        atomicAdd(&a.f.pkts[id], (unsigned long long)s_cnt[i]);
-        atomicAdd(&a.f.bytes[id], s_bytes[i]);
-        ex_first_last(a.f, id, gb + s_mn[i], gb + s_mx[i]);
+    if (cnt) {
+        atomicAdd(&f.pkts[cur], (unsigned long long)cnt);
+        atomicAdd(&f.bytes[cur], by);
+        // the piece ends this thread's range: it is the run's end unless the run goes on
+        const bool run_ends = (cur == k[kRunItems - 1] ? next != cur : true);
+        if (run_ends) {
+            f.last[cur] = pkt_base + pl;
+            f.end[cur] = tl_ts;
+        }
     }
-}
-
-// X3: the packet that is its flow's first (last) writes StartTime (EndTime).
-__global__ __launch_bounds__(256) void k_ex_times(const uint32_t *keyid, const int64_t *ts, uint64_t n,
-                                                  uint64_t pkt_base, FlowState f) {
-    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= n) return;
-    const uint32_t id = keyid[p];
-    if (id == GNS_ID_NONE) return;
-    const unsigned long long g = pkt_base + p;
-    if (f.first[id] == g) f.start[id] = ts[p];
-    if (f.last[id] == g) f.end[id] = ts[p];
 }
 
 __global__ __launch_bounds__(256) void k_ex_query(const uint8_t *flows, uint32_t stride, uint64_t n, uint32_t K,
@@ -341,7 +325,11 @@ struct gns_ex {
     uint64_t pkt = 0, batches = 0;
     uint64_t bmax = 0;
     uint32_t nblk_max = 0;
-    uint32_t *keyid = nullptr;
+    uint32_t *skey[2] = {nullptr, nullptr};  // X2 sort keys (in, out)
+    uint64_t *sval[2] = {nullptr, nullptr};  // X2 sort values (in, out)
+    void *sort_tmp = nullptr;                // rocPRIM radix sort scratch
+    size_t sort_tmp_bytes = 0;
+    uint32_t key_bits = 0;                   // sort key bits: flow ids < slots, invalid = slots
     uint64_t *pend[2] = {nullptr, nullptr};
     uint32_t *pcnt[2] = {nullptr, nullptr};
     uint32_t *ptotal = nullptr;
@@ -361,8 +349,9 @@ int ex_set_dev(gns_ex *ex) {
 
 void ex_free_all(gns_ex *ex) {
     dfree(ex->D.rec); dfree(ex->f.pkts); dfree(ex->f.bytes); dfree(ex->f.first); dfree(ex->f.last);
-    dfree(ex->f.start); dfree(ex->f.end); dfree(ex->keyid); dfree(ex->pend[0]); dfree(ex->pend[1]);
+    dfree(ex->f.start); dfree(ex->f.end); dfree(ex->pend[0]); dfree(ex->pend[1]);
     dfree(ex->pcnt[0]); dfree(ex->pcnt[1]); dfree(ex->ptotal); dfree(ex->stats); dfree(ex->stage);
+    dfree(ex->skey[0]); dfree(ex->skey[1]); dfree(ex->sval[0]); dfree(ex->sval[1]); dfree(ex->sort_tmp);
     if (ex->h_pin) (void)hipHostFree(ex->h_pin);
     ex->timer.destroy();
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
@@ -386,7 +375,8 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     GNS_HIP(hipMemsetAsync(ex->ptotal, 0, 8, s));
     if (++ex->epoch == 0) ex->epoch = 1;
     ExArgs x{};
-    x.x = xin; x.n = n; x.kp = ex->kp; x.D = ex->D; x.epoch = ex->epoch; x.keyid = ex->keyid;
+    x.x = xin; x.n = n; x.kp = ex->kp; x.D = ex->D; x.epoch = ex->epoch;
+    x.skey = ex->skey[0]; x.sval = ex->sval[0]; x.none_key = (uint32_t)ex->slots;
     x.pend = ex->pend[0]; x.pend_cnt = ex->pcnt[0]; x.pend_total = ex->ptotal; x.stats = ex->stats;
     {
         ScopedStage st(ex->timer, 0);
@@ -412,16 +402,18 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
         GNS_HIP(hipGetLastError());
         cur ^= 1;
     }
+    const uint32_t none_key = (uint32_t)ex->slots;
     {
         ScopedStage st(ex->timer, 2);
-        ExAggArgs g{ex->keyid, xin.in.sizes, n, ex->pkt, ex->f};
-        hipLaunchKernelGGL(k_ex_aggregate, dim3(nblk), dim3(kXThreads), 0, s, g);
-        GNS_HIP(hipGetLastError());
+        size_t tb = ex->sort_tmp_bytes;
+        GNS_HIP(rocprim::radix_sort_pairs(ex->sort_tmp, tb, ex->skey[0], ex->skey[1], ex->sval[0], ex->sval[1],
+                                          (size_t)n, 0u, ex->key_bits, s));
     }
     {
         ScopedStage st(ex->timer, 3);
-        hipLaunchKernelGGL(k_ex_times, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ex->keyid, xin.ts, n,
-                           ex->pkt, ex->f);
+        const uint64_t nt = (n + kRunItems - 1) / kRunItems;
+        hipLaunchKernelGGL(k_ex_runs, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, ex->skey[1], ex->sval[1],
+                           n, none_key, xin.ts, ex->pkt, ex->f);
         GNS_HIP(hipGetLastError());
     }
     ex->pkt += n;
@@ -541,11 +533,25 @@ int gns_ex_create(const gns_ex_params *p, gns_ex **out) {
         if ((rc = dalloc_t(&ex->D.rec, slots * ex->D.RW)) || (rc = dalloc_t(&ex->f.pkts, slots)) ||
             (rc = dalloc_t(&ex->f.bytes, slots)) || (rc = dalloc_t(&ex->f.first, slots)) ||
             (rc = dalloc_t(&ex->f.last, slots)) || (rc = dalloc_t(&ex->f.start, slots)) ||
-            (rc = dalloc_t(&ex->f.end, slots)) || (rc = dalloc_t(&ex->keyid, ex->bmax)) ||
+            (rc = dalloc_t(&ex->f.end, slots)) ||
             (rc = dalloc_t(&ex->pend[0], ex->bmax)) || (rc = dalloc_t(&ex->pend[1], ex->bmax)) ||
             (rc = dalloc_t(&ex->pcnt[0], ex->nblk_max)) || (rc = dalloc_t(&ex->pcnt[1], ex->nblk_max)) ||
-            (rc = dalloc_t(&ex->ptotal, 2)) || (rc = dalloc_t(&ex->stats, 8)))
+            (rc = dalloc_t(&ex->ptotal, 2)) || (rc = dalloc_t(&ex->stats, 8)) ||
+            (rc = dalloc_t(&ex->skey[0], ex->bmax)) || (rc = dalloc_t(&ex->skey[1], ex->bmax)) ||
+            (rc = dalloc_t(&ex->sval[0], ex->bmax)) || (rc = dalloc_t(&ex->sval[1], ex->bmax)))
             break;
+        {   // sort keys: flow ids < slots, invalid packets = slots
+            uint32_t kb = 1;
+            while ((1ull << kb) <= slots) kb++;
+            ex->key_bits = kb;
+            size_t t1 = 0;
+            if (rocprim::radix_sort_pairs(nullptr, t1, ex->skey[0], ex->skey[1], ex->sval[0], ex->sval[1],
+                                          (size_t)ex->bmax, 0u, kb, ex->stream) != hipSuccess) {
+                set_error("rocPRIM scratch query failed"); rc = GNS_E_HIP; break;
+            }
+            ex->sort_tmp_bytes = t1;
+            if ((rc = dalloc(&ex->sort_tmp, ex->sort_tmp_bytes)) != GNS_OK) break;
+        }
         if (hipHostMalloc(reinterpret_cast<void **>(&ex->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
         }
