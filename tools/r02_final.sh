@@ -10,7 +10,8 @@ timeout -k 10 300 python bench.py > gpurun_out/fin_bench.json 2> gpurun_out/fin_
 timeout -k 10 200 python bench.py --sketch superspread --no-cpu > gpurun_out/fin_ss_bench.json 2>&1 || exit 4
 timeout -k 10 200 python bench.py --width 16777216 --depth 8 --no-cpu --steps 3 --warmup 1 > gpurun_out/fin_c5_bench.json 2>&1 || exit 5
 timeout -k 10 300 python bench.py --sketch hybrid --steps 5 --warmup 1 > gpurun_out/fin_hybrid_bench.json 2>&1 || exit 6
+timeout -k 10 200 python bench.py --sketch exact --no-cpu > gpurun_out/fin_exact_bench.json 2>&1 || exit 8
 tools/pmc_cm.sh || exit 7
-for f in fin_bench fin_ss_bench fin_c5_bench fin_hybrid_bench; do
+for f in fin_bench fin_ss_bench fin_c5_bench fin_hybrid_bench fin_exact_bench; do
   python3 -c "import json; d=json.loads(open('gpurun_out/$f.json').read().strip().splitlines()[-1]); print('$f', d['value'], d.get('stage_ms_per_step'))"
 done
