@@ -305,7 +305,7 @@ def bench_thrift(args, torch, dist, world, rank, local):
     rwl = torch.empty((n,), dtype=torch.int32, device=f"cuda:{local}")
     rts = torch.empty((n,), dtype=torch.int64, device=f"cuda:{local}")
     L = _lib.load()
-    cm = CountMin(WIDTH, DEPTH, 1 << 20, 1000, flow_fields=FIELDS, seeds=row_seeds(DEPTH), max_flows=1 << 21,
+    cm = CountMin(WIDTH, DEPTH, 1 << 20, 1000, flow_fields=FIELDS, seeds=row_seeds(DEPTH), max_flows=args.max_flows,
                   batch_packets=n, device=local)
     bad = ct.c_uint64(0)
 
@@ -378,7 +378,7 @@ def bench_hybrid(args, torch, dist, world, rank, local):
     ts = torch.arange(n, dtype=torch.int64, device=f"cuda:{local}") * 100 + 1_700_000_000_000_000_000
     batch = HeaderBatch(hdr, wl, ts)
     ex = ExactTask("per_five_tuple", FIELDS, 128, device=local, max_flows=1 << 21, batch_packets=args.batch or n)
-    cm = CountMin(W, D, 1 << 20, 1000, flow_fields=FIELDS, seeds=row_seeds(D), max_flows=1 << 21,
+    cm = CountMin(W, D, 1 << 20, 1000, flow_fields=FIELDS, seeds=row_seeds(D), max_flows=args.max_flows,
                   batch_packets=args.batch or n, device=local)
     view = cm.view()
     # point-query keys: the 5-tuple keys of 2^16 packets of the stream (host copy, made once)
@@ -475,6 +475,46 @@ def bench_hybrid(args, torch, dist, world, rank, local):
         dist.destroy_process_group()
 
 
+def bench_windows(args, torch, dist, world, cm, step, barrier, n):
+    """configs[3]'s per-window cycle, timed after the headline steps: each window
+    inserts one step's packets, takes the shard's heavy hitters on the device
+    (gns_cm_heavy_hitters: candidates, dedupe, order) and all-gathers every
+    shard's list over RCCL (dist.allgather_heavy_arrays; flows are disjoint across
+    shards, so the union is the global list).  Max over ranks, like the steps."""
+    from go2netspectra_amd.dist import allgather_heavy_arrays
+    t_ins = t_hh = t_x = 0.0
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.windows):
+        a = time.perf_counter()
+        step()
+        cm.flush()
+        b = time.perf_counter()
+        arrs = cm.heavy_hitters_arrays()
+        c = time.perf_counter()
+        if world > 1:
+            arrs = allgather_heavy_arrays(arrs, world)
+        e = time.perf_counter()
+        t_ins += b - a
+        t_hh += c - b
+        t_x += e - c
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    W = args.windows
+    return {"windows": W, "value": round(n * W * world / el / 1e6, 2), "unit": "Mpackets/s",
+            "ms_per_window": round(el / W * 1e3, 3), "insert_ms": round(t_ins / W * 1e3, 3),
+            "heavy_hitters_ms": round(t_hh / W * 1e3, 3), "exchange_ms": round(t_x / W * 1e3, 3),
+            "global_heavy_hitters": {"count": int(len(arrs[1])), "size": int(len(arrs[3]))},
+            "collective": ("all-gather of packed (flow | value) rows, " + dist.get_backend()) if world > 1
+            else "none (one shard: the device list is already the global one)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -488,8 +528,11 @@ def main():
     ap.add_argument("--sketch", choices=["countmin", "superspread", "exact", "thrift", "hybrid"], default="countmin",
                     help="superspread = configs[2]; hybrid = configs[4]; exact = the exact aggregator "
                          "(none of them is the headline metric)")
-    ap.add_argument("--max-flows", type=int, default=1 << 21,
+    ap.add_argument("--max-flows", type=int, default=1 << 22,
                     help="flow dictionary capacity (slots = next power of two >= 2x)")
+    ap.add_argument("--windows", type=int, default=3,
+                    help="after the timed steps: W timed windows of insert + device heavy hitters + "
+                         "all-gather of every shard's list (configs[3] per-window exchange); 0 = off")
     ap.add_argument("--key", choices=["5tuple", "srcip"], default="5tuple",
                     help="flow key: full 5-tuple (37 B, primary) or [SrcIP] (16 B, the default task layout)")
     ap.add_argument("--flows", type=int, default=1 << 20,
@@ -603,7 +646,10 @@ def main():
     stages = cm.stage_times()
     counters = cm.counters()
 
-    # per-window exchange: all-gather heavy-hitter candidates (not timed)
+    window = None
+    if args.windows > 0 and not args.host_input:
+        window = bench_windows(args, torch, dist, world, cm, step, barrier, n)
+
     hh = cm.heavy_hitters()
     if world > 1:
         from go2netspectra_amd.dist import allgather_heavy
@@ -646,6 +692,8 @@ def main():
         "heavy_hitters": {"count": len(hh.Count), "size": len(hh.Size or [])},
         "engine_counters": counters,
     }
+    if window is not None:
+        line["window_exchange"] = window
     if (args.width, args.depth) != (WIDTH, DEPTH):
         wl2 = f"2^{args.width.bit_length() - 1}" if args.width & (args.width - 1) == 0 else str(args.width)
         line["metric"] = f"Mpackets/s CMS update (device-resident, d={args.depth} w={wl2})"

@@ -116,6 +116,61 @@ def allgather_heavy(hh: HeavyRecord, world: int) -> HeavyRecord:
     return HeavyRecord(Size=[HeavySize(f, v) for f, v in merged_s], Count=[HeavyCount(f, v) for f, v in merged_c])
 
 
+def merge_heavy_arrays(flows: np.ndarray, vals: np.ndarray):
+    """Union of flow-disjoint per-shard lists in canonical order: value desc, then
+    flow bytes asc (the tie order of CountMin.heavy_hitters, count_min.go:232-239).
+    Sorted on one 64-bit key (inverted value, first four key bytes); only runs
+    that tie on both are ordered by their full key bytes.  Shards own disjoint
+    flows (shard_of), so no flow appears twice."""
+    flows = np.ascontiguousarray(flows, np.uint8)
+    vals = np.asarray(vals, np.uint32)
+    n = len(vals)
+    if n == 0:
+        return flows, vals
+    K = flows.shape[1]
+    head = np.zeros((n, 4), np.uint8)
+    head[:, : min(K, 4)] = flows[:, : min(K, 4)]
+    comp = ((np.uint64(0xFFFFFFFF) - vals.astype(np.uint64)) << np.uint64(32)) | \
+        head.view(">u4").reshape(-1).astype(np.uint64)
+    o = np.argsort(comp, kind="stable")
+    c = comp[o]
+    tie = np.flatnonzero(c[1:] == c[:-1])
+    if len(tie):
+        i = 0
+        while i < len(tie):
+            a = tie[i]
+            b = a + 1
+            while i < len(tie) and tie[i] == b - 1:
+                b += 1
+                i += 1
+            run = o[a:b]
+            o[a:b] = run[sorted(range(len(run)), key=lambda j: flows[run[j]].tobytes())]
+    return flows[o], vals[o]
+
+
+def allgather_heavy_arrays(arrays, world: int):
+    """Per-window exchange on the array form of HeavyHitters (CountMin.heavy_hitters_arrays:
+    count flows [n,K], counts, size flows, sizes): two RCCL all-gathers of packed
+    (flow | value) rows, then the union in canonical order.  Same result as
+    allgather_heavy without per-flow Python objects (a 2^20-bucket window has ~10^5)."""
+    cf, cv, sf, sv = arrays
+    K = cf.shape[1] if cf.ndim == 2 else sf.shape[1]
+
+    def pack(f, v):
+        rows = np.zeros((len(v), K + 4), np.uint8)
+        if len(v):
+            rows[:, :K] = f[:, :K]
+            rows[:, K:] = np.ascontiguousarray(v, "<u4").view(np.uint8).reshape(-1, 4)
+        return rows
+
+    out = []
+    for f, v in ((cf, cv), (sf, sv)):
+        g = _allgather_rows(pack(f, v), world)
+        gv = np.ascontiguousarray(g[:, K:]).view("<u4").reshape(-1).astype(np.uint32)
+        out.extend(merge_heavy_arrays(g[:, :K], gv))
+    return tuple(out)
+
+
 # ---------------------------------------------------------------------------
 # Exact global mode (SURVEY §8e "exact global alternative"): every GPU sees the
 # whole stream but applies only the updates that fall in its slice of bucket

@@ -43,7 +43,7 @@ def _worker(rank, world, port, q):
     import sys
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
-    from go2netspectra_amd.dist import allgather_heavy
+    from go2netspectra_amd.dist import allgather_heavy, allgather_heavy_arrays
     from go2netspectra_amd.packets import PacketBatch
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -52,8 +52,16 @@ def _worker(rank, world, port, q):
     batch = PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"])
     hh, n = _shard_sketch(batch, rank, world)
     merged = allgather_heavy(hh, world)
+    # the array form (CountMin.heavy_hitters_arrays -> bench.py's per-window exchange)
+    def arr(items):
+        f = np.array([np.frombuffer(x, np.uint8) for x, _ in items], np.uint8).reshape(len(items), 16)
+        return f, np.array([v for _, v in items], np.uint32)
+    cf, cv = arr([(h.Flow, h.Count) for h in hh.Count])
+    sf, sv = arr([(h.Flow, h.Size) for h in hh.Size])
+    ga = allgather_heavy_arrays((cf, cv, sf, sv), world)
     if rank == 0:
-        q.put(([(h.Flow, h.Count) for h in merged.Count], [(h.Flow, h.Size) for h in merged.Size]))
+        q.put(([(h.Flow, h.Count) for h in merged.Count], [(h.Flow, h.Size) for h in merged.Size],
+               [(bytes(f), int(v)) for f, v in zip(ga[0], ga[1])], [(bytes(f), int(v)) for f, v in zip(ga[2], ga[3])]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -70,7 +78,7 @@ def test_two_rank_shard_and_allgather():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got_c, got_s = q.get(timeout=120)
+    got_c, got_s, arr_c, arr_s = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -85,6 +93,7 @@ def test_two_rank_shard_and_allgather():
         total += n
     assert total == len(batch)
     assert got_c == merge_heavy(lists_c) and got_s == merge_heavy(lists_s)
+    assert arr_c == got_c and arr_s == got_s
     assert len(got_c) > 0
 
 
