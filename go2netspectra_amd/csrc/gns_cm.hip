@@ -260,6 +260,9 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
     uint32_t rec[16];
     int res = CM_FULL;
     uint32_t out = 0;
+    // first probe (the home slot, loaded by the caller): 0 hit, 1 claimed in this
+    // launch, 2 empty, 3 another committed key (the key lies further along the chain)
+    int first = 0;
     if (ok) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -270,9 +273,45 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 #pragma unroll
         for (int i = 0; i < GNS_KWMAX; i++)
             if ((uint32_t)i < ((K + 3) >> 2)) eq = eq && (rec[1 + i] == kw[i]);
-        if (tag == a.epoch) { res = CM_PENDING; out = slot0; }
-        else if (eq) { res = CM_FOUND; out = slot0; }
-        else res = cm_find_or_claim(a.D, kw, K, tag == 0 ? slot0 : ((slot0 + 1u) & a.D.mask), a.epoch, &out, rec);
+        first = tag == a.epoch ? 1 : (eq ? 0 : (tag == 0 ? 2 : 3));
+        if (first == 0) { res = CM_FOUND; out = slot0; }
+        else if (first == 1) { res = CM_PENDING; out = slot0; }
+    }
+    // row buckets: from the record's cache (rows 0..3 of a committed flow), else hashed
+    uint32_t bk[RMAX];
+    const bool cached = bw && ok && first == 0;
+#pragma unroll
+    for (uint32_t rr = 0; rr < RMAX; rr++) bk[rr] = (rr < 4 && cached) ? rec[12 + rr] : 0u;
+    if (__ballot(ok && !cached) || (RMAX > 4 && d > 4)) {
+        uint32_t mk[GNS_KWMAX];
+        mm3_premix<GNS_KWMAX>(kw, K, mk);
+#pragma unroll
+        for (uint32_t rr = 0; rr < RMAX; rr++) {
+            if (rr >= d) break;
+            if (ok && (!cached || rr >= 4)) bk[rr] = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, K, a.g.seeds[rr]));
+        }
+    }
+    // designated-bucket slots of the row buckets (LDS lookups, reused by the rows loop)
+    int hs[RMAX];
+    bool anyhot = false;
+#pragma unroll
+    for (uint32_t rr = 0; rr < RMAX; rr++) {
+        hs[rr] = -1;
+        if (rr >= d) break;
+        if (ok) hs[rr] = hot_lookup(s_tab + rr * kHotTab, bk[rr]);
+        anyhot = anyhot || hs[rr] >= 0;
+    }
+    if (ok && first >= 2) {
+        // A committed flow displaced from its home slot is parked like a first-sight
+        // packet (k_resolve walks the rest of the chain next launch; its bucket codes
+        // are already hashed) instead of stalling the wave on a dependent probe.  The
+        // summaries treat a parked packet as foreign to every owner, which is exact
+        // only for a flow that owns no bucket: so a packet that touches a designated
+        // bucket walks the chain here.  An empty home slot is claimed here.
+        if (first == 3 && !anyhot) { res = CM_PENDING; out = (slot0 + 1u) & a.D.mask; }
+        else res = cm_find_or_claim(a.D, kw, K, first == 2 ? slot0 : ((slot0 + 1u) & a.D.mask), a.epoch, &out, rec);
+    }
+    if (ok) {
         if (res == CM_FULL) {
             a.keyid[p] = GNS_ID_NONE;
             atomicAdd(&s_full, 1u);
@@ -284,20 +323,6 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
         } else {
             a.keyid[p] = out;
             kid = out;
-        }
-    }
-    // row buckets: from the record's cache (rows 0..3 of a committed flow), else hashed
-    uint32_t bk[RMAX];
-    const bool cached = bw && res == CM_FOUND;
-#pragma unroll
-    for (uint32_t rr = 0; rr < RMAX; rr++) bk[rr] = (rr < 4 && cached) ? rec[12 + rr] : 0u;
-    if (__ballot(ok && !cached) || (RMAX > 4 && d > 4)) {
-        uint32_t mk[GNS_KWMAX];
-        mm3_premix<GNS_KWMAX>(kw, K, mk);
-#pragma unroll
-        for (uint32_t rr = 0; rr < RMAX; rr++) {
-            if (rr >= d) break;
-            if (ok && (!cached || rr >= 4)) bk[rr] = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, K, a.g.seeds[rr]));
         }
     }
     if (bw && res == CM_CLAIMED) {  // publish the bucket cache with the key (visible next launch)
@@ -315,7 +340,7 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
         int h = -1;
         if (ok) {
             const uint32_t b = bk[rr];
-            h = hot_lookup(s_tab + rr * kHotTab, b);
+            h = hs[rr];
             // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
 #ifndef GNS_ABL_NOIDX
             a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
@@ -525,10 +550,14 @@ __global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
     __shared__ uint32_t s_cnt, s_full;
     __shared__ uint8_t s_src[80];
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    const uint32_t cnt = a.cnt_in[blk];
+    if (cnt == 0) {  // block-uniform
+        if (tid == 0) a.cnt_out[blk] = 0;
+        return;
+    }
     stage_plan<MODE>(a.kp, s_src);
     if (tid == 0) { s_cnt = 0; s_full = 0; }
     __syncthreads();
-    const uint32_t cnt = a.cnt_in[blk];
     const uint64_t beg = (uint64_t)blk * kChunk;
     for (uint32_t i = tid; i < cnt; i += kExThreads) {
         const uint64_t v = a.pend_in[beg + i];
@@ -2560,18 +2589,22 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
             hipLaunchKernelGGL((k_extract<KIND, MODE, 0, 0, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
         GNS_HIP(hipGetLastError());
     }
-    // K1b: resolve parked packets until none remain
+    // K1b: resolve parked packets until none remain.  The first round is queued
+    // behind K1 without a host round trip (K1 parks the flows displaced from their
+    // home slot, so most batches have parked packets; a block with none exits at once).
     int cur = 0;
     for (int round = 0;; round++) {
-        GNS_HIP(hipMemcpyAsync(cm->h_pin, cm->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
-        GNS_HIP(hipMemcpyAsync(cm->h_pin + 2, cm->stats + 3, 8, hipMemcpyDeviceToHost, s));
-        GNS_HIP(hipStreamSynchronize(s));
-        if (cm->h_pin[2] | cm->h_pin[3]) {
-            set_error("flow dictionary full (%llu slots); raise max_flows",
-                      (unsigned long long)cm->dict_slots);
-            return GNS_E_FULL;
+        if (round > 0) {
+            GNS_HIP(hipMemcpyAsync(cm->h_pin, cm->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
+            GNS_HIP(hipMemcpyAsync(cm->h_pin + 2, cm->stats + 3, 8, hipMemcpyDeviceToHost, s));
+            GNS_HIP(hipStreamSynchronize(s));
+            if (cm->h_pin[2] | cm->h_pin[3]) {
+                set_error("flow dictionary full (%llu slots); raise max_flows",
+                          (unsigned long long)cm->dict_slots);
+                return GNS_E_FULL;
+            }
+            if (cm->h_pin[0] == 0) break;
         }
-        if (cm->h_pin[0] == 0) break;
         if (round > 64) { set_error("dictionary resolve did not converge"); return GNS_E_FULL; }
         GNS_HIP(hipMemsetAsync(cm->ptotal + (cur ^ 1), 0, 4, s));
         if (++cm->epoch == 0) cm->epoch = 1;
