@@ -48,12 +48,10 @@ __device__ __forceinline__ void to16(uint32_t (&tw)[10], uint32_t sver, uint32_t
     if (dver == 4u) { tw[7] = tw[4]; tw[4] = 0u; tw[5] = 0u; tw[6] = 0xFFFF0000u; }
 }
 
+// canonical tuple words (load_tuple) -> exact key with To16 IP fields
 template <int KIND, int MODE>
-__device__ __forceinline__ int ex_key(const ExIn &x, uint32_t K, const uint8_t *s_src, uint64_t p,
-                                      uint32_t (&kw)[GNS_KWMAX]) {
-    uint32_t tw[10];
-    const int st = load_tuple<KIND>(x.in, p, tw);
-    if (st != PARSE_OK) return st;
+__device__ __forceinline__ int ex_key_tw(const ExIn &x, uint32_t K, const uint8_t *s_src, uint64_t p,
+                                         uint32_t (&tw)[10], uint32_t (&kw)[GNS_KWMAX]) {
     uint32_t sv, dv;
     if constexpr (KIND == IN_HDR) { sv = tw[9] >> 24; dv = (tw[9] >> 16) & 0xFFu; }
     else { sv = dv = x.ipver ? x.ipver[p] : 4u; }
@@ -64,6 +62,15 @@ __device__ __forceinline__ int ex_key(const ExIn &x, uint32_t K, const uint8_t *
     tw[9] &= 0xFFu;
     make_key_m<MODE, GNS_KWMAX>(K, s_src, tw, kw);
     return PARSE_OK;
+}
+
+template <int KIND, int MODE>
+__device__ __forceinline__ int ex_key(const ExIn &x, uint32_t K, const uint8_t *s_src, uint64_t p,
+                                      uint32_t (&kw)[GNS_KWMAX]) {
+    uint32_t tw[10];
+    const int st = load_tuple<KIND>(x.in, p, tw);
+    if (st != PARSE_OK) return st;
+    return ex_key_tw<KIND, MODE>(x, K, s_src, p, tw, kw);
 }
 
 struct ExArgs {
@@ -80,6 +87,53 @@ struct ExArgs {
     unsigned long long *stats;  // 0 inserted, 1 dropped, 2 unsupported, 3 dict full
 };
 
+// Home-slot record of a key (issued early; consumed by ex_consume).
+__device__ __forceinline__ void ex_probe_issue(const DictDev &D, uint32_t slot, uint4 (&r4)[4]) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(D.rec + (size_t)slot * D.RW);
+#pragma unroll
+    for (int i = 0; i < 4; i++) r4[i] = (4u * i < D.RW) ? q[i] : make_uint4(0, 0, 0, 0);
+}
+
+// X1 second half for one packet: resolve the home-slot probe.  A hit gives the
+// flow id; a flow displaced from its home slot by another committed key is parked
+// (k_ex_resolve walks the rest of the chain in the next launch) instead of
+// stalling the wave on dependent probes; an empty home slot is claimed here.
+__device__ __forceinline__ void ex_consume(const ExArgs &a, uint64_t p, uint64_t beg, bool ok,
+                                           const uint32_t (&kw)[GNS_KWMAX], uint32_t K, uint32_t slot0,
+                                           const uint4 (&r4)[4], uint32_t *s_pend, uint32_t *s_full,
+                                           uint32_t &n_ok) {
+    if (!ok) return;
+    uint32_t rec[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        rec[4 * i] = r4[i].x; rec[4 * i + 1] = r4[i].y; rec[4 * i + 2] = r4[i].z; rec[4 * i + 3] = r4[i].w;
+    }
+    const uint32_t tag = rec[0];
+    bool eq = tag != 0 && tag != a.epoch;
+#pragma unroll
+    for (int i = 0; i < GNS_KWMAX; i++)
+        if ((uint32_t)i < ((K + 3) >> 2)) eq = eq && (rec[1 + i] == kw[i]);
+    uint32_t out = slot0;
+    int r = DICT_FOUND;
+    if (!eq) {
+        if (tag == a.epoch) r = DICT_PENDING;                                    // claimed in this launch
+        else if (tag != 0) { r = DICT_PENDING; out = (slot0 + 1u) & a.D.mask; }  // displaced
+        else r = dict_find_or_claim(a.D, kw, slot0, a.epoch, &out);              // empty: claim
+    }
+    if (r == DICT_FULL) {
+        a.skey[p] = a.none_key;
+        atomicAdd(s_full, 1u);
+        return;
+    }
+    n_ok++;
+    if (r == DICT_FOUND) {
+        a.skey[p] = out;
+    } else {
+        a.skey[p] = a.none_key;
+        a.pend[beg + atomicAdd(s_pend, 1u)] = (uint64_t)(p - beg) << 32 | out;
+    }
+}
+
 template <int KIND, int MODE>
 __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
     __shared__ uint8_t s_src[80];
@@ -92,28 +146,73 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
     const uint64_t beg = (uint64_t)blk * kXChunk;
     const uint64_t end = min(a.n, beg + kXChunk);
     uint32_t n_ok = 0;
-    for (uint64_t p = beg + tid; p < end; p += kXThreads) {
-        uint32_t kw[GNS_KWMAX];
-        a.sval[p] = p << 32 | a.x.in.sizes[p];
-        const int st = ex_key<KIND, MODE>(a.x, K, s_src, p, kw);
-        if (st != PARSE_OK) {
-            a.skey[p] = a.none_key;
-            atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
-            continue;
+    if constexpr (KIND == IN_HDR) {
+        // Two-stage software pipeline (as Count-Min's K1): iteration k parses packet
+        // k+1 and issues its home-slot probe (and the record prefetch of packet k+2),
+        // then consumes packet k, whose probe was issued one iteration earlier.
+        uint4 hv[4];
+        uint32_t hsz;
+        auto load_hdr = [&](uint64_t q) {
+            const uint64_t pc = min(q, end - 1);
+            const uint4 *r = reinterpret_cast<const uint4 *>(a.x.in.hdr + pc * 16);
+#pragma unroll
+            for (int i = 0; i < 4; i++) hv[i] = r[i];
+            hsz = a.x.in.sizes[pc];
+        };
+        auto stage_b = [&](uint64_t q, bool &okq, uint32_t (&kwq)[GNS_KWMAX], uint32_t &slotq, uint4 (&r4q)[4]) {
+            okq = q < end;
+            uint32_t cw[16];
+#pragma unroll
+            for (int i = 0; i < 4; i++) { cw[4 * i] = hv[i].x; cw[4 * i + 1] = hv[i].y; cw[4 * i + 2] = hv[i].z; cw[4 * i + 3] = hv[i].w; }
+            const uint32_t szq = hsz;
+            load_hdr(q + kXThreads);
+#pragma unroll
+            for (int i = 0; i < GNS_KWMAX; i++) kwq[i] = 0;
+            if (okq) {
+                a.sval[q] = q << 32 | szq;
+                uint32_t tw[10];
+                int st = parse_record_fast(cw, szq, true, tw);
+                if (st == PARSE_OK) st = ex_key_tw<KIND, MODE>(a.x, K, s_src, q, tw, kwq);
+                if (st != PARSE_OK) {
+                    a.skey[q] = a.none_key;
+                    atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
+                    okq = false;
+                }
+            }
+            slotq = mm3_n<GNS_KWMAX>(kwq, K, a.D.seed) & a.D.mask;
+            if (okq) ex_probe_issue(a.D, slotq, r4q);
+        };
+        load_hdr(beg + tid);
+        bool okc;
+        uint32_t kwc[GNS_KWMAX], slotc;
+        uint4 r4c[4];
+        stage_b(beg + tid, okc, kwc, slotc, r4c);
+        for (uint64_t p0 = beg; p0 < end; p0 += kXThreads) {  // wave-uniform trip count
+            bool okn = false;
+            uint32_t kwn[GNS_KWMAX], slotn = 0;
+            uint4 r4n[4];
+            if (p0 + kXThreads < end) stage_b(p0 + kXThreads + tid, okn, kwn, slotn, r4n);
+            ex_consume(a, p0 + tid, beg, okc, kwc, K, slotc, r4c, &s_pend, &s_full, n_ok);
+            okc = okn; slotc = slotn;
+#pragma unroll
+            for (int i = 0; i < GNS_KWMAX; i++) kwc[i] = kwn[i];
+#pragma unroll
+            for (int i = 0; i < 4; i++) r4c[i] = r4n[i];
         }
-        uint32_t out;
-        const int r = dict_find_or_claim(a.D, kw, mm3_n<GNS_KWMAX>(kw, K, a.D.seed) & a.D.mask, a.epoch, &out);
-        if (r == DICT_FULL) {
-            a.skey[p] = a.none_key;
-            atomicAdd(&s_full, 1u);
-            continue;
-        }
-        n_ok++;
-        if (r == DICT_FOUND) {
-            a.skey[p] = out;
-        } else {
-            a.skey[p] = a.none_key;
-            a.pend[beg + atomicAdd(&s_pend, 1u)] = (uint64_t)(p - beg) << 32 | out;
+    } else {
+        for (uint64_t p = beg + tid; p < end; p += kXThreads) {
+            uint32_t kw[GNS_KWMAX];
+            a.sval[p] = p << 32 | a.x.in.sizes[p];
+            const int st = ex_key<KIND, MODE>(a.x, K, s_src, p, kw);
+            if (st != PARSE_OK) {
+                a.skey[p] = a.none_key;
+                atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
+                continue;
+            }
+            const uint32_t slot0 = mm3_n<GNS_KWMAX>(kw, K, a.D.seed) & a.D.mask;
+            uint4 r4[4];
+            ex_probe_issue(a.D, slot0, r4);
+            ex_consume(a, p, beg, true, kw, K, slot0, r4, &s_pend, &s_full, n_ok);
         }
     }
     atomicAdd(&s_ok, n_ok);
@@ -142,10 +241,14 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
     __shared__ uint32_t s_cnt, s_full;
     const ExArgs &a = r.x;
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    const uint32_t cnt = r.cnt_in[blk];
+    if (cnt == 0) {  // block-uniform
+        if (tid == 0) r.cnt_out[blk] = 0;
+        return;
+    }
     stage_plan<MODE>(a.kp, s_src);
     if (tid == 0) { s_cnt = 0; s_full = 0; }
     __syncthreads();
-    const uint32_t cnt = r.cnt_in[blk];
     const uint64_t beg = (uint64_t)blk * kXChunk;
     for (uint32_t i = tid; i < cnt; i += kXThreads) {
         const uint64_t v = r.pend_in[beg + i];
@@ -383,13 +486,17 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
         hipLaunchKernelGGL((k_ex_extract<KIND, MODE>), dim3(nblk), dim3(kXThreads), 0, s, x);
         GNS_HIP(hipGetLastError());
     }
+    // resolve rounds; the first is queued behind X1 without a host round trip (X1
+    // parks the flows displaced from their home slot; a block with none exits at once)
     int cur = 0;
     for (int round = 0;; round++) {
-        GNS_HIP(hipMemcpyAsync(ex->h_pin, ex->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
-        GNS_HIP(hipMemcpyAsync(ex->h_pin + 2, ex->stats + 3, 8, hipMemcpyDeviceToHost, s));
-        GNS_HIP(hipStreamSynchronize(s));
-        if (ex->h_pin[2] | ex->h_pin[3]) { set_error("flow dictionary full; raise max_flows"); return GNS_E_FULL; }
-        if (ex->h_pin[0] == 0) break;
+        if (round > 0) {
+            GNS_HIP(hipMemcpyAsync(ex->h_pin, ex->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
+            GNS_HIP(hipMemcpyAsync(ex->h_pin + 2, ex->stats + 3, 8, hipMemcpyDeviceToHost, s));
+            GNS_HIP(hipStreamSynchronize(s));
+            if (ex->h_pin[2] | ex->h_pin[3]) { set_error("flow dictionary full; raise max_flows"); return GNS_E_FULL; }
+            if (ex->h_pin[0] == 0) break;
+        }
         if (round > 64) { set_error("dictionary resolve did not converge"); return GNS_E_FULL; }
         GNS_HIP(hipMemsetAsync(ex->ptotal + (cur ^ 1), 0, 4, s));
         if (++ex->epoch == 0) ex->epoch = 1;
