@@ -477,7 +477,7 @@ def bench_hybrid(args, torch, dist, world, rank, local):
 
 def bench_windows(args, torch, dist, world, cm, step, barrier, n):
     """configs[3]'s per-window cycle, timed after the headline steps: each window
-    inserts one step's packets, takes the shard's heavy hitters on the device
+    inserts --window-steps steps of packets, takes the shard's heavy hitters on the device
     (gns_cm_heavy_hitters: candidates, dedupe, order) and all-gathers every
     shard's list over RCCL (dist.allgather_heavy_arrays; flows are disjoint across
     shards, so the union is the global list).  Max over ranks, like the steps."""
@@ -488,7 +488,8 @@ def bench_windows(args, torch, dist, world, cm, step, barrier, n):
     t0 = time.perf_counter()
     for _ in range(args.windows):
         a = time.perf_counter()
-        step()
+        for _ in range(args.window_steps):
+            step()
         cm.flush()
         b = time.perf_counter()
         arrs = cm.heavy_hitters_arrays()
@@ -507,7 +508,8 @@ def bench_windows(args, torch, dist, world, cm, step, barrier, n):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     W = args.windows
-    return {"windows": W, "value": round(n * W * world / el / 1e6, 2), "unit": "Mpackets/s",
+    return {"windows": W, "steps_per_window": args.window_steps,
+            "value": round(n * args.window_steps * W * world / el / 1e6, 2), "unit": "Mpackets/s",
             "ms_per_window": round(el / W * 1e3, 3), "insert_ms": round(t_ins / W * 1e3, 3),
             "heavy_hitters_ms": round(t_hh / W * 1e3, 3), "exchange_ms": round(t_x / W * 1e3, 3),
             "global_heavy_hitters": {"count": int(len(arrs[1])), "size": int(len(arrs[3]))},
@@ -533,6 +535,8 @@ def main():
     ap.add_argument("--windows", type=int, default=3,
                     help="after the timed steps: W timed windows of insert + device heavy hitters + "
                          "all-gather of every shard's list (configs[3] per-window exchange); 0 = off")
+    ap.add_argument("--window-steps", type=int, default=20,
+                    help="steps per window (20 x 100M packets per GPU = 0.1 s of ingest; configs[3] says 1 s)")
     ap.add_argument("--key", choices=["5tuple", "srcip"], default="5tuple",
                     help="flow key: full 5-tuple (37 B, primary) or [SrcIP] (16 B, the default task layout)")
     ap.add_argument("--flows", type=int, default=1 << 20,
