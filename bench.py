@@ -483,6 +483,9 @@ def bench_windows(args, torch, dist, world, cm, step, barrier, n):
     shards, so the union is the global list).  Max over ranks, like the steps."""
     from go2netspectra_amd.dist import allgather_heavy_arrays
     t_ins = t_hh = t_x = 0.0
+    arrs = cm.heavy_hitters_arrays()  # warm: the read side's grow-only buffers
+    if world > 1:
+        allgather_heavy_arrays(arrs, world)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

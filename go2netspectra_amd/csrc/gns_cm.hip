@@ -2373,6 +2373,44 @@ __global__ __launch_bounds__(256) void k_hh_order_key(const uint32_t *uval, cons
     idx[j] = j;
 }
 
+// Full canonical order on the device (value desc, then all key bytes asc) as
+// stable LSD passes: 8-byte key chunks from the last to byte 4, then (value desc,
+// bytes 0..3).  perm holds unique-entry indices in the current order.
+__global__ __launch_bounds__(256) void k_hh_chunk_key(const uint32_t *perm, const uint8_t *ub, uint32_t K,
+                                                      uint32_t off, uint32_t n, uint64_t *key) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const uint8_t *b = ub + (uint64_t)perm[j] * K;
+    uint64_t k = 0;
+    for (uint32_t t = 0; t < 8; t++) k = k << 8 | (off + t < K ? b[off + t] : 0u);
+    key[j] = k;
+}
+
+__global__ __launch_bounds__(256) void k_hh_final_key(const uint32_t *perm, const uint32_t *uval, const uint8_t *ub,
+                                                      uint32_t K, uint32_t n, uint64_t *key) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t u = perm[j];
+    uint32_t be = 0;
+    for (uint32_t b = 0; b < 4; b++) be = be << 8 | (b < K ? ub[(uint64_t)u * K + b] : 0u);
+    key[j] = (uint64_t)(~uval[u]) << 32 | be;
+}
+
+__global__ __launch_bounds__(256) void k_hh_iota(uint32_t *perm, uint32_t n) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j < n) perm[j] = j;
+}
+
+// ordered output rows: flow bytes and values in list order (one D2H each)
+__global__ __launch_bounds__(256) void k_hh_gather(const uint32_t *perm, const uint8_t *ub, const uint32_t *uval,
+                                                   uint32_t K, uint32_t n, uint8_t *ob, uint32_t *ov) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t u = perm[j];
+    for (uint32_t t = 0; t < K; t++) ob[(uint64_t)j * K + t] = ub[(uint64_t)u * K + t];
+    ov[j] = uval[u];
+}
+
 __global__ __launch_bounds__(256) void k_hh_candidates(const uint32_t *val, const uint32_t *fp,
                                                        uint64_t cells, uint32_t thr,
                                                        uint64_t *cand, uint32_t *ncand, uint32_t cap) {
@@ -2435,7 +2473,14 @@ struct CmScratch {
     uint64_t u32a_n = 0, u32b_n = 0, u32c_n = 0, u32d_n = 0;
     uint8_t *tmp = nullptr;
     uint64_t tmp_n = 0;
+    uint8_t *obytes = nullptr;  // heavy hitters: ordered flow bytes
+    uint64_t obytes_n = 0;
+    uint8_t *hpin = nullptr;    // pinned host staging of the heavy-hitter rows (D2H into pageable
+    uint64_t hpin_n = 0;        // caller memory went through the runtime's slow path)
     void free_all() {
+        dfree(obytes); obytes = nullptr; obytes_n = 0;
+        if (hpin) (void)hipHostFree(hpin);
+        hpin = nullptr; hpin_n = 0;
         dfree(cand); dfree(ncand); dfree(ids); dfree(bytes); dfree(qkeys); dfree(qout);
         dfree(k64a); dfree(k64b); dfree(u32a); dfree(u32b); dfree(u32c); dfree(u32d); dfree(tmp);
         cand = nullptr; ncand = nullptr; ids = nullptr; bytes = nullptr; qkeys = nullptr; qout = nullptr;
@@ -2445,14 +2490,18 @@ struct CmScratch {
     }
 };
 
+// Grows by at least half of the request again: heavy-hitter lists grow window
+// by window over a period, and every reallocation (hipFree synchronizes the
+// device) cost more than the whole device-side list build.
 template <typename T>
 static int grow_buf(T **p, uint64_t &have, uint64_t need) {
     if (need <= have && *p) return GNS_OK;
     dfree(*p);
     *p = nullptr;
     have = 0;
-    GNS_TRY(dalloc(reinterpret_cast<void **>(p), std::max<uint64_t>(need, 1) * sizeof(T)));
-    have = need;
+    const uint64_t n = std::max<uint64_t>(need + need / 2, 1);
+    GNS_TRY(dalloc(reinterpret_cast<void **>(p), n * sizeof(T)));
+    have = n;
     return GNS_OK;
 }
 
@@ -3076,9 +3125,6 @@ static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_
     const uint32_t K = cm->K;
     // on the device: dedupe by flow keeping the max, then order by value desc
     uint32_t nu = 0;
-    std::vector<uint32_t> order, uval;
-    std::vector<uint64_t> okey;
-    std::vector<uint8_t> kb;
     if (nc) {
         const unsigned g = (nc + 255) / 256;
         GNS_TRY(grow_buf(&sc.k64a, sc.k64a_n, nc));
@@ -3099,48 +3145,60 @@ static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_
         GNS_HIP(hipMemcpyAsync(&nu, d_nu, 4, hipMemcpyDeviceToHost, st));
         GNS_HIP(hipStreamSynchronize(st));
     }
+    const uint64_t capn = *n_io;
+    *n_io = nu;
     if (nu) {
         const unsigned g = (nu + 255) / 256;
         const uint32_t Kb = K ? K : 1;
         GNS_TRY(grow_buf(&sc.bytes, sc.bytes_n, (uint64_t)nu * Kb));
+        GNS_TRY(grow_buf(&sc.obytes, sc.obytes_n, (uint64_t)nu * Kb));
         GNS_TRY(grow_buf(&sc.k64b, sc.k64b_n, (uint64_t)nu * 2));
         GNS_TRY(grow_buf(&sc.u32c, sc.u32c_n, (uint64_t)nu * 2));
+        GNS_TRY(grow_buf(&sc.u32d, sc.u32d_n, (uint64_t)nu));
         if (K) hipLaunchKernelGGL(k_ids_to_bytes, dim3(g), dim3(256), 0, st, sc.u32a, (uint64_t)nu, cm->D, sc.bytes);
-        hipLaunchKernelGGL(k_hh_order_key, dim3(g), dim3(256), 0, st, sc.u32b, sc.bytes, K, nu, sc.k64b, sc.u32c);
-        size_t tb = 0;
-        uint64_t *ko = sc.k64b + nu;
-        uint32_t *io = sc.u32c + nu;
-        if (rocprim::radix_sort_pairs(nullptr, tb, sc.k64b, ko, sc.u32c, io, (size_t)nu, 0u, 64u, st) != hipSuccess) {
-            set_error("heavy: radix sort size"); return GNS_E_HIP;
+        // canonical order, entirely on the device: stable LSD radix passes over the
+        // key bytes (8 at a time, last chunk first), then (value desc, bytes 0..3)
+        uint64_t *k0 = sc.k64b, *k1 = sc.k64b + nu;
+        uint32_t *p0 = sc.u32c, *p1 = sc.u32c + nu;
+        hipLaunchKernelGGL(k_hh_iota, dim3(g), dim3(256), 0, st, p0, nu);
+        auto sort_pass = [&](unsigned begin_bit) -> int {
+            size_t tb = 0;
+            if (rocprim::radix_sort_pairs(nullptr, tb, k0, k1, p0, p1, (size_t)nu, begin_bit, 64u, st) != hipSuccess) {
+                set_error("heavy: radix sort size"); return GNS_E_HIP;
+            }
+            GNS_TRY(grow_buf(&sc.tmp, sc.tmp_n, tb));
+            if (rocprim::radix_sort_pairs(sc.tmp, tb, k0, k1, p0, p1, (size_t)nu, begin_bit, 64u, st) != hipSuccess) {
+                set_error("heavy: radix sort"); return GNS_E_HIP;
+            }
+            std::swap(p0, p1);
+            return GNS_OK;
+        };
+        if (K > 4) {
+            for (int off = 4 + (int)((K - 4 - 1) / 8) * 8; off >= 4; off -= 8) {
+                const uint32_t nb = std::min<uint32_t>(8u, K - (uint32_t)off);
+                hipLaunchKernelGGL(k_hh_chunk_key, dim3(g), dim3(256), 0, st, p0, sc.bytes, K, (uint32_t)off, nu, k0);
+                GNS_TRY(sort_pass(64u - 8u * nb));
+            }
         }
-        GNS_TRY(grow_buf(&sc.tmp, sc.tmp_n, tb));
-        if (rocprim::radix_sort_pairs(sc.tmp, tb, sc.k64b, ko, sc.u32c, io, (size_t)nu, 0u, 64u, st) != hipSuccess) {
-            set_error("heavy: radix sort"); return GNS_E_HIP;
+        hipLaunchKernelGGL(k_hh_final_key, dim3(g), dim3(256), 0, st, p0, sc.u32b, sc.bytes, K, nu, k0);
+        GNS_TRY(sort_pass(0u));
+        hipLaunchKernelGGL(k_hh_gather, dim3(g), dim3(256), 0, st, p0, sc.bytes, sc.u32b, K, nu, sc.obytes, sc.u32d);
+        GNS_HIP(hipGetLastError());
+        const uint64_t m = std::min<uint64_t>(nu, capn);
+        const uint64_t fb = (flows && K) ? m * K : 0, vb = vals ? m * 4 : 0;
+        if (fb + vb > sc.hpin_n) {
+            if (sc.hpin) (void)hipHostFree(sc.hpin);
+            sc.hpin = nullptr; sc.hpin_n = 0;
+            const uint64_t want = (fb + vb) + (fb + vb) / 2;
+            GNS_HIP(hipHostMalloc(reinterpret_cast<void **>(&sc.hpin), want, hipHostMallocDefault));
+            sc.hpin_n = want;
         }
-        order.resize(nu); uval.resize(nu); okey.resize(nu); kb.resize((size_t)nu * Kb);
-        GNS_HIP(hipMemcpyAsync(order.data(), io, (uint64_t)nu * 4, hipMemcpyDeviceToHost, st));
-        GNS_HIP(hipMemcpyAsync(okey.data(), ko, (uint64_t)nu * 8, hipMemcpyDeviceToHost, st));
-        GNS_HIP(hipMemcpyAsync(uval.data(), sc.u32b, (uint64_t)nu * 4, hipMemcpyDeviceToHost, st));
-        if (K) GNS_HIP(hipMemcpyAsync(kb.data(), sc.bytes, (uint64_t)nu * K, hipMemcpyDeviceToHost, st));
+        if (fb) GNS_HIP(hipMemcpyAsync(sc.hpin, sc.obytes, fb, hipMemcpyDeviceToHost, st));
+        if (vb) GNS_HIP(hipMemcpyAsync(sc.hpin + fb, sc.u32d, vb, hipMemcpyDeviceToHost, st));
         GNS_HIP(hipStreamSynchronize(st));
-        // ties beyond the first four key bytes: order each run of equal sort keys by the full bytes
-        for (uint32_t i = 0; i < nu;) {
-            uint32_t j = i + 1;
-            while (j < nu && okey[j] == okey[i]) j++;
-            if (j - i > 1 && K > 4)
-                std::sort(order.begin() + i, order.begin() + j, [&](uint32_t x, uint32_t y) {
-                    return memcmp(&kb[(size_t)x * K], &kb[(size_t)y * K], K) < 0;
-                });
-            i = j;
-        }
+        if (fb) memcpy(flows, sc.hpin, fb);
+        if (vb) memcpy(vals, sc.hpin + fb, vb);
     }
-    std::vector<uint32_t> &perm = order;
-    const uint64_t capn = *n_io;
-    for (size_t i = 0; i < perm.size() && i < capn; i++) {
-        if (flows && K) memcpy(flows + i * K, &kb[(size_t)perm[i] * K], K);
-        if (vals) vals[i] = uval[perm[i]];
-    }
-    *n_io = perm.size();
     return GNS_OK;
 }
 

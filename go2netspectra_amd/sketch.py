@@ -88,15 +88,15 @@ def _cm_heavy_arrays(fn, h, key_bytes, hint=None):
     hint = hint if hint is not None else [0, 0]
     while True:
         cc, cs = max(hint[0], 1), max(hint[1], 1)
-        cf = np.zeros((cc, K), np.uint8)
-        cv = np.zeros(cc, np.uint32)
-        sf = np.zeros((cs, K), np.uint8)
-        sv = np.zeros(cs, np.uint32)
+        cf = np.empty((cc, K), np.uint8)  # rows [0, n) are written by the call
+        cv = np.empty(cc, np.uint32)
+        sf = np.empty((cs, K), np.uint8)
+        sv = np.empty(cs, np.uint32)
         nc, ns = ct.c_uint64(cc), ct.c_uint64(cs)
         check(fn(h, cf.ctypes.data, cv.ctypes.data, ct.byref(nc), sf.ctypes.data, sv.ctypes.data, ct.byref(ns)))
         if nc.value <= cc and ns.value <= cs:
             # next call: room for some growth, so a window usually needs one call
-            hint[0], hint[1] = nc.value + nc.value // 4 + 16, ns.value + ns.value // 4 + 16
+            hint[0], hint[1] = nc.value + nc.value // 2 + 64, ns.value + ns.value // 2 + 64
             return cf[:nc.value], cv[:nc.value], sf[:ns.value], sv[:ns.value]
         hint[0], hint[1] = max(hint[0], nc.value), max(hint[1], ns.value)
 
