@@ -100,6 +100,38 @@ def test_query_and_heavy_hitters(gpu, oracle):
     assert hh.Size is not None
 
 
+@pytest.mark.parametrize("K", [4, 8, 13, 16, 37])
+def test_heavy_hitter_ties_beyond_first_bytes(gpu, oracle, K):
+    """Equal counts AND equal first key bytes: the device orders ties by the full key
+    (stable radix passes over every 8-byte chunk), value desc then bytes asc, as the
+    oracle's canonical order of count_min.go:232-239."""
+    rng = np.random.default_rng(K)
+    cm, orc = make_pair(oracle, 65536, 3, K, st=1000, ct=10)
+    base = rng.integers(0, 256, K, dtype=np.uint8)
+    flows = np.repeat(base[None, :], 300, axis=0)
+    for i in range(300):  # differ only in the last two bytes, or only in byte 5 / the middle
+        if K >= 2:
+            flows[i, K - 2] = (i >> 8) & 0xFF
+            flows[i, K - 1] = i & 0xFF
+        if K > 5 and i % 5 == 0:
+            flows[i, 5] ^= 0x80
+        if K > 12 and i % 7 == 0:
+            flows[i, K // 2] ^= 0x40
+    flows = np.unique(flows, axis=0)
+    reps = 50 + np.arange(len(flows)) % 3  # three groups of equal counts
+    keys = np.repeat(flows, reps, axis=0)
+    keys = keys[rng.permutation(len(keys))]
+    sizes = np.full(len(keys), 100, np.uint32)
+    cm.insert_keys(keys, sizes)
+    orc.insert_keys(keys, sizes)
+    cm.flush()
+    hh = cm.heavy_hitters()
+    got_c = [(h.Flow, h.Count) for h in hh.Count]
+    assert got_c == orc.heavy("count")
+    assert [(h.Flow, h.Size) for h in hh.Size] == orc.heavy("size")
+    assert len(got_c) > 100 and len({v for _, v in got_c}) <= 6  # many ties
+
+
 @pytest.mark.parametrize("fields", [
     ["SrcIP"], ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"],
     ["DstIP", "SrcPort", "DstPort", "Protocol"], ["SrcPort", "SrcIP", "Protocol"], ["DstPort"],

@@ -143,3 +143,22 @@ def test_shard_of_is_mm3_of_src_slot(oracle):
     sh = shard_of(src, 8)
     for i in range(0, 500, 7):
         assert sh[i] == oracle.mm3(bytes(src[i]), 0xA5A5A5A5) % 8
+
+
+def test_merge_heavy_arrays_canonical_order():
+    """The array-form union (bench per-window exchange) orders like merge_heavy: value
+    desc, then full key bytes asc, also for ties beyond the first four key bytes."""
+    from go2netspectra_amd.dist import merge_heavy, merge_heavy_arrays
+    rng = np.random.default_rng(3)
+    for K in (2, 4, 16, 37):
+        n = 4000
+        f = rng.integers(0, 256, (n, K), dtype=np.uint8)
+        f[:, : min(K, 4)] = rng.integers(0, 2, (n, min(K, 4)))  # long runs tied on the first bytes
+        f = np.unique(f, axis=0)
+        v = rng.integers(0, 4, len(f)).astype(np.uint32)
+        perm = rng.permutation(len(f))
+        gf, gv = merge_heavy_arrays(f[perm], v[perm])
+        want = merge_heavy([[(bytes(f[i]), int(v[i])) for i in range(len(f))]])
+        assert [(bytes(a), int(b)) for a, b in zip(gf, gv)] == want
+    e = merge_heavy_arrays(np.zeros((0, 8), np.uint8), np.zeros(0, np.uint32))
+    assert len(e[0]) == 0 and len(e[1]) == 0
