@@ -116,6 +116,30 @@ def allgather_heavy(hh: HeavyRecord, world: int) -> HeavyRecord:
     return HeavyRecord(Size=[HeavySize(f, v) for f, v in merged_s], Count=[HeavyCount(f, v) for f, v in merged_c])
 
 
+def _sort_key(flows: np.ndarray, vals: np.ndarray) -> np.ndarray:
+    """One 64-bit key per row: inverted value (desc) over the first four key bytes."""
+    K = flows.shape[1]
+    head = np.zeros((len(vals), 4), np.uint8)
+    head[:, : min(K, 4)] = flows[:, : min(K, 4)]
+    return ((np.uint64(0xFFFFFFFF) - vals.astype(np.uint64)) << np.uint64(32)) | \
+        head.view(">u4").reshape(-1).astype(np.uint64)
+
+
+def _order_tie_runs(flows: np.ndarray, key_sorted: np.ndarray, o: np.ndarray) -> np.ndarray:
+    """o orders the rows by the 64-bit key; order each run of equal keys by the full key bytes."""
+    tie = np.flatnonzero(key_sorted[1:] == key_sorted[:-1])
+    i = 0
+    while i < len(tie):
+        a = tie[i]
+        b = a + 1
+        while i < len(tie) and tie[i] == b - 1:
+            b += 1
+            i += 1
+        run = o[a:b]
+        o[a:b] = run[sorted(range(len(run)), key=lambda j: flows[run[j]].tobytes())]
+    return o
+
+
 def merge_heavy_arrays(flows: np.ndarray, vals: np.ndarray):
     """Union of flow-disjoint per-shard lists in canonical order: value desc, then
     flow bytes asc (the tie order of CountMin.heavy_hitters, count_min.go:232-239).
@@ -124,35 +148,69 @@ def merge_heavy_arrays(flows: np.ndarray, vals: np.ndarray):
     flows (shard_of), so no flow appears twice."""
     flows = np.ascontiguousarray(flows, np.uint8)
     vals = np.asarray(vals, np.uint32)
-    n = len(vals)
-    if n == 0:
+    if len(vals) == 0:
         return flows, vals
-    K = flows.shape[1]
-    head = np.zeros((n, 4), np.uint8)
-    head[:, : min(K, 4)] = flows[:, : min(K, 4)]
-    comp = ((np.uint64(0xFFFFFFFF) - vals.astype(np.uint64)) << np.uint64(32)) | \
-        head.view(">u4").reshape(-1).astype(np.uint64)
-    o = np.argsort(comp, kind="stable")
-    c = comp[o]
-    tie = np.flatnonzero(c[1:] == c[:-1])
-    if len(tie):
-        i = 0
-        while i < len(tie):
-            a = tie[i]
-            b = a + 1
-            while i < len(tie) and tie[i] == b - 1:
-                b += 1
-                i += 1
-            run = o[a:b]
-            o[a:b] = run[sorted(range(len(run)), key=lambda j: flows[run[j]].tobytes())]
+    comp = _sort_key(flows, vals)
+    o = np.argsort(comp)
+    o = _order_tie_runs(flows, comp[o], o)
     return flows[o], vals[o]
+
+
+def _allgather_rows_dev(rows: np.ndarray, world: int):
+    """All-gather of packed rows; the result stays where the collective put it
+    (the GPU under RCCL), concatenated in rank order."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    counts = [int(x.item()) for x in ns]
+    mine = torch.zeros((max(max(counts), 1), rows.shape[1]), dtype=torch.uint8, device=dev)
+    if rows.shape[0]:
+        mine[: rows.shape[0]] = torch.from_numpy(rows).to(dev)
+    parts = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)], dim=0)
+
+
+def _canonical_rows(g, K: int) -> np.ndarray:
+    """Gathered (flow | value) rows -> host rows in canonical order.  The order is
+    built where the rows are (torch stable sorts: first four key bytes asc, then
+    value desc), one copy to the host, then only runs tied on both are ordered by
+    their full key bytes."""
+    import torch
+    n = g.shape[0]
+    if n == 0:
+        return np.zeros((0, K + 4), np.uint8)
+    if g.device.type == "cpu":  # gloo rehearsal: numpy sorts faster than torch's CPU stable sort
+        rows = g.numpy()
+        vals = np.ascontiguousarray(rows[:, K:]).view("<u4").reshape(-1)
+        comp = _sort_key(rows[:, :K], vals)
+        o = np.argsort(comp)
+        return rows[_order_tie_runs(rows[:, :K], comp[o], o)]
+    wv = g[:, K:K + 4].to(torch.int64)
+    val = wv[:, 0] | (wv[:, 1] << 8) | (wv[:, 2] << 16) | (wv[:, 3] << 24)
+    wh = g[:, : min(K, 4)].to(torch.int64)
+    head = torch.zeros(n, dtype=torch.int64, device=g.device)
+    for b in range(4):
+        head = (head << 8) | (wh[:, b] if b < K else 0)
+    o1 = torch.sort(head, stable=True).indices
+    o2 = torch.sort(-val[o1], stable=True).indices
+    rows = g[o1[o2]].cpu().numpy()
+    flows = rows[:, :K]
+    vals = np.ascontiguousarray(rows[:, K:]).view("<u4").reshape(-1)
+    comp = _sort_key(flows, vals)
+    o = _order_tie_runs(flows, comp, np.arange(n))
+    return rows[o]
 
 
 def allgather_heavy_arrays(arrays, world: int):
     """Per-window exchange on the array form of HeavyHitters (CountMin.heavy_hitters_arrays:
     count flows [n,K], counts, size flows, sizes): two RCCL all-gathers of packed
-    (flow | value) rows, then the union in canonical order.  Same result as
-    allgather_heavy without per-flow Python objects (a 2^20-bucket window has ~10^5)."""
+    (flow | value) rows, ordered on the GPU, then one copy to the host.  Same
+    result as allgather_heavy without per-flow Python objects (a 2^20-bucket window
+    has ~10^5 per shard)."""
     cf, cv, sf, sv = arrays
     K = cf.shape[1] if cf.ndim == 2 else sf.shape[1]
 
@@ -165,9 +223,8 @@ def allgather_heavy_arrays(arrays, world: int):
 
     out = []
     for f, v in ((cf, cv), (sf, sv)):
-        g = _allgather_rows(pack(f, v), world)
-        gv = np.ascontiguousarray(g[:, K:]).view("<u4").reshape(-1).astype(np.uint32)
-        out.extend(merge_heavy_arrays(g[:, :K], gv))
+        rows = _canonical_rows(_allgather_rows_dev(pack(f, v), world), K)
+        out.extend((rows[:, :K], np.ascontiguousarray(rows[:, K:]).view("<u4").reshape(-1).astype(np.uint32)))
     return tuple(out)
 
 

@@ -426,3 +426,24 @@ def test_view_answers_the_state_at_refresh_while_ingesting(gpu, oracle):
     view.refresh()
     assert not view.query_many(flows[:10]).any()
     view.close()
+
+
+def test_gathered_heavy_rows_order_on_device(gpu):
+    """dist._canonical_rows on a GPU tensor (the RCCL path of the per-window exchange)
+    orders like the host merge, ties beyond the first four key bytes included."""
+    import torch
+    from go2netspectra_amd.dist import _canonical_rows, merge_heavy_arrays
+    rng = np.random.default_rng(17)
+    for K in (4, 16, 37):
+        n = 50_000
+        rows = rng.integers(0, 256, (n, K + 4), dtype=np.uint8)
+        rows[:, :4] = rng.integers(0, 3, (n, 4))   # long runs tied on the first bytes
+        rows[:, K + 1:] = 0                         # values < 256: many ties
+        rows = np.unique(rows, axis=0)
+        rows = rows[np.unique(rows[:, :K], axis=0, return_index=True)[1]]  # disjoint flows
+        rows = rows[rng.permutation(len(rows))]
+        got = _canonical_rows(torch.from_numpy(rows).to("cuda"), K)
+        vals = np.ascontiguousarray(rows[:, K:]).view("<u4").reshape(-1)
+        wf, wv = merge_heavy_arrays(rows[:, :K], vals)
+        assert np.array_equal(got[:, :K], wf)
+        assert np.array_equal(np.ascontiguousarray(got[:, K:]).view("<u4").reshape(-1), wv)
