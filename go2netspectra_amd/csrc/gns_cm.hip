@@ -1187,6 +1187,7 @@ struct ApplyArgs {
     unsigned long long *stats;  // [5] replayed updates, [6] chunks, [7] chunks with a replay
     const uint64_t *entries;
     uint64_t *entries2;         // super-bin sub-partition scratch (sub_bits > 0)
+    const uint32_t *soff;       // [nbins][17] tile starts of each super-bin (k_subpart), or null
     const uint32_t *offsets;
     uint32_t nblk, nbins;
     const uint32_t *total;
@@ -1650,6 +1651,10 @@ struct SubLds {
     uint32_t soff[17];
 };
 constexpr uint32_t kSubPairs = kApItems * kApWaves;  // (item, wave) groups of a round, in stream order
+#ifndef GNS_SUBPART_LAUNCH
+#define GNS_SUBPART_LAUNCH 1
+#endif
+constexpr bool kSubpartLaunch = GNS_SUBPART_LAUNCH != 0;  // 0: K4 sub-partitions each super-bin itself
 
 // Two passes over the bin: per-tile totals (ballots), then rounds of kApChunk
 // updates in (item, wave, lane) = stream order: each (item, wave) group's
@@ -1754,10 +1759,30 @@ __device__ __forceinline__ void sub_partition(const uint64_t *ent, uint64_t *ent
     __syncthreads();
 }
 
+// Super-bin sub-partition as a launch of its own, one workgroup per super-bin and
+// two per CU (16 KB of LDS instead of K4's 156 KB), so that its barrier- and
+// latency-bound rounds overlap across workgroups instead of running inside K4's
+// one-workgroup-per-CU loop: the same stable partition by tile as sub_partition.
+__global__ __launch_bounds__(kApThreads) void k_subpart(ApplyArgs a, uint32_t *soff) {
+    __shared__ SubLds P;
+    __shared__ uint32_t cnt[2 * kSubPairs * 16];
+    const uint32_t bin = blockIdx.x;  // block-uniform exits below
+    const uint32_t nsub = 1u << a.g.sub_bits;
+    const uint32_t beg = a.offsets[bin];
+    const uint32_t end = (bin + 1 < a.g.nbins_all) ? a.offsets[bin + 1] : *a.total;
+    if (beg >= end) {
+        if (threadIdx.x <= nsub) soff[(uint64_t)bin * 17 + threadIdx.x] = 0;
+        return;
+    }
+    sub_partition(a.entries, a.entries2, beg, end, a.g.tile_bits, a.g.sub_bits, P, cnt);
+    if (threadIdx.x <= nsub) soff[(uint64_t)bin * 17 + threadIdx.x] = P.soff[threadIdx.x];
+}
+
 // Persistent: each workgroup takes bins from the size-ordered schedule through
 // a work counter, one bin ahead, so the next tile's state can be loaded while
 // the current tile is stored.
 struct ApplyTile {
+    uint32_t bin;
     uint32_t beg, end;  // update range in the bin (super-bin: sub-partitioned later)
     uint32_t r, bbase;  // row, first bucket of the bin
     bool valid;
@@ -1768,6 +1793,7 @@ __device__ __forceinline__ ApplyTile apply_bin(const ApplyArgs &a, uint32_t k) {
     t.valid = false;
     if (k >= a.g.nbins) return t;
     const uint32_t bin = a.order ? a.order[k] : k;
+    t.bin = bin;
     t.beg = a.offsets[bin];
     t.end = (bin + 1 < a.g.nbins_all) ? a.offsets[bin + 1] : *a.total;
     t.r = bin / a.g.ntiles;
@@ -1808,15 +1834,20 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
                 apply_tile(a, L, a.entries, cur.beg, cur.end, (uint64_t)cur.r * g.w + cur.bbase,
                            min(tw, g.w - cur.bbase), cur.bbase, pre, nb_cbase, nb_tn);
             } else {
+                const uint32_t nsub = 1u << g.sub_bits;
 #ifdef GNS_K4_PROF
                 const uint64_t t_sp = __builtin_amdgcn_s_memtime();
 #endif
-                sub_partition(a.entries, a.entries2, cur.beg, cur.end, g.tile_bits, g.sub_bits, P,
-                              reinterpret_cast<uint32_t *>(L.accN));
+                if (a.soff) {  // partitioned by k_subpart
+                    if (tid <= nsub) P.soff[tid] = a.soff[(uint64_t)cur.bin * 17 + tid];
+                    __syncthreads();
+                } else {
+                    sub_partition(a.entries, a.entries2, cur.beg, cur.end, g.tile_bits, g.sub_bits, P,
+                                  reinterpret_cast<uint32_t *>(L.accN));
+                }
 #ifdef GNS_K4_PROF
                 if (tid == 0) atomicAdd(&a.stats[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_sp));
 #endif
-                const uint32_t nsub = 1u << g.sub_bits;
                 for (uint32_t st = 0; st < nsub; st++) {
                     const uint32_t tbase = cur.bbase + (st << g.tile_bits);
                     const uint32_t sb = cur.beg + P.soff[st], se = cur.beg + P.soff[st + 1];
@@ -2525,6 +2556,7 @@ struct gns_cm {
     uint32_t *ptotal = nullptr;        // [2]
     uint32_t *hist = nullptr, *part = nullptr, *total = nullptr, *order = nullptr;
     uint64_t *entries = nullptr, *entries2 = nullptr;
+    uint32_t *soff = nullptr;          // [nbins][17] super-bin tile starts (sub_bits > 0)
     uint64_t *ovf = nullptr;
     uint32_t *ovf_cnt = nullptr;
     unsigned long long *stats = nullptr;  // [8]
@@ -2571,7 +2603,7 @@ int cm_free_all(gns_cm *cm) {
     dfree(cm->keyid); dfree(cm->idx);
     dfree(cm->pend[0]); dfree(cm->pend[1]); dfree(cm->pcnt[0]); dfree(cm->pcnt[1]);
     dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
-    dfree(cm->entries); dfree(cm->entries2); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats); dfree(cm->stage);
+    dfree(cm->entries); dfree(cm->entries2); dfree(cm->soff); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats); dfree(cm->stage);
     dfree(cm->work);
     dfree(cm->hot_ids); dfree(cm->segtot); dfree(cm->hflag); dfree(cm->hhist); dfree(cm->hthr); dfree(cm->hcnt);
     dfree(cm->hsum); dfree(cm->hflag2); dfree(cm->hres); dfree(cm->chk); dfree(cm->hot_tab);
@@ -2711,6 +2743,11 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs; a.work = cm->work;
         GNS_HIP(hipMemsetAsync(cm->work, 0, 4, s));
         ScopedStage st(cm->timer, 4);
+        if (g.sub_bits && kSubpartLaunch) {
+            hipLaunchKernelGGL(k_subpart, dim3(g.nbins), dim3(kApThreads), 0, s, a, cm->soff);
+            GNS_HIP(hipGetLastError());
+            a.soff = cm->soff;
+        }
         // persistent: one workgroup per CU (the tile LDS fills a CU), bins from the schedule counter
         hipLaunchKernelGGL(k_apply, dim3(std::min(g.nbins, cm->ncu)), dim3(kApThreads), 0, s, a);
         GNS_HIP(hipGetLastError());
@@ -2928,6 +2965,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (rc = dalloc_t(&cm->part, nscan)) || (rc = dalloc_t(&cm->total, 1)) ||
             (rc = dalloc_t(&cm->order, g.nbins)) || (rc = dalloc_t(&cm->entries, cm->bmax * g.d)) ||
             (g.sub_bits && (rc = dalloc_t(&cm->entries2, cm->bmax * g.d))) ||
+            (g.sub_bits && (rc = dalloc_t(&cm->soff, (uint64_t)g.nbins * 17))) ||
             (rc = dalloc_t(&cm->ovf, kOvfCap)) || (rc = dalloc_t(&cm->ovf_cnt, 1)) ||
             (rc = dalloc_t(&cm->stats, 16)) || (rc = dalloc_t(&cm->work, 4)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
             (rc = dalloc_t(&cm->segtot, (size_t)g.d * kHot * kHotSegs * 2)) || (rc = dalloc_t(&cm->hflag, g.d * kHot)) ||
