@@ -207,7 +207,7 @@ def bench_exact(args, torch, dist, world, rank, local):
     syn = SyntheticTraffic(shard=rank, nshards=world, device=local)
     hdr, wl = syn.generate(n)
     ts = torch.arange(n, dtype=torch.int64, device=f"cuda:{local}") * 100 + 1_700_000_000_000_000_000
-    task = ExactTask("per_five_tuple", FIELDS, 128, device=local, max_flows=1 << 21,
+    task = ExactTask("per_five_tuple", FIELDS, 128, device=local, max_flows=args.ex_max_flows,
                      batch_packets=args.batch or n)
     batch = HeaderBatch(hdr, wl, ts)
     for _ in range(args.warmup):
@@ -377,7 +377,7 @@ def bench_hybrid(args, torch, dist, world, rank, local):
     hdr, wl = syn.generate(n)
     ts = torch.arange(n, dtype=torch.int64, device=f"cuda:{local}") * 100 + 1_700_000_000_000_000_000
     batch = HeaderBatch(hdr, wl, ts)
-    ex = ExactTask("per_five_tuple", FIELDS, 128, device=local, max_flows=1 << 21, batch_packets=args.batch or n)
+    ex = ExactTask("per_five_tuple", FIELDS, 128, device=local, max_flows=args.ex_max_flows, batch_packets=args.batch or n)
     cm = CountMin(W, D, 1 << 20, 1000, flow_fields=FIELDS, seeds=row_seeds(D), max_flows=args.max_flows,
                   batch_packets=args.batch or n, device=local)
     view = cm.view()
@@ -535,6 +535,8 @@ def main():
                          "(none of them is the headline metric)")
     ap.add_argument("--max-flows", type=int, default=1 << 22,
                     help="flow dictionary capacity (slots = next power of two >= 2x)")
+    ap.add_argument("--ex-max-flows", type=int, default=1 << 21,
+                    help="exact aggregator flow dictionary capacity (--sketch exact / hybrid)")
     ap.add_argument("--windows", type=int, default=3,
                     help="after the timed steps: W timed windows of insert + device heavy hitters + "
                          "all-gather of every shard's list (configs[3] per-window exchange); 0 = off")

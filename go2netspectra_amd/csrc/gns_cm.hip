@@ -2521,16 +2521,16 @@ struct CmScratch {
     }
 };
 
-// Grows by at least half of the request again: heavy-hitter lists grow window
-// by window over a period, and every reallocation (hipFree synchronizes the
-// device) cost more than the whole device-side list build.
+// Grows to twice the request: heavy-hitter lists grow window by window over a
+// period, and every reallocation (hipFree synchronizes the device) cost more
+// than the whole device-side list build.
 template <typename T>
 static int grow_buf(T **p, uint64_t &have, uint64_t need) {
     if (need <= have && *p) return GNS_OK;
     dfree(*p);
     *p = nullptr;
     have = 0;
-    const uint64_t n = std::max<uint64_t>(need + need / 2, 1);
+    const uint64_t n = std::max<uint64_t>(2 * need, 1);
     GNS_TRY(dalloc(reinterpret_cast<void **>(p), n * sizeof(T)));
     have = n;
     return GNS_OK;
@@ -3227,7 +3227,7 @@ static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_
         if (fb + vb > sc.hpin_n) {
             if (sc.hpin) (void)hipHostFree(sc.hpin);
             sc.hpin = nullptr; sc.hpin_n = 0;
-            const uint64_t want = (fb + vb) + (fb + vb) / 2;
+            const uint64_t want = 2 * (fb + vb);
             GNS_HIP(hipHostMalloc(reinterpret_cast<void **>(&sc.hpin), want, hipHostMallocDefault));
             sc.hpin_n = want;
         }

@@ -96,7 +96,7 @@ def _cm_heavy_arrays(fn, h, key_bytes, hint=None):
         check(fn(h, cf.ctypes.data, cv.ctypes.data, ct.byref(nc), sf.ctypes.data, sv.ctypes.data, ct.byref(ns)))
         if nc.value <= cc and ns.value <= cs:
             # next call: room for some growth, so a window usually needs one call
-            hint[0], hint[1] = nc.value + nc.value // 2 + 64, ns.value + ns.value // 2 + 64
+            hint[0], hint[1] = 2 * nc.value + 64, 2 * ns.value + 64
             return cf[:nc.value], cv[:nc.value], sf[:ns.value], sv[:ns.value]
         hint[0], hint[1] = max(hint[0], nc.value), max(hint[1], ns.value)
 
