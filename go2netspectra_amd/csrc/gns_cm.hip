@@ -282,7 +282,13 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
     const bool cached = bw && ok && first == 0;
 #pragma unroll
     for (uint32_t rr = 0; rr < RMAX; rr++) bk[rr] = (rr < 4 && cached) ? rec[12 + rr] : 0u;
+#ifdef GNS_ABL_HICACHE  // timing ablation only (results not exact): rows >= 4 as if cached
+#pragma unroll
+    for (uint32_t rr = 4; rr < RMAX; rr++) if (cached) bk[rr] = rec[12 + (rr & 3)];
+    if (__ballot(ok && !cached)) {
+#else
     if (__ballot(ok && !cached) || (RMAX > 4 && d > 4)) {
+#endif
         uint32_t mk[GNS_KWMAX];
         mm3_premix<GNS_KWMAX>(kw, K, mk);
 #pragma unroll

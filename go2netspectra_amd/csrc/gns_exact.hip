@@ -15,9 +15,10 @@
 //
 //   X1  k_ex_extract   parse -> To16 tuple -> key -> flow id (dictionary)
 //   X1b k_ex_resolve   re-probe packets parked on a same-launch claim
-//   X2  radix sort of X1's (flow id, packet index << 32 | wire length) pairs
-//       by flow id (rocPRIM; stable, so each flow's packets stay in stream order)
-//   X3  k_ex_runs      over the sorted pairs: the first / last packet of each
+//   X2  radix sort of X1's 64-bit words (flow id | packet index | wire length)
+//       on the flow id bits (rocPRIM keys-only; stable, so each flow's packets
+//       stay in stream order)
+//   X3  k_ex_runs      over the sorted words: the first / last packet of each
 //                      flow's run writes StartTime (a new flow) / EndTime, the
 //                      counters take one atomic add per run piece
 // A Zipf batch touches a flow in many places; per-block LDS aggregation left
@@ -33,6 +34,22 @@
 namespace gns {
 
 constexpr int kXThreads = 256;
+
+// X2 needs a stable sort (a flow's packets stay in stream order); rocPRIM's merge-sort
+// path for batches up to 1M words did not keep equal flow fields in input order for a
+// keys-only sort over a bit range, so every batch above one block takes the Onesweep
+// LSD passes (stable by construction).
+#ifdef GNS_EX_RADIX_BITS
+using ExSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<GNS_EX_SORT_BLOCK, GNS_EX_SORT_ITEMS>,
+                                        rocprim::kernel_config<GNS_EX_SORT_BLOCK, GNS_EX_SORT_ITEMS>,
+                                        GNS_EX_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>,
+    0>;
+#else
+using ExSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                rocprim::default_config, 0>;
+#endif
 constexpr uint32_t kXChunk = 16384;
 
 struct ExIn {
@@ -79,13 +96,24 @@ struct ExArgs {
     KeyPlanN kp;
     DictDev D;
     uint32_t epoch;
-    uint32_t *skey;      // X2 sort keys: flow id, none_key for a packet without one
-    uint64_t *sval;      // X2 sort values: packet index << 32 | wire length
-    uint32_t none_key;
+    uint64_t *sk;        // X2 sort words: flow id | packet index | wire length (SortWord)
+    uint32_t none_key;   // flow field of a packet without a flow id (sorts last)
+    uint32_t sb, ib;     // SortWord field widths: wire length, packet index
     uint64_t *pend;
     uint32_t *pend_cnt, *pend_total;
     unsigned long long *stats;  // 0 inserted, 1 dropped, 2 unsupported, 3 dict full
 };
+
+// X2 sorts one 64-bit word per packet: flow id in the top bits (the radix sort's
+// key range), then the packet index within the batch (ib bits), then the wire
+// length (sb bits; a length >= 2^sb - 1 is stored as the escape 2^sb - 1 and
+// read back from the batch's length array by X3).  A keys-only sort of 8 bytes
+// per packet instead of 4-byte keys with 8-byte values.
+__device__ __forceinline__ uint64_t sort_word(uint32_t flow, uint64_t idx, uint32_t size, uint32_t sb,
+                                              uint32_t ib) {
+    const uint32_t esc = (1u << sb) - 1u;
+    return (uint64_t)flow << (ib + sb) | idx << sb | (size < esc ? size : esc);
+}
 
 // Home-slot record of a key (issued early; consumed by ex_consume).
 __device__ __forceinline__ void ex_probe_issue(const DictDev &D, uint32_t slot, uint4 (&r4)[4]) {
@@ -100,8 +128,8 @@ __device__ __forceinline__ void ex_probe_issue(const DictDev &D, uint32_t slot, 
 // stalling the wave on dependent probes; an empty home slot is claimed here.
 __device__ __forceinline__ void ex_consume(const ExArgs &a, uint64_t p, uint64_t beg, bool ok,
                                            const uint32_t (&kw)[GNS_KWMAX], uint32_t K, uint32_t slot0,
-                                           const uint4 (&r4)[4], uint32_t *s_pend, uint32_t *s_full,
-                                           uint32_t &n_ok) {
+                                           const uint4 (&r4)[4], uint32_t sz, uint32_t *s_pend,
+                                           uint32_t *s_full, uint32_t &n_ok) {
     if (!ok) return;
     uint32_t rec[16];
 #pragma unroll
@@ -121,17 +149,14 @@ __device__ __forceinline__ void ex_consume(const ExArgs &a, uint64_t p, uint64_t
         else r = dict_find_or_claim(a.D, kw, slot0, a.epoch, &out);              // empty: claim
     }
     if (r == DICT_FULL) {
-        a.skey[p] = a.none_key;
+        a.sk[p] = sort_word(a.none_key, p, sz, a.sb, a.ib);
         atomicAdd(s_full, 1u);
         return;
     }
     n_ok++;
-    if (r == DICT_FOUND) {
-        a.skey[p] = out;
-    } else {
-        a.skey[p] = a.none_key;
-        a.pend[beg + atomicAdd(s_pend, 1u)] = (uint64_t)(p - beg) << 32 | out;
-    }
+    // a parked packet keeps none_key until k_ex_resolve fills in its flow id
+    a.sk[p] = sort_word(r == DICT_FOUND ? out : a.none_key, p, sz, a.sb, a.ib);
+    if (r != DICT_FOUND) a.pend[beg + atomicAdd(s_pend, 1u)] = (uint64_t)(p - beg) << 32 | out;
 }
 
 template <int KIND, int MODE>
@@ -159,22 +184,22 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
             for (int i = 0; i < 4; i++) hv[i] = r[i];
             hsz = a.x.in.sizes[pc];
         };
-        auto stage_b = [&](uint64_t q, bool &okq, uint32_t (&kwq)[GNS_KWMAX], uint32_t &slotq, uint4 (&r4q)[4]) {
+        auto stage_b = [&](uint64_t q, bool &okq, uint32_t (&kwq)[GNS_KWMAX], uint32_t &slotq, uint4 (&r4q)[4],
+                           uint32_t &szq) {
             okq = q < end;
             uint32_t cw[16];
 #pragma unroll
             for (int i = 0; i < 4; i++) { cw[4 * i] = hv[i].x; cw[4 * i + 1] = hv[i].y; cw[4 * i + 2] = hv[i].z; cw[4 * i + 3] = hv[i].w; }
-            const uint32_t szq = hsz;
+            szq = hsz;
             load_hdr(q + kXThreads);
 #pragma unroll
             for (int i = 0; i < GNS_KWMAX; i++) kwq[i] = 0;
             if (okq) {
-                a.sval[q] = q << 32 | szq;
                 uint32_t tw[10];
                 int st = parse_record_fast(cw, szq, true, tw);
                 if (st == PARSE_OK) st = ex_key_tw<KIND, MODE>(a.x, K, s_src, q, tw, kwq);
                 if (st != PARSE_OK) {
-                    a.skey[q] = a.none_key;
+                    a.sk[q] = sort_word(a.none_key, q, szq, a.sb, a.ib);
                     atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
                     okq = false;
                 }
@@ -184,16 +209,16 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
         };
         load_hdr(beg + tid);
         bool okc;
-        uint32_t kwc[GNS_KWMAX], slotc;
+        uint32_t kwc[GNS_KWMAX], slotc, szc;
         uint4 r4c[4];
-        stage_b(beg + tid, okc, kwc, slotc, r4c);
+        stage_b(beg + tid, okc, kwc, slotc, r4c, szc);
         for (uint64_t p0 = beg; p0 < end; p0 += kXThreads) {  // wave-uniform trip count
             bool okn = false;
-            uint32_t kwn[GNS_KWMAX], slotn = 0;
+            uint32_t kwn[GNS_KWMAX], slotn = 0, szn = 0;
             uint4 r4n[4];
-            if (p0 + kXThreads < end) stage_b(p0 + kXThreads + tid, okn, kwn, slotn, r4n);
-            ex_consume(a, p0 + tid, beg, okc, kwc, K, slotc, r4c, &s_pend, &s_full, n_ok);
-            okc = okn; slotc = slotn;
+            if (p0 + kXThreads < end) stage_b(p0 + kXThreads + tid, okn, kwn, slotn, r4n, szn);
+            ex_consume(a, p0 + tid, beg, okc, kwc, K, slotc, r4c, szc, &s_pend, &s_full, n_ok);
+            okc = okn; slotc = slotn; szc = szn;
 #pragma unroll
             for (int i = 0; i < GNS_KWMAX; i++) kwc[i] = kwn[i];
 #pragma unroll
@@ -202,17 +227,17 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
     } else {
         for (uint64_t p = beg + tid; p < end; p += kXThreads) {
             uint32_t kw[GNS_KWMAX];
-            a.sval[p] = p << 32 | a.x.in.sizes[p];
+            const uint32_t sz = a.x.in.sizes[p];
             const int st = ex_key<KIND, MODE>(a.x, K, s_src, p, kw);
             if (st != PARSE_OK) {
-                a.skey[p] = a.none_key;
+                a.sk[p] = sort_word(a.none_key, p, sz, a.sb, a.ib);
                 atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
                 continue;
             }
             const uint32_t slot0 = mm3_n<GNS_KWMAX>(kw, K, a.D.seed) & a.D.mask;
             uint4 r4[4];
             ex_probe_issue(a.D, slot0, r4);
-            ex_consume(a, p, beg, true, kw, K, slot0, r4, &s_pend, &s_full, n_ok);
+            ex_consume(a, p, beg, true, kw, K, slot0, r4, sz, &s_pend, &s_full, n_ok);
         }
     }
     atomicAdd(&s_ok, n_ok);
@@ -257,7 +282,10 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
         (void)ex_key<KIND, MODE>(a.x, a.kp.K, s_src, p, kw);
         uint32_t out;
         const int res = dict_find_or_claim(a.D, kw, (uint32_t)v, a.epoch, &out);
-        if (res == DICT_FOUND) a.skey[p] = out;
+        if (res == DICT_FOUND) {  // X1 wrote the word with none_key: fill in the flow field
+            const uint32_t sh = a.ib + a.sb;
+            a.sk[p] = (a.sk[p] & ((1ull << sh) - 1ull)) | (uint64_t)out << sh;
+        }
         else if (res == DICT_PENDING) r.pend_out[beg + atomicAdd(&s_cnt, 1u)] = (v & 0xFFFFFFFF00000000ull) | out;
         else atomicAdd(&s_full, 1u);
     }
@@ -289,21 +317,28 @@ struct FlowState {
 #endif
 constexpr int kRunItems = GNS_RUN_ITEMS;
 extern "C" __device__ unsigned long long __ockl_wfred_add_u64(unsigned long long);
-__global__ __launch_bounds__(256) void k_ex_runs(const uint32_t *skey, const uint64_t *sval, uint64_t n,
-                                                 uint32_t none_key, const int64_t *ts, uint64_t pkt_base,
-                                                 FlowState f) {
+__global__ __launch_bounds__(256) void k_ex_runs(const uint64_t *sk, uint64_t n, uint32_t none_key, uint32_t sb,
+                                                 uint32_t ib, const uint32_t *sizes, const int64_t *ts,
+                                                 uint64_t pkt_base, FlowState f) {
     const uint64_t b0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kRunItems;
     if (b0 >= n) return;  // whole waves past the end exit together (n is rounded per wave below)
+    const uint32_t ks = sb + ib, esc = (1u << sb) - 1u;
+    const uint64_t imask = (1ull << ib) - 1ull;
     uint32_t k[kRunItems];
-    uint64_t v[kRunItems];
+    uint64_t v[kRunItems];  // packet index << 32 | wire length
 #pragma unroll
     for (int j = 0; j < kRunItems; j++) {
         const uint64_t i = b0 + j;
-        k[j] = i < n ? skey[i] : none_key;
-        v[j] = i < n ? sval[i] : 0ull;
+        const uint64_t w = i < n ? sk[i] : (uint64_t)none_key << ks;
+        k[j] = (uint32_t)(w >> ks);
+        const uint32_t s = (uint32_t)w & esc;
+        v[j] = ((w >> sb) & imask) << 32 | s;
     }
-    const uint32_t prev = b0 > 0 ? skey[b0 - 1] : ~0u;
-    const uint32_t next = b0 + kRunItems < n ? skey[b0 + kRunItems] : ~0u;
+#pragma unroll
+    for (int j = 0; j < kRunItems; j++)  // lengths too large for the word's field (rare)
+        if ((uint32_t)v[j] == esc && k[j] != none_key) v[j] = (v[j] & ~0xFFFFFFFFull) | sizes[v[j] >> 32];
+    const uint32_t prev = b0 > 0 ? (uint32_t)(sk[b0 - 1] >> ks) : ~0u;
+    const uint32_t next = b0 + kRunItems < n ? (uint32_t)(sk[b0 + kRunItems] >> ks) : ~0u;
     // a heavy flow covering the whole wave: one add per wave
     const uint32_t kw = __builtin_amdgcn_readfirstlane(k[0]);
     const bool inner = k[0] == kw && k[kRunItems - 1] == kw && prev == kw && next == kw;
@@ -428,11 +463,11 @@ struct gns_ex {
     uint64_t pkt = 0, batches = 0;
     uint64_t bmax = 0;
     uint32_t nblk_max = 0;
-    uint32_t *skey[2] = {nullptr, nullptr};  // X2 sort keys (in, out)
-    uint64_t *sval[2] = {nullptr, nullptr};  // X2 sort values (in, out)
+    uint64_t *sk[2] = {nullptr, nullptr};    // X2 sort words (in, out)
     void *sort_tmp = nullptr;                // rocPRIM radix sort scratch
     size_t sort_tmp_bytes = 0;
-    uint32_t key_bits = 0;                   // sort key bits: flow ids < slots, invalid = slots
+    uint32_t key_bits = 0;                   // flow field bits: flow ids < slots, invalid = slots
+    uint32_t sb = 0, ib = 0;                 // sort word: wire length bits, packet index bits
     uint64_t *pend[2] = {nullptr, nullptr};
     uint32_t *pcnt[2] = {nullptr, nullptr};
     uint32_t *ptotal = nullptr;
@@ -454,7 +489,7 @@ void ex_free_all(gns_ex *ex) {
     dfree(ex->D.rec); dfree(ex->f.pkts); dfree(ex->f.bytes); dfree(ex->f.first); dfree(ex->f.last);
     dfree(ex->f.start); dfree(ex->f.end); dfree(ex->pend[0]); dfree(ex->pend[1]);
     dfree(ex->pcnt[0]); dfree(ex->pcnt[1]); dfree(ex->ptotal); dfree(ex->stats); dfree(ex->stage);
-    dfree(ex->skey[0]); dfree(ex->skey[1]); dfree(ex->sval[0]); dfree(ex->sval[1]); dfree(ex->sort_tmp);
+    dfree(ex->sk[0]); dfree(ex->sk[1]); dfree(ex->sort_tmp);
     if (ex->h_pin) (void)hipHostFree(ex->h_pin);
     ex->timer.destroy();
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
@@ -479,7 +514,7 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     if (++ex->epoch == 0) ex->epoch = 1;
     ExArgs x{};
     x.x = xin; x.n = n; x.kp = ex->kp; x.D = ex->D; x.epoch = ex->epoch;
-    x.skey = ex->skey[0]; x.sval = ex->sval[0]; x.none_key = (uint32_t)ex->slots;
+    x.sk = ex->sk[0]; x.none_key = (uint32_t)ex->slots; x.sb = ex->sb; x.ib = ex->ib;
     x.pend = ex->pend[0]; x.pend_cnt = ex->pcnt[0]; x.pend_total = ex->ptotal; x.stats = ex->stats;
     {
         ScopedStage st(ex->timer, 0);
@@ -513,14 +548,14 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     {
         ScopedStage st(ex->timer, 2);
         size_t tb = ex->sort_tmp_bytes;
-        GNS_HIP(rocprim::radix_sort_pairs(ex->sort_tmp, tb, ex->skey[0], ex->skey[1], ex->sval[0], ex->sval[1],
-                                          (size_t)n, 0u, ex->key_bits, s));
+        GNS_HIP(rocprim::radix_sort_keys<ExSortConfig>(ex->sort_tmp, tb, ex->sk[0], ex->sk[1], (size_t)n, ex->sb + ex->ib,
+                                         ex->sb + ex->ib + ex->key_bits, s));
     }
     {
         ScopedStage st(ex->timer, 3);
         const uint64_t nt = (n + kRunItems - 1) / kRunItems;
-        hipLaunchKernelGGL(k_ex_runs, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, ex->skey[1], ex->sval[1],
-                           n, none_key, xin.ts, ex->pkt, ex->f);
+        hipLaunchKernelGGL(k_ex_runs, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, ex->sk[1], n, none_key,
+                           ex->sb, ex->ib, xin.in.sizes, xin.ts, ex->pkt, ex->f);
         GNS_HIP(hipGetLastError());
     }
     ex->pkt += n;
@@ -636,6 +671,15 @@ int gns_ex_create(const gns_ex_params *p, gns_ex **out) {
         ex->D.seed = 0x5BD1E995u;
         ex->bmax = p->batch_packets ? p->batch_packets : (16ull << 20);
         ex->bmax = std::min<uint64_t>(((ex->bmax + kXChunk - 1) / kXChunk) * kXChunk, 1ull << 31);
+        {   // sort word fields: flow ids < slots (invalid packets = slots), packet index, wire length
+            uint32_t kb = 1;
+            while ((1ull << kb) <= slots) kb++;
+            ex->key_bits = kb;
+            // keep >= 12 bits of wire length in the word (a longer one is read back by X3)
+            if (64 - kb - ceil_log2(ex->bmax) < 12) ex->bmax = 1ull << (52 - kb);
+            ex->ib = std::max<uint32_t>(1, ceil_log2(ex->bmax));
+            ex->sb = std::min<uint32_t>(31, 64 - kb - ex->ib);
+        }
         ex->nblk_max = (uint32_t)(ex->bmax / kXChunk);
         if ((rc = dalloc_t(&ex->D.rec, slots * ex->D.RW)) || (rc = dalloc_t(&ex->f.pkts, slots)) ||
             (rc = dalloc_t(&ex->f.bytes, slots)) || (rc = dalloc_t(&ex->f.first, slots)) ||
@@ -644,16 +688,13 @@ int gns_ex_create(const gns_ex_params *p, gns_ex **out) {
             (rc = dalloc_t(&ex->pend[0], ex->bmax)) || (rc = dalloc_t(&ex->pend[1], ex->bmax)) ||
             (rc = dalloc_t(&ex->pcnt[0], ex->nblk_max)) || (rc = dalloc_t(&ex->pcnt[1], ex->nblk_max)) ||
             (rc = dalloc_t(&ex->ptotal, 2)) || (rc = dalloc_t(&ex->stats, 8)) ||
-            (rc = dalloc_t(&ex->skey[0], ex->bmax)) || (rc = dalloc_t(&ex->skey[1], ex->bmax)) ||
-            (rc = dalloc_t(&ex->sval[0], ex->bmax)) || (rc = dalloc_t(&ex->sval[1], ex->bmax)))
+            (rc = dalloc_t(&ex->sk[0], ex->bmax)) || (rc = dalloc_t(&ex->sk[1], ex->bmax)))
             break;
-        {   // sort keys: flow ids < slots, invalid packets = slots
-            uint32_t kb = 1;
-            while ((1ull << kb) <= slots) kb++;
-            ex->key_bits = kb;
+        {
             size_t t1 = 0;
-            if (rocprim::radix_sort_pairs(nullptr, t1, ex->skey[0], ex->skey[1], ex->sval[0], ex->sval[1],
-                                          (size_t)ex->bmax, 0u, kb, ex->stream) != hipSuccess) {
+            const uint32_t lo = ex->sb + ex->ib;
+            if (rocprim::radix_sort_keys<ExSortConfig>(nullptr, t1, ex->sk[0], ex->sk[1], (size_t)ex->bmax, lo,
+                                         lo + ex->key_bits, ex->stream) != hipSuccess) {
                 set_error("rocPRIM scratch query failed"); rc = GNS_E_HIP; break;
             }
             ex->sort_tmp_bytes = t1;

@@ -177,3 +177,29 @@ def test_full_dictionary_is_cleared_by_reset(gpu, oracle):
     task.flush()
     orc.insert_hdr64(hdr2, t2["length"], ts2)
     assert gpu_flows(task) == orc.export()
+
+
+@pytest.mark.parametrize("batch", [16384, 1 << 24])
+def test_wire_lengths_beyond_the_sort_word_field(gpu, oracle, batch):
+    """X2 sorts one 64-bit word per packet (flow id | packet index | wire length): a
+    length that does not fit the word's length field (>= 2^sb - 1, the escape value
+    itself included) is read back from the batch's length array; ByteCount is a u64
+    sum (task.go:154-212)."""
+    from go2netspectra_amd import ExactTask, PacketBatch
+    rng = np.random.default_rng(31)
+    n = 120_000
+    t = random_tuples(rng, n, 400)
+    big = rng.random(n) < 0.2
+    lens = t["length"].copy()
+    lens[big] = rng.integers(1 << 12, 1 << 32, big.sum(), dtype=np.uint64).astype(np.uint32)
+    edge = np.flatnonzero(~big)[:64]  # every power-of-two boundary a field width could have
+    lens[edge] = (np.uint64(1) << (np.arange(64) % 32 + 1).astype(np.uint64)) - np.uint64(1) - (np.arange(64) // 32).astype(np.uint64)
+    lens[-1] = 0xFFFFFFFF
+    ts = rng.integers(-(1 << 50), 1 << 50, n).astype(np.int64)
+    task = ExactTask("big", FIVE, batch_packets=batch, max_flows=1 << 12)
+    ipver = np.where(t["v6"], 6, 4).astype(np.uint8)
+    task.process_packets(PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], lens, ipver, ts))
+    task.flush()
+    orc = oracle.Exact(FIVE)
+    orc.insert_tuples(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], ipver, lens, ts)
+    assert gpu_flows(task) == orc.export()
