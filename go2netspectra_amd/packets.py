@@ -126,7 +126,7 @@ class HeaderBatch:
 
 
 def read_pcap(path: str, limit: Optional[int] = None) -> HeaderBatch:
-    """pcap -> 64-byte records (C++ packer, one pass, no per-packet objects)."""
+    """pcap or pcapng -> 64-byte records (C++ packer, one pass, no per-packet objects)."""
     L = _lib.load()
     total = ct.c_uint64(0)
     if limit is None:
@@ -155,6 +155,60 @@ def write_pcap(path: str, frames, wirelens=None, snaplen: int = 65536, ts_ns=Non
             sec, usec = (i, 0) if ts_ns is None else divmod(int(ts_ns[i]) // 1000, 1_000_000)
             f.write(struct.pack("<IIII", sec, usec, len(fr), wl))
             f.write(fr)
+
+
+def write_pcapng(path: str, frames, wirelens=None, ts_units=None, tsresol=None, tsoffset=None,
+                  big_endian: bool = False, iface_of=None, n_ifaces: int = 1, snaplen: int = 0,
+                  simple: bool = False, sections=None, extra_blocks: bool = False) -> None:
+    """pcapng writer (tests / tools): one Section Header, n_ifaces Ethernet Interface
+    Description blocks (if_tsresol / if_tsoffset options when given), then one Enhanced
+    Packet block per frame (ts_units[i] in the interface's timestamp units; interface
+    iface_of[i]), or Simple Packet blocks when `simple`.  `sections`: indices of frames
+    before which a new section (with its own interface blocks) starts.  `extra_blocks`
+    interleaves blocks a reader must skip (name resolution, statistics, custom)."""
+    import struct
+    e = ">" if big_endian else "<"
+
+    def block(btype, body):
+        body = body + bytes(-len(body) % 4)
+        n = 12 + len(body)
+        return struct.pack(e + "II", btype, n) + body + struct.pack(e + "I", n)
+
+    def opt(code, val):
+        return struct.pack(e + "HH", code, len(val)) + val + bytes(-len(val) % 4)
+
+    def section():
+        out = block(0x0A0D0D0A, struct.pack(e + "IHHq", 0x1A2B3C4D, 1, 0, -1))
+        for _ in range(n_ifaces):
+            opts = b""
+            if tsresol is not None:
+                opts += opt(9, bytes([tsresol]))
+            if tsoffset is not None:
+                opts += opt(14, struct.pack(e + "q", tsoffset))
+            if opts:
+                opts += opt(0, b"")
+            out += block(1, struct.pack(e + "HHI", 1, 0, snaplen) + opts)
+        return out
+
+    starts = set(sections or ())
+    with open(path, "wb") as f:
+        f.write(section())
+        for i, fr in enumerate(frames):
+            if i in starts:
+                f.write(section())
+            fr = bytes(fr)
+            wl = len(fr) if wirelens is None else int(wirelens[i])
+            if extra_blocks and i % 7 == 3:
+                f.write(block(4, opt(1, b"\x0a\x00\x00\x01host\x00") + opt(0, b"")))  # name resolution
+                f.write(block(5, struct.pack(e + "III", 0, 0, 0)))                     # interface statistics
+                f.write(block(0x00000BAD, struct.pack(e + "I", 32473) + b"custom"))    # custom block
+            if simple:
+                f.write(block(3, struct.pack(e + "I", wl) + fr))
+            else:
+                t = i if ts_units is None else int(ts_units[i])
+                ifc = 0 if iface_of is None else int(iface_of[i])
+                f.write(block(6, struct.pack(e + "IIIII", ifc, (t >> 32) & 0xFFFFFFFF, t & 0xFFFFFFFF, len(fr), wl)
+                              + fr))
 
 
 class SyntheticTraffic:

@@ -243,9 +243,11 @@ int gns_synth_fill(gns_synth *s, uint8_t *hdr_dev, uint32_t *wirelen_dev, uint64
 /* flow tuple of each shard-local flow (for tests): src16,dst16 [flows*16] etc */
 int gns_synth_flows(gns_synth *s, uint32_t *n_flows);
 
-/* pcap file -> 64-byte records + wirelen (pkg/pcap/reader.go:35-49).
- * Returns the number of records written (<= cap) or a negative status;
- * *total = packets in the file. */
+/* capture file -> 64-byte records + wirelen (pkg/pcap/reader.go:35-49, which
+ * opens it with libpcap's pcap_open_offline: classic pcap in either byte order
+ * and time unit, or pcapng with any number of sections and interfaces;
+ * Ethernet link type only).  Returns the number of records written (<= cap) or
+ * a negative status; *total = packets in the file. */
 int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirelen, uint64_t cap,
                       uint64_t *total);
 

@@ -137,6 +137,87 @@ def test_pcap_packer_roundtrip(tmp_path):
         assert hb.wirelen[i] == wl[i]
 
 
+def _random_frames(rng, n):
+    from helpers import frame64
+    frames, wl = [], []
+    for i in range(n):
+        ln = int(rng.integers(60, 1500))
+        full = frame64(rng.integers(0, 256, 16, dtype=np.uint8), rng.integers(0, 256, 16, dtype=np.uint8),
+                       int(rng.integers(0, 65536)), int(rng.integers(0, 65536)), 6, ln) + bytes(max(0, ln - 64))
+        frames.append(full[: int(rng.integers(1, len(full) + 1))])  # snaplen truncation, down to 1 byte
+        wl.append(ln)
+    return frames, wl
+
+
+def _check_records(hb, frames, wl):
+    assert len(hb) == len(frames)
+    for i, fr in enumerate(frames):
+        c = min(64, len(fr))
+        assert bytes(hb.hdr[i, :c]) == fr[:c] and not hb.hdr[i, c:].any()
+        assert hb.wirelen[i] == wl[i]
+
+
+@pytest.mark.parametrize("big_endian", [False, True])
+@pytest.mark.parametrize("tsresol,tsoffset", [(None, None), (9, None), (3, 7), (0x94, -3), (12, 1_700_000_000)])
+def test_pcapng_enhanced_packets(tmp_path, big_endian, tsresol, tsoffset):
+    """pcapng as libpcap reads it (gopacket pcap.OpenOffline, reader.go:21): records and wire
+    lengths as in classic pcap; timestamps in the interface's if_tsresol units (10^-r, or
+    2^-r with the top bit set; default microseconds) plus if_tsoffset seconds, scaled to ns."""
+    rng = np.random.default_rng(5)
+    frames, wl = _random_frames(rng, 200)
+    units = (10 ** 6 if tsresol is None else (2 ** (tsresol & 0x7F) if tsresol & 0x80 else 10 ** tsresol))
+    ts_units = rng.integers(0, 2 ** 62, len(frames), dtype=np.uint64)
+    ts_units[:3] = [0, units - 1, units]
+    path = str(tmp_path / "t.pcapng")
+    g.write_pcapng(path, frames, wl, ts_units=ts_units, tsresol=tsresol, tsoffset=tsoffset, big_endian=big_endian,
+                   extra_blocks=True)
+    hb = g.read_pcap(path)
+    _check_records(hb, frames, wl)
+    off = tsoffset or 0
+    want = [((int(t) // units + off) * 10 ** 9 + (int(t) % units) * 10 ** 9 // units) for t in ts_units]
+    want = np.array([(w + 2 ** 63) % 2 ** 64 - 2 ** 63 for w in want], np.int64)  # the engine's int64 ns
+    assert np.array_equal(hb.ts, want)
+
+
+def test_pcapng_interfaces_sections_and_simple_packets(tmp_path):
+    rng = np.random.default_rng(6)
+    frames, wl = _random_frames(rng, 120)
+    p1 = str(tmp_path / "multi.pcapng")  # three interfaces, a second section half way
+    g.write_pcapng(p1, frames, wl, iface_of=rng.integers(0, 3, len(frames)), n_ifaces=3, sections=[60])
+    _check_records(g.read_pcap(p1), frames, wl)
+    p2 = str(tmp_path / "simple.pcapng")  # Simple Packet blocks: captured = min(wire length, snaplen)
+    full = [fr + bytes(w - len(fr)) for fr, w in zip(frames, wl)]
+    g.write_pcapng(p2, [f[:48] for f in full], wl, simple=True, snaplen=48)
+    hb = g.read_pcap(p2)
+    _check_records(hb, [f[:48] for f in full], wl)
+    assert not hb.ts.any()
+    assert len(g.read_pcap(p2, limit=10)) == 10
+
+
+def test_pcapng_rejects_what_libpcap_rejects(tmp_path):
+    import struct
+    from go2netspectra_amd._lib import GnsError
+    rng = np.random.default_rng(7)
+    frames, wl = _random_frames(rng, 10)
+    p = str(tmp_path / "badif.pcapng")  # a packet on an interface with no description block
+    g.write_pcapng(p, frames, wl, iface_of=[0] * 9 + [1])
+    with pytest.raises(GnsError, match="interface 1"):
+        g.read_pcap(p)
+    p = str(tmp_path / "raw.pcapng")  # non-Ethernet link type (101 = raw IP)
+    g.write_pcapng(p, frames, wl)
+    data = bytearray(open(p, "rb").read())
+    shb_len = struct.unpack_from("<I", data, 4)[0]
+    struct.pack_into("<H", data, shb_len + 8, 101)
+    open(p, "wb").write(bytes(data))
+    with pytest.raises(GnsError, match="linktype 101"):
+        g.read_pcap(p)
+    p = str(tmp_path / "trunc.pcapng")  # a truncated last block ends the capture
+    g.write_pcapng(p, frames, wl)
+    data = open(p, "rb").read()
+    open(p, "wb").write(data[:-10])
+    _check_records(g.read_pcap(p), frames[:9], wl[:9])
+
+
 def test_shard_of_is_mm3_of_src_slot(oracle):
     rng = np.random.default_rng(4)
     src = rng.integers(0, 256, (500, 16), dtype=np.uint8)
