@@ -111,6 +111,40 @@ func (c *CountMin) InsertTuples(src16, dst16 []byte, sport, dport []uint16, prot
 	return lastErr(C.gns_cm_insert_tuples(c.h, &t, C.uint64_t(n), C.GNS_MEM_HOST))
 }
 
+// InsertHeaders: 64-byte header records + wire lengths (PackCapture's output),
+// parsed on the GPU (pcap.Reader.ReadPackets + ParsePacketInto + ProcessPacket).
+func (c *CountMin) InsertHeaders(hdr []byte, wirelen []uint32) error {
+	if len(wirelen) == 0 {
+		return nil
+	}
+	return lastErr(C.gns_cm_insert_headers(c.h, (*C.uint8_t)(unsafe.Pointer(&hdr[0])),
+		(*C.uint32_t)(unsafe.Pointer(&wirelen[0])), C.uint64_t(len(wirelen)), C.GNS_MEM_HOST))
+}
+
+// PackCapture replaces pcap.NewReader + Reader.ReadPackets (pkg/pcap/reader.go:20-49)
+// on the ingest side: one pass over a classic pcap or pcapng file (what libpcap's
+// pcap_open_offline reads) into 64-byte header records, wire lengths and capture
+// timestamps in ns, ready for InsertHeaders.
+func PackCapture(path string) (hdr []byte, wirelen []uint32, tsNs []int64, err error) {
+	cpath := C.CString(path)
+	defer C.free(unsafe.Pointer(cpath))
+	var total C.uint64_t
+	if r := C.gns_pack_pcap(cpath, nil, nil, 0, &total); r < 0 {
+		return nil, nil, nil, lastErr(C.int(r))
+	}
+	n := int(total)
+	if n == 0 {
+		return nil, nil, nil, nil
+	}
+	hdr, wirelen, tsNs = make([]byte, 64*n), make([]uint32, n), make([]int64, n)
+	r := C.gns_pack_pcap_ts(cpath, (*C.uint8_t)(unsafe.Pointer(&hdr[0])), (*C.uint32_t)(unsafe.Pointer(&wirelen[0])),
+		(*C.int64_t)(unsafe.Pointer(&tsNs[0])), C.uint64_t(n), &total)
+	if r < 0 {
+		return nil, nil, nil, lastErr(C.int(r))
+	}
+	return hdr[:64*int(r)], wirelen[:r], tsNs[:r], nil
+}
+
 // Query implements statistic.Sketch (count_min.go:160-174).
 func (c *CountMin) Query(flow []byte) uint64 {
 	if len(flow) != c.keyBytes || len(flow) == 0 {
