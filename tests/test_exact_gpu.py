@@ -203,3 +203,35 @@ def test_wire_lengths_beyond_the_sort_word_field(gpu, oracle, batch):
     orc = oracle.Exact(FIVE)
     orc.insert_tuples(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], ipver, lens, ts)
     assert gpu_flows(task) == orc.export()
+
+
+def test_pcapng_capture_drives_exact_and_countmin(gpu, oracle, tmp_path):
+    """A pcapng capture (nanosecond if_tsresol, several interfaces, skipped blocks) read by the
+    host packer feeds the exact aggregator (StartTime/EndTime from the capture timestamps) and
+    Count-Min exactly as the restatements see the same records (reader.go:35-49 -> task.go)."""
+    import go2netspectra_amd as g
+    from go2netspectra_amd import CountMin, ExactTask
+    rng = np.random.default_rng(41)
+    t = random_tuples(rng, 30_000, 800, v6_frac=0.2)
+    hdr = frames_from_tuples(t, rng, vlan_frac=0.2)
+    ts = rng.integers(1 << 60, (1 << 60) + (1 << 40), len(hdr)).astype(np.uint64)
+    path = str(tmp_path / "c.pcapng")
+    g.write_pcapng(path, [bytes(r) for r in hdr], t["length"], ts_units=ts, tsresol=9,
+                   iface_of=rng.integers(0, 2, len(hdr)), n_ifaces=2, extra_blocks=True)
+    hb = g.read_pcap(path)
+    assert np.array_equal(hb.hdr, hdr) and np.array_equal(hb.wirelen, t["length"])
+    assert np.array_equal(hb.ts, ts.astype(np.int64))
+    task = ExactTask("cap", FIVE)
+    task.process_packets(hb)
+    task.flush()
+    orc = oracle.Exact(FIVE)
+    orc.insert_hdr64(hb.hdr, hb.wirelen, hb.ts)
+    assert gpu_flows(task) == orc.export()
+    seeds = np.array([0x9747B28C, 0x1B873593, 0xCC9E2D51], np.uint32)
+    cm = CountMin(4096, 3, 1 << 20, 50, flow_fields=FIVE, seeds=seeds, max_flows=1 << 14)
+    cm.insert_headers(hb.hdr, hb.wirelen)
+    cm.flush()
+    o = oracle.CountMin(4096, 3, 1 << 20, 50, 37, seeds)
+    o.insert_hdr64(hb.hdr, hb.wirelen, FIVE)
+    for a, b in zip(cm.export_state(), o.export()):
+        assert np.array_equal(a, b)
