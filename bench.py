@@ -393,6 +393,10 @@ def bench_hybrid(args, torch, dist, world, rank, local):
         ex.flush()
 
     def step():
+        if args.hybrid_serial:  # one host thread: the exact path, then the sketch path
+            ex_step()
+            cm.insert_headers(hdr, wl)
+            return
         te = threading.Thread(target=ex_step)
         te.start()
         cm.insert_headers(hdr, wl)
@@ -460,7 +464,8 @@ def bench_hybrid(args, torch, dist, world, rank, local):
         "config": {"workload": "configs[4]: exact per-5-tuple aggregator + Count-Min d=8 w=2^24 on the same "
                                "100M-packet window per GPU; per window a snapshot view, device-side heavy-hitter "
                                "extraction and 65,536 point queries on a reader thread concurrent with ingest",
-                   "packets_per_step_per_gpu": n, "windows_queried": len(windows)},
+                   "packets_per_step_per_gpu": n, "windows_queried": len(windows),
+                   "ingest": "serial (one thread)" if args.hybrid_serial else "concurrent (two streams, two threads)"},
         "queries": {"windows": len(windows), "latency_ms_avg": round(1e3 * sum(lat) / max(len(lat), 1), 3),
                     "latency_ms_max": round(1e3 * max(lat), 3) if lat else None,
                     "last_window_heavy_hitters": {"count": windows[-1][0], "size": windows[-1][1]} if windows else None},
@@ -542,6 +547,9 @@ def main():
                          "all-gather of every shard's list (configs[3] per-window exchange); 0 = off")
     ap.add_argument("--window-steps", type=int, default=20,
                     help="steps per window (20 x 100M packets per GPU = 0.1 s of ingest; configs[3] says 1 s)")
+    ap.add_argument("--hybrid-serial", action="store_true",
+                    help="--sketch hybrid: run the exact and sketch paths one after the other from one host "
+                         "thread instead of concurrently on two streams from two threads")
     ap.add_argument("--key", choices=["5tuple", "srcip"], default="5tuple",
                     help="flow key: full 5-tuple (37 B, primary) or [SrcIP] (16 B, the default task layout)")
     ap.add_argument("--flows", type=int, default=1 << 20,
