@@ -36,6 +36,7 @@ EXPORTED = [
     "gns_ex_query", "gns_ex_snapshot", "gns_ex_reset", "gns_ex_counters", "gns_ex_set_timing",
     "gns_ex_stage_times",
     "gns_thrift_decode", "gns_pack_pcap", "gns_pack_pcap_ts", "gns_last_error", "gns_version",
+    "gns_route_create", "gns_route_destroy", "gns_route_partition",
 ]
 
 
@@ -148,6 +149,8 @@ def load() -> ct.CDLL:
         "gns_pack_pcap": ([ct.c_char_p, vp, vp, u64, vp], ct.c_int64),
         "gns_pack_pcap_ts": ([ct.c_char_p, vp, vp, vp, u64, vp], ct.c_int64),
         "gns_last_error": ([], ct.c_char_p), "gns_version": ([], ct.c_char_p),
+        "gns_route_create": ([u32, i32, vp], i32), "gns_route_destroy": ([vp], i32),
+        "gns_route_partition": ([vp, vp, vp, u64, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

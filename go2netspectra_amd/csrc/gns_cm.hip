@@ -2494,7 +2494,7 @@ using namespace gns;
 struct CmScratch {
     uint64_t *cand = nullptr;
     uint32_t *ncand = nullptr;
-    uint32_t cap = 0;
+    uint64_t cap = 0;               // candidates sc.cand holds
     uint32_t *ids = nullptr;
     uint64_t ids_n = 0;
     uint8_t *bytes = nullptr;
@@ -2551,6 +2551,8 @@ struct gns_cm {
     uint32_t *C = nullptr, *S = nullptr, *Fc = nullptr, *Fs = nullptr;
     CmScratch rd;                 // read-side buffers of the handle's own queries (grow-only)
     std::atomic<uint32_t> period{0};  // bumped by reset: snapshot views taken before it are stale
+    std::mutex views_mu;              // guards `views` (view create/destroy vs reset / dictionary reclaim)
+    std::vector<gns_cm_view *> views; // live snapshot views: reset and reclaim wait for their calls
     DictDev D{};
     uint64_t dict_slots = 0;
     uint32_t epoch = 0;
@@ -3140,32 +3142,35 @@ int gns_cm_export_state(gns_cm *cm, uint32_t *C, uint32_t *S, uint8_t *FPc, uint
 static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_t *val, const uint32_t *fp,
                         uint32_t thr, uint8_t *flows, uint32_t *vals, uint64_t *n_io) {
     const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
-    const uint32_t cap = (uint32_t)std::min<uint64_t>(cells, 1ull << 26);
-    if (!sc.cand || !sc.ncand) {  // both or neither: a failed second allocation leaves neither
-        dfree(sc.cand); dfree(sc.ncand);
-        sc.cand = nullptr; sc.ncand = nullptr;
-        uint64_t *c = nullptr;
-        uint32_t *nn = nullptr;
-        GNS_TRY(dalloc(reinterpret_cast<void **>(&c), (uint64_t)cap * 8));
-        if (int rc = dalloc(reinterpret_cast<void **>(&nn), 16)) { dfree(c); return rc; }
-        sc.cand = c; sc.ncand = nn; sc.cap = cap;
+    if (!sc.ncand) GNS_TRY(dalloc(reinterpret_cast<void **>(&sc.ncand), 16));
+    // candidate buffer: grows to the number of cells at or above the threshold
+    // (no cap: a low threshold can make every bucket a candidate, d*w < 2^32)
+    uint32_t nc = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        if (!sc.cand) {
+            const uint64_t want = std::min<uint64_t>(cells, 1ull << 20);
+            GNS_TRY(dalloc(reinterpret_cast<void **>(&sc.cand), want * 8));
+            sc.cap = want;
+        }
+        hipError_t e = hipMemsetAsync(sc.ncand, 0, 4, st);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_hh_candidates, dim3((unsigned)((cells + 256 * kHhItems - 1) / (256 * kHhItems))), dim3(256), 0,
+                               st, val, fp, cells, thr, sc.cand, sc.ncand, (uint32_t)sc.cap);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(&nc, sc.ncand, 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) { set_error("heavy: %s", hipGetErrorString(e)); return GNS_E_HIP; }
+        if (nc <= sc.cap) break;
+        // more candidates than the buffer holds: grow to the count and run again
+        dfree(sc.cand);
+        sc.cand = nullptr;
+        sc.cap = 0;
+        const uint64_t want = std::min<uint64_t>(cells, (uint64_t)nc + nc / 8);
+        GNS_TRY(dalloc(reinterpret_cast<void **>(&sc.cand), want * 8));
+        sc.cap = want;
     }
     uint64_t *cand = sc.cand;
-    uint32_t *ncand = sc.ncand;
-    uint32_t nc = 0;
-    hipError_t e = hipMemsetAsync(ncand, 0, 4, st);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_hh_candidates, dim3((unsigned)((cells + 256 * kHhItems - 1) / (256 * kHhItems))), dim3(256), 0, st,
-                           val, fp, cells, thr, cand, ncand, cap);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) e = hipMemcpyAsync(&nc, ncand, 4, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) { set_error("heavy: %s", hipGetErrorString(e)); return GNS_E_HIP; }
-    if (nc > cap) {
-        set_error("heavy hitters: %u buckets reach the threshold %u (more than %u candidates)", nc, thr, cap);
-        return GNS_E_RANGE;
-    }
     const uint32_t K = cm->K;
     // on the device: dedupe by flow keeping the max, then order by value desc
     uint32_t nu = 0;
@@ -3301,15 +3306,26 @@ int gns_cm_view_create(gns_cm *cm, gns_cm_view **out) {
         }
     } while (0);
     if (rc) { view_free(v); delete v; return rc; }
+    {
+        std::lock_guard<std::mutex> reg(cm->views_mu);
+        cm->views.push_back(v);
+    }
     *out = v;
     return GNS_OK;
 }
 
 int gns_cm_view_destroy(gns_cm_view *v) {
     if (!v) return GNS_OK;
-    (void)hipSetDevice(v->cm->device);
-    std::lock_guard<std::mutex> lk(v->mu);
-    if (v->stream) (void)hipStreamSynchronize(v->stream);
+    gns_cm *cm = v->cm;
+    (void)hipSetDevice(cm->device);
+    {
+        std::lock_guard<std::mutex> reg(cm->views_mu);
+        cm->views.erase(std::remove(cm->views.begin(), cm->views.end(), v), cm->views.end());
+    }
+    {   // wait for a view call in progress; the mutex is released before the delete
+        std::lock_guard<std::mutex> lk(v->mu);
+        if (v->stream) (void)hipStreamSynchronize(v->stream);
+    }
     view_free(v);
     delete v;
     return GNS_OK;
@@ -3362,11 +3378,26 @@ int gns_cm_view_query(gns_cm_view *v, const uint8_t *keys, uint32_t stride, uint
     return cm_query_impl(cm, v->stream, v->rd, v->C, v->Fc, v->S, v->Fs, keys, stride, n, out);
 }
 
+// Holds every registered view's mutex: no view call is running (each one
+// synchronizes its stream before it returns), so the handle may rewrite what
+// the views read (the flow dictionary) and bump the period they check.
+struct ViewsQuiesced {
+    std::unique_lock<std::mutex> reg;
+    std::vector<std::unique_lock<std::mutex>> locks;
+    explicit ViewsQuiesced(gns_cm *cm) : reg(cm->views_mu) {
+        locks.reserve(cm->views.size());
+        for (gns_cm_view *v : cm->views) locks.emplace_back(v->mu);
+    }
+};
+
 int gns_cm_reset(gns_cm *cm) {
     if (!cm) return GNS_E_ARG;
     GNS_TRY(set_dev(cm));
-    GNS_TRY(cm_reset_state(cm));
+    // a view call that passed its period check still reads the dictionary: wait
+    // for it before the dictionary is cleared (views answer GNS_E_ARG afterwards)
+    ViewsQuiesced q(cm);
     cm->period.fetch_add(1);
+    GNS_TRY(cm_reset_state(cm));
     GNS_HIP(hipStreamSynchronize(cm->stream));
     return GNS_OK;
 }

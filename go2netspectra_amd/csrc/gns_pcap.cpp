@@ -94,7 +94,7 @@ int pcapng(FILE *f, const char *path, Sink &o) {
     using gns::set_error;
     std::vector<uint8_t> body(1 << 16);
     std::vector<Iface> ifs;
-    bool swap = false, have_shb = false;
+    bool swap = false, have_shb = false, first_swap = false;
     for (;;) {
         uint8_t bh[8];
         if (fread(bh, 1, 8, f) != 8) break;  // end of file (a partial block header: stop)
@@ -107,6 +107,13 @@ int pcapng(FILE *f, const char *path, Sink &o) {
             if (bom == 0x1A2B3C4Du) swap = false;
             else if (bom == 0x4D3C2B1Au) swap = true;
             else { set_error("%s: pcapng section with bad byte-order magic %08x", path, bom); return GNS_E_ARG; }
+            // libpcap's pcap_open_offline (which gopacket's OpenOffline calls) reads every
+            // section with the first one's byte order and rejects a file whose sections differ
+            if (!have_shb) first_swap = swap;
+            else if (swap != first_swap) {
+                set_error("%s: pcapng sections with different byte orders", path);
+                return GNS_E_ARG;
+            }
             if (swap) len = bswap32(len);
             if (len < 28 || (len & 3u)) { set_error("%s: bad pcapng section header length %u", path, len); return GNS_E_ARG; }
             if (body.size() < len) body.resize(len);

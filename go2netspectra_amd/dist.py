@@ -59,6 +59,88 @@ def split_batch(batch, world: int):
     return out
 
 
+class Router:
+    """Device-side stable partition of header records by owner shard
+    (gns_route_partition; the device form of shard_of / split_batch)."""
+
+    def __init__(self, nshards: int, device: int = 0):
+        import ctypes as ct
+        from . import _lib
+        self._L = _lib.load()
+        self.nshards = int(nshards)
+        self.device = device
+        h = ct.c_void_p()
+        _lib.check(self._L.gns_route_create(self.nshards, device, ct.byref(h)))
+        self._h = h
+        self._out = None
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.gns_route_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def partition(self, hdr, wirelen, out_hdr=None, out_wl=None):
+        """hdr [n,64] uint8 / wirelen [n] (device tensors) -> (out_hdr, out_wl, counts):
+        the records regrouped shard by shard, packet order kept inside each shard;
+        counts[g] = packets of shard g (numpy uint64)."""
+        import ctypes as ct
+        import torch
+        from . import _lib
+        n = int(wirelen.shape[0])
+        if out_hdr is None:
+            if self._out is None or self._out[0].shape[0] < n:
+                self._out = (torch.empty((n, 64), dtype=torch.uint8, device=hdr.device),
+                             torch.empty((n,), dtype=torch.int32, device=hdr.device))
+            out_hdr, out_wl = self._out[0][:n], self._out[1][:n]
+        counts = np.zeros(self.nshards, np.uint64)
+        _lib.check(self._L.gns_route_partition(self._h, hdr.data_ptr(), wirelen.data_ptr(), n, out_hdr.data_ptr(),
+                                               out_wl.data_ptr(), counts.ctypes.data))
+        return out_hdr, out_wl, counts
+
+
+def exchange_runs(run_hdr, run_wl, counts, world: int):
+    """All-to-all of shard runs (RCCL on the GPU, gloo on the CPU): run g of every
+    rank goes to rank g; the received runs are concatenated in source-rank order,
+    so with rank r holding slice r of the stream each rank receives exactly the
+    stable filter stream[shard_of(src) == rank].  counts: this rank's run lengths."""
+    import torch
+    import torch.distributed as dist
+    dev = run_hdr.device
+    send = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send)
+    rc = [int(x) for x in recv.tolist()]
+    sc = [int(c) for c in counts]
+    in_h = torch.empty((sum(rc), 64), dtype=torch.uint8, device=dev)
+    in_w = torch.empty((sum(rc),), dtype=run_wl.dtype, device=dev)
+    dist.all_to_all_single(in_h, run_hdr, output_split_sizes=rc, input_split_sizes=sc)
+    dist.all_to_all_single(in_w, run_wl, output_split_sizes=rc, input_split_sizes=sc)
+    return in_h, in_w
+
+
+def route_exchange(router: "Router", hdr, wirelen, world: int):
+    """configs[3] routing step: partition this rank's slice of the stream on the
+    device, then exchange the runs (exchange_runs).  Returns this rank's shard
+    stream (device tensors)."""
+    oh, ow, counts = router.partition(hdr, wirelen)
+    return exchange_runs(oh, ow, counts, world)
+
+
+def stable_split_records(hdr: np.ndarray, wirelen: np.ndarray, world: int, src16: np.ndarray):
+    """Host restatement of Router.partition for records whose SrcIP slots are known
+    (tests / CPU rehearsal): runs shard by shard in stream order, and their lengths."""
+    owner = shard_of(src16, world)
+    order = np.argsort(owner, kind="stable")
+    counts = np.bincount(owner, minlength=world).astype(np.uint64)
+    return hdr[order], wirelen[order], counts
+
+
 def _pack(items, K: int) -> np.ndarray:
     buf = np.zeros((len(items), K + 4), np.uint8)
     for i, (f, v) in enumerate(items):

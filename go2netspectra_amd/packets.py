@@ -212,7 +212,16 @@ def write_pcapng(path: str, frames, wirelens=None, ts_units=None, tsresol=None, 
 
 
 class SyntheticTraffic:
-    """Zipf 5-tuple header stream generated on the GPU (gns_synth_*)."""
+    """Zipf 5-tuple header stream generated on the GPU (gns_synth_*).
+
+    shard g of nshards (multi-GPU) is the STABLE FILTER of the
+    global stream: exactly the packets whose owner (dist.shard_of of the SrcIP
+    slot) is g, in stream order -- what the routing step (dist.route_exchange)
+    delivers to GPU g.  It is produced by generating the global stream in chunks
+    and keeping shard g's run of the device partition (gns_route_partition);
+    fill() continues where the previous call stopped."""
+
+    _CHUNK = 1 << 24
 
     def __init__(self, flows: int = 1 << 20, zipf_s: float = 1.1, shard: int = 0, nshards: int = 1,
                  device: int = 0, tuple_seed: int = 0x5EED0001, rank_seed: int = 0x5EED0002,
@@ -220,19 +229,63 @@ class SyntheticTraffic:
         """fanout > 0: every packet's DstIP is drawn Zipf(zipf_s) over `fanout`
         destinations (per-source fan-out, the SuperSpread C3 stream)."""
         self._L = _lib.load()
-        p = _lib.SynthParams(flows, zipf_s, tuple_seed, rank_seed, len_seed, shard, nshards, device, fanout)
+        if not 0 <= shard < max(nshards, 1):
+            raise ValueError(f"shard {shard} not in [0, {nshards})")
+        p = _lib.SynthParams(flows, zipf_s, tuple_seed, rank_seed, len_seed, 0, 1, device, fanout)
         h = ct.c_void_p()
         check(self._L.gns_synth_create(ct.byref(p), ct.byref(h)))
         self._h = h
         self.device = device
+        self.shard, self.nshards = shard, max(nshards, 1)
         nf = ct.c_uint32(0)
         check(self._L.gns_synth_flows(self._h, ct.byref(nf)))
-        self.shard_flows = nf.value
+        self.flows = nf.value
+        self._router = None
+        self._cursor = (0, 0, None)  # (shard packets delivered, global packets consumed, carried run)
 
-    def fill(self, hdr, wirelen, first: int = 0) -> None:
-        """Fill device tensors hdr[n,64] (uint8) and wirelen[n] (int32/uint32 view)."""
+    def _fill_global(self, hdr, wirelen, first: int) -> None:
         n = int(wirelen.shape[0])
         check(self._L.gns_synth_fill(self._h, hdr.data_ptr(), wirelen.data_ptr(), first, n))
+
+    def fill(self, hdr, wirelen, first: int = 0) -> None:
+        """Fill device tensors hdr[n,64] (uint8) and wirelen[n] (int32/uint32 view)
+        with packets first..first+n-1 of this shard's stream."""
+        if self.nshards == 1:
+            return self._fill_global(hdr, wirelen, first)
+        import torch
+        from .dist import Router
+        if self._router is None:
+            self._router = Router(self.nshards, self.device)
+        done, gpos, carry = self._cursor
+        if first != done:  # not a continuation: restart and skip to `first`
+            done, gpos, carry = 0, 0, None
+        n = int(wirelen.shape[0])
+        skip, got = first - done, 0
+        dev = torch.device("cuda", self.device)
+        while got < n:
+            if carry is None or carry[1].shape[0] == 0:
+                m = self._CHUNK
+                gh = torch.empty((m, 64), dtype=torch.uint8, device=dev)
+                gw = torch.empty((m,), dtype=torch.int32, device=dev)
+                self._fill_global(gh, gw, gpos)
+                gpos += m
+                oh, ow, counts = self._router.partition(gh, gw)
+                lo = int(counts[: self.shard].sum())
+                c = int(counts[self.shard])
+                carry = (oh[lo:lo + c].clone(), ow[lo:lo + c].clone())
+                continue
+            ch, cw = carry
+            if skip:
+                t = min(skip, cw.shape[0])
+                skip -= t
+                carry = (ch[t:], cw[t:])
+                continue
+            t = min(n - got, cw.shape[0])
+            hdr[got:got + t].copy_(ch[:t])
+            wirelen[got:got + t].copy_(cw[:t].view(wirelen.dtype))
+            got += t
+            carry = (ch[t:], cw[t:])
+        self._cursor = (first + n, gpos, carry)
 
     def generate(self, n: int, first: int = 0):
         import torch
@@ -243,6 +296,9 @@ class SyntheticTraffic:
         return hdr, wl
 
     def close(self) -> None:
+        if getattr(self, "_router", None) is not None:
+            self._router.close()
+            self._router = None
         if getattr(self, "_h", None):
             self._L.gns_synth_destroy(self._h)
             self._h = None

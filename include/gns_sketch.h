@@ -269,6 +269,24 @@ int gns_thrift_decode(const uint8_t *buf, uint64_t buf_bytes, const uint64_t *of
                       gns_mem where, int device);
 
 /* ------------------------------------------------------------------ */
+/* Flow routing for the multi-GPU path (BASELINE configs[3]) */
+/* ------------------------------------------------------------------ */
+/* Replaces the per-packet host split of the sharded deployment (a packet is
+ * owned by GPU mm3(SrcIP slot, 0xA5A5A5A5) % nshards, so every flow of a source
+ * lands on one GPU; go2netspectra_amd/dist.py shard_of is the host form).
+ * gns_route_partition reorders n DEVICE-resident 64-byte records (+ wire
+ * lengths) into nshards runs, shard by shard, keeping packet order inside each
+ * run (stable); counts[g] (host) = length of run g.  Records the parser drops
+ * or does not support go to shard 0.  The call returns after the device work.
+ * An all-to-all of run g to rank g, received runs concatenated in source-rank
+ * order, delivers to every GPU exactly its stable filter of the stream. */
+typedef struct gns_route gns_route;
+int gns_route_create(uint32_t nshards, int device, gns_route **out);  /* nshards <= 64 */
+int gns_route_destroy(gns_route *r);
+int gns_route_partition(gns_route *r, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
+                        uint8_t *out_hdr, uint32_t *out_wirelen, uint64_t *counts);
+
+/* ------------------------------------------------------------------ */
 /* Exact aggregator (internal/engine/impl/exact/task.go)               */
 /* ------------------------------------------------------------------ */
 /* Replaces exact.New (task.go:83-103), Task.ProcessPacket (:124-149),

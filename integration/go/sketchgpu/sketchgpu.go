@@ -159,26 +159,50 @@ func (c *CountMin) Query(flow []byte) uint64 {
 
 // HeavyHitters implements statistic.Sketch (count_min.go:178-247).
 func (c *CountMin) HeavyHitters() statistic.HeavyRecord {
-	var nc, ns C.uint64_t
-	if C.gns_cm_heavy_hitters(c.h, nil, nil, &nc, nil, nil, &ns) != C.GNS_OK {
-		return statistic.HeavyRecord{Size: []statistic.HeavySize{}, Count: []statistic.HeavyCount{}}
+	return cmHeavy(c.keyBytes, func(cf *C.uint8_t, cv *C.uint32_t, nc *C.uint64_t, sf *C.uint8_t, sv *C.uint32_t,
+		ns *C.uint64_t) C.int {
+		return C.gns_cm_heavy_hitters(c.h, cf, cv, nc, sf, sv, ns)
+	})
+}
+
+// cmHeavy runs a gns_cm_heavy_hitters-shaped call into Go buffers.  The call
+// reports the full list lengths, which may exceed the buffers when the state
+// changed since the sizing call (a View refreshed by its owner in between): the
+// loop grows the buffers and calls again, so a list is never sliced past them.
+func cmHeavy(K int, call func(cf *C.uint8_t, cv *C.uint32_t, nc *C.uint64_t, sf *C.uint8_t, sv *C.uint32_t,
+	ns *C.uint64_t) C.int) statistic.HeavyRecord {
+	empty := statistic.HeavyRecord{Size: []statistic.HeavySize{}, Count: []statistic.HeavyCount{}}
+	capC, capS := 64, 64
+	for tries := 0; tries < 8; tries++ {
+		cf := make([]byte, capC*K+1)
+		cv := make([]uint32, capC+1)
+		sf := make([]byte, capS*K+1)
+		sv := make([]uint32, capS+1)
+		nc, ns := C.uint64_t(capC), C.uint64_t(capS)
+		if call((*C.uint8_t)(unsafe.Pointer(&cf[0])), (*C.uint32_t)(unsafe.Pointer(&cv[0])), &nc,
+			(*C.uint8_t)(unsafe.Pointer(&sf[0])), (*C.uint32_t)(unsafe.Pointer(&sv[0])), &ns) != C.GNS_OK {
+			return empty
+		}
+		if int(nc) > capC || int(ns) > capS { // the lists outgrew the buffers: call again
+			if int(nc) > capC {
+				capC = 2 * int(nc)
+			}
+			if int(ns) > capS {
+				capS = 2 * int(ns)
+			}
+			continue
+		}
+		rec := statistic.HeavyRecord{Size: make([]statistic.HeavySize, 0, int(ns)),
+			Count: make([]statistic.HeavyCount, 0, int(nc))}
+		for i := 0; i < int(ns); i++ {
+			rec.Size = append(rec.Size, statistic.HeavySize{Flow: append([]byte(nil), sf[i*K:(i+1)*K]...), Size: sv[i]})
+		}
+		for i := 0; i < int(nc); i++ {
+			rec.Count = append(rec.Count, statistic.HeavyCount{Flow: append([]byte(nil), cf[i*K:(i+1)*K]...), Count: cv[i]})
+		}
+		return rec
 	}
-	K := c.keyBytes
-	cf := make([]byte, int(nc)*K+1)
-	cv := make([]uint32, int(nc)+1)
-	sf := make([]byte, int(ns)*K+1)
-	sv := make([]uint32, int(ns)+1)
-	C.gns_cm_heavy_hitters(c.h, (*C.uint8_t)(unsafe.Pointer(&cf[0])), (*C.uint32_t)(unsafe.Pointer(&cv[0])), &nc,
-		(*C.uint8_t)(unsafe.Pointer(&sf[0])), (*C.uint32_t)(unsafe.Pointer(&sv[0])), &ns)
-	rec := statistic.HeavyRecord{Size: make([]statistic.HeavySize, 0, int(ns)),
-		Count: make([]statistic.HeavyCount, 0, int(nc))}
-	for i := 0; i < int(ns); i++ {
-		rec.Size = append(rec.Size, statistic.HeavySize{Flow: append([]byte(nil), sf[i*K:(i+1)*K]...), Size: sv[i]})
-	}
-	for i := 0; i < int(nc); i++ {
-		rec.Count = append(rec.Count, statistic.HeavyCount{Flow: append([]byte(nil), cf[i*K:(i+1)*K]...), Count: cv[i]})
-	}
-	return rec
+	return empty
 }
 
 // Reset implements statistic.Sketch (count_min.go:249-265).
@@ -215,26 +239,10 @@ func (w *View) Refresh() error { return lastErr(C.gns_cm_view_refresh(w.v)) }
 
 // HeavyHitters is CountMin.HeavyHitters at the last Refresh, safe during inserts.
 func (w *View) HeavyHitters() statistic.HeavyRecord {
-	var nc, ns C.uint64_t
-	if C.gns_cm_view_heavy_hitters(w.v, nil, nil, &nc, nil, nil, &ns) != C.GNS_OK {
-		return statistic.HeavyRecord{Size: []statistic.HeavySize{}, Count: []statistic.HeavyCount{}}
-	}
-	K := w.keyBytes
-	cf := make([]byte, int(nc)*K+1)
-	cv := make([]uint32, int(nc)+1)
-	sf := make([]byte, int(ns)*K+1)
-	sv := make([]uint32, int(ns)+1)
-	C.gns_cm_view_heavy_hitters(w.v, (*C.uint8_t)(unsafe.Pointer(&cf[0])), (*C.uint32_t)(unsafe.Pointer(&cv[0])), &nc,
-		(*C.uint8_t)(unsafe.Pointer(&sf[0])), (*C.uint32_t)(unsafe.Pointer(&sv[0])), &ns)
-	rec := statistic.HeavyRecord{Size: make([]statistic.HeavySize, 0, int(ns)),
-		Count: make([]statistic.HeavyCount, 0, int(nc))}
-	for i := 0; i < int(ns); i++ {
-		rec.Size = append(rec.Size, statistic.HeavySize{Flow: append([]byte(nil), sf[i*K:(i+1)*K]...), Size: sv[i]})
-	}
-	for i := 0; i < int(nc); i++ {
-		rec.Count = append(rec.Count, statistic.HeavyCount{Flow: append([]byte(nil), cf[i*K:(i+1)*K]...), Count: cv[i]})
-	}
-	return rec
+	return cmHeavy(w.keyBytes, func(cf *C.uint8_t, cv *C.uint32_t, nc *C.uint64_t, sf *C.uint8_t, sv *C.uint32_t,
+		ns *C.uint64_t) C.int {
+		return C.gns_cm_view_heavy_hitters(w.v, cf, cv, nc, sf, sv, ns)
+	})
 }
 
 // Query is CountMin.Query at the last Refresh, safe during inserts.
@@ -335,19 +343,27 @@ func (s *SuperSpread) Query(flow []byte) uint64 {
 
 // HeavyHitters implements statistic.Sketch (super_spread.go:254-294): Size is nil.
 func (s *SuperSpread) HeavyHitters() statistic.HeavyRecord {
-	var n C.uint64_t
-	if C.gns_ss_heavy_hitters(s.h, nil, nil, &n) != C.GNS_OK {
-		return statistic.HeavyRecord{Count: []statistic.HeavyCount{}}
-	}
 	K := s.flowSize
-	fl := make([]byte, int(n)*K+1)
-	v := make([]uint32, int(n)+1)
-	C.gns_ss_heavy_hitters(s.h, (*C.uint8_t)(unsafe.Pointer(&fl[0])), (*C.uint32_t)(unsafe.Pointer(&v[0])), &n)
-	rec := statistic.HeavyRecord{Count: make([]statistic.HeavyCount, 0, int(n))}
-	for i := 0; i < int(n); i++ {
-		rec.Count = append(rec.Count, statistic.HeavyCount{Flow: append([]byte(nil), fl[i*K:(i+1)*K]...), Count: v[i]})
+	capN := 64
+	for tries := 0; tries < 8; tries++ {
+		fl := make([]byte, capN*K+1)
+		v := make([]uint32, capN+1)
+		n := C.uint64_t(capN)
+		if C.gns_ss_heavy_hitters(s.h, (*C.uint8_t)(unsafe.Pointer(&fl[0])), (*C.uint32_t)(unsafe.Pointer(&v[0])),
+			&n) != C.GNS_OK {
+			break
+		}
+		if int(n) > capN { // longer than the buffers: grow and call again
+			capN = 2 * int(n)
+			continue
+		}
+		rec := statistic.HeavyRecord{Count: make([]statistic.HeavyCount, 0, int(n))}
+		for i := 0; i < int(n); i++ {
+			rec.Count = append(rec.Count, statistic.HeavyCount{Flow: append([]byte(nil), fl[i*K:(i+1)*K]...), Count: v[i]})
+		}
+		return rec
 	}
-	return rec
+	return statistic.HeavyRecord{Count: []statistic.HeavyCount{}}
 }
 
 // Reset implements statistic.Sketch (super_spread.go:297-311).

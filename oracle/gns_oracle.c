@@ -217,7 +217,7 @@ struct or_cm {
 
 or_cm *or_cm_new(uint32_t width, uint32_t depth, uint32_t st, uint32_t ct, uint32_t K,
                  const uint32_t *seeds) {
-    /* defaults: count_min.go:11-16,128-140 */
+    /* defaults: count_min.go:11-16,47-59 */
     if (width == 0) width = 1u << 20;
     if (depth == 0) depth = 3;
     if (st == 0) st = 512 * 1024;
@@ -247,15 +247,15 @@ void or_cm_params(const or_cm *cm, uint32_t *w, uint32_t *d, uint32_t *st, uint3
 void or_cm_insert(or_cm *cm, const uint8_t *key, uint32_t size) {
     const uint32_t K = cm->K;
     for (uint32_t i = 0; i < cm->d; i++) {
-        size_t cell = (size_t)i * cm->w + or_mm3(key, K, cm->seed[i]) % cm->w; /* :177 */
+        size_t cell = (size_t)i * cm->w + or_mm3(key, K, cm->seed[i]) % cm->w; /* :96 */
         uint8_t *fs = cm->FPs + cell * K, *fc = cm->FPc + cell * K;
-        /* size half :181-209 */
+        /* size half :99-128 */
         uint32_t S = cm->S[cell];
         if (S == 0) { cm->S[cell] = size; memcpy(fs, key, K); }
         else if (memcmp(fs, key, K) == 0) cm->S[cell] = S + size; /* u32 wrap */
         else if (size > S) { cm->S[cell] = size; memcpy(fs, key, K); }
         else cm->S[cell] = S - size;
-        /* count half :211-235 */
+        /* count half :130-155 */
         uint32_t C = cm->C[cell];
         if (C == 0) { cm->C[cell] = 1; memcpy(fc, key, K); }
         else if (memcmp(fc, key, K) == 0) cm->C[cell] = C + 1;
@@ -441,7 +441,7 @@ uint32_t or_cm_heavy(const or_cm *cm, int which, uint8_t *flows, uint32_t *vals,
     size_t n = 0;
     for (size_t c = 0; c < cells; c++) {
         uint32_t v = which ? cm->S[c] : cm->C[c];
-        if (v > 0) { /* :269, :279 */
+        if (v > 0) { /* :188, :198 */
             it[n].fp = (which ? cm->FPs : cm->FPc) + c * cm->K;
             it[n].v = v;
             n++;

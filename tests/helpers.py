@@ -6,6 +6,35 @@ import struct
 import numpy as np
 
 
+def assert_same_flows(got: dict, want: dict, what: str = "flows") -> None:
+    """Dict-of-flows equality that names the first mismatches (a plain `==` inside a
+    test makes pytest diff two large dicts, which can take minutes)."""
+    if got == want:
+        return
+    missing = [k for k in want if k not in got]
+    extra = [k for k in got if k not in want]
+    diff = [k for k in want if k in got and got[k] != want[k]]
+    msg = [f"{what}: {len(got)} got vs {len(want)} expected; {len(missing)} missing, {len(extra)} extra, "
+           f"{len(diff)} differ"]
+    for k in diff[:3]:
+        msg.append(f"  {k!r}: got {got[k]!r} want {want[k]!r}")
+    for k in missing[:3]:
+        msg.append(f"  missing {k!r}: want {want[k]!r}")
+    for k in extra[:3]:
+        msg.append(f"  extra {k!r}: got {got[k]!r}")
+    raise AssertionError("\n".join(msg))
+
+
+def assert_same_list(got: list, want: list, what: str = "list") -> None:
+    """List equality that reports the first differing position instead of a difflib dump."""
+    if got == want:
+        return
+    for i, (a, b) in enumerate(zip(got, want)):
+        if a != b:
+            raise AssertionError(f"{what}: first difference at {i} of {len(got)}/{len(want)}: got {a!r} want {b!r}")
+    raise AssertionError(f"{what}: lengths differ: got {len(got)} want {len(want)}")
+
+
 def zipf_index(rng, n: int, nflows: int, s: float = 1.1) -> np.ndarray:
     p = np.arange(1, nflows + 1, dtype=np.float64) ** -s
     cdf = np.cumsum(p)

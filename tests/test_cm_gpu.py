@@ -4,7 +4,7 @@ through the C ABI with the sequential C oracle fed the same stream
 import numpy as np
 import pytest
 
-from helpers import frames_from_tuples, random_tuples, sizes_u32, zipf_keys
+from helpers import assert_same_list, frames_from_tuples, random_tuples, sizes_u32, zipf_keys
 
 pytestmark = pytest.mark.gpu
 
@@ -95,8 +95,8 @@ def test_query_and_heavy_hitters(gpu, oracle):
     absent = rng.integers(0, 256, (100, 16), dtype=np.uint8)
     assert np.array_equal(cm.query_many(absent), np.array([orc.query(bytes(f)) for f in absent], np.uint64))
     hh = cm.heavy_hitters()
-    assert [(h.Flow, h.Count) for h in hh.Count] == orc.heavy("count")
-    assert [(h.Flow, h.Size) for h in hh.Size] == orc.heavy("size")
+    assert_same_list([(h.Flow, h.Count) for h in hh.Count], orc.heavy("count"))
+    assert_same_list([(h.Flow, h.Size) for h in hh.Size], orc.heavy("size"))
     assert hh.Size is not None
 
 
@@ -127,8 +127,8 @@ def test_heavy_hitter_ties_beyond_first_bytes(gpu, oracle, K):
     cm.flush()
     hh = cm.heavy_hitters()
     got_c = [(h.Flow, h.Count) for h in hh.Count]
-    assert got_c == orc.heavy("count")
-    assert [(h.Flow, h.Size) for h in hh.Size] == orc.heavy("size")
+    assert_same_list(got_c, orc.heavy("count"))
+    assert_same_list([(h.Flow, h.Size) for h in hh.Size], orc.heavy("size"))
     assert len(got_c) > 100 and len({v for _, v in got_c}) <= 6  # many ties
 
 
@@ -292,7 +292,7 @@ def test_wide_rows_parity(gpu, oracle, w, d, K, nflows, n):
     q = cm.query_many(flows[:2000])
     assert np.array_equal(q, np.array([orc.query(bytes(f)) for f in flows[:2000]], np.uint64))
     hh = cm.heavy_hitters()
-    assert [(h.Flow, h.Count) for h in hh.Count] == orc.heavy("count")
+    assert_same_list([(h.Flow, h.Count) for h in hh.Count], orc.heavy("count"))
 
 
 @pytest.mark.parametrize("w,d,K,nflows,n", [
@@ -416,8 +416,8 @@ def test_view_answers_the_state_at_refresh_while_ingesting(gpu, oracle):
     orc.insert_keys(keys[a:b], sizes[a:b])
     view.refresh()                    # now the whole stream
     hh = view.heavy_hitters()
-    assert [(h.Flow, h.Count) for h in hh.Count] == orc.heavy("count")
-    assert [(h.Flow, h.Size) for h in hh.Size] == orc.heavy("size")
+    assert_same_list([(h.Flow, h.Count) for h in hh.Count], orc.heavy("count"))
+    assert_same_list([(h.Flow, h.Size) for h in hh.Size], orc.heavy("size"))
     cm.flush()
     assert_same_state(cm, orc)
     cm.reset()

@@ -1,0 +1,98 @@
+"""BASELINE configs checked against the oracle on the GPU, at the kernels and
+launch shapes the benchmarks time (verdict r2 #1):
+  configs[4]: 5-tuple header records at d=8 w=2^24 through insert_headers (the
+              1024-thread K1 instantiation k_extract<IN_HDR, ., 37, 0, 1024>),
+              and the hybrid bench's concurrent exact + Count-Min ingest on two
+              host threads / two streams (bench.py bench_hybrid).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from helpers import assert_same_flows, assert_same_list
+
+pytestmark = pytest.mark.gpu
+
+FIVE = ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"]
+
+
+def _same_state(cm, orc):
+    C, S, Fc, Fs = cm.export_state()
+    oC, oS, oFc, oFs = orc.export()
+    for name, a, b in (("C", C, oC), ("S", S, oS), ("FPc", Fc, oFc), ("FPs", Fs, oFs)):
+        if not np.array_equal(a, b):
+            bad = np.flatnonzero(a != b) if a.ndim == 1 else np.flatnonzero((a != b).any(axis=1))
+            raise AssertionError(f"{name} differs in {len(bad)} cells, first {bad[:5]}")
+
+
+def test_c5_geometry_header_records(gpu, oracle):
+    """configs[4] geometry (d=8, w=2^24) on device-resident 5-tuple header records,
+    2M Zipf packets in two calls: full state, queries and both heavy-hitter lists."""
+    import torch
+    from go2netspectra_amd import CountMin, SyntheticTraffic
+    n = 2_000_000
+    hdr, wl = SyntheticTraffic().generate(n)
+    seeds = np.random.default_rng(55).integers(0, 2**32, 8, dtype=np.uint64).astype(np.uint32)
+    cm = CountMin(1 << 24, 8, 1 << 18, 200, flow_fields=FIVE, seeds=seeds, max_flows=1 << 21)
+    cm.insert_headers(hdr[: n // 2], wl[: n // 2])
+    cm.insert_headers(hdr[n // 2:], wl[n // 2:])
+    cm.flush()
+    torch.cuda.synchronize()
+    orc = oracle.CountMin(1 << 24, 8, 1 << 18, 200, 37, seeds)
+    h, w = hdr.cpu().numpy(), wl.cpu().numpy().view(np.uint32)
+    assert orc.insert_hdr64(h, w, FIVE) == n
+    _same_state(cm, orc)
+    hh = cm.heavy_hitters()
+    assert_same_list([(x.Flow, x.Count) for x in hh.Count], orc.heavy("count"))
+    assert_same_list([(x.Flow, x.Size) for x in hh.Size], orc.heavy("size"))
+    keys = np.zeros((4096, 37), np.uint8)
+    keys[:, 0:4], keys[:, 16:20], keys[:, 32:36], keys[:, 36] = h[:4096, 26:30], h[:4096, 30:34], h[:4096, 34:38], h[:4096, 23]
+    assert np.array_equal(cm.query_many(keys), np.array([orc.query(bytes(k)) for k in keys], np.uint64))
+    del orc
+
+
+def test_hybrid_concurrent_exact_and_countmin(gpu, oracle):
+    """bench_hybrid's ingest: per window the exact aggregator runs on its own host
+    thread / stream while the Count-Min handle ingests the same records from the
+    main thread; a snapshot view answers heavy hitters after each window.  Both
+    engines must equal their sequential oracles."""
+    import torch
+    from go2netspectra_amd import CountMin, ExactTask, HeaderBatch, SyntheticTraffic
+    n, windows = 600_000, 3
+    syn = SyntheticTraffic()
+    seeds = np.random.default_rng(66).integers(0, 2**32, 8, dtype=np.uint64).astype(np.uint32)
+    ex = ExactTask("per_five_tuple", FIVE, 128, max_flows=1 << 21, batch_packets=n)
+    cm = CountMin(1 << 22, 8, 1 << 18, 200, flow_fields=FIVE, seeds=seeds, max_flows=1 << 21, batch_packets=n)
+    view = cm.view()
+    o_cm = oracle.CountMin(1 << 22, 8, 1 << 18, 200, 37, seeds)
+    o_ex = oracle.Exact(FIVE)
+    for k in range(windows):
+        hdr, wl = syn.generate(n, first=k * n)
+        ts = torch.arange(n, dtype=torch.int64, device="cuda") * 100 + k * n * 100 + 1_700_000_000_000_000_000
+        errs = []
+
+        def ex_step():
+            try:
+                ex.process_packets(HeaderBatch(hdr, wl, ts))
+                ex.flush()
+            except Exception as e:  # pragma: no cover - reported below
+                errs.append(e)
+
+        te = threading.Thread(target=ex_step)
+        te.start()
+        cm.insert_headers(hdr, wl)
+        te.join()
+        assert not errs, errs
+        view.refresh()
+        h, w = hdr.cpu().numpy(), wl.cpu().numpy().view(np.uint32)
+        o_cm.insert_hdr64(h, w, FIVE)
+        o_ex.insert_hdr64(h, w, ts.cpu().numpy())
+        hh = view.heavy_hitters()
+        assert_same_list([(x.Flow, x.Count) for x in hh.Count], o_cm.heavy("count"))
+        assert_same_list([(x.Flow, x.Size) for x in hh.Size], o_cm.heavy("size"))
+    cm.flush()
+    _same_state(cm, o_cm)
+    got = {f.Key: (f.StartTime, f.EndTime, f.PacketCount, f.ByteCount) for f in ex.flows()}
+    assert_same_flows(got, o_ex.export())
+    view.close()

@@ -153,3 +153,69 @@ def test_bucket_slices_allgather(world):
     for g, w in zip(got, want):
         assert np.array_equal(g, w)
     assert want[0].any()
+
+
+# --- configs[3] routing: each rank holds a contiguous slice of the stream, ----
+# partitions it by owner shard and exchanges the runs (all-to-all); every rank
+# must receive exactly the stable filter stream[shard_of(src) == rank] and its
+# sketch must equal the oracle fed that filter.
+def _route_stream(n=12_000):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import frames_from_tuples, random_tuples
+    rng = np.random.default_rng(77)
+    t = random_tuples(rng, n, 900)
+    return frames_from_tuples(t), t["length"], t["src16"]
+
+
+def _route_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from go2netspectra_amd.dist import exchange_runs, stable_split_records
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    hdr, wl, src = _route_stream()
+    sl = np.array_split(np.arange(len(wl)), world)[rank]     # this rank's slice of the stream
+    rh, rw, counts = stable_split_records(hdr[sl], wl[sl], world, src[sl])
+    in_h, in_w = exchange_runs(torch.from_numpy(np.ascontiguousarray(rh)),
+                               torch.from_numpy(np.ascontiguousarray(rw).view(np.int32)), counts, world)
+    q.put((rank, in_h.numpy().copy(), in_w.numpy().view(np.uint32).copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_route_exchange_delivers_the_stable_filter(world):
+    import sys
+    sys.path.insert(0, ROOT)
+    from go2netspectra_amd.dist import shard_of
+    from oracle import oracle as orc
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_route_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (h, w)) for r, h, w in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    hdr, wl, src = _route_stream()
+    owner = shard_of(src, world)
+    fields = ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"]
+    seeds = np.array([5, 6, 7], np.uint32)
+    total = 0
+    for g in range(world):
+        h, w = got[g]
+        assert np.array_equal(h, hdr[owner == g]) and np.array_equal(w, wl[owner == g])
+        total += len(w)
+        a = orc.CountMin(1024, 3, 50_000, 20, 37, seeds)
+        b = orc.CountMin(1024, 3, 50_000, 20, 37, seeds)
+        a.insert_hdr64(h, w, fields)
+        b.insert_hdr64(hdr[owner == g], wl[owner == g], fields)
+        for x, y in zip(a.export(), b.export()):
+            assert np.array_equal(x, y)
+    assert total == len(wl)

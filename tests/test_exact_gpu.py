@@ -5,7 +5,7 @@ string itself."""
 import numpy as np
 import pytest
 
-from helpers import frames_from_tuples, random_tuples
+from helpers import assert_same_flows, frames_from_tuples, random_tuples
 
 pytestmark = pytest.mark.gpu
 
@@ -52,7 +52,7 @@ def test_tuples_parity(gpu, oracle):
     want = orc.export()
     got = gpu_flows(task)
     assert len(got) == len(want)
-    assert got == want
+    assert_same_flows(got, want)
     snap = task.snapshot()
     assert snap.TaskName == "per_five_tuple" and len(snap.Shards) == 128
     assert sum(len(s.Flows) for s in snap.Shards) == len(want)
@@ -72,13 +72,13 @@ def test_headers_parity_and_reset(gpu, oracle, fields):
     orc = oracle.Exact(fields)
     done = orc.insert_hdr64(hdr, t["length"], ts)
     assert task.agg.counters()["inserted"] == done
-    assert gpu_flows(task) == orc.export()
+    assert_same_flows(gpu_flows(task), orc.export())
     task.reset()
     orc.reset()
     task.process_packets(HeaderBatch(hdr[:5000], t["length"][:5000], ts[:5000] + 7))
     orc.insert_hdr64(hdr[:5000], t["length"][:5000], ts[:5000] + 7)
     task.flush()
-    assert gpu_flows(task) == orc.export()
+    assert_same_flows(gpu_flows(task), orc.export())
 
 
 def test_query(gpu, oracle):
@@ -122,7 +122,7 @@ def test_synthetic_device_resident(gpu, oracle):
     torch.cuda.synchronize()
     orc = oracle.Exact(FIVE)
     assert orc.insert_hdr64(hdr.cpu().numpy(), wl.cpu().numpy().view(np.uint32), ts.cpu().numpy()) == 2_000_000
-    assert gpu_flows(task) == orc.export()
+    assert_same_flows(gpu_flows(task), orc.export())
 
 
 def test_manager_exact_group(gpu, oracle):
@@ -148,7 +148,7 @@ aggregator:
     orc.insert_hdr64(hdr, t["length"], ts)
     got = {k: (f.StartTime, f.EndTime, f.PacketCount, f.ByteCount)
            for s in snaps["per_five_tuple"].Shards for k, f in s.Flows.items()}
-    assert got == orc.export()
+    assert_same_flows(got, orc.export())
     task = mgr.tasks()[0]
     msg = task.alerter_msg([{"name": "r", "task_name": "per_five_tuple", "metric": "total_packets",
                              "operator": ">", "threshold": 100}])
@@ -176,7 +176,7 @@ def test_full_dictionary_is_cleared_by_reset(gpu, oracle):
     task.process_packets(HeaderBatch(hdr2, t2["length"], ts2))
     task.flush()
     orc.insert_hdr64(hdr2, t2["length"], ts2)
-    assert gpu_flows(task) == orc.export()
+    assert_same_flows(gpu_flows(task), orc.export())
 
 
 @pytest.mark.parametrize("batch", [16384, 1 << 24])
@@ -202,7 +202,7 @@ def test_wire_lengths_beyond_the_sort_word_field(gpu, oracle, batch):
     task.flush()
     orc = oracle.Exact(FIVE)
     orc.insert_tuples(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], ipver, lens, ts)
-    assert gpu_flows(task) == orc.export()
+    assert_same_flows(gpu_flows(task), orc.export())
 
 
 def test_pcapng_capture_drives_exact_and_countmin(gpu, oracle, tmp_path):
@@ -226,7 +226,7 @@ def test_pcapng_capture_drives_exact_and_countmin(gpu, oracle, tmp_path):
     task.flush()
     orc = oracle.Exact(FIVE)
     orc.insert_hdr64(hb.hdr, hb.wirelen, hb.ts)
-    assert gpu_flows(task) == orc.export()
+    assert_same_flows(gpu_flows(task), orc.export())
     seeds = np.array([0x9747B28C, 0x1B873593, 0xCC9E2D51], np.uint32)
     cm = CountMin(4096, 3, 1 << 20, 50, flow_fields=FIVE, seeds=seeds, max_flows=1 << 14)
     cm.insert_headers(hb.hdr, hb.wirelen)
@@ -235,3 +235,23 @@ def test_pcapng_capture_drives_exact_and_countmin(gpu, oracle, tmp_path):
     o.insert_hdr64(hb.hdr, hb.wirelen, FIVE)
     for a, b in zip(cm.export_state(), o.export()):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("batch", [4096, 300_000, 1_500_000])
+def test_start_end_times_with_heavy_ties_across_sort_paths(gpu, oracle, batch):
+    """X2 sorts the flow-id bits only and relies on a stable sort for StartTime /
+    EndTime (the first / last packet of each run).  Batch sizes span rocPRIM's
+    single-block, (disabled) merge-sort and Onesweep ranges; 40 flows make every
+    flow a long run of ties, timestamps are random so any reordering shows."""
+    from go2netspectra_amd import ExactTask, PacketBatch
+    rng = np.random.default_rng(batch)
+    n = 3_000_000
+    t = random_tuples(rng, n, 40, s=0.8)
+    ts = rng.integers(-(1 << 60), 1 << 60, n).astype(np.int64)
+    ipver = np.where(t["v6"], 6, 4).astype(np.uint8)
+    task = ExactTask("ties", FIVE, batch_packets=batch, max_flows=1 << 10)
+    task.process_packets(PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"], ipver, ts))
+    task.flush()
+    orc = oracle.Exact(FIVE)
+    orc.insert_tuples(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], ipver, t["length"], ts)
+    assert_same_flows(gpu_flows(task), orc.export())

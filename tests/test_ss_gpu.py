@@ -6,7 +6,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import frames_from_tuples, random_tuples, zipf_index
+from helpers import assert_same_list, frames_from_tuples, random_tuples, zipf_index
 
 pytestmark = pytest.mark.gpu
 
@@ -207,7 +207,7 @@ def test_synthetic_device_resident(gpu, oracle):
         got = orc.insert_hdr64(hdr.cpu().numpy(), wl.cpu().numpy().view(np.uint32), ["SrcIP"], ["DstIP"])
         assert got == 1_000_000
         assert_same_ss(ss, orc)
-    assert [(h.Flow, h.Count) for h in ss.heavy_hitters().Count] == orc.heavy()
+    assert_same_list([(h.Flow, h.Count) for h in ss.heavy_hitters().Count], orc.heavy())
 
 
 def test_superspreader_accuracy(gpu, oracle):
