@@ -46,8 +46,28 @@ def row_seeds(d):
     return np.array(out, np.uint32)
 
 
-def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, depth: int = DEPTH, fields=FIELDS):
-    """Timed CPU restatements on a bounded prefix of the same stream (rank 0)."""
+def host_cpu():
+    """The GPU box's host CPU as BASELINE.md asks it to be reported (nproc, lscpu model)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": avail, "model": model}
+
+
+def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, depth: int = DEPTH, fields=FIELDS,
+                 keep_state: bool = False):
+    """Timed CPU restatements on a bounded prefix of the same stream (rank 0).
+    keep_state: also return the sequential oracle (the parity check replays the
+    same prefix through the engine)."""
     from oracle import oracle as orc
     n = min(int(wl_dev.shape[0]), 24_000_000)
     hdr = hdr_dev[:n].cpu().numpy()
@@ -63,7 +83,9 @@ def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, dept
         done += m
     seq_rate = done / (time.perf_counter() - t0) / 1e6
     seq_n = done
-    del cm
+    seq_state = cm if keep_state else None
+    if not keep_state:
+        del cm
     # (2) restatement of the Go worker pool (shared sketch, CAS loops, shared cursor)
     threads = int(os.environ.get("GNS_CPU_THREADS", min(16, os.cpu_count() or 1)))
     cm = orc.CountMin(width, depth, 1 << 20, 1000, K, seeds)
@@ -74,12 +96,15 @@ def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, dept
         cm.insert_hdr64_pool(hdr[done:done + m], wl[done:done + m], fields, threads)
         done += m
     pool_rate = done / (time.perf_counter() - t0) / 1e6
-    return {
+    out = {
         "value": round(pool_rate, 3), "unit": "Mpackets/s", "cores": threads, "kind": "port",
-        "sample": f"first {done:,} packets of the same synthetic stream; C restatement of the Go worker pool "
-                  f"(count_min.go CAS loops + parse/encode, {threads} threads, shared cursor)",
+        "sample": f"first {done:,} packets of the same synthetic stream (window 0); C restatement of the Go "
+                  f"worker pool (count_min.go CAS loops + parse/encode, {threads} threads = the reference's "
+                  f"num_workers default, shared cursor)",
+        "host": host_cpu(),
         "sequential_oracle": {"value": round(seq_rate, 3), "cores": 1, "packets": seq_n},
     }
+    return (out, seq_state, seq_n) if keep_state else out
 
 
 def cpu_baseline_ss(hdr_dev, wl_dev, seconds: float = 10.0):
@@ -95,7 +120,7 @@ def cpu_baseline_ss(hdr_dev, wl_dev, seconds: float = 10.0):
         ss.insert_hdr64(hdr[done:done + m], wl[done:done + m], ["SrcIP"], ["DstIP"])
         done += m
     rate = done / (time.perf_counter() - t0) / 1e6
-    return {"value": round(rate, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port",
+    return {"value": round(rate, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port", "host": host_cpu(),
             "sample": f"first {done:,} packets of window 0; sequential C restatement of "
                       f"super_spread.go (parse + encode + HLL + MV), 1 thread"}
 
@@ -150,7 +175,7 @@ def bench_superspread(args, torch, dist, world, rank, local):
     pkts_per_launch = n * args.steps / max(dom_launches, 1)
     achieved = BYTES_PER_PKT * pkts_per_launch / (avg_ms * 1e-3) / 1e9
     traffic = None  # PMC HBM bytes per launch of the dominant kernel (tools/pmc_ss.sh)
-    tfile = os.path.join(ROOT, "profiles", "traffic_ss_latest.json")
+    tfile = os.path.join(ROOT, "profiles", f"traffic_ss_d{SS_D}_w{SS_W}.json")
     if os.path.exists(tfile):
         try:
             traffic = json.load(open(tfile)).get(dom)
@@ -195,7 +220,7 @@ def cpu_baseline_exact(hdr_dev, wl_dev, ts_dev, seconds: float = 10.0):
         ex.insert_hdr64(hdr[done:done + m], wl[done:done + m], ts[done:done + m])
         done += m
     rate = done / (time.perf_counter() - t0) / 1e6
-    return {"value": round(rate, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port",
+    return {"value": round(rate, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port", "host": host_cpu(),
             "sample": f"first {done:,} packets; sequential C restatement of exact/task.go (parse, Go key "
                       f"string, hash map), 1 thread"}
 
@@ -482,9 +507,10 @@ def bench_hybrid(args, torch, dist, world, rank, local):
         dist.destroy_process_group()
 
 
-def bench_windows(args, torch, dist, world, cm, step, barrier, n):
+def bench_windows(args, torch, dist, world, cm, timed_step, n):
     """configs[3]'s per-window cycle, timed after the headline steps: each window
-    inserts --window-steps steps of packets, takes the shard's heavy hitters on the device
+    inserts --window-steps fresh steps of packets (timed_step: generation outside
+    the timed part), takes the shard's heavy hitters on the device
     (gns_cm_heavy_hitters: candidates, dedupe, order) and all-gathers every
     shard's list over RCCL (dist.allgather_heavy_arrays; flows are disjoint across
     shards, so the union is the global list).  Max over ranks, like the steps."""
@@ -493,26 +519,21 @@ def bench_windows(args, torch, dist, world, cm, step, barrier, n):
     arrs = cm.heavy_hitters_arrays()  # warm: the read side's grow-only buffers
     if world > 1:
         allgather_heavy_arrays(arrs, world)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
     for _ in range(args.windows):
-        a = time.perf_counter()
         for _ in range(args.window_steps):
-            step()
-        cm.flush()
+            t_ins += timed_step()
+        if world > 1:
+            dist.barrier()
         b = time.perf_counter()
         arrs = cm.heavy_hitters_arrays()
         c = time.perf_counter()
         if world > 1:
             arrs = allgather_heavy_arrays(arrs, world)
+            dist.barrier()
         e = time.perf_counter()
-        t_ins += b - a
         t_hh += c - b
         t_x += e - c
-    torch.cuda.synchronize()
-    barrier()
-    el = time.perf_counter() - t0
+    el = t_ins + t_hh + t_x
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -544,14 +565,17 @@ def main():
                     help="flow dictionary capacity (slots = next power of two >= 2x)")
     ap.add_argument("--ex-max-flows", type=int, default=1 << 21,
                     help="exact aggregator flow dictionary capacity (--sketch exact / hybrid)")
-    ap.add_argument("--windows", type=int, default=3,
+    ap.add_argument("--windows", type=int, default=1,
                     help="after the timed steps: W timed windows of insert + device heavy hitters + "
                          "all-gather of every shard's list (configs[3] per-window exchange); 0 = off")
-    ap.add_argument("--window-steps", type=int, default=20,
-                    help="steps per window (20 x 100M packets per GPU = 0.1 s of ingest; configs[3] says 1 s)")
+    ap.add_argument("--window-steps", type=int, default=10,
+                    help="steps per window (fresh 100M-packet windows; configs[3] says a 1 s window)")
     ap.add_argument("--hybrid-serial", action="store_true",
                     help="--sketch hybrid: run the exact and sketch paths one after the other from one host "
                          "thread instead of concurrently on two streams from two threads")
+    ap.add_argument("--route", action="store_true",
+                    help="configs[3] pipeline (N > 1): each GPU holds a contiguous slice of the unsharded stream; "
+                         "the timed step partitions it on the device, all-to-alls the shard runs and inserts")
     ap.add_argument("--key", choices=["5tuple", "srcip"], default="5tuple",
                     help="flow key: full 5-tuple (37 B, primary) or [SrcIP] (16 B, the default task layout)")
     ap.add_argument("--flows", type=int, default=1 << 20,
@@ -594,40 +618,58 @@ def main():
     if args.sketch == "hybrid":
         return bench_hybrid(args, torch, dist, world, rank, local)
     n = args.packets
-    syn = SyntheticTraffic(flows=args.flows, shard=rank, nshards=world, device=local)
-    hdr, wl = syn.generate(n)
-    batch = args.batch or n
     fields = FIELDS if args.key == "5tuple" else ["SrcIP"]
+    K = 37 if args.key == "5tuple" else 16
+    dev = torch.device("cuda", local)
+    route = args.route and world > 1
+    # Input windows.  Every step inserts a FRESH window of the stream, generated on
+    # the device before the step's opening barrier and excluded from the timed sum:
+    #  - default (weak scaling): rank r's window k = packets [k*n, (k+1)*n) of its
+    #    shard stream, the stable filter stream[shard_of(src) == r] (what the
+    #    routing step delivers; SyntheticTraffic(shard, nshards));
+    #  - --route (configs[3] pipeline): rank r holds the contiguous slice
+    #    [(k*world + r)*n, ...) of the UNSHARDED stream; the timed step partitions
+    #    it on the device, all-to-alls the runs and inserts what it received.
+    syn = SyntheticTraffic(flows=args.flows, shard=0 if route else rank, nshards=1 if route else world, device=local)
+    hdr = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    wl = torch.empty((n,), dtype=torch.int32, device=dev)
+    win = [0]
+
+    def next_window():
+        k = win[0]
+        win[0] += 1
+        syn.fill(hdr, wl, first=(k * world + rank) * n if route else k * n)
+
+    batch = args.batch or n
     cm = CountMin(args.width, args.depth, 1 << 20, 1000, flow_fields=fields, seeds=row_seeds(args.depth),
                   max_flows=args.max_flows, batch_packets=batch, device=local)
+    router = None
+    if route:
+        from go2netspectra_amd.dist import Router
+        router = Router(world, local)
     torch.cuda.synchronize()
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    src_hdr, src_wl, tuples = hdr, wl, None
+    tuples = None
     window_out = None
-    if args.host_input:  # pinned host copies; the engine stages them H2D per device batch
+    pin = None
+    if args.host_input:  # pinned host buffers; the engine stages them H2D per device batch
         def pinned(a):
-            t = torch.empty(a.shape, dtype=a.dtype, pin_memory=True)
-            t.copy_(a)
-            return t
+            return torch.empty(a.shape, dtype=a.dtype, pin_memory=True)
         if args.host_input == "tuples":  # PacketInfo SoA (src16, dst16, ports, proto, length) = 41 B/packet
             from go2netspectra_amd.packets import PacketBatch
-            h = hdr.view(torch.int32).view(torch.uint8)
-            src16 = torch.zeros((n, 16), dtype=torch.uint8, device=hdr.device)
-            dst16 = torch.zeros((n, 16), dtype=torch.uint8, device=hdr.device)
-            src16[:, :4] = h[:, 26:30]
-            dst16[:, :4] = h[:, 30:34]
-            sport = (h[:, 34].to(torch.int32) << 8 | h[:, 35].to(torch.int32)).to(torch.int16)
-            dport = (h[:, 36].to(torch.int32) << 8 | h[:, 37].to(torch.int32)).to(torch.int16)
-            tuples = PacketBatch(pinned(src16).numpy(), pinned(dst16).numpy(), pinned(sport).numpy().view(np.uint16),
-                                 pinned(dport).numpy().view(np.uint16), pinned(h[:, 23].contiguous()).numpy(),
-                                 pinned(wl).numpy().view(np.uint32))
-            del src16, dst16, sport, dport
+            pin = {"src16": pinned(torch.empty((n, 16), dtype=torch.uint8)),
+                   "dst16": pinned(torch.empty((n, 16), dtype=torch.uint8)),
+                   "sport": pinned(torch.empty((n,), dtype=torch.int16)), "dport": pinned(torch.empty((n,), dtype=torch.int16)),
+                   "proto": pinned(torch.empty((n,), dtype=torch.uint8)), "length": pinned(torch.empty((n,), dtype=torch.int32))}
+            tuples = PacketBatch(pin["src16"].numpy(), pin["dst16"].numpy(), pin["sport"].numpy().view(np.uint16),
+                                 pin["dport"].numpy().view(np.uint16), pin["proto"].numpy(),
+                                 pin["length"].numpy().view(np.uint32))
         else:
-            src_hdr, src_wl = pinned(hdr).numpy(), pinned(wl).numpy().view(np.uint32)
+            pin = {"hdr": pinned(hdr), "wl": pinned(wl)}
         cnt_C = np.empty(args.depth * args.width, np.uint32)
         cnt_S = np.empty(args.depth * args.width, np.uint32)
 
@@ -635,29 +677,64 @@ def main():
             cm.export_counters(cnt_C, cnt_S)
             return cm.heavy_hitters_arrays()
 
-    def step():
+    def stage_host():  # untimed: this step's window into the pinned host buffers
+        if pin is None:
+            return
         if tuples is not None:
-            cm.insert_tuples(tuples)
+            h = hdr.view(torch.uint8)
+            src16 = torch.zeros((n, 16), dtype=torch.uint8, device=dev)
+            dst16 = torch.zeros((n, 16), dtype=torch.uint8, device=dev)
+            src16[:, :4] = h[:, 26:30]
+            dst16[:, :4] = h[:, 30:34]
+            pin["src16"].copy_(src16)
+            pin["dst16"].copy_(dst16)
+            pin["sport"].copy_((h[:, 34].to(torch.int32) << 8 | h[:, 35].to(torch.int32)).to(torch.int16))
+            pin["dport"].copy_((h[:, 36].to(torch.int32) << 8 | h[:, 37].to(torch.int32)).to(torch.int16))
+            pin["proto"].copy_(h[:, 23])
+            pin["length"].copy_(wl)
         else:
-            cm.insert_headers(src_hdr, src_wl)
+            pin["hdr"].copy_(hdr)
+            pin["wl"].copy_(wl)
+
+    def step():
+        if route:
+            from go2netspectra_amd.dist import exchange_runs
+            oh, ow, counts = router.partition(hdr, wl)
+            if dist.get_backend() != "nccl":  # gloo rehearsal: the exchange goes through host memory
+                ih, iw = exchange_runs(oh.cpu(), ow.cpu(), counts, world)
+                ih, iw = ih.to(dev), iw.to(dev)
+            else:
+                ih, iw = exchange_runs(oh, ow, counts, world)
+            cm.insert_headers(ih, iw)
+        elif tuples is not None:
+            cm.insert_tuples(tuples)
+        elif pin is not None:
+            cm.insert_headers(pin["hdr"].numpy(), pin["wl"].numpy().view(np.uint32))
+        else:
+            cm.insert_headers(hdr, wl)
         if window_out is not None:
             window_out()
 
-    for _ in range(args.warmup):
+    def timed_step():
+        """one fresh window: generated (untimed), then barrier + sync, the step, sync + barrier"""
+        next_window()
+        stage_host()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
         step()
         cm.flush()
+        torch.cuda.synchronize()
+        barrier()
+        return time.perf_counter() - t0
+
+    for _ in range(args.warmup):
+        timed_step()
     cm.set_timing(True)
     cm.stage_times(reset=True)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    elapsed = 0.0
     for _ in range(args.steps):
-        step()
-    cm.flush()
-    torch.cuda.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+        elapsed += timed_step()
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -666,8 +743,8 @@ def main():
     counters = cm.counters()
 
     window = None
-    if args.windows > 0 and not args.host_input:
-        window = bench_windows(args, torch, dist, world, cm, step, barrier, n)
+    if args.windows > 0 and not args.host_input and not route:
+        window = bench_windows(args, torch, dist, world, cm, timed_step, n)
 
     hh = cm.heavy_hitters()
     if world > 1:
@@ -683,9 +760,9 @@ def main():
     avg_ms = dom_ms / max(dom_launches, 1)
     pkts_per_launch = n * args.steps / max(dom_launches, 1)
     achieved = BYTES_PER_PKT * pkts_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "traffic_latest.json")
-    if os.path.exists(tfile):
+    traffic = None  # PMC record of THIS geometry only (tools/pmc_cm.sh -> profiles/traffic_cm_d*_w*_k*.json)
+    tfile = os.path.join(ROOT, "profiles", f"traffic_cm_d{args.depth}_w{args.width}_k{K}.json")
+    if os.path.exists(tfile) and not route and args.flows == 1 << 20:
         try:
             traffic = json.load(open(tfile)).get(dom)
         except Exception:
@@ -696,10 +773,13 @@ def main():
         "value": round(value, 2), "unit": "Mpackets/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-        "data": "synthetic (Zipf 1.1 over 2^20 5-tuples, 64-B Ethernet/IPv4/TCP|UDP records, on-device generator)",
+        "data": "synthetic (Zipf 1.1 over 2^20 5-tuples, 64-B Ethernet/IPv4/TCP|UDP records, on-device generator; "
+                "a fresh window of the stream per step, generated outside the timed region)",
         "config": {"workload": "configs[1]: Count-Min d=4 w=2^20, 100M Zipf(1.1) 5-tuple headers in HBM per GPU, "
                                "bit-exact counters", "packets_per_step_per_gpu": n, "device_batch": batch,
-                   "key": "5-tuple (37 B)", "parallelism": f"flow-hash shards x{world}"},
+                   "key": "5-tuple (37 B)" if K == 37 else "[SrcIP] (16 B)",
+                   "parallelism": f"flow-hash shards x{world}",
+                   "windows": f"steps use stream windows 0..{win[0] - 1} (warmup first), none replayed"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_packet": BYTES_PER_PKT, "kernel_avg_ms": round(avg_ms, 4),
@@ -720,18 +800,30 @@ def main():
                                       f"100M Zipf(1.1) 5-tuple headers in HBM per GPU, bit-exact counters")
         line["note"] = "not the headline metric (BASELINE.json metric is d=4 w=2^20)"
     if args.key != "5tuple":
-        line["config"]["key"] = "[SrcIP] (16 B)"
         line["note"] = "secondary key layout (SURVEY §8d); the headline uses the 5-tuple key"
     if args.flows != 1 << 20:
         line["config"]["flows"] = args.flows
         line["note"] = "not the headline metric (BASELINE.json stream has 2^20 flows)"
+    if route:
+        line["metric"] = "Mpackets/s routed CMS update (device partition + RCCL all-to-all + insert), d=4 w=2^20"
+        line["config"]["workload"] = ("configs[3]: each GPU holds a contiguous slice of the unsharded stream; a "
+                                      "timed step partitions it by owner shard on the device, exchanges the runs "
+                                      "(all-to-all) and inserts its shard's packets")
+        line["note"] = "not the headline metric: includes the routing exchange"
     if args.host_input:
         line["metric"] = ("Mpackets/s CMS update, HOST-resident input (PCIe H2D of %s + per-window D2H of "
                           "counter rows and heavy hitters), d=4 w=2^20" % args.host_input)
         line["note"] = "not the headline metric: inputs start in pinned host memory, outputs end in host memory"
         line["config"]["host_input"] = args.host_input
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(hdr, wl, width=args.width, depth=args.depth, fields=fields)
+        # CPU legs on a bounded prefix of window 0, then the parity check: the same
+        # prefix through a fresh engine handle must equal the sequential oracle
+        m = min(n, 24_000_000)
+        ph, pw = syn.generate(m, first=0)
+        base, orc_state, seq_n = cpu_baseline(ph, pw, width=args.width, depth=args.depth, fields=fields,
+                                              keep_state=True)
+        line["cpu_baseline"] = base
+        line["parity"] = parity_check(orc_state, ph[:seq_n], pw[:seq_n], args, fields)
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:
@@ -739,6 +831,26 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def parity_check(orc_state, hdr, wl, args, fields):
+    """After the timed region: the CPU leg's prefix (same packets, same seeds)
+    through a fresh engine handle, whole exported state compared with the
+    sequential oracle (C, S, both fingerprint arrays, both heavy-hitter lists)."""
+    from go2netspectra_amd import CountMin
+    cm = CountMin(args.width, args.depth, 1 << 20, 1000, flow_fields=fields, seeds=row_seeds(args.depth),
+                  max_flows=args.max_flows, batch_packets=args.batch or args.packets, device=hdr.device.index or 0)
+    cm.insert_headers(hdr, wl)
+    cm.flush()
+    got = cm.export_state()
+    want = orc_state.export()
+    same = {name: bool(np.array_equal(a, b)) for name, a, b in zip(("C", "S", "FPc", "FPs"), got, want)}
+    hh = cm.heavy_hitters()
+    same["heavy_count"] = [(h.Flow, h.Count) for h in hh.Count] == orc_state.heavy("count")
+    same["heavy_size"] = [(h.Flow, h.Size) for h in hh.Size] == orc_state.heavy("size")
+    cm.close()
+    return {"checked_packets": int(wl.shape[0]), "bit_exact": all(same.values()), "arrays": same,
+            "how": "the cpu_baseline sequential oracle's prefix of window 0 through a fresh handle"}
 
 
 if __name__ == "__main__":

@@ -160,6 +160,23 @@ def load() -> ct.CDLL:
     return L
 
 
+def device_ready(*arrays) -> None:
+    """Device tensors handed to the engine must be complete: the engines launch on
+    their own non-blocking streams, which are not ordered after torch's stream
+    that produced the data.  Synchronize torch's current stream of every device
+    involved (once per device) before the call."""
+    seen = set()
+    for a in arrays:
+        if a is None or not getattr(a, "is_cuda", False):
+            continue
+        d = a.device.index
+        if d in seen:
+            continue
+        seen.add(d)
+        import torch
+        torch.cuda.current_stream(a.device).synchronize()
+
+
 def check(code: int) -> None:
     if code != GNS_OK:
         msg = (load().gns_last_error() or b"").decode(errors="replace")

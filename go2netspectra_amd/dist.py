@@ -99,6 +99,7 @@ class Router:
                              torch.empty((n,), dtype=torch.int32, device=hdr.device))
             out_hdr, out_wl = self._out[0][:n], self._out[1][:n]
         counts = np.zeros(self.nshards, np.uint64)
+        _lib.device_ready(hdr, wirelen)
         _lib.check(self._L.gns_route_partition(self._h, hdr.data_ptr(), wirelen.data_ptr(), n, out_hdr.data_ptr(),
                                                out_wl.data_ptr(), counts.ctypes.data))
         return out_hdr, out_wl, counts

@@ -96,6 +96,7 @@ class ExactAggregator:
     def insert_headers(self, hdr, wirelen, ts) -> None:
         dev = [_is_dev(a) for a in (hdr, wirelen, ts)]
         if all(dev):
+            _lib.device_ready(hdr, wirelen, ts)
             where = _lib.MEM_DEVICE
         elif any(dev):
             raise ValueError("mix of host and device arrays")

@@ -88,6 +88,7 @@ class PacketBatch:
         arrs = [self.src16, self.dst16, self.sport, self.dport, self.proto, self.length]
         dev = [hasattr(a, "data_ptr") and getattr(a, "is_cuda", False) for a in arrs]
         if all(dev):
+            _lib.device_ready(*arrs, self.ipver, self.ts)
             t = _lib.Tuples(*[a.data_ptr() for a in arrs])
             return t, arrs, _lib.MEM_DEVICE
         if any(dev):
@@ -286,6 +287,7 @@ class SyntheticTraffic:
             got += t
             carry = (ch[t:], cw[t:])
         self._cursor = (first + n, gpos, carry)
+        torch.cuda.current_stream(dev).synchronize()  # like gns_synth_fill: complete on return
 
     def generate(self, n: int, first: int = 0):
         import torch

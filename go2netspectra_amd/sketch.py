@@ -65,6 +65,7 @@ def _host(x, dtype) -> np.ndarray:
 def _where(*arrays) -> int:
     dev = [_is_device(a) for a in arrays if a is not None]
     if dev and all(dev):
+        _lib.device_ready(*arrays)
         return _lib.MEM_DEVICE
     if any(dev):
         raise ValueError("mix of host and device arrays in one call")
