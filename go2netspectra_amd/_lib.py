@@ -37,6 +37,7 @@ EXPORTED = [
     "gns_ex_stage_times",
     "gns_thrift_decode", "gns_pack_pcap", "gns_pack_pcap_ts", "gns_last_error", "gns_version",
     "gns_route_create", "gns_route_destroy", "gns_route_partition",
+    "gns_cm_dict_stats", "gns_ss_dict_stats", "gns_ex_dict_stats",
 ]
 
 
@@ -151,6 +152,8 @@ def load() -> ct.CDLL:
         "gns_last_error": ([], ct.c_char_p), "gns_version": ([], ct.c_char_p),
         "gns_route_create": ([u32, i32, vp], i32), "gns_route_destroy": ([vp], i32),
         "gns_route_partition": ([vp, vp, vp, u64, vp, vp, vp], i32),
+        "gns_cm_dict_stats": ([vp, vp], i32), "gns_ss_dict_stats": ([vp, vp], i32),
+        "gns_ex_dict_stats": ([vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -175,6 +178,15 @@ def device_ready(*arrays) -> None:
         seen.add(d)
         import torch
         torch.cuda.current_stream(a.device).synchronize()
+
+
+DICT_STATS = ["reclaims", "dropped", "live", "claimed", "reclaim_us", "retried_batches"]
+
+
+def dict_stats(fn, h) -> dict:
+    out = (ct.c_uint64 * 6)()
+    check(fn(h, out))
+    return dict(zip(DICT_STATS, list(out)))
 
 
 def check(code: int) -> None:

@@ -22,6 +22,7 @@
 //                   sequential replay for the buckets where it is not.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -244,7 +245,7 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) { return __ockl_wfred
 // issued earlier by the caller), publish/hash the row buckets, bin codes,
 // block histogram and designated-bucket summaries.
 struct K1Lds {
-    uint32_t *s_tab, *s_hist, *s_hFc, *s_hFs, *s_nfc, *s_nfs, *s_smax, *s_pend, *s_full;
+    uint32_t *s_tab, *s_hist, *s_hFc, *s_hFs, *s_nfc, *s_nfs, *s_smax, *s_pend, *s_full, *s_claim;
     unsigned long long *s_os, *s_fs;
 };
 
@@ -331,6 +332,11 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
             kid = out;
         }
     }
+    {   // claim accounting (one LDS add per wave; the block flushes once, dict_flush_claims)
+        const uint64_t cmask = __ballot(res == CM_CLAIMED);
+        if (cmask && (threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)cmask) - 1))
+            atomicAdd(S.s_claim, (uint32_t)__popcll(cmask));
+    }
     if (bw && res == CM_CLAIMED) {  // publish the bucket cache with the key (visible next launch)
         uint32_t *tp = a.D.rec + (size_t)out * a.D.RW;
 #pragma unroll
@@ -397,7 +403,7 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 template <int KIND, int MODE, int KB, int DD, int NT>
 __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : 1) void k_extract(ExtractArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xsm[];
-    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
+    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_claim, s_abort;
     __shared__ uint8_t s_src[80];
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
     const uint32_t NS = a.g.d * kHot;
@@ -420,13 +426,14 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : 1) void k_extract(Ext
         s_hFs[i] = id != GNS_ID_NONE ? a.Fs[cell] : GNS_ID_NONE;
         s_nfc[i] = 0; s_nfs[i] = 0; s_smax[i] = 0; s_os[i] = 0; s_fs[i] = 0;
     }
-    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; }
+    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; s_claim = 0; s_abort = dict_aborted(a.D); }
     __syncthreads();
+    if (s_abort) return;  // the batch overflowed the dictionary: it is re-run after a reclaim
     const uint64_t beg = (uint64_t)blk * kChunk;
     const uint64_t end = min(a.n, beg + kChunk);
     const bool bw = a.D.bw != 0;
     uint32_t n_ok = 0;
-    const K1Lds S{s_tab, s_hist, s_hFc, s_hFs, s_nfc, s_nfs, s_smax, &s_pend, &s_full, s_os, s_fs};
+    const K1Lds S{s_tab, s_hist, s_hFc, s_hFs, s_nfc, s_nfs, s_smax, &s_pend, &s_full, &s_claim, s_os, s_fs};
     if constexpr (KIND == IN_HDR) {
         // Two-stage software pipeline over the block's packets: iteration k
         // parses packet k+1 and issues its dictionary probe (and the header
@@ -531,6 +538,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : 1) void k_extract(Ext
         if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
         if (s_unsup) atomicAdd(&a.stats[2], (unsigned long long)s_unsup);
         if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+        dict_flush_claims(a.D, s_claim, &a.stats[3]);
     }
 }
 
@@ -553,7 +561,7 @@ struct ResolveArgs {
 // K1b: packets parked on a slot claimed in the previous launch.
 template <int KIND, int MODE>
 __global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
-    __shared__ uint32_t s_cnt, s_full;
+    __shared__ uint32_t s_cnt, s_full, s_claim, s_abort;
     __shared__ uint8_t s_src[80];
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
     const uint32_t cnt = a.cnt_in[blk];
@@ -561,9 +569,13 @@ __global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
         if (tid == 0) a.cnt_out[blk] = 0;
         return;
     }
-    stage_plan<MODE>(a.kp, s_src);
-    if (tid == 0) { s_cnt = 0; s_full = 0; }
+    if (tid == 0) { s_cnt = 0; s_full = 0; s_claim = 0; s_abort = dict_aborted(a.D); }
     __syncthreads();
+    if (s_abort) {
+        if (tid == 0) a.cnt_out[blk] = 0;
+        return;
+    }
+    stage_plan<MODE>(a.kp, s_src);
     const uint64_t beg = (uint64_t)blk * kChunk;
     for (uint32_t i = tid; i < cnt; i += kExThreads) {
         const uint64_t v = a.pend_in[beg + i];
@@ -574,6 +586,7 @@ __global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
         const int r = cm_find_or_claim(a.D, kw, a.kp.K, (uint32_t)v, a.epoch, &out, rec);
         if (r == CM_FOUND || r == CM_CLAIMED) {
             a.keyid[p] = out;
+            if (r == CM_CLAIMED) atomicAdd(&s_claim, 1u);
             if (r == CM_CLAIMED && a.D.bw) {  // bucket cache, as in k_extract
                 uint32_t mk[GNS_KWMAX];
                 mm3_premix<GNS_KWMAX>(kw, a.kp.K, mk);
@@ -593,6 +606,7 @@ __global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
         a.cnt_out[blk] = s_cnt;
         if (s_cnt) atomicAdd(a.total_out, s_cnt);
         if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+        dict_flush_claims(a.D, s_claim, &a.stats[3]);
     }
 }
 
@@ -2555,6 +2569,14 @@ struct gns_cm {
     std::vector<gns_cm_view *> views; // live snapshot views: reset and reclaim wait for their calls
     DictDev D{};
     uint64_t dict_slots = 0;
+    uint64_t max_flows = 0;               // proactive reclaim once this many slots are claimed
+    uint64_t claimed = 0;                 // D.ctl[0] as of the last batch
+    bool full = false;                    // live flows + one 16K-packet batch exceed the dictionary (sticky)
+    uint32_t *dctl = nullptr;             // D.ctl: [0] claimed slots, [1] abort flag
+    DictScratch dsc;                      // rebuild scratch (grow-only)
+    unsigned long long *stats_bak = nullptr;  // [3] counters before the running batch (undone on abort)
+    uint64_t n_reclaim = 0, n_dropped = 0, last_live = 0, n_retry = 0;
+    double reclaim_ms = 0.0;
     uint32_t epoch = 0;
     uint64_t bmax = 0;
     uint32_t nblk_max = 0;
@@ -2588,6 +2610,28 @@ struct gns_cm {
     StageTimer timer;
 };
 
+struct gns_cm_view {
+    gns_cm *cm = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ready = nullptr;
+    uint32_t *C = nullptr, *S = nullptr, *Fc = nullptr, *Fs = nullptr;
+    CmScratch rd;
+    std::mutex mu;          // refresh vs queries: a refresh waits for the query in progress
+    uint32_t period = ~0u;  // handle period of the snapshot (~0: never refreshed)
+};
+
+// Holds every registered view's mutex: no view call is running (each one
+// synchronizes its stream before it returns), so the handle may rewrite what
+// the views read (the flow dictionary) and bump the period they check.
+struct ViewsQuiesced {
+    std::unique_lock<std::mutex> reg;
+    std::vector<std::unique_lock<std::mutex>> locks;
+    explicit ViewsQuiesced(gns_cm *cm) : reg(cm->views_mu) {
+        locks.reserve(cm->views.size());
+        for (gns_cm_view *v : cm->views) locks.emplace_back(v->mu);
+    }
+};
+
 namespace {
 
 int stage_reserve(gns_cm *cm, size_t bytes) {
@@ -2615,6 +2659,7 @@ int cm_free_all(gns_cm *cm) {
     dfree(cm->work);
     dfree(cm->hot_ids); dfree(cm->segtot); dfree(cm->hflag); dfree(cm->hhist); dfree(cm->hthr); dfree(cm->hcnt);
     dfree(cm->hsum); dfree(cm->hflag2); dfree(cm->hres); dfree(cm->chk); dfree(cm->hot_tab);
+    dfree(cm->dctl); dfree(cm->stats_bak); cm->dsc.free_all();
     if (cm->h_pin) (void)hipHostFree(cm->h_pin);
     cm->timer.destroy();
     if (cm->stream) (void)hipStreamDestroy(cm->stream);
@@ -2634,7 +2679,32 @@ int cm_reset_state(gns_cm *cm) {
     // the error words (3 dict-full, 4 ovf-full) belong to the period: a reset
     // empties the dictionary, so the next period starts without them
     GNS_HIP(hipMemsetAsync(cm->stats + 3, 0, 2 * sizeof(unsigned long long), cm->stream));
+    GNS_HIP(hipMemsetAsync(cm->dctl, 0, 16, cm->stream));
+    cm->claimed = 0;
+    cm->full = false;
     cm->warm = false;
+    return GNS_OK;
+}
+
+// Reclaim: rebuild the dictionary keeping the flows a bucket (or a snapshot
+// view) still names (gns_dict.hip).  Views are quiesced and their snapshots
+// remapped with the buckets, so a view answers exactly as before.
+int cm_reclaim(gns_cm *cm) {
+    ViewsQuiesced q(cm);
+    const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
+    std::vector<DictIds> ids{{cm->Fc, cells}, {cm->Fs, cells}};
+    for (gns_cm_view *v : cm->views)
+        if (v->period != ~0u) { ids.push_back({v->Fc, cells}); ids.push_back({v->Fs, cells}); }
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t before = cm->claimed;
+    uint64_t live = 0;
+    GNS_TRY(dict_rebuild(cm->D, cm->dict_slots, ids.data(), (int)ids.size(), nullptr, ids.data(), (int)ids.size(),
+                         cm->dict_slots, cm->stream, cm->dsc, &live, nullptr));
+    cm->reclaim_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    cm->n_reclaim++;
+    cm->n_dropped += before > live ? before - live : 0;
+    cm->claimed = live;
+    cm->last_live = live;
     return GNS_OK;
 }
 
@@ -2648,6 +2718,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
     ScopedStage total_stage(cm->timer, 5);
     // K1
     GNS_HIP(hipMemsetAsync(cm->ptotal, 0, 8, s));
+    GNS_HIP(hipMemsetAsync(cm->dctl + 1, 0, 4, s));  // abort flag of this batch
     GNS_HIP(hipMemsetAsync(cm->hflag2, 0, ((size_t)g.d * kHot + 2) * 4, s));
     if (++cm->epoch == 0) cm->epoch = 1;
     {
@@ -2686,7 +2757,9 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         if (round > 0) {
             GNS_HIP(hipMemcpyAsync(cm->h_pin, cm->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
             GNS_HIP(hipMemcpyAsync(cm->h_pin + 2, cm->stats + 3, 8, hipMemcpyDeviceToHost, s));
+            GNS_HIP(hipMemcpyAsync(cm->h_pin + 4, cm->dctl, 4, hipMemcpyDeviceToHost, s));
             GNS_HIP(hipStreamSynchronize(s));
+            cm->claimed = cm->h_pin[4];
             if (cm->h_pin[2] | cm->h_pin[3]) {
                 set_error("flow dictionary full (%llu slots); raise max_flows",
                           (unsigned long long)cm->dict_slots);
@@ -2808,6 +2881,67 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
     return GNS_OK;
 }
 
+InputDesc advance(const InputDesc &in, uint64_t off) {
+    InputDesc d = in;
+    if (d.hdr) d.hdr += off * 16;
+    if (d.src16) d.src16 += off * 16;
+    if (d.dst16) d.dst16 += off * 16;
+    if (d.sport) d.sport += off;
+    if (d.dport) d.dport += off;
+    if (d.proto) d.proto += off;
+    if (d.keys) d.keys += off * d.stride;
+    if (d.sizes) d.sizes += off;
+    return d;
+}
+
+template <int KIND>
+int cm_batch(gns_cm *cm, const InputDesc &d, uint64_t m) {
+    if constexpr (KIND == IN_KEYS) {
+        return cm_run_batch<KIND, PLAN_SLICE0>(cm, d, m);
+    } else {
+        switch (plan_mode(cm->kp)) {
+        case PLAN_SLICE0: return cm_run_batch<KIND, PLAN_SLICE0>(cm, d, m);
+        case PLAN_SLICE4: return cm_run_batch<KIND, PLAN_SLICE4>(cm, d, m);
+        default: return cm_run_batch<KIND, PLAN_GENERIC>(cm, d, m);
+        }
+    }
+}
+
+// One device batch (device-resident inputs) with dictionary recovery: a batch
+// whose new flows overflow the dictionary is aborted before it changes the
+// sketch, its counters are undone, the dead flows reclaimed and
+// the batch re-run in halves.  Only when even a 16K-packet batch does not fit
+// next to the live flows is the dictionary full (sticky until reset).
+template <int KIND>
+int cm_batch_recover(gns_cm *cm, const InputDesc &d, uint64_t m) {
+    if (m == 0) return GNS_OK;
+    if (cm->full) {
+        set_error("flow dictionary full (%llu slots, %llu live flows); raise max_flows",
+                  (unsigned long long)cm->dict_slots, (unsigned long long)cm->last_live);
+        return GNS_E_FULL;
+    }
+    if (cm->claimed >= cm->max_flows) GNS_TRY(cm_reclaim(cm));  // proactive: keep the load <= ~1/2
+    GNS_HIP(hipMemcpyAsync(cm->stats_bak, cm->stats, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, cm->stream));
+    const int rc = cm_batch<KIND>(cm, d, m);
+    if (rc != GNS_E_FULL) return rc;
+    // not applied: undo its counters, drop its claims and the dead flows
+    GNS_HIP(hipMemcpyAsync(cm->stats, cm->stats_bak, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, cm->stream));
+    GNS_HIP(hipMemsetAsync(cm->stats + 3, 0, sizeof(unsigned long long), cm->stream));
+    GNS_TRY(cm_reclaim(cm));
+    cm->n_retry++;
+    if (m <= kChunk) {
+        cm->full = true;
+        const unsigned long long one = 1;
+        GNS_HIP(hipMemcpy(cm->stats + 3, &one, sizeof(one), hipMemcpyHostToDevice));
+        set_error("flow dictionary full: %llu live flows plus one %u-packet batch exceed %llu slots; raise max_flows",
+                  (unsigned long long)cm->last_live, kChunk, (unsigned long long)cm->dict_slots);
+        return GNS_E_FULL;
+    }
+    const uint64_t h = ((m / 2 + kChunk - 1) / kChunk) * kChunk;
+    GNS_TRY(cm_batch_recover<KIND>(cm, d, h));
+    return cm_batch_recover<KIND>(cm, advance(d, h), m - h);
+}
+
 template <int KIND>
 int cm_insert(gns_cm *cm, InputDesc in, uint64_t n, gns_mem where) {
     GNS_TRY(set_dev(cm));
@@ -2817,14 +2951,7 @@ int cm_insert(gns_cm *cm, InputDesc in, uint64_t n, gns_mem where) {
         if (!cm->warm) m = std::min<uint64_t>(m, std::max<uint64_t>(kChunk * 64, cm->bmax / 32));
         InputDesc d = in;
         if (where == GNS_MEM_DEVICE) {
-            if (d.hdr) d.hdr += off * 16;
-            if (d.src16) d.src16 += off * 16;
-            if (d.dst16) d.dst16 += off * 16;
-            if (d.sport) d.sport += off;
-            if (d.dport) d.dport += off;
-            if (d.proto) d.proto += off;
-            if (d.keys) d.keys += off * d.stride;
-            if (d.sizes) d.sizes += off;
+            d = advance(in, off);
         } else {
             // stage host arrays into one device buffer (16-byte aligned pieces)
             const void *src[7] = {in.hdr ? (const void *)(in.hdr + off * 16) : nullptr,
@@ -2855,15 +2982,7 @@ int cm_insert(gns_cm *cm, InputDesc in, uint64_t n, gns_mem where) {
             d.sizes = reinterpret_cast<const uint32_t *>(p);
             if (d.keys) d.aligned = (d.stride % 4 == 0 && d.stride >= ((cm->K + 3) & ~3u)) ? 1u : 0u;
         }
-        if constexpr (KIND == IN_KEYS) {
-            GNS_TRY((cm_run_batch<KIND, PLAN_SLICE0>(cm, d, m)));
-        } else {
-            switch (plan_mode(cm->kp)) {
-            case PLAN_SLICE0: GNS_TRY((cm_run_batch<KIND, PLAN_SLICE0>(cm, d, m))); break;
-            case PLAN_SLICE4: GNS_TRY((cm_run_batch<KIND, PLAN_SLICE4>(cm, d, m))); break;
-            default: GNS_TRY((cm_run_batch<KIND, PLAN_GENERIC>(cm, d, m))); break;
-            }
-        }
+        GNS_TRY(cm_batch_recover<KIND>(cm, d, m));
     }
     return GNS_OK;
 }
@@ -2950,12 +3069,16 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         while (slots < 2 * mf) slots <<= 1;
         if (slots > (1ull << 30)) { set_error("max_flows too large"); rc = GNS_E_ARG; break; }
         cm->dict_slots = slots;
+        cm->max_flows = mf;
         cm->D.mask = (uint32_t)(slots - 1);
         cm->D.K = cm->K;
         cm->D.RW = dict_record_words_cm(cm->K);
         cm->D.bw = cm->D.RW == 16 && 1 + (cm->K + 3) / 4 <= 12 ? 1u : 0u;
         cm->D.seed = 0x2545F491u;
         if ((rc = dalloc_t(&cm->D.rec, slots * cm->D.RW)) != GNS_OK) break;
+        if ((rc = dalloc_t(&cm->dctl, 4)) != GNS_OK || (rc = dalloc_t(&cm->stats_bak, 3)) != GNS_OK) break;
+        cm->D.ctl = cm->dctl;
+        cm->D.cap = (uint32_t)(slots - slots / 4);  // claims beyond 3/4 load abort the batch (reclaim + retry)
         // batch buffers
         cm->bmax = p->batch_packets ? p->batch_packets : (16ull << 20);
         cm->bmax = ((cm->bmax + kChunk - 1) / kChunk) * kChunk;
@@ -3267,16 +3390,6 @@ int gns_cm_heavy_hitters(gns_cm *cm, uint8_t *count_flows, uint32_t *counts, uin
 // while workers insert, manager.go:139-159 -- here the read side sees a
 // consistent state taken at a point of the insert stream instead).
 // ---------------------------------------------------------------------------
-struct gns_cm_view {
-    gns_cm *cm = nullptr;
-    hipStream_t stream = nullptr;
-    hipEvent_t ready = nullptr;
-    uint32_t *C = nullptr, *S = nullptr, *Fc = nullptr, *Fs = nullptr;
-    CmScratch rd;
-    std::mutex mu;          // refresh vs queries: a refresh waits for the query in progress
-    uint32_t period = ~0u;  // handle period of the snapshot (~0: never refreshed)
-};
-
 static void view_free(gns_cm_view *v) {
     dfree(v->C); dfree(v->S); dfree(v->Fc); dfree(v->Fs);
     v->rd.free_all();
@@ -3378,18 +3491,6 @@ int gns_cm_view_query(gns_cm_view *v, const uint8_t *keys, uint32_t stride, uint
     return cm_query_impl(cm, v->stream, v->rd, v->C, v->Fc, v->S, v->Fs, keys, stride, n, out);
 }
 
-// Holds every registered view's mutex: no view call is running (each one
-// synchronizes its stream before it returns), so the handle may rewrite what
-// the views read (the flow dictionary) and bump the period they check.
-struct ViewsQuiesced {
-    std::unique_lock<std::mutex> reg;
-    std::vector<std::unique_lock<std::mutex>> locks;
-    explicit ViewsQuiesced(gns_cm *cm) : reg(cm->views_mu) {
-        locks.reserve(cm->views.size());
-        for (gns_cm_view *v : cm->views) locks.emplace_back(v->mu);
-    }
-};
-
 int gns_cm_reset(gns_cm *cm) {
     if (!cm) return GNS_E_ARG;
     GNS_TRY(set_dev(cm));
@@ -3442,6 +3543,13 @@ int gns_cm_counters(gns_cm *cm, uint64_t out[8]) {
 #else
     for (int i = 0; i < 8; i++) out[i] = h[i];
 #endif
+    return GNS_OK;
+}
+
+int gns_cm_dict_stats(gns_cm *cm, uint64_t out[6]) {
+    if (!cm || !out) return GNS_E_ARG;
+    out[0] = cm->n_reclaim; out[1] = cm->n_dropped; out[2] = cm->last_live; out[3] = cm->claimed;
+    out[4] = (uint64_t)(cm->reclaim_ms * 1000.0); out[5] = cm->n_retry;
     return GNS_OK;
 }
 

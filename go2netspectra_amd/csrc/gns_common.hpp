@@ -95,6 +95,25 @@ inline uint32_t dict_record_words_cm(uint32_t K) {
     return (K > 12 && w <= 12) ? 16u : dict_record_words(K);
 }
 
+// Flow-dictionary rebuild (gns_dict.hip): keep the records whose id some
+// array in `mark` names (or whose keep_nz entry is nonzero), reinsert them into
+// the cleared table -- or a new one of new_slots slots -- and rewrite the ids of
+// every array in `remap_arrays`.  D.rec / D.mask / slots are updated; the
+// scratch's remap (old slot -> new slot, ~0 = dropped) stays valid until the
+// next rebuild.  D.ctl[0] restarts at the live count.  Synchronizes stream s.
+struct DictIds {
+    uint32_t *ids;
+    uint64_t n;
+};
+struct DictScratch {
+    uint32_t *remap = nullptr, *stage = nullptr, *stage_slot = nullptr, *cnt = nullptr, *h_cnt = nullptr;
+    uint64_t remap_n = 0, stage_n = 0;
+    void free_all();
+};
+int dict_rebuild(DictDev &D, uint64_t &slots, const DictIds *mark, int nmark, const unsigned long long *keep_nz,
+                 DictIds *remap_arrays, int nremap, uint64_t new_slots, hipStream_t s, DictScratch &sc,
+                 uint64_t *live_out, uint32_t **old_rec_out);
+
 inline uint32_t ceil_log2(uint64_t x) {
     uint32_t b = 0;
     while ((1ull << b) < x) b++;

@@ -25,6 +25,7 @@
 // the tail flows (about a third of the packets) to global atomics, three per
 // packet; after the sort a flow is one contiguous run.
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <vector>
 
@@ -129,7 +130,7 @@ __device__ __forceinline__ void ex_probe_issue(const DictDev &D, uint32_t slot, 
 __device__ __forceinline__ void ex_consume(const ExArgs &a, uint64_t p, uint64_t beg, bool ok,
                                            const uint32_t (&kw)[GNS_KWMAX], uint32_t K, uint32_t slot0,
                                            const uint4 (&r4)[4], uint32_t sz, uint32_t *s_pend,
-                                           uint32_t *s_full, uint32_t &n_ok) {
+                                           uint32_t *s_full, uint32_t *s_claim, uint32_t &n_ok) {
     if (!ok) return;
     uint32_t rec[16];
 #pragma unroll
@@ -148,6 +149,10 @@ __device__ __forceinline__ void ex_consume(const ExArgs &a, uint64_t p, uint64_t
         else if (tag != 0) { r = DICT_PENDING; out = (slot0 + 1u) & a.D.mask; }  // displaced
         else r = dict_find_or_claim(a.D, kw, slot0, a.epoch, &out);              // empty: claim
     }
+    if (r == DICT_CLAIMED) {
+        atomicAdd(s_claim, 1u);
+        r = DICT_FOUND;
+    }
     if (r == DICT_FULL) {
         a.sk[p] = sort_word(a.none_key, p, sz, a.sb, a.ib);
         atomicAdd(s_full, 1u);
@@ -162,11 +167,15 @@ __device__ __forceinline__ void ex_consume(const ExArgs &a, uint64_t p, uint64_t
 template <int KIND, int MODE>
 __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
     __shared__ uint8_t s_src[80];
-    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
+    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_claim, s_abort;
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
-    stage_plan<MODE>(a.kp, s_src);
-    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; }
+    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; s_claim = 0; s_abort = dict_aborted(a.D); }
     __syncthreads();
+    if (s_abort) {  // the batch overflowed the dictionary: re-run after the table grows
+        if (tid == 0) a.pend_cnt[blk] = 0;
+        return;
+    }
+    stage_plan<MODE>(a.kp, s_src);
     const uint32_t K = a.kp.K;
     const uint64_t beg = (uint64_t)blk * kXChunk;
     const uint64_t end = min(a.n, beg + kXChunk);
@@ -217,7 +226,7 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
             uint32_t kwn[GNS_KWMAX], slotn = 0, szn = 0;
             uint4 r4n[4];
             if (p0 + kXThreads < end) stage_b(p0 + kXThreads + tid, okn, kwn, slotn, r4n, szn);
-            ex_consume(a, p0 + tid, beg, okc, kwc, K, slotc, r4c, szc, &s_pend, &s_full, n_ok);
+            ex_consume(a, p0 + tid, beg, okc, kwc, K, slotc, r4c, szc, &s_pend, &s_full, &s_claim, n_ok);
             okc = okn; slotc = slotn; szc = szn;
 #pragma unroll
             for (int i = 0; i < GNS_KWMAX; i++) kwc[i] = kwn[i];
@@ -237,7 +246,7 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
             const uint32_t slot0 = mm3_n<GNS_KWMAX>(kw, K, a.D.seed) & a.D.mask;
             uint4 r4[4];
             ex_probe_issue(a.D, slot0, r4);
-            ex_consume(a, p, beg, true, kw, K, slot0, r4, sz, &s_pend, &s_full, n_ok);
+            ex_consume(a, p, beg, true, kw, K, slot0, r4, sz, &s_pend, &s_full, &s_claim, n_ok);
         }
     }
     atomicAdd(&s_ok, n_ok);
@@ -249,6 +258,7 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
         if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
         if (s_unsup) atomicAdd(&a.stats[2], (unsigned long long)s_unsup);
         if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+        dict_flush_claims(a.D, s_claim, &a.stats[3]);
     }
 }
 
@@ -263,7 +273,7 @@ struct ExResolveArgs {
 template <int KIND, int MODE>
 __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
     __shared__ uint8_t s_src[80];
-    __shared__ uint32_t s_cnt, s_full;
+    __shared__ uint32_t s_cnt, s_full, s_claim, s_abort;
     const ExArgs &a = r.x;
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
     const uint32_t cnt = r.cnt_in[blk];
@@ -271,9 +281,13 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
         if (tid == 0) r.cnt_out[blk] = 0;
         return;
     }
-    stage_plan<MODE>(a.kp, s_src);
-    if (tid == 0) { s_cnt = 0; s_full = 0; }
+    if (tid == 0) { s_cnt = 0; s_full = 0; s_claim = 0; s_abort = dict_aborted(a.D); }
     __syncthreads();
+    if (s_abort) {
+        if (tid == 0) r.cnt_out[blk] = 0;
+        return;
+    }
+    stage_plan<MODE>(a.kp, s_src);
     const uint64_t beg = (uint64_t)blk * kXChunk;
     for (uint32_t i = tid; i < cnt; i += kXThreads) {
         const uint64_t v = r.pend_in[beg + i];
@@ -282,7 +296,8 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
         (void)ex_key<KIND, MODE>(a.x, a.kp.K, s_src, p, kw);
         uint32_t out;
         const int res = dict_find_or_claim(a.D, kw, (uint32_t)v, a.epoch, &out);
-        if (res == DICT_FOUND) {  // X1 wrote the word with none_key: fill in the flow field
+        if (res == DICT_CLAIMED) atomicAdd(&s_claim, 1u);
+        if (res == DICT_FOUND || res == DICT_CLAIMED) {  // X1 wrote the word with none_key: fill in the flow field
             const uint32_t sh = a.ib + a.sb;
             a.sk[p] = (a.sk[p] & ((1ull << sh) - 1ull)) | (uint64_t)out << sh;
         }
@@ -294,6 +309,7 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
         r.cnt_out[blk] = s_cnt;
         if (s_cnt) atomicAdd(r.total_out, s_cnt);
         if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+        dict_flush_claims(a.D, s_claim, &a.stats[3]);
     }
 }
 
@@ -416,9 +432,10 @@ __global__ __launch_bounds__(256) void k_ex_query(const uint8_t *flows, uint32_t
 }
 
 // occupied dictionary slots -> ids (snapshot)
-__global__ __launch_bounds__(256) void k_ex_list(DictDev D, uint64_t slots, uint32_t *ids, uint32_t *count) {
+__global__ __launch_bounds__(256) void k_ex_list(DictDev D, uint64_t slots, const unsigned long long *pkts,
+                                                 uint32_t *ids, uint32_t *count) {
     const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool occ = s < slots && D.rec[s * D.RW] != 0u;
+    const bool occ = s < slots && D.rec[s * D.RW] != 0u && pkts[s] != 0ull;
     const uint64_t m = __ballot(occ);
     if (m == 0) return;
     const uint32_t lane = __lane_id();
@@ -441,6 +458,16 @@ __global__ __launch_bounds__(256) void k_ex_gather(const uint32_t *ids, uint64_t
     start[p] = f.start[id]; end[p] = f.end[id]; pkts[p] = f.pkts[id]; bytes[p] = f.bytes[id];
 }
 
+// table growth: per-flow state follows its record to the new slot (gns_dict.hip remap)
+__global__ __launch_bounds__(256) void k_ex_permute(FlowState o, uint64_t slots, const uint32_t *remap, FlowState f) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= slots) return;
+    const uint32_t t = remap[s];
+    if (t == GNS_ID_NONE) return;
+    f.pkts[t] = o.pkts[s]; f.bytes[t] = o.bytes[s]; f.first[t] = o.first[s]; f.last[t] = o.last[s];
+    f.start[t] = o.start[s]; f.end[t] = o.end[s];
+}
+
 __global__ __launch_bounds__(256) void k_ex_init(FlowState f, uint64_t slots) {
     const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (s >= slots) return;
@@ -458,6 +485,12 @@ struct gns_ex {
     uint32_t K = 0;
     DictDev D{};
     uint64_t slots = 0;
+    uint64_t claimed = 0;                    // D.ctl[0] as of the last batch
+    uint32_t *dctl = nullptr;
+    DictScratch dsc;
+    unsigned long long *stats_bak = nullptr;
+    uint64_t n_grow = 0, n_retry = 0;
+    double grow_ms = 0.0;
     FlowState f{};
     uint32_t epoch = 0;
     uint64_t pkt = 0, batches = 0;
@@ -490,6 +523,7 @@ void ex_free_all(gns_ex *ex) {
     dfree(ex->f.start); dfree(ex->f.end); dfree(ex->pend[0]); dfree(ex->pend[1]);
     dfree(ex->pcnt[0]); dfree(ex->pcnt[1]); dfree(ex->ptotal); dfree(ex->stats); dfree(ex->stage);
     dfree(ex->sk[0]); dfree(ex->sk[1]); dfree(ex->sort_tmp);
+    dfree(ex->dctl); dfree(ex->stats_bak); ex->dsc.free_all();
     if (ex->h_pin) (void)hipHostFree(ex->h_pin);
     ex->timer.destroy();
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
@@ -497,6 +531,8 @@ void ex_free_all(gns_ex *ex) {
 
 int ex_clear(gns_ex *ex) {
     GNS_HIP(hipMemsetAsync(ex->D.rec, 0, ex->slots * ex->D.RW * 4, ex->stream));
+    GNS_HIP(hipMemsetAsync(ex->dctl, 0, 16, ex->stream));
+    ex->claimed = 0;
     GNS_HIP(hipMemsetAsync(ex->stats + 3, 0, sizeof(unsigned long long), ex->stream));  // dict-full word
     hipLaunchKernelGGL(k_ex_init, dim3((unsigned)((ex->slots + 255) / 256)), dim3(256), 0, ex->stream, ex->f,
                        ex->slots);
@@ -511,6 +547,7 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     const uint32_t nblk = (uint32_t)((n + kXChunk - 1) / kXChunk);
     ScopedStage total_stage(ex->timer, 5);
     GNS_HIP(hipMemsetAsync(ex->ptotal, 0, 8, s));
+    GNS_HIP(hipMemsetAsync(ex->dctl + 1, 0, 4, s));  // abort flag of this batch
     if (++ex->epoch == 0) ex->epoch = 1;
     ExArgs x{};
     x.x = xin; x.n = n; x.kp = ex->kp; x.D = ex->D; x.epoch = ex->epoch;
@@ -528,7 +565,9 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
         if (round > 0) {
             GNS_HIP(hipMemcpyAsync(ex->h_pin, ex->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
             GNS_HIP(hipMemcpyAsync(ex->h_pin + 2, ex->stats + 3, 8, hipMemcpyDeviceToHost, s));
+            GNS_HIP(hipMemcpyAsync(ex->h_pin + 4, ex->dctl, 4, hipMemcpyDeviceToHost, s));
             GNS_HIP(hipStreamSynchronize(s));
+            ex->claimed = ex->h_pin[4];
             if (ex->h_pin[2] | ex->h_pin[3]) { set_error("flow dictionary full; raise max_flows"); return GNS_E_FULL; }
             if (ex->h_pin[0] == 0) break;
         }
@@ -563,12 +602,123 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     return GNS_OK;
 }
 
+// Sort-word fields for the current table: flow ids < slots (invalid packets =
+// slots), packet index, wire length (>= 12 bits; a longer length is read back by X3).
+int ex_geometry(gns_ex *ex) {
+    uint32_t kb = 1;
+    while ((1ull << kb) <= ex->slots) kb++;
+    ex->key_bits = kb;
+    if (64 - kb - ceil_log2(ex->bmax) < 12) ex->bmax = 1ull << (52 - kb);
+    ex->nblk_max = (uint32_t)(ex->bmax / kXChunk);
+    ex->ib = std::max<uint32_t>(1, ceil_log2(ex->bmax));
+    ex->sb = std::min<uint32_t>(31, 64 - kb - ex->ib);
+    size_t t1 = 0;
+    const uint32_t lo = ex->sb + ex->ib;
+    if (rocprim::radix_sort_keys<ExSortConfig>(nullptr, t1, ex->sk[0], ex->sk[1], (size_t)ex->bmax, lo, lo + ex->key_bits,
+                                               ex->stream) != hipSuccess) {
+        set_error("rocPRIM scratch query failed");
+        return GNS_E_HIP;
+    }
+    if (t1 > ex->sort_tmp_bytes) {
+        dfree(ex->sort_tmp);
+        ex->sort_tmp = nullptr;
+        ex->sort_tmp_bytes = 0;
+        GNS_TRY(dalloc(&ex->sort_tmp, t1));
+        ex->sort_tmp_bytes = t1;
+    }
+    return GNS_OK;
+}
+
+// The exact aggregator keeps every flow of the period (exact/task.go:135-148
+// grows a Go map): when the dictionary fills, the table doubles.  Flows with
+// packets are reinserted (gns_dict.hip) and their state follows them; the
+// claims of an aborted batch (flows without packets yet) are dropped.
+int ex_grow(gns_ex *ex) {
+    const uint64_t old_slots = ex->slots, new_slots = old_slots * 2;
+    if (new_slots > (1ull << 30)) {
+        set_error("exact flow dictionary cannot grow beyond 2^30 slots (%llu flows)", (unsigned long long)ex->claimed);
+        return GNS_E_FULL;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    FlowState nf{};
+    int rc = GNS_OK;
+    if ((rc = dalloc_t(&nf.pkts, new_slots)) || (rc = dalloc_t(&nf.bytes, new_slots)) ||
+        (rc = dalloc_t(&nf.first, new_slots)) || (rc = dalloc_t(&nf.last, new_slots)) ||
+        (rc = dalloc_t(&nf.start, new_slots)) || (rc = dalloc_t(&nf.end, new_slots))) {
+        dfree(nf.pkts); dfree(nf.bytes); dfree(nf.first); dfree(nf.last); dfree(nf.start); dfree(nf.end);
+        return rc;
+    }
+    uint64_t slots = ex->slots, live = 0;
+    rc = dict_rebuild(ex->D, slots, nullptr, 0, ex->f.pkts, nullptr, 0, new_slots, ex->stream, ex->dsc, &live, nullptr);
+    if (rc != GNS_OK) {
+        dfree(nf.pkts); dfree(nf.bytes); dfree(nf.first); dfree(nf.last); dfree(nf.start); dfree(nf.end);
+        return rc;
+    }
+    hipLaunchKernelGGL(k_ex_init, dim3((unsigned)((new_slots + 255) / 256)), dim3(256), 0, ex->stream, nf, new_slots);
+    hipLaunchKernelGGL(k_ex_permute, dim3((unsigned)((old_slots + 255) / 256)), dim3(256), 0, ex->stream, ex->f,
+                       old_slots, ex->dsc.remap, nf);
+    GNS_HIP(hipGetLastError());
+    GNS_HIP(hipStreamSynchronize(ex->stream));
+    dfree(ex->f.pkts); dfree(ex->f.bytes); dfree(ex->f.first); dfree(ex->f.last); dfree(ex->f.start); dfree(ex->f.end);
+    ex->f = nf;
+    ex->slots = new_slots;
+    ex->D.cap = (uint32_t)(new_slots - new_slots / 4);
+    ex->claimed = live;
+    GNS_TRY(ex_geometry(ex));
+    ex->n_grow++;
+    ex->grow_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return GNS_OK;
+}
+
 template <int KIND>
 int ex_dispatch(gns_ex *ex, const ExIn &x, uint64_t n) {
     switch (plan_mode(ex->kp)) {
     case PLAN_SLICE0: return ex_run_batch<KIND, PLAN_SLICE0>(ex, x, n);
     case PLAN_SLICE4: return ex_run_batch<KIND, PLAN_SLICE4>(ex, x, n);
     default: return ex_run_batch<KIND, PLAN_GENERIC>(ex, x, n);
+    }
+}
+
+// One device batch with table growth: a batch that overflows the dictionary is
+// aborted before X3 touches the flow state, its counters are undone, the table
+// doubles and the batch runs again.
+ExIn ex_advance(const ExIn &x0, uint64_t off) {
+    ExIn x = x0;
+    InputDesc &d = x.in;
+    if (d.hdr) d.hdr += off * 16;
+    if (d.src16) d.src16 += off * 16;
+    if (d.dst16) d.dst16 += off * 16;
+    if (d.sport) d.sport += off;
+    if (d.dport) d.dport += off;
+    if (d.proto) d.proto += off;
+    if (d.sizes) d.sizes += off;
+    if (x.ipver) x.ipver += off;
+    x.ts += off;
+    return x;
+}
+
+template <int KIND>
+int ex_batch_recover(gns_ex *ex, const ExIn &x, uint64_t m) {
+    if (ex->claimed >= ex->slots / 2) GNS_TRY(ex_grow(ex));  // keep the load <= ~1/2
+    if (m > ex->bmax) {  // a grown table leaves fewer sort-word bits for the packet index
+        for (uint64_t off = 0; off < m; off += ex->bmax)
+            GNS_TRY(ex_batch_recover<KIND>(ex, ex_advance(x, off), std::min<uint64_t>(ex->bmax, m - off)));
+        return GNS_OK;
+    }
+    for (;;) {
+        GNS_HIP(hipMemcpyAsync(ex->stats_bak, ex->stats, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, ex->stream));
+        const int rc = ex_dispatch<KIND>(ex, x, m);
+        if (rc != GNS_E_FULL) return rc;
+        GNS_HIP(hipMemcpyAsync(ex->stats, ex->stats_bak, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, ex->stream));
+        GNS_HIP(hipMemsetAsync(ex->stats + 3, 0, sizeof(unsigned long long), ex->stream));
+        ex->n_retry++;
+        const int g = ex_grow(ex);
+        if (g != GNS_OK) {
+            const unsigned long long one = 1;
+            (void)hipMemcpy(ex->stats + 3, &one, sizeof(one), hipMemcpyHostToDevice);
+            return g;
+        }
+        if (m > ex->bmax) return ex_batch_recover<KIND>(ex, x, m);
     }
 }
 
@@ -581,15 +731,7 @@ int ex_insert(gns_ex *ex, const ExIn &x0, uint64_t n, gns_mem where) {
         InputDesc &d = x.in;
         const InputDesc &in = x0.in;
         if (where == GNS_MEM_DEVICE) {
-            if (d.hdr) d.hdr += off * 16;
-            if (d.src16) d.src16 += off * 16;
-            if (d.dst16) d.dst16 += off * 16;
-            if (d.sport) d.sport += off;
-            if (d.dport) d.dport += off;
-            if (d.proto) d.proto += off;
-            if (d.sizes) d.sizes += off;
-            if (x.ipver) x.ipver += off;
-            x.ts += off;
+            x = ex_advance(x0, off);
         } else {
             const void *src[9] = {in.hdr ? (const void *)(in.hdr + off * 16) : nullptr,
                                   in.src16 ? (const void *)(in.src16 + off * 16) : nullptr,
@@ -623,7 +765,7 @@ int ex_insert(gns_ex *ex, const ExIn &x0, uint64_t n, gns_mem where) {
                 p += (bytes[i] + 15) & ~size_t(15);
             }
         }
-        GNS_TRY(ex_dispatch<KIND>(ex, x, m));
+        GNS_TRY(ex_batch_recover<KIND>(ex, x, m));
     }
     return GNS_OK;
 }
@@ -671,14 +813,10 @@ int gns_ex_create(const gns_ex_params *p, gns_ex **out) {
         ex->D.seed = 0x5BD1E995u;
         ex->bmax = p->batch_packets ? p->batch_packets : (16ull << 20);
         ex->bmax = std::min<uint64_t>(((ex->bmax + kXChunk - 1) / kXChunk) * kXChunk, 1ull << 31);
-        {   // sort word fields: flow ids < slots (invalid packets = slots), packet index, wire length
+        {   // sort word fields (ex_geometry, before the batch buffers are sized)
             uint32_t kb = 1;
             while ((1ull << kb) <= slots) kb++;
-            ex->key_bits = kb;
-            // keep >= 12 bits of wire length in the word (a longer one is read back by X3)
             if (64 - kb - ceil_log2(ex->bmax) < 12) ex->bmax = 1ull << (52 - kb);
-            ex->ib = std::max<uint32_t>(1, ceil_log2(ex->bmax));
-            ex->sb = std::min<uint32_t>(31, 64 - kb - ex->ib);
         }
         ex->nblk_max = (uint32_t)(ex->bmax / kXChunk);
         if ((rc = dalloc_t(&ex->D.rec, slots * ex->D.RW)) || (rc = dalloc_t(&ex->f.pkts, slots)) ||
@@ -690,16 +828,10 @@ int gns_ex_create(const gns_ex_params *p, gns_ex **out) {
             (rc = dalloc_t(&ex->ptotal, 2)) || (rc = dalloc_t(&ex->stats, 8)) ||
             (rc = dalloc_t(&ex->sk[0], ex->bmax)) || (rc = dalloc_t(&ex->sk[1], ex->bmax)))
             break;
-        {
-            size_t t1 = 0;
-            const uint32_t lo = ex->sb + ex->ib;
-            if (rocprim::radix_sort_keys<ExSortConfig>(nullptr, t1, ex->sk[0], ex->sk[1], (size_t)ex->bmax, lo,
-                                         lo + ex->key_bits, ex->stream) != hipSuccess) {
-                set_error("rocPRIM scratch query failed"); rc = GNS_E_HIP; break;
-            }
-            ex->sort_tmp_bytes = t1;
-            if ((rc = dalloc(&ex->sort_tmp, ex->sort_tmp_bytes)) != GNS_OK) break;
-        }
+        if ((rc = ex_geometry(ex)) != GNS_OK) break;
+        if ((rc = dalloc_t(&ex->dctl, 4)) != GNS_OK || (rc = dalloc_t(&ex->stats_bak, 3)) != GNS_OK) break;
+        ex->D.ctl = ex->dctl;
+        ex->D.cap = (uint32_t)(slots - slots / 4);
         if (hipHostMalloc(reinterpret_cast<void **>(&ex->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
         }
@@ -793,7 +925,7 @@ int gns_ex_snapshot(gns_ex *ex, uint8_t *keys, int64_t *start_ns, int64_t *end_n
     hipError_t e = hipMemsetAsync(cnt, 0, 4, s);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_ex_list, dim3((unsigned)((ex->slots + 255) / 256)), dim3(256), 0, s, ex->D, ex->slots,
-                           ids, cnt);
+                           ex->f.pkts, ids, cnt);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpyAsync(&nf, cnt, 4, hipMemcpyDeviceToHost, s);
@@ -851,6 +983,13 @@ int gns_ex_counters(gns_ex *ex, uint64_t out[8]) {
     GNS_TRY(gns_ex_snapshot(ex, nullptr, nullptr, nullptr, nullptr, nullptr, &nf));
     out[0] = h[0]; out[1] = h[1]; out[2] = h[2]; out[3] = h[3];
     out[4] = nf; out[5] = ex->pkt; out[6] = ex->batches; out[7] = 0;
+    return GNS_OK;
+}
+
+int gns_ex_dict_stats(gns_ex *ex, uint64_t out[6]) {
+    if (!ex || !out) return GNS_E_ARG;
+    out[0] = ex->n_grow; out[1] = 0; out[2] = ex->slots; out[3] = ex->claimed;
+    out[4] = (uint64_t)(ex->grow_ms * 1000.0); out[5] = ex->n_retry;
     return GNS_OK;
 }
 

@@ -183,9 +183,29 @@ struct DictDev {
     uint32_t seed;     // slot hash seed
     uint32_t K;        // key bytes
     uint32_t bw;       // Count-Min: words 12..15 cache the flow's row 0..3 buckets
+    uint32_t *ctl;     // [0] slots claimed since the last rebuild / reset, [1] abort flag of the batch
+    uint32_t cap;      // claims beyond this abort the batch (the host reclaims and retries it)
 };
 
-enum { DICT_FOUND = 0, DICT_PENDING = 1, DICT_FULL = 2, DICT_ABSENT = 3 };
+enum { DICT_FOUND = 0, DICT_PENDING = 1, DICT_FULL = 2, DICT_ABSENT = 3, DICT_CLAIMED = 4 };
+
+// Claim accounting, one global atomic per block: the block's claims are added
+// to ctl[0]; crossing the cap raises the batch's abort flag and the caller's
+// dictionary-full word (the host then reclaims dead flows / grows the table and
+// re-runs the batch, which was not applied).
+__device__ __forceinline__ void dict_flush_claims(const DictDev &D, uint32_t n, unsigned long long *full_word) {
+    if (n == 0 || D.ctl == nullptr) return;
+    const uint32_t old = atomicAdd(&D.ctl[0], n);
+    if ((uint64_t)old + n > D.cap) {
+        atomicExch(&D.ctl[1], 1u);
+        atomicAdd(full_word, 1ull);
+    }
+}
+
+// the batch was aborted (read by one thread, then shared: block-uniform exits)
+__device__ __forceinline__ bool dict_aborted(const DictDev &D) {
+    return D.ctl != nullptr && __hip_atomic_load(&D.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
 #define GNS_DICT_MAX_PROBE 4096
 
 __device__ __forceinline__ void load_record(const DictDev &D, uint32_t slot, uint32_t (&r)[12]) {
@@ -198,7 +218,8 @@ __device__ __forceinline__ void load_record(const DictDev &D, uint32_t slot, uin
 }
 
 // Find the id of kw, claiming an empty slot for it if absent.
-// DICT_FOUND: *out = id.  DICT_PENDING: *out = slot to resume at next launch.
+// DICT_FOUND / DICT_CLAIMED (this lane inserted the key): *out = id.
+// DICT_PENDING: *out = slot to resume at next launch.
 __device__ __forceinline__ int dict_find_or_claim(const DictDev &D, const uint32_t (&kw)[GNS_KWMAX],
                                                   uint32_t slot, uint32_t epoch, uint32_t *out) {
     const uint32_t nkw = (D.K + 3) >> 2;
@@ -214,7 +235,7 @@ __device__ __forceinline__ int dict_find_or_claim(const DictDev &D, const uint32
                 for (int i = 0; i < GNS_KWMAX; i++)
                     if ((uint32_t)i < nkw) tp[1 + i] = kw[i];
                 *out = slot;
-                return DICT_FOUND;
+                return DICT_CLAIMED;
             }
             tag = old;
             if (tag != epoch) load_record(D, slot, r);  // committed earlier: need its key words

@@ -23,6 +23,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "gns_common.hpp"
@@ -306,11 +307,15 @@ struct SsIdsArgs {
 template <int KIND, int MF, int MM, bool FIRST>
 __global__ __launch_bounds__(kSsThreads) void k_ss_ids(SsIdsArgs r) {
     __shared__ uint8_t s_srcf[80], s_srcm[80];
-    __shared__ uint32_t s_cnt, s_full;
+    __shared__ uint32_t s_cnt, s_full, s_claim, s_abort;
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
     for (uint32_t j = tid; j < 80; j += kSsThreads) { s_srcf[j] = r.kpf.src[j]; s_srcm[j] = r.kpm.src[j]; }
-    if (tid == 0) { s_cnt = 0; s_full = 0; }
+    if (tid == 0) { s_cnt = 0; s_full = 0; s_claim = 0; s_abort = dict_aborted(r.D); }
     __syncthreads();
+    if (s_abort) {  // the batch overflowed the dictionary: it is re-run after a reclaim
+        if (tid == 0) r.cnt_out[blk] = 0;
+        return;
+    }
     const uint64_t beg = (uint64_t)blk * kSsIdChunk;
     const uint32_t cnt = FIRST ? (uint32_t)min<uint64_t>(kSsIdChunk, r.ns - beg) : r.cnt_in[blk];
     SsExtractArgs a{};
@@ -326,7 +331,8 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_ids(SsIdsArgs r) {
         if (FIRST) slot = mm3_n<GNS_KWMAX>(kwf, r.g.Kf, r.D.seed) & r.D.mask;
         uint32_t out;
         const int res = dict_find_or_claim(r.D, kwf, slot, r.epoch, &out);
-        if (res == DICT_FOUND) r.sval[q] = (uint64_t)out << 32 | (r.sval[q] & 0xFFFFFFFFull);
+        if (res == DICT_CLAIMED) atomicAdd(&s_claim, 1u);
+        if (res == DICT_FOUND || res == DICT_CLAIMED) r.sval[q] = (uint64_t)out << 32 | (r.sval[q] & 0xFFFFFFFFull);
         else if (res == DICT_PENDING) r.pend_out[beg + atomicAdd(&s_cnt, 1u)] = (q - beg) << 32 | out;
         else atomicAdd(&s_full, 1u);
     }
@@ -335,6 +341,7 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_ids(SsIdsArgs r) {
         r.cnt_out[blk] = s_cnt;
         if (s_cnt) atomicAdd(r.total_out, s_cnt);
         if (s_full) atomicAdd(&r.stats[3], (unsigned long long)s_full);
+        dict_flush_claims(r.D, s_claim, &r.stats[3]);
     }
 }
 
@@ -629,6 +636,13 @@ struct gns_ss {
     DictDev D{};
     uint64_t dict_slots = 0;
     uint64_t max_flows = 0;  // dictionary capacity (gns_ss_params.max_flows)
+    uint64_t claimed = 0;    // D.ctl[0] as of the last batch
+    bool full = false;       // live flows + one batch piece exceed the dictionary (sticky)
+    uint32_t *dctl = nullptr;
+    DictScratch dsc;
+    unsigned long long *stats_bak = nullptr;
+    uint64_t n_reclaim = 0, n_dropped = 0, last_live = 0, n_retry = 0;
+    double reclaim_ms = 0.0;
     uint32_t epoch = 0;
     uint64_t pkt = 0;     // records inserted since create (RNG packet index)
     bool s1_pipe = true;
@@ -667,6 +681,7 @@ void ss_free_all(gns_ss *ss) {
     dfree(ss->ptotal); dfree(ss->ckey); dfree(ss->ckey_s); dfree(ss->skey); dfree(ss->skey_s);
     dfree(ss->cval); dfree(ss->cval_s); dfree(ss->cmax); dfree(ss->sval); dfree(ss->sval_s);
     dfree(ss->counts); dfree(ss->heads); dfree(ss->cblk); dfree(ss->tmp); dfree(ss->stats); dfree(ss->stage);
+    dfree(ss->dctl); dfree(ss->stats_bak); ss->dsc.free_all();
     if (ss->h_pin) (void)hipHostFree(ss->h_pin);
     ss->timer.destroy();
     if (ss->stream) (void)hipStreamDestroy(ss->stream);
@@ -679,6 +694,9 @@ int ss_reset_state(gns_ss *ss, bool init) {
     GNS_HIP(hipMemsetAsync(ss->keys, 0xFF, cells * 4, ss->stream));
     GNS_HIP(hipMemsetAsync(ss->D.rec, 0, ss->dict_slots * ss->D.RW * 4, ss->stream));
     GNS_HIP(hipMemsetAsync(ss->stats + 3, 0, sizeof(unsigned long long), ss->stream));  // dict-full word
+    GNS_HIP(hipMemsetAsync(ss->dctl, 0, 16, ss->stream));
+    ss->claimed = 0;
+    ss->full = false;
     if (init) {  // pbits starts at 1.0 (:44); Reset leaves it untouched (:297-311)
         std::vector<double> ones(cells, 1.0);
         GNS_HIP(hipMemcpyAsync(ss->pbits, ones.data(), cells * 8, hipMemcpyHostToDevice, ss->stream));
@@ -736,7 +754,9 @@ int ss_encode_ids(gns_ss *ss, const InputDesc &in, uint32_t ns) {
         if (round == 0) continue;
         GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
         GNS_HIP(hipMemcpyAsync(ss->h_pin + 2, ss->stats + 3, 8, hipMemcpyDeviceToHost, s));
+        GNS_HIP(hipMemcpyAsync(ss->h_pin + 4, ss->dctl, 4, hipMemcpyDeviceToHost, s));
         GNS_HIP(hipStreamSynchronize(s));
+        ss->claimed = ss->h_pin[4];
         if (ss->h_pin[2] | ss->h_pin[3]) {
             set_error("flow dictionary full (max_flows %llu, %llu slots); raise max_flows",
                       (unsigned long long)ss->max_flows, (unsigned long long)ss->dict_slots);
@@ -756,6 +776,7 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     ScopedStage total_stage(ss->timer, 5);
     GNS_HIP(hipMemsetAsync(ss->ptotal, 0, 8, s));
     GNS_HIP(hipMemsetAsync(ss->counts, 0, 8, s));
+    GNS_HIP(hipMemsetAsync(ss->dctl + 1, 0, 4, s));  // abort flag of this batch
     if (++ss->epoch == 0) ss->epoch = 1;
     SsExtractArgs x{};
     x.in = in; x.n = n; x.kpf = ss->kpf; x.kpm = ss->kpm;
@@ -829,6 +850,82 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     return GNS_OK;
 }
 
+// Reclaim (gns_dict.hip): only flows that own a cell (keys[]) can be named by a
+// later comparison, query or heavy hitter; every other dictionary record is dropped.
+int ss_reclaim(gns_ss *ss) {
+    const uint64_t cells = (uint64_t)ss->g.d * ss->g.w;
+    DictIds ids{ss->keys, cells};
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t before = ss->claimed;
+    uint64_t live = 0;
+    GNS_TRY(dict_rebuild(ss->D, ss->dict_slots, &ids, 1, nullptr, &ids, 1, ss->dict_slots, ss->stream, ss->dsc, &live,
+                         nullptr));
+    ss->reclaim_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ss->n_reclaim++;
+    ss->n_dropped += before > live ? before - live : 0;
+    ss->claimed = live;
+    ss->last_live = live;
+    return GNS_OK;
+}
+
+InputDesc ss_advance(const InputDesc &in, uint64_t off) {
+    InputDesc d = in;
+    if (d.hdr) d.hdr += off * 16;
+    if (d.src16) d.src16 += off * 16;
+    if (d.dst16) d.dst16 += off * 16;
+    if (d.sport) d.sport += off;
+    if (d.dport) d.dport += off;
+    if (d.proto) d.proto += off;
+    if (d.keys) d.keys += off * d.stride;
+    if (d.keys2) d.keys2 += off * d.stride2;
+    if (d.sizes) d.sizes += off;
+    return d;
+}
+
+template <int KIND>
+int ss_batch(gns_ss *ss, const InputDesc &d, uint64_t m) {
+    if constexpr (KIND == IN_KEYS) {
+        return ss_run_batch<KIND, PLAN_GENERIC, PLAN_GENERIC>(ss, d, m);
+    } else if (plan_mode(ss->kpf) == PLAN_SLICE0 && plan_mode(ss->kpm) == PLAN_SLICE0) {
+        return ss_run_batch<KIND, PLAN_SLICE0, PLAN_SLICE0>(ss, d, m);
+    } else {
+        return ss_run_batch<KIND, PLAN_GENERIC, PLAN_GENERIC>(ss, d, m);
+    }
+}
+
+// A batch whose encodes overflow the dictionary is aborted in S3b, before any
+// state write: undo its counters, reclaim, re-run it in halves (the declared
+// RNG is indexed by record, so the split does not change any draw).
+template <int KIND>
+int ss_batch_recover(gns_ss *ss, const InputDesc &d, uint64_t m) {
+    if (m == 0) return GNS_OK;
+    if (ss->full) {
+        set_error("flow dictionary full (max_flows %llu, %llu slots, %llu live flows); raise max_flows",
+                  (unsigned long long)ss->max_flows, (unsigned long long)ss->dict_slots,
+                  (unsigned long long)ss->last_live);
+        return GNS_E_FULL;
+    }
+    if (ss->claimed >= ss->max_flows) GNS_TRY(ss_reclaim(ss));
+    GNS_HIP(hipMemcpyAsync(ss->stats_bak, ss->stats, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, ss->stream));
+    const int rc = ss_batch<KIND>(ss, d, m);
+    if (rc != GNS_E_FULL) return rc;
+    GNS_HIP(hipMemcpyAsync(ss->stats, ss->stats_bak, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, ss->stream));
+    GNS_HIP(hipMemsetAsync(ss->stats + 3, 0, sizeof(unsigned long long), ss->stream));
+    GNS_TRY(ss_reclaim(ss));
+    ss->n_retry++;
+    if (m <= kSsChunk) {
+        ss->full = true;
+        const unsigned long long one = 1;
+        GNS_HIP(hipMemcpy(ss->stats + 3, &one, sizeof(one), hipMemcpyHostToDevice));
+        set_error("flow dictionary full: %llu live flows plus one batch piece exceed max_flows %llu; raise max_flows",
+                  (unsigned long long)ss->last_live, (unsigned long long)ss->max_flows);
+        return GNS_E_FULL;
+    }
+    const uint64_t h = ((m / 2 + kSsChunk - 1) / kSsChunk) * kSsChunk;
+    GNS_TRY(ss_batch_recover<KIND>(ss, d, h));
+    return ss_batch_recover<KIND>(ss, ss_advance(d, h), m - h);
+}
+
 template <int KIND>
 int ss_insert(gns_ss *ss, InputDesc in, uint64_t n, gns_mem where) {
     GNS_TRY(ss_set_dev(ss));
@@ -836,15 +933,7 @@ int ss_insert(gns_ss *ss, InputDesc in, uint64_t n, gns_mem where) {
         const uint64_t m = std::min<uint64_t>(ss->bmax, n - off);
         InputDesc d = in;
         if (where == GNS_MEM_DEVICE) {
-            if (d.hdr) d.hdr += off * 16;
-            if (d.src16) d.src16 += off * 16;
-            if (d.dst16) d.dst16 += off * 16;
-            if (d.sport) d.sport += off;
-            if (d.dport) d.dport += off;
-            if (d.proto) d.proto += off;
-            if (d.keys) d.keys += off * d.stride;
-            if (d.keys2) d.keys2 += off * d.stride2;
-            if (d.sizes) d.sizes += off;
+            d = ss_advance(in, off);
         } else {
             const void *src[8] = {in.hdr ? (const void *)(in.hdr + off * 16) : nullptr,
                                   in.src16 ? (const void *)(in.src16 + off * 16) : nullptr,
@@ -882,13 +971,7 @@ int ss_insert(gns_ss *ss, InputDesc in, uint64_t n, gns_mem where) {
                 d.sizes = reinterpret_cast<const uint32_t *>(p);
             }
         }
-        if constexpr (KIND == IN_KEYS) {
-            GNS_TRY((ss_run_batch<KIND, PLAN_GENERIC, PLAN_GENERIC>(ss, d, m)));
-        } else if (plan_mode(ss->kpf) == PLAN_SLICE0 && plan_mode(ss->kpm) == PLAN_SLICE0) {
-            GNS_TRY((ss_run_batch<KIND, PLAN_SLICE0, PLAN_SLICE0>(ss, d, m)));
-        } else {
-            GNS_TRY((ss_run_batch<KIND, PLAN_GENERIC, PLAN_GENERIC>(ss, d, m)));
-        }
+        GNS_TRY(ss_batch_recover<KIND>(ss, d, m));
     }
     return GNS_OK;
 }
@@ -970,6 +1053,9 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
             ss->s1_pipe = !(env && env[0] == '0');
         }
         if ((rc = dalloc_t(&ss->D.rec, slots * ss->D.RW)) != GNS_OK) break;
+        if ((rc = dalloc_t(&ss->dctl, 4)) != GNS_OK || (rc = dalloc_t(&ss->stats_bak, 3)) != GNS_OK) break;
+        ss->D.ctl = ss->dctl;
+        ss->D.cap = (uint32_t)(slots - slots / 4);
         ss->bmax = p->batch_packets ? p->batch_packets : (8ull << 20);
         ss->bmax = std::min<uint64_t>(((ss->bmax + kSsChunk - 1) / kSsChunk) * kSsChunk, 1ull << kSsPktBits);
         ss->nblk_max = (uint32_t)(ss->bmax / kSsChunk);
@@ -1192,6 +1278,13 @@ int gns_ss_counters(gns_ss *ss, uint64_t out[8]) {
     GNS_HIP(hipMemcpy(h, ss->stats, sizeof(h), hipMemcpyDeviceToHost));
     out[0] = h[0]; out[1] = h[1]; out[2] = h[2]; out[3] = h[3]; out[4] = h[4];
     out[5] = ss->n_encodes; out[6] = ss->pkt; out[7] = ss->n_batches;
+    return GNS_OK;
+}
+
+int gns_ss_dict_stats(gns_ss *ss, uint64_t out[6]) {
+    if (!ss || !out) return GNS_E_ARG;
+    out[0] = ss->n_reclaim; out[1] = ss->n_dropped; out[2] = ss->last_live; out[3] = ss->claimed;
+    out[4] = (uint64_t)(ss->reclaim_ms * 1000.0); out[5] = ss->n_retry;
     return GNS_OK;
 }
 

@@ -144,6 +144,12 @@ class ExactAggregator:
         names = ["inserted", "dropped", "unsupported", "dict_full", "flows", "records", "batches", "_"]
         return {k: int(s[i]) for i, k in enumerate(names) if k != "_"}
 
+    def dict_stats(self) -> dict:
+        """Table growth counters (gns_ex_dict_stats): growths, -, slots, claimed, us, re-run batches."""
+        d = _lib.dict_stats(self._L.gns_ex_dict_stats, self._h)
+        return {"growths": d["reclaims"], "slots": d["live"], "claimed": d["claimed"], "grow_us": d["reclaim_us"],
+                "retried_batches": d["retried_batches"]}
+
     def set_timing(self, on: bool = True) -> None:
         check(self._L.gns_ex_set_timing(self._h, 1 if on else 0))
 

@@ -308,6 +308,10 @@ class CountMin:
                  "chunks_replay"]
         return dict(zip(names, list(c)))
 
+    def dict_stats(self) -> dict:
+        """Flow-dictionary reclaim counters (gns_cm_dict_stats)."""
+        return _lib.dict_stats(self._L.gns_cm_dict_stats, self._h)
+
     def set_timing(self, on: bool = True) -> None:
         check(self._L.gns_cm_set_timing(self._h, 1 if on else 0))
 
@@ -451,6 +455,10 @@ class SuperSpread:
         check(self._L.gns_ss_counters(self._h, s))
         names = ["inserted", "dropped", "unsupported", "dict_full", "candidates", "encodes", "records", "batches"]
         return {k: int(s[i]) for i, k in enumerate(names)}
+
+    def dict_stats(self) -> dict:
+        """Flow-dictionary reclaim counters (gns_ss_dict_stats)."""
+        return _lib.dict_stats(self._L.gns_ss_dict_stats, self._h)
 
     def set_timing(self, on: bool = True) -> None:
         check(self._L.gns_ss_set_timing(self._h, 1 if on else 0))

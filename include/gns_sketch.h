@@ -32,10 +32,18 @@
  *   - Flow keys are the reference EncodeFlow bytes (task.go:279-300): IP slots
  *     of 16 bytes with IPv4 left-aligned and zero padded, ports big-endian,
  *     protocol one byte; key_bytes <= 37 (task.go:74).
- *   - GNS_E_FULL ends the measurement period for the handle: the failing
- *     device batch is not applied (earlier device batches of the same call
- *     are) and every later insert returns GNS_E_FULL, until gns_*_reset()
- *     empties the sketch and its flow dictionary (the reference's period
+ *   - Flow dictionary (fingerprints are dense flow ids): memory
+ *     is bounded like the reference's fixed-size sketch (count_min.go:66-81),
+ *     whatever the number of distinct flows in a period.  Between device
+ *     batches the sketches reclaim the flows no bucket names any more (and,
+ *     for the exact aggregator, the table grows: exact/task.go:135-148 keeps
+ *     every flow).  A batch whose new flows overflow the dictionary is not
+ *     applied, the dictionary is rebuilt and the batch re-run (in halves for
+ *     the sketches).  Live ids are at most 2*depth*width (Count-Min) or
+ *     depth*width (SuperSpread), so with max_flows >= that + 16384 a sketch
+ *     never returns GNS_E_FULL.  GNS_E_FULL (live flows plus one 16K-packet
+ *     piece do not fit max_flows) ends the measurement period for the handle:
+ *     every later insert returns it until gns_*_reset() (the reference's period
  *     reset, manager.go:179-193).  Count-Min's GNS_E_RANGE (from flush: too
  *     many oversize packets in one device batch) is sticky the same way; the
  *     sketch is not exact after it.
@@ -97,8 +105,8 @@ typedef struct gns_cm_params {
     const uint32_t *seeds;                    /* depth row seeds (count_min.go:61-64 draws
                                                  them with rand.Uint32; here injected).
                                                  NULL -> splitmix64(0x9747B28C) stream */
-    uint64_t max_flows;                       /* distinct flows per measurement period
-                                                 (flow dictionary capacity); 0 -> 4M */
+    uint64_t max_flows;                       /* flow dictionary capacity (live + new flows of a
+                                                 batch; dead flows are reclaimed); 0 -> 4M */
     uint64_t batch_packets;                   /* device batch size; 0 -> 16M packets */
     int device;                               /* HIP device ordinal */
     uint32_t bucket_lo, bucket_hi;            /* bucket-range slice (SURVEY §8e exact global
@@ -147,6 +155,10 @@ int gns_cm_stats(gns_cm *cm, uint64_t stats[4]);
  * full, [4] size-overflow full, [5] tile updates replayed sequentially,
  * [6] tile chunks, [7] tile chunks with a replay */
 int gns_cm_counters(gns_cm *cm, uint64_t out[8]);
+/* flow dictionary: [0] reclaims, [1] dead flows dropped, [2] live flows after the
+ * last reclaim, [3] claimed slots now, [4] reclaim time (us, host clock incl. the
+ * rebuild's device work), [5] batches re-run after a dictionary overflow */
+int gns_cm_dict_stats(gns_cm *cm, uint64_t out[6]);
 int gns_cm_set_timing(gns_cm *cm, int on);
 int gns_cm_stage_times(gns_cm *cm, double ms[8], uint64_t launches[8], int reset);
 void *gns_cm_stream(gns_cm *cm); /* hipStream_t the handle launches on */
@@ -216,6 +228,7 @@ int gns_ss_stats(gns_ss *ss, uint64_t stats[4]);
 /* out[8]: inserted, dropped, unsupported, dictionary full, HLL candidates
  * (lz above the batch-entry register), HLL encodes, records, device batches */
 int gns_ss_counters(gns_ss *ss, uint64_t out[8]);
+int gns_ss_dict_stats(gns_ss *ss, uint64_t out[6]);  /* as gns_cm_dict_stats */
 int gns_ss_set_timing(gns_ss *ss, int on);
 int gns_ss_stage_times(gns_ss *ss, double ms[8], uint64_t launches[8], int reset);
 
@@ -298,7 +311,7 @@ int gns_route_partition(gns_route *r, const uint8_t *hdr, const uint32_t *wirele
 typedef struct gns_ex gns_ex;
 typedef struct gns_ex_params {
     gns_layout key;          /* key_fields (task.go:330-366) */
-    uint64_t max_flows;      /* distinct flows per measurement period (default 4M) */
+    uint64_t max_flows;      /* initial flow dictionary capacity (default 4M; the table grows) */
     uint64_t batch_packets;  /* device batch (default 16M) */
     int device;
 } gns_ex_params;
@@ -324,6 +337,9 @@ int gns_ex_snapshot(gns_ex *ex, uint8_t *keys, int64_t *start_ns, int64_t *end_n
 int gns_ex_reset(gns_ex *ex);
 /* out[8]: inserted, dropped, unsupported, dictionary full, flows, records, batches, 0 */
 int gns_ex_counters(gns_ex *ex, uint64_t out[8]);
+/* [0] table growths, [1] 0, [2] slots, [3] claimed slots, [4] growth time (us),
+ * [5] batches re-run after a dictionary overflow */
+int gns_ex_dict_stats(gns_ex *ex, uint64_t out[6]);
 int gns_ex_set_timing(gns_ex *ex, int on);
 /* stages: 0 extract, 1 resolve, 2 aggregate, 3 timestamps, 5 total */
 int gns_ex_stage_times(gns_ex *ex, double ms[8], uint64_t launches[8], int reset);

@@ -4,7 +4,7 @@ through the C ABI with the sequential C oracle fed the same stream
 import numpy as np
 import pytest
 
-from helpers import assert_same_list, frames_from_tuples, random_tuples, sizes_u32, zipf_keys
+from helpers import assert_same_list, frames_from_tuples, random_tuples, sizes_u32, zipf_index, zipf_keys
 
 pytestmark = pytest.mark.gpu
 
@@ -447,3 +447,41 @@ def test_gathered_heavy_rows_order_on_device(gpu):
         wf, wv = merge_heavy_arrays(rows[:, :K], vals)
         assert np.array_equal(got[:, :K], wf)
         assert np.array_equal(np.ascontiguousarray(got[:, K:]).view("<u4").reshape(-1), wv)
+
+
+@pytest.mark.parametrize("batch", [0, 40_000])
+def test_unbounded_distinct_flows_reclaim(gpu, oracle, batch):
+    """Memory bounded like the reference (count_min.go:66-81 is fixed-size): more
+    than 50x max_flows distinct flows in one period.  Flows no bucket names are
+    reclaimed between batches; a batch whose new flows overflow the dictionary is
+    undone, the dictionary rebuilt and the batch re-run in halves.  The state stays
+    bit-exact, no GNS_E_FULL, and a snapshot view taken mid-stream keeps answering
+    the state at its refresh across the reclaims (its ids are remapped too)."""
+    rng = np.random.default_rng(91 + batch)
+    w, d, K, max_flows = 2048, 2, 16, 16384   # live ids <= 2*d*w = 8192
+    cm, orc = make_pair(oracle, w, d, K, st=20_000, ct=30, max_flows=max_flows, batch_packets=batch)
+    view = cm.view()
+    heavy = rng.integers(0, 256, (300, K), dtype=np.uint8)
+    want_view = None
+    for part in range(6):
+        n = 200_000
+        uniq = rng.integers(0, 256, (n, K), dtype=np.uint8)
+        keys = np.where((rng.random(n) < 0.8)[:, None], uniq, heavy[zipf_index(rng, n, 300)])
+        sizes = sizes_u32(rng, n)
+        cm.insert_keys(keys, sizes)
+        orc.insert_keys(keys, sizes)
+        if part == 2:
+            view.refresh()
+            want_view = (orc.heavy("count"), orc.heavy("size"),
+                         np.array([orc.query(bytes(f)) for f in heavy], np.uint64))
+    cm.flush()
+    assert_same_state(cm, orc)
+    ds = cm.dict_stats()
+    assert ds["reclaims"] > 0 and ds["dropped"] > 50 * max_flows, ds
+    assert cm.counters()["dict_full"] == 0
+    hh = view.heavy_hitters()
+    assert_same_list([(h.Flow, h.Count) for h in hh.Count], want_view[0])
+    assert_same_list([(h.Flow, h.Size) for h in hh.Size], want_view[1])
+    assert np.array_equal(view.query_many(heavy), want_view[2])
+    assert_same_list([(h.Flow, h.Count) for h in cm.heavy_hitters().Count], orc.heavy("count"))
+    view.close()

@@ -155,19 +155,26 @@ aggregator:
     assert "Observed Value:</b> <code>20000 packets" in msg
 
 
-def test_full_dictionary_is_cleared_by_reset(gpu, oracle):
-    """GNS_E_FULL holds for the period; reset starts a clean one that matches the oracle."""
+def test_dictionary_grows_instead_of_failing(gpu, oracle):
+    """exact/task.go:135-148 keeps every flow of the period (a Go map grows): a
+    dictionary sized for 32 flows doubles as the flows arrive (the batch that
+    overflows is re-run on the grown table) and the result equals the oracle;
+    reset then starts a clean period."""
     from go2netspectra_amd import ExactTask, HeaderBatch
-    from go2netspectra_amd._lib import GNS_E_FULL, GnsError
     rng = np.random.default_rng(29)
-    task = ExactTask("tiny", FIVE, max_flows=32)
-    t = random_tuples(rng, 20_000, 3000, s=0.5)
+    task = ExactTask("tiny", FIVE, max_flows=32, batch_packets=1 << 16)
+    t = random_tuples(rng, 200_000, 60_000, s=0.5)
     hdr = frames_from_tuples(t, rng)
     ts = np.arange(len(hdr), dtype=np.int64)
-    with pytest.raises(GnsError) as e:
-        task.process_packets(HeaderBatch(hdr, t["length"], ts))
-        task.flush()
-    assert e.value.code == GNS_E_FULL
+    for part in np.array_split(np.arange(len(hdr)), 3):
+        task.process_packets(HeaderBatch(hdr[part], t["length"][part], ts[part]))
+    task.flush()
+    orc = oracle.Exact(FIVE)
+    orc.insert_hdr64(hdr, t["length"], ts)
+    assert_same_flows(gpu_flows(task), orc.export())
+    ds = task.agg.dict_stats()
+    assert ds["growths"] >= 8 and ds["slots"] >= 1 << 16, ds
+    assert task.agg.counters()["dict_full"] == 0
     task.reset()
     orc = oracle.Exact(FIVE)
     t2 = random_tuples(rng, 5000, 20)

@@ -282,3 +282,29 @@ def test_full_dictionary_is_cleared_by_reset(gpu, oracle):
         orc.insert(fl3, el3)
     ss.flush()
     assert_same_ss(ss, orc)
+
+
+@pytest.mark.parametrize("batch", [0, 50_000])
+def test_unbounded_distinct_flows_reclaim(gpu, oracle, batch):
+    """Memory bounded like the reference (super_spread.go:163-176 is fixed-size):
+    more than 50x max_flows distinct sources in one period.  Dead flows (owning
+    no cell) are reclaimed between batches, overflowing batches are re-run after
+    a reclaim, and the state stays bit-exact with no GNS_E_FULL."""
+    rng = np.random.default_rng(71 + batch)
+    max_flows = 32768   # live ids <= d*w = 2048; one 16K-packet piece of new flows must fit beside them
+    ss, orc = make_pair(oracle, 1024, 2, 32, 5, 16, 16, max_flows=max_flows, batch_packets=batch)
+    n_total = 0
+    for part in range(8):
+        n = 250_000
+        heavy, el, _ = spread_stream(rng, n, 200, 16, 16)
+        uniq = rng.integers(0, 256, (n, 16), dtype=np.uint8)  # new sources, one packet each
+        fl = np.where((rng.random(n) < 0.85)[:, None], uniq, heavy)
+        ss.insert_keys(fl, el)
+        orc.insert(fl, el)
+        n_total += n
+    ss.flush()
+    assert_same_ss(ss, orc)
+    ds = ss.dict_stats()
+    assert ds["reclaims"] > 0 and ds["dropped"] > 50 * max_flows, ds
+    assert ss.counters()["dict_full"] == 0
+    assert_same_list([(h.Flow, h.Count) for h in ss.heavy_hitters().Count], orc.heavy())
