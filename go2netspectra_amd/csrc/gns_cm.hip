@@ -2645,6 +2645,8 @@ int stage_reserve(gns_cm *cm, size_t bytes) {
 }
 
 int set_dev(gns_cm *cm) {
+    (void)hipGetLastError();  // a stale error of an earlier runtime call on this thread (e.g. the
+                              // host framework's) must not fail this call's launch checks
     GNS_HIP(hipSetDevice(cm->device));
     return GNS_OK;
 }
@@ -2909,26 +2911,40 @@ int cm_batch(gns_cm *cm, const InputDesc &d, uint64_t m) {
 
 // One device batch (device-resident inputs) with dictionary recovery: a batch
 // whose new flows overflow the dictionary is aborted before it changes the
-// sketch, its counters are undone, the dead flows reclaimed and
-// the batch re-run in halves.  Only when even a 16K-packet batch does not fit
-// next to the live flows is the dictionary full (sticky until reset).
+// sketch, its counters are undone and the dead flows reclaimed;
+// it is re-run as is once, then in halves.  Only when a 16K-packet batch does
+// not fit next to the live flows of a freshly rebuilt dictionary is the
+// dictionary full (sticky until reset).  fresh: the dictionary was rebuilt
+// right before this batch.
 template <int KIND>
-int cm_batch_recover(gns_cm *cm, const InputDesc &d, uint64_t m) {
+int cm_batch_recover(gns_cm *cm, const InputDesc &d, uint64_t m, bool fresh) {
     if (m == 0) return GNS_OK;
     if (cm->full) {
         set_error("flow dictionary full (%llu slots, %llu live flows); raise max_flows",
                   (unsigned long long)cm->dict_slots, (unsigned long long)cm->last_live);
         return GNS_E_FULL;
     }
-    if (cm->claimed >= cm->max_flows) GNS_TRY(cm_reclaim(cm));  // proactive: keep the load <= ~1/2
-    GNS_HIP(hipMemcpyAsync(cm->stats_bak, cm->stats, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, cm->stream));
-    const int rc = cm_batch<KIND>(cm, d, m);
-    if (rc != GNS_E_FULL) return rc;
-    // not applied: undo its counters, drop its claims and the dead flows
-    GNS_HIP(hipMemcpyAsync(cm->stats, cm->stats_bak, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, cm->stream));
-    GNS_HIP(hipMemsetAsync(cm->stats + 3, 0, sizeof(unsigned long long), cm->stream));
-    GNS_TRY(cm_reclaim(cm));
-    cm->n_retry++;
+    if (cm->claimed >= cm->max_flows) {  // proactive: keep the load <= ~1/2
+        GNS_TRY(cm_reclaim(cm));
+        fresh = true;
+    }
+    for (;;) {
+        GNS_HIP(hipMemcpyAsync(cm->stats_bak, cm->stats, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
+                               cm->stream));
+        const int rc = cm_batch<KIND>(cm, d, m);
+        if (rc != GNS_E_FULL) return rc;
+        // not applied: undo its counters, drop its claims and the dead flows
+        GNS_HIP(hipMemcpyAsync(cm->stats, cm->stats_bak, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
+                               cm->stream));
+        GNS_HIP(hipMemsetAsync(cm->stats + 3, 0, sizeof(unsigned long long), cm->stream));
+        GNS_TRY(cm_reclaim(cm));
+        cm->n_retry++;
+        if (!fresh) {  // the flows that died since the last rebuild may be room enough
+            fresh = true;
+            continue;
+        }
+        break;
+    }
     if (m <= kChunk) {
         cm->full = true;
         const unsigned long long one = 1;
@@ -2938,8 +2954,8 @@ int cm_batch_recover(gns_cm *cm, const InputDesc &d, uint64_t m) {
         return GNS_E_FULL;
     }
     const uint64_t h = ((m / 2 + kChunk - 1) / kChunk) * kChunk;
-    GNS_TRY(cm_batch_recover<KIND>(cm, d, h));
-    return cm_batch_recover<KIND>(cm, advance(d, h), m - h);
+    GNS_TRY(cm_batch_recover<KIND>(cm, d, h, true));
+    return cm_batch_recover<KIND>(cm, advance(d, h), m - h, false);
 }
 
 template <int KIND>
@@ -2982,7 +2998,7 @@ int cm_insert(gns_cm *cm, InputDesc in, uint64_t n, gns_mem where) {
             d.sizes = reinterpret_cast<const uint32_t *>(p);
             if (d.keys) d.aligned = (d.stride % 4 == 0 && d.stride >= ((cm->K + 3) & ~3u)) ? 1u : 0u;
         }
-        GNS_TRY(cm_batch_recover<KIND>(cm, d, m));
+        GNS_TRY(cm_batch_recover<KIND>(cm, d, m, false));
     }
     return GNS_OK;
 }

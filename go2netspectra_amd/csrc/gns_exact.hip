@@ -514,6 +514,7 @@ struct gns_ex {
 namespace {
 
 int ex_set_dev(gns_ex *ex) {
+    (void)hipGetLastError();  // clear a stale error of an earlier runtime call on this thread
     GNS_HIP(hipSetDevice(ex->device));
     return GNS_OK;
 }

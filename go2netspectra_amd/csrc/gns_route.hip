@@ -241,6 +241,7 @@ int gns_route_partition(gns_route *r, const uint8_t *hdr, const uint32_t *wirele
     }
     if (n >= (1ull << 32)) { set_error("route batch of %llu packets (max 2^32 - 1)", (unsigned long long)n); return GNS_E_RANGE; }
     if (n == 0) { for (uint32_t g = 0; g < r->G; g++) counts[g] = 0; return GNS_OK; }
+    (void)hipGetLastError();  // clear a stale error of an earlier runtime call on this thread
     GNS_HIP(hipSetDevice(r->device));
     const uint32_t nblk = (uint32_t)((n + kRtChunk - 1) / kRtChunk);
     if (r->shard_n < n) {

@@ -671,6 +671,7 @@ struct gns_ss {
 namespace {
 
 int ss_set_dev(gns_ss *ss) {
+    (void)hipGetLastError();  // clear a stale error of an earlier runtime call on this thread
     GNS_HIP(hipSetDevice(ss->device));
     return GNS_OK;
 }
@@ -894,10 +895,10 @@ int ss_batch(gns_ss *ss, const InputDesc &d, uint64_t m) {
 }
 
 // A batch whose encodes overflow the dictionary is aborted in S3b, before any
-// state write: undo its counters, reclaim, re-run it in halves (the declared
-// RNG is indexed by record, so the split does not change any draw).
+// state write: undo its counters, reclaim, re-run it once, then in halves (the
+// declared RNG is indexed by record, so the split does not change any draw).
 template <int KIND>
-int ss_batch_recover(gns_ss *ss, const InputDesc &d, uint64_t m) {
+int ss_batch_recover(gns_ss *ss, const InputDesc &d, uint64_t m, bool fresh) {
     if (m == 0) return GNS_OK;
     if (ss->full) {
         set_error("flow dictionary full (max_flows %llu, %llu slots, %llu live flows); raise max_flows",
@@ -905,14 +906,26 @@ int ss_batch_recover(gns_ss *ss, const InputDesc &d, uint64_t m) {
                   (unsigned long long)ss->last_live);
         return GNS_E_FULL;
     }
-    if (ss->claimed >= ss->max_flows) GNS_TRY(ss_reclaim(ss));
-    GNS_HIP(hipMemcpyAsync(ss->stats_bak, ss->stats, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, ss->stream));
-    const int rc = ss_batch<KIND>(ss, d, m);
-    if (rc != GNS_E_FULL) return rc;
-    GNS_HIP(hipMemcpyAsync(ss->stats, ss->stats_bak, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, ss->stream));
-    GNS_HIP(hipMemsetAsync(ss->stats + 3, 0, sizeof(unsigned long long), ss->stream));
-    GNS_TRY(ss_reclaim(ss));
-    ss->n_retry++;
+    if (ss->claimed >= ss->max_flows) {
+        GNS_TRY(ss_reclaim(ss));
+        fresh = true;
+    }
+    for (;;) {
+        GNS_HIP(hipMemcpyAsync(ss->stats_bak, ss->stats, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
+                               ss->stream));
+        const int rc = ss_batch<KIND>(ss, d, m);
+        if (rc != GNS_E_FULL) return rc;
+        GNS_HIP(hipMemcpyAsync(ss->stats, ss->stats_bak, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
+                               ss->stream));
+        GNS_HIP(hipMemsetAsync(ss->stats + 3, 0, sizeof(unsigned long long), ss->stream));
+        GNS_TRY(ss_reclaim(ss));
+        ss->n_retry++;
+        if (!fresh) {
+            fresh = true;
+            continue;
+        }
+        break;
+    }
     if (m <= kSsChunk) {
         ss->full = true;
         const unsigned long long one = 1;
@@ -922,8 +935,8 @@ int ss_batch_recover(gns_ss *ss, const InputDesc &d, uint64_t m) {
         return GNS_E_FULL;
     }
     const uint64_t h = ((m / 2 + kSsChunk - 1) / kSsChunk) * kSsChunk;
-    GNS_TRY(ss_batch_recover<KIND>(ss, d, h));
-    return ss_batch_recover<KIND>(ss, ss_advance(d, h), m - h);
+    GNS_TRY(ss_batch_recover<KIND>(ss, d, h, true));
+    return ss_batch_recover<KIND>(ss, ss_advance(d, h), m - h, false);
 }
 
 template <int KIND>
@@ -971,7 +984,7 @@ int ss_insert(gns_ss *ss, InputDesc in, uint64_t n, gns_mem where) {
                 d.sizes = reinterpret_cast<const uint32_t *>(p);
             }
         }
-        GNS_TRY(ss_batch_recover<KIND>(ss, d, m));
+        GNS_TRY(ss_batch_recover<KIND>(ss, d, m, false));
     }
     return GNS_OK;
 }

@@ -249,6 +249,7 @@ int gns_synth_destroy(gns_synth *s) {
 
 int gns_synth_fill(gns_synth *s, uint8_t *hdr_dev, uint32_t *wirelen_dev, uint64_t first, uint64_t n) {
     if (!s || (n && (!hdr_dev || !wirelen_dev))) { set_error("null argument"); return GNS_E_ARG; }
+    (void)hipGetLastError();  // clear a stale error of an earlier runtime call on this thread
     GNS_HIP(hipSetDevice(s->device));
     const uint64_t step = 1ull << 26;
     for (uint64_t off = 0; off < n; off += step) {

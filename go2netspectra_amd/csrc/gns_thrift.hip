@@ -99,6 +99,7 @@ extern "C" int gns_thrift_decode(const uint8_t *buf, uint64_t buf_bytes, const u
                                  uint8_t *hdr_out, uint32_t *wirelen_out, int64_t *ts_out, uint64_t *n_bad,
                                  gns_mem where, int device) {
     if (n && (!buf || !offsets || !hdr_out || !wirelen_out || !ts_out)) { set_error("null argument"); return GNS_E_ARG; }
+    (void)hipGetLastError();  // clear a stale error of an earlier runtime call on this thread
     GNS_HIP(hipSetDevice(device));
     if (n == 0) { if (n_bad) *n_bad = 0; return GNS_OK; }
     const uint8_t *dbuf = buf;

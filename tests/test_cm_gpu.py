@@ -364,8 +364,8 @@ def test_full_dictionary_is_cleared_by_reset(gpu, oracle):
         cm.insert_keys(small, sizes_u32(rng, 1000))  # still the same period
     cm.reset()
     orc.reset()
-    for _ in range(3):
-        small, _, _ = zipf_keys(rng, 5000, 40, 16)
+    for _ in range(3):  # <= 60 distinct flows: they fit the 64-flow dictionary
+        small, _, _ = zipf_keys(rng, 5000, 20, 16)
         sizes = sizes_u32(rng, 5000)
         cm.insert_keys(small, sizes)
         orc.insert_keys(small, sizes)
