@@ -507,6 +507,76 @@ def bench_hybrid(args, torch, dist, world, rank, local):
         dist.destroy_process_group()
 
 
+def bench_c1(args, torch, dist, world, rank, local):
+    """configs[0]: the pcap-analyzer path (cmd/pcap-analyzer -> offline.RunAnalyzer ->
+    pcap.Reader.ReadPackets -> workers -> Count-Min) on a 1M-packet capture in the
+    reference generator's format (scripts/pcapgen/main.go), Count-Min d=4 w=65536.
+    A step = the whole capture: the host packer reads the file into 64-byte records
+    (gns_pack_pcap), the engine inserts them from host memory (H2D staging included)
+    into a fresh period of the sketch.  The CPU legs time the C restatement of the Go
+    worker pool and the sequential oracle on the same records (plus the same pack)."""
+    from go2netspectra_amd import CountMin, read_pcap, write_pcapgen
+    from oracle import oracle as orc
+    n = args.c1_packets
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"gns_pcapgen_{n}.pcap")
+    if not os.path.exists(path):
+        write_pcapgen(path, n)
+    W, D = 65536, 4
+    seeds = row_seeds(D)
+    cm = CountMin(W, D, 1 << 20, 1000, flow_fields=FIELDS, seeds=seeds, max_flows=1 << 21, batch_packets=n, device=local)
+    t_pack = t_gpu = 0.0
+    hb = None
+    for k in range(args.warmup + args.steps):
+        cm.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hb = read_pcap(path)
+        t1 = time.perf_counter()
+        cm.insert_headers(hb.hdr, hb.wirelen)
+        cm.flush()
+        t2 = time.perf_counter()
+        if k >= args.warmup:
+            t_pack += t1 - t0
+            t_gpu += t2 - t1
+    K = args.steps
+    line = {
+        "metric": "Mpackets/s pcap-analyzer Count-Min d=4 w=65536 (pcap file -> packer -> GPU), 1M-packet pcapgen capture",
+        "value": round(n * K / (t_pack + t_gpu) / 1e6, 2), "unit": "Mpackets/s", "n_gpus": 1, "steps": K,
+        "warmup": args.warmup, "ms_per_step": round((t_pack + t_gpu) / K * 1e3, 3), "higher_is_better": True,
+        "scaling": "none", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic capture in scripts/pcapgen/main.go's format (go2netspectra_amd.write_pcapgen), "
+                f"{os.path.getsize(path) / 1e6:.0f} MB on local disk (page cache warm after the warmup)",
+        "config": {"workload": "configs[0]: pcap-analyzer, Count-Min d=4 w=65536, 5-tuple key, 1M packets",
+                   "packets": n, "pack_ms": round(t_pack / K * 1e3, 3), "insert_ms_incl_h2d": round(t_gpu / K * 1e3, 3),
+                   "insert_only_rate": round(n * K / t_gpu / 1e6, 2)},
+        "note": "not the headline metric; the reference pcap-analyzer is a CPU path (BASELINE configs[0])",
+    }
+    if not args.no_cpu:
+        o = orc.CountMin(W, D, 1 << 20, 1000, 37, seeds)
+        t0 = time.perf_counter()
+        o.insert_hdr64(hb.hdr, hb.wirelen, FIELDS)
+        seq_s = time.perf_counter() - t0
+        threads = int(os.environ.get("GNS_CPU_THREADS", 16))
+        p = orc.CountMin(W, D, 1 << 20, 1000, 37, seeds)
+        t0 = time.perf_counter()
+        p.insert_hdr64_pool(hb.hdr, hb.wirelen, FIELDS, threads)
+        pool_s = time.perf_counter() - t0
+        pack_s = t_pack / K
+        line["cpu_baseline"] = {
+            "value": round(n / (pack_s + pool_s) / 1e6, 3), "unit": "Mpackets/s", "cores": threads, "kind": "port",
+            "sample": f"the whole {n:,}-packet capture: the same packer, then the C restatement of the Go worker "
+                      f"pool ({threads} threads, count_min.go CAS loops); pool alone "
+                      f"{n / pool_s / 1e6:.2f} Mpkt/s",
+            "host": host_cpu(),
+            "sequential_oracle": {"value": round(n / (pack_s + seq_s) / 1e6, 3), "cores": 1,
+                                  "insert_only": round(n / seq_s / 1e6, 3)},
+        }
+        got, want = cm.export_state(), o.export()
+        line["parity"] = {"checked_packets": n, "bit_exact": all(bool(np.array_equal(a, b)) for a, b in zip(got, want)),
+                          "how": "the last step's sketch vs the sequential oracle on the same records"}
+    print(json.dumps(line), flush=True)
+
+
 def bench_windows(args, torch, dist, world, cm, timed_step, n):
     """configs[3]'s per-window cycle, timed after the headline steps: each window
     inserts --window-steps fresh steps of packets (timed_step: generation outside
@@ -558,6 +628,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--width", type=int, default=WIDTH, help="Count-Min width (2^24 = configs[4] geometry)")
     ap.add_argument("--depth", type=int, default=DEPTH, help="Count-Min depth (8 = configs[4] geometry)")
+    ap.add_argument("--config", choices=["c1", "c2"], default="c2",
+                    help="c1 = configs[0]: the pcap-analyzer path on a 1M-packet pcapgen capture (CM d=4 w=65536); "
+                         "c2 = configs[1], the headline")
+    ap.add_argument("--c1-packets", type=int, default=1_000_000)
     ap.add_argument("--sketch", choices=["countmin", "superspread", "exact", "thrift", "hybrid"], default="countmin",
                     help="superspread = configs[2]; hybrid = configs[4]; exact = the exact aggregator "
                          "(none of them is the headline metric)")
@@ -609,6 +683,8 @@ def main():
 
     from go2netspectra_amd import CountMin, SyntheticTraffic
 
+    if args.config == "c1":
+        return bench_c1(args, torch, dist, world, rank, local)
     if args.sketch == "superspread":
         return bench_superspread(args, torch, dist, world, rank, local)
     if args.sketch == "exact":
@@ -746,6 +822,19 @@ def main():
     if args.windows > 0 and not args.host_input and not route:
         window = bench_windows(args, torch, dist, world, cm, timed_step, n)
 
+    # flow dictionary: reclaims during the run, and the cost of one reclaim at a
+    # window boundary with this run's live set (untimed; inserts reclaim on their
+    # own when the dictionary reaches max_flows)
+    dict_run = cm.dict_stats()
+    torch.cuda.synchronize()
+    t_r = time.perf_counter()
+    cm.reclaim()
+    reclaim_ms = (time.perf_counter() - t_r) * 1e3
+    dict_after = cm.dict_stats()
+    dictionary = {"max_flows": args.max_flows, "reclaims_during_run": dict_run["reclaims"],
+                  "retried_batches": dict_run["retried_batches"], "claimed_before_reclaim": dict_run["claimed"],
+                  "live_flows": dict_after["live"], "one_reclaim_ms": round(reclaim_ms, 3)}
+
     hh = cm.heavy_hitters()
     if world > 1:
         from go2netspectra_amd.dist import allgather_heavy
@@ -790,6 +879,7 @@ def main():
         "stage_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()},
         "heavy_hitters": {"count": len(hh.Count), "size": len(hh.Size or [])},
         "engine_counters": counters,
+        "flow_dictionary": dictionary,
     }
     if window is not None:
         line["window_exchange"] = window

@@ -37,7 +37,7 @@ EXPORTED = [
     "gns_ex_stage_times",
     "gns_thrift_decode", "gns_pack_pcap", "gns_pack_pcap_ts", "gns_last_error", "gns_version",
     "gns_route_create", "gns_route_destroy", "gns_route_partition",
-    "gns_cm_dict_stats", "gns_ss_dict_stats", "gns_ex_dict_stats",
+    "gns_cm_dict_stats", "gns_ss_dict_stats", "gns_ex_dict_stats", "gns_cm_reclaim", "gns_ss_reclaim",
 ]
 
 
@@ -153,7 +153,7 @@ def load() -> ct.CDLL:
         "gns_route_create": ([u32, i32, vp], i32), "gns_route_destroy": ([vp], i32),
         "gns_route_partition": ([vp, vp, vp, u64, vp, vp, vp], i32),
         "gns_cm_dict_stats": ([vp, vp], i32), "gns_ss_dict_stats": ([vp, vp], i32),
-        "gns_ex_dict_stats": ([vp, vp], i32),
+        "gns_ex_dict_stats": ([vp, vp], i32), "gns_cm_reclaim": ([vp], i32), "gns_ss_reclaim": ([vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

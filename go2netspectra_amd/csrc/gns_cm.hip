@@ -3562,6 +3562,12 @@ int gns_cm_counters(gns_cm *cm, uint64_t out[8]) {
     return GNS_OK;
 }
 
+int gns_cm_reclaim(gns_cm *cm) {
+    if (!cm) return GNS_E_ARG;
+    GNS_TRY(set_dev(cm));
+    return cm_reclaim(cm);
+}
+
 int gns_cm_dict_stats(gns_cm *cm, uint64_t out[6]) {
     if (!cm || !out) return GNS_E_ARG;
     out[0] = cm->n_reclaim; out[1] = cm->n_dropped; out[2] = cm->last_live; out[3] = cm->claimed;

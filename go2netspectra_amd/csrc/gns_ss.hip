@@ -1294,6 +1294,12 @@ int gns_ss_counters(gns_ss *ss, uint64_t out[8]) {
     return GNS_OK;
 }
 
+int gns_ss_reclaim(gns_ss *ss) {
+    if (!ss) return GNS_E_ARG;
+    GNS_TRY(ss_set_dev(ss));
+    return ss_reclaim(ss);
+}
+
 int gns_ss_dict_stats(gns_ss *ss, uint64_t out[6]) {
     if (!ss || !out) return GNS_E_ARG;
     out[0] = ss->n_reclaim; out[1] = ss->n_dropped; out[2] = ss->last_live; out[3] = ss->claimed;

@@ -15,6 +15,7 @@ from __future__ import annotations
 import ctypes as ct
 import ipaddress
 import os
+import struct
 from dataclasses import dataclass
 from typing import Optional
 
@@ -156,6 +157,62 @@ def write_pcap(path: str, frames, wirelens=None, snaplen: int = 65536, ts_ns=Non
             sec, usec = (i, 0) if ts_ns is None else divmod(int(ts_ns[i]) // 1000, 1_000_000)
             f.write(struct.pack("<IIII", sec, usec, len(fr), wl))
             f.write(fr)
+
+
+def write_pcapgen(path: str, n: int, seed: int = 0x5EED0C1, t0_us: int = 1_700_000_000_000_000) -> None:
+    """A capture in the format of the reference's generator (scripts/pcapgen/main.go:17-97),
+    the input of BASELINE configs[0] (pcap-analyzer, Count-Min d=4 w=65536):
+      - classic pcap, pcapgo.NewWriter: microsecond magic, v2.4, snaplen 65536, Ethernet;
+      - per packet: Ethernet 00:11:22:33:44:55 -> 00:66:77:88:99:aa, IPv4 (IHL 5, TTL 64,
+        protocol TCP, random 4-byte source and destination), TCP SYN with random ports in
+        [1024, 65535), random seq/ack, window 14600, then 50..1449 random payload bytes
+        (main.go:43-47: rand.Intn(1400) + 50), i.e. frames of 104..1503 bytes;
+      - lengths fixed (FixLengths); the IPv4 header checksum is computed, the TCP checksum
+        is left 0 (gopacket does not verify checksums when decoding, parser.go never
+        reads them);
+      - timestamps: t0 + i microseconds (main.go:80 uses time.Now()).
+    Written with numpy in one pass (a 1M-packet capture is ~0.8 GB)."""
+    rng = np.random.default_rng(seed)
+    plen = rng.integers(50, 1450, n).astype(np.int64)
+    flen = 54 + plen
+    rec = 16 + flen
+    offs = 24 + np.concatenate([[0], np.cumsum(rec)[:-1]]).astype(np.int64)
+    total = 24 + int(rec.sum())
+    buf = np.frombuffer(bytearray(rng.bytes(total)), np.uint8).copy()  # payload bytes random
+    buf[:24] = np.frombuffer(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 65536, 1), np.uint8)
+    h = np.zeros((n, 70), np.uint8)
+    ts = t0_us + np.arange(n, dtype=np.int64)
+    h[:, 0:4] = (ts // 1_000_000).astype("<u4").view(np.uint8).reshape(n, 4)
+    h[:, 4:8] = (ts % 1_000_000).astype("<u4").view(np.uint8).reshape(n, 4)
+    h[:, 8:12] = flen.astype("<u4").view(np.uint8).reshape(n, 4)
+    h[:, 12:16] = h[:, 8:12]
+    e = 16
+    h[:, e:e + 6] = [0x00, 0x66, 0x77, 0x88, 0x99, 0xAA]
+    h[:, e + 6:e + 12] = [0x00, 0x11, 0x22, 0x33, 0x44, 0x55]
+    h[:, e + 12:e + 14] = [0x08, 0x00]
+    ip = e + 14
+    h[:, ip] = 0x45
+    h[:, ip + 2:ip + 4] = (flen - 14).astype(">u2").view(np.uint8).reshape(n, 2)
+    h[:, ip + 8] = 64
+    h[:, ip + 9] = 6
+    h[:, ip + 12:ip + 20] = rng.integers(0, 256, (n, 8), dtype=np.uint8)
+    words = h[:, ip:ip + 20].astype(np.uint32).reshape(n, 10, 2)
+    csum = (words[:, :, 0] << 8 | words[:, :, 1]).sum(axis=1)
+    csum = (csum & 0xFFFF) + (csum >> 16)
+    csum = (csum & 0xFFFF) + (csum >> 16)
+    h[:, ip + 10:ip + 12] = (~csum & 0xFFFF).astype(">u2").view(np.uint8).reshape(n, 2)
+    tcp = ip + 20
+    ports = rng.integers(1024, 65535, (n, 2)).astype(">u2")
+    h[:, tcp:tcp + 4] = ports.view(np.uint8).reshape(n, 4)
+    h[:, tcp + 4:tcp + 12] = rng.integers(0, 256, (n, 8), dtype=np.uint8)
+    h[:, tcp + 12] = 5 << 4
+    h[:, tcp + 13] = 0x02  # SYN
+    h[:, tcp + 14:tcp + 16] = [14600 >> 8, 14600 & 0xFF]
+    h[:, tcp + 16:tcp + 20] = 0
+    idx = offs[:, None] + np.arange(70)[None, :]
+    buf[idx] = h
+    with open(path, "wb") as f:
+        f.write(buf.tobytes())
 
 
 def write_pcapng(path: str, frames, wirelens=None, ts_units=None, tsresol=None, tsoffset=None,

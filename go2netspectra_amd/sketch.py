@@ -312,6 +312,10 @@ class CountMin:
         """Flow-dictionary reclaim counters (gns_cm_dict_stats)."""
         return _lib.dict_stats(self._L.gns_cm_dict_stats, self._h)
 
+    def reclaim(self) -> None:
+        """Drop the flows no bucket names from the dictionary now (gns_cm_reclaim)."""
+        check(self._L.gns_cm_reclaim(self._h))
+
     def set_timing(self, on: bool = True) -> None:
         check(self._L.gns_cm_set_timing(self._h, 1 if on else 0))
 
@@ -459,6 +463,9 @@ class SuperSpread:
     def dict_stats(self) -> dict:
         """Flow-dictionary reclaim counters (gns_ss_dict_stats)."""
         return _lib.dict_stats(self._L.gns_ss_dict_stats, self._h)
+
+    def reclaim(self) -> None:
+        check(self._L.gns_ss_reclaim(self._h))
 
     def set_timing(self, on: bool = True) -> None:
         check(self._L.gns_ss_set_timing(self._h, 1 if on else 0))

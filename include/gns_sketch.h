@@ -159,6 +159,8 @@ int gns_cm_counters(gns_cm *cm, uint64_t out[8]);
  * last reclaim, [3] claimed slots now, [4] reclaim time (us, host clock incl. the
  * rebuild's device work), [5] batches re-run after a dictionary overflow */
 int gns_cm_dict_stats(gns_cm *cm, uint64_t out[6]);
+/* reclaim now (e.g. at a window boundary; inserts also reclaim on their own) */
+int gns_cm_reclaim(gns_cm *cm);
 int gns_cm_set_timing(gns_cm *cm, int on);
 int gns_cm_stage_times(gns_cm *cm, double ms[8], uint64_t launches[8], int reset);
 void *gns_cm_stream(gns_cm *cm); /* hipStream_t the handle launches on */
@@ -229,6 +231,7 @@ int gns_ss_stats(gns_ss *ss, uint64_t stats[4]);
  * (lz above the batch-entry register), HLL encodes, records, device batches */
 int gns_ss_counters(gns_ss *ss, uint64_t out[8]);
 int gns_ss_dict_stats(gns_ss *ss, uint64_t out[6]);  /* as gns_cm_dict_stats */
+int gns_ss_reclaim(gns_ss *ss);
 int gns_ss_set_timing(gns_ss *ss, int on);
 int gns_ss_stage_times(gns_ss *ss, double ms[8], uint64_t launches[8], int reset);
 

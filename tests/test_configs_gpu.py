@@ -96,3 +96,28 @@ def test_hybrid_concurrent_exact_and_countmin(gpu, oracle):
     got = {f.Key: (f.StartTime, f.EndTime, f.PacketCount, f.ByteCount) for f in ex.flows()}
     assert_same_flows(got, o_ex.export())
     view.close()
+
+
+def test_c1_pcapgen_capture(gpu, oracle, tmp_path):
+    """configs[0]: a 1M-packet capture in the reference generator's format
+    (scripts/pcapgen/main.go: TCP SYN, uniform IPs / ports, 104..1503-byte frames),
+    read by the host packer (pkg/pcap/reader.go:35-49) and inserted from host
+    memory into Count-Min d=4 w=65536 (cmd/pcap-analyzer): full state and both
+    heavy-hitter lists equal the oracle fed the same records."""
+    from go2netspectra_amd import CountMin, read_pcap, write_pcapgen
+    path = str(tmp_path / "c1.pcap")
+    write_pcapgen(path, 1_000_000)
+    hb = read_pcap(path)
+    assert len(hb) == 1_000_000
+    seeds = np.random.default_rng(1).integers(0, 2**32, 4, dtype=np.uint64).astype(np.uint32)
+    cm = CountMin(65536, 4, 1000, 2, flow_fields=FIVE, seeds=seeds, max_flows=1 << 21)
+    cm.insert_headers(hb.hdr, hb.wirelen)
+    cm.flush()
+    assert cm.stats()["inserted"] == 1_000_000
+    orc = oracle.CountMin(65536, 4, 1000, 2, 37, seeds)
+    assert orc.insert_hdr64(hb.hdr, hb.wirelen, FIVE) == 1_000_000
+    _same_state(cm, orc)
+    hh = cm.heavy_hitters()
+    assert_same_list([(x.Flow, x.Count) for x in hh.Count], orc.heavy("count"))
+    assert_same_list([(x.Flow, x.Size) for x in hh.Size], orc.heavy("size"))
+    assert len(hh.Size) > 0 and len(hh.Count) > 0

@@ -243,3 +243,28 @@ def test_merge_heavy_arrays_canonical_order():
         assert [(bytes(a), int(b)) for a, b in zip(gf, gv)] == want
     e = merge_heavy_arrays(np.zeros((0, 8), np.uint8), np.zeros(0, np.uint32))
     assert len(e[0]) == 0 and len(e[1]) == 0
+
+
+def test_pcapgen_capture_format(tmp_path):
+    """configs[0]'s input, scripts/pcapgen/main.go:17-97: TCP SYN over IPv4, frames of
+    104..1503 bytes, ports in [1024, 65535), read back by the packer; every record is in
+    the device parser's fast subset and parses to the written tuple."""
+    import struct
+    import go2netspectra_amd as g
+    from oracle import oracle as orc
+    path = str(tmp_path / "pg.pcap")
+    g.write_pcapgen(path, 20_000, seed=3)
+    raw = open(path, "rb").read()
+    assert struct.unpack("<IHHiIII", raw[:24]) == (0xA1B2C3D4, 2, 4, 0, 0, 65536, 1)
+    hb = g.read_pcap(path)
+    assert len(hb) == 20_000
+    assert hb.wirelen.min() >= 104 and hb.wirelen.max() <= 1503
+    h = hb.hdr
+    assert (h[:, 12] == 8).all() and (h[:, 13] == 0).all() and (h[:, 14] == 0x45).all() and (h[:, 23] == 6).all()
+    assert (h[:, 47] == 0x02).all()  # SYN
+    sport = h[:, 34].astype(int) << 8 | h[:, 35]
+    assert sport.min() >= 1024 and sport.max() < 65535
+    assert (hb.ts[1:] - hb.ts[:-1] == 1000).all()  # microsecond steps, ns timestamps
+    for i in range(0, 20_000, 997):
+        st, s16, d16, sp, dp, pr = orc.parse_hdr64(bytes(h[i]), int(hb.wirelen[i]))
+        assert st == 0 and s16[:4] == bytes(h[i, 26:30]) and sp == sport[i] and pr == 6
