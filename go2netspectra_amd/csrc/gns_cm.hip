@@ -245,7 +245,7 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) { return __ockl_wfred
 // issued earlier by the caller), publish/hash the row buckets, bin codes,
 // block histogram and designated-bucket summaries.
 struct K1Lds {
-    uint32_t *s_tab, *s_hist, *s_hFc, *s_hFs, *s_nfc, *s_nfs, *s_smax, *s_pend, *s_full, *s_claim;
+    uint32_t *s_tab, *s_hist, *s_hFc, *s_hFs, *s_nfc, *s_nfs, *s_smax, *s_pend, *s_full;
     unsigned long long *s_os, *s_fs;
 };
 
@@ -309,14 +309,19 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
         anyhot = anyhot || hs[rr] >= 0;
     }
     if (ok && first >= 2) {
-        // A committed flow displaced from its home slot is parked like a first-sight
-        // packet (k_resolve walks the rest of the chain next launch; its bucket codes
-        // are already hashed) instead of stalling the wave on a dependent probe.  The
-        // summaries treat a parked packet as foreign to every owner, which is exact
-        // only for a flow that owns no bucket: so a packet that touches a designated
-        // bucket walks the chain here.  An empty home slot is claimed here.
-        if (first == 3 && !anyhot) { res = CM_PENDING; out = (slot0 + 1u) & a.D.mask; }
-        else res = cm_find_or_claim(a.D, kw, K, first == 2 ? slot0 : ((slot0 + 1u) & a.D.mask), a.epoch, &out, rec);
+        // A flow whose home slot is empty is new: it is parked for k_resolve, which
+        // claims it (and counts the claim against the dictionary cap; K1 stays at
+        // 128 VGPRs without spills only without that code).  A committed flow
+        // displaced from its home slot is parked too (k_resolve walks the rest of
+        // the chain next launch; its bucket codes are already hashed) instead of
+        // stalling the wave on a dependent probe.  The summaries treat a parked
+        // packet as foreign to every owner, which is exact only for a flow that owns
+        // no bucket (a new one does not): so a displaced packet that touches a
+        // designated bucket walks the chain here (the rare claims of that walk are
+        // not counted: the count restarts from the exact live set at every rebuild,
+        // and the probe limit still bounds the walks).
+        if (first == 2 || !anyhot) { res = CM_PENDING; out = first == 2 ? slot0 : ((slot0 + 1u) & a.D.mask); }
+        else res = cm_find_or_claim(a.D, kw, K, (slot0 + 1u) & a.D.mask, a.epoch, &out, rec);
     }
     if (ok) {
         if (res == CM_FULL) {
@@ -332,11 +337,7 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
             kid = out;
         }
     }
-    {   // claim accounting (one LDS add per wave; the block flushes once, dict_flush_claims)
-        const uint64_t cmask = __ballot(res == CM_CLAIMED);
-        if (cmask && (threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)cmask) - 1))
-            atomicAdd(S.s_claim, (uint32_t)__popcll(cmask));
-    }
+
     if (bw && res == CM_CLAIMED) {  // publish the bucket cache with the key (visible next launch)
         uint32_t *tp = a.D.rec + (size_t)out * a.D.RW;
 #pragma unroll
@@ -403,7 +404,7 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 template <int KIND, int MODE, int KB, int DD, int NT>
 __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : 1) void k_extract(ExtractArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xsm[];
-    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_claim, s_abort;
+    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
     __shared__ uint8_t s_src[80];
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
     const uint32_t NS = a.g.d * kHot;
@@ -426,14 +427,13 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : 1) void k_extract(Ext
         s_hFs[i] = id != GNS_ID_NONE ? a.Fs[cell] : GNS_ID_NONE;
         s_nfc[i] = 0; s_nfs[i] = 0; s_smax[i] = 0; s_os[i] = 0; s_fs[i] = 0;
     }
-    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; s_claim = 0; s_abort = dict_aborted(a.D); }
+    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; }
     __syncthreads();
-    if (s_abort) return;  // the batch overflowed the dictionary: it is re-run after a reclaim
     const uint64_t beg = (uint64_t)blk * kChunk;
     const uint64_t end = min(a.n, beg + kChunk);
     const bool bw = a.D.bw != 0;
     uint32_t n_ok = 0;
-    const K1Lds S{s_tab, s_hist, s_hFc, s_hFs, s_nfc, s_nfs, s_smax, &s_pend, &s_full, &s_claim, s_os, s_fs};
+    const K1Lds S{s_tab, s_hist, s_hFc, s_hFs, s_nfc, s_nfs, s_smax, &s_pend, &s_full, s_os, s_fs};
     if constexpr (KIND == IN_HDR) {
         // Two-stage software pipeline over the block's packets: iteration k
         // parses packet k+1 and issues its dictionary probe (and the header
@@ -538,7 +538,6 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : 1) void k_extract(Ext
         if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
         if (s_unsup) atomicAdd(&a.stats[2], (unsigned long long)s_unsup);
         if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
-        dict_flush_claims(a.D, s_claim, &a.stats[3]);
     }
 }
 

@@ -120,4 +120,5 @@ def test_c1_pcapgen_capture(gpu, oracle, tmp_path):
     hh = cm.heavy_hitters()
     assert_same_list([(x.Flow, x.Count) for x in hh.Count], orc.heavy("count"))
     assert_same_list([(x.Flow, x.Size) for x in hh.Size], orc.heavy("size"))
-    assert len(hh.Size) > 0 and len(hh.Count) > 0
+    n_size = len(hh.Size)
+    assert n_size > 0  # unique flows: count fingerprints never reach 2, sizes do reach 1000
