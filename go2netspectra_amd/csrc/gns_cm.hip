@@ -398,6 +398,20 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 #ifndef GNS_EX_MINW
 #define GNS_EX_MINW 4
 #endif
+// K1 at configs[4]'s geometry (d=8, 5-tuple key), A/B on one box (tools/ab_c5only.sh):
+//   two-stage pipeline, 1024 threads: 128 VGPRs + 66 spilled          5.42 ms / 100M
+//   two-stage pipeline,  768 threads: 148 VGPRs, 12 waves per CU      4.47-4.50
+//   plain loop,          768 threads:  92 VGPRs                        4.58-4.59
+//   plain loop,          640 threads (two blocks per CU by LDS)        5.28-5.30
+//   plain loop,         1024 threads:  93 VGPRs, 16 waves per CU      4.01-4.02   <- default
+#ifndef GNS_C5_THREADS
+#define GNS_C5_THREADS 1024
+#endif
+constexpr int kC5Threads = GNS_C5_THREADS;
+#ifndef GNS_C5_PIPE
+#define GNS_C5_PIPE 0
+#endif
+constexpr bool kC5Pipe = GNS_C5_PIPE != 0;
 // NT = threads per block: 256 (four blocks per CU) when the block's LDS fits four
 // times in a CU, else 1024 (one block of 16 waves: wide or deep sketches, whose
 // histogram and hot-slot tables take more than a quarter of the LDS).
@@ -434,7 +448,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : 1) void k_extract(Ext
     const bool bw = a.D.bw != 0;
     uint32_t n_ok = 0;
     const K1Lds S{s_tab, s_hist, s_hFc, s_hFs, s_nfc, s_nfs, s_smax, &s_pend, &s_full, s_os, s_fs};
-    if constexpr (KIND == IN_HDR) {
+    if constexpr (KIND == IN_HDR && (DD != 8 || kC5Pipe)) {
         // Two-stage software pipeline over the block's packets: iteration k
         // parses packet k+1 and issues its dictionary probe (and the header
         // prefetch of packet k+2), then consumes packet k, whose probe was
@@ -2731,8 +2745,12 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.stats = cm->stats;
         ScopedStage st(cm->timer, 0);
         const size_t lds = extract_lds_bytes(g.nbins_all, g.d);
-        if (lds > kExLdsSmall) {  // deep / wide sketch: one 1024-thread block per CU
-            if (cm->K == 37)
+        if (lds > kExLdsSmall) {  // deep / wide sketch: one large block per CU
+            // configs[4] (d=8, 5-tuple): the plain loop at 93 VGPRs, 16 waves per CU (the
+            // two-stage pipeline spilled 66 VGPRs at 1024 threads; see kC5Threads)
+            if (cm->K == 37 && g.d == 8)
+                hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 8, kC5Threads>), dim3(nblk), dim3(kC5Threads), lds, s, a);
+            else if (cm->K == 37)
                 hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 0, 1024>), dim3(nblk), dim3(1024), lds, s, a);
             else if (cm->K == 16)
                 hipLaunchKernelGGL((k_extract<KIND, MODE, 16, 0, 1024>), dim3(nblk), dim3(1024), lds, s, a);
