@@ -35,7 +35,7 @@ EXPORTED = [
     "gns_ex_create", "gns_ex_destroy", "gns_ex_insert_tuples", "gns_ex_insert_headers", "gns_ex_flush",
     "gns_ex_query", "gns_ex_snapshot", "gns_ex_reset", "gns_ex_counters", "gns_ex_set_timing",
     "gns_ex_stage_times",
-    "gns_thrift_decode", "gns_pack_pcap", "gns_pack_pcap_ts", "gns_last_error", "gns_version",
+    "gns_thrift_decode", "gns_pack_pcap", "gns_pack_pcap_ts", "gns_pack_counts", "gns_frame_record", "gns_last_error", "gns_version",
     "gns_route_create", "gns_route_destroy", "gns_route_partition",
     "gns_cm_dict_stats", "gns_ss_dict_stats", "gns_ex_dict_stats", "gns_cm_reclaim", "gns_ss_reclaim",
 ]
@@ -149,6 +149,8 @@ def load() -> ct.CDLL:
         "gns_thrift_decode": ([vp, u64, vp, u64, vp, vp, vp, vp, i32, i32], i32),
         "gns_pack_pcap": ([ct.c_char_p, vp, vp, u64, vp], ct.c_int64),
         "gns_pack_pcap_ts": ([ct.c_char_p, vp, vp, vp, u64, vp], ct.c_int64),
+        "gns_pack_counts": ([vp], ct.c_int),
+        "gns_frame_record": ([vp, ct.c_uint32, ct.c_uint32, vp], ct.c_int),
         "gns_last_error": ([], ct.c_char_p), "gns_version": ([], ct.c_char_p),
         "gns_route_create": ([u32, i32, vp], i32), "gns_route_destroy": ([vp], i32),
         "gns_route_partition": ([vp, vp, vp, u64, vp, vp, vp], i32),

@@ -114,6 +114,11 @@ int dict_rebuild(DictDev &D, uint64_t &slots, const DictIds *mark, int nmark, co
                  DictIds *remap_arrays, int nremap, uint64_t new_slots, hipStream_t s, DictScratch &sc,
                  uint64_t *live_out, uint32_t **old_rec_out);
 
+// gns_frame.cpp: one captured frame -> one 64-byte record for the device
+// parser.  Returns 0 = copied verbatim (device fast-path shape), 1 = decoded
+// into a pre-parsed 0x88B5 record, 2 = no IP layer (a record the device drops).
+int frame_record(const uint8_t *frame, uint32_t caplen, uint32_t wirelen, uint8_t *rec);
+
 inline uint32_t ceil_log2(uint64_t x) {
     uint32_t b = 0;
     while ((1ull << b) < x) b++;

@@ -71,6 +71,7 @@ __device__ __forceinline__ bool udp_tunnel_port(uint32_t p) {
     return p == 4789u || p == 6081u || p == 2152u;
 }
 
+// (byte 36 = proto; bytes 37..39 = 0: callers add the IP version bytes after it)
 __device__ __forceinline__ void set_ports(uint32_t (&tw)[10], uint32_t sport, uint32_t dport,
                                           uint32_t proto) {
     // bytes 32..35 = sport BE, dport BE; byte 36 = proto
@@ -82,7 +83,20 @@ __device__ __forceinline__ void set_ports(uint32_t (&tw)[10], uint32_t sport, ui
 // at bytes 12-13 and the L3 header at byte 14.  nv = number of removed tags
 // (the original L2 header length is 14 + 4*nv); lim = record bytes still
 // present (64 - 4*nv).  Offsets are compile-time constants: no dynamic
-// indexing into the record registers.
+// indexing into the record registers.  Writes the IP version bytes (38, 39).
+//
+// gopacket v1.1.19 keeps a layer whose decode fails with the fields it set
+// before the failing check (decodeIPv4 / decodeIPv6 / decodeTCP / decodeUDP
+// call p.AddLayer before returning the error), and parser.go:38-61 reads them:
+//   IPv4 data < 20 bytes       -> IPv4 layer with nil IPs: counted, zero IPs, proto 0
+//   IPv4 Length < 20, IHL < 5, IHL*4 > Length -> IPs + protocol, ports 0
+//   IPv6 data < 40 bytes       -> nil IPs, NextHeader 0
+//   IPv6 Length 0 (no HBH)     -> IPs + NextHeader, ports 0
+//   TCP < 20 bytes / UDP < 8   -> the layer with ports 0; a TCP data offset < 5 or
+//                                 beyond the data errs after the ports are read
+// Encapsulations and IPv6 extension chains whose inner layers gopacket decodes
+// further are UNSUPPORTED here: the host packer decodes such frames and hands
+// them over as pre-parsed 0x88B5 records.
 __device__ __forceinline__ int parse_l3(const uint32_t (&w)[16], uint32_t type, uint32_t wirelen,
                                         uint32_t nv, uint32_t (&tw)[10]) {
     constexpr int OFF = 14;
@@ -90,24 +104,25 @@ __device__ __forceinline__ int parse_l3(const uint32_t (&w)[16], uint32_t type, 
     const uint32_t lim = 64u - 4u * nv;
     const uint32_t l2len = wirelen > l2hdr ? wirelen - l2hdr : 0u;
     if (type == 0x0800u) {  // gopacket IPv4.DecodeFromBytes
+        if (l2len < 20) return PARSE_OK;  // nil IPs (version bytes 0), protocol 0, no ports
         const uint32_t ihl = rec_byte<OFF>(w) & 15u;
         uint32_t tot = rec_be16<OFF + 2>(w);
         if (tot == 0) tot = l2len;  // TSO
-        if (ihl < 5) return PARSE_DROP;
-        if (ihl > 5) return PARSE_UNSUPPORTED;
-        if (tot < 20 || l2len < 20) return PARSE_DROP;
         const uint32_t proto = rec_byte<OFF + 9>(w);
         tw[0] = rec_u32<OFF + 12>(w);  // parser.go:40-41: 4-byte IPv4, left-aligned slot
         tw[4] = rec_u32<OFF + 16>(w);
-        tw[9] = proto;
+        tw[9] = proto | 4u << 24 | 4u << 16;
+        if (tot < 20 || ihl < 5 || ihl * 4 > tot) return PARSE_OK;  // decode error: no further layers
+        if (ihl > 5) return PARSE_UNSUPPORTED;                      // options: the host packer
         const uint32_t frag = rec_be16<OFF + 6>(w);
         if (frag & 0x3FFFu) return PARSE_OK;  // MF or offset: LayerTypeFragment, ports 0
         const uint32_t avail = (tot < l2len ? tot : l2len) - 20u;
+        if (avail == 0) return PARSE_OK;      // empty payload: no next layer
         if (proto == 6u) {
-            if (avail < 20) return PARSE_OK;
-            const uint32_t doff = rec_byte<OFF + 32>(w) >> 4;  // byte 46 < lim for nv <= 2
-            if (doff < 5 || doff * 4 > avail) return PARSE_OK;
-            set_ports(tw, rec_be16<OFF + 20>(w), rec_be16<OFF + 22>(w), proto);
+            if (avail >= 20) {
+                set_ports(tw, rec_be16<OFF + 20>(w), rec_be16<OFF + 22>(w), proto);
+                tw[9] |= 4u << 24 | 4u << 16;
+            }
             return PARSE_OK;
         }
         if (proto == 17u) {
@@ -115,37 +130,42 @@ __device__ __forceinline__ int parse_l3(const uint32_t (&w)[16], uint32_t type, 
             const uint32_t sp = rec_be16<OFF + 20>(w), dp = rec_be16<OFF + 22>(w);
             if (udp_tunnel_port(sp) || udp_tunnel_port(dp)) return PARSE_UNSUPPORTED;
             set_ports(tw, sp, dp, proto);
+            tw[9] |= 4u << 24 | 4u << 16;
             return PARSE_OK;
         }
-        if (proto == 4u || proto == 41u || proto == 47u || proto == 51u || proto == 137u)
+        switch (proto) {  // inner layers gopacket decodes (HBH, IP-in-IP, routing, GRE, AH, dest opts, MPLS)
+        case 0: case 4: case 41: case 43: case 47: case 51: case 60: case 137:
             return PARSE_UNSUPPORTED;
-        return PARSE_OK;
+        default:
+            return PARSE_OK;  // ICMP, IPv6 fragment header, ESP, ...: ports 0
+        }
     }
     if (type == 0x86DDu) {  // gopacket IPv6.DecodeFromBytes
-        if (l2len < 40) return PARSE_DROP;
+        if (l2len < 40) return PARSE_OK;  // nil IPs, NextHeader 0
         const uint32_t plen = rec_be16<OFF + 4>(w);
         const uint32_t nh = rec_byte<OFF + 6>(w);
-        if (plen == 0) return PARSE_UNSUPPORTED;
         tw[0] = rec_u32<OFF + 8>(w);  tw[1] = rec_u32<OFF + 12>(w);
         tw[2] = rec_u32<OFF + 16>(w); tw[3] = rec_u32<OFF + 20>(w);
         tw[4] = rec_u32<OFF + 24>(w); tw[5] = rec_u32<OFF + 28>(w);
         tw[6] = rec_u32<OFF + 32>(w); tw[7] = rec_u32<OFF + 36>(w);
-        tw[9] = nh;  // parser.go:47: first NextHeader
+        tw[9] = nh | 6u << 24 | 6u << 16;  // parser.go:47: first NextHeader
+        if (nh == 0) return PARSE_UNSUPPORTED;  // hop-by-hop (jumbogram rules): the host packer
+        if (plen == 0) return PARSE_OK;         // "IPv6 length 0, but next header is ..."
         const uint32_t cap = l2len - 40u;
         const uint32_t avail = plen < cap ? plen : cap;
+        if (avail == 0) return PARSE_OK;
         switch (nh) {
-        case 0: case 43: case 44: case 51: case 60: case 135: case 139: case 140: case 253:
-        case 254: case 4: case 41: case 47: case 137:
+        case 4: case 41: case 43: case 47: case 51: case 60: case 137:
             return PARSE_UNSUPPORTED;
         default: break;
         }
         if (nh == 6u || nh == 17u) {
             if (avail < (nh == 6u ? 20u : 8u)) return PARSE_OK;
             if (OFF + 40 + 4 > lim) return PARSE_UNSUPPORTED;  // ports beyond the record
-            // the TCP data-offset byte (record byte 66 + 4*nv) is never inside the record
             const uint32_t sp = rec_be16<OFF + 40>(w), dp = rec_be16<OFF + 42>(w);
             if (nh == 17u && (udp_tunnel_port(sp) || udp_tunnel_port(dp))) return PARSE_UNSUPPORTED;
             set_ports(tw, sp, dp, nh);
+            tw[9] |= 6u << 24 | 6u << 16;
             return PARSE_OK;
         }
         return PARSE_OK;
@@ -196,16 +216,14 @@ __device__ __forceinline__ int parse_record(const uint32_t (&w)[16], uint32_t wi
         const uint32_t a2 = (i >= 3 && i + 2 < 16) ? w[i + 2 < 16 ? i + 2 : 15] : w[i];
         ws[i] = nv == 0 ? w[i] : (nv == 1 ? a1 : a2);
     }
-    const int st = parse_l3(ws, type, wirelen, nv, tw);
-    const uint32_t ver = type == 0x86DDu ? 6u : 4u;  // IP version of both addresses (bytes 38, 39)
-    tw[9] |= ver << 24 | ver << 16;
-    return st;
+    return parse_l3(ws, type, wirelen, nv, tw);
 }
 
 // Branch-free fast path for the dominant record shape: untagged Ethernet II,
-// IPv4 with IHL 5, not a fragment, TCP (data offset inside the datagram) or
-// UDP (no tunnel port).  Returns true and fills tw exactly as parse_record
-// would; false means "use parse_record" (tw is then garbage).
+// IPv4 with IHL 5, not a fragment, TCP (>= 20 bytes) or UDP (no tunnel port).
+// Returns true and fills tw exactly as parse_record would; false means "use
+// parse_record" (tw is then garbage).  The host packer copies exactly the
+// frames of this shape verbatim (gns_frame.cpp fast_shape).
 __device__ __forceinline__ bool parse_fast_ipv4(const uint32_t (&w)[16], uint32_t wirelen, uint32_t (&tw)[10]) {
     constexpr int OFF = 14;
     const uint32_t type = rec_be16<12>(w);
@@ -216,9 +234,8 @@ __device__ __forceinline__ bool parse_fast_ipv4(const uint32_t (&w)[16], uint32_
     const uint32_t proto = rec_byte<OFF + 9>(w);
     const uint32_t frag = rec_be16<OFF + 6>(w);
     const uint32_t avail = (tot < l2len ? tot : l2len) - 20u;  // wraps when < 20: rejected below
-    const uint32_t doff = rec_byte<OFF + 32>(w) >> 4;
     const uint32_t sp = rec_be16<OFF + 20>(w), dp = rec_be16<OFF + 22>(w);
-    const bool tcp = proto == 6u && avail >= 20u && doff >= 5u && doff * 4u <= avail;
+    const bool tcp = proto == 6u && avail >= 20u;
     const bool udp = proto == 17u && avail >= 8u && !udp_tunnel_port(sp) && !udp_tunnel_port(dp);
     const bool ok = type == 0x0800u && ihl == 5u && (frag & 0x3FFFu) == 0 && tot >= 20u && l2len >= 20u &&
                     (tcp || udp);

@@ -6,6 +6,12 @@
 // which parse on the GPU.  Wire length = pcap orig_len = gopacket
 // Metadata().Length (internal/protocol/parser.go:30-33).
 //
+// Each frame becomes one record (gns_frame.cpp frame_record): frames of the
+// device fast-path shape are copied verbatim (first 64 bytes), all others are
+// decoded here, on the whole captured frame, into pre-parsed 0x88B5 records
+// (or a record the device drops, for a frame without an IP layer), so no
+// record leaves the device parser "unsupported".
+//
 // Supported: classic pcap (micro- and nanosecond magic, either byte order) and
 // pcapng (any byte order, several sections and interfaces, if_tsresol /
 // if_tsoffset), linktype Ethernet (1); other linktypes are rejected.
@@ -20,17 +26,17 @@ namespace {
 inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 inline uint16_t bswap16(uint16_t x) { return __builtin_bswap16(x); }
 
+thread_local uint64_t t_counts[3];  // verbatim, escaped, dropped of this thread's last pack
+
 struct Sink {  // record output (the first `cap` packets) and counters
     uint8_t *hdr;
     uint32_t *wirelen;
     int64_t *ts_ns;
     uint64_t cap, written = 0, n = 0;
+    uint64_t kinds[3] = {0, 0, 0};
     void emit(const uint8_t *data, uint32_t incl, uint32_t orig, int64_t ts) {
         if (written < cap && hdr && wirelen) {
-            uint8_t *r = hdr + written * 64;
-            const uint32_t c = incl < 64 ? incl : 64;
-            memcpy(r, data, c);
-            if (c < 64) memset(r + c, 0, 64 - c);
+            kinds[gns::frame_record(data, incl, orig, hdr + written * 64)]++;
             wirelen[written] = orig;
             if (ts_ns) ts_ns[written] = ts;
             written++;
@@ -196,6 +202,7 @@ extern "C" int64_t gns_pack_pcap_ts(const char *path, uint8_t *hdr, uint32_t *wi
     std::vector<char> iobuf(1 << 22);
     setvbuf(f, iobuf.data(), _IOFBF, iobuf.size());
     Sink o{hdr, wirelen, ts_ns, cap};
+    memset(t_counts, 0, sizeof t_counts);
     int rc;
     uint8_t gh[24];
     if (fread(gh, 1, 8, f) != 8) { fclose(f); set_error("%s: short capture file header", path); return GNS_E_ARG; }
@@ -214,6 +221,7 @@ extern "C" int64_t gns_pack_pcap_ts(const char *path, uint8_t *hdr, uint32_t *wi
     }
     fclose(f);
     if (rc != GNS_OK) return rc;
+    memcpy(t_counts, o.kinds, sizeof t_counts);
     if (total) *total = o.n;
     return (int64_t)o.written;
 }
@@ -221,4 +229,10 @@ extern "C" int64_t gns_pack_pcap_ts(const char *path, uint8_t *hdr, uint32_t *wi
 extern "C" int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirelen, uint64_t cap,
                                  uint64_t *total) {
     return gns_pack_pcap_ts(path, hdr, wirelen, nullptr, cap, total);
+}
+
+extern "C" int gns_pack_counts(uint64_t out[3]) {
+    if (!out) { gns::set_error("null argument"); return GNS_E_ARG; }
+    memcpy(out, t_counts, sizeof t_counts);
+    return GNS_OK;
 }

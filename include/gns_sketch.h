@@ -126,8 +126,11 @@ int gns_cm_insert_keys(gns_cm *cm, const uint8_t *keys, uint32_t stride, const u
 int gns_cm_insert_tuples(gns_cm *cm, const gns_tuples *t, uint64_t n, gns_mem where);
 /* fused parse: hdr[n*64] = first 64 bytes of each frame (zero padded),
  * wirelen[n] = capture orig_len (= PacketInfo.Length, parser.go:30-33).
- * Records outside the fast-parse subset are skipped and counted
- * (gns_cm_stats); the host packer (gns_pack_pcap) never emits them. */
+ * Records outside the device parser's subset (gns_device.cuh parse_record:
+ * Ethernet II, <= 2 VLAN tags, IPv4 without options, IPv6 without extension
+ * headers, TCP/UDP, no tunnels) are skipped and counted (gns_cm_stats [2]);
+ * the host packer (gns_pack_pcap) never emits them: it decodes such frames
+ * itself (gns_frame_record). */
 int gns_cm_insert_headers(gns_cm *cm, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
                           gns_mem where);
 int gns_cm_flush(gns_cm *cm);
@@ -266,6 +269,24 @@ int gns_synth_flows(gns_synth *s, uint32_t *n_flows);
  * a negative status; *total = packets in the file. */
 int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirelen, uint64_t cap,
                       uint64_t *total);
+
+/* [0] frames copied verbatim, [1] frames decoded on the host into 0x88B5
+ * records, [2] frames without an IP layer, of the calling thread's last
+ * gns_pack_pcap[_ts] call (records written only) */
+int gns_pack_counts(uint64_t out[3]);
+
+/* One captured frame -> one 64-byte record (what gns_pack_pcap writes for it):
+ * a frame of the device fast-path shape (untagged IPv4, IHL 5, not a fragment,
+ * TCP or non-tunnel UDP, by both caplen and wirelen) is copied verbatim;
+ * any other frame is decoded here the way gopacket v1.1.19 + parser.go:23-67
+ * decode it -- Ethernet/LLC/SNAP, any number of 802.1Q tags, IPv4 options,
+ * IPv6 extension chains, IP-in-IP, GRE, VXLAN, Geneve, GTP-U, MPLS, PPPoE/PPP,
+ * EtherIP; first IPv4 layer else first IPv6, first TCP layer else first UDP --
+ * into a pre-parsed 0x88B5 record, or into a record the device drops when the
+ * frame has no IP layer ("not an IP packet", parser.go:48-49).
+ * Returns 0 verbatim, 1 decoded, 2 no IP layer, < 0 on a bad argument.
+ * Replaces the per-packet gopacket.NewPacket decode of reader.go:35-49. */
+int gns_frame_record(const uint8_t *frame, uint32_t caplen, uint32_t wirelen, uint8_t *rec64);
 
 /* as gns_pack_pcap, plus ts_ns[n] = capture timestamp in ns (PacketInfo.Timestamp,
  * parser.go:30-33; gopacket opens captures with nanosecond precision) */

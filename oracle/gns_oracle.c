@@ -88,31 +88,30 @@ int or_parse_hdr64_len(const uint8_t *r, uint32_t wirelen, or_tuple *t) {
         off += 4;
     }
     uint32_t l2len = wirelen > off ? wirelen - off : 0; /* bytes after the L2 header */
+    /* gopacket v1.1.19 decodeIPv4 / decodeIPv6 / decodeTCP / decodeUDP add the
+     * layer before returning a decode error, with the fields DecodeFromBytes set
+     * before the failing check; parser.go:38-61 reads those fields. */
     if (type == 0x0800) { /* gopacket IPv4.DecodeFromBytes */
         const uint8_t *ip = r + off;
+        if (l2len < 20) return OR_PARSE_OK; /* "Invalid ip4 header": nil IPs, Protocol 0 */
         uint32_t ihl = ip[0] & 15u;
         uint32_t tot = be16(ip + 2);
         if (tot == 0) tot = l2len; /* TSO: Length := len(data) */
-        if (ihl < 5) return OR_PARSE_DROP;      /* decode error -> no IP layer */
-        if (ihl > 5) return OR_PARSE_UNSUPPORTED; /* options: host packer */
-        if (tot < 20 || l2len < 20) return OR_PARSE_DROP;
         t->ipver = 4;
         t->dst_ipver = 4;
         t->proto = ip[9];                        /* parser.go:42 */
         memcpy(t->src, ip + 12, 4);               /* parser.go:40-41; task.go:281-286 */
         memcpy(t->dst, ip + 16, 4);
+        if (tot < 20 || ihl < 5 || ihl * 4 > tot) return OR_PARSE_OK; /* error: no next layer */
+        if (ihl > 5) return OR_PARSE_UNSUPPORTED; /* options: host packer */
         uint32_t frag = be16(ip + 6);
         if ((frag & 0x2000u) || (frag & 0x1FFFu)) return OR_PARSE_OK; /* LayerTypeFragment */
         uint32_t avail = (tot < l2len ? tot : l2len) - 20;
+        if (avail == 0) return OR_PARSE_OK; /* NextDecoder on an empty payload: no layer */
         const uint8_t *l4 = ip + 20;
-        uint32_t l4off = off + 20;
         switch (t->proto) {
-        case 6: /* gopacket TCP.DecodeFromBytes */
+        case 6: /* decodeTCP: ports are read before the data-offset checks */
             if (avail < 20) return OR_PARSE_OK;
-            if (l4off + 12 < 64) {
-                uint32_t doff = l4[12] >> 4;
-                if (doff < 5 || doff * 4 > avail) return OR_PARSE_OK;
-            }
             t->sport = be16(l4);
             t->dport = be16(l4 + 2);
             return OR_PARSE_OK;
@@ -123,7 +122,7 @@ int or_parse_hdr64_len(const uint8_t *r, uint32_t wirelen, or_tuple *t) {
             t->sport = be16(l4);
             t->dport = be16(l4 + 2);
             return OR_PARSE_OK;
-        case 4: case 41: case 47: case 51: case 137:
+        case 0: case 4: case 41: case 43: case 47: case 51: case 60: case 137:
             return OR_PARSE_UNSUPPORTED; /* inner layers could hold IPv4/TCP/UDP */
         default:
             return OR_PARSE_OK; /* ICMP etc.: ports stay 0 (parser.go:62) */
@@ -131,30 +130,27 @@ int or_parse_hdr64_len(const uint8_t *r, uint32_t wirelen, or_tuple *t) {
     }
     if (type == 0x86DD) { /* gopacket IPv6.DecodeFromBytes */
         const uint8_t *ip = r + off;
-        if (l2len < 40) return OR_PARSE_DROP;
+        if (l2len < 40) return OR_PARSE_OK; /* nil IPs, NextHeader 0 */
         uint32_t plen = be16(ip + 4);
         uint32_t nh = ip[6];
-        if (plen == 0) return OR_PARSE_UNSUPPORTED; /* jumbogram / TSO */
         t->ipver = 6;
         t->dst_ipver = 6;
         t->proto = (uint8_t)nh; /* parser.go:47: first NextHeader */
         memcpy(t->src, ip + 8, 16);
         memcpy(t->dst, ip + 24, 16);
+        if (nh == 0) return OR_PARSE_UNSUPPORTED; /* hop-by-hop / jumbogram: host packer */
+        if (plen == 0) return OR_PARSE_OK;        /* "IPv6 length 0, but next header is ..." */
         uint32_t cap = l2len - 40;
         uint32_t avail = plen < cap ? plen : cap;
+        if (avail == 0) return OR_PARSE_OK;
         const uint8_t *l4 = ip + 40;
         uint32_t l4off = off + 40;
         switch (nh) {
-        case 0: case 43: case 44: case 51: case 60: case 135: case 139: case 140: case 253:
-        case 254: case 4: case 41: case 47: case 137:
+        case 4: case 41: case 43: case 47: case 51: case 60: case 137:
             return OR_PARSE_UNSUPPORTED; /* extension headers / encapsulation */
         case 6:
             if (avail < 20) return OR_PARSE_OK;
             if (l4off + 4 > 64) return OR_PARSE_UNSUPPORTED;
-            if (l4off + 12 < 64) {
-                uint32_t doff = l4[12] >> 4;
-                if (doff < 5 || doff * 4 > avail) return OR_PARSE_OK;
-            }
             t->sport = be16(l4);
             t->dport = be16(l4 + 2);
             return OR_PARSE_OK;

@@ -134,8 +134,9 @@ PARSE = [
     ("qinq_ipv4_udp", frame(src=V4S, dst=V4D, sport=7, dport=8, proto=17, vlans=2), 200, OK, V4S, V4D, 7, 8, 17),
     ("ipv4_fragment_ports_zero", frame(src=V4S, dst=V4D, sport=1, dport=2, proto=6, frag=0x2000), 200, OK,
      V4S, V4D, 0, 0, 6),
-    ("ipv4_tcp_bad_doff_ports_zero", frame(src=V4S, dst=V4D, sport=1, dport=2, proto=6, doff=3), 200, OK,
-     V4S, V4D, 0, 0, 6),
+    # decodeTCP adds the layer with the ports it read before the data-offset check fails
+    ("ipv4_tcp_bad_doff_ports_read", frame(src=V4S, dst=V4D, sport=1, dport=2, proto=6, doff=3), 200, OK,
+     V4S, V4D, 1, 2, 6),
     ("ipv4_tcp_truncated_ports_zero", frame(src=V4S, dst=V4D, sport=1, dport=2, proto=6, total=30), 200, OK,
      V4S, V4D, 0, 0, 6),
     ("ipv6_tcp", frame(src=V6S, dst=V6D, sport=40000, dport=80, proto=6, v6=True), 200, OK, V6S, V6D, 40000, 80, 6),
@@ -147,7 +148,26 @@ PARSE = [
      None, None, 0, 0, 0),
     ("ipv4_options_unsupported", frame(src=V4S, dst=V4D, sport=1, dport=2, proto=6, ihl=6), 200, UNSUP,
      None, None, 0, 0, 0),
-    ("ipv4_bad_ihl_dropped", frame(src=V4S, dst=V4D, sport=1, dport=2, proto=6, ihl=4), 200, DROP,
+    # decodeIPv4 adds the layer before returning "Invalid (too small) IP header length":
+    # parser.go reads its IPs and protocol; no transport layer follows
+    # (frame() writes the "ports" at IHL*4 = 16 bytes into the header: over DstIP)
+    ("ipv4_bad_ihl_layer_kept", frame(src=V4S, dst=V4D, sport=1, dport=2, proto=6, ihl=4), 200, OK,
+     V4S, bytes([0, 1, 0, 2]), 0, 0, 6),
+    ("ipv4_total_below_20_layer_kept", frame(src=V4S, dst=V4D, sport=1, dport=2, proto=6, total=12), 200, OK,
+     V4S, V4D, 0, 0, 6),
+    # fewer than 20 bytes after Ethernet: "Invalid ip4 header" before any field is set (nil IPs)
+    ("ipv4_short_data_nil_ips", frame(src=V4S, dst=V4D, sport=1, dport=2, proto=6), 30, OK,
+     bytes(4), bytes(4), 0, 0, 0),
+    ("ipv6_short_data_nil_ips", frame(src=V6S, dst=V6D, sport=1, dport=2, proto=6, v6=True), 40, OK,
+     bytes(4), bytes(4), 0, 0, 0),
+    ("ipv6_length_zero_layer_kept", frame(src=V6S, dst=V6D, sport=1, dport=2, proto=6, v6=True, total=0), 200, OK,
+     V6S, V6D, 0, 0, 6),
+    ("ipv6_fragment_header_ports_zero", frame(src=V6S, dst=V6D, sport=1, dport=2, proto=44, v6=True), 200, OK,
+     V6S, V6D, 0, 0, 44),
+    ("ipv6_no_decoder_ports_zero", frame(src=V6S, dst=V6D, sport=1, dport=2, proto=135, v6=True), 200, OK,
+     V6S, V6D, 0, 0, 135),
+    ("ipv4_gre_unsupported", frame(src=V4S, dst=V4D, sport=0, dport=0, proto=47), 200, UNSUP, None, None, 0, 0, 0),
+    ("ipv4_proto0_hop_by_hop_unsupported", frame(src=V4S, dst=V4D, sport=0, dport=0, proto=0), 200, UNSUP,
      None, None, 0, 0, 0),
     ("vxlan_unsupported", frame(src=V4S, dst=V4D, sport=999, dport=4789, proto=17), 200, UNSUP, None, None, 0, 0, 0),
     ("ipip_unsupported", frame(src=V4S, dst=V4D, sport=0, dport=0, proto=4), 200, UNSUP, None, None, 0, 0, 0),
