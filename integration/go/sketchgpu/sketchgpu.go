@@ -145,6 +145,62 @@ func PackCapture(path string) (hdr []byte, wirelen []uint32, tsNs []int64, err e
 	return hdr[:64*int(r)], wirelen[:r], tsNs[:r], nil
 }
 
+// FrameRecord is the live-capture form of PackCapture (pcap.OpenLive feeding
+// gopacket.NewPacketSource): one captured frame (packet.Data(), CaptureInfo.Length
+// as wireLen) -> the 64-byte record PackCapture writes for it. kind: 0 copied
+// verbatim, 1 decoded on the host into a pre-parsed record, 2 no IP layer (the
+// engine drops the record, as ParsePacketInto returns "not an IP packet").
+func FrameRecord(frame []byte, wireLen uint32, rec []byte) (kind int, err error) {
+	if len(rec) < 64 {
+		return 0, errors.New("record buffer shorter than 64 bytes")
+	}
+	var p *C.uint8_t
+	if len(frame) > 0 {
+		p = (*C.uint8_t)(unsafe.Pointer(&frame[0]))
+	} else {
+		p = (*C.uint8_t)(unsafe.Pointer(&rec[0])) // any non-nil pointer; caplen 0
+	}
+	r := C.gns_frame_record(p, C.uint32_t(len(frame)), C.uint32_t(wireLen), (*C.uint8_t)(unsafe.Pointer(&rec[0])))
+	if r < 0 {
+		return 0, lastErr(r)
+	}
+	return int(r), nil
+}
+
+// Reclaim drops flow-dictionary entries no bucket names any more (inserts also
+// do it on their own when the dictionary fills); call it at a window boundary
+// to take the rebuild off the ingest path.
+func (c *CountMin) Reclaim() error { return lastErr(C.gns_cm_reclaim(c.h)) }
+
+// DictStats: reclaims, dead flows dropped, live flows after the last reclaim,
+// claimed slots, reclaim time (us), batches re-run after an overflow.
+func (c *CountMin) DictStats() (out [6]uint64, err error) {
+	err = lastErr(C.gns_cm_dict_stats(c.h, (*C.uint64_t)(unsafe.Pointer(&out[0]))))
+	return
+}
+
+// Router splits device-resident records by owning GPU (multi-GPU deployment:
+// flow-hash sharding by SrcIP, stable per shard); exchange the runs with an
+// all-to-all (RCCL) and insert each received run in source-rank order.
+type Router struct{ r *C.gns_route }
+
+func NewRouter(nshards uint32, device int) (*Router, error) {
+	var r *C.gns_route
+	if rc := C.gns_route_create(C.uint32_t(nshards), C.int(device), &r); rc != C.GNS_OK {
+		return nil, lastErr(rc)
+	}
+	return &Router{r: r}, nil
+}
+
+// Partition: hdr/wirelen/outHdr/outWirelen are device pointers (n records);
+// counts receives the run length of every shard.
+func (rt *Router) Partition(hdr, wirelen, outHdr, outWirelen unsafe.Pointer, n uint64, counts []uint64) error {
+	return lastErr(C.gns_route_partition(rt.r, (*C.uint8_t)(hdr), (*C.uint32_t)(wirelen), C.uint64_t(n),
+		(*C.uint8_t)(outHdr), (*C.uint32_t)(outWirelen), (*C.uint64_t)(unsafe.Pointer(&counts[0]))))
+}
+
+func (rt *Router) Close() { C.gns_route_destroy(rt.r) }
+
 // Query implements statistic.Sketch (count_min.go:160-174).
 func (c *CountMin) Query(flow []byte) uint64 {
 	if len(flow) != c.keyBytes || len(flow) == 0 {

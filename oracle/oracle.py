@@ -181,6 +181,15 @@ class CountMin:
         self.L.or_cm_export(self.h, _p(C), _p(S), _p(Fc), _p(Fs))
         return C, S, Fc[:, : self.K], Fs[:, : self.K]
 
+    def heavy_arrays(self, which: str):
+        """(flows [n, K] u8, values [n] u32) in the canonical order, without per-entry objects"""
+        w = 0 if which == "count" else 1
+        n = self.L.or_cm_heavy(self.h, w, None, None, 0)
+        flows = np.empty((max(n, 1), max(self.K, 1)), np.uint8)
+        vals = np.empty(max(n, 1), np.uint32)
+        self.L.or_cm_heavy(self.h, w, _p(flows), _p(vals), n)
+        return flows[:n, : self.K], vals[:n]
+
     def heavy(self, which: str):
         w = 0 if which == "count" else 1
         n = self.L.or_cm_heavy(self.h, w, None, None, 0)
