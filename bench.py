@@ -716,7 +716,8 @@ def main():
         win[0] += 1
         syn.fill(hdr, wl, first=(k * world + rank) * n if route else k * n)
 
-    batch = args.batch or n
+    # host input: 16M-packet device batches, so the H2D copy of batch i+1 overlaps batch i
+    batch = args.batch or (min(n, 1 << 24) if args.host_input else n)
     cm = CountMin(args.width, args.depth, 1 << 20, 1000, flow_fields=fields, seeds=row_seeds(args.depth),
                   max_flows=args.max_flows, batch_packets=batch, device=local)
     router = None

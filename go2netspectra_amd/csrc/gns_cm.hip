@@ -2617,9 +2617,12 @@ struct gns_cm {
     bool lds_ordered = false;             // k_lds_order_probe passed: K3 ranks by LDS adds
     bool k3_staged = true;                // K3s (LDS-staged runs) where the geometry allows; GNS_K3_STAGED=0: K3
     uint32_t *h_pin = nullptr;            // pinned host mirror of small counters
-    // staging for host inputs
-    uint8_t *stage = nullptr;
-    size_t stage_bytes = 0;
+    // staging for host inputs: two device buffers; batch i+1's H2D copies run on
+    // cstream while batch i computes on `stream` (events order the reuse)
+    uint8_t *stage[2] = {nullptr, nullptr};
+    size_t stage_bytes[2] = {0, 0};
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_used[2] = {nullptr, nullptr};
     StageTimer timer;
 };
 
@@ -2647,13 +2650,21 @@ struct ViewsQuiesced {
 
 namespace {
 
-int stage_reserve(gns_cm *cm, size_t bytes) {
-    if (cm->stage_bytes >= bytes) return GNS_OK;
-    dfree(cm->stage);
-    cm->stage = nullptr;
-    cm->stage_bytes = 0;
-    GNS_TRY(dalloc(reinterpret_cast<void **>(&cm->stage), bytes));
-    cm->stage_bytes = bytes;
+int stage_reserve(gns_cm *cm, int b, size_t bytes) {
+    if (!cm->cstream) {
+        GNS_HIP(hipStreamCreateWithFlags(&cm->cstream, hipStreamNonBlocking));
+        for (int i = 0; i < 2; i++) {
+            GNS_HIP(hipEventCreateWithFlags(&cm->ev_copied[i], hipEventDisableTiming));
+            GNS_HIP(hipEventCreateWithFlags(&cm->ev_used[i], hipEventDisableTiming));
+        }
+    }
+    if (cm->stage_bytes[b] >= bytes) return GNS_OK;
+    GNS_HIP(hipEventSynchronize(cm->ev_used[b]));  // the batch that read it is done
+    dfree(cm->stage[b]);
+    cm->stage[b] = nullptr;
+    cm->stage_bytes[b] = 0;
+    GNS_TRY(dalloc(reinterpret_cast<void **>(&cm->stage[b]), bytes));
+    cm->stage_bytes[b] = bytes;
     return GNS_OK;
 }
 
@@ -2670,7 +2681,13 @@ int cm_free_all(gns_cm *cm) {
     dfree(cm->keyid); dfree(cm->idx);
     dfree(cm->pend[0]); dfree(cm->pend[1]); dfree(cm->pcnt[0]); dfree(cm->pcnt[1]);
     dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
-    dfree(cm->entries); dfree(cm->entries2); dfree(cm->soff); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats); dfree(cm->stage);
+    dfree(cm->entries); dfree(cm->entries2); dfree(cm->soff); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats);
+    dfree(cm->stage[0]); dfree(cm->stage[1]);
+    for (int i = 0; i < 2; i++) {
+        if (cm->ev_copied[i]) (void)hipEventDestroy(cm->ev_copied[i]);
+        if (cm->ev_used[i]) (void)hipEventDestroy(cm->ev_used[i]);
+    }
+    if (cm->cstream) (void)hipStreamDestroy(cm->cstream);
     dfree(cm->work);
     dfree(cm->hot_ids); dfree(cm->segtot); dfree(cm->hflag); dfree(cm->hhist); dfree(cm->hthr); dfree(cm->hcnt);
     dfree(cm->hsum); dfree(cm->hflag2); dfree(cm->hres); dfree(cm->chk); dfree(cm->hot_tab);
@@ -2975,48 +2992,81 @@ int cm_batch_recover(gns_cm *cm, const InputDesc &d, uint64_t m, bool fresh) {
     return cm_batch_recover<KIND>(cm, advance(d, h), m - h, false);
 }
 
+// Host input: stage batch [off, off+m) into device buffer b on the copy stream,
+// after the batch that last read b has finished; d points into the buffer.
+int stage_host_batch(gns_cm *cm, int b, const InputDesc &in, uint64_t off, uint64_t m, InputDesc &d) {
+    d = in;
+    const void *src[7] = {in.hdr ? (const void *)(in.hdr + off * 16) : nullptr,
+                          in.src16 ? (const void *)(in.src16 + off * 16) : nullptr,
+                          in.dst16 ? (const void *)(in.dst16 + off * 16) : nullptr,
+                          in.sport ? (const void *)(in.sport + off) : nullptr,
+                          in.dport ? (const void *)(in.dport + off) : nullptr,
+                          in.proto ? (const void *)(in.proto + off) : nullptr,
+                          in.keys ? (const void *)(in.keys + off * in.stride) : nullptr};
+    const size_t bytes[7] = {in.hdr ? m * 64 : 0, in.src16 ? m * 16 : 0, in.dst16 ? m * 16 : 0,
+                             in.sport ? m * 2 : 0, in.dport ? m * 2 : 0, in.proto ? m : 0,
+                             in.keys ? m * in.stride : 0};
+    size_t tot = (m * 4 + 15) & ~size_t(15);
+    for (int i = 0; i < 7; i++) tot += (bytes[i] + 15) & ~size_t(15);
+    GNS_TRY(stage_reserve(cm, b, tot));
+    GNS_HIP(hipStreamWaitEvent(cm->cstream, cm->ev_used[b], 0));
+    uint8_t *p = cm->stage[b];
+    const void **dst[7] = {(const void **)&d.hdr, (const void **)&d.src16, (const void **)&d.dst16,
+                           (const void **)&d.sport, (const void **)&d.dport, (const void **)&d.proto,
+                           (const void **)&d.keys};
+    for (int i = 0; i < 7; i++) {
+        if (!bytes[i]) continue;
+        GNS_HIP(hipMemcpyAsync(p, src[i], bytes[i], hipMemcpyHostToDevice, cm->cstream));
+        *dst[i] = p;
+        p += (bytes[i] + 15) & ~size_t(15);
+    }
+    GNS_HIP(hipMemcpyAsync(p, in.sizes + off, m * 4, hipMemcpyHostToDevice, cm->cstream));
+    d.sizes = reinterpret_cast<const uint32_t *>(p);
+    if (d.keys) d.aligned = (d.stride % 4 == 0 && d.stride >= ((cm->K + 3) & ~3u)) ? 1u : 0u;
+    GNS_HIP(hipEventRecord(cm->ev_copied[b], cm->cstream));
+    return GNS_OK;
+}
+
 template <int KIND>
 int cm_insert(gns_cm *cm, InputDesc in, uint64_t n, gns_mem where) {
     GNS_TRY(set_dev(cm));
-    for (uint64_t off = 0, m = 0; off < n; off += m) {
-        m = std::min<uint64_t>(cm->bmax, n - off);
-        // cold start: a small first batch designates the heavy buckets early
-        if (!cm->warm) m = std::min<uint64_t>(m, std::max<uint64_t>(kChunk * 64, cm->bmax / 32));
-        InputDesc d = in;
-        if (where == GNS_MEM_DEVICE) {
-            d = advance(in, off);
-        } else {
-            // stage host arrays into one device buffer (16-byte aligned pieces)
-            const void *src[7] = {in.hdr ? (const void *)(in.hdr + off * 16) : nullptr,
-                                  in.src16 ? (const void *)(in.src16 + off * 16) : nullptr,
-                                  in.dst16 ? (const void *)(in.dst16 + off * 16) : nullptr,
-                                  in.sport ? (const void *)(in.sport + off) : nullptr,
-                                  in.dport ? (const void *)(in.dport + off) : nullptr,
-                                  in.proto ? (const void *)(in.proto + off) : nullptr,
-                                  in.keys ? (const void *)(in.keys + off * in.stride) : nullptr};
-            size_t bytes[7] = {in.hdr ? m * 64 : 0, in.src16 ? m * 16 : 0, in.dst16 ? m * 16 : 0,
-                               in.sport ? m * 2 : 0, in.dport ? m * 2 : 0, in.proto ? m : 0,
-                               in.keys ? m * in.stride : 0};
-            size_t tot = 0;
-            for (int i = 0; i < 7; i++) tot += (bytes[i] + 15) & ~size_t(15);
-            tot += (m * 4 + 15) & ~size_t(15);
-            GNS_TRY(stage_reserve(cm, tot));
-            uint8_t *p = cm->stage;
-            const void **dst[7] = {(const void **)&d.hdr, (const void **)&d.src16, (const void **)&d.dst16,
-                                   (const void **)&d.sport, (const void **)&d.dport, (const void **)&d.proto,
-                                   (const void **)&d.keys};
-            for (int i = 0; i < 7; i++) {
-                if (!bytes[i]) continue;
-                GNS_HIP(hipMemcpyAsync(p, src[i], bytes[i], hipMemcpyHostToDevice, cm->stream));
-                *dst[i] = p;
-                p += (bytes[i] + 15) & ~size_t(15);
-            }
-            GNS_HIP(hipMemcpyAsync(p, in.sizes + off, m * 4, hipMemcpyHostToDevice, cm->stream));
-            d.sizes = reinterpret_cast<const uint32_t *>(p);
-            if (d.keys) d.aligned = (d.stride % 4 == 0 && d.stride >= ((cm->K + 3) & ~3u)) ? 1u : 0u;
+    // batch sizes: a cold handle's small first batch designates the heavy buckets early
+    auto batch_len = [&](uint64_t off, bool warm) {
+        const uint64_t m = std::min<uint64_t>(cm->bmax, n - off);
+        return warm ? m : std::min<uint64_t>(m, std::max<uint64_t>(kChunk * 64, cm->bmax / 32));
+    };
+    if (where == GNS_MEM_DEVICE) {
+        for (uint64_t off = 0, m = 0; off < n; off += m) {
+            m = batch_len(off, cm->warm);
+            GNS_TRY(cm_batch_recover<KIND>(cm, advance(in, off), m, false));
         }
-        GNS_TRY(cm_batch_recover<KIND>(cm, d, m, false));
+        return GNS_OK;
     }
+    // host input, double-buffered: the copies of batch i+1 are queued on the copy
+    // stream before batch i runs (whose resolve rounds may wait on the host)
+    if (n == 0) return GNS_OK;
+    bool warm = cm->warm;
+    uint64_t off = 0, m = batch_len(0, warm);
+    InputDesc d;
+    GNS_TRY(stage_host_batch(cm, 0, in, 0, m, d));
+    for (int b = 0;; b ^= 1) {
+        const uint64_t noff = off + m;
+        const uint64_t nm = noff < n ? batch_len(noff, true) : 0;
+        InputDesc nd;
+        if (nm) GNS_TRY(stage_host_batch(cm, b ^ 1, in, noff, nm, nd));
+        GNS_HIP(hipStreamWaitEvent(cm->stream, cm->ev_copied[b], 0));
+        const int rc = cm_batch_recover<KIND>(cm, d, m, false);
+        GNS_HIP(hipEventRecord(cm->ev_used[b], cm->stream));
+        if (rc != GNS_OK) {
+            (void)hipStreamSynchronize(cm->cstream);  // no copy may outlive the caller's arrays
+            return rc;
+        }
+        if (!nm) break;
+        off = noff; m = nm; d = nd;
+    }
+    // the caller may reuse its host arrays on return: every copy has been consumed
+    // by a batch queued on the handle's stream; wait for the copies themselves
+    GNS_HIP(hipStreamSynchronize(cm->cstream));
     return GNS_OK;
 }
 

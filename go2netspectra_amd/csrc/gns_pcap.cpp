@@ -1,10 +1,15 @@
 // gns_pcap.cpp -- pcap file -> 64-byte header records + wire lengths.
 //
 // Replaces the per-packet gopacket/libpcap loop of pkg/pcap/reader.go:35-49 on
-// the ingest side: one sequential pass over the file, no per-packet heap
-// objects; the records feed gns_cm_insert_headers / gns_ss_insert_headers,
-// which parse on the GPU.  Wire length = pcap orig_len = gopacket
-// Metadata().Length (internal/protocol/parser.go:30-33).
+// the ingest side: the file is mapped read-only and walked once (record
+// boundaries only touch the 16-byte record headers and the first bytes of each
+// frame), no per-packet heap objects; the records feed gns_cm_insert_headers /
+// gns_ss_insert_headers, which parse on the GPU.  Wire length = pcap orig_len =
+// gopacket Metadata().Length (internal/protocol/parser.go:30-33).
+//
+// The walk collects frame descriptors in slabs of 2^17; each slab's records are
+// built by a few host threads (GNS_PACK_THREADS, default min(16, cores)), each
+// thread a contiguous range of the slab, so the output order is the file order.
 //
 // Each frame becomes one record (gns_frame.cpp frame_record): frames of the
 // device fast-path shape are copied verbatim (first 64 bytes), all others are
@@ -15,8 +20,16 @@
 // Supported: classic pcap (micro- and nanosecond magic, either byte order) and
 // pcapng (any byte order, several sections and interfaces, if_tsresol /
 // if_tsoffset), linktype Ethernet (1); other linktypes are rejected.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "gns_common.hpp"
@@ -28,25 +41,83 @@ inline uint16_t bswap16(uint16_t x) { return __builtin_bswap16(x); }
 
 thread_local uint64_t t_counts[3];  // verbatim, escaped, dropped of this thread's last pack
 
+struct Desc {
+    const uint8_t *frame;
+    uint32_t incl, orig;
+    int64_t ts;
+};
+
+int pack_threads() {
+    if (const char *e = getenv("GNS_PACK_THREADS")) {
+        const int v = atoi(e);
+        if (v > 0) return std::min(v, 64);
+    }
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(16u, hc ? hc : 1u));
+}
+
 struct Sink {  // record output (the first `cap` packets) and counters
     uint8_t *hdr;
     uint32_t *wirelen;
     int64_t *ts_ns;
     uint64_t cap, written = 0, n = 0;
     uint64_t kinds[3] = {0, 0, 0};
+    std::vector<Desc> slab;
+    int nthreads = 1;
+    static constexpr size_t kSlab = 1u << 17;
     void emit(const uint8_t *data, uint32_t incl, uint32_t orig, int64_t ts) {
-        if (written < cap && hdr && wirelen) {
-            kinds[gns::frame_record(data, incl, orig, hdr + written * 64)]++;
-            wirelen[written] = orig;
-            if (ts_ns) ts_ns[written] = ts;
-            written++;
-        }
         n++;
+        if (written + slab.size() >= cap || !hdr || !wirelen) return;
+        slab.push_back(Desc{data, incl, orig, ts});
+        if (slab.size() == kSlab) flush();
+    }
+    void flush() {  // build the slab's records (file order), several threads over contiguous ranges
+        const size_t m = slab.size();
+        if (!m) return;
+        const int T = (int)std::min<size_t>((size_t)nthreads, (m + 4095) / 4096);
+        uint64_t part[64][3] = {};
+        auto work = [&](int t) {
+            const size_t i0 = m * t / T, i1 = m * (t + 1) / T;
+            for (size_t i = i0; i < i1; i++) {
+                const Desc &dsc = slab[i];
+                const uint64_t j = written + i;
+                part[t][gns::frame_record(dsc.frame, dsc.incl, dsc.orig, hdr + j * 64)]++;
+                wirelen[j] = dsc.orig;
+                if (ts_ns) ts_ns[j] = dsc.ts;
+            }
+        };
+        if (T <= 1) {
+            work(0);
+        } else {
+            std::vector<std::thread> th;
+            th.reserve(T - 1);
+            for (int t = 1; t < T; t++) th.emplace_back(work, t);
+            work(0);
+            for (auto &x : th) x.join();
+        }
+        for (int t = 0; t < T; t++)
+            for (int k = 0; k < 3; k++) kinds[k] += part[t][k];
+        written += m;
+        slab.clear();
+    }
+};
+
+// The capture as one read-only byte range (mapped; read into memory when the
+// file cannot be mapped), consumed front to back.
+struct Cursor {
+    const uint8_t *p = nullptr;
+    size_t n = 0, off = 0;
+    // the next k bytes, or null at a (truncated) end
+    const uint8_t *take(size_t k) {
+        if (k > n - off) return nullptr;
+        const uint8_t *r = p + off;
+        off += k;
+        return r;
     }
 };
 
 // classic pcap records after the 24-byte file header
-int classic(FILE *f, const char *path, const uint8_t (&gh)[24], uint32_t magic, Sink &o) {
+int classic(Cursor &f, const char *path, const uint8_t *gh, uint32_t magic, Sink &o) {
     using gns::set_error;
     const bool nsec = magic == 0xa1b23c4du || magic == 0x4d3cb2a1u;
     const bool swap = magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u;
@@ -57,20 +128,18 @@ int classic(FILE *f, const char *path, const uint8_t (&gh)[24], uint32_t magic, 
         set_error("%s: linktype %u not supported (Ethernet only)", path, linktype);
         return GNS_E_ARG;
     }
-    std::vector<uint8_t> pkt(1 << 18);
     for (;;) {
-        uint8_t rh[16];
-        const size_t got = fread(rh, 1, 16, f);
-        if (got != 16) break;  // end of file, or a truncated trailer: gopacket stops too
+        const uint8_t *rh = f.take(16);
+        if (!rh) break;  // end of file, or a truncated trailer: gopacket stops too
         uint32_t incl, orig, tsec, tfrac;
         memcpy(&tsec, rh, 4);
         memcpy(&tfrac, rh + 4, 4);
         memcpy(&incl, rh + 8, 4);
         memcpy(&orig, rh + 12, 4);
         if (swap) { incl = bswap32(incl); orig = bswap32(orig); tsec = bswap32(tsec); tfrac = bswap32(tfrac); }
-        if (incl > pkt.size()) pkt.resize(incl);
-        if (fread(pkt.data(), 1, incl, f) != incl) break;
-        o.emit(pkt.data(), incl, orig, (int64_t)(int32_t)tsec * 1000000000ll + (int64_t)tfrac * (nsec ? 1 : 1000));
+        const uint8_t *pkt = f.take(incl);
+        if (!pkt) break;
+        o.emit(pkt, incl, orig, (int64_t)(int32_t)tsec * 1000000000ll + (int64_t)tfrac * (nsec ? 1 : 1000));
     }
     return GNS_OK;
 }
@@ -96,20 +165,21 @@ int64_t ng_ts_ns(const Iface &ifc, uint64_t t) {
     return (int64_t)(sec * 1000000000ull + ns);
 }
 
-int pcapng(FILE *f, const char *path, Sink &o) {
+int pcapng(Cursor &f, const char *path, Sink &o) {
     using gns::set_error;
-    std::vector<uint8_t> body(1 << 16);
     std::vector<Iface> ifs;
     bool swap = false, have_shb = false, first_swap = false;
     for (;;) {
-        uint8_t bh[8];
-        if (fread(bh, 1, 8, f) != 8) break;  // end of file (a partial block header: stop)
+        const uint8_t *bh = f.take(8);
+        if (!bh) break;  // end of file (a partial block header: stop)
         uint32_t type, len;
         memcpy(&type, bh, 4);
         memcpy(&len, bh + 4, 4);
         if (type == 0x0A0D0D0Au) {  // Section Header: its byte-order magic sets the byte order
+            const uint8_t *bp = f.take(4);
+            if (!bp) break;
             uint32_t bom;
-            if (fread(&bom, 1, 4, f) != 4) break;
+            memcpy(&bom, bp, 4);
             if (bom == 0x1A2B3C4Du) swap = false;
             else if (bom == 0x4D3C2B1Au) swap = true;
             else { set_error("%s: pcapng section with bad byte-order magic %08x", path, bom); return GNS_E_ARG; }
@@ -122,10 +192,10 @@ int pcapng(FILE *f, const char *path, Sink &o) {
             }
             if (swap) len = bswap32(len);
             if (len < 28 || (len & 3u)) { set_error("%s: bad pcapng section header length %u", path, len); return GNS_E_ARG; }
-            if (body.size() < len) body.resize(len);
-            if (fread(body.data(), 1, len - 12, f) != len - 12) break;
+            const uint8_t *sb = f.take(len - 12);
+            if (!sb) break;
             uint16_t major;
-            memcpy(&major, body.data(), 2);
+            memcpy(&major, sb, 2);
             if (swap) major = bswap16(major);
             if (major != 1) { set_error("%s: pcapng major version %u not supported", path, major); return GNS_E_ARG; }
             ifs.clear();  // interface ids are per section
@@ -136,9 +206,8 @@ int pcapng(FILE *f, const char *path, Sink &o) {
         if (swap) { type = bswap32(type); len = bswap32(len); }
         if (len < 12 || (len & 3u)) { set_error("%s: bad pcapng block length %u", path, len); return GNS_E_ARG; }
         const uint32_t bl = len - 12;  // body between the header and the trailing length
-        if (body.size() < bl + 4) body.resize(bl + 4);
-        if (fread(body.data(), 1, bl + 4, f) != bl + 4) break;  // truncated block: stop
-        const uint8_t *b = body.data();
+        const uint8_t *b = f.take((size_t)bl + 4);
+        if (!b) break;  // truncated block: stop
         auto u16 = [&](uint32_t off) { uint16_t v; memcpy(&v, b + off, 2); return swap ? bswap16(v) : v; };
         auto u32 = [&](uint32_t off) { uint32_t v; memcpy(&v, b + off, 4); return swap ? bswap32(v) : v; };
         if (type == 1u) {  // Interface Description
@@ -189,6 +258,42 @@ int pcapng(FILE *f, const char *path, Sink &o) {
     return GNS_OK;
 }
 
+// The capture file, mapped read-only (or read whole when it cannot be mapped).
+struct Capture {
+    int fd = -1;
+    void *map = nullptr;
+    size_t size = 0;
+    std::vector<uint8_t> copy;
+    const uint8_t *data() const { return map ? static_cast<const uint8_t *>(map) : copy.data(); }
+    int open_file(const char *path) {
+        fd = ::open(path, O_RDONLY | O_CLOEXEC);
+        if (fd < 0) { gns::set_error("cannot open %s", path); return GNS_E_ARG; }
+        struct stat st;
+        if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) {
+            size = (size_t)st.st_size;
+            map = mmap(nullptr, size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+            if (map == MAP_FAILED) map = nullptr;
+            else (void)madvise(map, size, MADV_SEQUENTIAL);
+        }
+        if (!map) {  // not mappable (a pipe, /dev/stdin ...): read it whole
+            copy.clear();
+            uint8_t buf[1 << 16];
+            for (;;) {
+                const ssize_t r = ::read(fd, buf, sizeof buf);
+                if (r < 0) { gns::set_error("cannot read %s", path); return GNS_E_ARG; }
+                if (r == 0) break;
+                copy.insert(copy.end(), buf, buf + r);
+            }
+            size = copy.size();
+        }
+        return GNS_OK;
+    }
+    ~Capture() {
+        if (map) munmap(map, size);
+        if (fd >= 0) ::close(fd);
+    }
+};
+
 }  // namespace
 
 // ts_ns: capture timestamps in ns (gopacket's pcap handle opens files with
@@ -197,30 +302,30 @@ extern "C" int64_t gns_pack_pcap_ts(const char *path, uint8_t *hdr, uint32_t *wi
                                     uint64_t cap, uint64_t *total) {
     using gns::set_error;
     if (!path) { set_error("null path"); return GNS_E_ARG; }
-    FILE *f = fopen(path, "rb");
-    if (!f) { set_error("cannot open %s", path); return GNS_E_ARG; }
-    std::vector<char> iobuf(1 << 22);
-    setvbuf(f, iobuf.data(), _IOFBF, iobuf.size());
+    Capture cf;
+    GNS_TRY(cf.open_file(path));
+    Cursor f{cf.data(), cf.size, 0};
     Sink o{hdr, wirelen, ts_ns, cap};
+    o.nthreads = pack_threads();
+    if (cap && hdr && wirelen) o.slab.reserve(std::min<uint64_t>(cap, Sink::kSlab));
     memset(t_counts, 0, sizeof t_counts);
     int rc;
-    uint8_t gh[24];
-    if (fread(gh, 1, 8, f) != 8) { fclose(f); set_error("%s: short capture file header", path); return GNS_E_ARG; }
+    const uint8_t *gh = f.take(8);
+    if (!gh) { set_error("%s: short capture file header", path); return GNS_E_ARG; }
     uint32_t magic;
     memcpy(&magic, gh, 4);
     if (magic == 0x0A0D0D0Au) {
-        if (fseek(f, 0, SEEK_SET) != 0) { fclose(f); set_error("%s: cannot rewind", path); return GNS_E_ARG; }
+        f.off = 0;
         rc = pcapng(f, path, o);
     } else if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du || magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u) {
-        if (fread(gh + 8, 1, 16, f) != 16) { fclose(f); set_error("%s: short pcap header", path); return GNS_E_ARG; }
+        if (!f.take(16)) { set_error("%s: short pcap header", path); return GNS_E_ARG; }
         rc = classic(f, path, gh, magic, o);
     } else {
-        fclose(f);
         set_error("%s: neither pcap nor pcapng (magic %08x)", path, magic);
         return GNS_E_ARG;
     }
-    fclose(f);
     if (rc != GNS_OK) return rc;
+    o.flush();
     memcpy(t_counts, o.kinds, sizeof t_counts);
     if (total) *total = o.n;
     return (int64_t)o.written;

@@ -131,19 +131,22 @@ def read_pcap(path: str, limit: Optional[int] = None) -> HeaderBatch:
     """pcap or pcapng -> 64-byte records (C++ packer, one pass, no per-packet objects)."""
     L = _lib.load()
     total = ct.c_uint64(0)
-    if limit is None:
-        r = L.gns_pack_pcap(os.fsencode(path), None, None, 0, ct.byref(total))
+    # one pass when the capacity guess holds (records of >= 76 bytes: a 16-byte record
+    # header and a 60-byte minimum Ethernet frame); otherwise a second pass at the exact
+    # count the first one reported.  The packer writes every byte of a record, so the
+    # buffers need no clearing (untouched capacity costs no memory).
+    cap = limit if limit is not None else max(1, (os.path.getsize(path) - 24) // 76 + 1)
+    while True:
+        hdr = np.empty((cap, 64), np.uint8)
+        wl = np.empty(cap, np.uint32)
+        ts = np.empty(cap, np.int64)
+        r = L.gns_pack_pcap_ts(os.fsencode(path), hdr.ctypes.data, wl.ctypes.data, ts.ctypes.data, cap,
+                               ct.byref(total))
         if r < 0:
             check(int(r))
-        limit = total.value
-    hdr = np.zeros((limit, 64), np.uint8)
-    wl = np.zeros(limit, np.uint32)
-    ts = np.zeros(limit, np.int64)
-    r = L.gns_pack_pcap_ts(os.fsencode(path), hdr.ctypes.data, wl.ctypes.data, ts.ctypes.data, limit,
-                           ct.byref(total))
-    if r < 0:
-        check(int(r))
-    return HeaderBatch(hdr[:r], wl[:r], ts[:r])
+        if limit is not None or total.value <= cap:
+            return HeaderBatch(hdr[:r], wl[:r], ts[:r])
+        cap = total.value
 
 
 def write_pcap(path: str, frames, wirelens=None, snaplen: int = 65536, ts_ns=None) -> None:
