@@ -240,6 +240,10 @@ __device__ __forceinline__ int cm_find_or_claim(const DictDev &D, const uint32_t
 extern "C" __device__ unsigned long long __ockl_wfred_add_u64(unsigned long long);
 extern "C" __device__ unsigned __ockl_wfred_add_u32(unsigned);
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) { return __ockl_wfred_add_u64(v); }
+extern "C" __device__ unsigned __ockl_wfred_max_u32(unsigned);
+#ifndef GNS_K1_HAGG
+#define GNS_K1_HAGG 0
+#endif
 
 // K1 second half for one packet: resolve the first dictionary probe (r4,
 // issued earlier by the caller), publish/hash the row buckets, bin codes,
@@ -360,18 +364,77 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 #endif
             binid = h >= 0 ? a.g.nbins + rr * kHot + (uint32_t)h : rr * a.g.ntiles + (b >> a.g.bin_bits);
         }
-        // heavy bins: one LDS add for the wave's majority bin
+        // heavy bins: one LDS add for the group of lanes sharing one bin -- the bin
+        // of the first lane with a designated bucket (where a wave's repeats are),
+        // else lane 0's
+#if GNS_K1_HAGG
+        const uint64_t hm = __ballot(h >= 0);
+        const uint32_t b0 = hm ? __builtin_amdgcn_readlane(binid, (uint32_t)__ffsll((long long)hm) - 1u)
+                               : __builtin_amdgcn_readfirstlane(binid);
+#else
         const uint32_t b0 = __builtin_amdgcn_readfirstlane(binid);
+#endif
         const uint64_t mm = __ballot(binid == b0 && b0 != 0xFFFFFFFFu);
         const uint32_t cnt = __popcll(mm);
         const bool agg = cnt >= 4;  // wave-uniform
         const bool inmaj = agg && binid == b0;
         const bool leader = inmaj && (uint32_t)__ffsll((long long)mm) - 1 == (threadIdx.x & 63u);
+#if defined(GNS_ABL_NOHIST)  // timing ablations only (results not exact)
+#elif defined(GNS_ABL_NOHOTHIST)
+        if (leader && b0 < a.g.nbins) atomicAdd(&s_hist[b0], cnt);
+        if (binid < a.g.nbins && !inmaj) atomicAdd(&s_hist[binid], 1u);
+#elif defined(GNS_ABL_NOCOLDHIST)
+        if (leader && b0 >= a.g.nbins) atomicAdd(&s_hist[b0], cnt);
+        if (binid != 0xFFFFFFFFu && binid >= a.g.nbins && !inmaj) atomicAdd(&s_hist[binid], 1u);
+#else
         if (leader) atomicAdd(&s_hist[b0], cnt);
         if (binid != 0xFFFFFFFFu && !inmaj) atomicAdd(&s_hist[binid], 1u);
+#endif
         // designated bucket: summary against the batch-entry owners
         uint64_t ownv = 0;
+#if GNS_K1_HAGG
+        // the group's summary is reduced across the wave and added by its leader;
+        // the other lanes with a designated bucket add their own
+        const bool hagg = agg && b0 >= a.g.nbins && b0 != 0xFFFFFFFFu;  // wave-uniform
+        bool fc = false, fsf = false;
         if (h >= 0) {
+            const uint32_t slot = rr * kHot + (uint32_t)h;
+            fc = kid != s_hFc[slot];
+            fsf = kid != s_hFs[slot];
+            if (!fsf) ownv = sz;
+            if (!(hagg && inmaj)) {
+                if (fc) atomicAdd(&s_nfc[slot], 1u);
+                if (fsf) {
+                    atomicAdd(&s_nfs[slot], 1u);
+                    atomicAdd(&s_fs[slot], (unsigned long long)sz);
+                    atomicMax(&s_smax[slot], sz);
+                }
+                if (ownv) atomicAdd(&s_os[slot], (unsigned long long)ownv);
+            }
+        }
+        if (hagg) {
+            const uint32_t gslot = b0 - a.g.nbins;
+            const uint32_t gfc = __popcll(__ballot(inmaj && fc));
+            const uint64_t gf = __ballot(inmaj && fsf);
+            const uint64_t gfs = wave_sum64(inmaj && fsf ? (uint64_t)sz : 0ull);
+            const uint64_t gos = wave_sum64(inmaj ? ownv : 0ull);
+            const uint32_t gmax = gf ? __ockl_wfred_max_u32(inmaj && fsf ? sz : 0u) : 0u;
+            if (leader) {
+                if (gfc) atomicAdd(&s_nfc[gslot], gfc);
+                if (gf) {
+                    atomicAdd(&s_nfs[gslot], (uint32_t)__popcll(gf));
+                    atomicAdd(&s_fs[gslot], (unsigned long long)gfs);
+                    atomicMax(&s_smax[gslot], gmax);
+                }
+                if (gos) atomicAdd(&s_os[gslot], (unsigned long long)gos);
+            }
+        }
+#else
+#ifdef GNS_ABL_NOHOTSUM
+        if (false) {
+#else
+        if (h >= 0) {
+#endif
             const uint32_t slot = rr * kHot + (uint32_t)h;
             if (kid != s_hFc[slot]) atomicAdd(&s_nfc[slot], 1u);
             if (kid != s_hFs[slot]) {
@@ -389,6 +452,7 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
         } else if (ownv) {
             atomicAdd(&s_os[binid - a.g.nbins], (unsigned long long)ownv);
         }
+#endif
     }
 }
 
@@ -403,9 +467,17 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 //   two-stage pipeline,  768 threads: 148 VGPRs, 12 waves per CU      4.47-4.50
 //   plain loop,          768 threads:  92 VGPRs                        4.58-4.59
 //   plain loop,          640 threads (two blocks per CU by LDS)        5.28-5.30
-//   plain loop,         1024 threads:  93 VGPRs, 16 waves per CU      4.01-4.02   <- default
+//   plain loop,         1024 threads:  93 VGPRs, 16 waves per CU      4.01-4.02
+//   plain loop,          512 threads:  95 VGPRs, two blocks per CU    3.52        <- default
+//     (round 3, tools/r03_ab_hagg.sh: same box, base 4.02-4.03; two independent
+//     blocks per CU overlap one block's LDS set-up / flush and barriers with the
+//     other's loop; the summaries' LDS atomics are what a lone block exposes:
+//     timing ablations without them 4.06 -> 3.50, without the cold-bin histogram
+//     adds 3.60, tools/r03_ab_hist.sh.  Reducing each designated bucket's lanes
+//     across the wave before one leader's atomics (GNS_K1_HAGG) measured slower:
+//     4.46 vs 4.02 here, 2.36 vs 2.22 at d=4)
 #ifndef GNS_C5_THREADS
-#define GNS_C5_THREADS 1024
+#define GNS_C5_THREADS 512
 #endif
 constexpr int kC5Threads = GNS_C5_THREADS;
 #ifndef GNS_C5_PIPE
@@ -416,7 +488,7 @@ constexpr bool kC5Pipe = GNS_C5_PIPE != 0;
 // times in a CU, else 1024 (one block of 16 waves: wide or deep sketches, whose
 // histogram and hot-slot tables take more than a quarter of the LDS).
 template <int KIND, int MODE, int KB, int DD, int NT>
-__global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : 1) void k_extract(ExtractArgs a) {
+__global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) void k_extract(ExtractArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xsm[];
     __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
     __shared__ uint8_t s_src[80];
@@ -2763,8 +2835,8 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         ScopedStage st(cm->timer, 0);
         const size_t lds = extract_lds_bytes(g.nbins_all, g.d);
         if (lds > kExLdsSmall) {  // deep / wide sketch: one large block per CU
-            // configs[4] (d=8, 5-tuple): the plain loop at 93 VGPRs, 16 waves per CU (the
-            // two-stage pipeline spilled 66 VGPRs at 1024 threads; see kC5Threads)
+            // configs[4] (d=8, 5-tuple): the plain loop, two 512-thread blocks per CU
+            // (see kC5Threads)
             if (cm->K == 37 && g.d == 8)
                 hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 8, kC5Threads>), dim3(nblk), dim3(kC5Threads), lds, s, a);
             else if (cm->K == 37)
