@@ -240,10 +240,6 @@ __device__ __forceinline__ int cm_find_or_claim(const DictDev &D, const uint32_t
 extern "C" __device__ unsigned long long __ockl_wfred_add_u64(unsigned long long);
 extern "C" __device__ unsigned __ockl_wfred_add_u32(unsigned);
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) { return __ockl_wfred_add_u64(v); }
-extern "C" __device__ unsigned __ockl_wfred_max_u32(unsigned);
-#ifndef GNS_K1_HAGG
-#define GNS_K1_HAGG 0
-#endif
 
 // K1 second half for one packet: resolve the first dictionary probe (r4,
 // issued earlier by the caller), publish/hash the row buckets, bin codes,
@@ -364,16 +360,8 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 #endif
             binid = h >= 0 ? a.g.nbins + rr * kHot + (uint32_t)h : rr * a.g.ntiles + (b >> a.g.bin_bits);
         }
-        // heavy bins: one LDS add for the group of lanes sharing one bin -- the bin
-        // of the first lane with a designated bucket (where a wave's repeats are),
-        // else lane 0's
-#if GNS_K1_HAGG
-        const uint64_t hm = __ballot(h >= 0);
-        const uint32_t b0 = hm ? __builtin_amdgcn_readlane(binid, (uint32_t)__ffsll((long long)hm) - 1u)
-                               : __builtin_amdgcn_readfirstlane(binid);
-#else
+        // heavy bins: one LDS add for the wave's majority bin
         const uint32_t b0 = __builtin_amdgcn_readfirstlane(binid);
-#endif
         const uint64_t mm = __ballot(binid == b0 && b0 != 0xFFFFFFFFu);
         const uint32_t cnt = __popcll(mm);
         const bool agg = cnt >= 4;  // wave-uniform
@@ -392,44 +380,6 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 #endif
         // designated bucket: summary against the batch-entry owners
         uint64_t ownv = 0;
-#if GNS_K1_HAGG
-        // the group's summary is reduced across the wave and added by its leader;
-        // the other lanes with a designated bucket add their own
-        const bool hagg = agg && b0 >= a.g.nbins && b0 != 0xFFFFFFFFu;  // wave-uniform
-        bool fc = false, fsf = false;
-        if (h >= 0) {
-            const uint32_t slot = rr * kHot + (uint32_t)h;
-            fc = kid != s_hFc[slot];
-            fsf = kid != s_hFs[slot];
-            if (!fsf) ownv = sz;
-            if (!(hagg && inmaj)) {
-                if (fc) atomicAdd(&s_nfc[slot], 1u);
-                if (fsf) {
-                    atomicAdd(&s_nfs[slot], 1u);
-                    atomicAdd(&s_fs[slot], (unsigned long long)sz);
-                    atomicMax(&s_smax[slot], sz);
-                }
-                if (ownv) atomicAdd(&s_os[slot], (unsigned long long)ownv);
-            }
-        }
-        if (hagg) {
-            const uint32_t gslot = b0 - a.g.nbins;
-            const uint32_t gfc = __popcll(__ballot(inmaj && fc));
-            const uint64_t gf = __ballot(inmaj && fsf);
-            const uint64_t gfs = wave_sum64(inmaj && fsf ? (uint64_t)sz : 0ull);
-            const uint64_t gos = wave_sum64(inmaj ? ownv : 0ull);
-            const uint32_t gmax = gf ? __ockl_wfred_max_u32(inmaj && fsf ? sz : 0u) : 0u;
-            if (leader) {
-                if (gfc) atomicAdd(&s_nfc[gslot], gfc);
-                if (gf) {
-                    atomicAdd(&s_nfs[gslot], (uint32_t)__popcll(gf));
-                    atomicAdd(&s_fs[gslot], (unsigned long long)gfs);
-                    atomicMax(&s_smax[gslot], gmax);
-                }
-                if (gos) atomicAdd(&s_os[gslot], (unsigned long long)gos);
-            }
-        }
-#else
 #ifdef GNS_ABL_NOHOTSUM
         if (false) {
 #else
@@ -452,7 +402,6 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
         } else if (ownv) {
             atomicAdd(&s_os[binid - a.g.nbins], (unsigned long long)ownv);
         }
-#endif
     }
 }
 
@@ -474,8 +423,10 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 //     other's loop; the summaries' LDS atomics are what a lone block exposes:
 //     timing ablations without them 4.06 -> 3.50, without the cold-bin histogram
 //     adds 3.60, tools/r03_ab_hist.sh.  Reducing each designated bucket's lanes
-//     across the wave before one leader's atomics (GNS_K1_HAGG) measured slower:
-//     4.46 vs 4.02 here, 2.36 vs 2.22 at d=4)
+//     across the wave before one leader's atomics (tried in round 3) measured slower:
+//     4.46 vs 4.02 here, 2.36 vs 2.22 at d=4; so did size sums as two 32-bit halves,
+//     3.86 vs 3.55 here and 3.28 vs 2.37 at d=4, tools/r03_gpu8.sh.  The plain loop
+//     at d=4 with five waves per SIMD (GNS_C2_PIPE=0 GNS_EX_MINW=5): 2.49 vs 2.37)
 #ifndef GNS_C5_THREADS
 #define GNS_C5_THREADS 512
 #endif
@@ -484,6 +435,10 @@ constexpr int kC5Threads = GNS_C5_THREADS;
 #define GNS_C5_PIPE 0
 #endif
 constexpr bool kC5Pipe = GNS_C5_PIPE != 0;
+#ifndef GNS_C2_PIPE
+#define GNS_C2_PIPE 1
+#endif
+constexpr bool kC2Pipe = GNS_C2_PIPE != 0;  // the two-stage pipeline for d != 8 header records
 // NT = threads per block: 256 (four blocks per CU) when the block's LDS fits four
 // times in a CU, else 1024 (one block of 16 waves: wide or deep sketches, whose
 // histogram and hot-slot tables take more than a quarter of the LDS).
@@ -520,7 +475,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
     const bool bw = a.D.bw != 0;
     uint32_t n_ok = 0;
     const K1Lds S{s_tab, s_hist, s_hFc, s_hFs, s_nfc, s_nfs, s_smax, &s_pend, &s_full, s_os, s_fs};
-    if constexpr (KIND == IN_HDR && (DD != 8 || kC5Pipe)) {
+    if constexpr (KIND == IN_HDR && (DD == 8 ? kC5Pipe : kC2Pipe)) {
         // Two-stage software pipeline over the block's packets: iteration k
         // parses packet k+1 and issues its dictionary probe (and the header
         // prefetch of packet k+2), then consumes packet k, whose probe was
