@@ -10,20 +10,32 @@
 // of the sketch layout (task.go:265-300) with every IP field in To16 form, in
 // the flow dictionary of gns_keys.cuh (full key bytes, exact compare).
 //
-// Counters are additive; only StartTime/EndTime depend on order: the
-// timestamps of the flow's first and last packet in stream order.
+// Nothing in task.go:124-149 depends on packet order except which packet is
+// the flow's first and last: PacketCount / ByteCount are sums, StartTime is
+// the timestamp of the packet with the smallest stream index, EndTime that of
+// the largest.  So every path below produces per-flow (count, bytes, min
+// index, max index) contributions, merged with add / min / max, and the
+// timestamps are looked up once per batch from the merged indices.
 //
-//   X1  k_ex_extract   parse -> To16 tuple -> key -> flow id (dictionary)
+//   X1  k_ex_extract   parse -> To16 tuple -> key -> flow id (dictionary);
+//                      packets of the batch's designated heavy flows (the 512
+//                      flows with the most packets so far) are aggregated in
+//                      LDS per block (per-block partials), every other packet
+//                      writes a 64-bit word (flow id | packet index | length)
 //   X1b k_ex_resolve   re-probe packets parked on a same-launch claim
-//   X2  radix sort of X1's 64-bit words (flow id | packet index | wire length)
-//       on the flow id bits (rocPRIM keys-only; stable, so each flow's packets
-//       stay in stream order)
-//   X3  k_ex_runs      over the sorted words: the first / last packet of each
-//                      flow's run writes StartTime (a new flow) / EndTime, the
-//                      counters take one atomic add per run piece
-// A Zipf batch touches a flow in many places; per-block LDS aggregation left
-// the tail flows (about a third of the packets) to global atomics, three per
-// packet; after the sort a flow is one contiguous run.
+//   H   k_ex_hot_reduce  the partials of each designated flow -> flow state
+//   C   k_ex_cscan / k_ex_ccopy  X1 writes the words of the other flows (the tail:
+//                      about 40% of a Zipf(1.1) stream) at the start of its block's
+//                      region; the regions are concatenated densely
+//   X2  radix sort of the tail words on the flow id bits (rocPRIM keys-only)
+//   X3  k_ex_runs      over the sorted words: one add / min / max per run piece
+//   T   k_ex_times     StartTime / EndTime of the flows the batch touched
+//   D   k_exh_*        designate the next batch's heavy flows
+// A Zipf batch touches a flow in many places; per-block LDS aggregation of
+// every flow left the tail flows to global atomics, three per packet; sorting
+// every packet made the sort the largest stage.  Designation sends the heavy
+// flows (whose packets would otherwise be most of the sort) through LDS and
+// sorts only the tail.
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -52,6 +64,32 @@ using ExSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim
                                                 rocprim::default_config, 0>;
 #endif
 constexpr uint32_t kXChunk = 16384;
+
+// Designated heavy flows: kExHot per batch, looked up by flow id in a 4-way
+// table of kExHotTab entries (id << 16 | hot slot; empty = ~0) that X1 keeps in LDS.
+#ifndef GNS_EX_HOT_BITS
+#define GNS_EX_HOT_BITS 9
+#endif
+constexpr uint32_t kExHotBits = GNS_EX_HOT_BITS;
+constexpr uint32_t kExHot = 1u << kExHotBits;
+constexpr uint32_t kExHotTab = 4 * kExHot;
+constexpr uint32_t kExHotMinKey = 6 * 8;  // designate only flows with >= 64 packets
+struct ExHotPart {  // one designated flow in one X1 block
+    uint32_t cnt, minp, maxp, pad;
+    unsigned long long bytes;
+};
+__device__ __forceinline__ uint32_t exh_group(uint32_t id) { return (id * 0x9E3779B1u) >> (32 - kExHotBits); }
+__device__ __forceinline__ int exh_lookup(const unsigned long long *tab, uint32_t id) {
+    const ulonglong2 *g = reinterpret_cast<const ulonglong2 *>(tab + exh_group(id) * 4);
+    const ulonglong2 a = g[0], b = g[1];
+    int h = -1;
+    constexpr unsigned long long m = kExHot - 1u;
+    h = (b.y >> 16) == id ? (int)(b.y & m) : h;
+    h = (b.x >> 16) == id ? (int)(b.x & m) : h;
+    h = (a.y >> 16) == id ? (int)(a.y & m) : h;
+    h = (a.x >> 16) == id ? (int)(a.x & m) : h;
+    return h;
+}
 
 struct ExIn {
     InputDesc in;
@@ -99,7 +137,12 @@ struct ExArgs {
     uint32_t epoch;
     uint64_t *sk;        // X2 sort words: flow id | packet index | wire length (SortWord)
     uint32_t none_key;   // flow field of a packet without a flow id (sorts last)
+    uint32_t hot_key;    // flow field of a designated flow's packet (none_key + 1: not sorted)
     uint32_t sb, ib;     // SortWord field widths: wire length, packet index
+    const unsigned long long *hot_tab;  // [kExHotTab] designated flows
+    ExHotPart *hpart;    // [kExHot][nblk] per-block partials
+    uint32_t *ccnt;      // [nblk] words X1 wrote at the start of its block's region
+    uint32_t nblk;
     uint64_t *pend;
     uint32_t *pend_cnt, *pend_total;
     unsigned long long *stats;  // 0 inserted, 1 dropped, 2 unsupported, 3 dict full
@@ -127,11 +170,39 @@ __device__ __forceinline__ void ex_probe_issue(const DictDev &D, uint32_t slot, 
 // flow id; a flow displaced from its home slot by another committed key is parked
 // (k_ex_resolve walks the rest of the chain in the next launch) instead of
 // stalling the wave on dependent probes; an empty home slot is claimed here.
-__device__ __forceinline__ void ex_consume(const ExArgs &a, uint64_t p, uint64_t beg, bool ok,
-                                           const uint32_t (&kw)[GNS_KWMAX], uint32_t K, uint32_t slot0,
-                                           const uint4 (&r4)[4], uint32_t sz, uint32_t *s_pend,
-                                           uint32_t *s_full, uint32_t *s_claim, uint32_t &n_ok) {
-    if (!ok) return;
+struct ExHotLds {
+    const unsigned long long *tab;
+    uint32_t *cnt, *minp, *maxp;
+    unsigned long long *bytes;
+};
+
+constexpr uint64_t kNoWord = ~0ull;
+// Word of a packet of an undesignated flow, written densely at the start of the
+// block's region (ballot + one LDS add per wave); returns its position in the
+// region (parked packets record it for k_ex_resolve), or ~0u for no word.
+__device__ __forceinline__ uint32_t ex_emit(const ExArgs &a, uint64_t beg, uint64_t w, uint32_t *s_ncold) {
+    const bool has = w != kNoWord;
+    const uint64_t m = __ballot(has);
+    if (!m) return ~0u;
+    const uint32_t lane = __lane_id();
+    const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1u;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(s_ncold, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (has) a.sk[beg + q] = w;
+    return has ? q : ~0u;
+}
+
+// X1 second half for one packet; returns the packet's word (kNoWord: none) and
+// whether it is parked (*park: the dictionary slot to resume from).
+__device__ __forceinline__ uint64_t ex_consume(const ExArgs &a, uint64_t p, uint64_t beg, bool ok,
+                                               const uint32_t (&kw)[GNS_KWMAX], uint32_t K, uint32_t slot0,
+                                               const uint4 (&r4)[4], uint32_t sz, uint32_t *s_full,
+                                               uint32_t *s_claim, uint32_t &n_ok, const ExHotLds &H,
+                                               uint32_t &park) {
+    park = ~0u;
+    if (!ok) return kNoWord;
     uint32_t rec[16];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -144,7 +215,18 @@ __device__ __forceinline__ void ex_consume(const ExArgs &a, uint64_t p, uint64_t
         if ((uint32_t)i < ((K + 3) >> 2)) eq = eq && (rec[1 + i] == kw[i]);
     uint32_t out = slot0;
     int r = DICT_FOUND;
-    if (!eq) {
+    if (eq) {  // a designated flow: aggregated in LDS, no word to sort
+        const int h = exh_lookup(H.tab, out);
+        if (h >= 0) {
+            const uint32_t lp = (uint32_t)(p - beg);
+            atomicAdd(&H.cnt[h], 1u);
+            atomicAdd(&H.bytes[h], (unsigned long long)sz);
+            atomicMin(&H.minp[h], lp);
+            atomicMax(&H.maxp[h], lp);
+            n_ok++;
+            return kNoWord;
+        }
+    } else {
         if (tag == a.epoch) r = DICT_PENDING;                                    // claimed in this launch
         else if (tag != 0) { r = DICT_PENDING; out = (slot0 + 1u) & a.D.mask; }  // displaced
         else r = dict_find_or_claim(a.D, kw, slot0, a.epoch, &out);              // empty: claim
@@ -154,22 +236,38 @@ __device__ __forceinline__ void ex_consume(const ExArgs &a, uint64_t p, uint64_t
         r = DICT_FOUND;
     }
     if (r == DICT_FULL) {
-        a.sk[p] = sort_word(a.none_key, p, sz, a.sb, a.ib);
         atomicAdd(s_full, 1u);
-        return;
+        return kNoWord;
     }
     n_ok++;
-    // a parked packet keeps none_key until k_ex_resolve fills in its flow id
-    a.sk[p] = sort_word(r == DICT_FOUND ? out : a.none_key, p, sz, a.sb, a.ib);
-    if (r != DICT_FOUND) a.pend[beg + atomicAdd(s_pend, 1u)] = (uint64_t)(p - beg) << 32 | out;
+    // a parked packet's word keeps none_key until k_ex_resolve fills in its flow id
+    if (r != DICT_FOUND) park = out;
+    return sort_word(r == DICT_FOUND ? out : a.none_key, p, sz, a.sb, a.ib);
+}
+
+// pend entry: packet (14 bits) | word position (14 bits) in the block | slot to resume from
+static_assert(kXChunk <= (1u << 14), "pend entries hold 14-bit block offsets");
+__device__ __forceinline__ uint64_t pend_entry(uint32_t lp, uint32_t q, uint32_t slot) {
+    return (uint64_t)lp << 50 | (uint64_t)q << 36 | slot;
+}
+__device__ __forceinline__ void ex_emit_park(const ExArgs &a, uint64_t beg, uint64_t p, uint64_t w, uint32_t park,
+                                             uint32_t *s_ncold, uint32_t *s_pend) {
+    const uint32_t q = ex_emit(a, beg, w, s_ncold);
+    if (park != ~0u) a.pend[beg + atomicAdd(s_pend, 1u)] = pend_entry((uint32_t)(p - beg), q, park);
 }
 
 template <int KIND, int MODE>
 __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
     __shared__ uint8_t s_src[80];
-    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_claim, s_abort;
+    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_claim, s_abort, s_ncold;
+    __shared__ __attribute__((aligned(16))) unsigned long long s_htab[kExHotTab];
+    __shared__ unsigned long long s_hby[kExHot];
+    __shared__ uint32_t s_hcnt[kExHot], s_hmin[kExHot], s_hmax[kExHot];
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
-    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; s_claim = 0; s_abort = dict_aborted(a.D); }
+    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; s_claim = 0; s_ncold = 0; s_abort = dict_aborted(a.D); }
+    for (uint32_t i = tid; i < kExHotTab; i += kXThreads) s_htab[i] = a.hot_tab[i];
+    for (uint32_t i = tid; i < kExHot; i += kXThreads) { s_hby[i] = 0; s_hcnt[i] = 0; s_hmin[i] = ~0u; s_hmax[i] = 0; }
+    const ExHotLds H{s_htab, s_hcnt, s_hmin, s_hmax, s_hby};
     __syncthreads();
     if (s_abort) {  // the batch overflowed the dictionary: re-run after the table grows
         if (tid == 0) a.pend_cnt[blk] = 0;
@@ -208,7 +306,6 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
                 int st = parse_record_fast(cw, szq, true, tw);
                 if (st == PARSE_OK) st = ex_key_tw<KIND, MODE>(a.x, K, s_src, q, tw, kwq);
                 if (st != PARSE_OK) {
-                    a.sk[q] = sort_word(a.none_key, q, szq, a.sb, a.ib);
                     atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
                     okq = false;
                 }
@@ -226,7 +323,9 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
             uint32_t kwn[GNS_KWMAX], slotn = 0, szn = 0;
             uint4 r4n[4];
             if (p0 + kXThreads < end) stage_b(p0 + kXThreads + tid, okn, kwn, slotn, r4n, szn);
-            ex_consume(a, p0 + tid, beg, okc, kwc, K, slotc, r4c, szc, &s_pend, &s_full, &s_claim, n_ok);
+            uint32_t park;
+            const uint64_t w = ex_consume(a, p0 + tid, beg, okc, kwc, K, slotc, r4c, szc, &s_full, &s_claim, n_ok, H, park);
+            ex_emit_park(a, beg, p0 + tid, w, park, &s_ncold, &s_pend);
             okc = okn; slotc = slotn; szc = szn;
 #pragma unroll
             for (int i = 0; i < GNS_KWMAX; i++) kwc[i] = kwn[i];
@@ -234,25 +333,39 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
             for (int i = 0; i < 4; i++) r4c[i] = r4n[i];
         }
     } else {
-        for (uint64_t p = beg + tid; p < end; p += kXThreads) {
+        for (uint64_t p0 = beg; p0 < end; p0 += kXThreads) {  // wave-uniform trip count
+            const uint64_t p = p0 + tid;
+            bool ok = p < end;
             uint32_t kw[GNS_KWMAX];
-            const uint32_t sz = a.x.in.sizes[p];
-            const int st = ex_key<KIND, MODE>(a.x, K, s_src, p, kw);
-            if (st != PARSE_OK) {
-                a.sk[p] = sort_word(a.none_key, p, sz, a.sb, a.ib);
-                atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
-                continue;
+            const uint32_t sz = ok ? a.x.in.sizes[p] : 0u;
+            if (ok) {
+                const int st = ex_key<KIND, MODE>(a.x, K, s_src, p, kw);
+                if (st != PARSE_OK) {
+                    atomicAdd(st == PARSE_DROP ? &s_drop : &s_unsup, 1u);
+                    ok = false;
+                }
             }
-            const uint32_t slot0 = mm3_n<GNS_KWMAX>(kw, K, a.D.seed) & a.D.mask;
             uint4 r4[4];
-            ex_probe_issue(a.D, slot0, r4);
-            ex_consume(a, p, beg, true, kw, K, slot0, r4, sz, &s_pend, &s_full, &s_claim, n_ok);
+            uint32_t slot0 = 0;
+            if (ok) {
+                slot0 = mm3_n<GNS_KWMAX>(kw, K, a.D.seed) & a.D.mask;
+                ex_probe_issue(a.D, slot0, r4);
+            }
+            uint32_t park;
+            const uint64_t w = ex_consume(a, p, beg, ok, kw, K, slot0, r4, sz, &s_full, &s_claim, n_ok, H, park);
+            ex_emit_park(a, beg, p, w, park, &s_ncold, &s_pend);
         }
     }
     atomicAdd(&s_ok, n_ok);
     __syncthreads();
+    for (uint32_t i = tid; i < kExHot; i += kXThreads) {
+        ExHotPart hp;
+        hp.cnt = s_hcnt[i]; hp.minp = s_hmin[i]; hp.maxp = s_hmax[i]; hp.pad = 0; hp.bytes = s_hby[i];
+        a.hpart[(uint64_t)i * a.nblk + blk] = hp;
+    }
     if (tid == 0) {
         a.pend_cnt[blk] = s_pend;
+        a.ccnt[blk] = s_ncold;
         if (s_pend) atomicAdd(a.pend_total, s_pend);
         if (s_ok) atomicAdd(&a.stats[0], (unsigned long long)s_ok);
         if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
@@ -291,17 +404,18 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
     const uint64_t beg = (uint64_t)blk * kXChunk;
     for (uint32_t i = tid; i < cnt; i += kXThreads) {
         const uint64_t v = r.pend_in[beg + i];
-        const uint64_t p = beg + (v >> 32);
+        const uint64_t p = beg + (v >> 50);
         uint32_t kw[GNS_KWMAX];
         (void)ex_key<KIND, MODE>(a.x, a.kp.K, s_src, p, kw);
         uint32_t out;
-        const int res = dict_find_or_claim(a.D, kw, (uint32_t)v, a.epoch, &out);
+        const int res = dict_find_or_claim(a.D, kw, (uint32_t)(v & 0xFFFFFFFFFull), a.epoch, &out);
         if (res == DICT_CLAIMED) atomicAdd(&s_claim, 1u);
         if (res == DICT_FOUND || res == DICT_CLAIMED) {  // X1 wrote the word with none_key: fill in the flow field
             const uint32_t sh = a.ib + a.sb;
-            a.sk[p] = (a.sk[p] & ((1ull << sh) - 1ull)) | (uint64_t)out << sh;
+            const uint64_t wq = beg + ((v >> 36) & 0x3FFFu);
+            a.sk[wq] = (a.sk[wq] & ((1ull << sh) - 1ull)) | (uint64_t)out << sh;
         }
-        else if (res == DICT_PENDING) r.pend_out[beg + atomicAdd(&s_cnt, 1u)] = (v & 0xFFFFFFFF00000000ull) | out;
+        else if (res == DICT_PENDING) r.pend_out[beg + atomicAdd(&s_cnt, 1u)] = (v & ~0xFFFFFFFFFull) | out;
         else atomicAdd(&s_full, 1u);
     }
     __syncthreads();
@@ -313,29 +427,96 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
     }
 }
 
-// per-flow state, one array per field (first/last: global packet index, ~0 / 0 = none
-// yet; start/end: StartTime / EndTime in ns).  (One 64-byte record per flow measured
-// slower: the two counter atomics of a run then hit one line.)
+// per-flow state, one array per field: first = stream index of the first packet (~0: none
+// yet), last = stream index of the last packet + 1 (0: none), start / end = StartTime /
+// EndTime in ns.  (One 64-byte record per flow measured slower: a run's two counter
+// atomics then hit one line.)
 struct FlowState {
     unsigned long long *pkts, *bytes, *first, *last;
     long long *start, *end;
 };
 
-// X3 over the sorted pairs: thread t takes kRunItems consecutive packets.  A
-// packet that starts its flow's run (the flow's first packet of the batch, the
-// sort being stable) sets StartTime when the flow is new; the one that ends it
-// sets EndTime; counters go to the flow with one atomic add per (thread, run)
-// piece, or per wave when the whole wave lies inside one run (a heavy flow).
-// task.go:154-212 per packet: PacketCount++, ByteCount += Length, StartTime on
-// the first packet, EndTime on every packet.
+extern "C" __device__ unsigned long long __ockl_wfred_add_u64(unsigned long long);
+extern "C" __device__ unsigned __ockl_wfred_min_u32(unsigned);
+extern "C" __device__ unsigned __ockl_wfred_max_u32(unsigned);
+extern "C" __device__ unsigned __ockl_wfred_add_u32(unsigned);
+extern "C" __device__ unsigned __ockl_wfscan_add_u32(unsigned, bool);
+
+// H: the per-block partials of each designated flow -> its flow state (one
+// workgroup per hot slot; the only writer of these flows until X3, whose
+// atomics then merge the flow's parked packets).
+__global__ __launch_bounds__(256) void k_ex_hot_reduce(const ExHotPart *hpart, uint32_t nblk, const uint32_t *hot_ids,
+                                                       uint64_t pkt_base, FlowState f) {
+    __shared__ unsigned long long s_by[4];
+    __shared__ uint32_t s_c[4], s_mn[4], s_mx[4];
+    const uint32_t slot = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t id = hot_ids[slot];
+    if (id == GNS_ID_NONE) return;  // block-uniform
+    uint32_t c = 0, mn = ~0u, mx = 0;
+    unsigned long long by = 0;
+    for (uint32_t b = tid; b < nblk; b += 256) {
+        const ExHotPart hp = hpart[(uint64_t)slot * nblk + b];
+        if (hp.cnt) {
+            c += hp.cnt; by += hp.bytes;
+            mn = min(mn, b * kXChunk + hp.minp);
+            mx = max(mx, b * kXChunk + hp.maxp);
+        }
+    }
+    c = __ockl_wfred_add_u32(c); by = __ockl_wfred_add_u64(by);
+    mn = __ockl_wfred_min_u32(mn); mx = __ockl_wfred_max_u32(mx);
+    if (lane == 0) { s_c[wave] = c; s_by[wave] = by; s_mn[wave] = mn; s_mx[wave] = mx; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 4; w++) { c += s_c[w]; by += s_by[w]; mn = min(mn, s_mn[w]); mx = max(mx, s_mx[w]); }
+        if (c) {
+            f.pkts[id] += c;
+            f.bytes[id] += by;
+            f.last[id] = max(f.last[id], pkt_base + mx + 1);
+            f.first[id] = min(f.first[id], pkt_base + mn);
+        }
+    }
+}
+
+// C: the tail words of every X1 block region, densely: an exclusive scan of
+// the regions' word counts (one workgroup), then a coalesced copy per region.
+__global__ __launch_bounds__(1024) void k_ex_cscan(const uint32_t *ccnt, uint32_t nblk, uint32_t *coff,
+                                                   uint32_t *total) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t per = (nblk + 1023) / 1024, b0 = tid * per;
+    uint32_t sum = 0;
+    for (uint32_t i = 0; i < per; i++) sum += b0 + i < nblk ? ccnt[b0 + i] : 0u;
+    const uint32_t inc = __ockl_wfscan_add_u32(sum, true);
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < wave; w++) base += s_w[w];
+    uint32_t run = base + inc - sum;
+    for (uint32_t i = 0; i < per; i++)
+        if (b0 + i < nblk) { coff[b0 + i] = run; run += ccnt[b0 + i]; }
+    if (tid == 1023) *total = base + inc;
+}
+__global__ __launch_bounds__(256) void k_ex_ccopy(const uint64_t *in, const uint32_t *ccnt, const uint32_t *coff,
+                                                  uint64_t *out) {
+    const uint32_t blk = blockIdx.x, cnt = ccnt[blk];
+    const uint64_t src = (uint64_t)blk * kXChunk, dst = coff[blk];
+    for (uint32_t i = threadIdx.x; i < cnt; i += 256) out[dst + i] = in[src + i];
+}
+
+// X3 over the sorted words of the tail flows: thread t takes kRunItems
+// consecutive words.  Each piece of a flow's run (a run split over threads
+// gives one piece per thread) adds its packets and bytes and merges its
+// smallest / largest stream index into first / last (task.go:135-148:
+// PacketCount++, ByteCount += Length, StartTime from the first packet,
+// EndTime from the last); a wave lying inside one run (a heavy tail flow)
+// merges once per wave.  first is merged only for flows without a packet
+// before this batch (first >= pkt_base).
 #ifndef GNS_RUN_ITEMS
 #define GNS_RUN_ITEMS 16
 #endif
 constexpr int kRunItems = GNS_RUN_ITEMS;
-extern "C" __device__ unsigned long long __ockl_wfred_add_u64(unsigned long long);
 __global__ __launch_bounds__(256) void k_ex_runs(const uint64_t *sk, uint64_t n, uint32_t none_key, uint32_t sb,
-                                                 uint32_t ib, const uint32_t *sizes, const int64_t *ts,
-                                                 uint64_t pkt_base, FlowState f) {
+                                                 uint32_t ib, const uint32_t *sizes, uint64_t pkt_base, FlowState f) {
     const uint64_t b0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kRunItems;
     if (b0 >= n) return;  // whole waves past the end exit together (n is rounded per wave below)
     const uint32_t ks = sb + ib, esc = (1u << sb) - 1u;
@@ -355,70 +536,137 @@ __global__ __launch_bounds__(256) void k_ex_runs(const uint64_t *sk, uint64_t n,
         if ((uint32_t)v[j] == esc && k[j] != none_key) v[j] = (v[j] & ~0xFFFFFFFFull) | sizes[v[j] >> 32];
     const uint32_t prev = b0 > 0 ? (uint32_t)(sk[b0 - 1] >> ks) : ~0u;
     const uint32_t next = b0 + kRunItems < n ? (uint32_t)(sk[b0 + kRunItems] >> ks) : ~0u;
-    // a heavy flow covering the whole wave: one add per wave
+    // a heavy flow covering the whole wave: one merge per wave
     const uint32_t kw = __builtin_amdgcn_readfirstlane(k[0]);
     const bool inner = k[0] == kw && k[kRunItems - 1] == kw && prev == kw && next == kw;
     const uint32_t lane = threadIdx.x & 63u;
     if (__ballot(true) == ~0ull && __ballot(inner) == ~0ull) {
         uint64_t by = 0;
+        uint32_t mn = ~0u, mx = 0;
 #pragma unroll
-        for (int j = 0; j < kRunItems; j++) by += (uint32_t)v[j];
+        for (int j = 0; j < kRunItems; j++) {
+            by += (uint32_t)v[j];
+            mn = min(mn, (uint32_t)(v[j] >> 32));
+            mx = max(mx, (uint32_t)(v[j] >> 32));
+        }
         const unsigned long long tot = __ockl_wfred_add_u64(by);
+        mn = __ockl_wfred_min_u32(mn);
+        mx = __ockl_wfred_max_u32(mx);
         if (lane == 0 && kw != none_key) {
             atomicAdd(&f.pkts[kw], (unsigned long long)(64 * kRunItems));
             atomicAdd(&f.bytes[kw], tot);
+            atomicMax(&f.last[kw], pkt_base + mx + 1);
+            if (f.first[kw] >= pkt_base) atomicMin(&f.first[kw], pkt_base + mn);
         }
         return;
     }
-    // pieces of runs (a run split over threads adds once per piece); the run's first
-    // packet sets StartTime when the flow is new, its last one EndTime.  The loads
-    // the walk depends on (a head's stored first-packet index, the timestamps of
-    // run heads and tails) are issued up front, all in flight together, instead of
-    // one dependent round trip per run.
+    // the first-packet word of each piece's flow, loaded up front (all in flight together)
     unsigned long long fst[kRunItems];
-    long long tsv[kRunItems];
 #pragma unroll
     for (int j = 0; j < kRunItems; j++) {
-        const bool valid = k[j] != none_key;
-        const bool head = valid && (j == 0 ? prev : k[j - 1]) != k[j];
-        const bool tail = valid && (j == kRunItems - 1 ? next : k[j + 1]) != k[j];
-        fst[j] = head ? f.first[k[j]] : 0ull;
-        tsv[j] = head || tail ? ts[(uint32_t)(v[j] >> 32)] : 0ll;
+        const bool pstart = k[j] != none_key && (j == 0 || k[j - 1] != k[j]);
+        fst[j] = pstart ? f.first[k[j]] : 0ull;
     }
-    uint32_t cur = k[0], cnt = 0, pl = 0;
-    unsigned long long by = 0;
-    long long tl_ts = 0;
+    uint32_t cur = k[0], cnt = 0, mn = ~0u, mx = 0;
+    unsigned long long by = 0, cf = fst[0];
+    auto merge = [&]() {
+        atomicAdd(&f.pkts[cur], (unsigned long long)cnt);
+        atomicAdd(&f.bytes[cur], by);
+        atomicMax(&f.last[cur], pkt_base + mx + 1);
+        if (cf >= pkt_base) atomicMin(&f.first[cur], pkt_base + mn);
+    };
 #pragma unroll
     for (int j = 0; j < kRunItems; j++) {
         const uint32_t id = k[j];
-        if (id == none_key) break;  // invalid packets sort last
+        if (id == none_key) break;  // padding past n sorts last
         const uint32_t pidx = (uint32_t)(v[j] >> 32);
-        if (id != cur) {  // a piece ends at its run's last packet
-            atomicAdd(&f.pkts[cur], (unsigned long long)cnt);
-            atomicAdd(&f.bytes[cur], by);
-            f.last[cur] = pkt_base + pl;
-            f.end[cur] = tl_ts;
-            cur = id; cnt = 0; by = 0;
-        }
-        if (fst[j] == ~0ull) {  // head of a new flow's run: its first packet ever (batches in order)
-            f.first[id] = pkt_base + pidx;
-            f.start[id] = tsv[j];
+        if (id != cur) {
+            merge();
+            cur = id; cnt = 0; by = 0; mn = ~0u; mx = 0; cf = fst[j];
         }
         cnt++;
         by += (uint32_t)v[j];
-        pl = pidx;
-        tl_ts = tsv[j];
+        mn = min(mn, pidx);
+        mx = max(mx, pidx);
     }
-    if (cnt) {
-        atomicAdd(&f.pkts[cur], (unsigned long long)cnt);
-        atomicAdd(&f.bytes[cur], by);
-        // the piece ends this thread's range: it is the run's end unless the run goes on
-        const bool run_ends = (cur == k[kRunItems - 1] ? next != cur : true);
-        if (run_ends) {
-            f.last[cur] = pkt_base + pl;
-            f.end[cur] = tl_ts;
-        }
+    if (cnt) merge();
+}
+
+// T: StartTime / EndTime from the merged stream indices of the flows this batch
+// touched (task.go:137,141-142).
+__global__ __launch_bounds__(256) void k_ex_times(FlowState f, uint64_t slots, uint64_t pkt_base, uint64_t n,
+                                                  const int64_t *ts) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= slots) return;
+    const unsigned long long l = f.last[s], fs = f.first[s];
+    if (l > pkt_base && l <= pkt_base + n) f.end[s] = ts[l - 1 - pkt_base];
+    if (fs >= pkt_base && fs < pkt_base + n) f.start[s] = ts[fs - pkt_base];
+}
+
+// D: designate the next batch's heavy flows: the flows in the largest 1/8-octave
+// bands of the packet count that together hold at most kExHot flows.
+__device__ __forceinline__ uint32_t exh_key(unsigned long long p) {
+    if (p < 8) return 0;
+    const uint32_t lz = 63u - (uint32_t)__clzll((long long)p);
+    return lz * 8u + (uint32_t)((p >> (lz - 3)) & 7u);
+}
+__global__ __launch_bounds__(256) void k_exh_hist(const unsigned long long *pkts, uint64_t slots, uint32_t *hist) {
+    __shared__ uint32_t h[512];
+    for (uint32_t i = threadIdx.x; i < 512; i += 256) h[i] = 0;
+    __syncthreads();
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * 256) {
+        const uint32_t k = exh_key(pkts[s]);
+        if (k >= kExHotMinKey) atomicAdd(&h[k], 1u);
     }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 512; i += 256)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+// threshold = the smallest key whose suffix count (flows with a key >= it) is <= kExHot
+__global__ __launch_bounds__(512) void k_exh_pick(const uint32_t *hist, uint32_t *thr) {
+    __shared__ uint32_t s_w[8];
+    __shared__ uint32_t s_t;
+    const uint32_t k = threadIdx.x, lane = k & 63u, wave = k >> 6;
+    if (k == 0) s_t = 512;
+    // suffix sums: scan over the reversed keys
+    const uint32_t r = 511u - k;  // thread k holds key r
+    const uint32_t v = r >= kExHotMinKey ? hist[r] : 0u;
+    const uint32_t inc = __ockl_wfscan_add_u32(v, true);
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < wave; w++) base += s_w[w];
+    const uint32_t suffix = base + inc;  // flows with a key >= r
+    if (r >= kExHotMinKey && suffix <= kExHot) atomicMin(&s_t, r);
+    __syncthreads();
+    if (k == 0) *thr = s_t;
+}
+__global__ __launch_bounds__(256) void k_exh_collect(const unsigned long long *pkts, uint64_t slots,
+                                                     const uint32_t *thr, uint32_t *cnt, uint32_t *hot_ids) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= slots) return;
+    const uint32_t k = exh_key(pkts[s]);
+    if (k >= *thr && k >= kExHotMinKey) {
+        const uint32_t q = atomicAdd(cnt, 1u);
+        if (q < kExHot) hot_ids[q] = (uint32_t)s;
+    }
+}
+// the lookup table: a flow whose 4-entry group is full is simply not designated
+__global__ __launch_bounds__(256) void k_exh_table(uint32_t *hot_ids, unsigned long long *hot_tab) {
+    __shared__ unsigned long long t[kExHotTab];
+    for (uint32_t i = threadIdx.x; i < kExHotTab; i += 256) t[i] = ~0ull;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kExHot; i += 256) {
+        const uint32_t id = hot_ids[i];
+        if (id == GNS_ID_NONE) continue;
+        const uint32_t g = exh_group(id) * 4;
+        bool in = false;
+        for (uint32_t e = 0; e < 4 && !in; e++)
+            in = atomicCAS(&t[g + e], ~0ull, (unsigned long long)id << 16 | i) == ~0ull;
+        if (!in) hot_ids[i] = GNS_ID_NONE;
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < kExHotTab; j += 256) hot_tab[j] = t[j];
 }
 
 __global__ __launch_bounds__(256) void k_ex_query(const uint8_t *flows, uint32_t stride, uint64_t n, uint32_t K,
@@ -496,7 +744,12 @@ struct gns_ex {
     uint64_t pkt = 0, batches = 0;
     uint64_t bmax = 0;
     uint32_t nblk_max = 0;
-    uint64_t *sk[2] = {nullptr, nullptr};    // X2 sort words (in, out)
+    uint64_t *sk[2] = {nullptr, nullptr};    // X1 words / compacted tail words; sorted back into sk[0]
+    uint32_t *hot_ids = nullptr;             // [kExHot] designated flows (GNS_ID_NONE: unused slot)
+    unsigned long long *hot_tab = nullptr;   // [kExHotTab] their lookup table
+    ExHotPart *hpart = nullptr;              // [kExHot][nblk_max]
+    uint32_t *hctl = nullptr;                // [0..511] count histogram, [512] threshold, [513] count, [514] tail words
+    uint32_t *ccnt = nullptr, *coff = nullptr;  // [nblk_max] X1 region word counts, their exclusive scan
     void *sort_tmp = nullptr;                // rocPRIM radix sort scratch
     size_t sort_tmp_bytes = 0;
     uint32_t key_bits = 0;                   // flow field bits: flow ids < slots, invalid = slots
@@ -524,10 +777,18 @@ void ex_free_all(gns_ex *ex) {
     dfree(ex->f.start); dfree(ex->f.end); dfree(ex->pend[0]); dfree(ex->pend[1]);
     dfree(ex->pcnt[0]); dfree(ex->pcnt[1]); dfree(ex->ptotal); dfree(ex->stats); dfree(ex->stage);
     dfree(ex->sk[0]); dfree(ex->sk[1]); dfree(ex->sort_tmp);
+    dfree(ex->hot_ids); dfree(ex->hot_tab); dfree(ex->hpart); dfree(ex->hctl); dfree(ex->ccnt); dfree(ex->coff);
     dfree(ex->dctl); dfree(ex->stats_bak); ex->dsc.free_all();
     if (ex->h_pin) (void)hipHostFree(ex->h_pin);
     ex->timer.destroy();
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
+}
+
+// no designated flows (after create / reset, and after a table growth renumbers the flows)
+int ex_hot_clear(gns_ex *ex) {
+    GNS_HIP(hipMemsetAsync(ex->hot_ids, 0xFF, kExHot * 4, ex->stream));
+    GNS_HIP(hipMemsetAsync(ex->hot_tab, 0xFF, kExHotTab * 8, ex->stream));
+    return GNS_OK;
 }
 
 int ex_clear(gns_ex *ex) {
@@ -535,6 +796,7 @@ int ex_clear(gns_ex *ex) {
     GNS_HIP(hipMemsetAsync(ex->dctl, 0, 16, ex->stream));
     ex->claimed = 0;
     GNS_HIP(hipMemsetAsync(ex->stats + 3, 0, sizeof(unsigned long long), ex->stream));  // dict-full word
+    GNS_TRY(ex_hot_clear(ex));
     hipLaunchKernelGGL(k_ex_init, dim3((unsigned)((ex->slots + 255) / 256)), dim3(256), 0, ex->stream, ex->f,
                        ex->slots);
     GNS_HIP(hipGetLastError());
@@ -552,7 +814,8 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     if (++ex->epoch == 0) ex->epoch = 1;
     ExArgs x{};
     x.x = xin; x.n = n; x.kp = ex->kp; x.D = ex->D; x.epoch = ex->epoch;
-    x.sk = ex->sk[0]; x.none_key = (uint32_t)ex->slots; x.sb = ex->sb; x.ib = ex->ib;
+    x.sk = ex->sk[0]; x.none_key = (uint32_t)ex->slots; x.hot_key = x.none_key + 1; x.sb = ex->sb; x.ib = ex->ib;
+    x.hot_tab = ex->hot_tab; x.hpart = ex->hpart; x.ccnt = ex->ccnt; x.nblk = nblk;
     x.pend = ex->pend[0]; x.pend_cnt = ex->pcnt[0]; x.pend_total = ex->ptotal; x.stats = ex->stats;
     {
         ScopedStage st(ex->timer, 0);
@@ -585,17 +848,43 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
         cur ^= 1;
     }
     const uint32_t none_key = (uint32_t)ex->slots;
-    {
+    const uint32_t ks = ex->sb + ex->ib;
+    uint64_t ncold = 0;
+    {   // designated flows' partials -> flow state; the tail's words, densely
+        ScopedStage st(ex->timer, 4);
+        hipLaunchKernelGGL(k_ex_hot_reduce, dim3(kExHot), dim3(256), 0, s, ex->hpart, nblk, ex->hot_ids, ex->pkt, ex->f);
+        hipLaunchKernelGGL(k_ex_cscan, dim3(1), dim3(1024), 0, s, ex->ccnt, nblk, ex->coff, ex->hctl + 514);
+        hipLaunchKernelGGL(k_ex_ccopy, dim3(nblk), dim3(256), 0, s, ex->sk[0], ex->ccnt, ex->coff, ex->sk[1]);
+        GNS_HIP(hipGetLastError());
+        GNS_HIP(hipMemcpyAsync(ex->h_pin + 8, ex->hctl + 514, 4, hipMemcpyDeviceToHost, s));
+    }
+    GNS_HIP(hipStreamSynchronize(s));  // the tail size sizes the sort
+    ncold = ex->h_pin[8];
+    if (ncold) {
         ScopedStage st(ex->timer, 2);
         size_t tb = ex->sort_tmp_bytes;
-        GNS_HIP(rocprim::radix_sort_keys<ExSortConfig>(ex->sort_tmp, tb, ex->sk[0], ex->sk[1], (size_t)n, ex->sb + ex->ib,
-                                         ex->sb + ex->ib + ex->key_bits, s));
+        GNS_HIP(rocprim::radix_sort_keys<ExSortConfig>(ex->sort_tmp, tb, ex->sk[1], ex->sk[0], (size_t)ncold, ks,
+                                                       ks + ex->key_bits, s));
     }
-    {
+    if (ncold) {
         ScopedStage st(ex->timer, 3);
-        const uint64_t nt = (n + kRunItems - 1) / kRunItems;
-        hipLaunchKernelGGL(k_ex_runs, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, ex->sk[1], n, none_key,
-                           ex->sb, ex->ib, xin.in.sizes, xin.ts, ex->pkt, ex->f);
+        const uint64_t nt = (ncold + kRunItems - 1) / kRunItems;
+        hipLaunchKernelGGL(k_ex_runs, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, ex->sk[0], ncold, none_key,
+                           ex->sb, ex->ib, xin.in.sizes, ex->pkt, ex->f);
+        GNS_HIP(hipGetLastError());
+    }
+    {   // timestamps of the touched flows; the next batch's designated flows
+        ScopedStage st(ex->timer, 4);
+        const unsigned sg = (unsigned)((ex->slots + 255) / 256);
+        hipLaunchKernelGGL(k_ex_times, dim3(sg), dim3(256), 0, s, ex->f, ex->slots, ex->pkt, n, xin.ts);
+        GNS_HIP(hipMemsetAsync(ex->hctl, 0, 514 * 4, s));
+        GNS_HIP(hipMemsetAsync(ex->hot_ids, 0xFF, kExHot * 4, s));
+        hipLaunchKernelGGL(k_exh_hist, dim3(std::min<unsigned>(sg, 2048)), dim3(256), 0, s, ex->f.pkts, ex->slots,
+                           ex->hctl);
+        hipLaunchKernelGGL(k_exh_pick, dim3(1), dim3(512), 0, s, ex->hctl, ex->hctl + 512);
+        hipLaunchKernelGGL(k_exh_collect, dim3(sg), dim3(256), 0, s, ex->f.pkts, ex->slots, ex->hctl + 512,
+                           ex->hctl + 513, ex->hot_ids);
+        hipLaunchKernelGGL(k_exh_table, dim3(1), dim3(256), 0, s, ex->hot_ids, ex->hot_tab);
         GNS_HIP(hipGetLastError());
     }
     ex->pkt += n;
@@ -666,6 +955,7 @@ int ex_grow(gns_ex *ex) {
     ex->D.cap = (uint32_t)(new_slots - new_slots / 4);
     ex->claimed = live;
     GNS_TRY(ex_geometry(ex));
+    GNS_TRY(ex_hot_clear(ex));  // designated ids name old slots
     ex->n_grow++;
     ex->grow_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return GNS_OK;
@@ -827,7 +1117,10 @@ int gns_ex_create(const gns_ex_params *p, gns_ex **out) {
             (rc = dalloc_t(&ex->pend[0], ex->bmax)) || (rc = dalloc_t(&ex->pend[1], ex->bmax)) ||
             (rc = dalloc_t(&ex->pcnt[0], ex->nblk_max)) || (rc = dalloc_t(&ex->pcnt[1], ex->nblk_max)) ||
             (rc = dalloc_t(&ex->ptotal, 2)) || (rc = dalloc_t(&ex->stats, 8)) ||
-            (rc = dalloc_t(&ex->sk[0], ex->bmax)) || (rc = dalloc_t(&ex->sk[1], ex->bmax)))
+            (rc = dalloc_t(&ex->sk[0], ex->bmax)) || (rc = dalloc_t(&ex->sk[1], ex->bmax)) ||
+            (rc = dalloc_t(&ex->hot_ids, kExHot)) || (rc = dalloc_t(&ex->hot_tab, kExHotTab)) ||
+            (rc = dalloc_t(&ex->hpart, (uint64_t)kExHot * ex->nblk_max)) || (rc = dalloc_t(&ex->hctl, 516)) ||
+            (rc = dalloc_t(&ex->ccnt, ex->nblk_max)) || (rc = dalloc_t(&ex->coff, ex->nblk_max)))
             break;
         if ((rc = ex_geometry(ex)) != GNS_OK) break;
         if ((rc = dalloc_t(&ex->dctl, 4)) != GNS_OK || (rc = dalloc_t(&ex->stats_bak, 3)) != GNS_OK) break;
