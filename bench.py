@@ -273,13 +273,14 @@ def bench_exact(args, torch, dist, world, rank, local):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     stages = task.agg.stage_times()
-    kern = {k: v for k, v in stages.items() if k in ("extract", "resolve", "sort", "walk")}
+    kern = {k: v for k, v in stages.items() if k in ("extract", "resolve", "partition", "aggregate")}
     dom = max(kern, key=lambda k: kern[k][0])
     dom_ms, dom_launches = kern[dom]
     avg_ms = dom_ms / max(dom_launches, 1)
-    # algorithmic bytes per packet: X1 reads the 68-B record; the sort reads and writes each
-    # 8-B word of the tail once at the least (an out-of-place sort); the walk reads the word
-    bpp = {"extract": BYTES_PER_PKT, "sort": 16, "walk": 8, "resolve": BYTES_PER_PKT}[dom]
+    # algorithmic bytes per packet: X1 reads the 68-B record; the partition reads and writes
+    # each 8-B word of the tail; the aggregation reads it (per packet of the whole batch these
+    # are upper bounds: only the tail has words)
+    bpp = {"extract": BYTES_PER_PKT, "partition": 16, "aggregate": 8, "resolve": BYTES_PER_PKT}[dom]
     achieved = bpp * (n * args.steps / max(dom_launches, 1)) / (avg_ms * 1e-3) / 1e9
     line = {
         "metric": "Mpackets/s exact per-5-tuple aggregation (device-resident)",

@@ -24,45 +24,30 @@
 //                      writes a 64-bit word (flow id | packet index | length)
 //   X1b k_ex_resolve   re-probe packets parked on a same-launch claim
 //   H   k_ex_hot_reduce  the partials of each designated flow -> flow state
-//   C   k_ex_cscan / k_ex_ccopy  X1 writes the words of the other flows (the tail:
-//                      about 40% of a Zipf(1.1) stream) at the start of its block's
-//                      region; the regions are concatenated densely
-//   X2  radix sort of the tail words on the flow id bits (rocPRIM keys-only)
-//   X3  k_ex_runs      over the sorted words: one add / min / max per run piece
+//   P   k_ex_phist / k_ex_pscan_* / k_ex_pscatter / k_ex_pagg  X1 writes the
+//                      words of the other flows (the tail: about 35% of a
+//                      Zipf(1.1) stream) at the start of its block's region; they
+//                      are partitioned into 512 bins of consecutive flow ids and
+//                      each bin is aggregated in an LDS hash table by one
+//                      workgroup, which merges each of its flows once
 //   T   k_ex_times     StartTime / EndTime of the flows the batch touched
 //   D   k_exh_*        designate the next batch's heavy flows
 // A Zipf batch touches a flow in many places; per-block LDS aggregation of
 // every flow left the tail flows to global atomics, three per packet; sorting
-// every packet made the sort the largest stage.  Designation sends the heavy
-// flows (whose packets would otherwise be most of the sort) through LDS and
-// sorts only the tail.
+// every packet (rocPRIM radix sort of 100M words) made the sort the largest
+// stage.  Designation sends the heavy flows through LDS; the tail needs no
+// order at all (add / min / max), only locality by flow id.
 #include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <vector>
 
 #include "gns_common.hpp"
-#include <rocprim/rocprim.hpp>
 
 namespace gns {
 
 constexpr int kXThreads = 256;
 
-// X2 needs a stable sort (a flow's packets stay in stream order); rocPRIM's merge-sort
-// path for batches up to 1M words did not keep equal flow fields in input order for a
-// keys-only sort over a bit range, so every batch above one block takes the Onesweep
-// LSD passes (stable by construction).
-#ifdef GNS_EX_RADIX_BITS
-using ExSortConfig = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<GNS_EX_SORT_BLOCK, GNS_EX_SORT_ITEMS>,
-                                        rocprim::kernel_config<GNS_EX_SORT_BLOCK, GNS_EX_SORT_ITEMS>,
-                                        GNS_EX_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>,
-    0>;
-#else
-using ExSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                rocprim::default_config, 0>;
-#endif
 constexpr uint32_t kXChunk = 16384;
 
 // Designated heavy flows: kExHot per batch, looked up by flow id in a 4-way
@@ -477,119 +462,211 @@ __global__ __launch_bounds__(256) void k_ex_hot_reduce(const ExHotPart *hpart, u
     }
 }
 
-// C: the tail words of every X1 block region, densely: an exclusive scan of
-// the regions' word counts (one workgroup), then a coalesced copy per region.
-__global__ __launch_bounds__(1024) void k_ex_cscan(const uint32_t *ccnt, uint32_t nblk, uint32_t *coff,
-                                                   uint32_t *total) {
-    __shared__ uint32_t s_w[16];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t per = (nblk + 1023) / 1024, b0 = tid * per;
+// P: the tail words go to kPBins bins of consecutive flow ids (order-free: no
+// stable partition is needed, the merge is add / min / max), then one
+// workgroup per bin aggregates its words in an LDS hash table and merges each
+// flow once.  Every flow id lies in exactly one bin, so the merge needs no
+// global atomics.
+//   P1 k_ex_phist     per X1 region: bin histogram  -> ph[blk][bin]
+//   P2 k_ex_pscan_*   exclusive offsets of every (region, bin) in bin-major order
+//   P3 k_ex_pscatter  per region, sub-passes of kPSub words staged bin by bin in
+//                     LDS and copied out as runs
+//   P4 k_ex_pagg      per bin: LDS hash (flow id -> count, bytes, min / max
+//                     index), flushed into the flow state
+constexpr uint32_t kPBinBits = 9;
+constexpr uint32_t kPBins = 1u << kPBinBits;
+constexpr uint32_t kPGroup = 64;  // regions per P2 group
+
+__global__ __launch_bounds__(256) void k_ex_phist(const uint64_t *in, const uint32_t *ccnt, uint32_t ks,
+                                                  uint32_t pshift, uint32_t *ph) {
+    __shared__ uint32_t h[kPBins];
+    const uint32_t blk = blockIdx.x, n = ccnt[blk];
+    for (uint32_t i = threadIdx.x; i < kPBins; i += 256) h[i] = 0;
+    __syncthreads();
+    const uint64_t *w = in + (uint64_t)blk * kXChunk;
+    for (uint32_t i = threadIdx.x; i < n; i += 256) atomicAdd(&h[(uint32_t)(w[i] >> ks) >> pshift], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kPBins; i += 256) ph[(uint64_t)blk * kPBins + i] = h[i];
+}
+// per group of kPGroup regions: bin sums
+__global__ __launch_bounds__(kPBins) void k_ex_pscan_a(const uint32_t *ph, uint32_t nblk, uint32_t *gs) {
+    const uint32_t g = blockIdx.x, b = threadIdx.x;
+    const uint32_t r1 = min(nblk, (g + 1) * kPGroup);
     uint32_t sum = 0;
-    for (uint32_t i = 0; i < per; i++) sum += b0 + i < nblk ? ccnt[b0 + i] : 0u;
-    const uint32_t inc = __ockl_wfscan_add_u32(sum, true);
+    for (uint32_t r = g * kPGroup; r < r1; r++) sum += ph[(uint64_t)r * kPBins + b];
+    gs[(uint64_t)g * kPBins + b] = sum;
+}
+// one workgroup: per bin, exclusive offsets of the groups; bin starts (pb[kPBins] = total)
+__global__ __launch_bounds__(kPBins) void k_ex_pscan_b(uint32_t *gs, uint32_t ng, uint32_t *pb) {
+    __shared__ uint32_t s_w[kPBins / 64];
+    const uint32_t b = threadIdx.x, lane = b & 63u, wave = b >> 6;
+    uint32_t run = 0;
+    for (uint32_t g = 0; g < ng; g++) {
+        const uint32_t x = gs[(uint64_t)g * kPBins + b];
+        gs[(uint64_t)g * kPBins + b] = run;
+        run += x;
+    }
+    const uint32_t inc = __ockl_wfscan_add_u32(run, true);
     if (lane == 63) s_w[wave] = inc;
     __syncthreads();
     uint32_t base = 0;
     for (uint32_t w = 0; w < wave; w++) base += s_w[w];
-    uint32_t run = base + inc - sum;
-    for (uint32_t i = 0; i < per; i++)
-        if (b0 + i < nblk) { coff[b0 + i] = run; run += ccnt[b0 + i]; }
-    if (tid == 1023) *total = base + inc;
+    const uint32_t start = base + inc - run;
+    pb[b] = start;
+    if (b == kPBins - 1) pb[kPBins] = base + inc;
+    for (uint32_t g = 0; g < ng; g++) gs[(uint64_t)g * kPBins + b] += start;
 }
-__global__ __launch_bounds__(256) void k_ex_ccopy(const uint64_t *in, const uint32_t *ccnt, const uint32_t *coff,
-                                                  uint64_t *out) {
-    const uint32_t blk = blockIdx.x, cnt = ccnt[blk];
-    const uint64_t src = (uint64_t)blk * kXChunk, dst = coff[blk];
-    for (uint32_t i = threadIdx.x; i < cnt; i += 256) out[dst + i] = in[src + i];
+// per group: the regions' offsets, in place over the histogram
+__global__ __launch_bounds__(kPBins) void k_ex_pscan_c(uint32_t *ph, uint32_t nblk, const uint32_t *gs) {
+    const uint32_t g = blockIdx.x, b = threadIdx.x;
+    const uint32_t r1 = min(nblk, (g + 1) * kPGroup);
+    uint32_t run = gs[(uint64_t)g * kPBins + b];
+    for (uint32_t r = g * kPGroup; r < r1; r++) {
+        const uint32_t x = ph[(uint64_t)r * kPBins + b];
+        ph[(uint64_t)r * kPBins + b] = run;
+        run += x;
+    }
 }
 
-// X3 over the sorted words of the tail flows: thread t takes kRunItems
-// consecutive words.  Each piece of a flow's run (a run split over threads
-// gives one piece per thread) adds its packets and bytes and merges its
-// smallest / largest stream index into first / last (task.go:135-148:
-// PacketCount++, ByteCount += Length, StartTime from the first packet,
-// EndTime from the last); a wave lying inside one run (a heavy tail flow)
-// merges once per wave.  first is merged only for flows without a packet
-// before this batch (first >= pkt_base).
-#ifndef GNS_RUN_ITEMS
-#define GNS_RUN_ITEMS 16
-#endif
-constexpr int kRunItems = GNS_RUN_ITEMS;
-__global__ __launch_bounds__(256) void k_ex_runs(const uint64_t *sk, uint64_t n, uint32_t none_key, uint32_t sb,
-                                                 uint32_t ib, const uint32_t *sizes, uint64_t pkt_base, FlowState f) {
-    const uint64_t b0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kRunItems;
-    if (b0 >= n) return;  // whole waves past the end exit together (n is rounded per wave below)
+constexpr uint32_t kPSub = 4096;  // words per P3 sub-pass
+constexpr uint32_t kPItems = kPSub / kPBins;
+__global__ __launch_bounds__(kPBins) void k_ex_pscatter(const uint64_t *in, const uint32_t *ccnt, const uint32_t *po,
+                                                        uint32_t ks, uint32_t pshift, uint64_t *out) {
+    __shared__ uint64_t stage[kPSub];
+    __shared__ uint16_t sbin[kPSub];
+    __shared__ uint32_t cnt[kPBins], lstart[kPBins], goff[kPBins], dummy[kPBins], s_w[kPBins / 64];
+    const uint32_t blk = blockIdx.x, n = ccnt[blk], tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    if (n == 0) return;  // block-uniform
+    const uint64_t *src = in + (uint64_t)blk * kXChunk;
+    goff[tid] = po[(uint64_t)blk * kPBins + tid];
+    cnt[tid] = 0;
+    __syncthreads();
+    for (uint32_t sp = 0; sp < n; sp += kPSub) {
+        uint64_t w[kPItems];
+        uint32_t bn[kPItems], rk[kPItems];
+#pragma unroll
+        for (uint32_t j = 0; j < kPItems; j++) {
+            const uint32_t i = sp + j * kPBins + tid;
+            w[j] = i < n ? src[i] : 0ull;
+            bn[j] = i < n ? (uint32_t)(w[j] >> ks) >> pshift : 0xFFFFu;
+        }
+        // ranks (any order): every lane adds, a lane without a word adds 0 to its own word
+#pragma unroll
+        for (uint32_t j = 0; j < kPItems; j++) {
+            uint32_t *ad = bn[j] != 0xFFFFu ? &cnt[bn[j]] : &dummy[tid];
+            rk[j] = atomicAdd(ad, bn[j] != 0xFFFFu ? 1u : 0u);
+        }
+        __syncthreads();
+        const uint32_t c = cnt[tid];
+        const uint32_t inc = __ockl_wfscan_add_u32(c, true);
+        if (lane == 63) s_w[wave] = inc;
+        __syncthreads();
+        uint32_t base = 0;
+        for (uint32_t v = 0; v < wave; v++) base += s_w[v];
+        lstart[tid] = base + inc - c;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kPItems; j++)
+            if (bn[j] != 0xFFFFu) {
+                const uint32_t pos = lstart[bn[j]] + rk[j];
+                stage[pos] = w[j];
+                sbin[pos] = (uint16_t)bn[j];
+            }
+        __syncthreads();
+        const uint32_t m = min(kPSub, n - sp);
+        for (uint32_t i = tid; i < m; i += kPBins) {
+            const uint32_t bb = sbin[i];
+            out[goff[bb] + (i - lstart[bb])] = stage[i];
+        }
+        __syncthreads();
+        goff[tid] += c;
+        cnt[tid] = 0;
+        __syncthreads();
+    }
+}
+
+// P4: one workgroup per bin.  Words in chunks of kAggChunk; before a chunk the
+// table is flushed if it could overflow (a bin with more distinct flows than
+// the table merges in several rounds; each flow's partial results add up).
+constexpr uint32_t kAggThreads = 1024;
+constexpr uint32_t kAggItems = 2;
+constexpr uint32_t kAggChunk = kAggThreads * kAggItems;
+constexpr uint32_t kAggCap = 6144;  // 24 B per entry
+static_assert(kAggCap > kAggChunk, "a chunk fits an empty table");
+__device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t *mn, uint32_t *mx,
+                                           unsigned long long *by, uint64_t pkt_base, FlowState f) {
+    for (uint32_t e = threadIdx.x; e < kAggCap; e += kAggThreads) {
+        const uint32_t id = key[e];
+        if (id == GNS_ID_NONE) continue;
+        f.pkts[id] += cn[e];
+        f.bytes[id] += by[e];
+        f.last[id] = max(f.last[id], pkt_base + mx[e] + 1);
+        const unsigned long long fs = f.first[id];
+        if (fs >= pkt_base) f.first[id] = min(fs, pkt_base + mn[e]);  // no packet before this batch
+        key[e] = GNS_ID_NONE; cn[e] = 0; mn[e] = ~0u; mx[e] = 0; by[e] = 0;
+    }
+}
+__global__ __launch_bounds__(kAggThreads) void k_ex_pagg(const uint64_t *in, const uint32_t *pb, uint32_t sb,
+                                                         uint32_t ib, const uint32_t *sizes, uint64_t pkt_base,
+                                                         FlowState f) {
+    __shared__ uint32_t key[kAggCap], cn[kAggCap], mn[kAggCap], mx[kAggCap];
+    __shared__ unsigned long long by[kAggCap];
+    __shared__ uint32_t s_n;
+    const uint32_t bin = blockIdx.x, tid = threadIdx.x;
+    const uint32_t beg = pb[bin], end = pb[bin + 1];
+    if (beg == end) return;  // block-uniform
+    for (uint32_t e = tid; e < kAggCap; e += kAggThreads) { key[e] = GNS_ID_NONE; cn[e] = 0; mn[e] = ~0u; mx[e] = 0; by[e] = 0; }
+    if (tid == 0) s_n = 0;
     const uint32_t ks = sb + ib, esc = (1u << sb) - 1u;
     const uint64_t imask = (1ull << ib) - 1ull;
-    uint32_t k[kRunItems];
-    uint64_t v[kRunItems];  // packet index << 32 | wire length
+    uint64_t wn[kAggItems];
 #pragma unroll
-    for (int j = 0; j < kRunItems; j++) {
-        const uint64_t i = b0 + j;
-        const uint64_t w = i < n ? sk[i] : (uint64_t)none_key << ks;
-        k[j] = (uint32_t)(w >> ks);
-        const uint32_t s = (uint32_t)w & esc;
-        v[j] = ((w >> sb) & imask) << 32 | s;
+    for (uint32_t j = 0; j < kAggItems; j++) {
+        const uint32_t i = beg + j * kAggThreads + tid;
+        wn[j] = i < end ? in[i] : ~0ull;
     }
-#pragma unroll
-    for (int j = 0; j < kRunItems; j++)  // lengths too large for the word's field (rare)
-        if ((uint32_t)v[j] == esc && k[j] != none_key) v[j] = (v[j] & ~0xFFFFFFFFull) | sizes[v[j] >> 32];
-    const uint32_t prev = b0 > 0 ? (uint32_t)(sk[b0 - 1] >> ks) : ~0u;
-    const uint32_t next = b0 + kRunItems < n ? (uint32_t)(sk[b0 + kRunItems] >> ks) : ~0u;
-    // a heavy flow covering the whole wave: one merge per wave
-    const uint32_t kw = __builtin_amdgcn_readfirstlane(k[0]);
-    const bool inner = k[0] == kw && k[kRunItems - 1] == kw && prev == kw && next == kw;
-    const uint32_t lane = threadIdx.x & 63u;
-    if (__ballot(true) == ~0ull && __ballot(inner) == ~0ull) {
-        uint64_t by = 0;
-        uint32_t mn = ~0u, mx = 0;
-#pragma unroll
-        for (int j = 0; j < kRunItems; j++) {
-            by += (uint32_t)v[j];
-            mn = min(mn, (uint32_t)(v[j] >> 32));
-            mx = max(mx, (uint32_t)(v[j] >> 32));
+    __syncthreads();
+    for (uint32_t c0 = beg; c0 < end; c0 += kAggChunk) {
+        if (s_n > kAggCap - kAggChunk) {  // block-uniform (read after the barrier)
+            __syncthreads();
+            pagg_flush(key, cn, mn, mx, by, pkt_base, f);
+            if (tid == 0) s_n = 0;
+            __syncthreads();
         }
-        const unsigned long long tot = __ockl_wfred_add_u64(by);
-        mn = __ockl_wfred_min_u32(mn);
-        mx = __ockl_wfred_max_u32(mx);
-        if (lane == 0 && kw != none_key) {
-            atomicAdd(&f.pkts[kw], (unsigned long long)(64 * kRunItems));
-            atomicAdd(&f.bytes[kw], tot);
-            atomicMax(&f.last[kw], pkt_base + mx + 1);
-            if (f.first[kw] >= pkt_base) atomicMin(&f.first[kw], pkt_base + mn);
-        }
-        return;
-    }
-    // the first-packet word of each piece's flow, loaded up front (all in flight together)
-    unsigned long long fst[kRunItems];
+        uint64_t w[kAggItems];
 #pragma unroll
-    for (int j = 0; j < kRunItems; j++) {
-        const bool pstart = k[j] != none_key && (j == 0 || k[j - 1] != k[j]);
-        fst[j] = pstart ? f.first[k[j]] : 0ull;
-    }
-    uint32_t cur = k[0], cnt = 0, mn = ~0u, mx = 0;
-    unsigned long long by = 0, cf = fst[0];
-    auto merge = [&]() {
-        atomicAdd(&f.pkts[cur], (unsigned long long)cnt);
-        atomicAdd(&f.bytes[cur], by);
-        atomicMax(&f.last[cur], pkt_base + mx + 1);
-        if (cf >= pkt_base) atomicMin(&f.first[cur], pkt_base + mn);
-    };
-#pragma unroll
-    for (int j = 0; j < kRunItems; j++) {
-        const uint32_t id = k[j];
-        if (id == none_key) break;  // padding past n sorts last
-        const uint32_t pidx = (uint32_t)(v[j] >> 32);
-        if (id != cur) {
-            merge();
-            cur = id; cnt = 0; by = 0; mn = ~0u; mx = 0; cf = fst[j];
+        for (uint32_t j = 0; j < kAggItems; j++) {
+            w[j] = wn[j];
+            const uint32_t i = c0 + kAggChunk + j * kAggThreads + tid;
+            wn[j] = i < end ? in[i] : ~0ull;
         }
-        cnt++;
-        by += (uint32_t)v[j];
-        mn = min(mn, pidx);
-        mx = max(mx, pidx);
+#pragma unroll
+        for (uint32_t j = 0; j < kAggItems; j++) {
+            if (w[j] == ~0ull) continue;
+            const uint32_t id = (uint32_t)(w[j] >> ks);
+            const uint32_t idx = (uint32_t)((w[j] >> sb) & imask);
+            uint32_t sz = (uint32_t)w[j] & esc;
+            if (sz == esc) sz = sizes[idx];  // lengths too large for the word's field (rare)
+            uint32_t h = (uint32_t)(((uint64_t)(id * 0x9E3779B1u) * kAggCap) >> 32);
+            for (;;) {
+                const uint32_t k = key[h];
+                if (k == id) break;
+                if (k == GNS_ID_NONE) {
+                    const uint32_t old = atomicCAS(&key[h], GNS_ID_NONE, id);
+                    if (old == GNS_ID_NONE) { atomicAdd(&s_n, 1u); break; }
+                    if (old == id) break;
+                }
+                h = h + 1 == kAggCap ? 0u : h + 1;
+            }
+            atomicAdd(&cn[h], 1u);
+            atomicAdd(&by[h], (unsigned long long)sz);
+            atomicMin(&mn[h], idx);
+            atomicMax(&mx[h], idx);
+        }
+        __syncthreads();
     }
-    if (cnt) merge();
+    __syncthreads();
+    pagg_flush(key, cn, mn, mx, by, pkt_base, f);
 }
 
 // T: StartTime / EndTime from the merged stream indices of the flows this batch
@@ -744,14 +821,13 @@ struct gns_ex {
     uint64_t pkt = 0, batches = 0;
     uint64_t bmax = 0;
     uint32_t nblk_max = 0;
-    uint64_t *sk[2] = {nullptr, nullptr};    // X1 words / compacted tail words; sorted back into sk[0]
+    uint64_t *sk[2] = {nullptr, nullptr};    // X1 block regions of tail words; the same partitioned by bin
     uint32_t *hot_ids = nullptr;             // [kExHot] designated flows (GNS_ID_NONE: unused slot)
     unsigned long long *hot_tab = nullptr;   // [kExHotTab] their lookup table
     ExHotPart *hpart = nullptr;              // [kExHot][nblk_max]
     uint32_t *hctl = nullptr;                // [0..511] count histogram, [512] threshold, [513] count, [514] tail words
-    uint32_t *ccnt = nullptr, *coff = nullptr;  // [nblk_max] X1 region word counts, their exclusive scan
-    void *sort_tmp = nullptr;                // rocPRIM radix sort scratch
-    size_t sort_tmp_bytes = 0;
+    uint32_t *ccnt = nullptr;                // [nblk_max] X1 region word counts
+    uint32_t *ph = nullptr, *pgs = nullptr, *pb = nullptr;  // P histograms / offsets, group sums, bin starts
     uint32_t key_bits = 0;                   // flow field bits: flow ids < slots, invalid = slots
     uint32_t sb = 0, ib = 0;                 // sort word: wire length bits, packet index bits
     uint64_t *pend[2] = {nullptr, nullptr};
@@ -776,8 +852,8 @@ void ex_free_all(gns_ex *ex) {
     dfree(ex->D.rec); dfree(ex->f.pkts); dfree(ex->f.bytes); dfree(ex->f.first); dfree(ex->f.last);
     dfree(ex->f.start); dfree(ex->f.end); dfree(ex->pend[0]); dfree(ex->pend[1]);
     dfree(ex->pcnt[0]); dfree(ex->pcnt[1]); dfree(ex->ptotal); dfree(ex->stats); dfree(ex->stage);
-    dfree(ex->sk[0]); dfree(ex->sk[1]); dfree(ex->sort_tmp);
-    dfree(ex->hot_ids); dfree(ex->hot_tab); dfree(ex->hpart); dfree(ex->hctl); dfree(ex->ccnt); dfree(ex->coff);
+    dfree(ex->sk[0]); dfree(ex->sk[1]); dfree(ex->ph); dfree(ex->pgs); dfree(ex->pb);
+    dfree(ex->hot_ids); dfree(ex->hot_tab); dfree(ex->hpart); dfree(ex->hctl); dfree(ex->ccnt);
     dfree(ex->dctl); dfree(ex->stats_bak); ex->dsc.free_all();
     if (ex->h_pin) (void)hipHostFree(ex->h_pin);
     ex->timer.destroy();
@@ -847,30 +923,29 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
         GNS_HIP(hipGetLastError());
         cur ^= 1;
     }
-    const uint32_t none_key = (uint32_t)ex->slots;
     const uint32_t ks = ex->sb + ex->ib;
-    uint64_t ncold = 0;
-    {   // designated flows' partials -> flow state; the tail's words, densely
+    // flow ids < slots = 2^(key_bits - 1): bin = id >> pshift
+    const uint32_t pshift = ex->key_bits - 1 > kPBinBits ? ex->key_bits - 1 - kPBinBits : 0u;
+    const uint32_t ng = (nblk + kPGroup - 1) / kPGroup;
+    {
         ScopedStage st(ex->timer, 4);
         hipLaunchKernelGGL(k_ex_hot_reduce, dim3(kExHot), dim3(256), 0, s, ex->hpart, nblk, ex->hot_ids, ex->pkt, ex->f);
-        hipLaunchKernelGGL(k_ex_cscan, dim3(1), dim3(1024), 0, s, ex->ccnt, nblk, ex->coff, ex->hctl + 514);
-        hipLaunchKernelGGL(k_ex_ccopy, dim3(nblk), dim3(256), 0, s, ex->sk[0], ex->ccnt, ex->coff, ex->sk[1]);
         GNS_HIP(hipGetLastError());
-        GNS_HIP(hipMemcpyAsync(ex->h_pin + 8, ex->hctl + 514, 4, hipMemcpyDeviceToHost, s));
     }
-    GNS_HIP(hipStreamSynchronize(s));  // the tail size sizes the sort
-    ncold = ex->h_pin[8];
-    if (ncold) {
+    {
         ScopedStage st(ex->timer, 2);
-        size_t tb = ex->sort_tmp_bytes;
-        GNS_HIP(rocprim::radix_sort_keys<ExSortConfig>(ex->sort_tmp, tb, ex->sk[1], ex->sk[0], (size_t)ncold, ks,
-                                                       ks + ex->key_bits, s));
+        hipLaunchKernelGGL(k_ex_phist, dim3(nblk), dim3(256), 0, s, ex->sk[0], ex->ccnt, ks, pshift, ex->ph);
+        hipLaunchKernelGGL(k_ex_pscan_a, dim3(ng), dim3(kPBins), 0, s, ex->ph, nblk, ex->pgs);
+        hipLaunchKernelGGL(k_ex_pscan_b, dim3(1), dim3(kPBins), 0, s, ex->pgs, ng, ex->pb);
+        hipLaunchKernelGGL(k_ex_pscan_c, dim3(ng), dim3(kPBins), 0, s, ex->ph, nblk, ex->pgs);
+        hipLaunchKernelGGL(k_ex_pscatter, dim3(nblk), dim3(kPBins), 0, s, ex->sk[0], ex->ccnt, ex->ph, ks, pshift,
+                           ex->sk[1]);
+        GNS_HIP(hipGetLastError());
     }
-    if (ncold) {
+    {
         ScopedStage st(ex->timer, 3);
-        const uint64_t nt = (ncold + kRunItems - 1) / kRunItems;
-        hipLaunchKernelGGL(k_ex_runs, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, ex->sk[0], ncold, none_key,
-                           ex->sb, ex->ib, xin.in.sizes, ex->pkt, ex->f);
+        hipLaunchKernelGGL(k_ex_pagg, dim3(kPBins), dim3(kAggThreads), 0, s, ex->sk[1], ex->pb, ex->sb, ex->ib,
+                           xin.in.sizes, ex->pkt, ex->f);
         GNS_HIP(hipGetLastError());
     }
     {   // timestamps of the touched flows; the next batch's designated flows
@@ -902,20 +977,6 @@ int ex_geometry(gns_ex *ex) {
     ex->nblk_max = (uint32_t)(ex->bmax / kXChunk);
     ex->ib = std::max<uint32_t>(1, ceil_log2(ex->bmax));
     ex->sb = std::min<uint32_t>(31, 64 - kb - ex->ib);
-    size_t t1 = 0;
-    const uint32_t lo = ex->sb + ex->ib;
-    if (rocprim::radix_sort_keys<ExSortConfig>(nullptr, t1, ex->sk[0], ex->sk[1], (size_t)ex->bmax, lo, lo + ex->key_bits,
-                                               ex->stream) != hipSuccess) {
-        set_error("rocPRIM scratch query failed");
-        return GNS_E_HIP;
-    }
-    if (t1 > ex->sort_tmp_bytes) {
-        dfree(ex->sort_tmp);
-        ex->sort_tmp = nullptr;
-        ex->sort_tmp_bytes = 0;
-        GNS_TRY(dalloc(&ex->sort_tmp, t1));
-        ex->sort_tmp_bytes = t1;
-    }
     return GNS_OK;
 }
 
@@ -1120,7 +1181,9 @@ int gns_ex_create(const gns_ex_params *p, gns_ex **out) {
             (rc = dalloc_t(&ex->sk[0], ex->bmax)) || (rc = dalloc_t(&ex->sk[1], ex->bmax)) ||
             (rc = dalloc_t(&ex->hot_ids, kExHot)) || (rc = dalloc_t(&ex->hot_tab, kExHotTab)) ||
             (rc = dalloc_t(&ex->hpart, (uint64_t)kExHot * ex->nblk_max)) || (rc = dalloc_t(&ex->hctl, 516)) ||
-            (rc = dalloc_t(&ex->ccnt, ex->nblk_max)) || (rc = dalloc_t(&ex->coff, ex->nblk_max)))
+            (rc = dalloc_t(&ex->ccnt, ex->nblk_max)) || (rc = dalloc_t(&ex->ph, (uint64_t)ex->nblk_max * kPBins)) ||
+            (rc = dalloc_t(&ex->pgs, (uint64_t)(ex->nblk_max / kPGroup + 1) * kPBins)) ||
+            (rc = dalloc_t(&ex->pb, kPBins + 1)))
             break;
         if ((rc = ex_geometry(ex)) != GNS_OK) break;
         if ((rc = dalloc_t(&ex->dctl, 4)) != GNS_OK || (rc = dalloc_t(&ex->stats_bak, 3)) != GNS_OK) break;

@@ -153,7 +153,7 @@ class ExactAggregator:
     def set_timing(self, on: bool = True) -> None:
         check(self._L.gns_ex_set_timing(self._h, 1 if on else 0))
 
-    STAGES = ["extract", "resolve", "sort", "walk", "hot", "total"]
+    STAGES = ["extract", "resolve", "partition", "aggregate", "hot", "total"]
 
     def stage_times(self, reset: bool = False) -> dict:
         ms = (ct.c_double * 8)()
