@@ -59,9 +59,15 @@ constexpr uint32_t kExHotBits = GNS_EX_HOT_BITS;
 constexpr uint32_t kExHot = 1u << kExHotBits;
 constexpr uint32_t kExHotTab = 4 * kExHot;
 constexpr uint32_t kExHotMinKey = 6 * 8;  // designate only flows with >= 64 packets
-struct ExHotPart {  // one designated flow in one X1 block
-    uint32_t cnt, minp, maxp, pad;
-    unsigned long long bytes;
+// One designated flow in one X1 block: bytes << 15 | packets (a block has at
+// most 2^14 packets of < 2^32 bytes, so neither field carries into the other)
+// and the largest packet index in the block.  No first-packet index: a flow is
+// designated only with >= 64 packets counted, so its first packet is known.
+constexpr uint32_t kHotCntBits = 15;
+static_assert(kXChunk < (1u << kHotCntBits), "per-block packet count field");
+struct ExHotPart {
+    unsigned long long cb;
+    uint32_t maxp, pad;
 };
 __device__ __forceinline__ uint32_t exh_group(uint32_t id) { return (id * 0x9E3779B1u) >> (32 - kExHotBits); }
 __device__ __forceinline__ int exh_lookup(const unsigned long long *tab, uint32_t id) {
@@ -157,8 +163,8 @@ __device__ __forceinline__ void ex_probe_issue(const DictDev &D, uint32_t slot, 
 // stalling the wave on dependent probes; an empty home slot is claimed here.
 struct ExHotLds {
     const unsigned long long *tab;
-    uint32_t *cnt, *minp, *maxp;
-    unsigned long long *bytes;
+    unsigned long long *cb;
+    uint32_t *maxp;
 };
 
 constexpr uint64_t kNoWord = ~0ull;
@@ -204,9 +210,7 @@ __device__ __forceinline__ uint64_t ex_consume(const ExArgs &a, uint64_t p, uint
         const int h = exh_lookup(H.tab, out);
         if (h >= 0) {
             const uint32_t lp = (uint32_t)(p - beg);
-            atomicAdd(&H.cnt[h], 1u);
-            atomicAdd(&H.bytes[h], (unsigned long long)sz);
-            atomicMin(&H.minp[h], lp);
+            atomicAdd(&H.cb[h], (unsigned long long)sz << kHotCntBits | 1ull);
             atomicMax(&H.maxp[h], lp);
             n_ok++;
             return kNoWord;
@@ -246,13 +250,13 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
     __shared__ uint8_t s_src[80];
     __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_claim, s_abort, s_ncold;
     __shared__ __attribute__((aligned(16))) unsigned long long s_htab[kExHotTab];
-    __shared__ unsigned long long s_hby[kExHot];
-    __shared__ uint32_t s_hcnt[kExHot], s_hmin[kExHot], s_hmax[kExHot];
+    __shared__ unsigned long long s_hcb[kExHot];
+    __shared__ uint32_t s_hmax[kExHot];
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
     if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; s_claim = 0; s_ncold = 0; s_abort = dict_aborted(a.D); }
     for (uint32_t i = tid; i < kExHotTab; i += kXThreads) s_htab[i] = a.hot_tab[i];
-    for (uint32_t i = tid; i < kExHot; i += kXThreads) { s_hby[i] = 0; s_hcnt[i] = 0; s_hmin[i] = ~0u; s_hmax[i] = 0; }
-    const ExHotLds H{s_htab, s_hcnt, s_hmin, s_hmax, s_hby};
+    for (uint32_t i = tid; i < kExHot; i += kXThreads) { s_hcb[i] = 0; s_hmax[i] = 0; }
+    const ExHotLds H{s_htab, s_hcb, s_hmax};
     __syncthreads();
     if (s_abort) {  // the batch overflowed the dictionary: re-run after the table grows
         if (tid == 0) a.pend_cnt[blk] = 0;
@@ -345,7 +349,7 @@ __global__ __launch_bounds__(kXThreads) void k_ex_extract(ExArgs a) {
     __syncthreads();
     for (uint32_t i = tid; i < kExHot; i += kXThreads) {
         ExHotPart hp;
-        hp.cnt = s_hcnt[i]; hp.minp = s_hmin[i]; hp.maxp = s_hmax[i]; hp.pad = 0; hp.bytes = s_hby[i];
+        hp.cb = s_hcb[i]; hp.maxp = s_hmax[i]; hp.pad = 0;
         a.hpart[(uint64_t)i * a.nblk + blk] = hp;
     }
     if (tid == 0) {
@@ -428,36 +432,37 @@ extern "C" __device__ unsigned __ockl_wfred_add_u32(unsigned);
 extern "C" __device__ unsigned __ockl_wfscan_add_u32(unsigned, bool);
 
 // H: the per-block partials of each designated flow -> its flow state (one
-// workgroup per hot slot; the only writer of these flows until X3, whose
-// atomics then merge the flow's parked packets).
+// workgroup per hot slot; the only writer of these flows until P4, which merges
+// the flow's packets that were parked in X1).  first stays: a designated flow
+// had packets before this batch.
 __global__ __launch_bounds__(256) void k_ex_hot_reduce(const ExHotPart *hpart, uint32_t nblk, const uint32_t *hot_ids,
                                                        uint64_t pkt_base, FlowState f) {
     __shared__ unsigned long long s_by[4];
-    __shared__ uint32_t s_c[4], s_mn[4], s_mx[4];
+    __shared__ uint32_t s_c[4], s_mx[4];
     const uint32_t slot = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t id = hot_ids[slot];
     if (id == GNS_ID_NONE) return;  // block-uniform
-    uint32_t c = 0, mn = ~0u, mx = 0;
+    uint32_t c = 0, mx = 0;
     unsigned long long by = 0;
     for (uint32_t b = tid; b < nblk; b += 256) {
         const ExHotPart hp = hpart[(uint64_t)slot * nblk + b];
-        if (hp.cnt) {
-            c += hp.cnt; by += hp.bytes;
-            mn = min(mn, b * kXChunk + hp.minp);
+        if (hp.cb) {
+            c += (uint32_t)(hp.cb & ((1u << kHotCntBits) - 1u));
+            by += hp.cb >> kHotCntBits;
             mx = max(mx, b * kXChunk + hp.maxp);
         }
     }
-    c = __ockl_wfred_add_u32(c); by = __ockl_wfred_add_u64(by);
-    mn = __ockl_wfred_min_u32(mn); mx = __ockl_wfred_max_u32(mx);
-    if (lane == 0) { s_c[wave] = c; s_by[wave] = by; s_mn[wave] = mn; s_mx[wave] = mx; }
+    c = __ockl_wfred_add_u32(c);
+    by = __ockl_wfred_add_u64(by);
+    mx = __ockl_wfred_max_u32(mx);
+    if (lane == 0) { s_c[wave] = c; s_by[wave] = by; s_mx[wave] = mx; }
     __syncthreads();
     if (tid == 0) {
-        for (int w = 1; w < 4; w++) { c += s_c[w]; by += s_by[w]; mn = min(mn, s_mn[w]); mx = max(mx, s_mx[w]); }
+        for (int w = 1; w < 4; w++) { c += s_c[w]; by += s_by[w]; mx = max(mx, s_mx[w]); }
         if (c) {
             f.pkts[id] += c;
             f.bytes[id] += by;
             f.last[id] = max(f.last[id], pkt_base + mx + 1);
-            f.first[id] = min(f.first[id], pkt_base + mn);
         }
     }
 }
@@ -585,13 +590,21 @@ __global__ __launch_bounds__(kPBins) void k_ex_pscatter(const uint64_t *in, cons
     }
 }
 
-// P4: one workgroup per bin.  Words in chunks of kAggChunk; before a chunk the
-// table is flushed if it could overflow (a bin with more distinct flows than
-// the table merges in several rounds; each flow's partial results add up).
+// P4: one workgroup per bin, two per CU.  Words in chunks of kAggChunk; before a
+// chunk the table is flushed if it could overflow (a bin with more distinct flows
+// than the table merges in several rounds; each flow's partial results add up).
+// A flow holding >= 6 of a wave's words (a heavy tail flow) has them folded into
+// one update (up to GNS_AGG_FOLD such flows per wave and chunk).
 constexpr uint32_t kAggThreads = 1024;
-constexpr uint32_t kAggItems = 2;
-constexpr uint32_t kAggChunk = kAggThreads * kAggItems;
-constexpr uint32_t kAggCap = 6144;  // 24 B per entry
+constexpr uint32_t kAggChunk = kAggThreads;
+#ifndef GNS_AGG_CAP
+#define GNS_AGG_CAP 3072
+#endif
+#ifndef GNS_AGG_FOLD
+#define GNS_AGG_FOLD 4
+#endif
+constexpr uint32_t kAggCap = GNS_AGG_CAP;  // 24 B per entry: 72 KB
+constexpr int kAggMinBlocks = kAggCap * 24 <= 78 * 1024 ? 2 : 1;
 static_assert(kAggCap > kAggChunk, "a chunk fits an empty table");
 __device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t *mn, uint32_t *mx,
                                            unsigned long long *by, uint64_t pkt_base, FlowState f) {
@@ -606,58 +619,75 @@ __device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t
         key[e] = GNS_ID_NONE; cn[e] = 0; mn[e] = ~0u; mx[e] = 0; by[e] = 0;
     }
 }
-__global__ __launch_bounds__(kAggThreads) void k_ex_pagg(const uint64_t *in, const uint32_t *pb, uint32_t sb,
-                                                         uint32_t ib, const uint32_t *sizes, uint64_t pkt_base,
-                                                         FlowState f) {
+__device__ __forceinline__ uint32_t pagg_slot(uint32_t *key, uint32_t id, uint32_t *s_n) {
+    uint32_t h = (uint32_t)(((uint64_t)(id * 0x9E3779B1u) * kAggCap) >> 32);
+    for (;;) {
+        const uint32_t k = key[h];
+        if (k == id) return h;
+        if (k == GNS_ID_NONE) {
+            const uint32_t old = atomicCAS(&key[h], GNS_ID_NONE, id);
+            if (old == GNS_ID_NONE) { atomicAdd(s_n, 1u); return h; }
+            if (old == id) return h;
+        }
+        h = h + 1 == kAggCap ? 0u : h + 1;
+    }
+}
+__global__ __launch_bounds__(kAggThreads, kAggMinBlocks) void k_ex_pagg(const uint64_t *in, const uint32_t *pb, uint32_t sb,
+                                                            uint32_t ib, const uint32_t *sizes, uint64_t pkt_base,
+                                                            FlowState f) {
     __shared__ uint32_t key[kAggCap], cn[kAggCap], mn[kAggCap], mx[kAggCap];
     __shared__ unsigned long long by[kAggCap];
     __shared__ uint32_t s_n;
-    const uint32_t bin = blockIdx.x, tid = threadIdx.x;
+    const uint32_t bin = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
     const uint32_t beg = pb[bin], end = pb[bin + 1];
     if (beg == end) return;  // block-uniform
     for (uint32_t e = tid; e < kAggCap; e += kAggThreads) { key[e] = GNS_ID_NONE; cn[e] = 0; mn[e] = ~0u; mx[e] = 0; by[e] = 0; }
     if (tid == 0) s_n = 0;
     const uint32_t ks = sb + ib, esc = (1u << sb) - 1u;
     const uint64_t imask = (1ull << ib) - 1ull;
-    uint64_t wn[kAggItems];
-#pragma unroll
-    for (uint32_t j = 0; j < kAggItems; j++) {
-        const uint32_t i = beg + j * kAggThreads + tid;
-        wn[j] = i < end ? in[i] : ~0ull;
-    }
+    uint64_t wn = beg + tid < end ? in[beg + tid] : ~0ull;
     __syncthreads();
-    for (uint32_t c0 = beg; c0 < end; c0 += kAggChunk) {
+    for (uint32_t c0 = beg; c0 < end; c0 += kAggChunk) {  // block-uniform trip count
         if (s_n > kAggCap - kAggChunk) {  // block-uniform (read after the barrier)
-            __syncthreads();
             pagg_flush(key, cn, mn, mx, by, pkt_base, f);
+            __syncthreads();
             if (tid == 0) s_n = 0;
             __syncthreads();
         }
-        uint64_t w[kAggItems];
-#pragma unroll
-        for (uint32_t j = 0; j < kAggItems; j++) {
-            w[j] = wn[j];
-            const uint32_t i = c0 + kAggChunk + j * kAggThreads + tid;
-            wn[j] = i < end ? in[i] : ~0ull;
+        const uint64_t w = wn;
+        {
+            const uint32_t i = c0 + kAggChunk + tid;
+            wn = i < end ? in[i] : ~0ull;
         }
-#pragma unroll
-        for (uint32_t j = 0; j < kAggItems; j++) {
-            if (w[j] == ~0ull) continue;
-            const uint32_t id = (uint32_t)(w[j] >> ks);
-            const uint32_t idx = (uint32_t)((w[j] >> sb) & imask);
-            uint32_t sz = (uint32_t)w[j] & esc;
-            if (sz == esc) sz = sizes[idx];  // lengths too large for the word's field (rare)
-            uint32_t h = (uint32_t)(((uint64_t)(id * 0x9E3779B1u) * kAggCap) >> 32);
-            for (;;) {
-                const uint32_t k = key[h];
-                if (k == id) break;
-                if (k == GNS_ID_NONE) {
-                    const uint32_t old = atomicCAS(&key[h], GNS_ID_NONE, id);
-                    if (old == GNS_ID_NONE) { atomicAdd(&s_n, 1u); break; }
-                    if (old == id) break;
-                }
-                h = h + 1 == kAggCap ? 0u : h + 1;
+        bool v = w != ~0ull;
+        const uint32_t id = v ? (uint32_t)(w >> ks) : GNS_ID_NONE;
+        const uint32_t idx = (uint32_t)((w >> sb) & imask);
+        uint32_t sz = (uint32_t)w & esc;
+        if (v && sz == esc) sz = sizes[idx];  // lengths too large for the word's field (rare)
+        // heavy flows holding many of the wave's words: one folded update each
+        // (same-address LDS atomics serialize lane by lane)
+#pragma unroll 1
+        for (int fold = 0; fold < GNS_AGG_FOLD; fold++) {
+            const uint64_t vm = __ballot(v);
+            if (!vm) break;  // wave-uniform
+            const uint32_t id0 = __shfl(id, (int)(__ffsll((long long)vm) - 1));
+            const bool in_m = v && id == id0;
+            const uint64_t m = __ballot(in_m);
+            if (__popcll(m) < 6) break;  // wave-uniform
+            const unsigned long long tb = __ockl_wfred_add_u64(in_m ? (unsigned long long)sz : 0ull);
+            const uint32_t tmn = __ockl_wfred_min_u32(in_m ? idx : ~0u);
+            const uint32_t tmx = __ockl_wfred_max_u32(in_m ? idx : 0u);
+            if (lane == (uint32_t)__ffsll((long long)m) - 1u) {
+                const uint32_t h = pagg_slot(key, id0, &s_n);
+                atomicAdd(&cn[h], (uint32_t)__popcll(m));
+                atomicAdd(&by[h], tb);
+                atomicMin(&mn[h], tmn);
+                atomicMax(&mx[h], tmx);
             }
+            v = v && !in_m;
+        }
+        if (v) {
+            const uint32_t h = pagg_slot(key, id, &s_n);
             atomicAdd(&cn[h], 1u);
             atomicAdd(&by[h], (unsigned long long)sz);
             atomicMin(&mn[h], idx);
@@ -665,7 +695,6 @@ __global__ __launch_bounds__(kAggThreads) void k_ex_pagg(const uint64_t *in, con
         }
         __syncthreads();
     }
-    __syncthreads();
     pagg_flush(key, cn, mn, mx, by, pkt_base, f);
 }
 
@@ -827,6 +856,7 @@ struct gns_ex {
     ExHotPart *hpart = nullptr;              // [kExHot][nblk_max]
     uint32_t *hctl = nullptr;                // [0..511] count histogram, [512] threshold, [513] count, [514] tail words
     uint32_t *ccnt = nullptr;                // [nblk_max] X1 region word counts
+    bool warm = false;                       // flows designated (a batch ran since create / reset / growth)
     uint32_t *ph = nullptr, *pgs = nullptr, *pb = nullptr;  // P histograms / offsets, group sums, bin starts
     uint32_t key_bits = 0;                   // flow field bits: flow ids < slots, invalid = slots
     uint32_t sb = 0, ib = 0;                 // sort word: wire length bits, packet index bits
@@ -862,6 +892,7 @@ void ex_free_all(gns_ex *ex) {
 
 // no designated flows (after create / reset, and after a table growth renumbers the flows)
 int ex_hot_clear(gns_ex *ex) {
+    ex->warm = false;
     GNS_HIP(hipMemsetAsync(ex->hot_ids, 0xFF, kExHot * 4, ex->stream));
     GNS_HIP(hipMemsetAsync(ex->hot_tab, 0xFF, kExHotTab * 8, ex->stream));
     return GNS_OK;
@@ -964,6 +995,7 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     }
     ex->pkt += n;
     ex->batches++;
+    ex->warm = true;
     return GNS_OK;
 }
 
@@ -1077,8 +1109,12 @@ int ex_batch_recover(gns_ex *ex, const ExIn &x, uint64_t m) {
 template <int KIND>
 int ex_insert(gns_ex *ex, const ExIn &x0, uint64_t n, gns_mem where) {
     GNS_TRY(ex_set_dev(ex));
-    for (uint64_t off = 0; off < n; off += ex->bmax) {
-        const uint64_t m = std::min<uint64_t>(ex->bmax, n - off);
+    for (uint64_t off = 0, m = 0; off < n; off += m) {
+        // a batch without designated flows sends every packet through P (the heavy
+        // flows serialise in P4's LDS atomics): keep it short, so that designation
+        // starts early (as Count-Min's cold start)
+        const uint64_t cap = ex->warm ? ex->bmax : std::min<uint64_t>(ex->bmax, std::max<uint64_t>(1ull << 20, ex->bmax / 32));
+        m = std::min<uint64_t>(cap, n - off);
         ExIn x = x0;
         InputDesc &d = x.in;
         const InputDesc &in = x0.in;
