@@ -376,6 +376,9 @@ template <int KIND, int MODE>
 __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
     __shared__ uint8_t s_src[80];
     __shared__ uint32_t s_cnt, s_full, s_claim, s_abort;
+    __shared__ __attribute__((aligned(16))) unsigned long long s_htab[kExHotTab];
+    __shared__ unsigned long long s_hcb[kExHot];
+    __shared__ uint32_t s_hmax[kExHot];
     const ExArgs &a = r.x;
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
     const uint32_t cnt = r.cnt_in[blk];
@@ -384,6 +387,8 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
         return;
     }
     if (tid == 0) { s_cnt = 0; s_full = 0; s_claim = 0; s_abort = dict_aborted(a.D); }
+    for (uint32_t j = tid; j < kExHotTab; j += kXThreads) s_htab[j] = a.hot_tab[j];
+    for (uint32_t j = tid; j < kExHot; j += kXThreads) { s_hcb[j] = 0; s_hmax[j] = 0; }
     __syncthreads();
     if (s_abort) {
         if (tid == 0) r.cnt_out[blk] = 0;
@@ -400,6 +405,14 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
         const int res = dict_find_or_claim(a.D, kw, (uint32_t)(v & 0xFFFFFFFFFull), a.epoch, &out);
         if (res == DICT_CLAIMED) atomicAdd(&s_claim, 1u);
         if (res == DICT_FOUND || res == DICT_CLAIMED) {  // X1 wrote the word with none_key: fill in the flow field
+            // a designated flow displaced from its home slot: into the block's partials
+            // (its word is marked hot_key and skipped by P), as X1 does at the home slot
+            const int h = res == DICT_FOUND ? exh_lookup(s_htab, out) : -1;
+            if (h >= 0) {
+                atomicAdd(&s_hcb[h], (unsigned long long)a.x.in.sizes[p] << kHotCntBits | 1ull);
+                atomicMax(&s_hmax[h], (uint32_t)(p - beg));
+                out = a.hot_key;
+            }
             const uint32_t sh = a.ib + a.sb;
             const uint64_t wq = beg + ((v >> 36) & 0x3FFFu);
             a.sk[wq] = (a.sk[wq] & ((1ull << sh) - 1ull)) | (uint64_t)out << sh;
@@ -408,6 +421,12 @@ __global__ __launch_bounds__(kXThreads) void k_ex_resolve(ExResolveArgs r) {
         else atomicAdd(&s_full, 1u);
     }
     __syncthreads();
+    for (uint32_t j = tid; j < kExHot; j += kXThreads)
+        if (s_hcb[j]) {  // X1 wrote this block's partials before this launch
+            ExHotPart *hp = a.hpart + (uint64_t)j * a.nblk + blk;
+            atomicAdd(&hp->cb, s_hcb[j]);
+            atomicMax(&hp->maxp, s_hmax[j]);
+        }
     if (tid == 0) {
         r.cnt_out[blk] = s_cnt;
         if (s_cnt) atomicAdd(r.total_out, s_cnt);
@@ -483,13 +502,16 @@ constexpr uint32_t kPBins = 1u << kPBinBits;
 constexpr uint32_t kPGroup = 64;  // regions per P2 group
 
 __global__ __launch_bounds__(256) void k_ex_phist(const uint64_t *in, const uint32_t *ccnt, uint32_t ks,
-                                                  uint32_t pshift, uint32_t *ph) {
+                                                  uint32_t pshift, uint32_t none_key, uint32_t *ph) {
     __shared__ uint32_t h[kPBins];
     const uint32_t blk = blockIdx.x, n = ccnt[blk];
     for (uint32_t i = threadIdx.x; i < kPBins; i += 256) h[i] = 0;
     __syncthreads();
     const uint64_t *w = in + (uint64_t)blk * kXChunk;
-    for (uint32_t i = threadIdx.x; i < n; i += 256) atomicAdd(&h[(uint32_t)(w[i] >> ks) >> pshift], 1u);
+    for (uint32_t i = threadIdx.x; i < n; i += 256) {
+        const uint32_t id = (uint32_t)(w[i] >> ks);
+        if (id < none_key) atomicAdd(&h[id >> pshift], 1u);  // (a resolved designated flow's word is skipped)
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < kPBins; i += 256) ph[(uint64_t)blk * kPBins + i] = h[i];
 }
@@ -536,7 +558,7 @@ __global__ __launch_bounds__(kPBins) void k_ex_pscan_c(uint32_t *ph, uint32_t nb
 constexpr uint32_t kPSub = 4096;  // words per P3 sub-pass
 constexpr uint32_t kPItems = kPSub / kPBins;
 __global__ __launch_bounds__(kPBins) void k_ex_pscatter(const uint64_t *in, const uint32_t *ccnt, const uint32_t *po,
-                                                        uint32_t ks, uint32_t pshift, uint64_t *out) {
+                                                        uint32_t ks, uint32_t pshift, uint32_t none_key, uint64_t *out) {
     __shared__ uint64_t stage[kPSub];
     __shared__ uint16_t sbin[kPSub];
     __shared__ uint32_t cnt[kPBins], lstart[kPBins], goff[kPBins], dummy[kPBins], s_w[kPBins / 64];
@@ -553,7 +575,8 @@ __global__ __launch_bounds__(kPBins) void k_ex_pscatter(const uint64_t *in, cons
         for (uint32_t j = 0; j < kPItems; j++) {
             const uint32_t i = sp + j * kPBins + tid;
             w[j] = i < n ? src[i] : 0ull;
-            bn[j] = i < n ? (uint32_t)(w[j] >> ks) >> pshift : 0xFFFFu;
+            const uint32_t id = (uint32_t)(w[j] >> ks);
+            bn[j] = i < n && id < none_key ? id >> pshift : 0xFFFFu;
         }
         // ranks (any order): every lane adds, a lane without a word adds 0 to its own word
 #pragma unroll
@@ -578,7 +601,8 @@ __global__ __launch_bounds__(kPBins) void k_ex_pscatter(const uint64_t *in, cons
                 sbin[pos] = (uint16_t)bn[j];
             }
         __syncthreads();
-        const uint32_t m = min(kPSub, n - sp);
+        uint32_t m = 0;  // words staged in this sub-pass (designated flows' words are not)
+        for (uint32_t v = 0; v < kPBins / 64; v++) m += s_w[v];
         for (uint32_t i = tid; i < m; i += kPBins) {
             const uint32_t bb = sbin[i];
             out[goff[bb] + (i - lstart[bb])] = stage[i];
@@ -757,22 +781,42 @@ __global__ __launch_bounds__(256) void k_exh_collect(const unsigned long long *p
         if (q < kExHot) hot_ids[q] = (uint32_t)s;
     }
 }
-// the lookup table: a flow whose 4-entry group is full is simply not designated
-__global__ __launch_bounds__(256) void k_exh_table(uint32_t *hot_ids, unsigned long long *hot_tab) {
+// the lookup table, heaviest flows first (64 at a time): a flow whose 4-entry group
+// is full is simply not designated, and that should be one of the lightest
+// (a heavy flow left in the tail would serialise its P4 bin)
+__global__ __launch_bounds__(kExHot) void k_exh_table(uint32_t *hot_ids, const unsigned long long *pkts,
+                                                      unsigned long long *hot_tab) {
     __shared__ unsigned long long t[kExHotTab];
-    for (uint32_t i = threadIdx.x; i < kExHotTab; i += 256) t[i] = ~0ull;
+    __shared__ unsigned long long s_p[kExHot];
+    __shared__ uint32_t s_ord[kExHot];
+    const uint32_t i = threadIdx.x;
+    for (uint32_t j = i; j < kExHotTab; j += kExHot) t[j] = ~0ull;
+    const uint32_t id = hot_ids[i];
+    const unsigned long long p = id != GNS_ID_NONE ? pkts[id] : 0ull;
+    s_p[i] = p;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < kExHot; i += 256) {
-        const uint32_t id = hot_ids[i];
-        if (id == GNS_ID_NONE) continue;
-        const uint32_t g = exh_group(id) * 4;
-        bool in = false;
-        for (uint32_t e = 0; e < 4 && !in; e++)
-            in = atomicCAS(&t[g + e], ~0ull, (unsigned long long)id << 16 | i) == ~0ull;
-        if (!in) hot_ids[i] = GNS_ID_NONE;
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < kExHot; j++) {
+        const unsigned long long q = s_p[j];
+        rank += (q > p || (q == p && j < i)) ? 1u : 0u;
     }
+    s_ord[rank] = i;
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < kExHotTab; j += 256) hot_tab[j] = t[j];
+    for (uint32_t r0 = 0; r0 < kExHot; r0 += 64) {
+        if (i < 64) {
+            const uint32_t h = s_ord[r0 + i];
+            const uint32_t hid = hot_ids[h];
+            if (hid != GNS_ID_NONE) {
+                const uint32_t g = exh_group(hid) * 4;
+                bool in = false;
+                for (uint32_t e = 0; e < 4 && !in; e++)
+                    in = atomicCAS(&t[g + e], ~0ull, (unsigned long long)hid << 16 | h) == ~0ull;
+                if (!in) hot_ids[h] = GNS_ID_NONE;
+            }
+        }
+        __syncthreads();
+    }
+    for (uint32_t j = i; j < kExHotTab; j += kExHot) hot_tab[j] = t[j];
 }
 
 __global__ __launch_bounds__(256) void k_ex_query(const uint8_t *flows, uint32_t stride, uint64_t n, uint32_t K,
@@ -965,12 +1009,13 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     }
     {
         ScopedStage st(ex->timer, 2);
-        hipLaunchKernelGGL(k_ex_phist, dim3(nblk), dim3(256), 0, s, ex->sk[0], ex->ccnt, ks, pshift, ex->ph);
+        const uint32_t none_key = (uint32_t)ex->slots;
+        hipLaunchKernelGGL(k_ex_phist, dim3(nblk), dim3(256), 0, s, ex->sk[0], ex->ccnt, ks, pshift, none_key, ex->ph);
         hipLaunchKernelGGL(k_ex_pscan_a, dim3(ng), dim3(kPBins), 0, s, ex->ph, nblk, ex->pgs);
         hipLaunchKernelGGL(k_ex_pscan_b, dim3(1), dim3(kPBins), 0, s, ex->pgs, ng, ex->pb);
         hipLaunchKernelGGL(k_ex_pscan_c, dim3(ng), dim3(kPBins), 0, s, ex->ph, nblk, ex->pgs);
         hipLaunchKernelGGL(k_ex_pscatter, dim3(nblk), dim3(kPBins), 0, s, ex->sk[0], ex->ccnt, ex->ph, ks, pshift,
-                           ex->sk[1]);
+                           none_key, ex->sk[1]);
         GNS_HIP(hipGetLastError());
     }
     {
@@ -990,7 +1035,7 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
         hipLaunchKernelGGL(k_exh_pick, dim3(1), dim3(512), 0, s, ex->hctl, ex->hctl + 512);
         hipLaunchKernelGGL(k_exh_collect, dim3(sg), dim3(256), 0, s, ex->f.pkts, ex->slots, ex->hctl + 512,
                            ex->hctl + 513, ex->hot_ids);
-        hipLaunchKernelGGL(k_exh_table, dim3(1), dim3(256), 0, s, ex->hot_ids, ex->hot_tab);
+        hipLaunchKernelGGL(k_exh_table, dim3(1), dim3(kExHot), 0, s, ex->hot_ids, ex->f.pkts, ex->hot_tab);
         GNS_HIP(hipGetLastError());
     }
     ex->pkt += n;
