@@ -643,23 +643,37 @@ __device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t
         key[e] = GNS_ID_NONE; cn[e] = 0; mn[e] = ~0u; mx[e] = 0; by[e] = 0;
     }
 }
+// Table slot of a flow: buckets of 4 keys read with one 16-byte LDS load; keys
+// fill a bucket's slots in order and spill to the next bucket only when it is
+// full, so a bucket with an empty slot and no match ends the search (a linear
+// probe of single keys measured long dependent chains at 2/3 load).
+constexpr uint32_t kAggBuckets = kAggCap / 4;
+static_assert(kAggCap % 4 == 0, "whole buckets");
 __device__ __forceinline__ uint32_t pagg_slot(uint32_t *key, uint32_t id, uint32_t *s_n) {
-    uint32_t h = (uint32_t)(((uint64_t)(id * 0x9E3779B1u) * kAggCap) >> 32);
+    uint32_t b = (uint32_t)(((uint64_t)(id * 0x9E3779B1u) * kAggBuckets) >> 32);
     for (;;) {
-        const uint32_t k = key[h];
-        if (k == id) return h;
-        if (k == GNS_ID_NONE) {
-            const uint32_t old = atomicCAS(&key[h], GNS_ID_NONE, id);
-            if (old == GNS_ID_NONE) { atomicAdd(s_n, 1u); return h; }
-            if (old == id) return h;
+        const uint4 k4 = reinterpret_cast<const uint4 *>(key)[b];
+        if (k4.x == id) return 4 * b;
+        if (k4.y == id) return 4 * b + 1;
+        if (k4.z == id) return 4 * b + 2;
+        if (k4.w == id) return 4 * b + 3;
+        const uint32_t e = k4.x == GNS_ID_NONE ? 0u : k4.y == GNS_ID_NONE ? 1u : k4.z == GNS_ID_NONE ? 2u
+                         : k4.w == GNS_ID_NONE ? 3u : 4u;
+        if (e == 4u) {  // full: the key, if present, is further along
+            b = b + 1 == kAggBuckets ? 0u : b + 1;
+            continue;
         }
-        h = h + 1 == kAggCap ? 0u : h + 1;
+        const uint32_t old = atomicCAS(&key[4 * b + e], GNS_ID_NONE, id);
+        if (old == GNS_ID_NONE) { atomicAdd(s_n, 1u); return 4 * b + e; }
+        if (old == id) return 4 * b + e;
+        // another flow took that slot: read the bucket again
     }
 }
 __global__ __launch_bounds__(kAggThreads, kAggMinBlocks) void k_ex_pagg(const uint64_t *in, const uint32_t *pb, uint32_t sb,
                                                             uint32_t ib, const uint32_t *sizes, uint64_t pkt_base,
                                                             FlowState f) {
-    __shared__ uint32_t key[kAggCap], cn[kAggCap], mn[kAggCap], mx[kAggCap];
+    __shared__ __attribute__((aligned(16))) uint32_t key[kAggCap];
+    __shared__ uint32_t cn[kAggCap], mn[kAggCap], mx[kAggCap];
     __shared__ unsigned long long by[kAggCap];
     __shared__ uint32_t s_n;
     const uint32_t bin = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
