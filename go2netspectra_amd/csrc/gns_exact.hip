@@ -621,6 +621,10 @@ __global__ __launch_bounds__(kPBins) void k_ex_pscatter(const uint64_t *in, cons
 // one update (up to GNS_AGG_FOLD such flows per wave and chunk).
 constexpr uint32_t kAggThreads = 1024;
 constexpr uint32_t kAggChunk = kAggThreads;
+#ifndef GNS_AGG_DEPTH
+#define GNS_AGG_DEPTH 1
+#endif
+constexpr uint32_t kAggDepth = GNS_AGG_DEPTH;  // chunks of words in flight
 #ifndef GNS_AGG_CAP
 #define GNS_AGG_CAP 3072
 #endif
@@ -683,7 +687,13 @@ __global__ __launch_bounds__(kAggThreads, kAggMinBlocks) void k_ex_pagg(const ui
     if (tid == 0) s_n = 0;
     const uint32_t ks = sb + ib, esc = (1u << sb) - 1u;
     const uint64_t imask = (1ull << ib) - 1ull;
-    uint64_t wn = beg + tid < end ? in[beg + tid] : ~0ull;
+    // the words of the next kAggDepth chunks are in flight (P4 is latency-bound on them)
+    uint64_t wq[kAggDepth];
+#pragma unroll
+    for (uint32_t j = 0; j < kAggDepth; j++) {
+        const uint32_t i = beg + j * kAggChunk + tid;
+        wq[j] = i < end ? in[i] : ~0ull;
+    }
     __syncthreads();
     for (uint32_t c0 = beg; c0 < end; c0 += kAggChunk) {  // block-uniform trip count
         if (s_n > kAggCap - kAggChunk) {  // block-uniform (read after the barrier)
@@ -692,10 +702,12 @@ __global__ __launch_bounds__(kAggThreads, kAggMinBlocks) void k_ex_pagg(const ui
             if (tid == 0) s_n = 0;
             __syncthreads();
         }
-        const uint64_t w = wn;
+        const uint64_t w = wq[0];
+#pragma unroll
+        for (uint32_t j = 0; j + 1 < kAggDepth; j++) wq[j] = wq[j + 1];
         {
-            const uint32_t i = c0 + kAggChunk + tid;
-            wn = i < end ? in[i] : ~0ull;
+            const uint32_t i = c0 + kAggDepth * kAggChunk + tid;
+            wq[kAggDepth - 1] = i < end ? in[i] : ~0ull;
         }
         bool v = w != ~0ull;
         const uint32_t id = v ? (uint32_t)(w >> ks) : GNS_ID_NONE;
