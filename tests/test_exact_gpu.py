@@ -249,10 +249,12 @@ def test_pcapng_capture_drives_exact_and_countmin(gpu, oracle, tmp_path):
 
 @pytest.mark.parametrize("batch", [4096, 300_000, 1_500_000])
 def test_start_end_times_with_heavy_ties_across_sort_paths(gpu, oracle, batch):
-    """X2 sorts the flow-id bits only and relies on a stable sort for StartTime /
-    EndTime (the first / last packet of each run).  Batch sizes span rocPRIM's
-    single-block, (disabled) merge-sort and Onesweep ranges; 40 flows make every
-    flow a long run of ties, timestamps are random so any reordering shows."""
+    """StartTime / EndTime come from the merged smallest / largest stream index of
+    every path (designated flows' LDS partials in X1 and X1b, the tail's per-bin
+    aggregation with wave folding).  Batch sizes span the cold-start cap, one and
+    several P3 sub-passes; 40 heavy flows are designated after the first batch
+    (and fold in P4 before it); timestamps are random so any wrong first / last
+    packet shows."""
     from go2netspectra_amd import ExactTask, PacketBatch
     rng = np.random.default_rng(batch)
     n = 3_000_000
@@ -265,3 +267,23 @@ def test_start_end_times_with_heavy_ties_across_sort_paths(gpu, oracle, batch):
     orc = oracle.Exact(FIVE)
     orc.insert_tuples(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], ipver, t["length"], ts)
     assert_same_flows(gpu_flows(task), orc.export())
+
+
+def test_tail_bins_with_more_flows_than_the_table(gpu, oracle):
+    """About 1.4M distinct tail flows in one batch: each of P4's 512 bins holds more
+    flows than its LDS table takes before a flush (2048), so bins merge in several
+    rounds; every flow's four fields must still equal the oracle's."""
+    from go2netspectra_amd import ExactTask, PacketBatch
+    rng = np.random.default_rng(11)
+    n = 3_000_000
+    t = random_tuples(rng, n, 3_000_000, s=0.3)
+    ts = rng.integers(0, 1 << 50, n).astype(np.int64)
+    ipver = np.where(t["v6"], 6, 4).astype(np.uint8)
+    task = ExactTask("wide", FIVE, batch_packets=1 << 22, max_flows=1 << 22)
+    task.process_packets(PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"], ipver, ts))
+    task.flush()
+    orc = oracle.Exact(FIVE)
+    orc.insert_tuples(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], ipver, t["length"], ts)
+    want = orc.export()
+    assert len(want) > 1_500_000
+    assert_same_flows(gpu_flows(task), want)
