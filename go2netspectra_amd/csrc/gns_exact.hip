@@ -636,14 +636,24 @@ constexpr int kAggMinBlocks = kAggCap * 24 <= 78 * 1024 ? 2 : 1;
 static_assert(kAggCap > kAggChunk, "a chunk fits an empty table");
 __device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t *mn, uint32_t *mx,
                                            unsigned long long *by, uint64_t pkt_base, FlowState f) {
-    for (uint32_t e = threadIdx.x; e < kAggCap; e += kAggThreads) {
-        const uint32_t id = key[e];
-        if (id == GNS_ID_NONE) continue;
-        f.pkts[id] += cn[e];
-        f.bytes[id] += by[e];
-        f.last[id] = max(f.last[id], pkt_base + mx[e] + 1);
-        const unsigned long long fs = f.first[id];
-        if (fs >= pkt_base) f.first[id] = min(fs, pkt_base + mn[e]);  // no packet before this batch
+    // every entry's four state words are loaded before any is merged (all in flight together)
+    constexpr uint32_t kPer = (kAggCap + kAggThreads - 1) / kAggThreads;
+    uint32_t id[kPer];
+    unsigned long long pk[kPer], bt[kPer], ls[kPer], fs[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t e = threadIdx.x + j * kAggThreads;
+        id[j] = e < kAggCap ? key[e] : GNS_ID_NONE;
+        if (id[j] != GNS_ID_NONE) { pk[j] = f.pkts[id[j]]; bt[j] = f.bytes[id[j]]; ls[j] = f.last[id[j]]; fs[j] = f.first[id[j]]; }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t e = threadIdx.x + j * kAggThreads;
+        if (id[j] == GNS_ID_NONE) continue;
+        f.pkts[id[j]] = pk[j] + cn[e];
+        f.bytes[id[j]] = bt[j] + by[e];
+        f.last[id[j]] = max(ls[j], pkt_base + mx[e] + 1);
+        if (fs[j] >= pkt_base) f.first[id[j]] = min(fs[j], pkt_base + mn[e]);  // no packet before this batch
         key[e] = GNS_ID_NONE; cn[e] = 0; mn[e] = ~0u; mx[e] = 0; by[e] = 0;
     }
 }
