@@ -528,10 +528,15 @@ __global__ __launch_bounds__(kPBins) void k_ex_pscan_b(uint32_t *gs, uint32_t ng
     __shared__ uint32_t s_w[kPBins / 64];
     const uint32_t b = threadIdx.x, lane = b & 63u, wave = b >> 6;
     uint32_t run = 0;
-    for (uint32_t g = 0; g < ng; g++) {
-        const uint32_t x = gs[(uint64_t)g * kPBins + b];
-        gs[(uint64_t)g * kPBins + b] = run;
-        run += x;
+    for (uint32_t g0 = 0; g0 < ng; g0 += 8) {  // 8 independent loads in flight, then the prefix
+        uint32_t x[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) x[j] = g0 + j < ng ? gs[(uint64_t)(g0 + j) * kPBins + b] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            if (g0 + j < ng) gs[(uint64_t)(g0 + j) * kPBins + b] = run;
+            run += x[j];
+        }
     }
     const uint32_t inc = __ockl_wfscan_add_u32(run, true);
     if (lane == 63) s_w[wave] = inc;
@@ -541,7 +546,14 @@ __global__ __launch_bounds__(kPBins) void k_ex_pscan_b(uint32_t *gs, uint32_t ng
     const uint32_t start = base + inc - run;
     pb[b] = start;
     if (b == kPBins - 1) pb[kPBins] = base + inc;
-    for (uint32_t g = 0; g < ng; g++) gs[(uint64_t)g * kPBins + b] += start;
+    for (uint32_t g0 = 0; g0 < ng; g0 += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) x[j] = g0 + j < ng ? gs[(uint64_t)(g0 + j) * kPBins + b] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+            if (g0 + j < ng) gs[(uint64_t)(g0 + j) * kPBins + b] = x[j] + start;
+    }
 }
 // per group: the regions' offsets, in place over the histogram
 __global__ __launch_bounds__(kPBins) void k_ex_pscan_c(uint32_t *ph, uint32_t nblk, const uint32_t *gs) {
