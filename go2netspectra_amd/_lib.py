@@ -182,11 +182,11 @@ def device_ready(*arrays) -> None:
         torch.cuda.current_stream(a.device).synchronize()
 
 
-DICT_STATS = ["reclaims", "dropped", "live", "claimed", "reclaim_us", "retried_batches"]
+DICT_STATS = ["reclaims", "dropped", "live", "claimed", "reclaim_us", "retried_batches", "slots", "growths"]
 
 
 def dict_stats(fn, h) -> dict:
-    out = (ct.c_uint64 * 6)()
+    out = (ct.c_uint64 * 8)()
     check(fn(h, out))
     return dict(zip(DICT_STATS, list(out)))
 

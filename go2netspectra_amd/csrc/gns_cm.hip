@@ -53,7 +53,7 @@ constexpr uint32_t kEntShift = 16;
 constexpr uint32_t kLowMask = (1u << kEntShift) - 1u;
 constexpr uint32_t kSizeEsc = 0xFFFFu;
 constexpr uint32_t kOvfFlag = 0x80000000u;
-constexpr uint32_t kOvfCap = 1u << 22;
+constexpr uint32_t kOvfCap = 1u << 20;             // initial overflow table (grows per batch as needed)
 constexpr uint32_t kMaxBinsAll = 4096;               // d * bins per row (k_order, K3 LDS)
 #ifndef GNS_EX_THREADS
 #define GNS_EX_THREADS 256
@@ -245,7 +245,7 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) { return __ockl_wfred
 // issued earlier by the caller), publish/hash the row buckets, bin codes,
 // block histogram and designated-bucket summaries.
 struct K1Lds {
-    uint32_t *s_tab, *s_hist, *s_hFc, *s_hFs, *s_nfc, *s_nfs, *s_smax, *s_pend, *s_full;
+    uint32_t *s_tab, *s_hist, *s_hFc, *s_hFs, *s_nfc, *s_nfs, *s_smax, *s_pend, *s_full, *s_claim;
     unsigned long long *s_os, *s_fs;
 };
 
@@ -283,13 +283,7 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
     const bool cached = bw && ok && first == 0;
 #pragma unroll
     for (uint32_t rr = 0; rr < RMAX; rr++) bk[rr] = (rr < 4 && cached) ? rec[12 + rr] : 0u;
-#ifdef GNS_ABL_HICACHE  // timing ablation only (results not exact): rows >= 4 as if cached
-#pragma unroll
-    for (uint32_t rr = 4; rr < RMAX; rr++) if (cached) bk[rr] = rec[12 + (rr & 3)];
-    if (__ballot(ok && !cached)) {
-#else
     if (__ballot(ok && !cached) || (RMAX > 4 && d > 4)) {
-#endif
         uint32_t mk[GNS_KWMAX];
         mm3_premix<GNS_KWMAX>(kw, K, mk);
 #pragma unroll
@@ -317,11 +311,13 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
         // stalling the wave on a dependent probe.  The summaries treat a parked
         // packet as foreign to every owner, which is exact only for a flow that owns
         // no bucket (a new one does not): so a displaced packet that touches a
-        // designated bucket walks the chain here (the rare claims of that walk are
-        // not counted: the count restarts from the exact live set at every rebuild,
-        // and the probe limit still bounds the walks).
+        // designated bucket walks the chain here (its rare claims count against the
+        // dictionary cap like k_resolve's, so the 3/4-load bound holds).
         if (first == 2 || !anyhot) { res = CM_PENDING; out = first == 2 ? slot0 : ((slot0 + 1u) & a.D.mask); }
-        else res = cm_find_or_claim(a.D, kw, K, (slot0 + 1u) & a.D.mask, a.epoch, &out, rec);
+        else {
+            res = cm_find_or_claim(a.D, kw, K, (slot0 + 1u) & a.D.mask, a.epoch, &out, rec);
+            if (res == CM_CLAIMED) atomicAdd(S.s_claim, 1u);
+        }
     }
     if (ok) {
         if (res == CM_FULL) {
@@ -345,7 +341,9 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
             if (rr < d) tp[12 + rr] = bk[rr];
     }
     if (!ok) sz = 0;
-    n_ok += ok ? 1u : 0u;
+    // low 16 bits: packets inserted; high 16: of them with a size taking the
+    // overflow side table (a block has <= kChunk packets, so neither carries)
+    n_ok += (ok ? 1u : 0u) + (sz >= kSizeEsc ? 0x10000u : 0u);
 #pragma unroll
     for (uint32_t rr = 0; rr < RMAX; rr++) {
         if (rr >= d) break;
@@ -355,9 +353,7 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
             const uint32_t b = bk[rr];
             h = hs[rr];
             // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
-#ifndef GNS_ABL_NOIDX
             a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
-#endif
             binid = h >= 0 ? a.g.nbins + rr * kHot + (uint32_t)h : rr * a.g.ntiles + (b >> a.g.bin_bits);
         }
         // heavy bins: one LDS add for the wave's majority bin
@@ -367,24 +363,11 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
         const bool agg = cnt >= 4;  // wave-uniform
         const bool inmaj = agg && binid == b0;
         const bool leader = inmaj && (uint32_t)__ffsll((long long)mm) - 1 == (threadIdx.x & 63u);
-#if defined(GNS_ABL_NOHIST)  // timing ablations only (results not exact)
-#elif defined(GNS_ABL_NOHOTHIST)
-        if (leader && b0 < a.g.nbins) atomicAdd(&s_hist[b0], cnt);
-        if (binid < a.g.nbins && !inmaj) atomicAdd(&s_hist[binid], 1u);
-#elif defined(GNS_ABL_NOCOLDHIST)
-        if (leader && b0 >= a.g.nbins) atomicAdd(&s_hist[b0], cnt);
-        if (binid != 0xFFFFFFFFu && binid >= a.g.nbins && !inmaj) atomicAdd(&s_hist[binid], 1u);
-#else
         if (leader) atomicAdd(&s_hist[b0], cnt);
         if (binid != 0xFFFFFFFFu && !inmaj) atomicAdd(&s_hist[binid], 1u);
-#endif
         // designated bucket: summary against the batch-entry owners
         uint64_t ownv = 0;
-#ifdef GNS_ABL_NOHOTSUM
-        if (false) {
-#else
         if (h >= 0) {
-#endif
             const uint32_t slot = rr * kHot + (uint32_t)h;
             if (kid != s_hFc[slot]) atomicAdd(&s_nfc[slot], 1u);
             if (kid != s_hFs[slot]) {
@@ -445,7 +428,7 @@ constexpr bool kC2Pipe = GNS_C2_PIPE != 0;  // the two-stage pipeline for d != 8
 template <int KIND, int MODE, int KB, int DD, int NT>
 __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) void k_extract(ExtractArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t xsm[];
-    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok;
+    __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_claim;
     __shared__ uint8_t s_src[80];
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
     const uint32_t NS = a.g.d * kHot;
@@ -468,13 +451,13 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
         s_hFs[i] = id != GNS_ID_NONE ? a.Fs[cell] : GNS_ID_NONE;
         s_nfc[i] = 0; s_nfs[i] = 0; s_smax[i] = 0; s_os[i] = 0; s_fs[i] = 0;
     }
-    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; }
+    if (tid == 0) { s_pend = 0; s_drop = 0; s_unsup = 0; s_full = 0; s_ok = 0; s_claim = 0; }
     __syncthreads();
     const uint64_t beg = (uint64_t)blk * kChunk;
     const uint64_t end = min(a.n, beg + kChunk);
     const bool bw = a.D.bw != 0;
     uint32_t n_ok = 0;
-    const K1Lds S{s_tab, s_hist, s_hFc, s_hFs, s_nfc, s_nfs, s_smax, &s_pend, &s_full, s_os, s_fs};
+    const K1Lds S{s_tab, s_hist, s_hFc, s_hFs, s_nfc, s_nfs, s_smax, &s_pend, &s_full, &s_claim, s_os, s_fs};
     if constexpr (KIND == IN_HDR && (DD == 8 ? kC5Pipe : kC2Pipe)) {
         // Two-stage software pipeline over the block's packets: iteration k
         // parses packet k+1 and issues its dictionary probe (and the header
@@ -575,10 +558,12 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
     if (tid == 0) {
         a.pend_cnt[blk] = s_pend;
         if (s_pend) atomicAdd(a.pend_total, s_pend);
-        if (s_ok) atomicAdd(&a.stats[0], (unsigned long long)s_ok);
+        if (s_ok & 0xFFFFu) atomicAdd(&a.stats[0], (unsigned long long)(s_ok & 0xFFFFu));
+        if (s_ok >> 16) atomicAdd(&a.stats[8], (unsigned long long)(s_ok >> 16));
         if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
         if (s_unsup) atomicAdd(&a.stats[2], (unsigned long long)s_unsup);
         if (s_full) atomicAdd(&a.stats[3], (unsigned long long)s_full);
+        dict_flush_claims(a.D, s_claim, &a.stats[3]);
     }
 }
 
@@ -759,6 +744,7 @@ struct ScatterArgs {
     uint64_t *entries;
     uint64_t *ovf;
     uint32_t *ovf_cnt;
+    uint32_t ovf_cap;         // entries ovf holds (>= d * the batch's oversize packets)
     const uint32_t *hot_ids;
     unsigned long long *stats;
     // hot_mode 0: tile bins only (designated buckets are summarized by K1);
@@ -897,12 +883,12 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
                     uint32_t lo = ids[i], sf = sz;
                     if (sz >= kSizeEsc) {
                         const uint32_t q = atomicAdd(a.ovf_cnt, 1u);
-                        if (q < kOvfCap) {
+                        if (q < a.ovf_cap) {
                             a.ovf[q] = (uint64_t)sz << 32 | ids[i];
                             lo = kOvfFlag | q;
                         } else {
                             atomicAdd(&a.stats[4], 1ull);
-                            lo = kOvfFlag | (kOvfCap - 1);
+                            lo = kOvfFlag | (a.ovf_cap - 1);
                         }
                         sf = kSizeEsc;
                     }
@@ -1073,12 +1059,12 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
                     uint32_t lo = ids[j], sf = sz;
                     if (sz >= kSizeEsc) {
                         const uint32_t q = atomicAdd(a.ovf_cnt, 1u);
-                        if (q < kOvfCap) {
+                        if (q < a.ovf_cap) {
                             a.ovf[q] = (uint64_t)sz << 32 | ids[j];
                             lo = kOvfFlag | q;
                         } else {
                             atomicAdd(&a.stats[4], 1ull);
-                            lo = kOvfFlag | (kOvfCap - 1);
+                            lo = kOvfFlag | (a.ovf_cap - 1);
                         }
                         sf = kSizeEsc;
                     }
@@ -2615,7 +2601,7 @@ struct gns_cm {
     uint32_t *dctl = nullptr;             // D.ctl: [0] claimed slots, [1] abort flag
     DictScratch dsc;                      // rebuild scratch (grow-only)
     unsigned long long *stats_bak = nullptr;  // [3] counters before the running batch (undone on abort)
-    uint64_t n_reclaim = 0, n_dropped = 0, last_live = 0, n_retry = 0;
+    uint64_t n_reclaim = 0, n_dropped = 0, last_live = 0, n_retry = 0, n_grow = 0;
     double reclaim_ms = 0.0;
     uint32_t epoch = 0;
     uint64_t bmax = 0;
@@ -2629,7 +2615,8 @@ struct gns_cm {
     uint32_t *soff = nullptr;          // [nbins][17] super-bin tile starts (sub_bits > 0)
     uint64_t *ovf = nullptr;
     uint32_t *ovf_cnt = nullptr;
-    unsigned long long *stats = nullptr;  // [8]
+    uint64_t ovf_cap = 0;                 // entries of ovf
+    unsigned long long *stats = nullptr;  // [8] counters (gns_cm_counters), [8] oversize packets of the batch
     uint32_t *hot_ids = nullptr;          // [d][kHot] designated buckets for the next batch
     uint32_t *hot_tab = nullptr;          // [d][kHotTab] their lookup groups
     long long *segtot = nullptr;          // [d*kHot][kHotSegs][2]
@@ -2746,21 +2733,33 @@ int cm_reset_state(gns_cm *cm) {
 }
 
 // Reclaim: rebuild the dictionary keeping the flows a bucket (or a snapshot
-// view) still names (gns_dict.hip).  Views are quiesced and their snapshots
-// remapped with the buckets, so a view answers exactly as before.
-int cm_reclaim(gns_cm *cm) {
+// view of the current period) still names (gns_dict.hip).  Views are quiesced
+// and their snapshots remapped with the buckets, so a view answers exactly as
+// before; a stale view (taken before a reset) names nothing: it answers
+// GNS_E_ARG until refreshed, which overwrites its ids.  The table doubles
+// while the live flows exceed a quarter of it, and to at least min_slots.
+void cm_dict_limits(gns_cm *cm) {
+    cm->D.cap = (uint32_t)(cm->dict_slots - cm->dict_slots / 4);  // claims beyond 3/4 load abort the batch
+    cm->max_flows = std::max<uint64_t>(cm->max_flows, cm->dict_slots / 2);  // proactive reclaim at load 1/2
+}
+
+int cm_reclaim(gns_cm *cm, uint64_t min_slots = 0) {
     ViewsQuiesced q(cm);
     const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
     std::vector<DictIds> ids{{cm->Fc, cells}, {cm->Fs, cells}};
+    const uint32_t period = cm->period.load();
     for (gns_cm_view *v : cm->views)
-        if (v->period != ~0u) { ids.push_back({v->Fc, cells}); ids.push_back({v->Fs, cells}); }
+        if (v->period == period) { ids.push_back({v->Fc, cells}); ids.push_back({v->Fs, cells}); }
     const auto t0 = std::chrono::steady_clock::now();
-    const uint64_t before = cm->claimed;
+    const uint64_t before = cm->claimed, slots0 = cm->dict_slots;
     uint64_t live = 0;
     GNS_TRY(dict_rebuild(cm->D, cm->dict_slots, ids.data(), (int)ids.size(), nullptr, ids.data(), (int)ids.size(),
-                         cm->dict_slots, cm->stream, cm->dsc, &live, nullptr));
+                         std::min(kDictMaxSlots, std::max(cm->dict_slots, min_slots)), cm->stream, cm->dsc, &live,
+                         nullptr, kDictMaxSlots));
     cm->reclaim_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     cm->n_reclaim++;
+    if (cm->dict_slots != slots0) cm->n_grow++;
+    cm_dict_limits(cm);
     cm->n_dropped += before > live ? before - live : 0;
     cm->claimed = live;
     cm->last_live = live;
@@ -2779,6 +2778,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
     GNS_HIP(hipMemsetAsync(cm->ptotal, 0, 8, s));
     GNS_HIP(hipMemsetAsync(cm->dctl + 1, 0, 4, s));  // abort flag of this batch
     GNS_HIP(hipMemsetAsync(cm->hflag2, 0, ((size_t)g.d * kHot + 2) * 4, s));
+    GNS_HIP(hipMemsetAsync(cm->stats + 8, 0, 8, s));  // oversize packets of this batch (K1)
     if (++cm->epoch == 0) cm->epoch = 1;
     {
         ExtractArgs a{};
@@ -2821,8 +2821,20 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
             GNS_HIP(hipMemcpyAsync(cm->h_pin, cm->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
             GNS_HIP(hipMemcpyAsync(cm->h_pin + 2, cm->stats + 3, 8, hipMemcpyDeviceToHost, s));
             GNS_HIP(hipMemcpyAsync(cm->h_pin + 4, cm->dctl, 4, hipMemcpyDeviceToHost, s));
+            if (round == 1) GNS_HIP(hipMemcpyAsync(cm->h_pin + 6, cm->stats + 8, 8, hipMemcpyDeviceToHost, s));
             GNS_HIP(hipStreamSynchronize(s));
             cm->claimed = cm->h_pin[4];
+            if (round == 1) {  // the overflow side table holds every oversize row-update of the batch
+                const uint64_t big = (uint64_t)cm->h_pin[6] | (uint64_t)cm->h_pin[7] << 32;
+                if (big * g.d > cm->ovf_cap) {
+                    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(big * g.d + big * g.d / 4, kOvfCap), 1ull << 31);
+                    dfree(cm->ovf);
+                    cm->ovf = nullptr;
+                    cm->ovf_cap = 0;
+                    GNS_TRY(dalloc_t(&cm->ovf, want));
+                    cm->ovf_cap = want;
+                }
+            }
             if (cm->h_pin[2] | cm->h_pin[3]) {
                 set_error("flow dictionary full (%llu slots); raise max_flows",
                           (unsigned long long)cm->dict_slots);
@@ -2861,7 +2873,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         ScatterArgs a{};
         a.n = n; a.g = g; a.keyid = cm->keyid; a.idx = cm->idx; a.sizes = in.sizes;
         a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
-        a.ovf_cnt = cm->ovf_cnt; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
+        a.ovf_cnt = cm->ovf_cnt; a.ovf_cap = (uint32_t)cm->ovf_cap; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
         a.hot_mode = 0; a.hflag2 = cm->hflag2; a.hany = cm->hflag2 + g.d * kHot;
         ScopedStage st(cm->timer, 3);
         if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 256 && g.d <= 8)
@@ -2916,7 +2928,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
             ScatterArgs a{};
             a.n = n; a.g = g; a.keyid = cm->keyid; a.idx = cm->idx; a.sizes = in.sizes;
             a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
-            a.ovf_cnt = cm->ovf_cnt; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
+            a.ovf_cnt = cm->ovf_cnt; a.ovf_cap = (uint32_t)cm->ovf_cap; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
             a.hot_mode = 1; a.hflag2 = cm->hflag2; a.hany = h.hany;
             if (cm->lds_ordered)
                 hipLaunchKernelGGL(k_scatter<1>, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
@@ -2972,16 +2984,18 @@ int cm_batch(gns_cm *cm, const InputDesc &d, uint64_t m) {
 
 // One device batch (device-resident inputs) with dictionary recovery: a batch
 // whose new flows overflow the dictionary is aborted before it changes the
-// sketch, its counters are undone and the dead flows reclaimed;
-// it is re-run as is once, then in halves.  Only when a 16K-packet batch does
-// not fit next to the live flows of a freshly rebuilt dictionary is the
-// dictionary full (sticky until reset).  fresh: the dictionary was rebuilt
-// right before this batch.
+// sketch, its counters are undone and its claims dropped with
+// the dead flows (reclaim); it is re-run as is once, then in halves.  A piece
+// of <= kChunk packets that does not fit a freshly rebuilt dictionary doubles
+// the table instead, so the engine keeps counting whatever the stream brings,
+// as the reference's fixed table of key bytes does (count_min.go:66-81,94-157):
+// live ids are bounded by 2*d*w, the table by kDictMaxSlots.  fresh: the
+// dictionary was rebuilt right before this batch.
 template <int KIND>
 int cm_batch_recover(gns_cm *cm, const InputDesc &d, uint64_t m, bool fresh) {
     if (m == 0) return GNS_OK;
     if (cm->full) {
-        set_error("flow dictionary full (%llu slots, %llu live flows); raise max_flows",
+        set_error("flow dictionary full (%llu slots, %llu live flows)",
                   (unsigned long long)cm->dict_slots, (unsigned long long)cm->last_live);
         return GNS_E_FULL;
     }
@@ -2998,21 +3012,26 @@ int cm_batch_recover(gns_cm *cm, const InputDesc &d, uint64_t m, bool fresh) {
         GNS_HIP(hipMemcpyAsync(cm->stats, cm->stats_bak, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
                                cm->stream));
         GNS_HIP(hipMemsetAsync(cm->stats + 3, 0, sizeof(unsigned long long), cm->stream));
-        GNS_TRY(cm_reclaim(cm));
         cm->n_retry++;
         if (!fresh) {  // the flows that died since the last rebuild may be room enough
+            GNS_TRY(cm_reclaim(cm));
             fresh = true;
             continue;
         }
-        break;
-    }
-    if (m <= kChunk) {
-        cm->full = true;
-        const unsigned long long one = 1;
-        GNS_HIP(hipMemcpy(cm->stats + 3, &one, sizeof(one), hipMemcpyHostToDevice));
-        set_error("flow dictionary full: %llu live flows plus one %u-packet batch exceed %llu slots; raise max_flows",
-                  (unsigned long long)cm->last_live, kChunk, (unsigned long long)cm->dict_slots);
-        return GNS_E_FULL;
+        if (m > kChunk) {  // split: each half meets a fresh dictionary
+            GNS_TRY(cm_reclaim(cm));
+            break;
+        }
+        if (cm->dict_slots >= kDictMaxSlots) {  // cannot happen below 2*d*w + kChunk ~ 3/4 * 2^30 live flows
+            GNS_TRY(cm_reclaim(cm));
+            cm->full = true;
+            const unsigned long long one = 1;
+            GNS_HIP(hipMemcpy(cm->stats + 3, &one, sizeof(one), hipMemcpyHostToDevice));
+            set_error("flow dictionary full: %llu live flows plus one %u-packet batch exceed %llu slots",
+                      (unsigned long long)cm->last_live, kChunk, (unsigned long long)cm->dict_slots);
+            return GNS_E_FULL;
+        }
+        GNS_TRY(cm_reclaim(cm, cm->dict_slots * 2));  // grow, then re-run the piece
     }
     const uint64_t h = ((m / 2 + kChunk - 1) / kChunk) * kChunk;
     GNS_TRY(cm_batch_recover<KIND>(cm, d, h, true));
@@ -3174,10 +3193,11 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (rc = dalloc_t(&cm->Fc, cells)) || (rc = dalloc_t(&cm->Fs, cells)))
             break;
         // flow dictionary: power of two >= 2 * max_flows
+        // (the initial capacity: the table grows with the live flows, see cm_reclaim)
         const uint64_t mf = p->max_flows ? p->max_flows : (4ull << 20);
         uint64_t slots = 1;
         while (slots < 2 * mf) slots <<= 1;
-        if (slots > (1ull << 30)) { set_error("max_flows too large"); rc = GNS_E_ARG; break; }
+        if (slots > kDictMaxSlots) { set_error("max_flows too large"); rc = GNS_E_ARG; break; }
         cm->dict_slots = slots;
         cm->max_flows = mf;
         cm->D.mask = (uint32_t)(slots - 1);
@@ -3188,13 +3208,13 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         if ((rc = dalloc_t(&cm->D.rec, slots * cm->D.RW)) != GNS_OK) break;
         if ((rc = dalloc_t(&cm->dctl, 4)) != GNS_OK || (rc = dalloc_t(&cm->stats_bak, 3)) != GNS_OK) break;
         cm->D.ctl = cm->dctl;
-        cm->D.cap = (uint32_t)(slots - slots / 4);  // claims beyond 3/4 load abort the batch (reclaim + retry)
+        cm_dict_limits(cm);
         // batch buffers
         cm->bmax = p->batch_packets ? p->batch_packets : (16ull << 20);
         cm->bmax = ((cm->bmax + kChunk - 1) / kChunk) * kChunk;
         if (cm->bmax > (1ull << 31)) { set_error("batch_packets too large"); rc = GNS_E_ARG; break; }
-        // update positions are u32: d * batch < 2^32
-        const uint64_t bcap = ((0xFFFFFFFFull / g.d) / kChunk) * kChunk;
+        // update positions are u32 and overflow-table slots 31-bit: d * batch <= 2^31
+        const uint64_t bcap = (((1ull << 31) / g.d) / kChunk) * kChunk;
         if (cm->bmax > bcap) cm->bmax = bcap;
         cm->nblk_max = (uint32_t)(cm->bmax / kChunk);
         // K2 scratch: group sums [ngrp][nbins_all] + bin totals [nbins_all]
@@ -3215,9 +3235,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (rc = dalloc_t(&cm->hflag2, g.d * kHot + 2)) || (rc = dalloc_t(&cm->hres, g.d * kHot * 2)) ||
             (rc = dalloc_t(&cm->chk, kChkCap)) || (rc = dalloc_t(&cm->hot_tab, (size_t)g.d * kHotTab)))
             break;
-#ifdef GNS_ABL_NOIDX
-        if (hipMemset(cm->idx, 0, (size_t)cm->bmax * g.d * 4) != hipSuccess) { rc = GNS_E_HIP; break; }
-#endif
+        cm->ovf_cap = kOvfCap;
         if (hipHostMalloc(reinterpret_cast<void **>(&cm->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
         }
@@ -3299,7 +3317,7 @@ int gns_cm_flush(gns_cm *cm) {
     cm->timer.collect();
     GNS_HIP(hipMemcpy(cm->h_pin, cm->stats + 4, 8, hipMemcpyDeviceToHost));
     if (cm->h_pin[0] | cm->h_pin[1]) {
-        set_error("more than %u packets of size >= 2^19-1 in one batch", kOvfCap);
+        set_error("overflow side table exhausted (internal error)");
         return GNS_E_RANGE;
     }
     return GNS_OK;
@@ -3662,10 +3680,11 @@ int gns_cm_reclaim(gns_cm *cm) {
     return cm_reclaim(cm);
 }
 
-int gns_cm_dict_stats(gns_cm *cm, uint64_t out[6]) {
+int gns_cm_dict_stats(gns_cm *cm, uint64_t out[8]) {
     if (!cm || !out) return GNS_E_ARG;
     out[0] = cm->n_reclaim; out[1] = cm->n_dropped; out[2] = cm->last_live; out[3] = cm->claimed;
     out[4] = (uint64_t)(cm->reclaim_ms * 1000.0); out[5] = cm->n_retry;
+    out[6] = cm->dict_slots; out[7] = cm->n_grow;
     return GNS_OK;
 }
 

@@ -110,9 +110,14 @@ struct DictScratch {
     uint64_t remap_n = 0, stage_n = 0;
     void free_all();
 };
+// grow_max != 0: the table also doubles (up to grow_max slots) while the live
+// flows exceed a quarter of it.
 int dict_rebuild(DictDev &D, uint64_t &slots, const DictIds *mark, int nmark, const unsigned long long *keep_nz,
                  DictIds *remap_arrays, int nremap, uint64_t new_slots, hipStream_t s, DictScratch &sc,
-                 uint64_t *live_out, uint32_t **old_rec_out);
+                 uint64_t *live_out, uint32_t **old_rec_out, uint64_t grow_max = 0);
+// Largest dictionary: flow ids are u32 slots below kDictMarked (0xFFFFFFFE /
+// GNS_ID_NONE are reserved); 2^30 slots keep a 64-byte-record table at 64 GB.
+constexpr uint64_t kDictMaxSlots = 1ull << 30;
 
 // gns_frame.cpp: one captured frame -> one 64-byte record for the device
 // parser.  Returns 0 = copied verbatim (device fast-path shape), 1 = decoded

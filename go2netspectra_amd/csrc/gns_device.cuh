@@ -252,9 +252,6 @@ __device__ __forceinline__ int parse_record_fast(const uint32_t (&w)[16], uint32
                                                  uint32_t (&tw)[10]) {
     const bool fast = parse_fast_ipv4(w, wirelen, tw);
     int st = PARSE_OK;
-#ifdef GNS_ABL_FASTONLY
-    return fast ? PARSE_OK : PARSE_UNSUPPORTED;  // ablation (timing only)
-#endif
     if (__ballot(valid && !fast)) {
         if (valid && !fast) st = parse_record(w, wirelen, tw);
     }

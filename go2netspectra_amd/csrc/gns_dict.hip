@@ -24,16 +24,20 @@
 
 namespace gns {
 
+// remap[] during a rebuild: GNS_ID_NONE = not named, kDictMarked = named (live if its
+// record is occupied), else the record's new slot.  A named id whose record is
+// empty (it cannot be, short of a caller bug) is never reinserted and remaps to
+// GNS_ID_NONE -- no fingerprint -- instead of aliasing a real slot.
 __global__ __launch_bounds__(256) void k_dict_mark(const uint32_t *ids, uint64_t n, uint64_t slots, uint32_t *remap) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const uint32_t id = ids[i];
-        if (id < slots) remap[id] = 0u;
+        if (id < slots) remap[id] = kDictMarked;
     }
 }
 
 __global__ __launch_bounds__(256) void k_dict_mark_nz(const unsigned long long *keep, uint64_t slots, uint32_t *remap) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * 256)
-        if (keep[i] != 0ull) remap[i] = 0u;
+        if (keep[i] != 0ull) remap[i] = kDictMarked;
 }
 
 // live = occupied and marked; stage them (record words, old slot) compactly
@@ -42,7 +46,7 @@ __global__ __launch_bounds__(256) void k_dict_gather(DictDev D, uint64_t slots, 
                                                      uint32_t *stage_slot, uint32_t *count) {
     for (uint64_t s0 = (uint64_t)blockIdx.x * 256; s0 < slots; s0 += (uint64_t)gridDim.x * 256) {  // wave-uniform
         const uint64_t s = s0 + threadIdx.x;
-        const bool live = s < slots && remap[s] == 0u && D.rec[s * D.RW] != 0u;
+        const bool live = s < slots && remap[s] == kDictMarked && D.rec[s * D.RW] != 0u;
         const uint64_t m = __ballot(live);
         if (m == 0) continue;
         const uint32_t lane = __lane_id();
@@ -86,7 +90,10 @@ __global__ __launch_bounds__(256) void k_dict_reinsert(DictDev D, const uint32_t
 __global__ __launch_bounds__(256) void k_dict_remap(uint32_t *ids, uint64_t n, uint64_t slots, const uint32_t *remap) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const uint32_t id = ids[i];
-        if (id < slots) ids[i] = remap[id];
+        if (id < slots) {
+            const uint32_t r = remap[id];
+            ids[i] = r < kDictMarked ? r : GNS_ID_NONE;
+        }
     }
 }
 
@@ -101,7 +108,7 @@ void DictScratch::free_all() {
 
 int dict_rebuild(DictDev &D, uint64_t &slots, const DictIds *mark, int nmark, const unsigned long long *keep_nz,
                  DictIds *remap_arrays, int nremap, uint64_t new_slots, hipStream_t s, DictScratch &sc,
-                 uint64_t *live_out, uint32_t **old_rec_out) {
+                 uint64_t *live_out, uint32_t **old_rec_out, uint64_t grow_max) {
     if (new_slots < slots) new_slots = slots;
     if (!sc.cnt) GNS_TRY(dalloc_t(&sc.cnt, 4));
     if (!sc.h_cnt && hipHostMalloc(reinterpret_cast<void **>(&sc.h_cnt), 16, 0) != hipSuccess) {
@@ -128,6 +135,9 @@ int dict_rebuild(DictDev &D, uint64_t &slots, const DictIds *mark, int nmark, co
     GNS_HIP(hipMemcpyAsync(sc.h_cnt, sc.cnt, 4, hipMemcpyDeviceToHost, s));
     GNS_HIP(hipStreamSynchronize(s));
     const uint64_t live = sc.h_cnt[0];
+    // growth: the live set alone past a quarter of the table doubles it (the
+    // reclaim that follows a batch then leaves at least half the slots free)
+    while (grow_max && live > new_slots / 4 && new_slots < grow_max) new_slots *= 2;
     if (live > new_slots - new_slots / 8) {
         set_error("flow dictionary: %llu live flows do not fit %llu slots", (unsigned long long)live,
                   (unsigned long long)new_slots);

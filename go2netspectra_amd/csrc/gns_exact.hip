@@ -909,7 +909,7 @@ __global__ __launch_bounds__(256) void k_ex_permute(FlowState o, uint64_t slots,
     const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (s >= slots) return;
     const uint32_t t = remap[s];
-    if (t == GNS_ID_NONE) return;
+    if (t >= kDictMarked) return;  // dropped (GNS_ID_NONE) or never reinserted
     f.pkts[t] = o.pkts[s]; f.bytes[t] = o.bytes[s]; f.first[t] = o.first[s]; f.last[t] = o.last[s];
     f.start[t] = o.start[s]; f.end[t] = o.end[s];
 }
@@ -1472,10 +1472,11 @@ int gns_ex_counters(gns_ex *ex, uint64_t out[8]) {
     return GNS_OK;
 }
 
-int gns_ex_dict_stats(gns_ex *ex, uint64_t out[6]) {
+int gns_ex_dict_stats(gns_ex *ex, uint64_t out[8]) {
     if (!ex || !out) return GNS_E_ARG;
     out[0] = ex->n_grow; out[1] = 0; out[2] = ex->slots; out[3] = ex->claimed;
     out[4] = (uint64_t)(ex->grow_ms * 1000.0); out[5] = ex->n_retry;
+    out[6] = ex->slots; out[7] = ex->n_grow;
     return GNS_OK;
 }
 

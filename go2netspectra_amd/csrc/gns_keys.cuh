@@ -187,6 +187,9 @@ struct DictDev {
     uint32_t cap;      // claims beyond this abort the batch (the host reclaims and retries it)
 };
 
+// rebuild mark (gns_dict.hip); ids are slots below it
+constexpr uint32_t kDictMarked = 0xFFFFFFFEu;
+
 enum { DICT_FOUND = 0, DICT_PENDING = 1, DICT_FULL = 2, DICT_ABSENT = 3, DICT_CLAIMED = 4 };
 
 // Claim accounting, one global atomic per block: the block's claims are added

@@ -641,7 +641,7 @@ struct gns_ss {
     uint32_t *dctl = nullptr;
     DictScratch dsc;
     unsigned long long *stats_bak = nullptr;
-    uint64_t n_reclaim = 0, n_dropped = 0, last_live = 0, n_retry = 0;
+    uint64_t n_reclaim = 0, n_dropped = 0, last_live = 0, n_retry = 0, n_grow = 0;
     double reclaim_ms = 0.0;
     uint32_t epoch = 0;
     uint64_t pkt = 0;     // records inserted since create (RNG packet index)
@@ -852,17 +852,27 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
 }
 
 // Reclaim (gns_dict.hip): only flows that own a cell (keys[]) can be named by a
-// later comparison, query or heavy hitter; every other dictionary record is dropped.
-int ss_reclaim(gns_ss *ss) {
+// later comparison, query or heavy hitter; every other dictionary record is
+// dropped.  The table doubles while the live flows exceed a quarter of it (live
+// ids are at most d*w), and to at least min_slots.
+void ss_dict_limits(gns_ss *ss) {
+    ss->D.cap = (uint32_t)(ss->dict_slots - ss->dict_slots / 4);
+    ss->max_flows = std::max<uint64_t>(ss->max_flows, ss->dict_slots / 2);
+}
+
+int ss_reclaim(gns_ss *ss, uint64_t min_slots = 0) {
     const uint64_t cells = (uint64_t)ss->g.d * ss->g.w;
     DictIds ids{ss->keys, cells};
     const auto t0 = std::chrono::steady_clock::now();
-    const uint64_t before = ss->claimed;
+    const uint64_t before = ss->claimed, slots0 = ss->dict_slots;
     uint64_t live = 0;
-    GNS_TRY(dict_rebuild(ss->D, ss->dict_slots, &ids, 1, nullptr, &ids, 1, ss->dict_slots, ss->stream, ss->dsc, &live,
-                         nullptr));
+    GNS_TRY(dict_rebuild(ss->D, ss->dict_slots, &ids, 1, nullptr, &ids, 1,
+                         std::min(kDictMaxSlots, std::max(ss->dict_slots, min_slots)), ss->stream, ss->dsc, &live,
+                         nullptr, kDictMaxSlots));
     ss->reclaim_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     ss->n_reclaim++;
+    if (ss->dict_slots != slots0) ss->n_grow++;
+    ss_dict_limits(ss);
     ss->n_dropped += before > live ? before - live : 0;
     ss->claimed = live;
     ss->last_live = live;
@@ -896,13 +906,15 @@ int ss_batch(gns_ss *ss, const InputDesc &d, uint64_t m) {
 
 // A batch whose encodes overflow the dictionary is aborted in S3b, before any
 // state write: undo its counters, reclaim, re-run it once, then in halves (the
-// declared RNG is indexed by record, so the split does not change any draw).
+// declared RNG is indexed by record, so the split does not change any draw); a
+// piece of <= kSsChunk records that does not fit a fresh dictionary doubles the
+// table instead, so every stream is counted (super_spread.go:182-235 has no
+// failure mode).
 template <int KIND>
 int ss_batch_recover(gns_ss *ss, const InputDesc &d, uint64_t m, bool fresh) {
     if (m == 0) return GNS_OK;
     if (ss->full) {
-        set_error("flow dictionary full (max_flows %llu, %llu slots, %llu live flows); raise max_flows",
-                  (unsigned long long)ss->max_flows, (unsigned long long)ss->dict_slots,
+        set_error("flow dictionary full (%llu slots, %llu live flows)", (unsigned long long)ss->dict_slots,
                   (unsigned long long)ss->last_live);
         return GNS_E_FULL;
     }
@@ -918,21 +930,26 @@ int ss_batch_recover(gns_ss *ss, const InputDesc &d, uint64_t m, bool fresh) {
         GNS_HIP(hipMemcpyAsync(ss->stats, ss->stats_bak, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
                                ss->stream));
         GNS_HIP(hipMemsetAsync(ss->stats + 3, 0, sizeof(unsigned long long), ss->stream));
-        GNS_TRY(ss_reclaim(ss));
         ss->n_retry++;
         if (!fresh) {
+            GNS_TRY(ss_reclaim(ss));
             fresh = true;
             continue;
         }
-        break;
-    }
-    if (m <= kSsChunk) {
-        ss->full = true;
-        const unsigned long long one = 1;
-        GNS_HIP(hipMemcpy(ss->stats + 3, &one, sizeof(one), hipMemcpyHostToDevice));
-        set_error("flow dictionary full: %llu live flows plus one batch piece exceed max_flows %llu; raise max_flows",
-                  (unsigned long long)ss->last_live, (unsigned long long)ss->max_flows);
-        return GNS_E_FULL;
+        if (m > kSsChunk) {
+            GNS_TRY(ss_reclaim(ss));
+            break;
+        }
+        if (ss->dict_slots >= kDictMaxSlots) {
+            GNS_TRY(ss_reclaim(ss));
+            ss->full = true;
+            const unsigned long long one = 1;
+            GNS_HIP(hipMemcpy(ss->stats + 3, &one, sizeof(one), hipMemcpyHostToDevice));
+            set_error("flow dictionary full: %llu live flows plus one batch piece exceed %llu slots",
+                      (unsigned long long)ss->last_live, (unsigned long long)ss->dict_slots);
+            return GNS_E_FULL;
+        }
+        GNS_TRY(ss_reclaim(ss, ss->dict_slots * 2));
     }
     const uint64_t h = ((m / 2 + kSsChunk - 1) / kSsChunk) * kSsChunk;
     GNS_TRY(ss_batch_recover<KIND>(ss, d, h, true));
@@ -1053,7 +1070,7 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
             break;
         uint64_t slots = 1;
         const uint64_t mf = p->max_flows ? p->max_flows : (4ull << 20);
-        if (mf > (1ull << 30)) { set_error("max_flows > 2^30"); rc = GNS_E_ARG; break; }
+        if (2 * mf > kDictMaxSlots) { set_error("max_flows > 2^29"); rc = GNS_E_ARG; break; }
         ss->max_flows = mf;
         while (slots < 2 * mf) slots <<= 1;
         ss->dict_slots = slots;
@@ -1068,7 +1085,7 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
         if ((rc = dalloc_t(&ss->D.rec, slots * ss->D.RW)) != GNS_OK) break;
         if ((rc = dalloc_t(&ss->dctl, 4)) != GNS_OK || (rc = dalloc_t(&ss->stats_bak, 3)) != GNS_OK) break;
         ss->D.ctl = ss->dctl;
-        ss->D.cap = (uint32_t)(slots - slots / 4);
+        ss_dict_limits(ss);
         ss->bmax = p->batch_packets ? p->batch_packets : (8ull << 20);
         ss->bmax = std::min<uint64_t>(((ss->bmax + kSsChunk - 1) / kSsChunk) * kSsChunk, 1ull << kSsPktBits);
         ss->nblk_max = (uint32_t)(ss->bmax / kSsChunk);
@@ -1300,10 +1317,11 @@ int gns_ss_reclaim(gns_ss *ss) {
     return ss_reclaim(ss);
 }
 
-int gns_ss_dict_stats(gns_ss *ss, uint64_t out[6]) {
+int gns_ss_dict_stats(gns_ss *ss, uint64_t out[8]) {
     if (!ss || !out) return GNS_E_ARG;
     out[0] = ss->n_reclaim; out[1] = ss->n_dropped; out[2] = ss->last_live; out[3] = ss->claimed;
     out[4] = (uint64_t)(ss->reclaim_ms * 1000.0); out[5] = ss->n_retry;
+    out[6] = ss->dict_slots; out[7] = ss->n_grow;
     return GNS_OK;
 }
 

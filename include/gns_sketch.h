@@ -32,22 +32,27 @@
  *   - Flow keys are the reference EncodeFlow bytes (task.go:279-300): IP slots
  *     of 16 bytes with IPv4 left-aligned and zero padded, ports big-endian,
  *     protocol one byte; key_bytes <= 37 (task.go:74).
- *   - Flow dictionary (fingerprints are dense flow ids): memory
- *     is bounded like the reference's fixed-size sketch (count_min.go:66-81),
- *     whatever the number of distinct flows in a period.  Between device
- *     batches the sketches reclaim the flows no bucket names any more (and,
- *     for the exact aggregator, the table grows: exact/task.go:135-148 keeps
- *     every flow).  A batch whose new flows overflow the dictionary is not
- *     applied, the dictionary is rebuilt and the batch re-run (in halves for
- *     the sketches).  Live ids are at most 2*depth*width (Count-Min) or
- *     depth*width (SuperSpread), so with max_flows >= that + 16384 a sketch
- *     never returns GNS_E_FULL.  GNS_E_FULL (live flows plus one 16K-packet
- *     piece do not fit max_flows) ends the measurement period for the handle:
- *     every later insert returns it until gns_*_reset() (the reference's period
- *     reset, manager.go:179-193).  Count-Min's GNS_E_RANGE (from flush: too
- *     many oversize packets in one device batch) is sticky the same way; the
- *     sketch is not exact after it.
- */
+ *   - Flow dictionary (fingerprints are dense flow ids): the
+ *     reference's buckets hold key bytes (count_min.go:66-81), so Insert has no
+ *     failure mode whatever the traffic (count_min.go:94-157).  Here a bucket
+ *     names a dictionary slot; between device batches the sketches reclaim the
+ *     flows no bucket names any more and the table DOUBLES while the live flows
+ *     exceed a quarter of it (live ids are at most 2*depth*width for Count-Min,
+ *     depth*width for SuperSpread).  A batch whose new flows overflow the table
+ *     is not applied: the dictionary is rebuilt and the batch re-run (in
+ *     halves; a piece of 16K packets that still does not fit grows the table).
+ *     max_flows is only the INITIAL capacity.  GNS_E_FULL is left only for a
+ *     table of 2^30 slots (64 GB of 64-byte records) that cannot take one 16K
+ *     piece next to its live flows -- beyond any sketch with depth*width <=
+ *     2^27 -- and then holds until gns_*_reset() (the period reset,
+ *     manager.go:179-193).  The exact aggregator's table grows the same way.
+ *   - Sizes >= 2^16-1 take an overflow side table that grows with the batch
+ *     (no per-batch limit).
+ *   - Deviations from NewCountMin (count_min.go:47-60), which accepts any
+ *     geometry: depth <= 8 (GNS_E_ARG) and width < 2^25 (GNS_E_RANGE; at depth
+ *     8 also width <= 2^25 / bins limit, see gns_cm_create's message).  Batches
+ *     are capped at 2^31 / depth packets (longer inserts are split).
+  */
 #ifndef GNS_SKETCH_H
 #define GNS_SKETCH_H
 #include <stddef.h>
@@ -62,8 +67,8 @@ typedef enum gns_status {
     GNS_E_ARG = -1,    /* bad argument (log.Fatalf / panic sites in the reference) */
     GNS_E_HIP = -2,    /* HIP runtime error */
     GNS_E_OOM = -3,    /* device allocation failed */
-    GNS_E_FULL = -4,   /* flow dictionary capacity exhausted (raise max_flows) */
-    GNS_E_RANGE = -5,  /* batch exceeds an internal limit (see message) */
+    GNS_E_FULL = -4,   /* flow dictionary at its 2^30-slot limit (see the rules above) */
+    GNS_E_RANGE = -5,  /* geometry beyond a documented limit (see message) */
     GNS_E_NODEV = -6   /* no usable HIP device */
 } gns_status;
 
@@ -105,8 +110,8 @@ typedef struct gns_cm_params {
     const uint32_t *seeds;                    /* depth row seeds (count_min.go:61-64 draws
                                                  them with rand.Uint32; here injected).
                                                  NULL -> splitmix64(0x9747B28C) stream */
-    uint64_t max_flows;                       /* flow dictionary capacity (live + new flows of a
-                                                 batch; dead flows are reclaimed); 0 -> 4M */
+    uint64_t max_flows;                       /* INITIAL flow dictionary capacity (it grows with
+                                                 the live flows; dead flows are reclaimed); 0 -> 4M */
     uint64_t batch_packets;                   /* device batch size; 0 -> 16M packets */
     int device;                               /* HIP device ordinal */
     uint32_t bucket_lo, bucket_hi;            /* bucket-range slice (SURVEY §8e exact global
@@ -160,8 +165,9 @@ int gns_cm_stats(gns_cm *cm, uint64_t stats[4]);
 int gns_cm_counters(gns_cm *cm, uint64_t out[8]);
 /* flow dictionary: [0] reclaims, [1] dead flows dropped, [2] live flows after the
  * last reclaim, [3] claimed slots now, [4] reclaim time (us, host clock incl. the
- * rebuild's device work), [5] batches re-run after a dictionary overflow */
-int gns_cm_dict_stats(gns_cm *cm, uint64_t out[6]);
+ * rebuild's device work), [5] batches re-run after a dictionary overflow,
+ * [6] dictionary slots now, [7] table growths */
+int gns_cm_dict_stats(gns_cm *cm, uint64_t out[8]);
 /* reclaim now (e.g. at a window boundary; inserts also reclaim on their own) */
 int gns_cm_reclaim(gns_cm *cm);
 int gns_cm_set_timing(gns_cm *cm, int on);
@@ -205,17 +211,13 @@ typedef struct gns_ss_params {
     uint64_t hll_master;               /* derives each GeneralHLL's seeds[0..1] */
     uint64_t rng_seed;                 /* keys the declared generator replacing rand.Float64 */
     uint64_t batch_packets;
-    uint64_t max_flows;                /* flow dictionary capacity; 0 -> 4M (2^22) */
+    uint64_t max_flows;                /* initial flow dictionary capacity (grows); 0 -> 4M */
     int device;
 } gns_ss_params;
 
-/* The SuperSpread flow dictionary (max_flows) holds the flows that ever encoded
- * in the period (only they can own a cell, so only they can be named by a key,
- * a query or a heavy hitter).  An insert that would exceed it returns
- * GNS_E_FULL naming max_flows; the device batch (<= batch_packets records) in
- * which it happened is not applied, earlier device batches of the same call
- * are.  gns_ss_counters() out[6] (records) tells how far the stream got, and
- * gns_ss_reset starts a new period with an empty dictionary. */
+/* The SuperSpread flow dictionary holds the flows that own a cell (only they
+ * can be named by a key, a query or a heavy hitter); it is reclaimed and grows
+ * like Count-Min's (see the rules above), so inserts do not fail on it. */
 int gns_ss_create(const gns_ss_params *p, gns_ss **out);
 int gns_ss_destroy(gns_ss *ss);
 int gns_ss_insert_keys(gns_ss *ss, const uint8_t *flows, uint32_t fstride, const uint8_t *elems,
@@ -233,7 +235,7 @@ int gns_ss_stats(gns_ss *ss, uint64_t stats[4]);
 /* out[8]: inserted, dropped, unsupported, dictionary full, HLL candidates
  * (lz above the batch-entry register), HLL encodes, records, device batches */
 int gns_ss_counters(gns_ss *ss, uint64_t out[8]);
-int gns_ss_dict_stats(gns_ss *ss, uint64_t out[6]);  /* as gns_cm_dict_stats */
+int gns_ss_dict_stats(gns_ss *ss, uint64_t out[8]);  /* as gns_cm_dict_stats */
 int gns_ss_reclaim(gns_ss *ss);
 int gns_ss_set_timing(gns_ss *ss, int on);
 int gns_ss_stage_times(gns_ss *ss, double ms[8], uint64_t launches[8], int reset);
@@ -362,8 +364,8 @@ int gns_ex_reset(gns_ex *ex);
 /* out[8]: inserted, dropped, unsupported, dictionary full, flows, records, batches, 0 */
 int gns_ex_counters(gns_ex *ex, uint64_t out[8]);
 /* [0] table growths, [1] 0, [2] slots, [3] claimed slots, [4] growth time (us),
- * [5] batches re-run after a dictionary overflow */
-int gns_ex_dict_stats(gns_ex *ex, uint64_t out[6]);
+ * [5] batches re-run after a dictionary overflow, [6] slots, [7] growths */
+int gns_ex_dict_stats(gns_ex *ex, uint64_t out[8]);
 int gns_ex_set_timing(gns_ex *ex, int on);
 /* stages: 0 extract, 1 resolve, 2 aggregate, 3 timestamps, 5 total */
 int gns_ex_stage_times(gns_ex *ex, double ms[8], uint64_t launches[8], int reset);

@@ -338,3 +338,24 @@ def thrift_messages(rng, n, nflows=500, bad_frac=0.1, v6_frac=0.3):
                 m = bytes(rng.integers(0, 256, int(rng.integers(1, 80)), dtype=np.uint8))
         msgs.append(m)
     return msgs
+
+
+def pcapgen_records(rng, n: int):
+    """scripts/pcapgen/main.go:17-97-shaped traffic as 64-byte records, vectorized:
+    Ethernet / IPv4 (IHL 5) / TCP SYN with uniform random addresses and ports, so
+    practically every packet is a new flow; frames of 104-1503 bytes (wire length)."""
+    hdr = np.zeros((n, 64), np.uint8)
+    hdr[:, 0:6] = np.frombuffer(b"\x00\x66\x77\x88\x99\xaa", np.uint8)
+    hdr[:, 6:12] = np.frombuffer(b"\x00\x11\x22\x33\x44\x55", np.uint8)
+    hdr[:, 12] = 0x08
+    wl = rng.integers(104, 1504, n).astype(np.uint32)
+    tot = wl - 14
+    hdr[:, 14] = 0x45
+    hdr[:, 16] = (tot >> 8).astype(np.uint8)
+    hdr[:, 17] = (tot & 0xFF).astype(np.uint8)
+    hdr[:, 22] = 64
+    hdr[:, 23] = 6
+    hdr[:, 26:38] = rng.integers(0, 256, (n, 12), dtype=np.uint8)  # src, dst, sport, dport
+    hdr[:, 46] = 0x50  # data offset 5
+    hdr[:, 47] = 0x02  # SYN
+    return hdr, wl
