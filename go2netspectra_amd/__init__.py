@@ -10,15 +10,15 @@ from ._lib import GnsError, build, load
 from .config import Config, ExactTaskDef, SketchTaskDef, load_config, parse_config
 from .exact import ExactAggregator, ExactTask, NewExact, SnapshotData
 from .factory import Manager, TaskGroup, create, register_aggregator
-from .packets import (HeaderBatch, PacketBatch, SyntheticTraffic, ip_slot, read_pcap, write_pcap, write_pcapgen,
-                      write_pcapng)
+from .packets import (HeaderBatch, PacketBatch, SyntheticTraffic, compact_headers, ip_slot, read_pcap,
+                      read_pcap_compact, write_pcap, write_pcapgen, write_pcapng)
 from .sketch import CountMin, CountMinView, HeavyCount, HeavyRecord, HeavySize, SuperSpread
 from .task import New, SketchTask, decode_flow
 
 __all__ = [
     "GnsError", "build", "load", "Config", "SketchTaskDef", "load_config", "parse_config", "Manager",
     "TaskGroup", "create", "register_aggregator", "HeaderBatch", "PacketBatch", "SyntheticTraffic",
-    "ip_slot", "read_pcap", "write_pcap", "write_pcapgen", "write_pcapng", "CountMin", "CountMinView", "HeavyCount", "HeavyRecord", "HeavySize",
+    "ip_slot", "read_pcap", "read_pcap_compact", "compact_headers", "write_pcap", "write_pcapgen", "write_pcapng", "CountMin", "CountMinView", "HeavyCount", "HeavyRecord", "HeavySize",
     "SuperSpread", "New", "SketchTask", "decode_flow", "ExactTaskDef", "ExactAggregator", "ExactTask",
     "NewExact", "SnapshotData",
 ]

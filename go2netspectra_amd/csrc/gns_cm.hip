@@ -2635,6 +2635,8 @@ struct gns_cm {
     // cstream while batch i computes on `stream` (events order the reuse)
     uint8_t *stage[2] = {nullptr, nullptr};
     size_t stage_bytes[2] = {0, 0};
+    uint32_t *side_dev = nullptr;         // staged side records of a compact host insert
+    uint64_t side_n = 0;
     hipStream_t cstream = nullptr;
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_used[2] = {nullptr, nullptr};
     StageTimer timer;
@@ -2696,7 +2698,7 @@ int cm_free_all(gns_cm *cm) {
     dfree(cm->pend[0]); dfree(cm->pend[1]); dfree(cm->pcnt[0]); dfree(cm->pcnt[1]);
     dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
     dfree(cm->entries); dfree(cm->entries2); dfree(cm->soff); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats);
-    dfree(cm->stage[0]); dfree(cm->stage[1]);
+    dfree(cm->stage[0]); dfree(cm->stage[1]); dfree(cm->side_dev);
     for (int i = 0; i < 2; i++) {
         if (cm->ev_copied[i]) (void)hipEventDestroy(cm->ev_copied[i]);
         if (cm->ev_used[i]) (void)hipEventDestroy(cm->ev_used[i]);
@@ -2789,7 +2791,12 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.stats = cm->stats;
         ScopedStage st(cm->timer, 0);
         const size_t lds = extract_lds_bytes(g.nbins_all, g.d);
-        if (lds > kExLdsSmall) {  // deep / wide sketch: one large block per CU
+        if constexpr (KIND == IN_REC16) {  // PCIe-bound host path: runtime key width and depth
+            if (lds > kExLdsSmall)
+                hipLaunchKernelGGL((k_extract<KIND, MODE, 0, 0, 1024>), dim3(nblk), dim3(1024), lds, s, a);
+            else
+                hipLaunchKernelGGL((k_extract<KIND, MODE, 0, 0, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
+        } else if (lds > kExLdsSmall) {  // deep / wide sketch: one large block per CU
             // configs[4] (d=8, 5-tuple): the plain loop, two 512-thread blocks per CU
             // (see kC5Threads)
             if (cm->K == 37 && g.d == 8)
@@ -2965,6 +2972,7 @@ InputDesc advance(const InputDesc &in, uint64_t off) {
     if (d.dport) d.dport += off;
     if (d.proto) d.proto += off;
     if (d.keys) d.keys += off * d.stride;
+    if (d.rec16) d.rec16 += off * 4;
     if (d.sizes) d.sizes += off;
     return d;
 }
@@ -3042,25 +3050,27 @@ int cm_batch_recover(gns_cm *cm, const InputDesc &d, uint64_t m, bool fresh) {
 // after the batch that last read b has finished; d points into the buffer.
 int stage_host_batch(gns_cm *cm, int b, const InputDesc &in, uint64_t off, uint64_t m, InputDesc &d) {
     d = in;
-    const void *src[7] = {in.hdr ? (const void *)(in.hdr + off * 16) : nullptr,
-                          in.src16 ? (const void *)(in.src16 + off * 16) : nullptr,
-                          in.dst16 ? (const void *)(in.dst16 + off * 16) : nullptr,
-                          in.sport ? (const void *)(in.sport + off) : nullptr,
-                          in.dport ? (const void *)(in.dport + off) : nullptr,
-                          in.proto ? (const void *)(in.proto + off) : nullptr,
-                          in.keys ? (const void *)(in.keys + off * in.stride) : nullptr};
-    const size_t bytes[7] = {in.hdr ? m * 64 : 0, in.src16 ? m * 16 : 0, in.dst16 ? m * 16 : 0,
-                             in.sport ? m * 2 : 0, in.dport ? m * 2 : 0, in.proto ? m : 0,
-                             in.keys ? m * in.stride : 0};
+    constexpr int NA = 8;
+    const void *src[NA] = {in.hdr ? (const void *)(in.hdr + off * 16) : nullptr,
+                           in.src16 ? (const void *)(in.src16 + off * 16) : nullptr,
+                           in.dst16 ? (const void *)(in.dst16 + off * 16) : nullptr,
+                           in.sport ? (const void *)(in.sport + off) : nullptr,
+                           in.dport ? (const void *)(in.dport + off) : nullptr,
+                           in.proto ? (const void *)(in.proto + off) : nullptr,
+                           in.keys ? (const void *)(in.keys + off * in.stride) : nullptr,
+                           in.rec16 ? (const void *)(in.rec16 + off * 4) : nullptr};
+    const size_t bytes[NA] = {in.hdr ? m * 64 : 0, in.src16 ? m * 16 : 0, in.dst16 ? m * 16 : 0,
+                              in.sport ? m * 2 : 0, in.dport ? m * 2 : 0, in.proto ? m : 0,
+                              in.keys ? m * in.stride : 0, in.rec16 ? m * 16 : 0};
     size_t tot = (m * 4 + 15) & ~size_t(15);
-    for (int i = 0; i < 7; i++) tot += (bytes[i] + 15) & ~size_t(15);
+    for (int i = 0; i < NA; i++) tot += (bytes[i] + 15) & ~size_t(15);
     GNS_TRY(stage_reserve(cm, b, tot));
     GNS_HIP(hipStreamWaitEvent(cm->cstream, cm->ev_used[b], 0));
     uint8_t *p = cm->stage[b];
-    const void **dst[7] = {(const void **)&d.hdr, (const void **)&d.src16, (const void **)&d.dst16,
-                           (const void **)&d.sport, (const void **)&d.dport, (const void **)&d.proto,
-                           (const void **)&d.keys};
-    for (int i = 0; i < 7; i++) {
+    const void **dst[NA] = {(const void **)&d.hdr, (const void **)&d.src16, (const void **)&d.dst16,
+                            (const void **)&d.sport, (const void **)&d.dport, (const void **)&d.proto,
+                            (const void **)&d.keys, (const void **)&d.rec16};
+    for (int i = 0; i < NA; i++) {
         if (!bytes[i]) continue;
         GNS_HIP(hipMemcpyAsync(p, src[i], bytes[i], hipMemcpyHostToDevice, cm->cstream));
         *dst[i] = p;
@@ -3308,6 +3318,31 @@ int gns_cm_insert_headers(gns_cm *cm, const uint8_t *hdr, const uint32_t *wirele
     in.hdr = reinterpret_cast<const uint32_t *>(hdr);
     in.sizes = wirelen;
     return cm_insert<IN_HDR>(cm, in, n, where);
+}
+
+int gns_cm_insert_compact(gns_cm *cm, const uint8_t *rec16, const uint32_t *wirelen, uint64_t n,
+                          const uint8_t *side64, uint64_t n_side, gns_mem where) {
+    if (!cm || (n && (!rec16 || !wirelen)) || (n_side && !side64)) { set_error("null argument"); return GNS_E_ARG; }
+    InputDesc in{};
+    in.rec16 = reinterpret_cast<const uint32_t *>(rec16);
+    in.sizes = wirelen;
+    in.side = reinterpret_cast<const uint32_t *>(side64);
+    if (where == GNS_MEM_HOST && n_side) {
+        // the side records of the whole call, staged once (escapes index them globally);
+        // the batches of the previous call may still read the buffer
+        GNS_TRY(set_dev(cm));
+        GNS_HIP(hipStreamSynchronize(cm->stream));
+        if (cm->side_n < n_side) {
+            dfree(cm->side_dev);
+            cm->side_dev = nullptr;
+            cm->side_n = 0;
+            GNS_TRY(dalloc_t(&cm->side_dev, n_side * 16));
+            cm->side_n = n_side;
+        }
+        GNS_HIP(hipMemcpy(cm->side_dev, side64, n_side * 64, hipMemcpyHostToDevice));
+        in.side = cm->side_dev;
+    }
+    return cm_insert<IN_REC16>(cm, in, n, where);
 }
 
 int gns_cm_flush(gns_cm *cm) {

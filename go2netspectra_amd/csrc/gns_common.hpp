@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -123,6 +124,9 @@ constexpr uint64_t kDictMaxSlots = 1ull << 30;
 // parser.  Returns 0 = copied verbatim (device fast-path shape), 1 = decoded
 // into a pre-parsed 0x88B5 record, 2 = no IP layer (a record the device drops).
 int frame_record(const uint8_t *frame, uint32_t caplen, uint32_t wirelen, uint8_t *rec);
+// frame_record's record (and its return code) -> compact 16-byte record; returns
+// the class (kRecSide: the caller stores the side index in word 0)
+int compact_record(int code, const uint8_t *rec, uint8_t *out16);
 
 inline uint32_t ceil_log2(uint64_t x) {
     uint32_t b = 0;

@@ -516,3 +516,42 @@ extern "C" int gns_frame_record(const uint8_t *frame, uint32_t caplen, uint32_t 
     if (!frame || !rec64) { gns::set_error("null argument"); return GNS_E_ARG; }
     return gns::frame_record(frame, caplen, wirelen, rec64);
 }
+
+// Compact host record (IN_REC16, gns_keys.cuh) of a record frame_record wrote
+// (code = its return value): the IPv4 tuple exactly as the device parser reads
+// it from that record -- a verbatim frame has the fast-path shape, so the tuple
+// sits at fixed offsets (parse_fast_ipv4); a 0x88B5 record carries it as
+// fields (parse_record) -- or the drop class, or kRecSide when the tuple does
+// not fit (IPv6 addresses): the caller then appends the 64-byte record to the
+// side array and stores its index in word 0.
+namespace gns {
+int compact_record(int code, const uint8_t *rec, uint8_t *out16) {
+    memset(out16, 0, 16);
+    if (code == 0) {
+        memcpy(out16, rec + 26, 4);      // IPv4 source (left-aligned slot)
+        memcpy(out16 + 4, rec + 30, 4);  // destination
+        memcpy(out16 + 8, rec + 34, 4);  // ports, big-endian bytes
+        out16[12] = rec[23];
+        out16[14] = 4;
+        out16[15] = 4;
+        return gns::kRecTuple;
+    }
+    if (code == 2) {
+        out16[13] = gns::kRecDrop;
+        return gns::kRecDrop;
+    }
+    bool narrow = rec[14] == 1;
+    for (int i = 4; i < 16 && narrow; i++) narrow = rec[16 + i] == 0 && rec[32 + i] == 0;
+    if (!narrow) {
+        out16[13] = gns::kRecSide;
+        return gns::kRecSide;
+    }
+    memcpy(out16, rec + 16, 4);
+    memcpy(out16 + 4, rec + 32, 4);
+    memcpy(out16 + 8, rec + 48, 4);
+    out16[12] = rec[52];
+    out16[15] = rec[15];
+    out16[14] = rec[53] ? rec[53] : rec[15];
+    return gns::kRecTuple;
+}
+}  // namespace gns

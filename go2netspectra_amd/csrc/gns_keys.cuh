@@ -15,7 +15,18 @@
 
 namespace gns {
 
-enum InputKind { IN_HDR = 0, IN_TUPLE = 1, IN_KEYS = 2 };
+enum InputKind { IN_HDR = 0, IN_TUPLE = 1, IN_KEYS = 2, IN_REC16 = 3 };
+
+// Compact host record (IN_REC16): 16 bytes + the wire length,
+// for the PCIe-bound host-inclusive path.  Words = canonical tuple words
+// {tw[0], tw[4], tw[8], tw[9]}: IPv4 source / destination (left-aligned
+// slots), ports, protocol | IP versions << 16.  Tuple byte 37 (bits 8..15 of
+// word 3) is zero in every tuple and carries the record class instead:
+//   kRecTuple  the IPv4 tuple above;
+//   kRecDrop   no IP layer (parser.go:48-49: not counted);
+//   kRecSide   anything else (IPv6, unsupported shapes): word 0 indexes a
+//              64-byte record in the side array, parsed as gns_*_insert_headers would.
+enum { kRecTuple = 0, kRecDrop = 1, kRecSide = 2 };
 
 struct InputDesc {
     const uint32_t *hdr;      // IN_HDR: n*16 words
@@ -27,6 +38,8 @@ struct InputDesc {
     const uint8_t *keys;      // IN_KEYS: flow keys, n*stride bytes
     const uint8_t *keys2;     // IN_KEYS: element keys (SuperSpread)
     const uint32_t *sizes;    // per-packet size (wirelen / length / sizes)
+    const uint32_t *rec16;    // IN_REC16: n*4 words
+    const uint32_t *side;     // IN_REC16: 64-byte records named by kRecSide escapes
     uint32_t stride, stride2;
     uint32_t aligned;         // bit0: keys word-loadable, bit1: keys2 word-loadable
 };
@@ -116,6 +129,26 @@ __device__ __forceinline__ int load_tuple(const InputDesc &in, uint64_t p, uint3
             w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
         }
         return parse_record_fast(w, in.sizes[p], true, tw);
+    } else if constexpr (KIND == IN_REC16) {
+        const uint4 r = *reinterpret_cast<const uint4 *>(in.rec16 + p * 4);
+        const uint32_t cls = (r.w >> 8) & 0xFFu;
+        tw[0] = r.x; tw[1] = 0; tw[2] = 0; tw[3] = 0;
+        tw[4] = r.y; tw[5] = 0; tw[6] = 0; tw[7] = 0;
+        tw[8] = r.z; tw[9] = r.w;
+        if (cls == kRecTuple) return PARSE_OK;
+        if (cls == kRecDrop) return PARSE_DROP;
+        int st = PARSE_UNSUPPORTED;
+        if (cls == kRecSide) {
+            uint32_t w[16];
+            const uint4 *q = reinterpret_cast<const uint4 *>(in.side + (uint64_t)r.x * 16);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint4 v = q[i];
+                w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+            }
+            st = parse_record(w, in.sizes[p], tw);
+        }
+        return st;
     } else {
         const uint4 s = *reinterpret_cast<const uint4 *>(in.src16 + p * 16);
         const uint4 d = *reinterpret_cast<const uint4 *>(in.dst16 + p * 16);

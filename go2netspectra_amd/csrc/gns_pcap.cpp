@@ -62,12 +62,17 @@ struct Sink {  // record output (the first `cap` packets) and counters
     int64_t *ts_ns;
     uint64_t cap, written = 0, n = 0;
     uint64_t kinds[3] = {0, 0, 0};
+    // compact mode (gns_pack_pcap_compact): 16-byte records into rec16, the
+    // records that do not fit into side64 (side_cap of them; side_need counts all)
+    uint8_t *rec16 = nullptr, *side64 = nullptr;
+    uint64_t side_cap = 0, side_need = 0;
     std::vector<Desc> slab;
     int nthreads = 1;
     static constexpr size_t kSlab = 1u << 17;
+    bool out_ok() const { return (hdr || rec16) && wirelen; }
     void emit(const uint8_t *data, uint32_t incl, uint32_t orig, int64_t ts) {
         n++;
-        if (written + slab.size() >= cap || !hdr || !wirelen) return;
+        if (written + slab.size() >= cap || !out_ok()) return;
         slab.push_back(Desc{data, incl, orig, ts});
         if (slab.size() == kSlab) flush();
     }
@@ -76,12 +81,21 @@ struct Sink {  // record output (the first `cap` packets) and counters
         if (!m) return;
         const int T = (int)std::min<size_t>((size_t)nthreads, (m + 4095) / 4096);
         uint64_t part[64][3] = {};
+        std::vector<std::vector<uint8_t>> side(T);   // per thread: its side records, in order
+        std::vector<std::vector<uint64_t>> at(T);    // and the packets that name them
         auto work = [&](int t) {
             const size_t i0 = m * t / T, i1 = m * (t + 1) / T;
+            uint8_t tmp[64];
             for (size_t i = i0; i < i1; i++) {
                 const Desc &dsc = slab[i];
                 const uint64_t j = written + i;
-                part[t][gns::frame_record(dsc.frame, dsc.incl, dsc.orig, hdr + j * 64)]++;
+                uint8_t *r = rec16 ? tmp : hdr + j * 64;
+                const int code = gns::frame_record(dsc.frame, dsc.incl, dsc.orig, r);
+                part[t][code]++;
+                if (rec16 && gns::compact_record(code, r, rec16 + j * 16) == gns::kRecSide) {
+                    side[t].insert(side[t].end(), r, r + 64);
+                    at[t].push_back(j);
+                }
                 wirelen[j] = dsc.orig;
                 if (ts_ns) ts_ns[j] = dsc.ts;
             }
@@ -95,8 +109,15 @@ struct Sink {  // record output (the first `cap` packets) and counters
             work(0);
             for (auto &x : th) x.join();
         }
-        for (int t = 0; t < T; t++)
+        for (int t = 0; t < T; t++) {
             for (int k = 0; k < 3; k++) kinds[k] += part[t][k];
+            for (size_t q = 0; q < at[t].size(); q++) {  // side indices in file order
+                const uint64_t idx = side_need++;
+                const uint32_t w0 = (uint32_t)idx;
+                memcpy(rec16 + at[t][q] * 16, &w0, 4);
+                if (idx < side_cap && side64) memcpy(side64 + idx * 64, side[t].data() + q * 64, 64);
+            }
+        }
         written += m;
         slab.clear();
     }
@@ -296,18 +317,16 @@ struct Capture {
 
 }  // namespace
 
-// ts_ns: capture timestamps in ns (gopacket's pcap handle opens files with
-// nanosecond precision: usec files scale by 1000, nsec files as recorded).
-extern "C" int64_t gns_pack_pcap_ts(const char *path, uint8_t *hdr, uint32_t *wirelen, int64_t *ts_ns,
-                                    uint64_t cap, uint64_t *total) {
+namespace {
+
+int64_t pack(const char *path, Sink &o, uint64_t *total) {
     using gns::set_error;
     if (!path) { set_error("null path"); return GNS_E_ARG; }
     Capture cf;
     GNS_TRY(cf.open_file(path));
     Cursor f{cf.data(), cf.size, 0};
-    Sink o{hdr, wirelen, ts_ns, cap};
     o.nthreads = pack_threads();
-    if (cap && hdr && wirelen) o.slab.reserve(std::min<uint64_t>(cap, Sink::kSlab));
+    if (o.cap && o.out_ok()) o.slab.reserve(std::min<uint64_t>(o.cap, Sink::kSlab));
     memset(t_counts, 0, sizeof t_counts);
     int rc;
     const uint8_t *gh = f.take(8);
@@ -329,6 +348,35 @@ extern "C" int64_t gns_pack_pcap_ts(const char *path, uint8_t *hdr, uint32_t *wi
     memcpy(t_counts, o.kinds, sizeof t_counts);
     if (total) *total = o.n;
     return (int64_t)o.written;
+}
+
+}  // namespace
+
+// ts_ns: capture timestamps in ns (gopacket's pcap handle opens files with
+// nanosecond precision: usec files scale by 1000, nsec files as recorded).
+extern "C" int64_t gns_pack_pcap_ts(const char *path, uint8_t *hdr, uint32_t *wirelen, int64_t *ts_ns,
+                                    uint64_t cap, uint64_t *total) {
+    Sink o{hdr, wirelen, ts_ns, cap};
+    return pack(path, o, total);
+}
+
+// compact records (IN_REC16) for the PCIe-bound host path: 16 bytes + the wire
+// length per packet, the frames whose tuple is not an IPv4 one as 64-byte side
+// records (GNS_E_RANGE when side_cap is too small: *n_side = the number needed)
+extern "C" int64_t gns_pack_pcap_compact(const char *path, uint8_t *rec16, uint32_t *wirelen, uint64_t cap,
+                                         uint8_t *side64, uint64_t side_cap, uint64_t *n_side, uint64_t *total) {
+    Sink o{nullptr, wirelen, nullptr, cap};
+    o.rec16 = rec16;
+    o.side64 = side64;
+    o.side_cap = side_cap;
+    const int64_t r = pack(path, o, total);
+    if (n_side) *n_side = o.side_need;
+    if (r >= 0 && o.side_need > side_cap) {
+        gns::set_error("%s: %llu side records needed, room for %llu", path, (unsigned long long)o.side_need,
+                       (unsigned long long)side_cap);
+        return GNS_E_RANGE;
+    }
+    return r;
 }
 
 extern "C" int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirelen, uint64_t cap,

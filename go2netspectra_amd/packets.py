@@ -149,6 +149,50 @@ def read_pcap(path: str, limit: Optional[int] = None) -> HeaderBatch:
         cap = total.value
 
 
+def read_pcap_compact(path: str, limit: Optional[int] = None):
+    """pcap or pcapng -> compact records (rec16 [n, 16], wirelen [n], side [n_side, 64]);
+    see include/gns_sketch.h gns_cm_insert_compact."""
+    L = _lib.load()
+    total, nside = ct.c_uint64(0), ct.c_uint64(0)
+    cap = limit if limit is not None else max(1, (os.path.getsize(path) - 24) // 76 + 1)
+    side_cap = max(1024, cap // 64)
+    while True:
+        rec = np.empty((cap, 16), np.uint8)
+        wl = np.empty(cap, np.uint32)
+        side = np.empty((side_cap, 64), np.uint8)
+        r = L.gns_pack_pcap_compact(os.fsencode(path), rec.ctypes.data, wl.ctypes.data, cap, side.ctypes.data,
+                                    side_cap, ct.byref(nside), ct.byref(total))
+        if r == _lib.GNS_E_RANGE and nside.value > side_cap:
+            side_cap = nside.value
+            continue
+        if r < 0:
+            check(int(r))
+        if limit is not None or total.value <= cap:
+            return rec[:r], wl[:r], side[:nside.value]
+        cap = total.value
+
+
+def compact_headers(hdr, wirelen):
+    """Device-resident 64-byte records (torch uint8 [n, 64] + wire lengths) -> compact
+    records on the same device: (rec16 [n, 16] uint8, side [n_side, 64] uint8)."""
+    import torch
+    L = _lib.load()
+    n = int(wirelen.shape[0])
+    _lib.device_ready(hdr, wirelen)
+    rec = torch.empty((n, 16), dtype=torch.uint8, device=hdr.device)
+    cap = max(1024, n // 256)
+    while True:
+        side = torch.empty((cap, 64), dtype=torch.uint8, device=hdr.device)
+        ns = ct.c_uint64(0)
+        r = L.gns_compact_headers(hdr.data_ptr(), wirelen.data_ptr(), n, rec.data_ptr(), side.data_ptr(), cap,
+                                  ct.byref(ns), hdr.device.index or 0)
+        if r == _lib.GNS_E_RANGE:
+            cap = ns.value
+            continue
+        check(r)
+        return rec, side[:ns.value]
+
+
 def write_pcap(path: str, frames, wirelens=None, snaplen: int = 65536, ts_ns=None) -> None:
     """Classic little-endian microsecond pcap writer (tests / tools)."""
     import struct

@@ -230,6 +230,20 @@ class CountMin:
         n = int(wirelen.shape[0])
         check(self._L.gns_cm_insert_headers(self._h, _ptr(hdr), _ptr(wirelen), n, where))
 
+    def insert_compact(self, rec16, wirelen, side=None) -> None:
+        """Compact 16-byte records [n, 16] + wire lengths [n] (+ the 64-byte side
+        records their escapes name, [n_side, 64]): the same stream as the 64-byte
+        records they were made from (packets.compact_headers / read_pcap_compact)."""
+        where = _where(rec16, wirelen, side)
+        if where == _lib.MEM_HOST:
+            rec16 = _host(rec16, np.uint8)
+            wirelen = _host(wirelen, np.uint32)
+            side = _host(side, np.uint8) if side is not None else None
+        n = int(wirelen.shape[0])
+        ns = int(side.shape[0]) if side is not None else 0
+        check(self._L.gns_cm_insert_compact(self._h, _ptr(rec16), _ptr(wirelen), n,
+                                            _ptr(side) if ns else None, ns, where))
+
     def flush(self) -> None:
         check(self._L.gns_cm_flush(self._h))
 

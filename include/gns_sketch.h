@@ -138,6 +138,19 @@ int gns_cm_insert_tuples(gns_cm *cm, const gns_tuples *t, uint64_t n, gns_mem wh
  * itself (gns_frame_record). */
 int gns_cm_insert_headers(gns_cm *cm, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
                           gns_mem where);
+/* Compact records (the PCIe-bound host-inclusive path): rec16[n*16]
+ * = the canonical tuple the device parser derives from a 64-byte record, in 16
+ * bytes + wirelen[n] (20 B/packet instead of 68):
+ *   word 0 IPv4 source, word 1 IPv4 destination (the left-aligned slots' first
+ *   4 bytes), word 2 ports (big-endian bytes), word 3 = protocol | class << 8 |
+ *   destination IP version << 16 | source IP version << 24;
+ *   class 0 = that tuple, 1 = no IP layer (not counted, parser.go:48-49),
+ *   2 = escape: word 0 indexes side64[n_side*64], a 64-byte record parsed as
+ *   gns_cm_insert_headers parses it (IPv6 tuples, unsupported shapes).
+ * The insert equals gns_cm_insert_headers of the records the compact form was
+ * made from.  Producers: gns_pack_pcap_compact (host), gns_compact_headers (device). */
+int gns_cm_insert_compact(gns_cm *cm, const uint8_t *rec16, const uint32_t *wirelen, uint64_t n,
+                          const uint8_t *side64, uint64_t n_side, gns_mem where);
 int gns_cm_flush(gns_cm *cm);
 /* out[i] = count<<32 | size, count_min.go:160-174 */
 int gns_cm_query(gns_cm *cm, const uint8_t *keys, uint32_t stride, uint64_t n, uint64_t *out);
@@ -271,6 +284,16 @@ int gns_synth_flows(gns_synth *s, uint32_t *n_flows);
  * a negative status; *total = packets in the file. */
 int64_t gns_pack_pcap(const char *path, uint8_t *hdr, uint32_t *wirelen, uint64_t cap,
                       uint64_t *total);
+
+/* as gns_pack_pcap, into compact records (see gns_cm_insert_compact): frames whose
+ * tuple is not an IPv4 one go to side64 (side_cap records; *n_side = the number
+ * written, or needed: GNS_E_RANGE when it exceeds side_cap) */
+int64_t gns_pack_pcap_compact(const char *path, uint8_t *rec16, uint32_t *wirelen, uint64_t cap,
+                              uint8_t *side64, uint64_t side_cap, uint64_t *n_side, uint64_t *total);
+/* 64-byte records -> compact records on the device (all pointers DEVICE memory of
+ * `device`; inputs complete before the call); *n_side as above */
+int gns_compact_headers(const uint8_t *hdr, const uint32_t *wirelen, uint64_t n, uint8_t *rec16,
+                        uint8_t *side64, uint64_t side_cap, uint64_t *n_side, int device);
 
 /* [0] frames copied verbatim, [1] frames decoded on the host into 0x88B5
  * records, [2] frames without an IP layer, of the calling thread's last

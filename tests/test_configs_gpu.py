@@ -217,3 +217,22 @@ def test_encapsulated_capture_decoded_on_host(gpu, oracle, tmp_path):
     assert_same_list([(x.Flow, x.Count) for x in hh.Count], orc.heavy("count"))
     assert_same_list([(x.Flow, x.Size) for x in hh.Size], orc.heavy("size"))
     assert len(hh.Count) > 0 and len(hh.Size) > 0
+    # the same capture as compact records (host packer), staged in several device batches,
+    # and as compact records made on the device from the 64-byte records
+    import torch
+    from go2netspectra_amd import compact_headers, read_pcap_compact
+    rec, cwl, side = read_pcap_compact(path)
+    assert len(side) > 0 and np.array_equal(cwl, hb.wirelen)
+    cm2 = CountMin(65536, 4, 20000, 50, flow_fields=FIVE, seeds=seeds, max_flows=1 << 20, batch_packets=70_000)
+    cm2.insert_compact(rec, cwl, side)
+    cm2.flush()
+    assert cm2.stats() == st
+    _same_state(cm2, orc)
+    dh = torch.from_numpy(hb.hdr).cuda()
+    dw = torch.from_numpy(hb.wirelen.view(np.int32)).cuda()
+    drec, dside = compact_headers(dh, dw)
+    cm3 = CountMin(65536, 4, 20000, 50, flow_fields=FIVE, seeds=seeds, max_flows=1 << 20)
+    cm3.insert_compact(drec, dw, dside)
+    cm3.flush()
+    assert cm3.stats() == st
+    _same_state(cm3, orc)

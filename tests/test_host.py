@@ -265,3 +265,41 @@ def test_pcapgen_capture_format(tmp_path):
     for i in range(0, 20_000, 997):
         st, s16, d16, sp, dp, pr = orc.parse_hdr64(bytes(h[i]), int(hb.wirelen[i]))
         assert st == 0 and s16[:4] == bytes(h[i, 26:30]) and sp == sport[i] and pr == 6
+
+
+def test_compact_packer_equals_the_parsed_records(tmp_path):
+    """gns_pack_pcap_compact: every compact record is the tuple the device parser reads
+    from the 64-byte record gns_pack_pcap writes for the same frame (the C oracle's
+    parse of that record), the drop class for frames without an IP layer, or an
+    escape naming that exact 64-byte record in the side array."""
+    from oracle import oracle as orc
+    from test_configs_gpu import _encap_flows
+    rng = np.random.default_rng(5)
+    flows = _encap_flows(rng, 800)
+    frames, wl = _random_frames(rng, 400)  # plain IPv4/TCP, truncated captures included
+    frames += [f for f, _ in flows]
+    wl += [w for _, w in flows]
+    frames += frames[:50]
+    wl += wl[:50]
+    path = str(tmp_path / "c.pcap")
+    g.write_pcap(path, frames, wl)
+    hb = g.read_pcap(path)
+    rec, cwl, side = g.read_pcap_compact(path)
+    assert len(rec) == len(hb) == len(frames) and np.array_equal(cwl, hb.wirelen)
+    seen = {0: 0, 1: 0, 2: 0}
+    for j in range(len(rec)):
+        cls = int(rec[j, 13])
+        seen[cls] += 1
+        st, src, dst, sp, dp, pr = orc.parse_hdr64(bytes(hb.hdr[j]), int(cwl[j]))
+        if cls == 0:
+            assert st == 0, j
+            assert src[4:] == bytes(12) and dst[4:] == bytes(12)
+            assert bytes(rec[j, 0:4]) == src[:4] and bytes(rec[j, 4:8]) == dst[:4]
+            assert bytes(rec[j, 8:12]) == bytes([sp >> 8, sp & 255, dp >> 8, dp & 255]) and rec[j, 12] == pr
+        elif cls == 1:
+            assert st == 1, j  # PARSE_DROP
+        else:
+            assert cls == 2
+            k = int(rec[j, 0:4].view("<u4")[0])
+            assert bytes(side[k]) == bytes(hb.hdr[j])
+    assert seen[0] > 0 and seen[1] > 0 and seen[2] > 0, seen
