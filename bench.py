@@ -674,7 +674,7 @@ def main():
                     help="flow key: full 5-tuple (37 B, primary) or [SrcIP] (16 B, the default task layout)")
     ap.add_argument("--flows", type=int, default=1 << 20,
                     help="distinct flows of the synthetic stream (experiments; the headline uses 2^20)")
-    ap.add_argument("--host-input", nargs="?", const="headers", choices=["headers", "tuples"], default=None,
+    ap.add_argument("--host-input", nargs="?", const="headers", choices=["headers", "tuples", "compact"], default=None,
                     help="time inserts from pinned host memory plus the per-window D2H of counters and heavy "
                          "hitters (PCIe-inclusive rate, for DESIGN.md): 64-B header records or 41-B PacketInfo "
                          "tuples (the live path's pre-parsed form)")
@@ -765,6 +765,9 @@ def main():
             tuples = PacketBatch(pin["src16"].numpy(), pin["dst16"].numpy(), pin["sport"].numpy().view(np.uint16),
                                  pin["dport"].numpy().view(np.uint16), pin["proto"].numpy(),
                                  pin["length"].numpy().view(np.uint32))
+        elif args.host_input == "compact":  # 16-B compact records + wire length = 20 B/packet (+ side records)
+            pin = {"rec": pinned(torch.empty((n, 16), dtype=torch.uint8)), "wl": pinned(wl),
+                   "side": pinned(torch.empty((max(1024, n // 256), 64), dtype=torch.uint8)), "ns": 0}
         else:
             pin = {"hdr": pinned(hdr), "wl": pinned(wl)}
         cnt_C = np.empty(args.depth * args.width, np.uint32)
@@ -789,6 +792,13 @@ def main():
             pin["dport"].copy_((h[:, 36].to(torch.int32) << 8 | h[:, 37].to(torch.int32)).to(torch.int16))
             pin["proto"].copy_(h[:, 23])
             pin["length"].copy_(wl)
+        elif "rec" in pin:
+            from go2netspectra_amd import compact_headers
+            rec, side = compact_headers(hdr, wl)
+            pin["rec"].copy_(rec)
+            pin["wl"].copy_(wl)
+            pin["ns"] = int(side.shape[0])
+            pin["side"][: pin["ns"]].copy_(side)
         else:
             pin["hdr"].copy_(hdr)
             pin["wl"].copy_(wl)
@@ -805,6 +815,9 @@ def main():
             cm.insert_headers(ih, iw)
         elif tuples is not None:
             cm.insert_tuples(tuples)
+        elif pin is not None and "rec" in pin:
+            cm.insert_compact(pin["rec"].numpy(), pin["wl"].numpy().view(np.uint32),
+                              pin["side"][: pin["ns"]].numpy() if pin["ns"] else None)
         elif pin is not None:
             cm.insert_headers(pin["hdr"].numpy(), pin["wl"].numpy().view(np.uint32))
         else:
@@ -870,8 +883,8 @@ def main():
     avg_ms = dom_ms / max(dom_launches, 1)
     pkts_per_launch = n * args.steps / max(dom_launches, 1)
     achieved = BYTES_PER_PKT * pkts_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = None  # PMC record of THIS geometry only (tools/pmc_cm.sh -> profiles/traffic_cm_d*_w*_k*.json)
-    tfile = os.path.join(ROOT, "profiles", f"traffic_cm_d{args.depth}_w{args.width}_k{K}.json")
+    traffic = None  # PMC record of THIS geometry and device batch only (tools/pmc_cm.sh -> profiles/traffic_cm_*.json)
+    tfile = os.path.join(ROOT, "profiles", f"traffic_cm_d{args.depth}_w{args.width}_k{K}_b{batch}.json")
     if os.path.exists(tfile) and not route and args.flows == 1 << 20:
         try:
             traffic = json.load(open(tfile)).get(dom)

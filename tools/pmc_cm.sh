@@ -4,7 +4,7 @@
 #   corrected by tools/pmc_traffic.py), two SQ counter passes.  One pass per run.
 # usage: TAG=c5 BENCH_ARGS="--width 16777216 --depth 8" tools/pmc_cm.sh
 #   then: tools/pmc_traffic.py gpurun_out/pmc_$TAG/fetch/*counter_collection.csv \
-#         gpurun_out/pmc_$TAG/write/*counter_collection.csv profiles/traffic_cm_d8_w16777216_k37.json
+#         gpurun_out/pmc_$TAG/write/*counter_collection.csv profiles/traffic_cm_d8_w16777216_k37_b100000000.json (geometry + device batch)
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out
 T=${TAG:-c2}
 O=gpurun_out/pmc_$T
