@@ -60,7 +60,13 @@ def host_cpu():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = None
-    return {"nproc": os.cpu_count(), "affinity_cpus": avail, "model": model}
+    quota = None  # cgroup v2 CPU quota (the box's CPU share), in CPUs
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity_cpus": avail, "cgroup_cpu_quota": quota, "model": model}
 
 
 def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, depth: int = DEPTH, fields=FIELDS,
@@ -96,6 +102,19 @@ def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, dept
         cm.insert_hdr64_pool(hdr[done:done + m], wl[done:done + m], fields, threads)
         done += m
     pool_rate = done / (time.perf_counter() - t0) / 1e6
+    # (3) the same pool on every core this process may run on (all host cores)
+    try:
+        allc = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allc = os.cpu_count() or 1
+    cm = orc.CountMin(width, depth, 1 << 20, 1000, K, seeds)
+    done_all, t0 = 0, time.perf_counter()
+    while done_all < n and time.perf_counter() - t0 < seconds / 2:
+        m = min(chunk, n - done_all)
+        cm.insert_hdr64_pool(hdr[done_all:done_all + m], wl[done_all:done_all + m], fields, allc)
+        done_all += m
+    all_rate = done_all / (time.perf_counter() - t0) / 1e6
+    del cm
     out = {
         "value": round(pool_rate, 3), "unit": "Mpackets/s", "cores": threads, "kind": "port",
         "sample": f"first {done:,} packets of the same synthetic stream (window 0); C restatement of the Go "
@@ -103,6 +122,9 @@ def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, dept
                   f"num_workers default, shared cursor)",
         "host": host_cpu(),
         "sequential_oracle": {"value": round(seq_rate, 3), "cores": 1, "packets": seq_n},
+        "all_cores_pool": {"value": round(all_rate, 3), "cores": allc, "packets": done_all,
+                           "what": "BASELINE.md B1: the same worker-pool restatement with one thread per core "
+                                   "of this process's CPU affinity set (nproc)"},
     }
     return (out, seq_state, seq_n) if keep_state else out
 
@@ -805,13 +827,8 @@ def main():
 
     def step():
         if route:
-            from go2netspectra_amd.dist import exchange_runs
-            oh, ow, counts = router.partition(hdr, wl)
-            if dist.get_backend() != "nccl":  # gloo rehearsal: the exchange goes through host memory
-                ih, iw = exchange_runs(oh.cpu(), ow.cpu(), counts, world)
-                ih, iw = ih.to(dev), iw.to(dev)
-            else:
-                ih, iw = exchange_runs(oh, ow, counts, world)
+            from go2netspectra_amd.dist import route_exchange
+            ih, iw = route_exchange(router, hdr, wl, world)
             cm.insert_headers(ih, iw)
         elif tuples is not None:
             cm.insert_tuples(tuples)

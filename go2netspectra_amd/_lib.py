@@ -38,7 +38,7 @@ EXPORTED = [
     "gns_thrift_decode", "gns_pack_pcap", "gns_pack_pcap_ts", "gns_pack_counts", "gns_frame_record", "gns_last_error", "gns_version",
     "gns_route_create", "gns_route_destroy", "gns_route_partition",
     "gns_cm_dict_stats", "gns_ss_dict_stats", "gns_ex_dict_stats", "gns_cm_reclaim", "gns_ss_reclaim",
-    "gns_cm_insert_compact", "gns_pack_pcap_compact", "gns_compact_headers",
+    "gns_cm_insert_compact", "gns_pack_pcap_compact", "gns_compact_headers", "gns_route_partition_async",
 ]
 
 
@@ -160,6 +160,7 @@ def load() -> ct.CDLL:
         "gns_cm_insert_compact": ([vp, vp, vp, u64, vp, u64, i32], i32),
         "gns_pack_pcap_compact": ([ct.c_char_p, vp, vp, u64, vp, u64, vp, vp], ct.c_int64),
         "gns_compact_headers": ([vp, vp, u64, vp, vp, u64, vp, i32], i32),
+        "gns_route_partition_async": ([vp, vp, vp, u64, vp, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

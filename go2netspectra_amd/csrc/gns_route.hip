@@ -170,6 +170,10 @@ __global__ __launch_bounds__(kRtThreads) void k_route_scatter(RouteArgs a) {
     }
 }
 
+__global__ void k_route_counts64(const uint32_t *totals, uint32_t G, int64_t *out) {
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) out[g] = (int64_t)totals[g];
+}
+
 }  // namespace gns
 
 using namespace gns;
@@ -234,6 +238,33 @@ int gns_route_destroy(gns_route *r) {
     return GNS_OK;
 }
 
+static int route_launch(gns_route *r, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n, uint8_t *out_hdr,
+                        uint32_t *out_wirelen, hipStream_t st) {
+    const uint32_t nblk = (uint32_t)((n + kRtChunk - 1) / kRtChunk);
+    if (r->shard_n < n || r->hist_n < (uint64_t)nblk * r->G) {
+        GNS_HIP(hipStreamSynchronize(st));  // an earlier partition may still read the scratch
+        if (r->shard_n < n) {
+            dfree(r->shard); r->shard = nullptr; r->shard_n = 0;
+            GNS_TRY(dalloc_t(&r->shard, n));
+            r->shard_n = n;
+        }
+        if (r->hist_n < (uint64_t)nblk * r->G) {
+            dfree(r->hist); r->hist = nullptr; r->hist_n = 0;
+            GNS_TRY(dalloc_t(&r->hist, (uint64_t)nblk * r->G));
+            r->hist_n = (uint64_t)nblk * r->G;
+        }
+    }
+    RouteArgs a{};
+    a.hdr = reinterpret_cast<const uint32_t *>(hdr); a.wl = wirelen; a.n = n; a.G = r->G; a.gbits = r->gbits;
+    a.shard = r->shard; a.hist = r->hist; a.nblk = nblk;
+    a.out_hdr = reinterpret_cast<uint32_t *>(out_hdr); a.out_wl = out_wirelen; a.totals = r->totals;
+    hipLaunchKernelGGL(k_route_count, dim3(nblk), dim3(kRtThreads), 0, st, a);
+    hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(k_route_scatter, dim3(nblk), dim3(kRtThreads), 0, st, a);
+    GNS_HIP(hipGetLastError());
+    return GNS_OK;
+}
+
 int gns_route_partition(gns_route *r, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n, uint8_t *out_hdr,
                         uint32_t *out_wirelen, uint64_t *counts) {
     if (!r || !counts || (n && (!hdr || !wirelen || !out_hdr || !out_wirelen))) {
@@ -243,28 +274,29 @@ int gns_route_partition(gns_route *r, const uint8_t *hdr, const uint32_t *wirele
     if (n == 0) { for (uint32_t g = 0; g < r->G; g++) counts[g] = 0; return GNS_OK; }
     (void)hipGetLastError();  // clear a stale error of an earlier runtime call on this thread
     GNS_HIP(hipSetDevice(r->device));
-    const uint32_t nblk = (uint32_t)((n + kRtChunk - 1) / kRtChunk);
-    if (r->shard_n < n) {
-        dfree(r->shard); r->shard = nullptr; r->shard_n = 0;
-        GNS_TRY(dalloc_t(&r->shard, n));
-        r->shard_n = n;
-    }
-    if (r->hist_n < (uint64_t)nblk * r->G) {
-        dfree(r->hist); r->hist = nullptr; r->hist_n = 0;
-        GNS_TRY(dalloc_t(&r->hist, (uint64_t)nblk * r->G));
-        r->hist_n = (uint64_t)nblk * r->G;
-    }
-    RouteArgs a{};
-    a.hdr = reinterpret_cast<const uint32_t *>(hdr); a.wl = wirelen; a.n = n; a.G = r->G; a.gbits = r->gbits;
-    a.shard = r->shard; a.hist = r->hist; a.nblk = nblk;
-    a.out_hdr = reinterpret_cast<uint32_t *>(out_hdr); a.out_wl = out_wirelen; a.totals = r->totals;
-    hipLaunchKernelGGL(k_route_count, dim3(nblk), dim3(kRtThreads), 0, r->stream, a);
-    hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, r->stream, a);
-    hipLaunchKernelGGL(k_route_scatter, dim3(nblk), dim3(kRtThreads), 0, r->stream, a);
-    GNS_HIP(hipGetLastError());
+    GNS_TRY(route_launch(r, hdr, wirelen, n, out_hdr, out_wirelen, r->stream));
     GNS_HIP(hipMemcpyAsync(r->h_tot, r->totals, r->G * 4, hipMemcpyDeviceToHost, r->stream));
     GNS_HIP(hipStreamSynchronize(r->stream));
     for (uint32_t g = 0; g < r->G; g++) counts[g] = r->h_tot[g];
+    return GNS_OK;
+}
+
+int gns_route_partition_async(gns_route *r, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
+                              uint8_t *out_hdr, uint32_t *out_wirelen, int64_t *counts_dev, void *stream) {
+    if (!r || !counts_dev || (n && (!hdr || !wirelen || !out_hdr || !out_wirelen))) {
+        set_error("null argument"); return GNS_E_ARG;
+    }
+    if (n >= (1ull << 32)) { set_error("route batch of %llu packets (max 2^32 - 1)", (unsigned long long)n); return GNS_E_RANGE; }
+    (void)hipGetLastError();
+    GNS_HIP(hipSetDevice(r->device));
+    hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : r->stream;
+    if (n == 0) {
+        GNS_HIP(hipMemsetAsync(counts_dev, 0, r->G * 8, st));
+        return GNS_OK;
+    }
+    GNS_TRY(route_launch(r, hdr, wirelen, n, out_hdr, out_wirelen, st));
+    hipLaunchKernelGGL(k_route_counts64, dim3(1), dim3(64), 0, st, r->totals, r->G, counts_dev);
+    GNS_HIP(hipGetLastError());
     return GNS_OK;
 }
 

@@ -72,7 +72,6 @@ class Router:
         h = ct.c_void_p()
         _lib.check(self._L.gns_route_create(self.nshards, device, ct.byref(h)))
         self._h = h
-        self._out = None
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -85,23 +84,41 @@ class Router:
         except Exception:
             pass
 
+    def _outputs(self, hdr, n, out_hdr, out_wl):
+        import torch
+        if (out_hdr is None) != (out_wl is None):
+            raise ValueError("out_hdr and out_wl go together")
+        if out_hdr is None:  # fresh tensors (torch's caching allocator): results never alias
+            return (torch.empty((n, 64), dtype=torch.uint8, device=hdr.device),
+                    torch.empty((n,), dtype=torch.int32, device=hdr.device))
+        if out_hdr.shape[0] < n or out_wl.shape[0] < n or out_hdr.numel() < 64 * n:
+            raise ValueError(f"output buffers hold fewer than {n} records")
+        return out_hdr[:n], out_wl[:n]
+
     def partition(self, hdr, wirelen, out_hdr=None, out_wl=None):
         """hdr [n,64] uint8 / wirelen [n] (device tensors) -> (out_hdr, out_wl, counts):
         the records regrouped shard by shard, packet order kept inside each shard;
-        counts[g] = packets of shard g (numpy uint64)."""
-        import ctypes as ct
-        import torch
+        counts[g] = packets of shard g (numpy uint64).  Returns after the device work."""
         from . import _lib
         n = int(wirelen.shape[0])
-        if out_hdr is None:
-            if self._out is None or self._out[0].shape[0] < n:
-                self._out = (torch.empty((n, 64), dtype=torch.uint8, device=hdr.device),
-                             torch.empty((n,), dtype=torch.int32, device=hdr.device))
-            out_hdr, out_wl = self._out[0][:n], self._out[1][:n]
+        out_hdr, out_wl = self._outputs(hdr, n, out_hdr, out_wl)
         counts = np.zeros(self.nshards, np.uint64)
         _lib.device_ready(hdr, wirelen)
         _lib.check(self._L.gns_route_partition(self._h, hdr.data_ptr(), wirelen.data_ptr(), n, out_hdr.data_ptr(),
                                                out_wl.data_ptr(), counts.ctypes.data))
+        return out_hdr, out_wl, counts
+
+    def partition_async(self, hdr, wirelen, out_hdr=None, out_wl=None):
+        """As partition, queued on torch's current stream without a host wait: counts
+        is a device int64 tensor [nshards] (the all-to-all's split sizes)."""
+        import torch
+        from . import _lib
+        n = int(wirelen.shape[0])
+        out_hdr, out_wl = self._outputs(hdr, n, out_hdr, out_wl)
+        counts = torch.empty((self.nshards,), dtype=torch.int64, device=hdr.device)
+        st = torch.cuda.current_stream(hdr.device).cuda_stream
+        _lib.check(self._L.gns_route_partition_async(self._h, hdr.data_ptr(), wirelen.data_ptr(), n,
+                                                     out_hdr.data_ptr(), out_wl.data_ptr(), counts.data_ptr(), st))
         return out_hdr, out_wl, counts
 
 
@@ -109,27 +126,44 @@ def exchange_runs(run_hdr, run_wl, counts, world: int):
     """All-to-all of shard runs (RCCL on the GPU, gloo on the CPU): run g of every
     rank goes to rank g; the received runs are concatenated in source-rank order,
     so with rank r holding slice r of the stream each rank receives exactly the
-    stable filter stream[shard_of(src) == rank].  counts: this rank's run lengths."""
+    stable filter stream[shard_of(src) == rank].
+
+    counts: this rank's run lengths, a device int64 tensor (Router.partition_async)
+    or host integers.  One all-to-all of the counts, ONE host read of the send and
+    receive split sizes, then the record and wire-length all-to-alls issued back to
+    back (asynchronous) and waited together."""
     import torch
     import torch.distributed as dist
     dev = run_hdr.device
-    send = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
+    if torch.is_tensor(counts):
+        send = counts.to(device=dev, dtype=torch.int64)
+    else:
+        send = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send)
-    rc = [int(x) for x in recv.tolist()]
-    sc = [int(c) for c in counts]
+    both = torch.cat([send, recv]).cpu().tolist()  # the one host read of the exchange
+    sc, rc = [int(x) for x in both[:world]], [int(x) for x in both[world:]]
     in_h = torch.empty((sum(rc), 64), dtype=torch.uint8, device=dev)
     in_w = torch.empty((sum(rc),), dtype=run_wl.dtype, device=dev)
-    dist.all_to_all_single(in_h, run_hdr, output_split_sizes=rc, input_split_sizes=sc)
-    dist.all_to_all_single(in_w, run_wl, output_split_sizes=rc, input_split_sizes=sc)
+    w1 = dist.all_to_all_single(in_h, run_hdr[: sum(sc)], output_split_sizes=rc, input_split_sizes=sc,
+                                async_op=True)
+    w2 = dist.all_to_all_single(in_w, run_wl[: sum(sc)], output_split_sizes=rc, input_split_sizes=sc,
+                                async_op=True)
+    w1.wait()
+    w2.wait()
     return in_h, in_w
 
 
 def route_exchange(router: "Router", hdr, wirelen, world: int):
     """configs[3] routing step: partition this rank's slice of the stream on the
-    device, then exchange the runs (exchange_runs).  Returns this rank's shard
-    stream (device tensors)."""
-    oh, ow, counts = router.partition(hdr, wirelen)
+    device (counts stay on the device), then exchange the runs (exchange_runs).
+    Returns this rank's shard stream (device tensors).  Under gloo (CPU
+    rehearsal) the runs travel through host memory and come back to the device."""
+    import torch.distributed as dist
+    oh, ow, counts = router.partition_async(hdr, wirelen)
+    if dist.get_backend() != "nccl":
+        ih, iw = exchange_runs(oh.cpu(), ow.cpu(), counts.cpu(), world)
+        return ih.to(hdr.device), iw.to(hdr.device)
     return exchange_runs(oh, ow, counts, world)
 
 

@@ -347,6 +347,12 @@ int gns_route_create(uint32_t nshards, int device, gns_route **out);  /* nshards
 int gns_route_destroy(gns_route *r);
 int gns_route_partition(gns_route *r, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
                         uint8_t *out_hdr, uint32_t *out_wirelen, uint64_t *counts);
+/* The same partition queued on `stream` (a hipStream_t; NULL = the router's own)
+ * without waiting: counts_dev[g] (DEVICE int64) = length of run g once the stream
+ * reaches it -- the all-to-all's split sizes stay on the device until the one
+ * host read the exchange needs (dist.exchange_runs). */
+int gns_route_partition_async(gns_route *r, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
+                              uint8_t *out_hdr, uint32_t *out_wirelen, int64_t *counts_dev, void *stream);
 
 /* ------------------------------------------------------------------ */
 /* Exact aggregator (internal/engine/impl/exact/task.go)               */
