@@ -5,9 +5,12 @@
 //   - CountMin: a statistic.Sketch (internal/engine/impl/sketch/statistic/sketch.go:5-10)
 //     whose Insert/Query/HeavyHitters/Reset run on the GPU, plus InsertBatch for the
 //     batched path;
-//   - a "sketch_gpu" aggregator registered with factory.RegisterAggregator
-//     (internal/factory/task_factory.go:24) whose Task batches PacketInfo and submits them
-//     with gns_cm_insert_tuples instead of one CAS insert per packet per worker.
+//   - SuperSpread and Exact, the same way;
+//   - task.go: GPUTask, a model.Task (internal/model/task.go:6-15) registered as the
+//     "sketch_gpu" aggregator with factory.RegisterAggregator
+//     (internal/factory/task_factory.go:24), whose ProcessPacket batches PacketInfo and
+//     submits the batch with gns_{cm,ss}_insert_tuples instead of one CAS insert per
+//     packet per worker.
 //
 // Build: CGO_CFLAGS="-I<repo>/include" CGO_LDFLAGS="-L<repo>/go2netspectra_amd -lgns_sketch".
 // Not compiled in the build container (no Go toolchain there).
@@ -45,8 +48,9 @@ type CountMin struct {
 }
 
 // sticky keeps the first failure of a measurement period and logs it the way
-// the reference logs a dropped packet (task.go:162-166).  GNS_E_FULL is sticky
-// in the engine too: every later insert fails until Reset.
+// the reference logs a dropped packet (task.go:162-166).  The engine has no
+// traffic-dependent failure left (its flow dictionary grows, include/gns_sketch.h),
+// so this reports device / runtime errors.
 func sticky(dst *error, err error) {
 	if err != nil && *dst == nil {
 		*dst = err
@@ -173,8 +177,8 @@ func FrameRecord(frame []byte, wireLen uint32, rec []byte) (kind int, err error)
 func (c *CountMin) Reclaim() error { return lastErr(C.gns_cm_reclaim(c.h)) }
 
 // DictStats: reclaims, dead flows dropped, live flows after the last reclaim,
-// claimed slots, reclaim time (us), batches re-run after an overflow.
-func (c *CountMin) DictStats() (out [6]uint64, err error) {
+// claimed slots, reclaim time (us), batches re-run after an overflow, slots, growths.
+func (c *CountMin) DictStats() (out [8]uint64, err error) {
 	err = lastErr(C.gns_cm_dict_stats(c.h, (*C.uint64_t)(unsafe.Pointer(&out[0]))))
 	return
 }
