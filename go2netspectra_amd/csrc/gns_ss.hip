@@ -11,16 +11,15 @@
 //     value lz exceeds the register's value at its time, i.e. the exclusive
 //     prefix max of earlier updates to the same (cell, register).  Only
 //     packets with lz > the batch-entry register can encode (registers only
-//     grow): they are emitted as candidates, radix-sorted by (cell, register,
-//     packet) and a segmented inclusive max-scan gives every candidate the
-//     register value it would see.
+//     grow): they are emitted as candidates, partitioned by cell bins and, per
+//     bin, radix-sorted by (cell, register, packet) in LDS, where a segmented
+//     max gives every candidate the register value it would see (k_sp_*).
 //   * pbits (:105-109) and the sampled majority-vote counter (:200-233) are
 //     sequential per cell: the successful encodes (at most maxValue per
-//     register per batch, sparse) are sorted by (cell, packet) and every cell
-//     is walked in stream order by one lane.
+//     register per batch, sparse) are sorted by (cell, packet) in the same LDS
+//     pass and every cell is walked in stream order by one lane.
 #include <cstdlib>
 #include <cstring>
-#include <rocprim/rocprim.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -28,6 +27,7 @@
 
 #include "gns_common.hpp"
 #include "gns_gomath.cuh"
+#include "gns_scan.cuh"
 
 namespace gns {
 
@@ -294,7 +294,8 @@ struct SsIdsArgs {
     KeyPlanN kpf, kpm;
     SsGeom g;
     DictDev D;
-    uint32_t epoch, ns;
+    uint32_t epoch;
+    const uint32_t *ns;  // encodes of the batch (device count)
     const uint64_t *skey;
     uint64_t *sval;
     const uint64_t *pend_in;
@@ -304,110 +305,56 @@ struct SsIdsArgs {
     unsigned long long *stats;
 };
 
+// Grid-stride over chunks of kSsIdChunk encodes: chunk c = blockIdx.x + k * gridDim.x
+// (its parked list at pend[c * kSsIdChunk ...], its count at cnt[c]).
 template <int KIND, int MF, int MM, bool FIRST>
 __global__ __launch_bounds__(kSsThreads) void k_ss_ids(SsIdsArgs r) {
     __shared__ uint8_t s_srcf[80], s_srcm[80];
     __shared__ uint32_t s_cnt, s_full, s_claim, s_abort;
-    const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    const uint32_t tid = threadIdx.x;
     for (uint32_t j = tid; j < 80; j += kSsThreads) { s_srcf[j] = r.kpf.src[j]; s_srcm[j] = r.kpm.src[j]; }
-    if (tid == 0) { s_cnt = 0; s_full = 0; s_claim = 0; s_abort = dict_aborted(r.D); }
+    if (tid == 0) { s_full = 0; s_claim = 0; s_abort = dict_aborted(r.D); }
     __syncthreads();
-    if (s_abort) {  // the batch overflowed the dictionary: it is re-run after a reclaim
-        if (tid == 0) r.cnt_out[blk] = 0;
-        return;
-    }
-    const uint64_t beg = (uint64_t)blk * kSsIdChunk;
-    const uint32_t cnt = FIRST ? (uint32_t)min<uint64_t>(kSsIdChunk, r.ns - beg) : r.cnt_in[blk];
+    const uint32_t ns = *r.ns;
+    const uint32_t nch = (ns + kSsIdChunk - 1) / kSsIdChunk;
     SsExtractArgs a{};
     a.in = r.in; a.kpf = r.kpf; a.kpm = r.kpm; a.g = r.g;
-    for (uint32_t i = tid; i < cnt; i += kSsThreads) {
-        uint64_t q;
-        uint32_t slot = 0;
-        if (FIRST) q = beg + i;
-        else { const uint64_t v = r.pend_in[beg + i]; q = beg + (v >> 32); slot = (uint32_t)v; }
-        const uint64_t p = r.skey[q] & ((1ull << kSsPktBits) - 1);
-        uint32_t kwf[GNS_KWMAX], kwm[kSsNW];
-        (void)ss_keys<KIND, MF, MM>(a, s_srcf, s_srcm, p, kwf, kwm);  // parsed OK in S1
-        if (FIRST) slot = mm3_n<GNS_KWMAX>(kwf, r.g.Kf, r.D.seed) & r.D.mask;
-        uint32_t out;
-        const int res = dict_find_or_claim(r.D, kwf, slot, r.epoch, &out);
-        if (res == DICT_CLAIMED) atomicAdd(&s_claim, 1u);
-        if (res == DICT_FOUND || res == DICT_CLAIMED) r.sval[q] = (uint64_t)out << 32 | (r.sval[q] & 0xFFFFFFFFull);
-        else if (res == DICT_PENDING) r.pend_out[beg + atomicAdd(&s_cnt, 1u)] = (q - beg) << 32 | out;
-        else atomicAdd(&s_full, 1u);
+    for (uint32_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {  // block-uniform
+        if (s_abort) {  // the batch overflowed the dictionary: it is re-run after a reclaim
+            if (tid == 0) r.cnt_out[ch] = 0;
+            continue;
+        }
+        if (tid == 0) s_cnt = 0;
+        __syncthreads();
+        const uint64_t beg = (uint64_t)ch * kSsIdChunk;
+        const uint32_t cnt = FIRST ? (uint32_t)min<uint64_t>(kSsIdChunk, ns - beg) : r.cnt_in[ch];
+        for (uint32_t i = tid; i < cnt; i += kSsThreads) {
+            uint64_t q;
+            uint32_t slot = 0;
+            if (FIRST) q = beg + i;
+            else { const uint64_t v = r.pend_in[beg + i]; q = beg + (v >> 32); slot = (uint32_t)v; }
+            const uint64_t p = r.skey[q] & ((1ull << kSsPktBits) - 1);
+            uint32_t kwf[GNS_KWMAX], kwm[kSsNW];
+            (void)ss_keys<KIND, MF, MM>(a, s_srcf, s_srcm, p, kwf, kwm);  // parsed OK in S1
+            if (FIRST) slot = mm3_n<GNS_KWMAX>(kwf, r.g.Kf, r.D.seed) & r.D.mask;
+            uint32_t out;
+            const int res = dict_find_or_claim(r.D, kwf, slot, r.epoch, &out);
+            if (res == DICT_CLAIMED) atomicAdd(&s_claim, 1u);
+            if (res == DICT_FOUND || res == DICT_CLAIMED) r.sval[q] = (uint64_t)out << 32 | (r.sval[q] & 0xFFFFFFFFull);
+            else if (res == DICT_PENDING) r.pend_out[beg + atomicAdd(&s_cnt, 1u)] = (q - beg) << 32 | out;
+            else atomicAdd(&s_full, 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            r.cnt_out[ch] = s_cnt;
+            if (s_cnt) atomicAdd(r.total_out, s_cnt);
+        }
     }
     __syncthreads();
     if (tid == 0) {
-        r.cnt_out[blk] = s_cnt;
-        if (s_cnt) atomicAdd(r.total_out, s_cnt);
         if (s_full) atomicAdd(&r.stats[3], (unsigned long long)s_full);
         dict_flush_claims(r.D, s_claim, &r.stats[3]);
     }
-}
-
-// S1b: block regions -> one dense candidate array (sort input)
-__global__ __launch_bounds__(256) void k_ss_compact(const uint64_t *rkey, const uint32_t *rval, const uint32_t *cblk,
-                                                    uint32_t d, uint64_t *okey, uint32_t *oval) {
-    const uint32_t blk = blockIdx.x;
-    const uint32_t cnt = cblk[blk], base = cblk[gridDim.x + blk];
-    const uint64_t r = (uint64_t)blk * kSsChunk * d;
-    for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
-        okey[base + i] = rkey[r + i];
-        oval[base + i] = rval[r + i];
-    }
-}
-
-// S3: which candidates encode.  inclusive max of lz per (cell, register)
-// segment is in cmax; the register a candidate sees is max(entry register,
-// previous candidate's inclusive max).
-struct SsSuccArgs {
-    const uint64_t *ckey;
-    const uint32_t *cval, *cmax;
-    uint32_t n;
-    const uint8_t *regs;
-    uint32_t m;
-    uint64_t *skey;  // (cell << 27) | packet
-    uint64_t *sval;  // flow id << 32 | reg | lz << 8 | old << 16 (the id, filled in by S3b, rides
-                     // along the sort, so S5's sequential walk has no dependent id load)
-    uint32_t *scount;
-};
-
-// kSsSuccItems candidates per lane; one global atomic per workgroup reserves
-// the encodes' slots (S4 sorts them, so their order here does not matter).
-constexpr uint32_t kSsSuccItems = 8;
-__global__ __launch_bounds__(256) void k_ss_success(SsSuccArgs a) {
-    __shared__ uint32_t s_n, s_base;
-    if (threadIdx.x == 0) s_n = 0;
-    __syncthreads();
-    const uint32_t k0 = blockIdx.x * 256 * kSsSuccItems + threadIdx.x;
-    uint64_t ok[kSsSuccItems], ov[kSsSuccItems];
-    uint32_t cnt = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kSsSuccItems; i++) {
-        const uint32_t k = k0 + i * 256;
-        ok[i] = ~0ull;
-        if (k >= a.n) continue;
-        const uint64_t key = a.ckey[k];
-        const uint64_t seg = key >> kSsPktBits;
-        const uint32_t lz = a.cval[k];
-        uint32_t old = a.regs[seg];
-        if (k > 0 && (a.ckey[k - 1] >> kSsPktBits) == seg) old = max(old, a.cmax[k - 1]);
-        if (lz > old) {
-            const uint64_t cell = seg / a.m;
-            const uint32_t reg = (uint32_t)(seg % a.m);
-            ok[i] = cell << kSsPktBits | (key & ((1ull << kSsPktBits) - 1));
-            ov[i] = (uint64_t)GNS_ID_NONE << 32 | (reg | lz << 8 | old << 16);
-            cnt++;
-        }
-    }
-    const uint32_t off = cnt ? atomicAdd(&s_n, cnt) : 0u;
-    __syncthreads();
-    if (threadIdx.x == 0) s_base = s_n ? atomicAdd(a.scount, s_n) : 0u;
-    __syncthreads();
-    uint32_t q = s_base + off;
-#pragma unroll
-    for (uint32_t i = 0; i < kSsSuccItems; i++)
-        if (ok[i] != ~0ull) { a.skey[q] = ok[i]; a.sval[q] = ov[i]; q++; }
 }
 
 // S5: every cell's encodes in stream order: register write, pbits (:105-109),
@@ -421,7 +368,7 @@ __global__ __launch_bounds__(256) void k_ss_success(SsSuccArgs a) {
 struct SsApplyArgs {
     const uint64_t *skey;
     const uint64_t *sval;  // flow id << 32 | reg | lz << 8 | old << 16
-    uint32_t n;
+    const uint32_t *ns;    // encodes of the batch (device count)
     SsGeom g;
     uint64_t pkt_base;
     uint8_t *regs;
@@ -433,37 +380,6 @@ struct SsApplyArgs {
     uint32_t cells;
 };
 
-// S5 segment starts (one per touched cell; order is irrelevant: cells are
-// independent), so the per-cell walks run on fully populated waves instead of
-// one sparse lane per 64 encodes.
-// Each workgroup covers kSsHeadItems encodes per lane; the heads it finds take
-// one global atomic per workgroup (a per-head atomic on the one counter
-// serialized 65K times per batch).
-constexpr uint32_t kSsHeadItems = 8;
-__global__ __launch_bounds__(256) void k_ss_heads(const uint64_t *skey, uint32_t n, uint32_t *heads,
-                                                  uint32_t cells) {
-    __shared__ uint32_t s_n, s_base;
-    if (threadIdx.x == 0) s_n = 0;
-    __syncthreads();
-    const uint32_t k0 = blockIdx.x * 256 * kSsHeadItems + threadIdx.x;
-    bool hd[kSsHeadItems];
-    uint32_t cnt = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kSsHeadItems; i++) {
-        const uint32_t k = k0 + i * 256;
-        hd[i] = k < n && (k == 0 || (skey[k - 1] >> kSsPktBits) != (skey[k] >> kSsPktBits));
-        cnt += hd[i];
-    }
-    const uint32_t off = cnt ? atomicAdd(&s_n, cnt) : 0u;
-    __syncthreads();
-    if (threadIdx.x == 0) s_base = s_n ? atomicAdd(&heads[cells], s_n) : 0u;
-    __syncthreads();
-    uint32_t q = s_base + off;
-#pragma unroll
-    for (uint32_t i = 0; i < kSsHeadItems; i++)
-        if (hd[i]) heads[q++] = k0 + i * 256;
-}
-
 #pragma clang fp contract(off)
 __global__ __launch_bounds__(256) void k_ss_walk_pbits(SsApplyArgs a) {
     __shared__ double s_t[256];  // go_pow_int(base, k) / m for every register value k
@@ -472,14 +388,15 @@ __global__ __launch_bounds__(256) void k_ss_walk_pbits(SsApplyArgs a) {
     __syncthreads();
     const uint32_t hi = blockIdx.x * 256 + threadIdx.x;
     if (hi >= a.heads[a.cells]) return;
+    const uint32_t nenc = *a.ns;
     const uint32_t k0 = a.heads[hi];
     const uint64_t cell = a.skey[k0] >> kSsPktBits;
     double pb = a.pbits[cell];
     uint64_t vc = a.sval[k0];
     for (uint32_t k = k0;;) {
         const uint32_t kn = k + 1;
-        const uint64_t kx = kn < a.n ? a.skey[kn] : ~0ull;
-        const uint64_t vx = kn < a.n ? a.sval[kn] : 0ull;
+        const uint64_t kx = kn < nenc ? a.skey[kn] : ~0ull;
+        const uint64_t vx = kn < nenc ? a.sval[kn] : 0ull;
         const uint32_t v = (uint32_t)vc;
         const uint32_t reg = v & 0xFFu, lz = (v >> 8) & 0xFFu, old = (v >> 16) & 0xFFu;
         a.regs[cell * a.g.m + reg] = (uint8_t)lz;
@@ -493,8 +410,8 @@ __global__ __launch_bounds__(256) void k_ss_walk_pbits(SsApplyArgs a) {
 }
 
 __global__ __launch_bounds__(256) void k_ss_sample(SsApplyArgs a) {
-    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= a.n) return;
+    const uint32_t nenc = *a.ns;
+    for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < nenc; k += gridDim.x * 256) {
     const double tempP = a.tp[k];
     int64_t vv = 0;
     if (tempP != -1.0) {                                                  // :196
@@ -511,11 +428,13 @@ __global__ __launch_bounds__(256) void k_ss_sample(SsApplyArgs a) {
         }
     }
     a.rep[k] = vv;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
     const uint32_t hi = blockIdx.x * 256 + threadIdx.x;
     if (hi >= a.heads[a.cells]) return;
+    const uint32_t nenc = *a.ns;
     const uint32_t k0 = a.heads[hi];
     const uint64_t cell = a.skey[k0] >> kSsPktBits;
     const uint32_t row = (uint32_t)(cell / a.g.w);
@@ -529,10 +448,10 @@ __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
     double lc = a.tp[k0];
     for (uint32_t k = k0;;) {
         const uint32_t kn = k + 1;  // the next encode's inputs load while this one runs
-        const uint64_t kx = kn < a.n ? a.skey[kn] : ~0ull;
-        const uint64_t vx = kn < a.n ? a.sval[kn] : 0ull;
-        const int64_t rx = kn < a.n ? a.rep[kn] : 0;
-        const double lx = kn < a.n ? a.tp[kn] : 0.0;
+        const uint64_t kx = kn < nenc ? a.skey[kn] : ~0ull;
+        const uint64_t vx = kn < nenc ? a.sval[kn] : 0ull;
+        const int64_t rx = kn < nenc ? a.rep[kn] : 0;
+        const double lx = kn < nenc ? a.tp[kn] : 0.0;
         int64_t vv = rc;
         const uint32_t f = (uint32_t)(vc >> 32);
         const uint64_t pkt = a.pkt_base + (kc & ((1ull << kSsPktBits) - 1));
@@ -613,9 +532,506 @@ __global__ __launch_bounds__(256) void k_ss_ids_to_bytes(const uint32_t *ids, ui
     }
 }
 
-struct SegKey {  // (cell*m + reg) of a candidate key
-    __host__ __device__ uint64_t operator()(uint64_t k) const { return k >> kSsPktBits; }
+// ---------------------------------------------------------------------------
+// Candidate pipeline without a library sort or a host round trip (round 4):
+//   P1 k_sp_hist     per S1 block region, histogram of its candidates over NB
+//                    bins of consecutive cells (block-major, as Count-Min's K1)
+//   P2 k_tscan_*     bin-major offsets (gns_scan.cuh)
+//   P3 k_sp_scatter  candidates into their bins as packed words
+//                    local seg << 35 | packet << 8 | lz, staged in LDS and copied
+//                    out bin by bin (order inside a bin is free: the packet rides along)
+//   P4 k_sp_bins     persistent, one 1024-thread workgroup per bin at a time:
+//                    the bin (or each group of whole cells of a large bin, split
+//                    by a cell histogram) is radix-sorted in LDS by (seg, packet);
+//                    a segmented max gives every candidate the register value it
+//                    would see (super_spread.go:90-103), so it encodes iff lz
+//                    exceeds it; the encodes are sorted by (cell, packet) in LDS
+//                    and written with one global atomic per group, plus the heads
+//                    of the cells (S5's walks).  A cell with more candidates than
+//                    fit LDS (a superspreader in a batch that starts from low
+//                    registers) takes the order-free form of the same test: the
+//                    earliest packet per (register, lz) by LDS atomicMin, suffix
+//                    minima over lz, and a candidate encodes iff it is the earliest
+//                    packet with an lz >= its own.
+// Every launch is sized from host-known bounds; counts stay on the device.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSpCap = 8192;        // items a P4 workgroup holds in LDS
+constexpr uint32_t kSpThreads = 1024;
+constexpr uint32_t kSpWaves = kSpThreads / 64;
+constexpr uint32_t kSpPer = kSpCap / kSpThreads;   // 8 items per thread
+constexpr uint32_t kSpSub = 4096;        // P3 candidates staged per sub-pass
+constexpr uint32_t kSpMaxBins = 4096;
+constexpr uint32_t kSpMaxCpb = 8192;     // cells per bin (P4's cell histogram)
+constexpr uint32_t kSpV = 34;            // lz values (geometric values are <= 33)
+
+struct SpGeom {
+    uint32_t nb, cpb, cpb_bits, m, mbits;  // bins, cells per bin (power of two), m (mbits: log2 m if power of two, else 0xFF)
+    uint32_t lbits;                        // bits of a local seg (cpb * m)
+    uint32_t cells;
 };
+
+__device__ __forceinline__ uint64_t sp_cell(const SpGeom &s, uint64_t seg) {
+    return s.mbits != 0xFFu ? seg >> s.mbits : seg / s.m;
+}
+
+// P1
+__global__ __launch_bounds__(256) void k_sp_hist(const uint64_t *ckey, const uint32_t *cblk, uint32_t d, SpGeom s,
+                                                 uint32_t *hist) {
+    __shared__ uint32_t h[kSpMaxBins];
+    const uint32_t blk = blockIdx.x, tid = threadIdx.x;
+    for (uint32_t i = tid; i < s.nb; i += 256) h[i] = 0;
+    __syncthreads();
+    const uint32_t cnt = cblk[blk];
+    const uint64_t *r = ckey + (uint64_t)blk * kSsChunk * d;
+    for (uint32_t i = tid; i < cnt; i += 256) {
+        const uint64_t cell = sp_cell(s, r[i] >> kSsPktBits);
+        atomicAdd(&h[(uint32_t)(cell >> s.cpb_bits)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < s.nb; i += 256) hist[(uint64_t)blk * s.nb + i] = h[i];
+}
+
+// P3: kSpSub-candidate sub-passes: count per bin, local starts, stage by bin, copy out runs
+__global__ __launch_bounds__(256) void k_sp_scatter(const uint64_t *ckey, const uint32_t *cval, const uint32_t *cblk,
+                                                    uint32_t d, SpGeom s, const uint32_t *offs, uint64_t *words) {
+    __shared__ uint32_t gpos[kSpMaxBins], cnt[kSpMaxBins];
+    __shared__ uint64_t stage[kSpSub];
+    __shared__ uint16_t sbin[kSpSub];
+    __shared__ uint32_t wsum[4];
+    const uint32_t blk = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    for (uint32_t i = tid; i < s.nb; i += 256) { gpos[i] = offs[(uint64_t)blk * s.nb + i]; cnt[i] = 0; }
+    __syncthreads();
+    const uint32_t n = cblk[blk];
+    const uint64_t base = (uint64_t)blk * kSsChunk * d;
+    constexpr uint32_t kPer = kSpSub / 256;
+    const uint32_t per = (s.nb + 255) / 256;  // bins per thread in the local scan
+    for (uint32_t c0 = 0; c0 < n; c0 += kSpSub) {
+        const uint32_t m = min(kSpSub, n - c0);
+        uint64_t w[kPer];
+        uint32_t b[kPer], rk[kPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j++) {
+            const uint32_t i = j * 256 + tid;
+            b[j] = 0xFFFFFFFFu;
+            if (i < m) {
+                const uint64_t key = ckey[base + c0 + i];
+                const uint64_t seg = key >> kSsPktBits;
+                const uint64_t cell = sp_cell(s, seg);
+                const uint32_t bin = (uint32_t)(cell >> s.cpb_bits);
+                const uint64_t local = seg - ((uint64_t)bin << s.cpb_bits) * s.m;
+                w[j] = local << 35 | (key & ((1ull << kSsPktBits) - 1)) << 8 | (cval[base + c0 + i] & 0xFFu);
+                b[j] = bin;
+                rk[j] = atomicAdd(&cnt[bin], 1u);
+            }
+        }
+        __syncthreads();
+        // exclusive scan of the bin counts (per bins per thread, then the waves)
+        uint32_t sum = 0;
+        for (uint32_t q = 0; q < per; q++) {
+            const uint32_t i = tid * per + q;
+            sum += i < s.nb ? cnt[i] : 0u;
+        }
+        const uint32_t inc = wave_incl_scan(sum);
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint32_t run = inc - sum;
+        for (uint32_t v = 0; v < wave; v++) run += wsum[v];
+        for (uint32_t q = 0; q < per; q++) {
+            const uint32_t i = tid * per + q;
+            if (i < s.nb) { const uint32_t c = cnt[i]; cnt[i] = run; run += c; }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j++)
+            if (b[j] != 0xFFFFFFFFu) {
+                const uint32_t pos = cnt[b[j]] + rk[j];
+                stage[pos] = w[j];
+                sbin[pos] = (uint16_t)b[j];
+            }
+        __syncthreads();
+        for (uint32_t i = tid; i < m; i += 256) {
+            const uint32_t bin = sbin[i];
+            words[gpos[bin] + (i - cnt[bin])] = stage[i];
+        }
+        __syncthreads();
+        // advance each bin's global cursor by its count (next starts - this start), clear
+        for (uint32_t i = tid; i < s.nb; i += 256) {
+            const uint32_t nx = i + 1 < s.nb ? cnt[i + 1] : m;
+            gpos[i] += nx - cnt[i];
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < s.nb; i += 256) cnt[i] = 0;
+        __syncthreads();
+    }
+}
+
+struct SpArgs {
+    SpGeom s;
+    const uint64_t *words;   // bin-major candidates (P3)
+    uint64_t *words2;        // scratch of the same size (large bins, grouped by cells)
+    const uint32_t *bstart;  // [nb] bin starts (the exclusive scan of the bin totals)
+    const uint32_t *total;   // candidates in the batch
+    const uint8_t *regs;     // batch-entry registers
+    uint64_t *skey, *sval;   // encodes out: cell << 27 | packet, GNS_ID_NONE << 32 | reg | lz << 8 | old << 16
+    uint32_t *scount;        // encodes written (device count)
+    uint32_t *heads;         // [cells]: cell starts in skey, count at [cells]
+    uint32_t *work;          // bin counter of the persistent grid
+    unsigned long long *err; // a cell with more encodes than LDS holds (cannot happen below 8192)
+};
+
+constexpr uint32_t kSpMaxG = 512;       // cell groups of a large bin per window
+constexpr uint32_t kSpHalf = kSpCap / 2;  // group slot width (candidates)
+struct SpLds {
+    uint64_t a[kSpCap], b[kSpCap];
+    uint32_t cnt[256 * kSpWaves];  // radix counters, digit-major [digit][wave]
+    uint32_t gtab[3 * kSpMaxG];    // groups of a window: start, count, first cell
+    uint32_t gcur[kSpMaxG];
+    uint32_t wsum[kSpWaves + 2];
+    uint32_t bin, n_succ, gbase, ngrp, cend;
+    uint32_t agg_seg[kSpWaves], agg_mx[kSpWaves], agg_fl[kSpWaves];
+};
+
+// Exclusive scan of one value per thread over the workgroup; returns this
+// thread's start.  Uses L.wsum; synchronises.
+__device__ __forceinline__ uint32_t sp_block_excl(SpLds &L, uint32_t v) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t inc = wave_incl_scan(v);
+    __syncthreads();  // earlier readers of wsum are done
+    if (lane == 63) L.wsum[wave] = inc;
+    __syncthreads();
+    uint32_t run = inc - v;
+    for (uint32_t w = 0; w < wave; w++) run += L.wsum[w];
+    __syncthreads();
+    return run;
+}
+
+// Stable LSD radix sort (8-bit digits) of n <= kSpCap items of L.a / L.b by bits
+// [lo, hi); src is a or b; returns where the result is.  Item idx lives in lane
+// idx % 64 of wave idx / 512 (slot (idx / 64) % 8): a wave owns 512 consecutive
+// items, so returning LDS adds (same-address lanes served in lane order, the
+// Count-Min K3 property, measured on gfx950: tools/lds_order.hip) give stable ranks.
+__device__ uint64_t *sp_sort(SpLds &L, uint64_t *src, uint32_t n, uint32_t lo, uint32_t hi) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    uint64_t *dst = src == L.a ? L.b : L.a;
+    for (uint32_t sh = lo; sh < hi; sh += 8) {
+        const uint32_t nd = min(8u, hi - sh), ndig = 1u << nd, dmask = ndig - 1u;
+        for (uint32_t dg = lane; dg < ndig; dg += 64) L.cnt[dg * kSpWaves + wave] = 0;
+        uint64_t x[kSpPer];
+        uint32_t dg[kSpPer], rk[kSpPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kSpPer; j++) {
+            const uint32_t idx = wave * (kSpPer * 64) + j * 64 + lane;
+            const bool v = idx < n;
+            x[j] = v ? src[idx] : 0ull;
+            dg[j] = (uint32_t)(x[j] >> sh) & dmask;
+            rk[j] = atomicAdd(&L.cnt[dg[j] * kSpWaves + wave], v ? 1u : 0u);
+        }
+        __syncthreads();
+        // exclusive scan over (digit, wave): ndig * 16 <= 4096 counters, 4 per thread
+        const uint32_t nc = ndig * kSpWaves;
+        uint32_t c[4], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t i = tid * 4 + q;
+            c[q] = i < nc ? L.cnt[i] : 0u;
+            sum += c[q];
+        }
+        const uint32_t inc = wave_incl_scan(sum);
+        if (lane == 63) L.wsum[wave] = inc;
+        __syncthreads();
+        uint32_t run = inc - sum;
+        for (uint32_t w = 0; w < wave; w++) run += L.wsum[w];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t i = tid * 4 + q;
+            if (i < nc) L.cnt[i] = run;
+            run += c[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kSpPer; j++) {
+            const uint32_t idx = wave * (kSpPer * 64) + j * 64 + lane;
+            if (idx < n) dst[L.cnt[dg[j] * kSpWaves + wave] + rk[j]] = x[j];
+        }
+        __syncthreads();
+        uint64_t *t = src; src = dst; dst = t;
+    }
+    return src;
+}
+
+// Encodes of one group of whole cells (n <= kSpCap candidates in *src): sort by
+// (local seg, packet), segmented running max of lz per register, encode test
+// against the batch-entry register, encodes sorted by (cell, packet), written
+// out with their cell heads.  bin0seg = first seg of the bin.
+__device__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, uint32_t n, uint64_t bin0seg, uint64_t bin0cell) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    uint64_t *srt = sp_sort(L, src, n, 8, 35 + a.s.lbits);
+    uint64_t *out = srt == L.a ? L.b : L.a;
+    // thread-major: thread t holds sorted positions [8t, 8t + 8)
+    const uint32_t p0 = tid * kSpPer;
+    uint64_t x[kSpPer];
+    uint32_t seg_last = 0xFFFFFFFFu, mx = 0, full = 1, have = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kSpPer; j++) {
+        x[j] = p0 + j < n ? srt[p0 + j] : ~0ull;
+        if (p0 + j < n) {
+            const uint32_t sg = (uint32_t)(x[j] >> 35), lz = (uint32_t)x[j] & 0xFFu;
+            if (have && sg != seg_last) { full = 0; mx = 0; }
+            if (!have || sg != seg_last) mx = 0;
+            mx = max(mx, lz);
+            seg_last = sg;
+            have = 1;
+        }
+    }
+    // exclusive segmented max over the threads: aggregate (seg_last, mx, full, have);
+    // combine(L, R) = !R.have ? L : (R.full && R.seg == L.seg ? (seg, max, L.full, 1) : R)
+    uint32_t cs = seg_last, cm = mx, cf = full, ch = have;  // inclusive, built with shuffles
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t ls = __shfl_up(cs, o), lm = __shfl_up(cm, o), lf = __shfl_up(cf, o), lh = __shfl_up(ch, o);
+        if (lane >= o && lh) {
+            if (!ch) { cs = ls; cm = lm; cf = lf; ch = 1; }
+            else if (cf && cs == ls) { cm = max(cm, lm); cf = lf; }
+        }
+    }
+    if (lane == 63) { L.agg_seg[wave] = cs; L.agg_mx[wave] = cm; L.agg_fl[wave] = cf | (ch << 1); }
+    __syncthreads();
+    // carry into this thread = inclusive value of the previous lane, preceded by the earlier waves
+    uint32_t ps = __shfl_up(cs, 1), pm = __shfl_up(cm, 1), pf = __shfl_up(cf, 1), ph = __shfl_up(ch, 1);
+    if (lane == 0) ph = 0;
+    uint32_t ws = 0xFFFFFFFFu, wm = 0, wh = 0;  // waves before this one: last seg and its running max
+    for (uint32_t w = 0; w < wave; w++) {
+        const uint32_t rs = L.agg_seg[w], rm = L.agg_mx[w], rf = L.agg_fl[w] & 1u, rh = L.agg_fl[w] >> 1;
+        if (!rh) continue;
+        if (wh && rf && rs == ws) wm = max(wm, rm);
+        else { ws = rs; wm = rm; wh = 1; }
+    }
+    uint32_t carry_seg = 0xFFFFFFFFu, carry_mx = 0;
+    if (ph) {
+        carry_seg = ps; carry_mx = pm;
+        if (pf && wh && ws == ps) carry_mx = max(carry_mx, wm);
+    } else if (wh) {
+        carry_seg = ws; carry_mx = wm;
+    }
+    // encode test
+    uint32_t succ = 0;
+    uint64_t item[kSpPer];
+    uint32_t rseg = carry_seg, rmx = carry_mx;
+#pragma unroll
+    for (uint32_t j = 0; j < kSpPer; j++) {
+        item[j] = ~0ull;
+        if (p0 + j < n) {
+            const uint32_t sg = (uint32_t)(x[j] >> 35), lz = (uint32_t)x[j] & 0xFFu;
+            const uint32_t pk = (uint32_t)(x[j] >> 8) & ((1u << kSsPktBits) - 1u);
+            if (sg != rseg) { rseg = sg; rmx = 0; }
+            const uint64_t seg = bin0seg + sg;
+            const uint32_t old = max((uint32_t)a.regs[seg], rmx);
+            if (lz > old) {
+                const uint64_t cl = sp_cell(a.s, (uint64_t)sg);  // cell within the bin
+                const uint32_t reg = (uint32_t)((uint64_t)sg - cl * a.s.m);
+                item[j] = (cl << kSsPktBits | pk) << 24 | (uint64_t)(reg | lz << 8 | old << 16);
+                succ++;
+            }
+            rmx = max(rmx, lz);
+        }
+    }
+    // compact the encodes into `out` (order kept), then sort them by (cell, packet)
+    const uint32_t inc = wave_incl_scan(succ);
+    if (lane == 63) L.wsum[wave] = inc;
+    __syncthreads();
+    uint32_t q = inc - succ, ns = 0;
+    for (uint32_t w = 0; w < kSpWaves; w++) { if (w < wave) q += L.wsum[w]; ns += L.wsum[w]; }
+#pragma unroll
+    for (uint32_t j = 0; j < kSpPer; j++)
+        if (item[j] != ~0ull) out[q++] = item[j];
+    __syncthreads();
+    if (ns == 0) return;
+    uint32_t cbits = 0;
+    while ((1u << cbits) < a.s.cpb) cbits++;
+    uint64_t *es = sp_sort(L, out, ns, 24, 24 + kSsPktBits + cbits);
+    if (tid == 0) L.gbase = atomicAdd(a.scount, ns);
+    __syncthreads();
+    const uint32_t gb = L.gbase;
+    for (uint32_t i0 = 0; i0 < ns; i0 += kSpThreads) {  // block-uniform trip count
+        const uint32_t i = i0 + tid;
+        bool head = false;
+        if (i < ns) {
+            const uint64_t e = es[i];
+            const uint64_t ck = e >> 24;
+            const uint64_t cell = bin0cell + (ck >> kSsPktBits);
+            a.skey[gb + i] = cell << kSsPktBits | (ck & ((1ull << kSsPktBits) - 1));
+            a.sval[gb + i] = (uint64_t)GNS_ID_NONE << 32 | (e & 0xFFFFFFull);
+            head = i == 0 || (es[i - 1] >> (24 + kSsPktBits)) != (ck >> kSsPktBits);
+        }
+        const uint64_t hm = __ballot(head);
+        if (hm) {
+            const int leader = __ffsll((unsigned long long)hm) - 1;
+            uint32_t hb = 0;
+            if ((int)lane == leader) hb = atomicAdd(&a.heads[a.s.cells], (uint32_t)__popcll(hm));
+            hb = __shfl(hb, leader);
+            if (head) a.heads[hb + __popcll(hm & ((1ull << lane) - 1ull))] = gb + i;
+        }
+    }
+    __syncthreads();
+}
+
+// One cell with more candidates than LDS holds: the order-free form.  For every
+// (register, lz) the earliest packet (LDS atomicMin), then suffix minima over lz:
+// S[reg][v] = earliest packet with an lz >= v.  A candidate (reg, p, lz) encodes iff
+// S[reg][lz] == p; the register value it sees is the largest v < lz with
+// S[reg][v] < p, or the batch-entry register.
+__device__ void sp_giant(const SpArgs &a, SpLds &L, const uint64_t *w2, uint32_t n, uint64_t bin0seg, uint64_t cellg,
+                         uint32_t cl_in_bin) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t m = a.s.m;
+    uint32_t *S = reinterpret_cast<uint32_t *>(L.a);  // [m][kSpV] (m <= 256: 34 KB of the 64 KB)
+    const uint64_t seg0 = (uint64_t)cl_in_bin * m;   // local seg of the cell's register 0
+    for (uint32_t i = tid; i < m * kSpV; i += kSpThreads) S[i] = 0xFFFFFFFFu;
+    if (tid == 0) L.n_succ = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kSpThreads) {
+        const uint64_t x = __hip_atomic_load(w2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t reg = (uint32_t)((x >> 35) - seg0), lz = min((uint32_t)x & 0xFFu, kSpV - 1);
+        atomicMin(&S[reg * kSpV + lz], (uint32_t)(x >> 8) & ((1u << kSsPktBits) - 1u));
+    }
+    __syncthreads();
+    for (uint32_t r = tid; r < m; r += kSpThreads) {
+        uint32_t run = 0xFFFFFFFFu;
+        for (int v = (int)kSpV - 1; v >= 0; v--) { run = min(run, S[r * kSpV + v]); S[r * kSpV + v] = run; }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kSpThreads) {
+        const uint64_t x = __hip_atomic_load(w2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t reg = (uint32_t)((x >> 35) - seg0), lz = (uint32_t)x & 0xFFu;
+        const uint32_t pk = (uint32_t)(x >> 8) & ((1u << kSsPktBits) - 1u);
+        if (S[reg * kSpV + lz] != pk) continue;
+        const uint32_t entry = a.regs[(cellg * m) + reg];
+        uint32_t old = entry;
+        for (int v = (int)lz - 1; v > (int)entry; v--)
+            if (S[reg * kSpV + v] < pk) { old = (uint32_t)v; break; }
+        const uint32_t q = atomicAdd(&L.n_succ, 1u);
+        if (q < kSpCap) L.b[q] = (uint64_t)pk << 24 | (uint64_t)(reg | lz << 8 | old << 16);
+    }
+    __syncthreads();
+    uint32_t ns = L.n_succ;
+    if (ns > kSpCap) {
+        if (tid == 0) atomicAdd(a.err, 1ull);
+        ns = kSpCap;
+    }
+    if (ns == 0) return;
+    uint64_t *es = sp_sort(L, L.b, ns, 24, 24 + kSsPktBits);
+    if (tid == 0) {
+        L.gbase = atomicAdd(a.scount, ns);
+        a.heads[atomicAdd(&a.heads[a.s.cells], 1u)] = L.gbase;
+    }
+    __syncthreads();
+    const uint32_t gb = L.gbase;
+    for (uint32_t i = tid; i < ns; i += kSpThreads) {
+        const uint64_t e = es[i];
+        a.skey[gb + i] = cellg << kSsPktBits | (e >> 24);
+        a.sval[gb + i] = (uint64_t)GNS_ID_NONE << 32 | (e & 0xFFFFFFull);
+    }
+    __syncthreads();
+    (void)lane;
+}
+
+// P4: persistent; bins from a work counter.
+__global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t spsm[];
+    SpLds &L = *reinterpret_cast<SpLds *>(spsm);
+    const uint32_t tid = threadIdx.x;
+    for (;;) {
+        if (tid == 0) L.bin = atomicAdd(a.work, 1u);
+        __syncthreads();
+        const uint32_t bin = L.bin;
+        __syncthreads();
+        if (bin >= a.s.nb) return;
+        const uint32_t b0 = a.bstart[bin];
+        const uint32_t b1 = bin + 1 < a.s.nb ? a.bstart[bin + 1] : *a.total;
+        const uint32_t n = b1 - b0;
+        if (n == 0) continue;
+        const uint64_t bin0cell = (uint64_t)bin << a.s.cpb_bits;
+        const uint64_t bin0seg = bin0cell * a.s.m;
+        if (n <= kSpCap) {
+            for (uint32_t i = tid; i < n; i += kSpThreads) L.a[i] = a.words[b0 + i];
+            __syncthreads();
+            sp_group(a, L, L.a, n, bin0seg, bin0cell);
+            continue;
+        }
+        // a large bin: windows of cells.  Per window a cell histogram, its exclusive
+        // scan P, and groups by position: the cells with P in [s * kSpHalf, (s + 1) *
+        // kSpHalf) and at most kSpHalf candidates each form group 2s (< kSpCap
+        // candidates), a cell with more forms group 2s + 1 alone (at most one such
+        // cell starts per slot) and takes the order-free path.  The window's
+        // candidates are grouped into words2, then the groups run one by one.
+        uint32_t *ccnt = reinterpret_cast<uint32_t *>(L.b);  // [cpb] candidates per cell
+        uint32_t *cgid = ccnt + kSpMaxCpb;                   // [cpb] group of the cell
+        const uint32_t per = (a.s.cpb + kSpThreads - 1) / kSpThreads;  // <= 8 cells per thread
+        for (uint32_t cw = 0; cw < a.s.cpb;) {
+            for (uint32_t c = tid; c < a.s.cpb; c += kSpThreads) ccnt[c] = 0;
+            for (uint32_t g = tid; g < kSpMaxG; g += kSpThreads) { L.gtab[3 * g + 1] = 0; L.gtab[3 * g + 2] = 0xFFFFFFFFu; }
+            if (tid == 0) L.cend = a.s.cpb;
+            __syncthreads();
+            for (uint32_t i = tid; i < n; i += kSpThreads) {
+                const uint32_t c = (uint32_t)sp_cell(a.s, a.words[b0 + i] >> 35);
+                if (c >= cw) atomicAdd(&ccnt[c], 1u);
+            }
+            __syncthreads();
+            uint32_t k[8], sum = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t c = tid * per + q;
+                k[q] = (q < per && c < a.s.cpb) ? ccnt[c] : 0u;
+                sum += k[q];
+            }
+            uint32_t run = sp_block_excl(L, sum);
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t c = tid * per + q;
+                if (k[q]) {
+                    const uint32_t slot = run / kSpHalf;
+                    if (slot < kSpMaxG / 2) {
+                        const uint32_t g = 2 * slot + (k[q] > kSpHalf ? 1u : 0u);
+                        cgid[c] = g;
+                        atomicAdd(&L.gtab[3 * g + 1], k[q]);
+                        atomicMin(&L.gtab[3 * g + 2], c);
+                    } else {
+                        atomicMin(&L.cend, c);  // this cell opens the next window
+                    }
+                }
+                run += k[q];
+            }
+            __syncthreads();
+            // group starts: exclusive scan of the kSpMaxG group counts (one per thread)
+            const uint32_t gn_t = tid < kSpMaxG ? L.gtab[3 * tid + 1] : 0u;
+            const uint32_t gs_t = sp_block_excl(L, gn_t);
+            if (tid < kSpMaxG) { L.gtab[3 * tid] = gs_t; L.gcur[tid] = gs_t; }
+            __syncthreads();
+            const uint32_t ce = L.cend;
+            for (uint32_t i = tid; i < n; i += kSpThreads) {
+                const uint64_t x = a.words[b0 + i];
+                const uint32_t c = (uint32_t)sp_cell(a.s, x >> 35);
+                if (c >= cw && c < ce) a.words2[b0 + atomicAdd(&L.gcur[cgid[c]], 1u)] = x;
+            }
+            __threadfence();
+            __syncthreads();
+            for (uint32_t g = 0; g < kSpMaxG; g++) {
+                const uint32_t gs = L.gtab[3 * g], gn = L.gtab[3 * g + 1], gf = L.gtab[3 * g + 2];
+                if (gn == 0) continue;  // block-uniform
+                __syncthreads();
+                if (g & 1u) {
+                    sp_giant(a, L, a.words2 + b0 + gs, gn, bin0seg, bin0cell + gf, gf);
+                } else {
+                    for (uint32_t i = tid; i < gn; i += kSpThreads)
+                        L.a[i] = __hip_atomic_load(a.words2 + b0 + gs + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __syncthreads();
+                    sp_group(a, L, L.a, gn, bin0seg, bin0cell);
+                }
+            }
+            __syncthreads();
+            cw = ce;
+        }
+    }
+}
 
 }  // namespace gns
 
@@ -653,14 +1069,19 @@ struct gns_ss {
     uint32_t *pcnt[2] = {nullptr, nullptr};
     uint32_t *ptotal = nullptr;
     uint64_t ccap = 0;
+    // candidates (S1) -> ckey / cval; bin-major words (P3) -> ckey_s; P4 scratch
+    // skey_s; encodes (P4) -> skey / sval.  After P4 the candidate buffers hold
+    // S3b's parked lists, then S5's per-encode scratch.
     uint64_t *ckey = nullptr, *ckey_s = nullptr, *skey = nullptr, *skey_s = nullptr;
-    uint32_t *cval = nullptr, *cval_s = nullptr, *cmax = nullptr;
-    uint64_t *sval = nullptr, *sval_s = nullptr;
-    uint32_t *counts = nullptr;  // [0] candidates, [1] successes
+    uint32_t *cval = nullptr;
+    uint64_t *sval = nullptr;
+    uint32_t *counts = nullptr;  // [0] candidates, [1] encodes, [2] P4 bin counter, [3] candidates (P2)
     uint32_t *heads = nullptr;   // [cells + 1]: S5 segment starts (unordered), then their count
     uint32_t *cblk = nullptr;
-    void *tmp = nullptr;
-    size_t tmp_bytes = 0;
+    SpGeom sp{};
+    uint32_t ncu = 0;
+    uint32_t *shist = nullptr;   // [nblk][nb] per-block bin histogram -> offsets
+    uint32_t *spart = nullptr;   // [ngrp][nb] group partials, then [nb] bin starts
     unsigned long long *stats = nullptr;
     uint32_t *h_pin = nullptr;
     uint8_t *stage = nullptr;
@@ -680,8 +1101,8 @@ void ss_free_all(gns_ss *ss) {
     dfree(ss->regs); dfree(ss->pbits); dfree(ss->values); dfree(ss->keys); dfree(ss->D.rec);
     dfree(ss->pcnt[0]); dfree(ss->pcnt[1]);
     dfree(ss->ptotal); dfree(ss->ckey); dfree(ss->ckey_s); dfree(ss->skey); dfree(ss->skey_s);
-    dfree(ss->cval); dfree(ss->cval_s); dfree(ss->cmax); dfree(ss->sval); dfree(ss->sval_s);
-    dfree(ss->counts); dfree(ss->heads); dfree(ss->cblk); dfree(ss->tmp); dfree(ss->stats); dfree(ss->stage);
+    dfree(ss->cval); dfree(ss->sval); dfree(ss->shist); dfree(ss->spart);
+    dfree(ss->counts); dfree(ss->heads); dfree(ss->cblk); dfree(ss->stats); dfree(ss->stage);
     dfree(ss->dctl); dfree(ss->stats_bak); ss->dsc.free_all();
     if (ss->h_pin) (void)hipHostFree(ss->h_pin);
     ss->timer.destroy();
@@ -706,32 +1127,20 @@ int ss_reset_state(gns_ss *ss, bool init) {
     return GNS_OK;
 }
 
-size_t ss_tmp_need(gns_ss *ss, uint64_t n) {
-    size_t a = 0, b = 0, c = 0;
-    const unsigned bits = kSsPktBits + ceil_log2((uint64_t)ss->g.d * ss->g.w * ss->g.m) + 1;
-    (void)rocprim::radix_sort_pairs(nullptr, a, ss->ckey, ss->ckey_s, ss->cval, ss->cval_s, (size_t)n, 0u,
-                                    std::min(64u, bits), ss->stream);
-    auto kit = rocprim::make_transform_iterator(ss->ckey_s, SegKey());
-    (void)rocprim::inclusive_scan_by_key(nullptr, b, kit, ss->cval_s, ss->cmax, (size_t)n,
-                                         rocprim::maximum<uint32_t>(), rocprim::equal_to<uint64_t>(),
-                                         ss->stream);
-    (void)rocprim::radix_sort_pairs(nullptr, c, ss->skey, ss->skey_s, ss->sval, ss->sval_s, (size_t)n, 0u,
-                                    std::min(64u, bits), ss->stream);
-    return std::max(std::max(a, b), c) + 256;
-}
-
-// S3b driver: flow ids of the ns encodes (sval high words), with the
-// first-sight resolve rounds (a key claimed in this launch parks its other
-// encodes until the claim is committed).  The candidate buffers are free
-// after S3: ckey / ckey_s hold the parked lists.  Runs before any state is
-// written, so a full dictionary leaves the sketch unchanged.
+// S3b driver: flow ids of the encodes (sval high words; their count stays on
+// the device), with the first-sight resolve rounds (a key claimed in this launch
+// parks its other encodes until the claim is committed).  The candidate buffers
+// are free after P4: ckey / ckey_s hold the parked lists.  Runs before any state
+// is written, so an overflowing dictionary leaves the sketch unchanged.  The
+// batch's one host round trip is here: after the second round, whether a third
+// is needed (rarely) and whether the dictionary overflowed.
 template <int KIND, int MF, int MM>
-int ss_encode_ids(gns_ss *ss, const InputDesc &in, uint32_t ns) {
+int ss_encode_ids(gns_ss *ss, const InputDesc &in) {
     hipStream_t s = ss->stream;
-    const uint32_t nb = (ns + kSsIdChunk - 1) / kSsIdChunk;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((ss->ccap + kSsIdChunk - 1) / kSsIdChunk, 2048);
     uint64_t *pend[2] = {ss->ckey, ss->ckey_s};
     SsIdsArgs r{};
-    r.in = in; r.kpf = ss->kpf; r.kpm = ss->kpm; r.g = ss->g; r.D = ss->D; r.ns = ns;
+    r.in = in; r.kpf = ss->kpf; r.kpm = ss->kpm; r.g = ss->g; r.D = ss->D; r.ns = ss->counts + 1;
     r.skey = ss->skey; r.sval = ss->sval; r.stats = ss->stats;
     ScopedStage st(ss->timer, 1);
     GNS_HIP(hipMemsetAsync(ss->ptotal, 0, 8, s));
@@ -743,9 +1152,9 @@ int ss_encode_ids(gns_ss *ss, const InputDesc &in, uint32_t ns) {
         r.pend_out = pend[cur ^ 1]; r.cnt_out = ss->pcnt[cur ^ 1]; r.total_out = ss->ptotal + (cur ^ 1);
         if (round == 0) {
             r.pend_out = pend[0]; r.cnt_out = ss->pcnt[0]; r.total_out = ss->ptotal;
-            hipLaunchKernelGGL((k_ss_ids<KIND, MF, MM, true>), dim3(nb), dim3(kSsThreads), 0, s, r);
+            hipLaunchKernelGGL((k_ss_ids<KIND, MF, MM, true>), dim3(grid), dim3(kSsThreads), 0, s, r);
         } else {
-            hipLaunchKernelGGL((k_ss_ids<KIND, MF, MM, false>), dim3(nb), dim3(kSsThreads), 0, s, r);
+            hipLaunchKernelGGL((k_ss_ids<KIND, MF, MM, false>), dim3(grid), dim3(kSsThreads), 0, s, r);
             cur ^= 1;
         }
         GNS_HIP(hipGetLastError());
@@ -756,11 +1165,21 @@ int ss_encode_ids(gns_ss *ss, const InputDesc &in, uint32_t ns) {
         GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
         GNS_HIP(hipMemcpyAsync(ss->h_pin + 2, ss->stats + 3, 8, hipMemcpyDeviceToHost, s));
         GNS_HIP(hipMemcpyAsync(ss->h_pin + 4, ss->dctl, 4, hipMemcpyDeviceToHost, s));
+        if (round == 1) {
+            GNS_HIP(hipMemcpyAsync(ss->h_pin + 5, ss->counts + 1, 4, hipMemcpyDeviceToHost, s));
+            GNS_HIP(hipMemcpyAsync(ss->h_pin + 6, ss->stats + 6, 8, hipMemcpyDeviceToHost, s));
+        }
         GNS_HIP(hipStreamSynchronize(s));
+        if (round == 1 && (ss->h_pin[6] | ss->h_pin[7])) {  // P4: a cell's encodes exceed kSpCap
+            GNS_HIP(hipMemsetAsync(ss->stats + 6, 0, 8, s));
+            set_error("a cell has more than %u encodes in one batch: use a smaller batch_packets", kSpCap);
+            return GNS_E_RANGE;
+        }
+        if (round == 1) ss->n_encodes += ss->h_pin[5];
         ss->claimed = ss->h_pin[4];
         if (ss->h_pin[2] | ss->h_pin[3]) {
-            set_error("flow dictionary full (max_flows %llu, %llu slots); raise max_flows",
-                      (unsigned long long)ss->max_flows, (unsigned long long)ss->dict_slots);
+            if (round == 1) ss->n_encodes -= ss->h_pin[5];  // the batch is re-run
+            set_error("flow dictionary full (%llu slots)", (unsigned long long)ss->dict_slots);
             return GNS_E_FULL;
         }
         if (ss->h_pin[0] == 0) return GNS_OK;
@@ -774,9 +1193,12 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     if (n == 0) return GNS_OK;
     hipStream_t s = ss->stream;
     const uint32_t nblk = (uint32_t)((n + kSsChunk - 1) / kSsChunk);
+    const uint32_t cells = ss->g.d * ss->g.w;
+    const SpGeom &sg = ss->sp;
     ScopedStage total_stage(ss->timer, 5);
     GNS_HIP(hipMemsetAsync(ss->ptotal, 0, 8, s));
-    GNS_HIP(hipMemsetAsync(ss->counts, 0, 8, s));
+    GNS_HIP(hipMemsetAsync(ss->counts, 0, 16, s));     // [0] candidates, [1] encodes, [2] P4 bin counter
+    GNS_HIP(hipMemsetAsync(ss->heads + cells, 0, 4, s));
     GNS_HIP(hipMemsetAsync(ss->dctl + 1, 0, 4, s));  // abort flag of this batch
     if (++ss->epoch == 0) ss->epoch = 1;
     SsExtractArgs x{};
@@ -799,52 +1221,37 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
             hipLaunchKernelGGL((k_ss_extract<KIND, MF, MM, 0, 0>), dim3(nblk), dim3(kSsThreads), 0, s, x);
         GNS_HIP(hipGetLastError());
     }
-    GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->counts, 4, hipMemcpyDeviceToHost, s));
-    GNS_HIP(hipStreamSynchronize(s));
-    const uint32_t nc = ss->h_pin[0];
-    if (nc > 0) {
-        const unsigned bits = std::min(64u, kSsPktBits + ceil_log2((uint64_t)ss->g.d * ss->g.w * ss->g.m) + 1);
-        {
-            ScopedStage st(ss->timer, 2);
-            hipLaunchKernelGGL(k_ss_compact, dim3(nblk), dim3(256), 0, s, ss->ckey, ss->cval, ss->cblk, ss->g.d,
-                               ss->ckey_s, ss->cval_s);
-            GNS_HIP(hipGetLastError());
-            size_t tb = ss->tmp_bytes;
-            if (rocprim::radix_sort_pairs(ss->tmp, tb, ss->ckey_s, ss->ckey, ss->cval_s, ss->cval, (size_t)nc, 0u,
-                                          bits, s) != hipSuccess) { set_error("candidate sort failed"); return GNS_E_HIP; }
-            auto kit = rocprim::make_transform_iterator(ss->ckey, SegKey());
-            tb = ss->tmp_bytes;
-            if (rocprim::inclusive_scan_by_key(ss->tmp, tb, kit, ss->cval, ss->cmax, (size_t)nc,
-                                               rocprim::maximum<uint32_t>(), rocprim::equal_to<uint64_t>(),
-                                               s) != hipSuccess) { set_error("segmented max failed"); return GNS_E_HIP; }
-            SsSuccArgs a{ss->ckey, ss->cval, ss->cmax, nc, ss->regs, ss->g.m, ss->skey, ss->sval, ss->counts + 1};
-            hipLaunchKernelGGL(k_ss_success, dim3((nc + 256 * kSsSuccItems - 1) / (256 * kSsSuccItems)), dim3(256), 0, s, a);
-            GNS_HIP(hipGetLastError());
-        }
-        GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->counts + 1, 4, hipMemcpyDeviceToHost, s));
-        GNS_HIP(hipStreamSynchronize(s));
-        const uint32_t ns = ss->h_pin[0];
-        if (ns > 0) GNS_TRY((ss_encode_ids<KIND, MF, MM>(ss, in, ns)));
-        ss->n_encodes += ns;
-        if (ns > 0) {
-            ScopedStage st(ss->timer, 3);
-            const unsigned bits2 = std::min(64u, kSsPktBits + ceil_log2((uint64_t)ss->g.d * ss->g.w) + 1);
-            size_t tb = ss->tmp_bytes;
-            if (rocprim::radix_sort_pairs(ss->tmp, tb, ss->skey, ss->skey_s, ss->sval, ss->sval_s, (size_t)ns, 0u,
-                                          bits2, s) != hipSuccess) { set_error("encode sort failed"); return GNS_E_HIP; }
-            // the sort's sources are free now: pbits-before and repeat counts go there
-            const uint32_t cells = ss->g.d * ss->g.w;
-            SsApplyArgs a{ss->skey_s, ss->sval_s, ns, ss->g, ss->pkt, ss->regs, ss->pbits, ss->values, ss->keys,
-                          reinterpret_cast<double *>(ss->skey), reinterpret_cast<int64_t *>(ss->sval), ss->heads, cells};
-            const uint32_t hgrid = (std::min<uint32_t>(ns, cells) + 255) / 256;  // segments <= touched cells
-            GNS_HIP(hipMemsetAsync(ss->heads + cells, 0, 4, s));
-            hipLaunchKernelGGL(k_ss_heads, dim3((ns + 256 * kSsHeadItems - 1) / (256 * kSsHeadItems)), dim3(256), 0, s,
-                               ss->skey_s, ns, ss->heads, cells);
-            hipLaunchKernelGGL(k_ss_walk_pbits, dim3(hgrid), dim3(256), 0, s, a);
-            hipLaunchKernelGGL(k_ss_sample, dim3((ns + 255) / 256), dim3(256), 0, s, a);
-            hipLaunchKernelGGL(k_ss_walk_mv, dim3(hgrid), dim3(256), 0, s, a);
-            GNS_HIP(hipGetLastError());
-        }
+    {   // P1-P4: candidates -> encodes sorted by (cell, packet), heads; no host round trip
+        ScopedStage st(ss->timer, 2);
+        const uint32_t ngrp = (nblk + kTGrp - 1) / kTGrp;
+        const dim3 g2((sg.nb + 255) / 256, ngrp);
+        uint32_t *tot = ss->spart + (size_t)ngrp * sg.nb;
+        hipLaunchKernelGGL(k_sp_hist, dim3(nblk), dim3(256), 0, s, ss->ckey, ss->cblk, ss->g.d, sg, ss->shist);
+        hipLaunchKernelGGL(k_tscan_part, g2, dim3(256), 0, s, ss->shist, nblk, sg.nb, ss->spart);
+        hipLaunchKernelGGL(k_tscan_mid, dim3((sg.nb + 255) / 256), dim3(256), 0, s, ss->spart, ngrp, sg.nb, tot);
+        hipLaunchKernelGGL(k_tscan_bins, dim3(1), dim3(1024), 0, s, tot, sg.nb, ss->counts + 3);
+        hipLaunchKernelGGL(k_tscan_down, g2, dim3(256), 0, s, ss->shist, nblk, sg.nb, ss->spart, tot);
+        hipLaunchKernelGGL(k_sp_scatter, dim3(nblk), dim3(256), 0, s, ss->ckey, ss->cval, ss->cblk, ss->g.d, sg,
+                           ss->shist, ss->ckey_s);
+        SpArgs pa{};
+        pa.s = sg; pa.words = ss->ckey_s; pa.words2 = ss->skey_s; pa.bstart = tot; pa.total = ss->counts + 3;
+        pa.regs = ss->regs; pa.skey = ss->skey; pa.sval = ss->sval; pa.scount = ss->counts + 1;
+        pa.heads = ss->heads; pa.work = ss->counts + 2; pa.err = ss->stats + 6;
+        hipLaunchKernelGGL(k_sp_bins, dim3(std::min(sg.nb, ss->ncu)), dim3(kSpThreads), sizeof(SpLds), s, pa);
+        GNS_HIP(hipGetLastError());
+    }
+    GNS_TRY((ss_encode_ids<KIND, MF, MM>(ss, in)));
+    {
+        ScopedStage st(ss->timer, 3);
+        // the candidate buffers are free now: pbits-before and repeat counts go there
+        SsApplyArgs a{ss->skey, ss->sval, ss->counts + 1, ss->g, ss->pkt, ss->regs, ss->pbits, ss->values, ss->keys,
+                      reinterpret_cast<double *>(ss->ckey), reinterpret_cast<int64_t *>(ss->skey_s), ss->heads, cells};
+        const uint32_t hgrid = (cells + 255) / 256;  // one lane per touched cell at most
+        const uint32_t egrid = (uint32_t)std::min<uint64_t>((ss->ccap + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_ss_walk_pbits, dim3(hgrid), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_ss_sample, dim3(egrid), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_ss_walk_mv, dim3(hgrid), dim3(256), 0, s, a);
+        GNS_HIP(hipGetLastError());
     }
     ss->pkt += n;  // every record advances the RNG packet index
     ss->n_batches++;
@@ -1059,6 +1466,29 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
         g.hll_master = p->hll_master;
         g.rng_seed = p->rng_seed;
         if ((uint64_t)g.d * g.w * g.m > (1ull << 36)) { set_error("d*w*m too large"); rc = GNS_E_ARG; break; }
+        {   // P1-P4 bins: cpb (a power of two) consecutive cells, about 512 bins
+            SpGeom &sg = ss->sp;
+            const uint64_t cells = (uint64_t)g.d * g.w;
+            sg.cpb = 1; sg.cpb_bits = 0;
+            while ((uint64_t)sg.cpb * 512 < cells && sg.cpb < kSpMaxCpb) { sg.cpb <<= 1; sg.cpb_bits++; }
+            const uint64_t nb = (cells + sg.cpb - 1) / sg.cpb;
+            if (nb > kSpMaxBins) {
+                set_error("SuperSpread: depth * width <= %u cells", kSpMaxBins * kSpMaxCpb);
+                rc = GNS_E_ARG;
+                break;
+            }
+            sg.nb = (uint32_t)nb;
+            sg.m = g.m;
+            sg.mbits = (g.m & (g.m - 1)) == 0 ? (uint32_t)__builtin_ctz(g.m) : 0xFFu;
+            sg.lbits = 0;
+            while ((1ull << sg.lbits) < (uint64_t)sg.cpb * g.m) sg.lbits++;
+            sg.cells = (uint32_t)cells;
+            int dev = 0, ncu = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+                ncu = 256;
+            ss->ncu = (uint32_t)ncu;
+        }
         if (hipStreamCreateWithFlags(&ss->stream, hipStreamNonBlocking) != hipSuccess) {
             set_error("hipStreamCreate failed"); rc = GNS_E_HIP; break;
         }
@@ -1095,13 +1525,12 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
             (rc = dalloc_t(&ss->pcnt[1], nblk_enc)) || (rc = dalloc_t(&ss->ptotal, 2)) ||
             (rc = dalloc_t(&ss->ckey, ss->ccap)) || (rc = dalloc_t(&ss->ckey_s, ss->ccap)) ||
             (rc = dalloc_t(&ss->skey, ss->ccap)) || (rc = dalloc_t(&ss->skey_s, ss->ccap)) ||
-            (rc = dalloc_t(&ss->cval, ss->ccap)) || (rc = dalloc_t(&ss->cval_s, ss->ccap)) ||
-            (rc = dalloc_t(&ss->cmax, ss->ccap)) || (rc = dalloc_t(&ss->sval, ss->ccap)) ||
-            (rc = dalloc_t(&ss->sval_s, ss->ccap)) || (rc = dalloc_t(&ss->counts, 4)) || (rc = dalloc_t(&ss->cblk, 2ull * ss->nblk_max)) ||
+            (rc = dalloc_t(&ss->cval, ss->ccap)) || (rc = dalloc_t(&ss->sval, ss->ccap)) ||
+            (rc = dalloc_t(&ss->counts, 4)) || (rc = dalloc_t(&ss->cblk, 2ull * ss->nblk_max)) ||
+            (rc = dalloc_t(&ss->shist, (uint64_t)ss->nblk_max * ss->sp.nb)) ||
+            (rc = dalloc_t(&ss->spart, ((uint64_t)(ss->nblk_max + kTGrp - 1) / kTGrp + 1) * ss->sp.nb)) ||
             (rc = dalloc_t(&ss->stats, 8)))
             break;
-        ss->tmp_bytes = ss_tmp_need(ss, ss->ccap);
-        if ((rc = dalloc(&ss->tmp, ss->tmp_bytes)) != GNS_OK) break;
         if (hipHostMalloc(reinterpret_cast<void **>(&ss->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
         }
