@@ -677,6 +677,7 @@ struct SpArgs {
     uint32_t *heads;         // [cells]: cell starts in skey, count at [cells]
     uint32_t *work;          // bin counter of the persistent grid
     unsigned long long *err; // a cell with more encodes than LDS holds (cannot happen below 8192)
+    uint32_t maxg;           // groups per window of a large bin (kSpMaxG; GNS_SS_SPG, tests only)
 };
 
 constexpr uint32_t kSpMaxG = 512;       // cell groups of a large bin per window
@@ -968,7 +969,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
         const uint32_t per = (a.s.cpb + kSpThreads - 1) / kSpThreads;  // <= 8 cells per thread
         for (uint32_t cw = 0; cw < a.s.cpb;) {
             for (uint32_t c = tid; c < a.s.cpb; c += kSpThreads) ccnt[c] = 0;
-            for (uint32_t g = tid; g < kSpMaxG; g += kSpThreads) { L.gtab[3 * g + 1] = 0; L.gtab[3 * g + 2] = 0xFFFFFFFFu; }
+            for (uint32_t g = tid; g < a.maxg; g += kSpThreads) { L.gtab[3 * g + 1] = 0; L.gtab[3 * g + 2] = 0xFFFFFFFFu; }
             if (tid == 0) L.cend = a.s.cpb;
             __syncthreads();
             for (uint32_t i = tid; i < n; i += kSpThreads) {
@@ -989,7 +990,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
                 const uint32_t c = tid * per + q;
                 if (k[q]) {
                     const uint32_t slot = run / kSpHalf;
-                    if (slot < kSpMaxG / 2) {
+                    if (slot < a.maxg / 2) {
                         const uint32_t g = 2 * slot + (k[q] > kSpHalf ? 1u : 0u);
                         cgid[c] = g;
                         atomicAdd(&L.gtab[3 * g + 1], k[q]);
@@ -1001,10 +1002,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
                 run += k[q];
             }
             __syncthreads();
-            // group starts: exclusive scan of the kSpMaxG group counts (one per thread)
-            const uint32_t gn_t = tid < kSpMaxG ? L.gtab[3 * tid + 1] : 0u;
+            // group starts: exclusive scan of the group counts (one per thread)
+            const uint32_t gn_t = tid < a.maxg ? L.gtab[3 * tid + 1] : 0u;
             const uint32_t gs_t = sp_block_excl(L, gn_t);
-            if (tid < kSpMaxG) { L.gtab[3 * tid] = gs_t; L.gcur[tid] = gs_t; }
+            if (tid < a.maxg) { L.gtab[3 * tid] = gs_t; L.gcur[tid] = gs_t; }
             __syncthreads();
             const uint32_t ce = L.cend;
             for (uint32_t i = tid; i < n; i += kSpThreads) {
@@ -1014,7 +1015,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
             }
             __threadfence();
             __syncthreads();
-            for (uint32_t g = 0; g < kSpMaxG; g++) {
+            for (uint32_t g = 0; g < a.maxg; g++) {
                 const uint32_t gs = L.gtab[3 * g], gn = L.gtab[3 * g + 1], gf = L.gtab[3 * g + 2];
                 if (gn == 0) continue;  // block-uniform
                 __syncthreads();
@@ -1080,6 +1081,7 @@ struct gns_ss {
     uint32_t *cblk = nullptr;
     SpGeom sp{};
     uint32_t ncu = 0;
+    uint32_t sp_maxg = 0;        // P4 groups per window of a large bin
     uint32_t *shist = nullptr;   // [nblk][nb] per-block bin histogram -> offsets
     uint32_t *spart = nullptr;   // [ngrp][nb] group partials, then [nb] bin starts
     unsigned long long *stats = nullptr;
@@ -1237,6 +1239,7 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         pa.s = sg; pa.words = ss->ckey_s; pa.words2 = ss->skey_s; pa.bstart = tot; pa.total = ss->counts + 3;
         pa.regs = ss->regs; pa.skey = ss->skey; pa.sval = ss->sval; pa.scount = ss->counts + 1;
         pa.heads = ss->heads; pa.work = ss->counts + 2; pa.err = ss->stats + 6;
+        pa.maxg = ss->sp_maxg;
         hipLaunchKernelGGL(k_sp_bins, dim3(std::min(sg.nb, ss->ncu)), dim3(kSpThreads), sizeof(SpLds), s, pa);
         GNS_HIP(hipGetLastError());
     }
@@ -1488,6 +1491,9 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
                 hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
                 ncu = 256;
             ss->ncu = (uint32_t)ncu;
+            const char *env = getenv("GNS_SS_SPG");  // tests: small windows exercise the window loop
+            const long v = env ? strtol(env, nullptr, 10) : 0;
+            ss->sp_maxg = (v >= 2 && v <= (long)kSpMaxG) ? (uint32_t)(v & ~1L) : kSpMaxG;
         }
         if (hipStreamCreateWithFlags(&ss->stream, hipStreamNonBlocking) != hipSuccess) {
             set_error("hipStreamCreate failed"); rc = GNS_E_HIP; break;

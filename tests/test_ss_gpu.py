@@ -309,3 +309,24 @@ def test_unbounded_distinct_flows_reclaim(gpu, oracle, batch):
     assert ds["reclaims"] > 0 and ds["dropped"] > 4 * max_flows, ds
     assert ss.counters()["dict_full"] == 0
     assert_same_list([(h.Flow, h.Count) for h in ss.heavy_hitters().Count], orc.heavy())
+
+
+@pytest.mark.parametrize("spg", [None, "8", "2"])
+def test_large_bins_giant_cells_and_windows(gpu, oracle, monkeypatch, spg):
+    """P4's large-bin path (gns_ss.hip k_sp_bins): one device batch from empty
+    registers, so every packet-row is a candidate; a source with 30% of the packets
+    gives cells of > 4096 candidates (the order-free form) inside multi-cell bins.
+    GNS_SS_SPG shrinks the per-window group table so the window loop runs many times."""
+    if spg is not None:
+        monkeypatch.setenv("GNS_SS_SPG", spg)
+    rng = np.random.default_rng(909)
+    n = 1_000_000
+    ss, orc = make_pair(oracle, 4096, 2, 64, 5, 16, 16, thr=100, batch_packets=n)
+    fl, el, flows = spread_stream(rng, n, 50_000, 16, 16, s=1.05, elem_pool=1 << 19)
+    heavy = rng.random(n) < 0.3
+    fl[heavy] = flows[7]
+    ss.insert_keys(fl, el)
+    ss.flush()
+    orc.insert(fl, el)
+    assert_same_ss(ss, orc)
+    assert_same_list([(h.Flow, h.Count) for h in ss.heavy_hitters().Count], orc.heavy())
