@@ -455,7 +455,7 @@ extern "C" __device__ unsigned __ockl_wfscan_add_u32(unsigned, bool);
 // the flow's packets that were parked in X1).  first stays: a designated flow
 // had packets before this batch.
 __global__ __launch_bounds__(256) void k_ex_hot_reduce(const ExHotPart *hpart, uint32_t nblk, const uint32_t *hot_ids,
-                                                       uint64_t pkt_base, FlowState f) {
+                                                       uint64_t pkt_base, FlowState f, uint32_t *touch, uint32_t *tcnt) {
     __shared__ unsigned long long s_by[4];
     __shared__ uint32_t s_c[4], s_mx[4];
     const uint32_t slot = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -482,6 +482,7 @@ __global__ __launch_bounds__(256) void k_ex_hot_reduce(const ExHotPart *hpart, u
             f.pkts[id] += c;
             f.bytes[id] += by;
             f.last[id] = max(f.last[id], pkt_base + mx + 1);
+            touch[atomicAdd(tcnt, 1u)] = id;  // designated flows never reach P
         }
     }
 }
@@ -646,8 +647,22 @@ constexpr uint32_t kAggDepth = GNS_AGG_DEPTH;  // chunks of words in flight
 constexpr uint32_t kAggCap = GNS_AGG_CAP;  // 24 B per entry: 72 KB
 constexpr int kAggMinBlocks = kAggCap * 24 <= 78 * 1024 ? 2 : 1;
 static_assert(kAggCap > kAggChunk, "a chunk fits an empty table");
+// Touched-flow list (T and D read it instead of scanning the table): a flow is
+// appended when its first merge of the batch lands (its last index is then still
+// from an earlier batch), so each flow appears once.
+__device__ __forceinline__ void touch_append(bool app, uint32_t id, uint32_t *touch, uint32_t *tcnt) {
+    const uint64_t m = __ballot(app);
+    if (!m) return;  // wave-uniform
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)__lane_id() == leader) base = atomicAdd(tcnt, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (app) touch[base + __popcll(m & ((1ull << __lane_id()) - 1ull))] = id;
+}
+
 __device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t *mn, uint32_t *mx,
-                                           unsigned long long *by, uint64_t pkt_base, FlowState f) {
+                                           unsigned long long *by, uint64_t pkt_base, FlowState f, uint32_t *touch,
+                                           uint32_t *tcnt) {
     // every entry's four state words are loaded before any is merged (all in flight together)
     constexpr uint32_t kPer = (kAggCap + kAggThreads - 1) / kAggThreads;
     uint32_t id[kPer];
@@ -661,6 +676,7 @@ __device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t
 #pragma unroll
     for (uint32_t j = 0; j < kPer; j++) {
         const uint32_t e = threadIdx.x + j * kAggThreads;
+        touch_append(id[j] != GNS_ID_NONE && ls[j] <= pkt_base, id[j], touch, tcnt);
         if (id[j] == GNS_ID_NONE) continue;
         f.pkts[id[j]] = pk[j] + cn[e];
         f.bytes[id[j]] = bt[j] + by[e];
@@ -697,7 +713,7 @@ __device__ __forceinline__ uint32_t pagg_slot(uint32_t *key, uint32_t id, uint32
 }
 __global__ __launch_bounds__(kAggThreads, kAggMinBlocks) void k_ex_pagg(const uint64_t *in, const uint32_t *pb, uint32_t sb,
                                                             uint32_t ib, const uint32_t *sizes, uint64_t pkt_base,
-                                                            FlowState f) {
+                                                            FlowState f, uint32_t *touch, uint32_t *tcnt) {
     __shared__ __attribute__((aligned(16))) uint32_t key[kAggCap];
     __shared__ uint32_t cn[kAggCap], mn[kAggCap], mx[kAggCap];
     __shared__ unsigned long long by[kAggCap];
@@ -719,7 +735,7 @@ __global__ __launch_bounds__(kAggThreads, kAggMinBlocks) void k_ex_pagg(const ui
     __syncthreads();
     for (uint32_t c0 = beg; c0 < end; c0 += kAggChunk) {  // block-uniform trip count
         if (s_n > kAggCap - kAggChunk) {  // block-uniform (read after the barrier)
-            pagg_flush(key, cn, mn, mx, by, pkt_base, f);
+            pagg_flush(key, cn, mn, mx, by, pkt_base, f, touch, tcnt);
             __syncthreads();
             if (tid == 0) s_n = 0;
             __syncthreads();
@@ -767,18 +783,20 @@ __global__ __launch_bounds__(kAggThreads, kAggMinBlocks) void k_ex_pagg(const ui
         }
         __syncthreads();
     }
-    pagg_flush(key, cn, mn, mx, by, pkt_base, f);
+    pagg_flush(key, cn, mn, mx, by, pkt_base, f, touch, tcnt);
 }
 
 // T: StartTime / EndTime from the merged stream indices of the flows this batch
 // touched (task.go:137,141-142).
-__global__ __launch_bounds__(256) void k_ex_times(FlowState f, uint64_t slots, uint64_t pkt_base, uint64_t n,
-                                                  const int64_t *ts) {
-    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (s >= slots) return;
-    const unsigned long long l = f.last[s], fs = f.first[s];
-    if (l > pkt_base && l <= pkt_base + n) f.end[s] = ts[l - 1 - pkt_base];
-    if (fs >= pkt_base && fs < pkt_base + n) f.start[s] = ts[fs - pkt_base];
+__global__ __launch_bounds__(256) void k_ex_times(FlowState f, const uint32_t *touch, const uint32_t *tcnt,
+                                                  uint64_t pkt_base, uint64_t n, const int64_t *ts) {
+    const uint32_t nt = *tcnt;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nt; i += gridDim.x * 256) {
+        const uint32_t s = touch[i];
+        const unsigned long long l = f.last[s], fs = f.first[s];
+        if (l > pkt_base && l <= pkt_base + n) f.end[s] = ts[l - 1 - pkt_base];
+        if (fs >= pkt_base && fs < pkt_base + n) f.start[s] = ts[fs - pkt_base];
+    }
 }
 
 // D: designate the next batch's heavy flows: the flows in the largest 1/8-octave
@@ -788,12 +806,16 @@ __device__ __forceinline__ uint32_t exh_key(unsigned long long p) {
     const uint32_t lz = 63u - (uint32_t)__clzll((long long)p);
     return lz * 8u + (uint32_t)((p >> (lz - 3)) & 7u);
 }
-__global__ __launch_bounds__(256) void k_exh_hist(const unsigned long long *pkts, uint64_t slots, uint32_t *hist) {
+// (over the flows the batch touched: a flow designated now had packets in this
+// batch; the choice only steers performance, every choice is exact)
+__global__ __launch_bounds__(256) void k_exh_hist(const unsigned long long *pkts, const uint32_t *touch,
+                                                  const uint32_t *tcnt, uint32_t *hist) {
     __shared__ uint32_t h[512];
     for (uint32_t i = threadIdx.x; i < 512; i += 256) h[i] = 0;
     __syncthreads();
-    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * 256) {
-        const uint32_t k = exh_key(pkts[s]);
+    const uint32_t nt = *tcnt;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nt; i += gridDim.x * 256) {
+        const uint32_t k = exh_key(pkts[touch[i]]);
         if (k >= kExHotMinKey) atomicAdd(&h[k], 1u);
     }
     __syncthreads();
@@ -819,14 +841,17 @@ __global__ __launch_bounds__(512) void k_exh_pick(const uint32_t *hist, uint32_t
     __syncthreads();
     if (k == 0) *thr = s_t;
 }
-__global__ __launch_bounds__(256) void k_exh_collect(const unsigned long long *pkts, uint64_t slots,
-                                                     const uint32_t *thr, uint32_t *cnt, uint32_t *hot_ids) {
-    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (s >= slots) return;
-    const uint32_t k = exh_key(pkts[s]);
-    if (k >= *thr && k >= kExHotMinKey) {
-        const uint32_t q = atomicAdd(cnt, 1u);
-        if (q < kExHot) hot_ids[q] = (uint32_t)s;
+__global__ __launch_bounds__(256) void k_exh_collect(const unsigned long long *pkts, const uint32_t *touch,
+                                                     const uint32_t *tcnt, const uint32_t *thr, uint32_t *cnt,
+                                                     uint32_t *hot_ids) {
+    const uint32_t nt = *tcnt;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nt; i += gridDim.x * 256) {
+        const uint32_t s = touch[i];
+        const uint32_t k = exh_key(pkts[s]);
+        if (k >= *thr && k >= kExHotMinKey) {
+            const uint32_t q = atomicAdd(cnt, 1u);
+            if (q < kExHot) hot_ids[q] = s;
+        }
     }
 }
 // the lookup table, heaviest flows first (64 at a time): a flow whose 4-entry group
@@ -946,7 +971,8 @@ struct gns_ex {
     uint32_t *hot_ids = nullptr;             // [kExHot] designated flows (GNS_ID_NONE: unused slot)
     unsigned long long *hot_tab = nullptr;   // [kExHotTab] their lookup table
     ExHotPart *hpart = nullptr;              // [kExHot][nblk_max]
-    uint32_t *hctl = nullptr;                // [0..511] count histogram, [512] threshold, [513] count, [514] tail words
+    uint32_t *hctl = nullptr;                // [0..511] count histogram, [512] threshold, [513] count, [514] tail words, [515] touched
+    uint32_t *touch = nullptr;               // [bmax + kExHot] flows the batch touched (T, D)
     uint32_t *ccnt = nullptr;                // [nblk_max] X1 region word counts
     bool warm = false;                       // flows designated (a batch ran since create / reset / growth)
     uint32_t *ph = nullptr, *pgs = nullptr, *pb = nullptr;  // P histograms / offsets, group sums, bin starts
@@ -975,7 +1001,7 @@ void ex_free_all(gns_ex *ex) {
     dfree(ex->f.start); dfree(ex->f.end); dfree(ex->pend[0]); dfree(ex->pend[1]);
     dfree(ex->pcnt[0]); dfree(ex->pcnt[1]); dfree(ex->ptotal); dfree(ex->stats); dfree(ex->stage);
     dfree(ex->sk[0]); dfree(ex->sk[1]); dfree(ex->ph); dfree(ex->pgs); dfree(ex->pb);
-    dfree(ex->hot_ids); dfree(ex->hot_tab); dfree(ex->hpart); dfree(ex->hctl); dfree(ex->ccnt);
+    dfree(ex->hot_ids); dfree(ex->touch); dfree(ex->hot_tab); dfree(ex->hpart); dfree(ex->hctl); dfree(ex->ccnt);
     dfree(ex->dctl); dfree(ex->stats_bak); ex->dsc.free_all();
     if (ex->h_pin) (void)hipHostFree(ex->h_pin);
     ex->timer.destroy();
@@ -1052,7 +1078,9 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     const uint32_t ng = (nblk + kPGroup - 1) / kPGroup;
     {
         ScopedStage st(ex->timer, 4);
-        hipLaunchKernelGGL(k_ex_hot_reduce, dim3(kExHot), dim3(256), 0, s, ex->hpart, nblk, ex->hot_ids, ex->pkt, ex->f);
+        GNS_HIP(hipMemsetAsync(ex->hctl + 515, 0, 4, s));  // touched flows of this batch
+        hipLaunchKernelGGL(k_ex_hot_reduce, dim3(kExHot), dim3(256), 0, s, ex->hpart, nblk, ex->hot_ids, ex->pkt, ex->f,
+                           ex->touch, ex->hctl + 515);
         GNS_HIP(hipGetLastError());
     }
     {
@@ -1069,20 +1097,20 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     {
         ScopedStage st(ex->timer, 3);
         hipLaunchKernelGGL(k_ex_pagg, dim3(kPBins), dim3(kAggThreads), 0, s, ex->sk[1], ex->pb, ex->sb, ex->ib,
-                           xin.in.sizes, ex->pkt, ex->f);
+                           xin.in.sizes, ex->pkt, ex->f, ex->touch, ex->hctl + 515);
         GNS_HIP(hipGetLastError());
     }
     {   // timestamps of the touched flows; the next batch's designated flows
         ScopedStage st(ex->timer, 4);
-        const unsigned sg = (unsigned)((ex->slots + 255) / 256);
-        hipLaunchKernelGGL(k_ex_times, dim3(sg), dim3(256), 0, s, ex->f, ex->slots, ex->pkt, n, xin.ts);
+        // sized by the batch, not the table: at most n + kExHot flows are touched
+        const unsigned sg = (unsigned)std::min<uint64_t>((n + kExHot + 255) / 256, 2048);
+        hipLaunchKernelGGL(k_ex_times, dim3(sg), dim3(256), 0, s, ex->f, ex->touch, ex->hctl + 515, ex->pkt, n, xin.ts);
         GNS_HIP(hipMemsetAsync(ex->hctl, 0, 514 * 4, s));
         GNS_HIP(hipMemsetAsync(ex->hot_ids, 0xFF, kExHot * 4, s));
-        hipLaunchKernelGGL(k_exh_hist, dim3(std::min<unsigned>(sg, 2048)), dim3(256), 0, s, ex->f.pkts, ex->slots,
-                           ex->hctl);
+        hipLaunchKernelGGL(k_exh_hist, dim3(sg), dim3(256), 0, s, ex->f.pkts, ex->touch, ex->hctl + 515, ex->hctl);
         hipLaunchKernelGGL(k_exh_pick, dim3(1), dim3(512), 0, s, ex->hctl, ex->hctl + 512);
-        hipLaunchKernelGGL(k_exh_collect, dim3(sg), dim3(256), 0, s, ex->f.pkts, ex->slots, ex->hctl + 512,
-                           ex->hctl + 513, ex->hot_ids);
+        hipLaunchKernelGGL(k_exh_collect, dim3(sg), dim3(256), 0, s, ex->f.pkts, ex->touch, ex->hctl + 515,
+                           ex->hctl + 512, ex->hctl + 513, ex->hot_ids);
         hipLaunchKernelGGL(k_exh_table, dim3(1), dim3(kExHot), 0, s, ex->hot_ids, ex->f.pkts, ex->hot_tab);
         GNS_HIP(hipGetLastError());
     }
@@ -1308,7 +1336,7 @@ int gns_ex_create(const gns_ex_params *p, gns_ex **out) {
             (rc = dalloc_t(&ex->pcnt[0], ex->nblk_max)) || (rc = dalloc_t(&ex->pcnt[1], ex->nblk_max)) ||
             (rc = dalloc_t(&ex->ptotal, 2)) || (rc = dalloc_t(&ex->stats, 8)) ||
             (rc = dalloc_t(&ex->sk[0], ex->bmax)) || (rc = dalloc_t(&ex->sk[1], ex->bmax)) ||
-            (rc = dalloc_t(&ex->hot_ids, kExHot)) || (rc = dalloc_t(&ex->hot_tab, kExHotTab)) ||
+            (rc = dalloc_t(&ex->hot_ids, kExHot)) || (rc = dalloc_t(&ex->touch, ex->bmax + kExHot)) || (rc = dalloc_t(&ex->hot_tab, kExHotTab)) ||
             (rc = dalloc_t(&ex->hpart, (uint64_t)kExHot * ex->nblk_max)) || (rc = dalloc_t(&ex->hctl, 516)) ||
             (rc = dalloc_t(&ex->ccnt, ex->nblk_max)) || (rc = dalloc_t(&ex->ph, (uint64_t)ex->nblk_max * kPBins)) ||
             (rc = dalloc_t(&ex->pgs, (uint64_t)(ex->nblk_max / kPGroup + 1) * kPBins)) ||
