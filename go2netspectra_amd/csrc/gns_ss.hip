@@ -431,64 +431,80 @@ __global__ __launch_bounds__(256) void k_ss_sample(SsApplyArgs a) {
     }
 }
 
+// S5c, one wave per touched cell: the wave loads 64 encodes of the cell's chain
+// at a time (coalesced) and steps through the sampled ones only (ballot), the
+// scalar MV state wave-uniform and the encode's fields read with v_readlane.  A
+// superspreader's cell holds thousands of encodes, most unsampled: a lane per
+// cell paid one dependent load round trip per encode.
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int j) { return __builtin_amdgcn_readlane(v, j); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int j) {
+    return (uint64_t)rl32((uint32_t)(v >> 32), j) << 32 | rl32((uint32_t)v, j);
+}
+
 __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
-    const uint32_t hi = blockIdx.x * 256 + threadIdx.x;
-    if (hi >= a.heads[a.cells]) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nh = a.heads[a.cells];
     const uint32_t nenc = *a.ns;
-    const uint32_t k0 = a.heads[hi];
-    const uint64_t cell = a.skey[k0] >> kSsPktBits;
-    const uint32_t row = (uint32_t)(cell / a.g.w);
-    uint32_t val = a.values[cell], key = a.keys[cell];
-    // b^-val and log1m(b^-val) depend only on val: kept for the next foreign
-    // encode while val does not change
-    uint32_t mval = 0xFFFFFFFFu;
-    double mppp = 0.0, ml1m = 0.0;
-    uint64_t kc = a.skey[k0], vc = a.sval[k0];
-    int64_t rc = a.rep[k0];
-    double lc = a.tp[k0];
-    for (uint32_t k = k0;;) {
-        const uint32_t kn = k + 1;  // the next encode's inputs load while this one runs
-        const uint64_t kx = kn < nenc ? a.skey[kn] : ~0ull;
-        const uint64_t vx = kn < nenc ? a.sval[kn] : 0ull;
-        const int64_t rx = kn < nenc ? a.rep[kn] : 0;
-        const double lx = kn < nenc ? a.tp[kn] : 0.0;
-        int64_t vv = rc;
-        const uint32_t f = (uint32_t)(vc >> 32);
-        const uint64_t pkt = a.pkt_base + (kc & ((1ull << kSsPktBits) - 1));
-        uint32_t draw = 1;
-        while (vv > 0) {                                                    // :207-233
-            if (val == 0 || key == f) {  // every remaining iteration increments (:211-220)
-                if (val == 0) key = f;
-                val = (uint32_t)((uint64_t)val + (uint64_t)vv);
-                break;
+    for (uint32_t hi = blockIdx.x * 4 + (threadIdx.x >> 6); hi < nh; hi += gridDim.x * 4) {  // wave-uniform
+        const uint32_t k0 = a.heads[hi];
+        const uint64_t cell = a.skey[k0] >> kSsPktBits;
+        const uint32_t row = (uint32_t)(cell / a.g.w);
+        uint32_t val = a.values[cell], key = a.keys[cell];
+        // b^-val and log1m(b^-val) depend only on val: kept for the next foreign
+        // encode while val does not change
+        uint32_t mval = 0xFFFFFFFFu;
+        double mppp = 0.0, ml1m = 0.0;
+        for (uint32_t w0 = k0;; w0 += 64) {
+            const uint32_t k = w0 + lane;
+            const uint64_t kx = k < nenc ? a.skey[k] : ~0ull;
+            const uint64_t inm = __ballot((kx >> kSsPktBits) == cell);  // a prefix: the chain is contiguous
+            const uint32_t len = inm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~inm);
+            int64_t rx = 0;
+            uint64_t vx = 0;
+            double lx = 0.0;
+            if (lane < len) { rx = a.rep[k]; vx = a.sval[k]; lx = a.tp[k]; }
+            uint64_t sm = __ballot(lane < len && rx > 0);
+            while (sm) {
+                const int j = __ffsll((unsigned long long)sm) - 1;
+                sm &= sm - 1;
+                int64_t vv = (int64_t)rl64((uint64_t)rx, j);
+                const uint32_t f = rl32((uint32_t)(vx >> 32), j);
+                const uint64_t pkt = a.pkt_base + (rl64(kx, j) & ((1ull << kSsPktBits) - 1));
+                const double lc = __longlong_as_double((long long)rl64((uint64_t)__double_as_longlong(lx), j));
+                uint32_t draw = 1;
+                while (vv > 0) {                                                    // :207-233
+                    if (val == 0 || key == f) {  // every remaining iteration increments (:211-220)
+                        if (val == 0) key = f;
+                        val = (uint32_t)((uint64_t)val + (uint64_t)vv);
+                        break;
+                    }
+                    if (val != mval) {
+                        mval = val;
+                        mppp = go_pow_int(a.g.b, -(double)val);                         // :222
+                        ml1m = (mppp > 0 && mppp < 1) ? gm_log1m(mppp) : 0.0;
+                    }
+                    const double ppp = mppp;
+                    if (!(ppp > 0)) break;  // underflow: no later iteration can decrement
+                    if (ppp >= 1) {         // b <= 1: every iteration decrements
+                        const int64_t dec = (int64_t)val < vv ? (int64_t)val : vv;
+                        val -= (uint32_t)dec;
+                        vv -= dec;
+                        continue;
+                    }
+                    // declared generator: failed iterations before the next decrement
+                    // (:223-227) as one geometric waiting time; the first draw's log came from S5b
+                    const double lu = draw == 1 ? lc : gm_log(1.0 - ss_uniform(a.g.rng_seed, pkt, row, draw));
+                    draw++;
+                    const double q = lu / ml1m;
+                    if (!(q < (double)vv)) break;
+                    vv -= (int64_t)floor(q) + 1;
+                    val -= 1;
+                }
             }
-            if (val != mval) {
-                mval = val;
-                mppp = go_pow_int(a.g.b, -(double)val);                         // :222
-                ml1m = (mppp > 0 && mppp < 1) ? gm_log1m(mppp) : 0.0;
-            }
-            const double ppp = mppp;
-            if (!(ppp > 0)) break;  // underflow: no later iteration can decrement
-            if (ppp >= 1) {         // b <= 1: every iteration decrements
-                const int64_t dec = (int64_t)val < vv ? (int64_t)val : vv;
-                val -= (uint32_t)dec;
-                vv -= dec;
-                continue;
-            }
-            // declared generator: failed iterations before the next decrement
-            // (:223-227) as one geometric waiting time; the first draw's log came from S5b
-            const double lu = draw == 1 ? lc : gm_log(1.0 - ss_uniform(a.g.rng_seed, pkt, row, draw));
-            draw++;
-            const double q = lu / ml1m;
-            if (!(q < (double)vv)) break;
-            vv -= (int64_t)floor(q) + 1;
-            val -= 1;
+            if (len < 64) break;
         }
-        if ((kx >> kSsPktBits) != cell) break;
-        k = kn; kc = kx; vc = vx; rc = rx; lc = lx;
+        if (lane == 0) { a.values[cell] = val; a.keys[cell] = key; }
     }
-    a.values[cell] = val;
-    a.keys[cell] = key;
 }
 #pragma clang fp contract(on)
 
@@ -676,6 +692,7 @@ struct SpArgs {
     uint32_t *scount;        // encodes written (device count)
     uint32_t *heads;         // [cells]: cell starts in skey, count at [cells]
     uint32_t *work;          // bin counter of the persistent grid
+    const uint32_t *order;   // [nb] bins, largest first (k_sp_order)
     unsigned long long *err; // a cell with more encodes than LDS holds (cannot happen below 8192)
     uint32_t maxg;           // groups per window of a large bin (kSpMaxG; GNS_SS_SPG, tests only)
 };
@@ -691,6 +708,27 @@ struct SpLds {
     uint32_t bin, n_succ, gbase, ngrp, cend;
     uint32_t agg_seg[kSpWaves], agg_mx[kSpWaves], agg_fl[kSpWaves];
 };
+
+// f(i, x) for every x = src[i], i < n, with eight loads per thread in flight
+// (a loop of one load per trip waits a full memory round trip per trip).  Words
+// another wave of this workgroup wrote before a __syncthreads() are visible to
+// plain loads (same CU, same L1).
+template <typename F>
+__device__ __forceinline__ void sp_for8(const uint64_t *src, uint32_t n, F f) {
+    for (uint32_t i0 = 0; i0 < n; i0 += kSpThreads * 8) {  // block-uniform
+        uint64_t x[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t i = i0 + j * kSpThreads + threadIdx.x;
+            x[j] = i < n ? src[i] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t i = i0 + j * kSpThreads + threadIdx.x;
+            if (i < n) f(i, x[j]);
+        }
+    }
+}
 
 // Exclusive scan of one value per thread over the workgroup; returns this
 // thread's start.  Uses L.wsum; synchronises.
@@ -889,29 +927,27 @@ __device__ void sp_giant(const SpArgs &a, SpLds &L, const uint64_t *w2, uint32_t
     for (uint32_t i = tid; i < m * kSpV; i += kSpThreads) S[i] = 0xFFFFFFFFu;
     if (tid == 0) L.n_succ = 0;
     __syncthreads();
-    for (uint32_t i = tid; i < n; i += kSpThreads) {
-        const uint64_t x = __hip_atomic_load(w2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sp_for8(w2, n, [&](uint32_t, uint64_t x) {
         const uint32_t reg = (uint32_t)((x >> 35) - seg0), lz = min((uint32_t)x & 0xFFu, kSpV - 1);
         atomicMin(&S[reg * kSpV + lz], (uint32_t)(x >> 8) & ((1u << kSsPktBits) - 1u));
-    }
+    });
     __syncthreads();
     for (uint32_t r = tid; r < m; r += kSpThreads) {
         uint32_t run = 0xFFFFFFFFu;
         for (int v = (int)kSpV - 1; v >= 0; v--) { run = min(run, S[r * kSpV + v]); S[r * kSpV + v] = run; }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < n; i += kSpThreads) {
-        const uint64_t x = __hip_atomic_load(w2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sp_for8(w2, n, [&](uint32_t, uint64_t x) {
         const uint32_t reg = (uint32_t)((x >> 35) - seg0), lz = (uint32_t)x & 0xFFu;
         const uint32_t pk = (uint32_t)(x >> 8) & ((1u << kSsPktBits) - 1u);
-        if (S[reg * kSpV + lz] != pk) continue;
+        if (S[reg * kSpV + lz] != pk) return;
         const uint32_t entry = a.regs[(cellg * m) + reg];
         uint32_t old = entry;
         for (int v = (int)lz - 1; v > (int)entry; v--)
             if (S[reg * kSpV + v] < pk) { old = (uint32_t)v; break; }
         const uint32_t q = atomicAdd(&L.n_succ, 1u);
         if (q < kSpCap) L.b[q] = (uint64_t)pk << 24 | (uint64_t)(reg | lz << 8 | old << 16);
-    }
+    });
     __syncthreads();
     uint32_t ns = L.n_succ;
     if (ns > kSpCap) {
@@ -935,13 +971,56 @@ __device__ void sp_giant(const SpArgs &a, SpLds &L, const uint64_t *w2, uint32_t
     (void)lane;
 }
 
-// P4: persistent; bins from a work counter.
+// P4 schedule: bins by decreasing size (1/8-octave classes; the order inside a
+// class is arbitrary), so a superspreader's bin starts first instead of setting
+// the tail.  One workgroup, nb <= kSpMaxBins.
+__global__ __launch_bounds__(1024) void k_sp_order(const uint32_t *bstart, const uint32_t *total, uint32_t nb,
+                                                   uint32_t *order) {
+    constexpr uint32_t NK = 33 * 8;
+    __shared__ uint32_t s_cnt[NK];
+    __shared__ uint16_t s_key[kSpMaxBins];
+    for (uint32_t k = threadIdx.x; k < NK; k += 1024) s_cnt[k] = 0;
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += 1024) {
+        const uint32_t sz = (b + 1 < nb ? bstart[b + 1] : *total) - bstart[b];
+        const uint32_t lz = __clz(sz);
+        const uint32_t key = sz == 0 ? 0u : (32u - lz) * 8u + ((sz << lz) >> 28 & 7u);
+        s_key[b] = (uint16_t)key;
+        atomicAdd(&s_cnt[key], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // descending exclusive scan of the class counts
+        constexpr uint32_t PER = (NK + 63) / 64;
+        const uint32_t lane = threadIdx.x;
+        uint32_t x[PER], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t k = lane * PER + q;  // k-th class from the top
+            x[q] = k < NK ? s_cnt[NK - 1 - k] : 0u;
+            sum += x[q];
+        }
+        uint32_t run = wave_incl_scan(sum) - sum;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t k = lane * PER + q;
+            if (k < NK) s_cnt[NK - 1 - k] = run;
+            run += x[q];
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += 1024) order[atomicAdd(&s_cnt[s_key[b]], 1u)] = b;
+}
+
+// P4: persistent; bins from a work counter, largest first.
 __global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t spsm[];
     SpLds &L = *reinterpret_cast<SpLds *>(spsm);
     const uint32_t tid = threadIdx.x;
     for (;;) {
-        if (tid == 0) L.bin = atomicAdd(a.work, 1u);
+        if (tid == 0) {
+            const uint32_t k = atomicAdd(a.work, 1u);
+            L.bin = k < a.s.nb ? a.order[k] : 0xFFFFFFFFu;
+        }
         __syncthreads();
         const uint32_t bin = L.bin;
         __syncthreads();
@@ -953,7 +1032,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
         const uint64_t bin0cell = (uint64_t)bin << a.s.cpb_bits;
         const uint64_t bin0seg = bin0cell * a.s.m;
         if (n <= kSpCap) {
-            for (uint32_t i = tid; i < n; i += kSpThreads) L.a[i] = a.words[b0 + i];
+            sp_for8(a.words + b0, n, [&](uint32_t i, uint64_t x) { L.a[i] = x; });
             __syncthreads();
             sp_group(a, L, L.a, n, bin0seg, bin0cell);
             continue;
@@ -972,10 +1051,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
             for (uint32_t g = tid; g < a.maxg; g += kSpThreads) { L.gtab[3 * g + 1] = 0; L.gtab[3 * g + 2] = 0xFFFFFFFFu; }
             if (tid == 0) L.cend = a.s.cpb;
             __syncthreads();
-            for (uint32_t i = tid; i < n; i += kSpThreads) {
-                const uint32_t c = (uint32_t)sp_cell(a.s, a.words[b0 + i] >> 35);
+            sp_for8(a.words + b0, n, [&](uint32_t, uint64_t x) {
+                const uint32_t c = (uint32_t)sp_cell(a.s, x >> 35);
                 if (c >= cw) atomicAdd(&ccnt[c], 1u);
-            }
+            });
             __syncthreads();
             uint32_t k[8], sum = 0;
 #pragma unroll
@@ -1008,12 +1087,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
             if (tid < a.maxg) { L.gtab[3 * tid] = gs_t; L.gcur[tid] = gs_t; }
             __syncthreads();
             const uint32_t ce = L.cend;
-            for (uint32_t i = tid; i < n; i += kSpThreads) {
-                const uint64_t x = a.words[b0 + i];
+            sp_for8(a.words + b0, n, [&](uint32_t, uint64_t x) {
                 const uint32_t c = (uint32_t)sp_cell(a.s, x >> 35);
                 if (c >= cw && c < ce) a.words2[b0 + atomicAdd(&L.gcur[cgid[c]], 1u)] = x;
-            }
-            __threadfence();
+            });
             __syncthreads();
             for (uint32_t g = 0; g < a.maxg; g++) {
                 const uint32_t gs = L.gtab[3 * g], gn = L.gtab[3 * g + 1], gf = L.gtab[3 * g + 2];
@@ -1022,8 +1099,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
                 if (g & 1u) {
                     sp_giant(a, L, a.words2 + b0 + gs, gn, bin0seg, bin0cell + gf, gf);
                 } else {
-                    for (uint32_t i = tid; i < gn; i += kSpThreads)
-                        L.a[i] = __hip_atomic_load(a.words2 + b0 + gs + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    sp_for8(a.words2 + b0 + gs, gn, [&](uint32_t i, uint64_t x) { L.a[i] = x; });
                     __syncthreads();
                     sp_group(a, L, L.a, gn, bin0seg, bin0cell);
                 }
@@ -1084,6 +1160,7 @@ struct gns_ss {
     uint32_t sp_maxg = 0;        // P4 groups per window of a large bin
     uint32_t *shist = nullptr;   // [nblk][nb] per-block bin histogram -> offsets
     uint32_t *spart = nullptr;   // [ngrp][nb] group partials, then [nb] bin starts
+    uint32_t *sorder = nullptr;  // [nb] P4 schedule
     unsigned long long *stats = nullptr;
     uint32_t *h_pin = nullptr;
     uint8_t *stage = nullptr;
@@ -1103,7 +1180,7 @@ void ss_free_all(gns_ss *ss) {
     dfree(ss->regs); dfree(ss->pbits); dfree(ss->values); dfree(ss->keys); dfree(ss->D.rec);
     dfree(ss->pcnt[0]); dfree(ss->pcnt[1]);
     dfree(ss->ptotal); dfree(ss->ckey); dfree(ss->ckey_s); dfree(ss->skey); dfree(ss->skey_s);
-    dfree(ss->cval); dfree(ss->sval); dfree(ss->shist); dfree(ss->spart);
+    dfree(ss->cval); dfree(ss->sval); dfree(ss->shist); dfree(ss->spart); dfree(ss->sorder);
     dfree(ss->counts); dfree(ss->heads); dfree(ss->cblk); dfree(ss->stats); dfree(ss->stage);
     dfree(ss->dctl); dfree(ss->stats_bak); ss->dsc.free_all();
     if (ss->h_pin) (void)hipHostFree(ss->h_pin);
@@ -1240,6 +1317,8 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         pa.regs = ss->regs; pa.skey = ss->skey; pa.sval = ss->sval; pa.scount = ss->counts + 1;
         pa.heads = ss->heads; pa.work = ss->counts + 2; pa.err = ss->stats + 6;
         pa.maxg = ss->sp_maxg;
+        pa.order = ss->sorder;
+        hipLaunchKernelGGL(k_sp_order, dim3(1), dim3(1024), 0, s, tot, ss->counts + 3, sg.nb, ss->sorder);
         hipLaunchKernelGGL(k_sp_bins, dim3(std::min(sg.nb, ss->ncu)), dim3(kSpThreads), sizeof(SpLds), s, pa);
         GNS_HIP(hipGetLastError());
     }
@@ -1253,7 +1332,8 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         const uint32_t egrid = (uint32_t)std::min<uint64_t>((ss->ccap + 255) / 256, 4096);
         hipLaunchKernelGGL(k_ss_walk_pbits, dim3(hgrid), dim3(256), 0, s, a);
         hipLaunchKernelGGL(k_ss_sample, dim3(egrid), dim3(256), 0, s, a);
-        hipLaunchKernelGGL(k_ss_walk_mv, dim3(hgrid), dim3(256), 0, s, a);
+        const uint32_t wgrid = std::min<uint32_t>((cells + 3) / 4, 16384);  // one wave per touched cell
+        hipLaunchKernelGGL(k_ss_walk_mv, dim3(wgrid), dim3(256), 0, s, a);
         GNS_HIP(hipGetLastError());
     }
     ss->pkt += n;  // every record advances the RNG packet index
@@ -1535,7 +1615,7 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
             (rc = dalloc_t(&ss->counts, 4)) || (rc = dalloc_t(&ss->cblk, 2ull * ss->nblk_max)) ||
             (rc = dalloc_t(&ss->shist, (uint64_t)ss->nblk_max * ss->sp.nb)) ||
             (rc = dalloc_t(&ss->spart, ((uint64_t)(ss->nblk_max + kTGrp - 1) / kTGrp + 1) * ss->sp.nb)) ||
-            (rc = dalloc_t(&ss->stats, 8)))
+            (rc = dalloc_t(&ss->sorder, ss->sp.nb)) || (rc = dalloc_t(&ss->stats, 8)))
             break;
         if (hipHostMalloc(reinterpret_cast<void **>(&ss->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
