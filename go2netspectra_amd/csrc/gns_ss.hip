@@ -377,6 +377,7 @@ struct SsApplyArgs {
     double *tp;    // [n] pbits before each encode (S5a -> S5b); then log(1 - first MV draw) (S5b -> S5c)
     int64_t *rep;  // [n] MV repeat count, 0 = not sampled (S5b -> S5c)
     const uint32_t *heads;  // segment starts, [nh] count at heads[cells]
+    const uint32_t *hlen;   // encodes per segment
     uint32_t cells;
 };
 
@@ -431,79 +432,114 @@ __global__ __launch_bounds__(256) void k_ss_sample(SsApplyArgs a) {
     }
 }
 
-// S5c, one wave per touched cell: the wave loads 64 encodes of the cell's chain
-// at a time (coalesced) and steps through the sampled ones only (ballot), the
-// scalar MV state wave-uniform and the encode's fields read with v_readlane.  A
-// superspreader's cell holds thousands of encodes, most unsampled: a lane per
-// cell paid one dependent load round trip per encode.
+// S5c: the MV loop over a cell's sampled encodes (super_spread.go:206-233).
+// Lane per cell, as S5a; a cell with a long chain (a superspreader's: thousands
+// of encodes, few sampled) is walked by the whole wave afterwards, 64 encodes
+// per coalesced load and only the sampled ones stepped through (ballot), the MV
+// state wave-uniform and the encode's fields read with v_readlane -- a lane
+// walking it would pay one dependent load round trip per encode.
+constexpr uint32_t kSsLongChain = 48;
+
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int j) { return __builtin_amdgcn_readlane(v, j); }
 __device__ __forceinline__ uint64_t rl64(uint64_t v, int j) {
     return (uint64_t)rl32((uint32_t)(v >> 32), j) << 32 | rl32((uint32_t)v, j);
 }
 
+// one sampled encode: vv repeats of the MV step for flow f (state in val/key)
+struct MvState {
+    uint32_t val, key, mval;
+    double mppp, ml1m;
+};
+__device__ __forceinline__ void mv_encode(const SsApplyArgs &a, MvState &st, int64_t vv, uint32_t f, uint64_t pkt,
+                                          uint32_t row, double lc) {
+    uint32_t draw = 1;
+    while (vv > 0) {                                                    // :207-233
+        if (st.val == 0 || st.key == f) {  // every remaining iteration increments (:211-220)
+            if (st.val == 0) st.key = f;
+            st.val = (uint32_t)((uint64_t)st.val + (uint64_t)vv);
+            break;
+        }
+        // b^-val and log1m(b^-val) depend only on val: kept for the next foreign
+        // encode while val does not change
+        if (st.val != st.mval) {
+            st.mval = st.val;
+            st.mppp = go_pow_int(a.g.b, -(double)st.val);                   // :222
+            st.ml1m = (st.mppp > 0 && st.mppp < 1) ? gm_log1m(st.mppp) : 0.0;
+        }
+        const double ppp = st.mppp;
+        if (!(ppp > 0)) break;  // underflow: no later iteration can decrement
+        if (ppp >= 1) {         // b <= 1: every iteration decrements
+            const int64_t dec = (int64_t)st.val < vv ? (int64_t)st.val : vv;
+            st.val -= (uint32_t)dec;
+            vv -= dec;
+            continue;
+        }
+        // declared generator: failed iterations before the next decrement
+        // (:223-227) as one geometric waiting time; the first draw's log came from S5b
+        const double lu = draw == 1 ? lc : gm_log(1.0 - ss_uniform(a.g.rng_seed, pkt, row, draw));
+        draw++;
+        const double q = lu / st.ml1m;
+        if (!(q < (double)vv)) break;
+        vv -= (int64_t)floor(q) + 1;
+        st.val -= 1;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t hi = blockIdx.x * 256 + threadIdx.x;
     const uint32_t nh = a.heads[a.cells];
     const uint32_t nenc = *a.ns;
-    for (uint32_t hi = blockIdx.x * 4 + (threadIdx.x >> 6); hi < nh; hi += gridDim.x * 4) {  // wave-uniform
+    const bool valid = hi < nh;
+    const uint32_t len = valid ? a.hlen[hi] : 0u;
+    if (valid && len <= kSsLongChain) {
         const uint32_t k0 = a.heads[hi];
         const uint64_t cell = a.skey[k0] >> kSsPktBits;
         const uint32_t row = (uint32_t)(cell / a.g.w);
-        uint32_t val = a.values[cell], key = a.keys[cell];
-        // b^-val and log1m(b^-val) depend only on val: kept for the next foreign
-        // encode while val does not change
-        uint32_t mval = 0xFFFFFFFFu;
-        double mppp = 0.0, ml1m = 0.0;
-        for (uint32_t w0 = k0;; w0 += 64) {
-            const uint32_t k = w0 + lane;
-            const uint64_t kx = k < nenc ? a.skey[k] : ~0ull;
-            const uint64_t inm = __ballot((kx >> kSsPktBits) == cell);  // a prefix: the chain is contiguous
-            const uint32_t len = inm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~inm);
+        MvState st{a.values[cell], a.keys[cell], 0xFFFFFFFFu, 0.0, 0.0};
+        uint64_t kc = a.skey[k0], vc = a.sval[k0];
+        int64_t rc = a.rep[k0];
+        double lc = a.tp[k0];
+        for (uint32_t k = k0;;) {
+            const uint32_t kn = k + 1;  // the next encode's inputs load while this one runs
+            const uint64_t kx = kn < nenc ? a.skey[kn] : ~0ull;
+            const uint64_t vx = kn < nenc ? a.sval[kn] : 0ull;
+            const int64_t rx = kn < nenc ? a.rep[kn] : 0;
+            const double lx = kn < nenc ? a.tp[kn] : 0.0;
+            mv_encode(a, st, rc, (uint32_t)(vc >> 32), a.pkt_base + (kc & ((1ull << kSsPktBits) - 1)), row, lc);
+            if ((kx >> kSsPktBits) != cell) break;
+            k = kn; kc = kx; vc = vx; rc = rx; lc = lx;
+        }
+        a.values[cell] = st.val;
+        a.keys[cell] = st.key;
+    }
+    // long chains of this wave's cells, one after another, by the whole wave
+    uint64_t lm = __ballot(valid && len > kSsLongChain);
+    while (lm) {  // wave-uniform
+        const int jl = __ffsll((unsigned long long)lm) - 1;
+        lm &= lm - 1;
+        const uint32_t hj = rl32(hi, jl), nj = rl32(len, jl);
+        const uint32_t k0 = a.heads[hj];
+        const uint64_t cell = a.skey[k0] >> kSsPktBits;
+        const uint32_t row = (uint32_t)(cell / a.g.w);
+        MvState st{a.values[cell], a.keys[cell], 0xFFFFFFFFu, 0.0, 0.0};
+        for (uint32_t w0 = 0; w0 < nj; w0 += 64) {
+            const uint32_t k = k0 + w0 + lane;
+            const bool in = w0 + lane < nj;
+            uint64_t kx = 0, vx = 0;
             int64_t rx = 0;
-            uint64_t vx = 0;
             double lx = 0.0;
-            if (lane < len) { rx = a.rep[k]; vx = a.sval[k]; lx = a.tp[k]; }
-            uint64_t sm = __ballot(lane < len && rx > 0);
+            if (in) { kx = a.skey[k]; rx = a.rep[k]; vx = a.sval[k]; lx = a.tp[k]; }
+            uint64_t sm = __ballot(in && rx > 0);
             while (sm) {
                 const int j = __ffsll((unsigned long long)sm) - 1;
                 sm &= sm - 1;
-                int64_t vv = (int64_t)rl64((uint64_t)rx, j);
-                const uint32_t f = rl32((uint32_t)(vx >> 32), j);
-                const uint64_t pkt = a.pkt_base + (rl64(kx, j) & ((1ull << kSsPktBits) - 1));
-                const double lc = __longlong_as_double((long long)rl64((uint64_t)__double_as_longlong(lx), j));
-                uint32_t draw = 1;
-                while (vv > 0) {                                                    // :207-233
-                    if (val == 0 || key == f) {  // every remaining iteration increments (:211-220)
-                        if (val == 0) key = f;
-                        val = (uint32_t)((uint64_t)val + (uint64_t)vv);
-                        break;
-                    }
-                    if (val != mval) {
-                        mval = val;
-                        mppp = go_pow_int(a.g.b, -(double)val);                         // :222
-                        ml1m = (mppp > 0 && mppp < 1) ? gm_log1m(mppp) : 0.0;
-                    }
-                    const double ppp = mppp;
-                    if (!(ppp > 0)) break;  // underflow: no later iteration can decrement
-                    if (ppp >= 1) {         // b <= 1: every iteration decrements
-                        const int64_t dec = (int64_t)val < vv ? (int64_t)val : vv;
-                        val -= (uint32_t)dec;
-                        vv -= dec;
-                        continue;
-                    }
-                    // declared generator: failed iterations before the next decrement
-                    // (:223-227) as one geometric waiting time; the first draw's log came from S5b
-                    const double lu = draw == 1 ? lc : gm_log(1.0 - ss_uniform(a.g.rng_seed, pkt, row, draw));
-                    draw++;
-                    const double q = lu / ml1m;
-                    if (!(q < (double)vv)) break;
-                    vv -= (int64_t)floor(q) + 1;
-                    val -= 1;
-                }
+                const double lcj = __longlong_as_double((long long)rl64((uint64_t)__double_as_longlong(lx), j));
+                mv_encode(a, st, (int64_t)rl64((uint64_t)rx, j), rl32((uint32_t)(vx >> 32), j),
+                          a.pkt_base + (rl64(kx, j) & ((1ull << kSsPktBits) - 1)), row, lcj);
             }
-            if (len < 64) break;
         }
-        if (lane == 0) { a.values[cell] = val; a.keys[cell] = key; }
+        if (lane == 0) { a.values[cell] = st.val; a.keys[cell] = st.key; }
     }
 }
 #pragma clang fp contract(on)
@@ -691,6 +727,7 @@ struct SpArgs {
     uint64_t *skey, *sval;   // encodes out: cell << 27 | packet, GNS_ID_NONE << 32 | reg | lz << 8 | old << 16
     uint32_t *scount;        // encodes written (device count)
     uint32_t *heads;         // [cells]: cell starts in skey, count at [cells]
+    uint32_t *hlen;          // [cells]: encodes of the cell of heads[i]
     uint32_t *work;          // bin counter of the persistent grid
     const uint32_t *order;   // [nb] bins, largest first (k_sp_order)
     unsigned long long *err; // a cell with more encodes than LDS holds (cannot happen below 8192)
@@ -887,6 +924,7 @@ __device__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, uint32_t n, u
     uint32_t cbits = 0;
     while ((1u << cbits) < a.s.cpb) cbits++;
     uint64_t *es = sp_sort(L, out, ns, 24, 24 + kSsPktBits + cbits);
+    uint64_t *tbl = es == L.a ? L.b : L.a;  // [cpb] per cell: head index << 32 | start in es
     if (tid == 0) L.gbase = atomicAdd(a.scount, ns);
     __syncthreads();
     const uint32_t gb = L.gbase;
@@ -907,7 +945,20 @@ __device__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, uint32_t n, u
             uint32_t hb = 0;
             if ((int)lane == leader) hb = atomicAdd(&a.heads[a.s.cells], (uint32_t)__popcll(hm));
             hb = __shfl(hb, leader);
-            if (head) a.heads[hb + __popcll(hm & ((1ull << lane) - 1ull))] = gb + i;
+            if (head) {
+                const uint32_t h = hb + __popcll(hm & ((1ull << lane) - 1ull));
+                a.heads[h] = gb + i;
+                tbl[(uint32_t)(es[i] >> (24 + kSsPktBits))] = (uint64_t)h << 32 | i;  // cell -> (head, start)
+            }
+        }
+    }
+    __syncthreads();
+    // chain lengths (S5c walks long chains with the whole wave): the last encode of each cell
+    for (uint32_t i = tid; i < ns; i += kSpThreads) {
+        const uint32_t c = (uint32_t)(es[i] >> (24 + kSsPktBits));
+        if (i + 1 == ns || (uint32_t)(es[i + 1] >> (24 + kSsPktBits)) != c) {
+            const uint64_t t = tbl[c];
+            a.hlen[t >> 32] = i + 1 - (uint32_t)t;
         }
     }
     __syncthreads();
@@ -958,7 +1009,9 @@ __device__ void sp_giant(const SpArgs &a, SpLds &L, const uint64_t *w2, uint32_t
     uint64_t *es = sp_sort(L, L.b, ns, 24, 24 + kSsPktBits);
     if (tid == 0) {
         L.gbase = atomicAdd(a.scount, ns);
-        a.heads[atomicAdd(&a.heads[a.s.cells], 1u)] = L.gbase;
+        const uint32_t h = atomicAdd(&a.heads[a.s.cells], 1u);
+        a.heads[h] = L.gbase;
+        a.hlen[h] = ns;
     }
     __syncthreads();
     const uint32_t gb = L.gbase;
@@ -1154,6 +1207,7 @@ struct gns_ss {
     uint64_t *sval = nullptr;
     uint32_t *counts = nullptr;  // [0] candidates, [1] encodes, [2] P4 bin counter, [3] candidates (P2)
     uint32_t *heads = nullptr;   // [cells + 1]: S5 segment starts (unordered), then their count
+    uint32_t *hlen = nullptr;    // [cells]: encodes per segment
     uint32_t *cblk = nullptr;
     SpGeom sp{};
     uint32_t ncu = 0;
@@ -1181,7 +1235,7 @@ void ss_free_all(gns_ss *ss) {
     dfree(ss->pcnt[0]); dfree(ss->pcnt[1]);
     dfree(ss->ptotal); dfree(ss->ckey); dfree(ss->ckey_s); dfree(ss->skey); dfree(ss->skey_s);
     dfree(ss->cval); dfree(ss->sval); dfree(ss->shist); dfree(ss->spart); dfree(ss->sorder);
-    dfree(ss->counts); dfree(ss->heads); dfree(ss->cblk); dfree(ss->stats); dfree(ss->stage);
+    dfree(ss->counts); dfree(ss->heads); dfree(ss->hlen); dfree(ss->cblk); dfree(ss->stats); dfree(ss->stage);
     dfree(ss->dctl); dfree(ss->stats_bak); ss->dsc.free_all();
     if (ss->h_pin) (void)hipHostFree(ss->h_pin);
     ss->timer.destroy();
@@ -1315,7 +1369,7 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         SpArgs pa{};
         pa.s = sg; pa.words = ss->ckey_s; pa.words2 = ss->skey_s; pa.bstart = tot; pa.total = ss->counts + 3;
         pa.regs = ss->regs; pa.skey = ss->skey; pa.sval = ss->sval; pa.scount = ss->counts + 1;
-        pa.heads = ss->heads; pa.work = ss->counts + 2; pa.err = ss->stats + 6;
+        pa.heads = ss->heads; pa.hlen = ss->hlen; pa.work = ss->counts + 2; pa.err = ss->stats + 6;
         pa.maxg = ss->sp_maxg;
         pa.order = ss->sorder;
         hipLaunchKernelGGL(k_sp_order, dim3(1), dim3(1024), 0, s, tot, ss->counts + 3, sg.nb, ss->sorder);
@@ -1327,13 +1381,13 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         ScopedStage st(ss->timer, 3);
         // the candidate buffers are free now: pbits-before and repeat counts go there
         SsApplyArgs a{ss->skey, ss->sval, ss->counts + 1, ss->g, ss->pkt, ss->regs, ss->pbits, ss->values, ss->keys,
-                      reinterpret_cast<double *>(ss->ckey), reinterpret_cast<int64_t *>(ss->skey_s), ss->heads, cells};
+                      reinterpret_cast<double *>(ss->ckey), reinterpret_cast<int64_t *>(ss->skey_s), ss->heads,
+                      ss->hlen, cells};
         const uint32_t hgrid = (cells + 255) / 256;  // one lane per touched cell at most
         const uint32_t egrid = (uint32_t)std::min<uint64_t>((ss->ccap + 255) / 256, 4096);
         hipLaunchKernelGGL(k_ss_walk_pbits, dim3(hgrid), dim3(256), 0, s, a);
         hipLaunchKernelGGL(k_ss_sample, dim3(egrid), dim3(256), 0, s, a);
-        const uint32_t wgrid = std::min<uint32_t>((cells + 3) / 4, 16384);  // one wave per touched cell
-        hipLaunchKernelGGL(k_ss_walk_mv, dim3(wgrid), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_ss_walk_mv, dim3(hgrid), dim3(256), 0, s, a);
         GNS_HIP(hipGetLastError());
     }
     ss->pkt += n;  // every record advances the RNG packet index
@@ -1549,11 +1603,15 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
         g.hll_master = p->hll_master;
         g.rng_seed = p->rng_seed;
         if ((uint64_t)g.d * g.w * g.m > (1ull << 36)) { set_error("d*w*m too large"); rc = GNS_E_ARG; break; }
-        {   // P1-P4 bins: cpb (a power of two) consecutive cells, about 512 bins
+        {   // P1-P4 bins: cpb (a power of two) consecutive cells, about 2048 bins, so a
+            // steady batch's bins fit P4's LDS whole (GNS_SS_BINS: A/B of the target)
             SpGeom &sg = ss->sp;
             const uint64_t cells = (uint64_t)g.d * g.w;
+            const char *benv = getenv("GNS_SS_BINS");
+            const long tb = benv ? strtol(benv, nullptr, 10) : 2048;
+            const uint64_t target = (tb >= 64 && tb <= (long)kSpMaxBins) ? (uint64_t)tb : 2048;
             sg.cpb = 1; sg.cpb_bits = 0;
-            while ((uint64_t)sg.cpb * 512 < cells && sg.cpb < kSpMaxCpb) { sg.cpb <<= 1; sg.cpb_bits++; }
+            while ((uint64_t)sg.cpb * target < cells && sg.cpb < kSpMaxCpb) { sg.cpb <<= 1; sg.cpb_bits++; }
             const uint64_t nb = (cells + sg.cpb - 1) / sg.cpb;
             if (nb > kSpMaxBins) {
                 set_error("SuperSpread: depth * width <= %u cells", kSpMaxBins * kSpMaxCpb);
@@ -1582,7 +1640,7 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
         const uint64_t cells = (uint64_t)g.d * g.w;
         if ((rc = dalloc_t(&ss->regs, cells * g.m)) || (rc = dalloc_t(&ss->pbits, cells)) ||
             (rc = dalloc_t(&ss->values, cells)) || (rc = dalloc_t(&ss->keys, cells)) ||
-            (rc = dalloc_t(&ss->heads, cells + 1)))
+            (rc = dalloc_t(&ss->heads, cells + 1)) || (rc = dalloc_t(&ss->hlen, cells)))
             break;
         uint64_t slots = 1;
         const uint64_t mf = p->max_flows ? p->max_flows : (4ull << 20);
