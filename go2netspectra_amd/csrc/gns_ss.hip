@@ -54,7 +54,6 @@ struct SsExtractArgs {
     KeyPlanN kpf, kpm;
     SsGeom g;
     const uint8_t *regs;
-    const uint8_t *rsnap;  // batch-entry registers as nibbles, min(reg, 15) (k_ss_snap)
     uint64_t *ckey;     // candidates: (cell*m + reg) << 27 | packet, block regions of chunk*d
     uint32_t *cval;     // lz
     uint32_t *ccount;   // total candidates
@@ -108,29 +107,6 @@ __device__ __forceinline__ int ss_keys(const SsExtractArgs &a, const uint8_t *s_
     }
 }
 
-// Register snapshot for S1's test: min(reg, 15) as a nibble, so the 2 x 4 MB of
-// registers the default task tests at random become 4 MB that an XCD's L2 holds.
-// A register at 15 or more reads as 15, so the test lets a few more candidates
-// through (lz > 15, probability 2^-15 per row); P4 tests them against the full
-// register and drops them.
-__device__ __forceinline__ uint32_t snap_reg(const uint8_t *rs, uint64_t seg) {
-    const uint32_t b = rs[seg >> 1];
-    return (seg & 1) ? b >> 4 : b & 15u;
-}
-__global__ __launch_bounds__(256) void k_ss_snap(const uint8_t *regs, uint64_t nregs, uint8_t *rsnap) {
-    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // 16 registers per thread
-    if (t * 16 >= nregs) return;
-    const uint4 v = reinterpret_cast<const uint4 *>(regs)[t];
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint32_t o[2] = {0, 0};
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        const uint32_t r = min((w[i >> 2] >> (8 * (i & 3))) & 0xFFu, 15u);
-        o[i >> 3] |= r << (4 * (i & 7));
-    }
-    reinterpret_cast<uint2 *>(rsnap)[t] = make_uint2(o[0], o[1]);
-}
-
 // S1: keys, flow id, per-row HLL encode test against the batch-entry registers
 // KF/KM: flow / merged key bytes when known at compile time (16/32 for the
 // default task SrcIP / SrcIP|DstIP), 0 = runtime.
@@ -172,7 +148,7 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
             const uint32_t h1 = mm3_chain<kSsNW>(mkm, Km, s1);
             const uint32_t idx = mpow2 ? (h1 & mmask) : h1 % a.g.m;  // :87-88
             const uint64_t seg = cell * a.g.m + idx;
-            const bool want = lz > snap_reg(a.rsnap, seg);  // can encode only if above the batch-entry register
+            const bool want = lz > a.regs[seg];  // can encode only if above the batch-entry register
             const uint32_t q = wave_alloc(&s_cc, want);
             if (want) {
                 rkey[q] = seg << kSsPktBits | (p & ((1ull << kSsPktBits) - 1));
@@ -266,7 +242,7 @@ __global__ __launch_bounds__(kSsThreads, GNS_SS_MINW) void k_ss_extract_hdr(SsEx
             const uint32_t h1 = mm3_chain<kSsNW>(mkm, KM, s1);
             const uint32_t idx = mpow2 ? (h1 & mmask) : h1 % a.g.m;  // :87-88
             segq[rr] = cell * a.g.m + idx;
-            regq[rr] = okq ? snap_reg(a.rsnap, segq[rr]) : 0xFFu;
+            regq[rr] = okq ? (uint32_t)a.regs[segq[rr]] : 0xFFu;
         }
     };
     load_hdr(beg + tid);
@@ -1017,7 +993,6 @@ __device__ void sp_giant(const SpArgs &a, SpLds &L, const uint64_t *w2, uint32_t
         const uint32_t pk = (uint32_t)(x >> 8) & ((1u << kSsPktBits) - 1u);
         if (S[reg * kSpV + lz] != pk) return;
         const uint32_t entry = a.regs[(cellg * m) + reg];
-        if (lz <= entry) return;  // let through by S1's register snapshot (a register >= 15)
         uint32_t old = entry;
         for (int v = (int)lz - 1; v > (int)entry; v--)
             if (S[reg * kSpV + v] < pk) { old = (uint32_t)v; break; }
@@ -1202,7 +1177,6 @@ struct gns_ss {
     KeyPlanN kpf{}, kpm{};
     uint32_t thr = 0;
     uint8_t *regs = nullptr;
-    uint8_t *rsnap = nullptr;    // S1's nibble snapshot of regs
     double *pbits = nullptr;
     uint32_t *values = nullptr, *keys = nullptr;
     DictDev D{};
@@ -1257,7 +1231,7 @@ int ss_set_dev(gns_ss *ss) {
 }
 
 void ss_free_all(gns_ss *ss) {
-    dfree(ss->regs); dfree(ss->rsnap); dfree(ss->pbits); dfree(ss->values); dfree(ss->keys); dfree(ss->D.rec);
+    dfree(ss->regs); dfree(ss->pbits); dfree(ss->values); dfree(ss->keys); dfree(ss->D.rec);
     dfree(ss->pcnt[0]); dfree(ss->pcnt[1]);
     dfree(ss->ptotal); dfree(ss->ckey); dfree(ss->ckey_s); dfree(ss->skey); dfree(ss->skey_s);
     dfree(ss->cval); dfree(ss->sval); dfree(ss->shist); dfree(ss->spart); dfree(ss->sorder);
@@ -1355,11 +1329,6 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     const uint32_t cells = ss->g.d * ss->g.w;
     const SpGeom &sg = ss->sp;
     ScopedStage total_stage(ss->timer, 5);
-    {
-        const uint64_t nregs = (uint64_t)cells * ss->g.m;
-        hipLaunchKernelGGL(k_ss_snap, dim3((unsigned)((nregs + 16 * 256 - 1) / (16 * 256))), dim3(256), 0, s, ss->regs,
-                           nregs, ss->rsnap);
-    }
     GNS_HIP(hipMemsetAsync(ss->ptotal, 0, 8, s));
     GNS_HIP(hipMemsetAsync(ss->counts, 0, 16, s));     // [0] candidates, [1] encodes, [2] P4 bin counter
     GNS_HIP(hipMemsetAsync(ss->heads + cells, 0, 4, s));
@@ -1367,7 +1336,7 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     if (++ss->epoch == 0) ss->epoch = 1;
     SsExtractArgs x{};
     x.in = in; x.n = n; x.kpf = ss->kpf; x.kpm = ss->kpm;
-    x.g = ss->g; x.regs = ss->regs; x.rsnap = ss->rsnap;
+    x.g = ss->g; x.regs = ss->regs;
     x.ckey = ss->ckey; x.cval = ss->cval; x.ccount = ss->counts; x.cblk = ss->cblk; x.stats = ss->stats;
     {
         ScopedStage st(ss->timer, 0);
@@ -1669,7 +1638,7 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
         }
         ss->timer.stream = ss->stream;
         const uint64_t cells = (uint64_t)g.d * g.w;
-        if ((rc = dalloc_t(&ss->regs, cells * g.m)) || (rc = dalloc_t(&ss->rsnap, (cells * g.m + 1) / 2)) || (rc = dalloc_t(&ss->pbits, cells)) ||
+        if ((rc = dalloc_t(&ss->regs, cells * g.m)) || (rc = dalloc_t(&ss->pbits, cells)) ||
             (rc = dalloc_t(&ss->values, cells)) || (rc = dalloc_t(&ss->keys, cells)) ||
             (rc = dalloc_t(&ss->heads, cells + 1)) || (rc = dalloc_t(&ss->hlen, cells)))
             break;
