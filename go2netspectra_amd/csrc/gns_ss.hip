@@ -767,6 +767,17 @@ __device__ __forceinline__ void sp_for8(const uint64_t *src, uint32_t n, F f) {
     }
 }
 
+// Prefix over the kSpWaves per-wave values in ws[] (after a barrier): this wave's
+// exclusive start and the total, from one LDS load and one DPP scan (a loop over
+// the earlier waves waited one LDS round trip per wave, in every radix pass).
+__device__ __forceinline__ uint32_t sp_wave_prefix(const uint32_t *ws, uint32_t *total = nullptr) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t x = lane < kSpWaves ? ws[lane] : 0u;
+    const uint32_t inc = wave_incl_scan(x);
+    if (total) *total = __shfl(inc, 63);
+    return __shfl(inc - x, (int)wave);
+}
+
 // Exclusive scan of one value per thread over the workgroup; returns this
 // thread's start.  Uses L.wsum; synchronises.
 __device__ __forceinline__ uint32_t sp_block_excl(SpLds &L, uint32_t v) {
@@ -775,8 +786,7 @@ __device__ __forceinline__ uint32_t sp_block_excl(SpLds &L, uint32_t v) {
     __syncthreads();  // earlier readers of wsum are done
     if (lane == 63) L.wsum[wave] = inc;
     __syncthreads();
-    uint32_t run = inc - v;
-    for (uint32_t w = 0; w < wave; w++) run += L.wsum[w];
+    const uint32_t run = inc - v + sp_wave_prefix(L.wsum);
     __syncthreads();
     return run;
 }
@@ -815,8 +825,7 @@ __device__ uint64_t *sp_sort(SpLds &L, uint64_t *src, uint32_t n, uint32_t lo, u
         const uint32_t inc = wave_incl_scan(sum);
         if (lane == 63) L.wsum[wave] = inc;
         __syncthreads();
-        uint32_t run = inc - sum;
-        for (uint32_t w = 0; w < wave; w++) run += L.wsum[w];
+        uint32_t run = inc - sum + sp_wave_prefix(L.wsum);
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) {
             const uint32_t i = tid * 4 + q;
@@ -874,12 +883,21 @@ __device__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, uint32_t n, u
     // carry into this thread = inclusive value of the previous lane, preceded by the earlier waves
     uint32_t ps = __shfl_up(cs, 1), pm = __shfl_up(cm, 1), pf = __shfl_up(cf, 1), ph = __shfl_up(ch, 1);
     if (lane == 0) ph = 0;
-    uint32_t ws = 0xFFFFFFFFu, wm = 0, wh = 0;  // waves before this one: last seg and its running max
-    for (uint32_t w = 0; w < wave; w++) {
-        const uint32_t rs = L.agg_seg[w], rm = L.agg_mx[w], rf = L.agg_fl[w] & 1u, rh = L.agg_fl[w] >> 1;
-        if (!rh) continue;
-        if (wh && rf && rs == ws) wm = max(wm, rm);
-        else { ws = rs; wm = rm; wh = 1; }
+    // waves before this one (their last seg and its running max): the same segmented
+    // scan over the wave aggregates, lane w holding wave w's, then lane wave - 1's value
+    uint32_t ws, wm, wh;
+    {
+        uint32_t as = 0xFFFFFFFFu, am = 0, af = 1, ah = 0;
+        if (lane < kSpWaves) { as = L.agg_seg[lane]; am = L.agg_mx[lane]; af = L.agg_fl[lane] & 1u; ah = L.agg_fl[lane] >> 1; }
+        for (uint32_t o = 1; o < kSpWaves; o <<= 1) {
+            const uint32_t ls = __shfl_up(as, o), lm = __shfl_up(am, o), lf = __shfl_up(af, o), lh = __shfl_up(ah, o);
+            if (lane >= o && lh) {
+                if (!ah) { as = ls; am = lm; af = lf; ah = 1; }
+                else if (af && as == ls) { am = max(am, lm); af = lf; }
+            }
+        }
+        const int src = wave > 0 ? (int)wave - 1 : 0;
+        ws = __shfl(as, src); wm = __shfl(am, src); wh = wave > 0 ? __shfl(ah, src) : 0u;
     }
     uint32_t carry_seg = 0xFFFFFFFFu, carry_mx = 0;
     if (ph) {
@@ -914,8 +932,8 @@ __device__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, uint32_t n, u
     const uint32_t inc = wave_incl_scan(succ);
     if (lane == 63) L.wsum[wave] = inc;
     __syncthreads();
-    uint32_t q = inc - succ, ns = 0;
-    for (uint32_t w = 0; w < kSpWaves; w++) { if (w < wave) q += L.wsum[w]; ns += L.wsum[w]; }
+    uint32_t ns = 0;
+    uint32_t q = inc - succ + sp_wave_prefix(L.wsum, &ns);
 #pragma unroll
     for (uint32_t j = 0; j < kSpPer; j++)
         if (item[j] != ~0ull) out[q++] = item[j];
@@ -1603,13 +1621,14 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
         g.hll_master = p->hll_master;
         g.rng_seed = p->rng_seed;
         if ((uint64_t)g.d * g.w * g.m > (1ull << 36)) { set_error("d*w*m too large"); rc = GNS_E_ARG; break; }
-        {   // P1-P4 bins: cpb (a power of two) consecutive cells, about 2048 bins, so a
-            // steady batch's bins fit P4's LDS whole (GNS_SS_BINS: A/B of the target)
+        {   // P1-P4 bins: cpb (a power of two) consecutive cells, about 512 bins (P4's
+            // fixed cost per bin outweighs fitting more bins in LDS whole: 512 / 1024 /
+            // 2048 bins measured 0.54 / 0.70 / 1.01 ms per 100M; GNS_SS_BINS for A/B)
             SpGeom &sg = ss->sp;
             const uint64_t cells = (uint64_t)g.d * g.w;
             const char *benv = getenv("GNS_SS_BINS");
-            const long tb = benv ? strtol(benv, nullptr, 10) : 2048;
-            const uint64_t target = (tb >= 64 && tb <= (long)kSpMaxBins) ? (uint64_t)tb : 2048;
+            const long tb = benv ? strtol(benv, nullptr, 10) : 512;
+            const uint64_t target = (tb >= 64 && tb <= (long)kSpMaxBins) ? (uint64_t)tb : 512;
             sg.cpb = 1; sg.cpb_bits = 0;
             while ((uint64_t)sg.cpb * target < cells && sg.cpb < kSpMaxCpb) { sg.cpb <<= 1; sg.cpb_bits++; }
             const uint64_t nb = (cells + sg.cpb - 1) / sg.cpb;
