@@ -1230,6 +1230,7 @@ struct gns_ss {
     SpGeom sp{};
     uint32_t ncu = 0;
     uint32_t sp_maxg = 0;        // P4 groups per window of a large bin
+    bool debug = false;          // GNS_SS_DEBUG
     uint32_t *shist = nullptr;   // [nblk][nb] per-block bin histogram -> offsets
     uint32_t *spart = nullptr;   // [ngrp][nb] group partials, then [nb] bin starts
     uint32_t *sorder = nullptr;  // [nb] P4 schedule
@@ -1382,6 +1383,19 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         hipLaunchKernelGGL(k_tscan_mid, dim3((sg.nb + 255) / 256), dim3(256), 0, s, ss->spart, ngrp, sg.nb, tot);
         hipLaunchKernelGGL(k_tscan_bins, dim3(1), dim3(1024), 0, s, tot, sg.nb, ss->counts + 3);
         hipLaunchKernelGGL(k_tscan_down, g2, dim3(256), 0, s, ss->shist, nblk, sg.nb, ss->spart, tot);
+        if (ss->debug) {  // GNS_SS_DEBUG: the batch's bin sizes on stderr (synchronises; diagnosis only)
+            std::vector<uint32_t> h(sg.nb + 1);
+            GNS_HIP(hipMemcpyAsync(h.data(), tot, sg.nb * 4, hipMemcpyDeviceToHost, s));
+            GNS_HIP(hipMemcpyAsync(h.data() + sg.nb, ss->counts + 3, 4, hipMemcpyDeviceToHost, s));
+            GNS_HIP(hipStreamSynchronize(s));
+            std::vector<uint32_t> sz(sg.nb);
+            uint32_t big = 0;
+            for (uint32_t b = 0; b < sg.nb; b++) { sz[b] = h[b + 1] - h[b]; big += sz[b] > kSpCap; }
+            std::sort(sz.begin(), sz.end());
+            fprintf(stderr, "gns_ss batch %llu: %u candidates, %u bins, %u above %u; largest %u %u %u, median %u\n",
+                    (unsigned long long)ss->n_batches, h[sg.nb], sg.nb, big, kSpCap, sz[sg.nb - 1],
+                    sg.nb > 1 ? sz[sg.nb - 2] : 0u, sg.nb > 2 ? sz[sg.nb - 3] : 0u, sz[sg.nb / 2]);
+        }
         hipLaunchKernelGGL(k_sp_scatter, dim3(nblk), dim3(256), 0, s, ss->ckey, ss->cval, ss->cblk, ss->g.d, sg,
                            ss->shist, ss->ckey_s);
         SpArgs pa{};
@@ -1648,6 +1662,7 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
                 hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
                 ncu = 256;
             ss->ncu = (uint32_t)ncu;
+            ss->debug = getenv("GNS_SS_DEBUG") != nullptr;
             const char *env = getenv("GNS_SS_SPG");  // tests: small windows exercise the window loop
             const long v = env ? strtol(env, nullptr, 10) : 0;
             ss->sp_maxg = (v >= 2 && v <= (long)kSpMaxG) ? (uint32_t)(v & ~1L) : kSpMaxG;
