@@ -608,9 +608,9 @@ __global__ __launch_bounds__(256) void k_ss_ids_to_bytes(const uint32_t *ids, ui
 // Every launch is sized from host-known bounds; counts stay on the device.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSpCap = 8192;        // items a P4 workgroup holds in LDS
-constexpr uint32_t kSpThreads = 1024;
+constexpr uint32_t kSpThreads = 512;     // 8 waves, 16 items per thread (1024 threads spilled at 128 VGPRs)
 constexpr uint32_t kSpWaves = kSpThreads / 64;
-constexpr uint32_t kSpPer = kSpCap / kSpThreads;   // 8 items per thread
+constexpr uint32_t kSpPer = kSpCap / kSpThreads;   // 16 items per thread
 constexpr uint32_t kSpSub = 4096;        // P3 candidates staged per sub-pass
 constexpr uint32_t kSpMaxBins = 4096;
 constexpr uint32_t kSpMaxCpb = 8192;     // cells per bin (P4's cell histogram)
@@ -796,7 +796,7 @@ __device__ __forceinline__ uint32_t sp_block_excl(SpLds &L, uint32_t v) {
 // idx % 64 of wave idx / 512 (slot (idx / 64) % 8): a wave owns 512 consecutive
 // items, so returning LDS adds (same-address lanes served in lane order, the
 // Count-Min K3 property, measured on gfx950: tools/lds_order.hip) give stable ranks.
-__device__ uint64_t *sp_sort(SpLds &L, uint64_t *src, uint32_t n, uint32_t lo, uint32_t hi) {
+__device__ __forceinline__ uint64_t *sp_sort(SpLds &L, uint64_t *src, uint32_t n, uint32_t lo, uint32_t hi) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     uint64_t *dst = src == L.a ? L.b : L.a;
     for (uint32_t sh = lo; sh < hi; sh += 8) {
@@ -848,7 +848,7 @@ __device__ uint64_t *sp_sort(SpLds &L, uint64_t *src, uint32_t n, uint32_t lo, u
 // (local seg, packet), segmented running max of lz per register, encode test
 // against the batch-entry register, encodes sorted by (cell, packet), written
 // out with their cell heads.  bin0seg = first seg of the bin.
-__device__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, uint32_t n, uint64_t bin0seg, uint64_t bin0cell) {
+__device__ __noinline__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, uint32_t n, uint64_t bin0seg, uint64_t bin0cell) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     uint64_t *srt = sp_sort(L, src, n, 8, 35 + a.s.lbits);
     uint64_t *out = srt == L.a ? L.b : L.a;
@@ -987,7 +987,7 @@ __device__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, uint32_t n, u
 // S[reg][v] = earliest packet with an lz >= v.  A candidate (reg, p, lz) encodes iff
 // S[reg][lz] == p; the register value it sees is the largest v < lz with
 // S[reg][v] < p, or the batch-entry register.
-__device__ void sp_giant(const SpArgs &a, SpLds &L, const uint64_t *w2, uint32_t n, uint64_t bin0seg, uint64_t cellg,
+__device__ __noinline__ void sp_giant(const SpArgs &a, SpLds &L, const uint64_t *w2, uint32_t n, uint64_t bin0seg, uint64_t cellg,
                          uint32_t cl_in_bin) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t m = a.s.m;
@@ -1116,7 +1116,8 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
         // candidates are grouped into words2, then the groups run one by one.
         uint32_t *ccnt = reinterpret_cast<uint32_t *>(L.b);  // [cpb] candidates per cell
         uint32_t *cgid = ccnt + kSpMaxCpb;                   // [cpb] group of the cell
-        const uint32_t per = (a.s.cpb + kSpThreads - 1) / kSpThreads;  // <= 8 cells per thread
+        constexpr uint32_t kCpt = kSpMaxCpb / kSpThreads;                // cells per thread at most
+        const uint32_t per = (a.s.cpb + kSpThreads - 1) / kSpThreads;
         for (uint32_t cw = 0; cw < a.s.cpb;) {
             for (uint32_t c = tid; c < a.s.cpb; c += kSpThreads) ccnt[c] = 0;
             for (uint32_t g = tid; g < a.maxg; g += kSpThreads) { L.gtab[3 * g + 1] = 0; L.gtab[3 * g + 2] = 0xFFFFFFFFu; }
@@ -1127,16 +1128,16 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_bins(SpArgs a) {
                 if (c >= cw) atomicAdd(&ccnt[c], 1u);
             });
             __syncthreads();
-            uint32_t k[8], sum = 0;
+            uint32_t k[kCpt], sum = 0;
 #pragma unroll
-            for (uint32_t q = 0; q < 8; q++) {
+            for (uint32_t q = 0; q < kCpt; q++) {
                 const uint32_t c = tid * per + q;
                 k[q] = (q < per && c < a.s.cpb) ? ccnt[c] : 0u;
                 sum += k[q];
             }
             uint32_t run = sp_block_excl(L, sum);
 #pragma unroll
-            for (uint32_t q = 0; q < 8; q++) {
+            for (uint32_t q = 0; q < kCpt; q++) {
                 const uint32_t c = tid * per + q;
                 if (k[q]) {
                     const uint32_t slot = run / kSpHalf;
