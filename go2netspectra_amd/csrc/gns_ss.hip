@@ -732,6 +732,7 @@ struct SpArgs {
     const uint32_t *order;   // [nb] bins, largest first (k_sp_order)
     unsigned long long *err; // a cell with more encodes than LDS holds (cannot happen below 8192)
     uint32_t maxg;           // groups per window of a large bin (kSpMaxG; GNS_SS_SPG, tests only)
+    unsigned long long *prof;  // GNS_SS_DEBUG: P4 phase cycles (sp_group), else null
 };
 
 constexpr uint32_t kSpMaxG = 512;       // cell groups of a large bin per window
@@ -850,7 +851,17 @@ __device__ __forceinline__ uint64_t *sp_sort(SpLds &L, uint64_t *src, uint32_t n
 // out with their cell heads.  bin0seg = first seg of the bin.
 __device__ __noinline__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, uint32_t n, uint64_t bin0seg, uint64_t bin0cell) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    uint64_t tprev = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+    auto mark = [&](int i) {  // diagnosis only (GNS_SS_DEBUG)
+        if (a.prof && tid == 0) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            atomicAdd(&a.prof[i], (unsigned long long)(t - tprev));
+            tprev = t;
+        }
+    };
+    if (a.prof && tid == 0) atomicAdd(&a.prof[7], 1ull);
     uint64_t *srt = sp_sort(L, src, n, 8, 35 + a.s.lbits);
+    mark(0);
     uint64_t *out = srt == L.a ? L.b : L.a;
     // thread-major: thread t holds sorted positions [8t, 8t + 8)
     const uint32_t p0 = tid * kSpPer;
@@ -941,7 +952,9 @@ __device__ __noinline__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, 
     if (ns == 0) return;
     uint32_t cbits = 0;
     while ((1u << cbits) < a.s.cpb) cbits++;
+    mark(1);
     uint64_t *es = sp_sort(L, out, ns, 24, 24 + kSsPktBits + cbits);
+    mark(2);
     uint64_t *tbl = es == L.a ? L.b : L.a;  // [cpb] per cell: head index << 32 | start in es
     if (tid == 0) L.gbase = atomicAdd(a.scount, ns);
     __syncthreads();
@@ -971,6 +984,7 @@ __device__ __noinline__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, 
         }
     }
     __syncthreads();
+    mark(3);
     // chain lengths (S5c walks long chains with the whole wave): the last encode of each cell
     for (uint32_t i = tid; i < ns; i += kSpThreads) {
         const uint32_t c = (uint32_t)(es[i] >> (24 + kSsPktBits));
@@ -980,6 +994,7 @@ __device__ __noinline__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, 
         }
     }
     __syncthreads();
+    mark(4);
 }
 
 // One cell with more candidates than LDS holds: the order-free form.  For every
@@ -1232,6 +1247,7 @@ struct gns_ss {
     uint32_t ncu = 0;
     uint32_t sp_maxg = 0;        // P4 groups per window of a large bin
     bool debug = false;          // GNS_SS_DEBUG
+    unsigned long long *sprof = nullptr;  // [8] P4 phase ticks (debug)
     uint32_t *shist = nullptr;   // [nblk][nb] per-block bin histogram -> offsets
     uint32_t *spart = nullptr;   // [ngrp][nb] group partials, then [nb] bin starts
     uint32_t *sorder = nullptr;  // [nb] P4 schedule
@@ -1255,7 +1271,7 @@ void ss_free_all(gns_ss *ss) {
     dfree(ss->pcnt[0]); dfree(ss->pcnt[1]);
     dfree(ss->ptotal); dfree(ss->ckey); dfree(ss->ckey_s); dfree(ss->skey); dfree(ss->skey_s);
     dfree(ss->cval); dfree(ss->sval); dfree(ss->shist); dfree(ss->spart); dfree(ss->sorder);
-    dfree(ss->counts); dfree(ss->heads); dfree(ss->hlen); dfree(ss->cblk); dfree(ss->stats); dfree(ss->stage);
+    dfree(ss->counts); dfree(ss->heads); dfree(ss->hlen); dfree(ss->sprof); dfree(ss->cblk); dfree(ss->stats); dfree(ss->stage);
     dfree(ss->dctl); dfree(ss->stats_bak); ss->dsc.free_all();
     if (ss->h_pin) (void)hipHostFree(ss->h_pin);
     ss->timer.destroy();
@@ -1404,9 +1420,19 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         pa.regs = ss->regs; pa.skey = ss->skey; pa.sval = ss->sval; pa.scount = ss->counts + 1;
         pa.heads = ss->heads; pa.hlen = ss->hlen; pa.work = ss->counts + 2; pa.err = ss->stats + 6;
         pa.maxg = ss->sp_maxg;
+        pa.prof = ss->debug ? ss->sprof : nullptr;
+        if (ss->debug) GNS_HIP(hipMemsetAsync(ss->sprof, 0, 8 * 8, s));
         pa.order = ss->sorder;
         hipLaunchKernelGGL(k_sp_order, dim3(1), dim3(1024), 0, s, tot, ss->counts + 3, sg.nb, ss->sorder);
         hipLaunchKernelGGL(k_sp_bins, dim3(std::min(sg.nb, ss->ncu)), dim3(kSpThreads), sizeof(SpLds), s, pa);
+        if (ss->debug) {
+            unsigned long long h[8];
+            GNS_HIP(hipMemcpyAsync(h, ss->sprof, sizeof h, hipMemcpyDeviceToHost, s));
+            GNS_HIP(hipStreamSynchronize(s));
+            const double g = h[7] ? (double)h[7] : 1.0;
+            fprintf(stderr, "gns_ss P4: %llu groups; per group (memtime ticks) sort1 %.0f scan %.0f sort2 %.0f write %.0f tails %.0f\n",
+                    h[7], h[0] / g, h[1] / g, h[2] / g, h[3] / g, h[4] / g);
+        }
         GNS_HIP(hipGetLastError());
     }
     GNS_TRY((ss_encode_ids<KIND, MF, MM>(ss, in)));
@@ -1708,7 +1734,7 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
             (rc = dalloc_t(&ss->counts, 4)) || (rc = dalloc_t(&ss->cblk, 2ull * ss->nblk_max)) ||
             (rc = dalloc_t(&ss->shist, (uint64_t)ss->nblk_max * ss->sp.nb)) ||
             (rc = dalloc_t(&ss->spart, ((uint64_t)(ss->nblk_max + kTGrp - 1) / kTGrp + 1) * ss->sp.nb)) ||
-            (rc = dalloc_t(&ss->sorder, ss->sp.nb)) || (rc = dalloc_t(&ss->stats, 8)))
+            (rc = dalloc_t(&ss->sorder, ss->sp.nb)) || (rc = dalloc_t(&ss->sprof, 8)) || (rc = dalloc_t(&ss->stats, 8)))
             break;
         if (hipHostMalloc(reinterpret_cast<void **>(&ss->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
