@@ -800,6 +800,9 @@ __device__ __forceinline__ uint32_t sp_block_excl(SpLds &L, uint32_t v) {
 __device__ __forceinline__ uint64_t *sp_sort(SpLds &L, uint64_t *src, uint32_t n, uint32_t lo, uint32_t hi) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     uint64_t *dst = src == L.a ? L.b : L.a;
+    // items per lane for this n (block-uniform): a wave owns pt * 64 consecutive items,
+    // so a small sort runs pt (not kSpPer) item slots per lane in every pass
+    const uint32_t pt = (n + kSpThreads - 1) / kSpThreads;
     for (uint32_t sh = lo; sh < hi; sh += 8) {
         const uint32_t nd = min(8u, hi - sh), ndig = 1u << nd, dmask = ndig - 1u;
         for (uint32_t dg = lane; dg < ndig; dg += 64) L.cnt[dg * kSpWaves + wave] = 0;
@@ -807,7 +810,8 @@ __device__ __forceinline__ uint64_t *sp_sort(SpLds &L, uint64_t *src, uint32_t n
         uint32_t dg[kSpPer], rk[kSpPer];
 #pragma unroll
         for (uint32_t j = 0; j < kSpPer; j++) {
-            const uint32_t idx = wave * (kSpPer * 64) + j * 64 + lane;
+            if (j >= pt) continue;  // block-uniform
+            const uint32_t idx = wave * pt * 64 + j * 64 + lane;
             const bool v = idx < n;
             x[j] = v ? src[idx] : 0ull;
             dg[j] = (uint32_t)(x[j] >> sh) & dmask;
@@ -836,7 +840,8 @@ __device__ __forceinline__ uint64_t *sp_sort(SpLds &L, uint64_t *src, uint32_t n
         __syncthreads();
 #pragma unroll
         for (uint32_t j = 0; j < kSpPer; j++) {
-            const uint32_t idx = wave * (kSpPer * 64) + j * 64 + lane;
+            if (j >= pt) continue;  // block-uniform
+            const uint32_t idx = wave * pt * 64 + j * 64 + lane;
             if (idx < n) dst[L.cnt[dg[j] * kSpWaves + wave] + rk[j]] = x[j];
         }
         __syncthreads();
@@ -863,12 +868,14 @@ __device__ __noinline__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, 
     uint64_t *srt = sp_sort(L, src, n, 8, 35 + a.s.lbits);
     mark(0);
     uint64_t *out = srt == L.a ? L.b : L.a;
-    // thread-major: thread t holds sorted positions [8t, 8t + 8)
-    const uint32_t p0 = tid * kSpPer;
+    // thread-major: thread t holds sorted positions [pt * t, pt * t + pt)
+    const uint32_t pt = (n + kSpThreads - 1) / kSpThreads;
+    const uint32_t p0 = tid * pt;
     uint64_t x[kSpPer];
     uint32_t seg_last = 0xFFFFFFFFu, mx = 0, full = 1, have = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kSpPer; j++) {
+        if (j >= pt) continue;  // block-uniform
         x[j] = p0 + j < n ? srt[p0 + j] : ~0ull;
         if (p0 + j < n) {
             const uint32_t sg = (uint32_t)(x[j] >> 35), lz = (uint32_t)x[j] & 0xFFu;
@@ -924,6 +931,7 @@ __device__ __noinline__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, 
 #pragma unroll
     for (uint32_t j = 0; j < kSpPer; j++) {
         item[j] = ~0ull;
+        if (j >= pt) continue;  // block-uniform
         if (p0 + j < n) {
             const uint32_t sg = (uint32_t)(x[j] >> 35), lz = (uint32_t)x[j] & 0xFFu;
             const uint32_t pk = (uint32_t)(x[j] >> 8) & ((1u << kSsPktBits) - 1u);
@@ -946,8 +954,10 @@ __device__ __noinline__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, 
     uint32_t ns = 0;
     uint32_t q = inc - succ + sp_wave_prefix(L.wsum, &ns);
 #pragma unroll
-    for (uint32_t j = 0; j < kSpPer; j++)
+    for (uint32_t j = 0; j < kSpPer; j++) {
+        if (j >= pt) continue;  // block-uniform
         if (item[j] != ~0ull) out[q++] = item[j];
+    }
     __syncthreads();
     if (ns == 0) return;
     uint32_t cbits = 0;
