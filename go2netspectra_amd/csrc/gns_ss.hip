@@ -211,13 +211,14 @@ __global__ __launch_bounds__(kSsThreads, GNS_SS_MINW) void k_ss_extract_hdr(SsEx
         for (int i = 0; i < 4; i++) { cw[4 * i] = hv[i].x; cw[4 * i + 1] = hv[i].y; cw[4 * i + 2] = hv[i].z; cw[4 * i + 3] = hv[i].w; }
         const uint32_t szq = hsz;
         load_hdr(q + kSsThreads);
-        uint32_t kwf[GNS_KWMAX], kwm[kSsNW];
+        uint32_t kwf[GNS_KWMAX], kwm[kSsNW], tw[10];
 #pragma unroll
         for (int i = 0; i < GNS_KWMAX; i++) kwf[i] = 0;
 #pragma unroll
         for (int i = 0; i < kSsNW; i++) kwm[i] = 0;
+#pragma unroll
+        for (int i = 0; i < 10; i++) tw[i] = 0;
         if (okq) {
-            uint32_t tw[10];
             const int st = parse_record_fast(cw, szq, true, tw);
             if (st == PARSE_OK) {
                 make_key_m<MF, GNS_KWMAX>(KF, s_srcf, tw, kwf);
@@ -227,22 +228,44 @@ __global__ __launch_bounds__(kSsThreads, GNS_SS_MINW) void k_ss_extract_hdr(SsEx
                 okq = false;
             }
         }
-        uint32_t mkf[GNS_KWMAX], mkm[kSsNW];
-        mm3_premix<GNS_KWMAX>(kwf, KF, mkf);
-        mm3_premix<kSsNW>(kwm, KM, mkm);
+        auto rows = [&](const uint32_t (&mkf)[GNS_KWMAX], const uint32_t (&mkm)[kSsNW]) {
 #pragma unroll
-        for (int rr = 0; rr < DD; rr++) {
-            const uint32_t j = ss_row_index(a.g, mm3_chain<GNS_KWMAX>(mkf, KF, a.g.seeds[rr]));
-            const uint64_t cell = (uint64_t)rr * a.g.w + j;
-            uint32_t s0, s1;
-            ss_hll_seeds(a.g.hll_master, cell, s0, s1);
-            const uint32_t h0 = mm3_chain<kSsNW>(mkm, KM, s0);  // geometricHash :66-70
-            uint32_t lz = (h0 ? (uint32_t)__clz(h0) : 32u) + 1u;
-            lzq[rr] = lz > a.g.maxv ? a.g.maxv : lz;
-            const uint32_t h1 = mm3_chain<kSsNW>(mkm, KM, s1);
-            const uint32_t idx = mpow2 ? (h1 & mmask) : h1 % a.g.m;  // :87-88
-            segq[rr] = cell * a.g.m + idx;
-            regq[rr] = okq ? (uint32_t)a.regs[segq[rr]] : 0xFFu;
+            for (int rr = 0; rr < DD; rr++) {
+                const uint32_t j = ss_row_index(a.g, mm3_chain<GNS_KWMAX>(mkf, KF, a.g.seeds[rr]));
+                const uint64_t cell = (uint64_t)rr * a.g.w + j;
+                uint32_t s0, s1;
+                ss_hll_seeds(a.g.hll_master, cell, s0, s1);
+                const uint32_t h0 = mm3_chain<kSsNW>(mkm, KM, s0);  // geometricHash :66-70
+                uint32_t lz = (h0 ? (uint32_t)__clz(h0) : 32u) + 1u;
+                lzq[rr] = lz > a.g.maxv ? a.g.maxv : lz;
+                const uint32_t h1 = mm3_chain<kSsNW>(mkm, KM, s1);
+                const uint32_t idx = mpow2 ? (h1 & mmask) : h1 % a.g.m;  // :87-88
+                segq[rr] = cell * a.g.m + idx;
+                regq[rr] = okq ? (uint32_t)a.regs[segq[rr]] : 0xFFu;
+            }
+        };
+        uint32_t mkf[GNS_KWMAX], mkm[kSsNW];
+        // the default task's keys are the source / source and destination 16-byte
+        // address slots (PLAN_SLICE0): when every lane of the wave holds IPv4
+        // addresses, 12 of the 16 key words are zero, and with the zeros as
+        // constants their mixing and chain steps fold away (same hash values)
+        const bool wide = okq && (tw[1] | tw[2] | tw[3] | tw[5] | tw[6] | tw[7]) != 0;
+        if (MF == PLAN_SLICE0 && MM == PLAN_SLICE0 && KF == 16 && KM == 32 && __ballot(wide) == 0) {  // wave-uniform
+            uint32_t kf4[GNS_KWMAX], km4[kSsNW];
+#pragma unroll
+            for (int i = 0; i < GNS_KWMAX; i++) kf4[i] = 0;
+#pragma unroll
+            for (int i = 0; i < kSsNW; i++) km4[i] = 0;
+            kf4[0] = kwf[0];
+            km4[0] = kwm[0];
+            km4[4] = kwm[4];
+            mm3_premix<GNS_KWMAX>(kf4, KF, mkf);
+            mm3_premix<kSsNW>(km4, KM, mkm);
+            rows(mkf, mkm);
+        } else {
+            mm3_premix<GNS_KWMAX>(kwf, KF, mkf);
+            mm3_premix<kSsNW>(kwm, KM, mkm);
+            rows(mkf, mkm);
         }
     };
     load_hdr(beg + tid);
