@@ -411,6 +411,9 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 //     4.46 vs 4.02 here, 2.36 vs 2.22 at d=4; so did size sums as two 32-bit halves,
 //     3.86 vs 3.55 here and 3.28 vs 2.37 at d=4, tools/r03_gpu8.sh.  The plain loop
 //     at d=4 with five waves per SIMD (GNS_C2_PIPE=0 GNS_EX_MINW=5): 2.49 vs 2.37)
+#ifndef GNS_K1_V4HASH
+#define GNS_K1_V4HASH 1  // A/B: 0 hashes every wave's 5-tuple key generically
+#endif
 #ifndef GNS_C5_THREADS
 #define GNS_C5_THREADS 512
 #endif
@@ -494,8 +497,25 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
                 }
             }
             uint32_t mk[GNS_KWMAX];
-            mm3_premix<GNS_KWMAX>(kwq, K, mk);
-            slotq = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
+            // the 5-tuple key (PLAN_SLICE0, 37 bytes) of an IPv4 packet has six zero words
+            // (the address slots' upper 12 bytes): when the whole wave is IPv4 they are
+            // hashed as constants, which folds their mixing and chain steps (same slot)
+            bool v4w = false;
+            if constexpr (GNS_K1_V4HASH && MODE == PLAN_SLICE0 && KB == 37 && GNS_KWMAX >= 10) {
+                const bool wide = okq && (kwq[1] | kwq[2] | kwq[3] | kwq[5] | kwq[6] | kwq[7]) != 0;
+                v4w = __ballot(wide) == 0;  // wave-uniform
+            }
+            if (v4w) {
+                uint32_t k4[GNS_KWMAX];
+#pragma unroll
+                for (int i = 0; i < GNS_KWMAX; i++) k4[i] = 0;
+                k4[0] = kwq[0]; k4[4] = kwq[4]; k4[8] = kwq[8]; k4[9] = kwq[9];
+                mm3_premix<GNS_KWMAX>(k4, K, mk);
+                slotq = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
+            } else {
+                mm3_premix<GNS_KWMAX>(kwq, K, mk);
+                slotq = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
+            }
             if (okq) {
                 const uint4 *rq = reinterpret_cast<const uint4 *>(a.D.rec + (size_t)slotq * a.D.RW);
 #pragma unroll
