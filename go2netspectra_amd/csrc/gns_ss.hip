@@ -766,7 +766,7 @@ struct SpLds {
     uint32_t gtab[3 * kSpMaxG];    // groups of a window: start, count, first cell
     uint32_t gcur[kSpMaxG];
     uint32_t wsum[kSpWaves + 2];
-    uint32_t bin, n_succ, gbase, ngrp, cend;
+    uint32_t bin, n_succ, gbase, hbase, ngrp, cend;
     uint32_t agg_seg[kSpWaves], agg_mx[kSpWaves], agg_fl[kSpWaves];
 };
 
@@ -804,13 +804,13 @@ __device__ __forceinline__ uint32_t sp_wave_prefix(const uint32_t *ws, uint32_t 
 
 // Exclusive scan of one value per thread over the workgroup; returns this
 // thread's start.  Uses L.wsum; synchronises.
-__device__ __forceinline__ uint32_t sp_block_excl(SpLds &L, uint32_t v) {
+__device__ __forceinline__ uint32_t sp_block_excl(SpLds &L, uint32_t v, uint32_t *total = nullptr) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t inc = wave_incl_scan(v);
     __syncthreads();  // earlier readers of wsum are done
     if (lane == 63) L.wsum[wave] = inc;
     __syncthreads();
-    const uint32_t run = inc - v + sp_wave_prefix(L.wsum);
+    const uint32_t run = inc - v + sp_wave_prefix(L.wsum, total);
     __syncthreads();
     return run;
 }
@@ -987,33 +987,35 @@ __device__ __noinline__ void sp_group(const SpArgs &a, SpLds &L, uint64_t *src, 
     while ((1u << cbits) < a.s.cpb) cbits++;
     mark(1);
     uint64_t *es = sp_sort(L, out, ns, 24, 24 + kSsPktBits + cbits);
-    mark(2);
     uint64_t *tbl = es == L.a ? L.b : L.a;  // [cpb] per cell: head index << 32 | start in es
-    if (tid == 0) L.gbase = atomicAdd(a.scount, ns);
+    mark(2);
+    // the group's heads (first encode of each cell): counted per thread, then one global
+    // add for all their slots (an add per wave on the one counter every workgroup
+    // shares was most of P4's time)
+    auto is_head = [&](uint32_t i) {
+        return i == 0 || (uint32_t)(es[i - 1] >> (24 + kSsPktBits)) != (uint32_t)(es[i] >> (24 + kSsPktBits));
+    };
+    uint32_t nhd = 0;
+    for (uint32_t i = tid; i < ns; i += kSpThreads) nhd += is_head(i) ? 1u : 0u;
+    uint32_t htot = 0;
+    uint32_t hpos = sp_block_excl(L, nhd, &htot);
+    if (tid == 0) {
+        L.gbase = atomicAdd(a.scount, ns);
+        L.hbase = atomicAdd(&a.heads[a.s.cells], htot);
+    }
     __syncthreads();
     const uint32_t gb = L.gbase;
-    for (uint32_t i0 = 0; i0 < ns; i0 += kSpThreads) {  // block-uniform trip count
-        const uint32_t i = i0 + tid;
-        bool head = false;
-        if (i < ns) {
-            const uint64_t e = es[i];
-            const uint64_t ck = e >> 24;
-            const uint64_t cell = bin0cell + (ck >> kSsPktBits);
-            a.skey[gb + i] = cell << kSsPktBits | (ck & ((1ull << kSsPktBits) - 1));
-            a.sval[gb + i] = (uint64_t)GNS_ID_NONE << 32 | (e & 0xFFFFFFull);
-            head = i == 0 || (es[i - 1] >> (24 + kSsPktBits)) != (ck >> kSsPktBits);
-        }
-        const uint64_t hm = __ballot(head);
-        if (hm) {
-            const int leader = __ffsll((unsigned long long)hm) - 1;
-            uint32_t hb = 0;
-            if ((int)lane == leader) hb = atomicAdd(&a.heads[a.s.cells], (uint32_t)__popcll(hm));
-            hb = __shfl(hb, leader);
-            if (head) {
-                const uint32_t h = hb + __popcll(hm & ((1ull << lane) - 1ull));
-                a.heads[h] = gb + i;
-                tbl[(uint32_t)(es[i] >> (24 + kSsPktBits))] = (uint64_t)h << 32 | i;  // cell -> (head, start)
-            }
+    hpos += L.hbase;
+    for (uint32_t i = tid; i < ns; i += kSpThreads) {
+        const uint64_t e = es[i];
+        const uint64_t ck = e >> 24;
+        const uint64_t cell = bin0cell + (ck >> kSsPktBits);
+        a.skey[gb + i] = cell << kSsPktBits | (ck & ((1ull << kSsPktBits) - 1));
+        a.sval[gb + i] = (uint64_t)GNS_ID_NONE << 32 | (e & 0xFFFFFFull);
+        if (is_head(i)) {
+            a.heads[hpos] = gb + i;
+            tbl[(uint32_t)(ck >> kSsPktBits)] = (uint64_t)hpos << 32 | i;  // cell -> (head, start)
+            hpos++;
         }
     }
     __syncthreads();
