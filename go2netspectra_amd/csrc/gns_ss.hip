@@ -554,6 +554,43 @@ __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
             double lx = 0.0;
             if (in) { kx = a.skey[k]; rx = a.rep[k]; vx = a.sval[k]; lx = a.tp[k]; }
             uint64_t sm = __ballot(in && rx > 0);
+            if (sm && st.val != 0) {
+                // Speculate over the window: the owner's encodes add vv (u32 wrap, :211-220)
+                // and every other sampled encode leaves (val, key) alone -- its first draw
+                // (the log from S5b) waits past all vv repeats (:223-227), or b^-val
+                // underflows.  Each lane evaluates that test against the val it would see;
+                // the first lane where it does not hold (a decrement, a takeover at val 0,
+                // b <= 1) and everything after it run the sequential loop below, from the
+                // exact state before that lane.  Same operations on the same values, so
+                // bit-identical, and a chain's common case costs one step per window.
+                const bool samp = in && rx > 0;
+                const uint32_t f = (uint32_t)(vx >> 32);
+                const bool own = samp && f == st.key;
+                const uint32_t add = own ? (uint32_t)(uint64_t)rx : 0u;
+                const uint32_t inc = wave_incl_scan(add);
+                const uint32_t vb = st.val + (inc - add);  // val before this lane
+                bool fail = false;
+                if (samp && !own) {
+                    if (vb == 0) {
+                        fail = true;
+                    } else {
+                        const double ppp = go_pow_int(a.g.b, -(double)vb);   // :222
+                        if (ppp > 0) {
+                            if (ppp >= 1) fail = true;
+                            else if (lx / gm_log1m(ppp) < (double)rx) fail = true;
+                        }
+                    }
+                }
+                const uint64_t fm = __ballot(fail);
+                if (!fm) {
+                    st.val += __shfl(inc, 63);
+                    sm = 0;
+                } else {
+                    const int F = __ffsll((unsigned long long)fm) - 1;
+                    st.val = rl32(vb, F);
+                    sm &= ~((1ull << F) - 1ull);  // lanes before F are settled
+                }
+            }
             while (sm) {
                 const int j = __ffsll((unsigned long long)sm) - 1;
                 sm &= sm - 1;
