@@ -546,13 +546,25 @@ __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
         const uint64_t cell = a.skey[k0] >> kSsPktBits;
         const uint32_t row = (uint32_t)(cell / a.g.w);
         MvState st{a.values[cell], a.keys[cell], 0xFFFFFFFFu, 0.0, 0.0};
+        // windows of 64 encodes, three loads ahead of the one being stepped (a
+        // superspreader's chain is thousands of encodes: the step is short, the load is not)
+        struct Win { uint64_t k, v; int64_t r; double l; };
+        auto ld = [&](uint32_t w0) {
+            Win x{0ull, 0ull, 0, 0.0};
+            if (w0 + lane < nj) {
+                const uint32_t k = k0 + w0 + lane;
+                x.k = a.skey[k]; x.r = a.rep[k]; x.v = a.sval[k]; x.l = a.tp[k];
+            }
+            return x;
+        };
+        Win n1 = ld(0), n2 = ld(64), n3 = ld(128), n4 = ld(192);
         for (uint32_t w0 = 0; w0 < nj; w0 += 64) {
-            const uint32_t k = k0 + w0 + lane;
+            const Win cw = n1;
+            n1 = n2; n2 = n3; n3 = n4; n4 = ld(w0 + 256);
             const bool in = w0 + lane < nj;
-            uint64_t kx = 0, vx = 0;
-            int64_t rx = 0;
-            double lx = 0.0;
-            if (in) { kx = a.skey[k]; rx = a.rep[k]; vx = a.sval[k]; lx = a.tp[k]; }
+            const uint64_t kx = cw.k, vx = cw.v;
+            const int64_t rx = cw.r;
+            const double lx = cw.l;
             uint64_t sm = __ballot(in && rx > 0);
             if (sm && st.val != 0) {
                 // Speculate over the window: the owner's encodes add vv (u32 wrap, :211-220)
@@ -1504,6 +1516,16 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
             const double g = h[7] ? (double)h[7] : 1.0;
             fprintf(stderr, "gns_ss P4: %llu groups; per group (memtime ticks) sort1 %.0f scan %.0f sort2 %.0f write %.0f tails %.0f\n",
                     h[7], h[0] / g, h[1] / g, h[2] / g, h[3] / g, h[4] / g);
+            uint32_t nh = 0;
+            GNS_HIP(hipMemcpy(&nh, ss->heads + cells, 4, hipMemcpyDeviceToHost));
+            std::vector<uint32_t> hl(nh);
+            if (nh) GNS_HIP(hipMemcpy(hl.data(), ss->hlen, nh * 4ull, hipMemcpyDeviceToHost));
+            std::sort(hl.begin(), hl.end());
+            uint64_t enc = 0, longc = 0, longe = 0;
+            for (uint32_t v : hl) { enc += v; if (v > kSsLongChain) { longc++; longe += v; } }
+            fprintf(stderr, "gns_ss chains: %u cells, %llu encodes, longest %u %u %u, median %u, %llu above %u holding %llu\n",
+                    nh, (unsigned long long)enc, nh ? hl[nh - 1] : 0u, nh > 1 ? hl[nh - 2] : 0u, nh > 2 ? hl[nh - 3] : 0u,
+                    nh ? hl[nh / 2] : 0u, (unsigned long long)longc, kSsLongChain, (unsigned long long)longe);
         }
         GNS_HIP(hipGetLastError());
     }
