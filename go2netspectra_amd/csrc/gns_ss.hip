@@ -473,8 +473,12 @@ struct MvState {
     uint32_t val, key, mval;
     double mppp, ml1m;
 };
+// b^-val and log1m(b^-val) for val < kSsMvTab, computed once per workgroup into LDS
+// with the same functions: a foreign encode's decrements (val - 1 each) then read
+// them instead of a pow and a log1m per decrement.
+constexpr uint32_t kSsMvTab = 2048;
 __device__ __forceinline__ void mv_encode(const SsApplyArgs &a, MvState &st, int64_t vv, uint32_t f, uint64_t pkt,
-                                          uint32_t row, double lc) {
+                                          uint32_t row, double lc, const double *tpp, const double *tl1m) {
     uint32_t draw = 1;
     while (vv > 0) {                                                    // :207-233
         if (st.val == 0 || st.key == f) {  // every remaining iteration increments (:211-220)
@@ -486,8 +490,13 @@ __device__ __forceinline__ void mv_encode(const SsApplyArgs &a, MvState &st, int
         // encode while val does not change
         if (st.val != st.mval) {
             st.mval = st.val;
-            st.mppp = go_pow_int(a.g.b, -(double)st.val);                   // :222
-            st.ml1m = (st.mppp > 0 && st.mppp < 1) ? gm_log1m(st.mppp) : 0.0;
+            if (st.val < kSsMvTab) {
+                st.mppp = tpp[st.val];
+                st.ml1m = tl1m[st.val];
+            } else {
+                st.mppp = go_pow_int(a.g.b, -(double)st.val);               // :222
+                st.ml1m = (st.mppp > 0 && st.mppp < 1) ? gm_log1m(st.mppp) : 0.0;
+            }
         }
         const double ppp = st.mppp;
         if (!(ppp > 0)) break;  // underflow: no later iteration can decrement
@@ -509,6 +518,13 @@ __device__ __forceinline__ void mv_encode(const SsApplyArgs &a, MvState &st, int
 }
 
 __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
+    __shared__ double s_pp[kSsMvTab], s_l1m[kSsMvTab];
+    for (uint32_t v = threadIdx.x; v < kSsMvTab; v += 256) {
+        const double p = go_pow_int(a.g.b, -(double)v);
+        s_pp[v] = p;
+        s_l1m[v] = (p > 0 && p < 1) ? gm_log1m(p) : 0.0;
+    }
+    __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t hi = blockIdx.x * 256 + threadIdx.x;
     const uint32_t nh = a.heads[a.cells];
@@ -529,7 +545,8 @@ __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
             const uint64_t vx = kn < nenc ? a.sval[kn] : 0ull;
             const int64_t rx = kn < nenc ? a.rep[kn] : 0;
             const double lx = kn < nenc ? a.tp[kn] : 0.0;
-            mv_encode(a, st, rc, (uint32_t)(vc >> 32), a.pkt_base + (kc & ((1ull << kSsPktBits) - 1)), row, lc);
+            mv_encode(a, st, rc, (uint32_t)(vc >> 32), a.pkt_base + (kc & ((1ull << kSsPktBits) - 1)), row, lc, s_pp,
+                      s_l1m);
             if ((kx >> kSsPktBits) != cell) break;
             k = kn; kc = kx; vc = vx; rc = rx; lc = lx;
         }
@@ -586,10 +603,10 @@ __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
                     if (vb == 0) {
                         fail = true;
                     } else {
-                        const double ppp = go_pow_int(a.g.b, -(double)vb);   // :222
+                        const double ppp = vb < kSsMvTab ? s_pp[vb] : go_pow_int(a.g.b, -(double)vb);   // :222
                         if (ppp > 0) {
                             if (ppp >= 1) fail = true;
-                            else if (lx / gm_log1m(ppp) < (double)rx) fail = true;
+                            else if (lx / (vb < kSsMvTab ? s_l1m[vb] : gm_log1m(ppp)) < (double)rx) fail = true;
                         }
                     }
                 }
@@ -608,7 +625,7 @@ __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
                 sm &= sm - 1;
                 const double lcj = __longlong_as_double((long long)rl64((uint64_t)__double_as_longlong(lx), j));
                 mv_encode(a, st, (int64_t)rl64((uint64_t)rx, j), rl32((uint32_t)(vx >> 32), j),
-                          a.pkt_base + (rl64(kx, j) & ((1ull << kSsPktBits) - 1)), row, lcj);
+                          a.pkt_base + (rl64(kx, j) & ((1ull << kSsPktBits) - 1)), row, lcj, s_pp, s_l1m);
             }
         }
         if (lane == 0) { a.values[cell] = st.val; a.keys[cell] = st.key; }
