@@ -11,6 +11,7 @@ run() {  # name, seconds, bench args...
     tail -c 400 $O/$n.json
 }
 run headline 300 --no-cpu &&
+run default 500 &&
 run ss 300 --sketch superspread --no-cpu &&
 run host_compact 300 --host-input compact --no-cpu &&
 run host_headers 300 --host-input headers --no-cpu &&
