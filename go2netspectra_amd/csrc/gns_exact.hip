@@ -649,16 +649,8 @@ constexpr int kAggMinBlocks = kAggCap * 24 <= 78 * 1024 ? 2 : 1;
 static_assert(kAggCap > kAggChunk, "a chunk fits an empty table");
 // Touched-flow list (T and D read it instead of scanning the table): a flow is
 // appended when its first merge of the batch lands (its last index is then still
-// from an earlier batch), so each flow appears once.
-__device__ __forceinline__ void touch_append(bool app, uint32_t id, uint32_t *touch, uint32_t *tcnt) {
-    const uint64_t m = __ballot(app);
-    if (!m) return;  // wave-uniform
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    uint32_t base = 0;
-    if ((int)__lane_id() == leader) base = atomicAdd(tcnt, (uint32_t)__popcll(m));
-    base = __shfl(base, leader);
-    if (app) touch[base + __popcll(m & ((1ull << __lane_id()) - 1ull))] = id;
-}
+// from an earlier batch), so each flow appears once.  One global add per flush
+// for the whole workgroup's appends (the counter is shared by every workgroup).
 
 __device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t *mn, uint32_t *mx,
                                            unsigned long long *by, uint64_t pkt_base, FlowState f, uint32_t *touch,
@@ -673,10 +665,28 @@ __device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t
         id[j] = e < kAggCap ? key[e] : GNS_ID_NONE;
         if (id[j] != GNS_ID_NONE) { pk[j] = f.pkts[id[j]]; bt[j] = f.bytes[id[j]]; ls[j] = f.last[id[j]]; fs[j] = f.first[id[j]]; }
     }
+    {
+        __shared__ uint32_t s_tw[kAggThreads / 64], s_tbase;
+        const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j++) c += (id[j] != GNS_ID_NONE && ls[j] <= pkt_base) ? 1u : 0u;
+        const uint32_t inc = __ockl_wfscan_add_u32(c, true);
+        if (lane == 63) s_tw[wave] = inc;
+        __syncthreads();
+        const uint32_t x = lane < kAggThreads / 64 ? s_tw[lane] : 0u;
+        const uint32_t winc = __ockl_wfscan_add_u32(x, true);
+        const uint32_t tot = __shfl(winc, 63);  // (all lanes active)
+        if (threadIdx.x == 0) s_tbase = atomicAdd(tcnt, tot);
+        __syncthreads();
+        uint32_t pos = s_tbase + __shfl(winc - x, (int)wave) + inc - c;
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j++)
+            if (id[j] != GNS_ID_NONE && ls[j] <= pkt_base) touch[pos++] = id[j];
+    }
 #pragma unroll
     for (uint32_t j = 0; j < kPer; j++) {
         const uint32_t e = threadIdx.x + j * kAggThreads;
-        touch_append(id[j] != GNS_ID_NONE && ls[j] <= pkt_base, id[j], touch, tcnt);
         if (id[j] == GNS_ID_NONE) continue;
         f.pkts[id[j]] = pk[j] + cn[e];
         f.bytes[id[j]] = bt[j] + by[e];
