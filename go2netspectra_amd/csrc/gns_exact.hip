@@ -482,7 +482,7 @@ __global__ __launch_bounds__(256) void k_ex_hot_reduce(const ExHotPart *hpart, u
             f.pkts[id] += c;
             f.bytes[id] += by;
             f.last[id] = max(f.last[id], pkt_base + mx + 1);
-            touch[atomicAdd(tcnt, 1u)] = id;  // designated flows never reach P
+            if (touch) touch[atomicAdd(tcnt, 1u)] = id;  // designated flows never reach P
         }
     }
 }
@@ -644,6 +644,7 @@ constexpr uint32_t kAggDepth = GNS_AGG_DEPTH;  // chunks of words in flight
 #ifndef GNS_AGG_FOLD
 #define GNS_AGG_FOLD 4
 #endif
+constexpr uint64_t kExListSlots = 1ull << 23;  // T/D read the touched list above this many slots
 constexpr uint32_t kAggCap = GNS_AGG_CAP;  // 24 B per entry: 72 KB
 constexpr int kAggMinBlocks = kAggCap * 24 <= 78 * 1024 ? 2 : 1;
 static_assert(kAggCap > kAggChunk, "a chunk fits an empty table");
@@ -665,7 +666,7 @@ __device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t
         id[j] = e < kAggCap ? key[e] : GNS_ID_NONE;
         if (id[j] != GNS_ID_NONE) { pk[j] = f.pkts[id[j]]; bt[j] = f.bytes[id[j]]; ls[j] = f.last[id[j]]; fs[j] = f.first[id[j]]; }
     }
-    {
+    if (touch) {  // block-uniform: list mode (a large table)
         __shared__ uint32_t s_tw[kAggThreads / 64], s_tbase;
         const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
         uint32_t c = 0;
@@ -798,11 +799,13 @@ __global__ __launch_bounds__(kAggThreads, kAggMinBlocks) void k_ex_pagg(const ui
 
 // T: StartTime / EndTime from the merged stream indices of the flows this batch
 // touched (task.go:137,141-142).
+// touch == nullptr: every slot (a sequential scan, cheaper while the table is small);
+// else the batch's touched-flow list (random gathers, but a cost that follows the batch)
 __global__ __launch_bounds__(256) void k_ex_times(FlowState f, const uint32_t *touch, const uint32_t *tcnt,
-                                                  uint64_t pkt_base, uint64_t n, const int64_t *ts) {
-    const uint32_t nt = *tcnt;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nt; i += gridDim.x * 256) {
-        const uint32_t s = touch[i];
+                                                  uint64_t slots, uint64_t pkt_base, uint64_t n, const int64_t *ts) {
+    const uint64_t nt = touch ? *tcnt : slots;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nt; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t s = touch ? touch[i] : (uint32_t)i;
         const unsigned long long l = f.last[s], fs = f.first[s];
         if (l > pkt_base && l <= pkt_base + n) f.end[s] = ts[l - 1 - pkt_base];
         if (fs >= pkt_base && fs < pkt_base + n) f.start[s] = ts[fs - pkt_base];
@@ -819,13 +822,13 @@ __device__ __forceinline__ uint32_t exh_key(unsigned long long p) {
 // (over the flows the batch touched: a flow designated now had packets in this
 // batch; the choice only steers performance, every choice is exact)
 __global__ __launch_bounds__(256) void k_exh_hist(const unsigned long long *pkts, const uint32_t *touch,
-                                                  const uint32_t *tcnt, uint32_t *hist) {
+                                                  const uint32_t *tcnt, uint64_t slots, uint32_t *hist) {
     __shared__ uint32_t h[512];
     for (uint32_t i = threadIdx.x; i < 512; i += 256) h[i] = 0;
     __syncthreads();
-    const uint32_t nt = *tcnt;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nt; i += gridDim.x * 256) {
-        const uint32_t k = exh_key(pkts[touch[i]]);
+    const uint64_t nt = touch ? *tcnt : slots;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nt; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t k = exh_key(pkts[touch ? touch[i] : (uint32_t)i]);
         if (k >= kExHotMinKey) atomicAdd(&h[k], 1u);
     }
     __syncthreads();
@@ -852,11 +855,11 @@ __global__ __launch_bounds__(512) void k_exh_pick(const uint32_t *hist, uint32_t
     if (k == 0) *thr = s_t;
 }
 __global__ __launch_bounds__(256) void k_exh_collect(const unsigned long long *pkts, const uint32_t *touch,
-                                                     const uint32_t *tcnt, const uint32_t *thr, uint32_t *cnt,
-                                                     uint32_t *hot_ids) {
-    const uint32_t nt = *tcnt;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nt; i += gridDim.x * 256) {
-        const uint32_t s = touch[i];
+                                                     const uint32_t *tcnt, uint64_t slots, const uint32_t *thr,
+                                                     uint32_t *cnt, uint32_t *hot_ids) {
+    const uint64_t nt = touch ? *tcnt : slots;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nt; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t s = touch ? touch[i] : (uint32_t)i;
         const uint32_t k = exh_key(pkts[s]);
         if (k >= *thr && k >= kExHotMinKey) {
             const uint32_t q = atomicAdd(cnt, 1u);
@@ -961,6 +964,7 @@ using namespace gns;
 
 struct gns_ex {
     int device = 0;
+    bool force_list = false;  // GNS_EX_LIST=1: T/D over the touched list at any table size (tests)
     hipStream_t stream = nullptr;
     KeyPlanN kp{};
     uint32_t K = 0;
@@ -1082,6 +1086,10 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
         GNS_HIP(hipGetLastError());
         cur ^= 1;
     }
+    // T and D over the batch's touched-flow list once the table is large (a table that
+    // grew with the period would make a full scan cost more than the batch); below
+    // that, a sequential scan of every slot is cheaper than the list's random gathers
+    uint32_t *touch = (ex->slots > kExListSlots || ex->force_list) ? ex->touch : nullptr;
     const uint32_t ks = ex->sb + ex->ib;
     // flow ids < slots = 2^(key_bits - 1): bin = id >> pshift
     const uint32_t pshift = ex->key_bits - 1 > kPBinBits ? ex->key_bits - 1 - kPBinBits : 0u;
@@ -1090,7 +1098,7 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
         ScopedStage st(ex->timer, 4);
         GNS_HIP(hipMemsetAsync(ex->hctl + 515, 0, 4, s));  // touched flows of this batch
         hipLaunchKernelGGL(k_ex_hot_reduce, dim3(kExHot), dim3(256), 0, s, ex->hpart, nblk, ex->hot_ids, ex->pkt, ex->f,
-                           ex->touch, ex->hctl + 515);
+                           touch, ex->hctl + 515);
         GNS_HIP(hipGetLastError());
     }
     {
@@ -1107,19 +1115,20 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     {
         ScopedStage st(ex->timer, 3);
         hipLaunchKernelGGL(k_ex_pagg, dim3(kPBins), dim3(kAggThreads), 0, s, ex->sk[1], ex->pb, ex->sb, ex->ib,
-                           xin.in.sizes, ex->pkt, ex->f, ex->touch, ex->hctl + 515);
+                           xin.in.sizes, ex->pkt, ex->f, touch, ex->hctl + 515);
         GNS_HIP(hipGetLastError());
     }
     {   // timestamps of the touched flows; the next batch's designated flows
         ScopedStage st(ex->timer, 4);
-        // sized by the batch, not the table: at most n + kExHot flows are touched
-        const unsigned sg = (unsigned)std::min<uint64_t>((n + kExHot + 255) / 256, 2048);
-        hipLaunchKernelGGL(k_ex_times, dim3(sg), dim3(256), 0, s, ex->f, ex->touch, ex->hctl + 515, ex->pkt, n, xin.ts);
+        const unsigned sg = (unsigned)std::min<uint64_t>(((touch ? n + kExHot : ex->slots) + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_ex_times, dim3(sg), dim3(256), 0, s, ex->f, touch, ex->hctl + 515, ex->slots, ex->pkt, n,
+                           xin.ts);
         GNS_HIP(hipMemsetAsync(ex->hctl, 0, 514 * 4, s));
         GNS_HIP(hipMemsetAsync(ex->hot_ids, 0xFF, kExHot * 4, s));
-        hipLaunchKernelGGL(k_exh_hist, dim3(sg), dim3(256), 0, s, ex->f.pkts, ex->touch, ex->hctl + 515, ex->hctl);
+        hipLaunchKernelGGL(k_exh_hist, dim3(std::min(sg, 2048u)), dim3(256), 0, s, ex->f.pkts, touch, ex->hctl + 515,
+                           ex->slots, ex->hctl);
         hipLaunchKernelGGL(k_exh_pick, dim3(1), dim3(512), 0, s, ex->hctl, ex->hctl + 512);
-        hipLaunchKernelGGL(k_exh_collect, dim3(sg), dim3(256), 0, s, ex->f.pkts, ex->touch, ex->hctl + 515,
+        hipLaunchKernelGGL(k_exh_collect, dim3(sg), dim3(256), 0, s, ex->f.pkts, touch, ex->hctl + 515, ex->slots,
                            ex->hctl + 512, ex->hctl + 513, ex->hot_ids);
         hipLaunchKernelGGL(k_exh_table, dim3(1), dim3(kExHot), 0, s, ex->hot_ids, ex->f.pkts, ex->hot_tab);
         GNS_HIP(hipGetLastError());
@@ -1330,6 +1339,10 @@ int gns_ex_create(const gns_ex_params *p, gns_ex **out) {
         ex->D.K = ex->K;
         ex->D.RW = dict_record_words(ex->K);
         ex->D.seed = 0x5BD1E995u;
+        {
+            const char *env = getenv("GNS_EX_LIST");
+            ex->force_list = env && env[0] == '1';
+        }
         ex->bmax = p->batch_packets ? p->batch_packets : (16ull << 20);
         ex->bmax = std::min<uint64_t>(((ex->bmax + kXChunk - 1) / kXChunk) * kXChunk, 1ull << 31);
         {   // sort word fields (ex_geometry, before the batch buffers are sized)

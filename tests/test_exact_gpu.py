@@ -247,8 +247,8 @@ def test_pcapng_capture_drives_exact_and_countmin(gpu, oracle, tmp_path):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("batch", [4096, 300_000, 1_500_000])
-def test_start_end_times_with_heavy_ties_across_sort_paths(gpu, oracle, batch):
+@pytest.mark.parametrize("batch,touched_list", [(4096, False), (300_000, False), (1_500_000, False), (300_000, True)])
+def test_start_end_times_with_heavy_ties_across_sort_paths(gpu, oracle, monkeypatch, batch, touched_list):
     """StartTime / EndTime come from the merged smallest / largest stream index of
     every path (designated flows' LDS partials in X1 and X1b, the tail's per-bin
     aggregation with wave folding).  Batch sizes span the cold-start cap, one and
@@ -256,6 +256,8 @@ def test_start_end_times_with_heavy_ties_across_sort_paths(gpu, oracle, batch):
     (and fold in P4 before it); timestamps are random so any wrong first / last
     packet shows."""
     from go2netspectra_amd import ExactTask, PacketBatch
+    if touched_list:  # T and D over the batch's touched-flow list (large tables) instead of a slot scan
+        monkeypatch.setenv("GNS_EX_LIST", "1")
     rng = np.random.default_rng(batch)
     n = 3_000_000
     t = random_tuples(rng, n, 40, s=0.8)
@@ -269,11 +271,14 @@ def test_start_end_times_with_heavy_ties_across_sort_paths(gpu, oracle, batch):
     assert_same_flows(gpu_flows(task), orc.export())
 
 
-def test_tail_bins_with_more_flows_than_the_table(gpu, oracle):
+@pytest.mark.parametrize("touched_list", [False, True])
+def test_tail_bins_with_more_flows_than_the_table(gpu, oracle, monkeypatch, touched_list):
     """About 1.4M distinct tail flows in one batch: each of P4's 512 bins holds more
     flows than its LDS table takes before a flush (2048), so bins merge in several
     rounds; every flow's four fields must still equal the oracle's."""
     from go2netspectra_amd import ExactTask, PacketBatch
+    if touched_list:
+        monkeypatch.setenv("GNS_EX_LIST", "1")
     rng = np.random.default_rng(11)
     n = 3_000_000
     t = random_tuples(rng, n, 3_000_000, s=0.3)
