@@ -56,8 +56,7 @@ struct SsExtractArgs {
     const uint8_t *regs;
     uint64_t *ckey;     // candidates: (cell*m + reg) << 27 | packet, block regions of chunk*d
     uint32_t *cval;     // lz
-    uint32_t *ccount;   // total candidates
-    uint32_t *cblk;     // [2*nblk]: per-block count, per-block output base
+    uint32_t *cblk;     // [nblk]: candidates per block (in the block's own region)
     unsigned long long *stats;  // 0 inserted, 1 dropped, 2 unsupported, 3 dict full, 4 candidates, 5 encodes
 };
 
@@ -160,7 +159,6 @@ __global__ __launch_bounds__(kSsThreads) void k_ss_extract(SsExtractArgs a) {
     __syncthreads();
     if (tid == 0) {
         a.cblk[blk] = s_cc;
-        a.cblk[gridDim.x + blk] = s_cc ? atomicAdd(a.ccount, s_cc) : 0u;
         if (s_cc) atomicAdd(&a.stats[4], (unsigned long long)s_cc);
         if (s_ok) atomicAdd(&a.stats[0], (unsigned long long)s_ok);
         if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
@@ -297,7 +295,6 @@ __global__ __launch_bounds__(kSsThreads, GNS_SS_MINW) void k_ss_extract_hdr(SsEx
     __syncthreads();
     if (tid == 0) {
         a.cblk[blk] = s_cc;
-        a.cblk[gridDim.x + blk] = s_cc ? atomicAdd(a.ccount, s_cc) : 0u;
         if (s_cc) atomicAdd(&a.stats[4], (unsigned long long)s_cc);
         if (s_ok) atomicAdd(&a.stats[0], (unsigned long long)s_ok);
         if (s_drop) atomicAdd(&a.stats[1], (unsigned long long)s_drop);
@@ -1340,7 +1337,7 @@ struct gns_ss {
     uint64_t *ckey = nullptr, *ckey_s = nullptr, *skey = nullptr, *skey_s = nullptr;
     uint32_t *cval = nullptr;
     uint64_t *sval = nullptr;
-    uint32_t *counts = nullptr;  // [0] candidates, [1] encodes, [2] P4 bin counter, [3] candidates (P2)
+    uint32_t *counts = nullptr;  // [1] encodes, [2] P4 bin counter, [3] candidates (P2); [0] unused
     uint32_t *heads = nullptr;   // [cells + 1]: S5 segment starts (unordered), then their count
     uint32_t *hlen = nullptr;    // [cells]: encodes per segment
     uint32_t *cblk = nullptr;
@@ -1467,14 +1464,14 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     const SpGeom &sg = ss->sp;
     ScopedStage total_stage(ss->timer, 5);
     GNS_HIP(hipMemsetAsync(ss->ptotal, 0, 8, s));
-    GNS_HIP(hipMemsetAsync(ss->counts, 0, 16, s));     // [0] candidates, [1] encodes, [2] P4 bin counter
+    GNS_HIP(hipMemsetAsync(ss->counts, 0, 16, s));     // [1] encodes, [2] P4 bin counter, [3] candidates (P2)
     GNS_HIP(hipMemsetAsync(ss->heads + cells, 0, 4, s));
     GNS_HIP(hipMemsetAsync(ss->dctl + 1, 0, 4, s));  // abort flag of this batch
     if (++ss->epoch == 0) ss->epoch = 1;
     SsExtractArgs x{};
     x.in = in; x.n = n; x.kpf = ss->kpf; x.kpm = ss->kpm;
     x.g = ss->g; x.regs = ss->regs;
-    x.ckey = ss->ckey; x.cval = ss->cval; x.ccount = ss->counts; x.cblk = ss->cblk; x.stats = ss->stats;
+    x.ckey = ss->ckey; x.cval = ss->cval; x.cblk = ss->cblk; x.stats = ss->stats;
     {
         ScopedStage st(ss->timer, 0);
         bool piped = false;
