@@ -16,6 +16,8 @@ run ss 300 --sketch superspread --no-cpu &&
 run host_compact 300 --host-input compact --no-cpu &&
 run host_headers 300 --host-input headers --no-cpu &&
 run c5 400 --width 16777216 --depth 8 --no-cpu &&
+run exact 300 --sketch exact --no-cpu &&
+run hybrid 500 --sketch hybrid --no-cpu &&
 echo "== rocprof headline" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_cm -o cm -- \
     python3 bench.py --no-cpu --steps 5 --warmup 2 > $O/prof_cm.log 2>&1 &&
