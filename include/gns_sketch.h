@@ -230,7 +230,11 @@ typedef struct gns_ss_params {
 
 /* The SuperSpread flow dictionary holds the flows that own a cell (only they
  * can be named by a key, a query or a heavy hitter); it is reclaimed and grows
- * like Count-Min's (see the rules above), so inserts do not fail on it. */
+ * like Count-Min's (see the rules above), so inserts do not fail on it.
+ * Deviations (GNS_E_ARG at create): depth <= 8, m <= 256, size <= 8, merged
+ * key <= 74 bytes, depth * width <= 2^25 cells.  An insert returns GNS_E_RANGE,
+ * with the sketch unchanged, if one cell gets more than 8192 encodes in one
+ * device batch (m = 256 only); a smaller batch_packets avoids it. */
 int gns_ss_create(const gns_ss_params *p, gns_ss **out);
 int gns_ss_destroy(gns_ss *ss);
 int gns_ss_insert_keys(gns_ss *ss, const uint8_t *flows, uint32_t fstride, const uint8_t *elems,
