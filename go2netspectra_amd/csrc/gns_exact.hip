@@ -454,6 +454,7 @@ extern "C" __device__ unsigned __ockl_wfscan_add_u32(unsigned, bool);
 // workgroup per hot slot; the only writer of these flows until P4, which merges
 // the flow's packets that were parked in X1).  first stays: a designated flow
 // had packets before this batch.
+template <bool LIST>
 __global__ __launch_bounds__(256) void k_ex_hot_reduce(const ExHotPart *hpart, uint32_t nblk, const uint32_t *hot_ids,
                                                        uint64_t pkt_base, FlowState f, uint32_t *touch, uint32_t *tcnt) {
     __shared__ unsigned long long s_by[4];
@@ -482,7 +483,7 @@ __global__ __launch_bounds__(256) void k_ex_hot_reduce(const ExHotPart *hpart, u
             f.pkts[id] += c;
             f.bytes[id] += by;
             f.last[id] = max(f.last[id], pkt_base + mx + 1);
-            if (touch) touch[atomicAdd(tcnt, 1u)] = id;  // designated flows never reach P
+            if constexpr (LIST) touch[atomicAdd(tcnt, 1u)] = id;  // designated flows never reach P
         }
     }
 }
@@ -653,6 +654,7 @@ static_assert(kAggCap > kAggChunk, "a chunk fits an empty table");
 // from an earlier batch), so each flow appears once.  One global add per flush
 // for the whole workgroup's appends (the counter is shared by every workgroup).
 
+template <bool LIST>
 __device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t *mn, uint32_t *mx,
                                            unsigned long long *by, uint64_t pkt_base, FlowState f, uint32_t *touch,
                                            uint32_t *tcnt) {
@@ -666,7 +668,7 @@ __device__ __forceinline__ void pagg_flush(uint32_t *key, uint32_t *cn, uint32_t
         id[j] = e < kAggCap ? key[e] : GNS_ID_NONE;
         if (id[j] != GNS_ID_NONE) { pk[j] = f.pkts[id[j]]; bt[j] = f.bytes[id[j]]; ls[j] = f.last[id[j]]; fs[j] = f.first[id[j]]; }
     }
-    if (touch) {  // block-uniform: list mode (a large table)
+    if constexpr (LIST) {  // the touched-flow list (large tables only: the scan variant compiles without it)
         __shared__ uint32_t s_tw[kAggThreads / 64], s_tbase;
         const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
         uint32_t c = 0;
@@ -722,6 +724,7 @@ __device__ __forceinline__ uint32_t pagg_slot(uint32_t *key, uint32_t id, uint32
         // another flow took that slot: read the bucket again
     }
 }
+template <bool LIST>
 __global__ __launch_bounds__(kAggThreads, kAggMinBlocks) void k_ex_pagg(const uint64_t *in, const uint32_t *pb, uint32_t sb,
                                                             uint32_t ib, const uint32_t *sizes, uint64_t pkt_base,
                                                             FlowState f, uint32_t *touch, uint32_t *tcnt) {
@@ -746,7 +749,7 @@ __global__ __launch_bounds__(kAggThreads, kAggMinBlocks) void k_ex_pagg(const ui
     __syncthreads();
     for (uint32_t c0 = beg; c0 < end; c0 += kAggChunk) {  // block-uniform trip count
         if (s_n > kAggCap - kAggChunk) {  // block-uniform (read after the barrier)
-            pagg_flush(key, cn, mn, mx, by, pkt_base, f, touch, tcnt);
+            pagg_flush<LIST>(key, cn, mn, mx, by, pkt_base, f, touch, tcnt);
             __syncthreads();
             if (tid == 0) s_n = 0;
             __syncthreads();
@@ -794,22 +797,18 @@ __global__ __launch_bounds__(kAggThreads, kAggMinBlocks) void k_ex_pagg(const ui
         }
         __syncthreads();
     }
-    pagg_flush(key, cn, mn, mx, by, pkt_base, f, touch, tcnt);
+    pagg_flush<LIST>(key, cn, mn, mx, by, pkt_base, f, touch, tcnt);
 }
 
 // T: StartTime / EndTime from the merged stream indices of the flows this batch
 // touched (task.go:137,141-142).
-// touch == nullptr: every slot (a sequential scan, cheaper while the table is small);
-// else the batch's touched-flow list (random gathers, but a cost that follows the batch)
-__global__ __launch_bounds__(256) void k_ex_times(FlowState f, const uint32_t *touch, const uint32_t *tcnt,
-                                                  uint64_t slots, uint64_t pkt_base, uint64_t n, const int64_t *ts) {
-    const uint64_t nt = touch ? *tcnt : slots;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nt; i += (uint64_t)gridDim.x * 256) {
-        const uint32_t s = touch ? touch[i] : (uint32_t)i;
-        const unsigned long long l = f.last[s], fs = f.first[s];
-        if (l > pkt_base && l <= pkt_base + n) f.end[s] = ts[l - 1 - pkt_base];
-        if (fs >= pkt_base && fs < pkt_base + n) f.start[s] = ts[fs - pkt_base];
-    }
+__global__ __launch_bounds__(256) void k_ex_times(FlowState f, uint64_t slots, uint64_t pkt_base, uint64_t n,
+                                                  const int64_t *ts) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= slots) return;
+    const unsigned long long l = f.last[s], fs = f.first[s];
+    if (l > pkt_base && l <= pkt_base + n) f.end[s] = ts[l - 1 - pkt_base];
+    if (fs >= pkt_base && fs < pkt_base + n) f.start[s] = ts[fs - pkt_base];
 }
 
 // D: designate the next batch's heavy flows: the flows in the largest 1/8-octave
@@ -819,16 +818,12 @@ __device__ __forceinline__ uint32_t exh_key(unsigned long long p) {
     const uint32_t lz = 63u - (uint32_t)__clzll((long long)p);
     return lz * 8u + (uint32_t)((p >> (lz - 3)) & 7u);
 }
-// (over the flows the batch touched: a flow designated now had packets in this
-// batch; the choice only steers performance, every choice is exact)
-__global__ __launch_bounds__(256) void k_exh_hist(const unsigned long long *pkts, const uint32_t *touch,
-                                                  const uint32_t *tcnt, uint64_t slots, uint32_t *hist) {
+__global__ __launch_bounds__(256) void k_exh_hist(const unsigned long long *pkts, uint64_t slots, uint32_t *hist) {
     __shared__ uint32_t h[512];
     for (uint32_t i = threadIdx.x; i < 512; i += 256) h[i] = 0;
     __syncthreads();
-    const uint64_t nt = touch ? *tcnt : slots;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nt; i += (uint64_t)gridDim.x * 256) {
-        const uint32_t k = exh_key(pkts[touch ? touch[i] : (uint32_t)i]);
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * 256) {
+        const uint32_t k = exh_key(pkts[s]);
         if (k >= kExHotMinKey) atomicAdd(&h[k], 1u);
     }
     __syncthreads();
@@ -854,12 +849,50 @@ __global__ __launch_bounds__(512) void k_exh_pick(const uint32_t *hist, uint32_t
     __syncthreads();
     if (k == 0) *thr = s_t;
 }
-__global__ __launch_bounds__(256) void k_exh_collect(const unsigned long long *pkts, const uint32_t *touch,
+__global__ __launch_bounds__(256) void k_exh_collect(const unsigned long long *pkts, uint64_t slots,
+                                                     const uint32_t *thr, uint32_t *cnt, uint32_t *hot_ids) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= slots) return;
+    const uint32_t k = exh_key(pkts[s]);
+    if (k >= *thr && k >= kExHotMinKey) {
+        const uint32_t q = atomicAdd(cnt, 1u);
+        if (q < kExHot) hot_ids[q] = (uint32_t)s;
+    }
+}
+// T and D over the batch's touched-flow list instead of every slot: tables above
+// kExListSlots (a table that grew with the period), where a scan would cost more
+// than the batch.  The list's random gathers cost more than the scan below that.
+__global__ __launch_bounds__(256) void k_ex_times_list(FlowState f, const uint32_t *touch, const uint32_t *tcnt,
+                                                  uint64_t slots, uint64_t pkt_base, uint64_t n, const int64_t *ts) {
+    const uint64_t nt = *tcnt;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nt; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t s = touch[i];
+        const unsigned long long l = f.last[s], fs = f.first[s];
+        if (l > pkt_base && l <= pkt_base + n) f.end[s] = ts[l - 1 - pkt_base];
+        if (fs >= pkt_base && fs < pkt_base + n) f.start[s] = ts[fs - pkt_base];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_exh_hist_list(const unsigned long long *pkts, const uint32_t *touch,
+                                                  const uint32_t *tcnt, uint64_t slots, uint32_t *hist) {
+    __shared__ uint32_t h[512];
+    for (uint32_t i = threadIdx.x; i < 512; i += 256) h[i] = 0;
+    __syncthreads();
+    const uint64_t nt = *tcnt;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nt; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t k = exh_key(pkts[touch[i]]);
+        if (k >= kExHotMinKey) atomicAdd(&h[k], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 512; i += 256)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+__global__ __launch_bounds__(256) void k_exh_collect_list(const unsigned long long *pkts, const uint32_t *touch,
                                                      const uint32_t *tcnt, uint64_t slots, const uint32_t *thr,
                                                      uint32_t *cnt, uint32_t *hot_ids) {
-    const uint64_t nt = touch ? *tcnt : slots;
+    const uint64_t nt = *tcnt;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nt; i += (uint64_t)gridDim.x * 256) {
-        const uint32_t s = touch ? touch[i] : (uint32_t)i;
+        const uint32_t s = touch[i];
         const uint32_t k = exh_key(pkts[s]);
         if (k >= *thr && k >= kExHotMinKey) {
             const uint32_t q = atomicAdd(cnt, 1u);
@@ -1097,8 +1130,12 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     {
         ScopedStage st(ex->timer, 4);
         GNS_HIP(hipMemsetAsync(ex->hctl + 515, 0, 4, s));  // touched flows of this batch
-        hipLaunchKernelGGL(k_ex_hot_reduce, dim3(kExHot), dim3(256), 0, s, ex->hpart, nblk, ex->hot_ids, ex->pkt, ex->f,
-                           touch, ex->hctl + 515);
+        if (touch)
+            hipLaunchKernelGGL(k_ex_hot_reduce<true>, dim3(kExHot), dim3(256), 0, s, ex->hpart, nblk, ex->hot_ids, ex->pkt,
+                               ex->f, touch, ex->hctl + 515);
+        else
+            hipLaunchKernelGGL(k_ex_hot_reduce<false>, dim3(kExHot), dim3(256), 0, s, ex->hpart, nblk, ex->hot_ids, ex->pkt,
+                               ex->f, touch, ex->hctl + 515);
         GNS_HIP(hipGetLastError());
     }
     {
@@ -1114,22 +1151,38 @@ int ex_run_batch(gns_ex *ex, const ExIn &xin, uint64_t n) {
     }
     {
         ScopedStage st(ex->timer, 3);
-        hipLaunchKernelGGL(k_ex_pagg, dim3(kPBins), dim3(kAggThreads), 0, s, ex->sk[1], ex->pb, ex->sb, ex->ib,
+        if (touch)
+            hipLaunchKernelGGL(k_ex_pagg<true>, dim3(kPBins), dim3(kAggThreads), 0, s, ex->sk[1], ex->pb, ex->sb, ex->ib,
+                           xin.in.sizes, ex->pkt, ex->f, touch, ex->hctl + 515);
+        else
+            hipLaunchKernelGGL(k_ex_pagg<false>, dim3(kPBins), dim3(kAggThreads), 0, s, ex->sk[1], ex->pb, ex->sb, ex->ib,
                            xin.in.sizes, ex->pkt, ex->f, touch, ex->hctl + 515);
         GNS_HIP(hipGetLastError());
     }
     {   // timestamps of the touched flows; the next batch's designated flows
         ScopedStage st(ex->timer, 4);
-        const unsigned sg = (unsigned)std::min<uint64_t>(((touch ? n + kExHot : ex->slots) + 255) / 256, 4096);
-        hipLaunchKernelGGL(k_ex_times, dim3(sg), dim3(256), 0, s, ex->f, touch, ex->hctl + 515, ex->slots, ex->pkt, n,
-                           xin.ts);
-        GNS_HIP(hipMemsetAsync(ex->hctl, 0, 514 * 4, s));
-        GNS_HIP(hipMemsetAsync(ex->hot_ids, 0xFF, kExHot * 4, s));
-        hipLaunchKernelGGL(k_exh_hist, dim3(std::min(sg, 2048u)), dim3(256), 0, s, ex->f.pkts, touch, ex->hctl + 515,
-                           ex->slots, ex->hctl);
-        hipLaunchKernelGGL(k_exh_pick, dim3(1), dim3(512), 0, s, ex->hctl, ex->hctl + 512);
-        hipLaunchKernelGGL(k_exh_collect, dim3(sg), dim3(256), 0, s, ex->f.pkts, touch, ex->hctl + 515, ex->slots,
-                           ex->hctl + 512, ex->hctl + 513, ex->hot_ids);
+        if (touch) {
+            const unsigned sg = (unsigned)std::min<uint64_t>((n + kExHot + 255) / 256, 4096);
+            hipLaunchKernelGGL(k_ex_times_list, dim3(sg), dim3(256), 0, s, ex->f, touch, ex->hctl + 515, ex->slots, ex->pkt,
+                               n, xin.ts);
+            GNS_HIP(hipMemsetAsync(ex->hctl, 0, 514 * 4, s));
+            GNS_HIP(hipMemsetAsync(ex->hot_ids, 0xFF, kExHot * 4, s));
+            hipLaunchKernelGGL(k_exh_hist_list, dim3(std::min(sg, 2048u)), dim3(256), 0, s, ex->f.pkts, touch,
+                               ex->hctl + 515, ex->slots, ex->hctl);
+            hipLaunchKernelGGL(k_exh_pick, dim3(1), dim3(512), 0, s, ex->hctl, ex->hctl + 512);
+            hipLaunchKernelGGL(k_exh_collect_list, dim3(sg), dim3(256), 0, s, ex->f.pkts, touch, ex->hctl + 515,
+                               ex->slots, ex->hctl + 512, ex->hctl + 513, ex->hot_ids);
+        } else {
+            const unsigned sg = (unsigned)((ex->slots + 255) / 256);
+            hipLaunchKernelGGL(k_ex_times, dim3(sg), dim3(256), 0, s, ex->f, ex->slots, ex->pkt, n, xin.ts);
+            GNS_HIP(hipMemsetAsync(ex->hctl, 0, 514 * 4, s));
+            GNS_HIP(hipMemsetAsync(ex->hot_ids, 0xFF, kExHot * 4, s));
+            hipLaunchKernelGGL(k_exh_hist, dim3(std::min<unsigned>(sg, 2048)), dim3(256), 0, s, ex->f.pkts, ex->slots,
+                               ex->hctl);
+            hipLaunchKernelGGL(k_exh_pick, dim3(1), dim3(512), 0, s, ex->hctl, ex->hctl + 512);
+            hipLaunchKernelGGL(k_exh_collect, dim3(sg), dim3(256), 0, s, ex->f.pkts, ex->slots, ex->hctl + 512,
+                               ex->hctl + 513, ex->hot_ids);
+        }
         hipLaunchKernelGGL(k_exh_table, dim3(1), dim3(kExHot), 0, s, ex->hot_ids, ex->f.pkts, ex->hot_tab);
         GNS_HIP(hipGetLastError());
     }
