@@ -630,38 +630,6 @@ __global__ __launch_bounds__(256) void k_ss_walk_mv(SsApplyArgs a) {
 }
 #pragma clang fp contract(on)
 
-// S5 schedule: the touched cells by decreasing chain length (256 length classes,
-// any order inside a class), so the 64 lanes of a walk wave hold chains of about
-// the same length instead of the batch's longest chain setting every wave's time.
-// Block-major class histograms, the shared K2 scan, then a per-block scatter.
-constexpr uint32_t kHsCls = 256;
-__device__ __forceinline__ uint32_t hs_class(uint32_t len) { return kHsCls - 1u - min(len, kHsCls - 1u); }
-__global__ __launch_bounds__(256) void k_hs_hist(const uint32_t *heads, const uint32_t *hlen, uint32_t cells,
-                                                 uint32_t *hist) {
-    __shared__ uint32_t h[kHsCls];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t hi = blockIdx.x * 256 + threadIdx.x;
-    if (hi < heads[cells]) atomicAdd(&h[hs_class(hlen[hi])], 1u);
-    __syncthreads();
-    hist[(uint64_t)blockIdx.x * kHsCls + threadIdx.x] = h[threadIdx.x];
-}
-__global__ __launch_bounds__(256) void k_hs_scatter(const uint32_t *heads, const uint32_t *hlen, uint32_t cells,
-                                                    const uint32_t *offs, uint32_t *heads2, uint32_t *hlen2) {
-    __shared__ uint32_t cur[kHsCls];
-    cur[threadIdx.x] = offs[(uint64_t)blockIdx.x * kHsCls + threadIdx.x];
-    __syncthreads();
-    const uint32_t hi = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t nh = heads[cells];
-    if (hi == 0) heads2[cells] = nh;
-    if (hi < nh) {
-        const uint32_t len = hlen[hi];
-        const uint32_t pos = atomicAdd(&cur[hs_class(len)], 1u);
-        heads2[pos] = heads[hi];
-        hlen2[pos] = len;
-    }
-}
-
 // Query (super_spread.go:238-249)
 struct SsQueryArgs {
     const uint8_t *flows;
@@ -1372,8 +1340,6 @@ struct gns_ss {
     uint32_t *counts = nullptr;  // [1] encodes, [2] P4 bin counter, [3] candidates (P2); [0] unused
     uint32_t *heads = nullptr;   // [cells + 1]: S5 segment starts (unordered), then their count
     uint32_t *hlen = nullptr;    // [cells]: encodes per segment
-    uint32_t *heads2 = nullptr, *hlen2 = nullptr;  // the same, by decreasing length (S5's order)
-    uint32_t *hhist = nullptr, *hpart = nullptr;   // their class histograms and scan
     uint32_t *cblk = nullptr;
     SpGeom sp{};
     uint32_t ncu = 0;
@@ -1403,7 +1369,7 @@ void ss_free_all(gns_ss *ss) {
     dfree(ss->pcnt[0]); dfree(ss->pcnt[1]);
     dfree(ss->ptotal); dfree(ss->ckey); dfree(ss->ckey_s); dfree(ss->skey); dfree(ss->skey_s);
     dfree(ss->cval); dfree(ss->sval); dfree(ss->shist); dfree(ss->spart); dfree(ss->sorder);
-    dfree(ss->counts); dfree(ss->heads); dfree(ss->hlen); dfree(ss->heads2); dfree(ss->hlen2); dfree(ss->hhist); dfree(ss->hpart); dfree(ss->sprof); dfree(ss->cblk); dfree(ss->stats); dfree(ss->stage);
+    dfree(ss->counts); dfree(ss->heads); dfree(ss->hlen); dfree(ss->sprof); dfree(ss->cblk); dfree(ss->stats); dfree(ss->stage);
     dfree(ss->dctl); dfree(ss->stats_bak); ss->dsc.free_all();
     if (ss->h_pin) (void)hipHostFree(ss->h_pin);
     ss->timer.destroy();
@@ -1581,21 +1547,10 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     {
         ScopedStage st(ss->timer, 3);
         // the candidate buffers are free now: pbits-before and repeat counts go there
-        const uint32_t hgrid = (cells + 255) / 256;  // one lane per touched cell at most
-        {   // chains by decreasing length (k_hs_*)
-            const uint32_t hng = (hgrid + kTGrp - 1) / kTGrp;
-            uint32_t *htot = ss->hpart + (size_t)hng * kHsCls;
-            hipLaunchKernelGGL(k_hs_hist, dim3(hgrid), dim3(256), 0, s, ss->heads, ss->hlen, cells, ss->hhist);
-            hipLaunchKernelGGL(k_tscan_part, dim3(1, hng), dim3(256), 0, s, ss->hhist, hgrid, kHsCls, ss->hpart);
-            hipLaunchKernelGGL(k_tscan_mid, dim3(1), dim3(256), 0, s, ss->hpart, hng, kHsCls, htot);
-            hipLaunchKernelGGL(k_tscan_bins, dim3(1), dim3(1024), 0, s, htot, kHsCls, htot + kHsCls);
-            hipLaunchKernelGGL(k_tscan_down, dim3(1, hng), dim3(256), 0, s, ss->hhist, hgrid, kHsCls, ss->hpart, htot);
-            hipLaunchKernelGGL(k_hs_scatter, dim3(hgrid), dim3(256), 0, s, ss->heads, ss->hlen, cells, ss->hhist,
-                               ss->heads2, ss->hlen2);
-        }
         SsApplyArgs a{ss->skey, ss->sval, ss->counts + 1, ss->g, ss->pkt, ss->regs, ss->pbits, ss->values, ss->keys,
-                      reinterpret_cast<double *>(ss->ckey), reinterpret_cast<int64_t *>(ss->skey_s), ss->heads2,
-                      ss->hlen2, cells};
+                      reinterpret_cast<double *>(ss->ckey), reinterpret_cast<int64_t *>(ss->skey_s), ss->heads,
+                      ss->hlen, cells};
+        const uint32_t hgrid = (cells + 255) / 256;  // one lane per touched cell at most
         const uint32_t egrid = (uint32_t)std::min<uint64_t>((ss->ccap + 255) / 256, 4096);
         hipLaunchKernelGGL(k_ss_walk_pbits, dim3(hgrid), dim3(256), 0, s, a);
         hipLaunchKernelGGL(k_ss_sample, dim3(egrid), dim3(256), 0, s, a);
@@ -1854,10 +1809,7 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
         const uint64_t cells = (uint64_t)g.d * g.w;
         if ((rc = dalloc_t(&ss->regs, cells * g.m)) || (rc = dalloc_t(&ss->pbits, cells)) ||
             (rc = dalloc_t(&ss->values, cells)) || (rc = dalloc_t(&ss->keys, cells)) ||
-            (rc = dalloc_t(&ss->heads, cells + 1)) || (rc = dalloc_t(&ss->hlen, cells)) ||
-            (rc = dalloc_t(&ss->heads2, cells + 1)) || (rc = dalloc_t(&ss->hlen2, cells)) ||
-            (rc = dalloc_t(&ss->hhist, ((cells + 255) / 256) * (uint64_t)kHsCls)) ||
-            (rc = dalloc_t(&ss->hpart, (((cells + 255) / 256 + kTGrp - 1) / kTGrp + 2) * (uint64_t)kHsCls)))
+            (rc = dalloc_t(&ss->heads, cells + 1)) || (rc = dalloc_t(&ss->hlen, cells)))
             break;
         uint64_t slots = 1;
         const uint64_t mf = p->max_flows ? p->max_flows : (4ull << 20);
