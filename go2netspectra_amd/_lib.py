@@ -20,6 +20,7 @@ ERRORS = {-1: "GNS_E_ARG", -2: "GNS_E_HIP", -3: "GNS_E_OOM", -4: "GNS_E_FULL", -
 MEM_HOST, MEM_DEVICE = 0, 1
 
 FIELD_IDS = {"SrcIP": 1, "DstIP": 2, "SrcPort": 3, "DstPort": 4, "Protocol": 5}
+FIELD_NAMES = {v: k for k, v in FIELD_IDS.items()}
 FIELD_SIZE = {"SrcIP": 16, "DstIP": 16, "SrcPort": 2, "DstPort": 2, "Protocol": 1}
 
 EXPORTED = [
@@ -39,6 +40,8 @@ EXPORTED = [
     "gns_route_create", "gns_route_destroy", "gns_route_partition",
     "gns_cm_dict_stats", "gns_ss_dict_stats", "gns_ex_dict_stats", "gns_cm_reclaim", "gns_ss_reclaim",
     "gns_cm_insert_compact", "gns_pack_pcap_compact", "gns_compact_headers", "gns_route_partition_async",
+    "gns_route_owner_fields", "gns_route_create_keyed", "gns_route_owner_layout", "gns_route_owner_keys",
+    "gns_device_alloc", "gns_device_free",
 ]
 
 
@@ -61,6 +64,9 @@ class Layout(ct.Structure):
         for i, f in enumerate(fields):
             lay.fields[i] = FIELD_IDS.get(f, 0)  # unknown names contribute 0 bytes (task.go:335)
         return lay
+
+    def names(self):
+        return [FIELD_NAMES.get(int(self.fields[i]), "") for i in range(self.n_fields)]
 
 
 class Tuples(ct.Structure):
@@ -161,6 +167,11 @@ def load() -> ct.CDLL:
         "gns_pack_pcap_compact": ([ct.c_char_p, vp, vp, u64, vp, u64, vp, vp], ct.c_int64),
         "gns_compact_headers": ([vp, vp, u64, vp, vp, u64, vp, i32], i32),
         "gns_route_partition_async": ([vp, vp, vp, u64, vp, vp, vp, vp], i32),
+        "gns_route_owner_fields": ([vp, u32, vp], i32),
+        "gns_route_create_keyed": ([u32, vp, i32, vp], i32),
+        "gns_route_owner_layout": ([vp, vp], i32),
+        "gns_route_owner_keys": ([vp, vp, vp, u32, u64, vp, i32], i32),
+        "gns_device_alloc": ([u64, i32, vp], i32), "gns_device_free": ([vp, i32], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

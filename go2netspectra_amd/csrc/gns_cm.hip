@@ -65,6 +65,8 @@ constexpr size_t kExLdsSmall = 40 * 1024;             // K1 LDS above this: 1024
 #define GNS_CHUNK 16384
 #endif
 constexpr uint32_t kChunk = GNS_CHUNK;              // packets per K1/K3 block
+// K1 packs a block's packet count (low 16 bits) and oversize count (high 16) in one word
+static_assert(kChunk < 65536, "GNS_CHUNK must stay below 2^16 (K1's packed per-block counts)");
 #ifndef GNS_SC_THREADS
 #define GNS_SC_THREADS 512
 #endif
@@ -3261,6 +3263,7 @@ int gns_cm_insert_compact(gns_cm *cm, const uint8_t *rec16, const uint32_t *wire
     in.rec16 = reinterpret_cast<const uint32_t *>(rec16);
     in.sizes = wirelen;
     in.side = reinterpret_cast<const uint32_t *>(side64);
+    in.n_side = side64 ? n_side : 0;
     if (where == GNS_MEM_HOST && n_side) {
         // the side records of the whole call, staged once (escapes index them globally);
         // the batches of the previous call may still read the buffer

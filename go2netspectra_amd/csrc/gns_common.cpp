@@ -162,5 +162,26 @@ void default_seeds(uint32_t *out, uint32_t n) {
 
 }  // namespace gns
 
+extern "C" int gns_device_alloc(uint64_t bytes, int device, void **out) {
+    if (!out) { gns::set_error("null argument"); return GNS_E_ARG; }
+    *out = nullptr;
+    (void)hipGetLastError();
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        gns::set_error("no HIP device available");
+        return GNS_E_NODEV;
+    }
+    if (device < 0 || device >= ndev) { gns::set_error("device %d out of range", device); return GNS_E_ARG; }
+    if (hipSetDevice(device) != hipSuccess) { gns::set_error("hipSetDevice(%d) failed", device); return GNS_E_HIP; }
+    return gns::dalloc(out, bytes);
+}
+
+extern "C" int gns_device_free(void *p, int device) {
+    if (!p) return GNS_OK;
+    if (hipSetDevice(device) != hipSuccess) { gns::set_error("hipSetDevice(%d) failed", device); return GNS_E_HIP; }
+    return hipFree(p) == hipSuccess ? GNS_OK : GNS_E_HIP;
+}
+
 extern "C" const char *gns_last_error(void) { return gns::g_last_error.c_str(); }
 extern "C" const char *gns_version(void) { return "gns-sketch 0.1 (gfx950)"; }

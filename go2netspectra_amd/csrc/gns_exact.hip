@@ -483,7 +483,10 @@ __global__ __launch_bounds__(256) void k_ex_hot_reduce(const ExHotPart *hpart, u
             f.pkts[id] += c;
             f.bytes[id] += by;
             f.last[id] = max(f.last[id], pkt_base + mx + 1);
-            if constexpr (LIST) touch[atomicAdd(tcnt, 1u)] = id;  // designated flows never reach P
+            // H lists the designated flows it updated; P lists a flow only on its first merge
+            // of the batch (last <= pkt_base), and H has already moved `last` past pkt_base
+            // here, so parked packets of a designated flow never add a second entry
+            if constexpr (LIST) touch[atomicAdd(tcnt, 1u)] = id;
         }
     }
 }

@@ -40,6 +40,7 @@ struct InputDesc {
     const uint32_t *sizes;    // per-packet size (wirelen / length / sizes)
     const uint32_t *rec16;    // IN_REC16: n*4 words
     const uint32_t *side;     // IN_REC16: 64-byte records named by kRecSide escapes
+    uint64_t n_side;          // IN_REC16: records in side (an escape at or past it is unsupported)
     uint32_t stride, stride2;
     uint32_t aligned;         // bit0: keys word-loadable, bit1: keys2 word-loadable
 };
@@ -138,7 +139,7 @@ __device__ __forceinline__ int load_tuple(const InputDesc &in, uint64_t p, uint3
         if (cls == kRecTuple) return PARSE_OK;
         if (cls == kRecDrop) return PARSE_DROP;
         int st = PARSE_UNSUPPORTED;
-        if (cls == kRecSide) {
+        if (cls == kRecSide && (uint64_t)r.x < in.n_side) {  // a short or missing side array: unsupported, never read
             uint32_t w[16];
             const uint4 *q = reinterpret_cast<const uint4 *>(in.side + (uint64_t)r.x * 16);
 #pragma unroll

@@ -1637,6 +1637,18 @@ int ss_batch_recover(gns_ss *ss, const InputDesc &d, uint64_t m, bool fresh) {
         GNS_HIP(hipMemcpyAsync(ss->stats_bak, ss->stats, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
                                ss->stream));
         const int rc = ss_batch<KIND>(ss, d, m);
+        if (rc == GNS_E_RANGE && m > kSpCap) {
+            // P4: a cell got more than kSpCap encodes (S3b aborts before any state write).
+            // Undo S1's counters and split: a cell takes at most one encode per record, so
+            // pieces of <= kSpCap records always fit (the RNG is indexed by record, so the
+            // split changes no draw)
+            GNS_HIP(hipMemcpyAsync(ss->stats, ss->stats_bak, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
+                                   ss->stream));
+            ss->n_retry++;
+            const uint64_t h = m > 2ull * kSsChunk ? ((m / 2 + kSsChunk - 1) / kSsChunk) * kSsChunk : m / 2;
+            GNS_TRY(ss_batch_recover<KIND>(ss, d, h, false));
+            return ss_batch_recover<KIND>(ss, ss_advance(d, h), m - h, false);
+        }
         if (rc != GNS_E_FULL) return rc;
         GNS_HIP(hipMemcpyAsync(ss->stats, ss->stats_bak, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
                                ss->stream));

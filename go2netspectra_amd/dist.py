@@ -3,11 +3,26 @@
 Count-Min buckets are (fingerprint, counter) pairs under order-dependent
 majority-vote rules (count_min.go:99-155): they are NOT additive, so summing
 counter rows across GPUs (all-reduce) would not produce the sketch of the
-union stream.  The path therefore shards by flow: packets are routed to the
-GPU that owns their SrcIP (every flow of a source lands on one GPU, SURVEY.md
-§8e), each GPU runs an exact sketch of its sub-stream, queries go to the owner
-shard, and the only collective is the per-window all-gather of heavy-hitter
+union stream.  The path therefore shards by flow: every packet
+goes to the GPU that owns its flow, each GPU runs an exact sketch of its
+sub-stream, queries go to the owner shard (routed_query), and the only
+collective on the data path is the per-window all-gather of heavy-hitter
 candidates (flows are disjoint across shards, so the global list is a union).
+
+Ownership.  A flow key is the task's configured fields (task.go:265-300; any
+non-empty field list is legal, config.go:59).  The owner key is a set of fields
+that EVERY task of the Manager keys on, so that every flow of every task lands
+on one shard (owner_fields):
+  * [SrcIP] when every task's key contains SrcIP (the default tasks and
+    BASELINE configs[3], "sharded by src-IP": every flow of a source shares a GPU);
+  * otherwise the fields the tasks share, in canonical order -- for one task its
+    whole flow key, e.g. ["DstIP"] or ["DstPort", "Protocol"];
+  * no shared field: no owner exists, ValueError.
+owner = mm3(owner key, 0xA5A5A5A5) % world, with every IP slot folded
+(an IPv4-mapped IPv6 slot hashes as the IPv4 slot), so the owner is a function
+of the EncodeFlow bytes and of the exact aggregator's To16 key alike.  The
+device form is gns_route.hip (Router); the functions here are its host
+restatement (CPU tests, host-side splits).
 """
 from __future__ import annotations
 
@@ -16,22 +31,32 @@ import numpy as np
 from .sketch import HeavyCount, HeavyRecord, HeavySize
 
 SHARD_SEED = 0xA5A5A5A5
+CANON_FIELDS = ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"]
+_FIELD_SIZE = {"SrcIP": 16, "DstIP": 16, "SrcPort": 2, "DstPort": 2, "Protocol": 1}
 
 
-def _mm3_16(slots: np.ndarray, seed: int) -> np.ndarray:
-    """MurmurHash3_x86_32 of [n,16] uint8 rows (vectorised; hash.go:13-53)."""
+def _mm3_rows(rows: np.ndarray, seed: int) -> np.ndarray:
+    """MurmurHash3_x86_32 of every row of a [n, K] uint8 array (vectorised; hash.go:13-53)."""
+    rows = np.ascontiguousarray(rows, np.uint8)
+    n, K = rows.shape
     c1, c2 = np.uint32(0xCC9E2D51), np.uint32(0x1B873593)
-    w = np.ascontiguousarray(slots, np.uint8).view("<u4").reshape(-1, 4)
-    h = np.full(w.shape[0], seed, np.uint32)
+    pad = np.zeros((n, (K + 3) // 4 * 4), np.uint8)
+    pad[:, :K] = rows
+    w = pad.view("<u4").reshape(n, pad.shape[1] // 4)
+    h = np.full(n, seed, np.uint32)
     with np.errstate(over="ignore"):
-        for i in range(4):
+        for i in range(K // 4):
             k = w[:, i].astype(np.uint32) * c1
             k = (k << np.uint32(15)) | (k >> np.uint32(17))
             k = k * c2
             h ^= k
             h = (h << np.uint32(13)) | (h >> np.uint32(19))
             h = h * np.uint32(5) + np.uint32(0xE6546B64)
-        h ^= np.uint32(16)
+        if K & 3:
+            k = w[:, K // 4].astype(np.uint32) * c1
+            k = (k << np.uint32(15)) | (k >> np.uint32(17))
+            h ^= k * c2
+        h ^= np.uint32(K)
         h ^= h >> np.uint32(16)
         h = h * np.uint32(0x85EBCA6B)
         h ^= h >> np.uint32(13)
@@ -40,38 +65,135 @@ def _mm3_16(slots: np.ndarray, seed: int) -> np.ndarray:
     return h
 
 
+def _mm3_16(slots: np.ndarray, seed: int) -> np.ndarray:
+    return _mm3_rows(np.asarray(slots, np.uint8).reshape(-1, 16), seed)
+
+
+def canon_slots(a16: np.ndarray) -> np.ndarray:
+    """[n, 16] IP slots with IPv4-mapped IPv6 (::ffff:a.b.c.d) folded to the IPv4 slot."""
+    a = np.array(a16, np.uint8, copy=True).reshape(-1, 16)
+    m = (a[:, :10] == 0).all(axis=1) & (a[:, 10] == 0xFF) & (a[:, 11] == 0xFF)
+    a[m, :4] = a[m, 12:16]
+    a[m, 4:] = 0
+    return a
+
+
+def owner_fields(task_fields) -> list:
+    """The owner key of a set of tasks (gns_route_owner_fields): [SrcIP] when every
+    task keys on SrcIP, else the fields all tasks share in canonical order.
+    task_fields: one field list per task (sketch FlowFields / exact KeyFields)."""
+    sets = [set(f for f in (fs or []) if f in _FIELD_SIZE) for fs in task_fields]
+    if not sets:
+        raise ValueError("no tasks to shard")
+    if all("SrcIP" in fs for fs in sets):
+        return ["SrcIP"]
+    common = [f for f in CANON_FIELDS if all(f in fs for fs in sets)]
+    if not common:
+        raise ValueError(f"the tasks' flow keys {[list(fs or []) for fs in task_fields]} share no field: no shard "
+                         "owns every flow of every task (shard each task set on its own router)")
+    return common
+
+
+def _owner_key(fields: dict, owner: list) -> np.ndarray:
+    """Owner key rows from per-field byte arrays (IP slots folded)."""
+    parts = []
+    for f in owner:
+        a = np.asarray(fields[f], np.uint8)
+        parts.append(canon_slots(a) if f in ("SrcIP", "DstIP") else (a if a.ndim == 2 else a.reshape(-1, 1)))
+    return np.ascontiguousarray(np.concatenate(parts, axis=1))
+
+
+def owner_of_tuples(src16, dst16, sport, dport, proto, world: int, owner=("SrcIP",)) -> np.ndarray:
+    """Owner shard of every packet (PacketInfo fields as EncodeFlow lays them out)."""
+    n = len(np.asarray(src16).reshape(-1, 16))
+    if world <= 1:
+        return np.zeros(n, np.int64)
+    fields = {"SrcIP": src16, "DstIP": dst16,
+              "SrcPort": np.asarray(sport, ">u2").view(np.uint8).reshape(-1, 2) if sport is not None else None,
+              "DstPort": np.asarray(dport, ">u2").view(np.uint8).reshape(-1, 2) if dport is not None else None,
+              "Protocol": np.asarray(proto, np.uint8).reshape(-1, 1) if proto is not None else None}
+    return (_mm3_rows(_owner_key(fields, list(owner)), SHARD_SEED) % np.uint32(world)).astype(np.int64)
+
+
+def owner_of_keys(keys, key_fields, world: int, owner=("SrcIP",)) -> np.ndarray:
+    """Owner shard of flow keys [n, K] laid out as key_fields (a task's EncodeFlow bytes):
+    the shard whose sketch holds the flow (gns_route_owner_keys on the device)."""
+    keys = np.ascontiguousarray(keys, np.uint8)
+    if keys.ndim != 2:
+        keys = keys.reshape(keys.shape[0], -1) if keys.size else np.zeros((len(keys), 0), np.uint8)
+    fields, off = {}, 0
+    for f in key_fields:
+        sz = _FIELD_SIZE.get(f, 0)
+        fields.setdefault(f, keys[:, off:off + sz])
+        off += sz
+    missing = [f for f in owner if f not in fields]
+    if missing:
+        raise ValueError(f"key fields {list(key_fields)} lack owner field(s) {missing}")
+    if world <= 1:
+        return np.zeros(keys.shape[0], np.int64)
+    return (_mm3_rows(_owner_key(fields, list(owner)), SHARD_SEED) % np.uint32(world)).astype(np.int64)
+
+
 def shard_of(src16: np.ndarray, world: int) -> np.ndarray:
-    """Owner GPU of each packet: mm3(SrcIP slot, 0xA5A5A5A5) % world."""
+    """Owner GPU of each packet under the [SrcIP] owner key: mm3(SrcIP slot, 0xA5A5A5A5) % world."""
     if world <= 1:
         return np.zeros(len(src16), np.int64)
-    return (_mm3_16(src16, SHARD_SEED) % np.uint32(world)).astype(np.int64)
+    return (_mm3_16(canon_slots(src16), SHARD_SEED) % np.uint32(world)).astype(np.int64)
 
 
-def split_batch(batch, world: int):
+def split_batch(batch, world: int, owner=("SrcIP",)):
     """Stable split of a host PacketBatch into per-shard batches (order kept)."""
     from .packets import PacketBatch
-    owner = shard_of(np.asarray(batch.src16), world)
+    own = owner_of_tuples(batch.src16, batch.dst16, batch.sport, batch.dport, batch.proto, world, owner)
     out = []
     for g in range(world):
-        m = owner == g
+        m = own == g
         out.append(PacketBatch(batch.src16[m], batch.dst16[m], batch.sport[m], batch.dport[m],
-                               batch.proto[m], batch.length[m]))
+                               batch.proto[m], batch.length[m],
+                               None if batch.ipver is None else batch.ipver[m],
+                               None if batch.ts is None else batch.ts[m]))
     return out
 
 
 class Router:
     """Device-side stable partition of header records by owner shard
-    (gns_route_partition; the device form of shard_of / split_batch)."""
+    (gns_route_partition; the device form of owner_of_tuples / split_batch) and
+    the owner of query keys (gns_route_owner_keys)."""
 
-    def __init__(self, nshards: int, device: int = 0):
+    def __init__(self, nshards: int, device: int = 0, owner=("SrcIP",)):
         import ctypes as ct
         from . import _lib
         self._L = _lib.load()
         self.nshards = int(nshards)
         self.device = device
+        self.owner = list(owner)
         h = ct.c_void_p()
-        _lib.check(self._L.gns_route_create(self.nshards, device, ct.byref(h)))
+        lay = _lib.Layout.of(self.owner)
+        _lib.check(self._L.gns_route_create_keyed(self.nshards, ct.byref(lay), device, ct.byref(h)))
         self._h = h
+
+    def owner_of_keys(self, keys, key_fields):
+        """Owner shard of flow keys [n, K] laid out as key_fields (host numpy -> numpy int64;
+        a device tensor -> a device int32 tensor)."""
+        import ctypes as ct
+        from . import _lib
+        lay = _lib.Layout.of(list(key_fields))
+        if hasattr(keys, "data_ptr") and getattr(keys, "is_cuda", False):
+            import torch
+            n = int(keys.shape[0])
+            keys = keys.reshape(n, -1).contiguous()
+            out = torch.empty((n,), dtype=torch.int32, device=keys.device)
+            _lib.device_ready(keys)
+            _lib.check(self._L.gns_route_owner_keys(self._h, ct.byref(lay), keys.data_ptr(), int(keys.shape[1]) if n else 1,
+                                                    n, out.data_ptr(), _lib.MEM_DEVICE))
+            return out
+        keys = np.ascontiguousarray(keys, np.uint8)
+        n = keys.shape[0]
+        keys = keys.reshape(n, -1) if n else np.zeros((0, max(_lib.layout_bytes(key_fields), 1)), np.uint8)
+        out = np.zeros(n, np.uint32)
+        _lib.check(self._L.gns_route_owner_keys(self._h, ct.byref(lay), keys.ctypes.data, keys.shape[1], n,
+                                                out.ctypes.data, _lib.MEM_HOST))
+        return out.astype(np.int64)
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -167,13 +289,59 @@ def route_exchange(router: "Router", hdr, wirelen, world: int):
     return exchange_runs(oh, ow, counts, world)
 
 
-def stable_split_records(hdr: np.ndarray, wirelen: np.ndarray, world: int, src16: np.ndarray):
-    """Host restatement of Router.partition for records whose SrcIP slots are known
-    (tests / CPU rehearsal): runs shard by shard in stream order, and their lengths."""
-    owner = shard_of(src16, world)
-    order = np.argsort(owner, kind="stable")
-    counts = np.bincount(owner, minlength=world).astype(np.uint64)
+def stable_split_records(hdr: np.ndarray, wirelen: np.ndarray, world: int, src16: np.ndarray = None, own=None):
+    """Host restatement of Router.partition for records whose owners are known
+    (tests / CPU rehearsal): runs shard by shard in stream order, and their lengths.
+    own: owner shard per record (owner_of_tuples); default: the SrcIP owner of src16."""
+    if own is None:
+        own = shard_of(src16, world)
+    order = np.argsort(own, kind="stable")
+    counts = np.bincount(own, minlength=world).astype(np.uint64)
     return hdr[order], wirelen[order], counts
+
+
+def _coll_device():
+    import torch
+    import torch.distributed as dist
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def routed_query(query_many, keys, key_fields, world: int, owner=("SrcIP",), router: "Router" = None):
+    """Owner-routed batched Query ("queries are routed to the owner
+    shard"; Sketch.Query count_min.go:160-174 / super_spread.go:238-249 answered
+    by the shard whose sketch holds the flow).  Collective: every rank calls it
+    with its own batch of flow keys [n, K] (laid out as key_fields, n may differ
+    or be 0).  Keys go to their owners in one all-to-all, each owner answers the
+    keys it received with its local query_many (CountMin / SuperSpread / exact
+    .query_many), and the answers come back in a second all-to-all, in the
+    caller's order.  router: a Router computes the owners on the GPU; without
+    one, the host restatement owner_of_keys does."""
+    import torch
+    import torch.distributed as dist
+    keys = np.ascontiguousarray(keys, np.uint8)
+    n = keys.shape[0]
+    K = max(sum(_FIELD_SIZE.get(f, 0) for f in key_fields), 1)
+    keys = keys.reshape(n, -1) if n else np.zeros((0, K), np.uint8)
+    own = router.owner_of_keys(keys, key_fields) if router is not None else owner_of_keys(keys, key_fields, world, owner)
+    order = np.argsort(own, kind="stable")
+    sc = np.bincount(own, minlength=world).astype(np.int64)
+    dev = _coll_device()
+    send = torch.from_numpy(sc).to(dev)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send)
+    rc = [int(x) for x in recv.cpu().tolist()]
+    scl = [int(x) for x in sc]
+    out_keys = torch.from_numpy(np.ascontiguousarray(keys[order])).to(dev)
+    in_keys = torch.empty((sum(rc), keys.shape[1]), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(in_keys, out_keys, output_split_sizes=rc, input_split_sizes=scl)
+    mine = in_keys.cpu().numpy()
+    ans = np.asarray(query_many(mine) if len(mine) else np.zeros(0, np.uint64), np.uint64)
+    back = torch.empty((n,), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(back, torch.from_numpy(np.ascontiguousarray(ans).view(np.int64)).to(dev),
+                           output_split_sizes=scl, input_split_sizes=rc)
+    out = np.empty(n, np.uint64)
+    out[order] = back.cpu().numpy().view(np.uint64)
+    return out
 
 
 def _pack(items, K: int) -> np.ndarray:

@@ -62,6 +62,14 @@ RegisterAggregator = register_aggregator
 Create = create
 
 
+def key_fields(task) -> List[str]:
+    """The fields a task keys its flows on: FlowFields (sketch, task.go:265-300) or
+    KeyFields (exact, exact/task.go:330-366)."""
+    if hasattr(task, "flow_fields"):
+        return list(task.flow_fields)
+    return list(task.agg.key_fields)
+
+
 class Manager:
     """Batch-submission replacement of manager.Manager."""
 
@@ -74,6 +82,13 @@ class Manager:
 
     def start(self) -> None:
         self.started = True
+
+    def owner_fields(self) -> List[str]:
+        """The owner key for sharding this Manager's tasks over GPUs (dist.owner_fields):
+        every task sees every packet (manager.go:232-244), so one owner must hold
+        each flow of every task.  Raises ValueError when the tasks share no key field."""
+        from .dist import owner_fields
+        return owner_fields([key_fields(t) for t in self.tasks()])
 
     def process(self, batch) -> None:
         """processPacket (manager.go:232-244) for a whole batch: fan out to every task."""

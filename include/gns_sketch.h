@@ -232,9 +232,10 @@ typedef struct gns_ss_params {
  * can be named by a key, a query or a heavy hitter); it is reclaimed and grows
  * like Count-Min's (see the rules above), so inserts do not fail on it.
  * Deviations (GNS_E_ARG at create): depth <= 8, m <= 256, size <= 8, merged
- * key <= 74 bytes, depth * width <= 2^25 cells.  An insert returns GNS_E_RANGE,
- * with the sketch unchanged, if one cell gets more than 8192 encodes in one
- * device batch (m = 256 only); a smaller batch_packets avoids it. */
+ * key <= 74 bytes, depth * width <= 2^25 cells.  A device batch in which one
+ * cell gets more than 8192 encodes (possible with m = 256 only) is undone before
+ * any state write and re-run in halves (a cell takes at most one encode per
+ * record), so inserts do not fail on it. */
 int gns_ss_create(const gns_ss_params *p, gns_ss **out);
 int gns_ss_destroy(gns_ss *ss);
 int gns_ss_insert_keys(gns_ss *ss, const uint8_t *flows, uint32_t fstride, const uint8_t *elems,
@@ -337,26 +338,57 @@ int gns_thrift_decode(const uint8_t *buf, uint64_t buf_bytes, const uint64_t *of
 /* ------------------------------------------------------------------ */
 /* Flow routing for the multi-GPU path (BASELINE configs[3]) */
 /* ------------------------------------------------------------------ */
-/* Replaces the per-packet host split of the sharded deployment (a packet is
- * owned by GPU mm3(SrcIP slot, 0xA5A5A5A5) % nshards, so every flow of a source
- * lands on one GPU; go2netspectra_amd/dist.py shard_of is the host form).
- * gns_route_partition reorders n DEVICE-resident 64-byte records (+ wire
+/* Replaces the per-packet host split of the sharded deployment (SURVEY §8e:
+ * "sharded by src-IP ... use the full key when SrcIP is not in the key";
+ * go2netspectra_amd/dist.py owner_fields / owner_of_* are the host form).
+ *
+ * Every flow of every task must be owned by ONE shard, so that each shard's
+ * sketch is exact for its sub-stream.  A router hashes an OWNER KEY made of
+ * fields that every task's flow key contains (a flow key is the configured
+ * fields, task.go:265-300; any non-empty field list is legal, config.go:59):
+ * shard = mm3(owner key, 0xA5A5A5A5) % nshards.  IP slots enter the owner key
+ * with an IPv4-mapped IPv6 slot folded to its IPv4 slot, so the owner is a
+ * function of the EncodeFlow bytes and of the exact aggregator's To16 key alike.
+ *
+ * gns_route_owner_fields: the owner key of a set of tasks (a Manager's tasks,
+ * manager.go:139-159 runs them on every packet): [SrcIP] when every task's key
+ * holds SrcIP (configs[3]), else the fields common to all tasks in canonical
+ * order (SrcIP, DstIP, SrcPort, DstPort, Protocol) -- for one task its whole
+ * flow key.  GNS_E_ARG (with a message) when the tasks share no field: no
+ * single owner exists for such a set.  Host logic only (no device needed). */
+int gns_route_owner_fields(const gns_layout *tasks, uint32_t n_tasks, gns_layout *owner);
+typedef struct gns_route gns_route;
+/* nshards <= 64; owner = gns_route_owner_fields' result (or any non-empty field set) */
+int gns_route_create_keyed(uint32_t nshards, const gns_layout *owner, int device, gns_route **out);
+/* = gns_route_create_keyed with owner [SrcIP] */
+int gns_route_create(uint32_t nshards, int device, gns_route **out);
+int gns_route_destroy(gns_route *r);
+int gns_route_owner_layout(gns_route *r, gns_layout *owner);
+/* gns_route_partition reorders n DEVICE-resident 64-byte records (+ wire
  * lengths) into nshards runs, shard by shard, keeping packet order inside each
  * run (stable); counts[g] (host) = length of run g.  Records the parser drops
  * or does not support go to shard 0.  The call returns after the device work.
  * An all-to-all of run g to rank g, received runs concatenated in source-rank
  * order, delivers to every GPU exactly its stable filter of the stream. */
-typedef struct gns_route gns_route;
-int gns_route_create(uint32_t nshards, int device, gns_route **out);  /* nshards <= 64 */
-int gns_route_destroy(gns_route *r);
 int gns_route_partition(gns_route *r, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
                         uint8_t *out_hdr, uint32_t *out_wirelen, uint64_t *counts);
 /* The same partition queued on `stream` (a hipStream_t; NULL = the router's own)
  * without waiting: counts_dev[g] (DEVICE int64) = length of run g once the stream
  * reaches it -- the all-to-all's split sizes stay on the device until the one
- * host read the exchange needs (dist.exchange_runs). */
+ * host read the exchange needs (dist.exchange_runs).  Partitions of one router
+ * are ordered after each other whatever streams they are queued on (they share
+ * its scratch). */
 int gns_route_partition_async(gns_route *r, const uint8_t *hdr, const uint32_t *wirelen, uint64_t n,
                               uint8_t *out_hdr, uint32_t *out_wirelen, int64_t *counts_dev, void *stream);
+/* Owner-routed queries (SURVEY §8e "queries are routed to the owner shard";
+ * Sketch.Query, count_min.go:160-174 / super_spread.go:238-249, answers from the
+ * shard that holds the flow): owner[i] = the shard owning flow key i, keys laid
+ * out as key_layout (the querying task's FlowFields; it must contain every owner
+ * field, else GNS_E_ARG).  keys and owner both in `where`; returns after the
+ * device work.  dist.routed_query / the Go Router's QueryRouted exchange the
+ * keys by owner, query each shard's handle and return the answers in order. */
+int gns_route_owner_keys(gns_route *r, const gns_layout *key_layout, const uint8_t *keys, uint32_t stride,
+                         uint64_t n, uint32_t *owner, gns_mem where);
 
 /* ------------------------------------------------------------------ */
 /* Exact aggregator (internal/engine/impl/exact/task.go)               */
@@ -402,6 +434,12 @@ int gns_ex_dict_stats(gns_ex *ex, uint64_t out[8]);
 int gns_ex_set_timing(gns_ex *ex, int on);
 /* stages: 0 extract, 1 resolve, 2 aggregate, 3 timestamps, 5 total */
 int gns_ex_stage_times(gns_ex *ex, double ms[8], uint64_t launches[8], int reset);
+
+/* Device buffers for callers without a device allocator of their own (the cgo
+ * binding's ThriftDecoder: gns_thrift_decode writes device records that
+ * gns_*_insert_headers then reads with GNS_MEM_DEVICE). */
+int gns_device_alloc(uint64_t bytes, int device, void **out);
+int gns_device_free(void *p, int device);
 
 const char *gns_last_error(void);
 const char *gns_version(void);

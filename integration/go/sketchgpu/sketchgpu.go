@@ -25,7 +25,9 @@ import "C"
 
 import (
 	"errors"
+	"fmt"
 	"log"
+	"sync"
 	"unsafe"
 
 	"Go2NetSpectra/internal/engine/impl/sketch/statistic"
@@ -183,17 +185,51 @@ func (c *CountMin) DictStats() (out [8]uint64, err error) {
 	return
 }
 
-// Router splits device-resident records by owning GPU (multi-GPU deployment:
-// flow-hash sharding by SrcIP, stable per shard); exchange the runs with an
-// all-to-all (RCCL) and insert each received run in source-rank order.
-type Router struct{ r *C.gns_route }
-
-func NewRouter(nshards uint32, device int) (*Router, error) {
-	var r *C.gns_route
-	if rc := C.gns_route_create(C.uint32_t(nshards), C.int(device), &r); rc != C.GNS_OK {
-		return nil, lastErr(rc)
+func layoutOf(fields []string) (l C.gns_layout) {
+	l.n_fields = C.uint32_t(len(fields))
+	for i, f := range fields {
+		l.fields[i] = fieldIDs[f]
 	}
-	return &Router{r: r}, nil
+	return
+}
+
+// Router shards a node's traffic over its GPUs by flow (SURVEY §8e): records are
+// split on the device by owning GPU (stable per shard; exchange the runs with an
+// all-to-all and insert each received run in source-rank order), and queries are
+// answered by the shard that owns the flow.  The owner key is the fields every
+// task keys on (gns_route_owner_fields): [SrcIP] when each task's flow key holds
+// SrcIP, otherwise the fields the tasks share -- for one task its whole flow key
+// (a flow key without SrcIP is legal, config.go:59).
+type Router struct {
+	r       *C.gns_route
+	nshards int
+}
+
+// NewRouter shards by SrcIP (every task keys on SrcIP).
+func NewRouter(nshards uint32, device int) (*Router, error) {
+	return NewKeyedRouter(nshards, [][]string{{"SrcIP"}}, device)
+}
+
+// NewKeyedRouter derives the owner key from the tasks' flow fields (one slice per
+// task: SketchTaskDef.FlowFields / exact KeyFields); it fails when the tasks share
+// no field, since no GPU could then own every flow of every task.
+func NewKeyedRouter(nshards uint32, taskFields [][]string, device int) (*Router, error) {
+	if len(taskFields) == 0 {
+		return nil, errors.New("sketchgpu: no tasks to shard")
+	}
+	lays := make([]C.gns_layout, len(taskFields))
+	for i, f := range taskFields {
+		lays[i] = layoutOf(f)
+	}
+	var owner C.gns_layout
+	if err := lastErr(C.gns_route_owner_fields(&lays[0], C.uint32_t(len(lays)), &owner)); err != nil {
+		return nil, err
+	}
+	var r *C.gns_route
+	if err := lastErr(C.gns_route_create_keyed(C.uint32_t(nshards), &owner, C.int(device), &r)); err != nil {
+		return nil, err
+	}
+	return &Router{r: r, nshards: int(nshards)}, nil
 }
 
 // Partition: hdr/wirelen/outHdr/outWirelen are device pointers (n records);
@@ -201,6 +237,77 @@ func NewRouter(nshards uint32, device int) (*Router, error) {
 func (rt *Router) Partition(hdr, wirelen, outHdr, outWirelen unsafe.Pointer, n uint64, counts []uint64) error {
 	return lastErr(C.gns_route_partition(rt.r, (*C.uint8_t)(hdr), (*C.uint32_t)(wirelen), C.uint64_t(n),
 		(*C.uint8_t)(outHdr), (*C.uint32_t)(outWirelen), (*C.uint64_t)(unsafe.Pointer(&counts[0]))))
+}
+
+// Owners returns the shard owning each of the len(keys)/stride flow keys (laid out as
+// keyFields, the querying task's FlowFields; they must contain every owner field).
+func (rt *Router) Owners(keyFields []string, keys []byte, stride uint32) ([]uint32, error) {
+	if stride == 0 {
+		return nil, errors.New("sketchgpu: zero key stride")
+	}
+	n := len(keys) / int(stride)
+	own := make([]uint32, n+1)
+	if n == 0 {
+		return own[:0], nil
+	}
+	lay := layoutOf(keyFields)
+	err := lastErr(C.gns_route_owner_keys(rt.r, &lay, (*C.uint8_t)(unsafe.Pointer(&keys[0])), C.uint32_t(stride),
+		C.uint64_t(n), (*C.uint32_t)(unsafe.Pointer(&own[0])), C.GNS_MEM_HOST))
+	return own[:n], err
+}
+
+// BatchQuerier is a shard's batched Query (CountMin, SuperSpread, Exact).
+type BatchQuerier interface {
+	QueryBatch(keys []byte, stride uint32) ([]uint64, error)
+}
+
+// QueryRouted answers Query(flow) (count_min.go:160-174, super_spread.go:238-249) for
+// len(keys)/stride flow keys, each from the shard owning its flow: shards[g] is the
+// handle on GPU g (one process driving the node's GPUs).  The shards answer
+// concurrently, every key once; the answers come back in key order.
+func (rt *Router) QueryRouted(shards []BatchQuerier, keyFields []string, keys []byte, stride uint32) ([]uint64, error) {
+	if len(shards) != rt.nshards {
+		return nil, fmt.Errorf("sketchgpu: %d shard handles for a %d-shard router", len(shards), rt.nshards)
+	}
+	own, err := rt.Owners(keyFields, keys, stride)
+	if err != nil {
+		return nil, err
+	}
+	per := make([][]int, rt.nshards)
+	for i, g := range own {
+		per[g] = append(per[g], i)
+	}
+	out := make([]uint64, len(own))
+	errs := make([]error, rt.nshards)
+	var wg sync.WaitGroup
+	for g, idx := range per {
+		if len(idx) == 0 {
+			continue
+		}
+		wg.Add(1)
+		go func(g int, idx []int) {
+			defer wg.Done()
+			buf := make([]byte, 0, len(idx)*int(stride))
+			for _, i := range idx {
+				buf = append(buf, keys[i*int(stride):(i+1)*int(stride)]...)
+			}
+			ans, err := shards[g].QueryBatch(buf, stride)
+			if err != nil {
+				errs[g] = err
+				return
+			}
+			for j, i := range idx {
+				out[i] = ans[j]
+			}
+		}(g, idx)
+	}
+	wg.Wait()
+	for _, e := range errs {
+		if e != nil {
+			return nil, e
+		}
+	}
+	return out, nil
 }
 
 func (rt *Router) Close() { C.gns_route_destroy(rt.r) }
@@ -215,6 +322,18 @@ func (c *CountMin) Query(flow []byte) uint64 {
 		return 0
 	}
 	return uint64(out)
+}
+
+// QueryBatch: Query for len(keys)/stride flows in one device call (count<<32 | size).
+func (c *CountMin) QueryBatch(keys []byte, stride uint32) ([]uint64, error) {
+	n := len(keys) / int(stride)
+	out := make([]uint64, n+1)
+	if n == 0 {
+		return out[:0], nil
+	}
+	err := lastErr(C.gns_cm_query(c.h, (*C.uint8_t)(unsafe.Pointer(&keys[0])), C.uint32_t(stride), C.uint64_t(n),
+		(*C.uint64_t)(unsafe.Pointer(&out[0]))))
+	return out[:n], err
 }
 
 // HeavyHitters implements statistic.Sketch (count_min.go:178-247).
@@ -401,6 +520,18 @@ func (s *SuperSpread) Query(flow []byte) uint64 {
 	return uint64(out)
 }
 
+// QueryBatch: Query for len(keys)/stride flows in one device call.
+func (s *SuperSpread) QueryBatch(keys []byte, stride uint32) ([]uint64, error) {
+	n := len(keys) / int(stride)
+	out := make([]uint64, n+1)
+	if n == 0 {
+		return out[:0], nil
+	}
+	err := lastErr(C.gns_ss_query(s.h, (*C.uint8_t)(unsafe.Pointer(&keys[0])), C.uint32_t(stride), C.uint64_t(n),
+		(*C.uint64_t)(unsafe.Pointer(&out[0]))))
+	return out[:n], err
+}
+
 // HeavyHitters implements statistic.Sketch (super_spread.go:254-294): Size is nil.
 func (s *SuperSpread) HeavyHitters() statistic.HeavyRecord {
 	K := s.flowSize
@@ -488,6 +619,18 @@ func (e *Exact) Query(flow []byte) uint64 {
 	return uint64(out)
 }
 
+// QueryBatch: Query for len(keys)/stride flows in one device call (PacketCount<<32 | ByteCount).
+func (e *Exact) QueryBatch(keys []byte, stride uint32) ([]uint64, error) {
+	n := len(keys) / int(stride)
+	out := make([]uint64, n+1)
+	if n == 0 {
+		return out[:0], nil
+	}
+	err := lastErr(C.gns_ex_query(e.h, (*C.uint8_t)(unsafe.Pointer(&keys[0])), C.uint32_t(stride), C.uint64_t(n),
+		(*C.uint64_t)(unsafe.Pointer(&out[0]))))
+	return out[:n], err
+}
+
 // Flows returns the snapshot arrays; the task rebuilds statistic.Flow (Key string via
 // net.IP(key[i:i+16]).String(), Fields, StartTime = time.Unix(0, start[i]), ...).
 func (e *Exact) Flows() (keys []byte, start, end []int64, pkts, bytes []uint64, err error) {
@@ -511,3 +654,96 @@ func (e *Exact) Reset() { C.gns_ex_reset(e.h) }
 
 // Close releases the device state.
 func (e *Exact) Close() { C.gns_ex_destroy(e.h) }
+
+// ThriftDecoder holds the device buffers one batch of NATS messages decodes into
+// (ns-engine's live path: stream_aggregator.go:85 decodes one PacketInfo message
+// at a time with probe.UnmarshalPacketInfo, packetcodec.go:97-108; here a whole
+// batch is decoded on the GPU into the engine's pre-parsed records).
+type ThriftDecoder struct {
+	rec, wirelen, ts unsafe.Pointer
+	capacity         int
+	device           int
+}
+
+// NewThriftDecoder allocates room for `capacity` messages per batch on `device`.
+func NewThriftDecoder(capacity, device int) (*ThriftDecoder, error) {
+	d := &ThriftDecoder{capacity: capacity, device: device}
+	for _, b := range []struct {
+		p     *unsafe.Pointer
+		bytes int
+	}{{&d.rec, 64 * capacity}, {&d.wirelen, 4 * capacity}, {&d.ts, 8 * capacity}} {
+		if err := lastErr(C.gns_device_alloc(C.uint64_t(b.bytes), C.int(device), b.p)); err != nil {
+			d.Close()
+			return nil, err
+		}
+	}
+	return d, nil
+}
+
+// decode turns msgs (back to back; offs[i] = start of message i, offs[n] = len(msgs))
+// into device records; bad counts the messages the reference would reject.
+func (d *ThriftDecoder) decode(msgs []byte, offs []uint64) (n int, bad uint64, err error) {
+	n = len(offs) - 1
+	if n <= 0 {
+		return 0, 0, nil
+	}
+	if n > d.capacity {
+		return 0, 0, fmt.Errorf("sketchgpu: %d messages for a %d-message decoder", n, d.capacity)
+	}
+	var nb C.uint64_t
+	err = lastErr(C.gns_thrift_decode((*C.uint8_t)(unsafe.Pointer(&msgs[0])), C.uint64_t(len(msgs)),
+		(*C.uint64_t)(unsafe.Pointer(&offs[0])), C.uint64_t(n), (*C.uint8_t)(d.rec), (*C.uint32_t)(d.wirelen),
+		(*C.int64_t)(d.ts), &nb, C.GNS_MEM_HOST, C.int(d.device)))
+	return n, uint64(nb), err
+}
+
+// Close frees the device buffers.
+func (d *ThriftDecoder) Close() {
+	for _, p := range []unsafe.Pointer{d.rec, d.wirelen, d.ts} {
+		if p != nil {
+			C.gns_device_free(p, C.int(d.device))
+		}
+	}
+	d.rec, d.wirelen, d.ts = nil, nil, nil
+}
+
+// InsertThriftBatch decodes a batch of PacketInfo messages on the GPU and inserts
+// the packets (ProcessPacket for each message, task.go:156-169).  It returns once
+// the decoder's buffers are free again.
+func (c *CountMin) InsertThriftBatch(d *ThriftDecoder, msgs []byte, offs []uint64) (bad uint64, err error) {
+	n, bad, err := d.decode(msgs, offs)
+	if err != nil || n == 0 {
+		return bad, err
+	}
+	if err = lastErr(C.gns_cm_insert_headers(c.h, (*C.uint8_t)(d.rec), (*C.uint32_t)(d.wirelen), C.uint64_t(n),
+		C.GNS_MEM_DEVICE)); err != nil {
+		return bad, err
+	}
+	return bad, lastErr(C.gns_cm_flush(c.h))
+}
+
+// InsertThriftBatch for SuperSpread (see CountMin.InsertThriftBatch).
+func (s *SuperSpread) InsertThriftBatch(d *ThriftDecoder, msgs []byte, offs []uint64) (bad uint64, err error) {
+	n, bad, err := d.decode(msgs, offs)
+	if err != nil || n == 0 {
+		return bad, err
+	}
+	if err = lastErr(C.gns_ss_insert_headers(s.h, (*C.uint8_t)(d.rec), (*C.uint32_t)(d.wirelen), C.uint64_t(n),
+		C.GNS_MEM_DEVICE)); err != nil {
+		return bad, err
+	}
+	return bad, lastErr(C.gns_ss_flush(s.h))
+}
+
+// InsertThriftBatch for the exact aggregator (the messages' TimestampUnixNano kept).
+func (e *Exact) InsertThriftBatch(d *ThriftDecoder, msgs []byte, offs []uint64) (bad uint64, err error) {
+	n, bad, err := d.decode(msgs, offs)
+	if err != nil || n == 0 {
+		return bad, err
+	}
+	if err = lastErr(C.gns_ex_insert_headers(e.h, (*C.uint8_t)(d.rec), (*C.uint32_t)(d.wirelen), (*C.int64_t)(d.ts),
+		C.uint64_t(n), C.GNS_MEM_DEVICE)); err != nil {
+		return bad, err
+	}
+	return bad, lastErr(C.gns_ex_flush(e.h))
+}

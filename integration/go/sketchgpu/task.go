@@ -1,23 +1,33 @@
-package sketchgpu
-
 // GPUTask: the model.Task (internal/model/task.go:6-15) a maintainer registers
 // next to the reference's "sketch" aggregator.  It has the reference sketch.Task's
 // surface (internal/engine/impl/sketch/task.go:91-243) -- same SketchTaskDef keys,
 // same Snapshot payload (statistic.HeavyRecord), same Query / Fields /
 // DecodeFlowFunc / AlerterMsg -- but ProcessPacket appends the packet to a host
-// batch instead of inserting it: every `BatchPackets` packets (and before every
-// Snapshot, Query and Reset) the batch goes to the GPU in one
-// gns_{cm,ss}_insert_tuples call, where EncodeFlow (task.go:265-300) and the d
-// seeded MurmurHash3 updates run.  The Manager's workers (manager.go:218-244)
-// keep calling ProcessPacket concurrently; the batch is filled under a mutex, so
-// the stream order the GPU applies is the order in which packets reached it (the
-// reference's workers race on the buckets, SURVEY.md §0.2).
+// batch instead of inserting it.  The Manager's workers (manager.go:218-244) keep
+// calling ProcessPacket concurrently, as they call the reference's lock-free
+// ProcessPacket (task.go:156-169):
+//   - under the task's mutex a worker only appends to the current batch and, when
+//     it is full, hands it to the submitter (a channel send) and takes an empty
+//     one from the free list -- no device work is done under the lock;
+//   - ONE submitter goroutine per task owns the device handle: it inserts the full
+//     batches in the order they were handed over (gns_{cm,ss}_insert_tuples, where
+//     EncodeFlow, task.go:265-300, and the d seeded MurmurHash3 updates run), so
+//     the stream the GPU applies is the order in which packets reached the batch
+//     (the reference's workers race on the buckets instead, SURVEY.md §0.2);
+//   - Query / Snapshot / Reset hand over the pending packets, then run on the
+//     submitter behind every batch handed over before them, and wait for it: they
+//     see every packet processed before the call, and the handle is only ever
+//     used from one goroutine (include/gns_sketch.h rules).
+// The workers stall only when the GPU is `Inflight` batches behind.
 //
 // Registration (the "sketch_gpu" aggregator type, configs' aggregator.types):
 //
 //	import _ "Go2NetSpectra/integration/go/sketchgpu"   // in manager.go, beside the sketch import
 //
-// Not compiled in the build container (no Go toolchain there).
+// Not compiled in the build container (no Go toolchain there); tests/test_gputask_replay_gpu.py
+// replays this file's call sequence through the C ABI (integration/c/gputask_replay.c).
+
+toolchain there).
 
 import (
 	"fmt"
@@ -35,6 +45,10 @@ import (
 
 // BatchPackets is the host batch handed to the GPU in one insert.
 var BatchPackets = 1 << 16
+
+// Inflight is the number of full batches that may wait for the submitter before
+// ProcessPacket blocks (host memory: Inflight+2 batches per task).
+var Inflight = 2
 
 // Device is the HIP device ordinal the tasks of this process use.
 var Device = 0
@@ -90,6 +104,32 @@ func fieldBytes(fields []string) uint32 {
 	return n
 }
 
+// pktBatch is one host batch of PacketInfo as SoA (the layout gns_tuples reads).
+type pktBatch struct {
+	src16, dst16 []byte
+	sport, dport []uint16
+	proto        []uint8
+	length       []uint32
+}
+
+func newPktBatch(b int) *pktBatch {
+	return &pktBatch{src16: make([]byte, 0, 16*b), dst16: make([]byte, 0, 16*b), sport: make([]uint16, 0, b),
+		dport: make([]uint16, 0, b), proto: make([]uint8, 0, b), length: make([]uint32, 0, b)}
+}
+
+func (b *pktBatch) clear() {
+	b.src16, b.dst16 = b.src16[:0], b.dst16[:0]
+	b.sport, b.dport, b.proto, b.length = b.sport[:0], b.dport[:0], b.proto[:0], b.length[:0]
+}
+
+// job is one unit of the submitter's queue: a batch to insert, or a call on the
+// handle (fn) whose caller waits on done.
+type job struct {
+	b    *pktBatch
+	fn   func()
+	done chan struct{}
+}
+
 // GPUTask implements model.Task on a GPU Count-Min (skt_type 0) or SuperSpread (1).
 type GPUTask struct {
 	name       string
@@ -98,14 +138,14 @@ type GPUTask struct {
 	cm         *CountMin
 	ss         *SuperSpread
 
-	mu     sync.Mutex
-	src16  []byte
-	dst16  []byte
-	sport  []uint16
-	dport  []uint16
-	proto  []uint8
-	length []uint32
-	err    error // first failed insert of the period
+	mu   sync.Mutex // guards cur and the order of sends on work
+	cur  *pktBatch
+	work chan job       // to the submitter, in hand-over order
+	free chan *pktBatch // empty batches back from the submitter
+	quit chan struct{}  // closed by Close after the last job
+
+	errMu sync.Mutex
+	err   error // first failed insert of the period
 }
 
 // NewGPUTask replaces sketch.New (task.go:106-138).  Row seeds: NewCountMin's
@@ -127,70 +167,110 @@ func NewGPUTask(cfg config.SketchTaskDef) (*GPUTask, error) {
 	if err != nil {
 		return nil, err
 	}
-	t.reserve()
+	t.cur = newPktBatch(BatchPackets)
+	t.work = make(chan job, Inflight)
+	t.free = make(chan *pktBatch, Inflight+1)
+	for i := 0; i < Inflight+1; i++ {
+		t.free <- newPktBatch(BatchPackets)
+	}
+	t.quit = make(chan struct{})
+	go t.submitter()
 	return t, nil
 }
 
-func (t *GPUTask) reserve() {
-	b := BatchPackets
-	t.src16, t.dst16 = make([]byte, 0, 16*b), make([]byte, 0, 16*b)
-	t.sport, t.dport = make([]uint16, 0, b), make([]uint16, 0, b)
-	t.proto, t.length = make([]uint8, 0, b), make([]uint32, 0, b)
+// submitter owns the device handle: batches and calls in hand-over order.
+func (t *GPUTask) submitter() {
+	defer close(t.quit)
+	for j := range t.work {
+		if j.b != nil {
+			t.insert(j.b)
+			j.b.clear()
+			t.free <- j.b
+		}
+		if j.fn != nil {
+			j.fn()
+		}
+		if j.done != nil {
+			close(j.done)
+		}
+	}
+}
+
+// insert submits one batch.  The reference logs a packet it cannot insert and
+// goes on (task.go:162-166); a failed batch is logged the same way and kept for Err().
+func (t *GPUTask) insert(b *pktBatch) {
+	var err error
+	if t.cm != nil {
+		err = t.cm.InsertTuples(b.src16, b.dst16, b.sport, b.dport, b.proto, b.length)
+	} else {
+		err = t.ss.InsertTuples(b.src16, b.dst16, b.sport, b.dport, b.proto, b.length)
+	}
+	if err != nil {
+		t.errMu.Lock()
+		if t.err == nil {
+			t.err = err
+		}
+		t.errMu.Unlock()
+		log.Printf("Error inserting a batch for task '%s': %v", t.name, err)
+	}
 }
 
 // ProcessPacket (task.go:156-169) for the GPU: the PacketInfo joins the batch;
-// EncodeFlow and the sketch update run on the device at the next flush.
+// EncodeFlow and the sketch update run on the device when the batch is submitted.
 func (t *GPUTask) ProcessPacket(p *model.PacketInfo) {
 	var s, d [16]byte
 	copy(s[:], p.FiveTuple.SrcIP) // 4-byte IPv4 left-aligned, zero padded (task.go:281-286)
 	copy(d[:], p.FiveTuple.DstIP)
 	t.mu.Lock()
-	t.src16 = append(t.src16, s[:]...)
-	t.dst16 = append(t.dst16, d[:]...)
-	t.sport = append(t.sport, p.FiveTuple.SrcPort)
-	t.dport = append(t.dport, p.FiveTuple.DstPort)
-	t.proto = append(t.proto, p.FiveTuple.Protocol)
-	t.length = append(t.length, uint32(p.Length)) // task.go:168
-	if len(t.length) >= BatchPackets {
-		t.flushLocked()
+	b := t.cur
+	b.src16 = append(b.src16, s[:]...)
+	b.dst16 = append(b.dst16, d[:]...)
+	b.sport = append(b.sport, p.FiveTuple.SrcPort)
+	b.dport = append(b.dport, p.FiveTuple.DstPort)
+	b.proto = append(b.proto, p.FiveTuple.Protocol)
+	b.length = append(b.length, uint32(p.Length)) // task.go:168
+	if len(b.length) >= BatchPackets {
+		t.handOverLocked()
 	}
 	t.mu.Unlock()
 }
 
-// flushLocked submits the pending batch (mutex held).  The reference logs a
-// packet it cannot insert and goes on (task.go:162-166); a failed batch is
-// logged the same way and kept for Err().
-func (t *GPUTask) flushLocked() {
-	if len(t.length) == 0 {
+// handOverLocked queues the current batch (mutex held, so batches keep their order)
+// and starts an empty one.
+func (t *GPUTask) handOverLocked() {
+	if len(t.cur.length) == 0 {
 		return
 	}
-	var err error
-	if t.cm != nil {
-		err = t.cm.InsertTuples(t.src16, t.dst16, t.sport, t.dport, t.proto, t.length)
-	} else {
-		err = t.ss.InsertTuples(t.src16, t.dst16, t.sport, t.dport, t.proto, t.length)
-	}
-	if err != nil {
-		if t.err == nil {
-			t.err = err
-		}
-		log.Printf("Error inserting a batch for task '%s': %v", t.name, err)
-	}
-	t.src16, t.dst16 = t.src16[:0], t.dst16[:0]
-	t.sport, t.dport, t.proto, t.length = t.sport[:0], t.dport[:0], t.proto[:0], t.length[:0]
+	t.work <- job{b: t.cur}
+	t.cur = <-t.free
 }
 
-// Flush submits the pending batch now (e.g. at the end of a capture).
-func (t *GPUTask) Flush() {
+// call runs fn on the submitter after every packet processed so far, and waits.
+func (t *GPUTask) call(fn func()) {
+	done := make(chan struct{})
 	t.mu.Lock()
-	t.flushLocked()
+	t.handOverLocked()
+	t.work <- job{fn: fn, done: done}
 	t.mu.Unlock()
+	<-done
+}
+
+// Flush submits the pending batch and waits until the GPU has it (e.g. at the end of a capture).
+func (t *GPUTask) Flush() { t.call(nil) }
+
+// Close drains the queue and stops the submitter; the task is unusable afterwards.
+func (t *GPUTask) Close() {
+	t.Flush()
+	t.mu.Lock()
+	close(t.work)
+	t.mu.Unlock()
+	<-t.quit
 }
 
 // Err reports the first failed batch since the last Reset.
 func (t *GPUTask) Err() error {
-	t.mu.Lock()
-	defer t.mu.Unlock()
+	t.errMu.Lock()
+	defer t.errMu.Unlock()
 	return t.err
 }
 
@@ -205,27 +285,26 @@ func (t *GPUTask) sk() statistic.Sketch {
 
 // Query (task.go:171-174) of the state after every packet processed so far.
 func (t *GPUTask) Query(flow []byte) uint64 {
-	t.mu.Lock()
-	defer t.mu.Unlock()
-	t.flushLocked()
-	return t.sk().Query(flow)
+	var v uint64
+	t.call(func() { v = t.sk().Query(flow) })
+	return v
 }
 
 // Snapshot (task.go:176-179): the heavy hitters of every packet processed so far.
 func (t *GPUTask) Snapshot() interface{} {
-	t.mu.Lock()
-	defer t.mu.Unlock()
-	t.flushLocked()
-	return t.sk().HeavyHitters()
+	var rec statistic.HeavyRecord
+	t.call(func() { rec = t.sk().HeavyHitters() })
+	return rec
 }
 
-// Reset (task.go:181-184): the pending batch belongs to the period that ends.
+// Reset (task.go:181-184): the packets processed before the call belong to the period that ends.
 func (t *GPUTask) Reset() {
-	t.mu.Lock()
-	defer t.mu.Unlock()
-	t.flushLocked()
-	t.sk().Reset()
-	t.err = nil
+	t.call(func() {
+		t.sk().Reset()
+		t.errMu.Lock()
+		t.err = nil
+		t.errMu.Unlock()
+	})
 }
 
 // DecodeFlowFunc (task.go:150-153): the reference's DecodeFlow (it reads no task state).

@@ -236,3 +236,18 @@ def test_encapsulated_capture_decoded_on_host(gpu, oracle, tmp_path):
     cm3.flush()
     assert cm3.stats() == st
     _same_state(cm3, orc)
+    # a short or missing side array (advisor r4): escapes past it are counted as
+    # unsupported and never read; everything else is applied as before
+    cls = rec[:, 13]
+    idx = np.ascontiguousarray(rec[:, :4]).view("<u4").reshape(-1)
+    for keep in (len(side) // 2, 0):
+        lost = (cls == 2) & (idx >= keep)
+        assert lost.any()
+        cm4 = CountMin(65536, 4, 20000, 50, flow_fields=FIVE, seeds=seeds, max_flows=1 << 20, batch_packets=70_000)
+        cm4.insert_compact(rec, cwl, side[:keep] if keep else None)
+        cm4.flush()
+        s4 = cm4.stats()
+        assert s4["unsupported"] == int(lost.sum()) and s4["dropped"] == n_arp
+        o4 = oracle.CountMin(65536, 4, 20000, 50, 37, seeds)
+        o4.insert_hdr64(hb.hdr[~lost], hb.wirelen[~lost], FIVE)
+        _same_state(cm4, o4)

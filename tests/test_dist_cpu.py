@@ -219,3 +219,204 @@ def test_route_exchange_delivers_the_stable_filter(world):
         for x, y in zip(a.export(), b.export()):
             assert np.array_equal(x, y)
     assert total == len(wl)
+
+
+# --- the owner key follows the tasks' flow keys, and queries are -----
+# routed to the owner shard.  A key without SrcIP (legal, config.go:59) shards by
+# the whole key; every rank's routed query must equal the answer of the shard
+# holding the flow (the oracle fed that shard's stable filter).
+def test_owner_fields_rule_c_equals_host():
+    import ctypes as ct
+    import sys
+    sys.path.insert(0, ROOT)
+    from go2netspectra_amd import _lib
+    from go2netspectra_amd.dist import owner_fields
+    L = _lib.load()
+    cases = [[["SrcIP"]], [["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"], ["SrcIP"]], [["DstIP"]],
+             [["DstPort", "Protocol"]], [["Protocol", "DstPort", "DstIP"], ["DstPort", "Protocol"]],
+             [["DstIP"], ["SrcIP"]], [["SrcPort"], ["DstPort"]], [["DstIP", "Bogus"], ["DstIP"]]]
+    for tasks in cases:
+        arr = (_lib.Layout * len(tasks))(*[_lib.Layout.of(t) for t in tasks])
+        o = _lib.Layout()
+        rc = L.gns_route_owner_fields(arr, len(tasks), ct.byref(o))
+        try:
+            want = owner_fields(tasks)
+        except ValueError:
+            want = None
+        if want is None:
+            assert rc == _lib.GNS_E_ARG and b"share no field" in L.gns_last_error()
+        else:
+            assert rc == 0 and o.names() == want, (tasks, o.names(), want)
+
+
+def test_manager_owner_fields():
+    import sys
+    sys.path.insert(0, ROOT)
+    from go2netspectra_amd.dist import owner_fields
+    from go2netspectra_amd.factory import key_fields
+
+    class T:  # stand-ins with the Task attributes the rule reads (no device needed)
+        def __init__(self, f):
+            self.flow_fields = f
+    assert owner_fields([key_fields(T(["SrcIP", "DstIP"])), key_fields(T(["SrcIP"]))]) == ["SrcIP"]
+    with pytest.raises(ValueError, match="share no field"):
+        owner_fields([key_fields(T(["DstIP"])), key_fields(T(["SrcPort"]))])
+
+
+def test_owner_folds_v4_mapped_slots():
+    """An IPv4-mapped IPv6 slot and the IPv4 slot have one owner (the exact
+    aggregator keys both as ::ffff:a.b.c.d, exact/task.go:330-366)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from go2netspectra_amd.dist import owner_of_keys, owner_of_tuples, shard_of
+    rng = np.random.default_rng(5)
+    v4 = np.zeros((500, 16), np.uint8)
+    v4[:, :4] = rng.integers(0, 256, (500, 4))
+    mapped = np.zeros((500, 16), np.uint8)
+    mapped[:, 10:12] = 0xFF
+    mapped[:, 12:] = v4[:, :4]
+    for G in (2, 3, 8):
+        assert np.array_equal(shard_of(v4, G), shard_of(mapped, G))
+        a = owner_of_keys(v4, ["DstIP"], G, ["DstIP"])
+        b = owner_of_keys(mapped, ["DstIP"], G, ["DstIP"])
+        c = owner_of_tuples(v4, mapped, None, None, None, G, ["DstIP"])
+        assert np.array_equal(a, b) and np.array_equal(a, c)
+
+
+KEYED_LAYOUTS = {"dstip": ["DstIP"], "dport_proto": ["DstPort", "Protocol"]}
+
+
+def _keyed_stream(n=10_000):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import random_tuples
+    return random_tuples(np.random.default_rng(91), n, 700)
+
+
+def _keyed_queries(t, rank, fields):
+    """rank's query batch: keys of stream packets (present flows) plus random keys."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from go2netspectra_amd.packets import PacketBatch
+    b = PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"])
+    keys = b.keys(fields)
+    rng = np.random.default_rng(1000 + rank)
+    pick = keys[rng.integers(0, len(keys), 300 + 50 * rank)]
+    junk = rng.integers(0, 256, (40, keys.shape[1]), dtype=np.uint8)
+    return np.concatenate([pick, junk])
+
+
+def _keyed_oracle(t, fields, world, g):
+    """Oracle Count-Min fed shard g's stable filter under the task's owner key."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from go2netspectra_amd.dist import owner_fields, owner_of_tuples
+    from go2netspectra_amd.packets import PacketBatch
+    from oracle import oracle as orc
+    own = owner_of_tuples(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], world, owner_fields([fields]))
+    m = own == g
+    b = PacketBatch(t["src16"][m], t["dst16"][m], t["sport"][m], t["dport"][m], t["proto"][m], t["length"][m])
+    keys = b.keys(fields)
+    cm = orc.CountMin(256, 3, 50_000, 40, keys.shape[1], np.array([11, 12, 13], np.uint32))
+    if len(b):
+        cm.insert_keys(keys, b.length)
+    return cm, m
+
+
+def _keyed_worker(rank, world, port, layout, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from go2netspectra_amd.dist import exchange_runs, owner_fields, owner_of_tuples, routed_query
+    from go2netspectra_amd.packets import PacketBatch
+    from oracle import oracle as orc
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fields = KEYED_LAYOUTS[layout]
+    owner = owner_fields([fields])
+    t = _keyed_stream()
+    sl = np.array_split(np.arange(len(t["length"])), world)[rank]  # this rank's slice of the stream
+    own = owner_of_tuples(t["src16"][sl], t["dst16"][sl], t["sport"][sl], t["dport"][sl], t["proto"][sl], world, owner)
+    order = np.argsort(own, kind="stable")
+    counts = np.bincount(own, minlength=world)
+    # the "records" exchanged are the packets' indices in the global stream (int64 rows)
+    idx = torch.from_numpy(np.ascontiguousarray(sl[order]).astype(np.int64).view(np.uint8).reshape(-1, 8))
+    got, _ = _exchange_rows(idx, counts, world)
+    got = got.numpy().view(np.int64).reshape(-1)
+    b = PacketBatch(t["src16"][got], t["dst16"][got], t["sport"][got], t["dport"][got], t["proto"][got],
+                    t["length"][got])
+    keys = b.keys(fields)
+    cm = orc.CountMin(256, 3, 50_000, 40, keys.shape[1], np.array([11, 12, 13], np.uint32))
+    if len(b):
+        cm.insert_keys(keys, b.length)
+    qk = _keyed_queries(t, rank, fields)
+    ans = routed_query(lambda ks: np.array([cm.query(bytes(k)) for k in ks], np.uint64), qk, fields, world, owner)
+    # a rank with nothing to ask still takes part in the collective
+    empty = routed_query(lambda ks: np.array([cm.query(bytes(k)) for k in ks], np.uint64),
+                         qk[:0] if rank == 0 else qk[:7], fields, world, owner)
+    q.put((rank, got.copy(), ans.copy(), empty.copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _exchange_rows(rows, counts, world):
+    """exchange_runs for fixed-width rows of any byte width (the index rows of the test)."""
+    import torch
+    import torch.distributed as dist
+    send = torch.tensor([int(c) for c in counts], dtype=torch.int64)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send)
+    sc, rc = send.tolist(), recv.tolist()
+    out = torch.empty((sum(rc), rows.shape[1]), dtype=rows.dtype)
+    dist.all_to_all_single(out, rows, output_split_sizes=rc, input_split_sizes=sc)
+    return out, rc
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("layout", sorted(KEYED_LAYOUTS))
+def test_keyed_sharding_and_routed_queries(world, layout):
+    import sys
+    sys.path.insert(0, ROOT)
+    from go2netspectra_amd.dist import owner_fields, owner_of_keys
+    fields = KEYED_LAYOUTS[layout]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_keyed_worker, args=(r, world, port, layout, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (g, a, e)) for r, g, a, e in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    t = _keyed_stream()
+    shards = [_keyed_oracle(t, fields, world, g) for g in range(world)]
+    total = 0
+    for g in range(world):
+        got, _, _ = res[g]
+        assert np.array_equal(got, np.flatnonzero(shards[g][1]))  # the full-key stable filter, in order
+        total += len(got)
+    assert total == len(t["length"])
+    owner = owner_fields([fields])
+    nonzero = 0
+    for r in range(world):
+        qk = _keyed_queries(t, r, fields)
+        own = owner_of_keys(qk, fields, world, owner)
+        want = np.array([shards[o][0].query(bytes(k)) for o, k in zip(own, qk)], np.uint64)
+        assert np.array_equal(res[r][1], want)
+        nonzero += int((want != 0).sum())
+        e = res[r][2]
+        assert len(e) == (0 if r == 0 else 7) and np.array_equal(e, want[:len(e)])
+    assert nonzero > 0
+    # a flow never splits: every packet of one flow key went to one shard
+    from go2netspectra_amd.packets import PacketBatch
+    b = PacketBatch(t["src16"], t["dst16"], t["sport"], t["dport"], t["proto"], t["length"])
+    keys = b.keys(fields)
+    where = np.zeros(len(keys), np.int64)
+    for g in range(world):
+        where[shards[g][1]] = g
+    _, inv = np.unique(keys, axis=0, return_inverse=True)
+    for u in range(inv.max() + 1):
+        assert len(set(where[inv.reshape(-1) == u])) == 1

@@ -98,3 +98,53 @@ def test_shard_stream_through_engine_equals_oracle_on_filter(gpu, oracle, g):
     assert np.array_equal(Fc, oFc) and np.array_equal(Fs, oFs)
     hh = cm.heavy_hitters()
     assert_same_list([(x.Flow, x.Count) for x in hh.Count], orc.heavy("count"))
+
+
+@pytest.mark.parametrize("owner_key", [["DstIP"], ["DstPort", "Protocol"], ["SrcIP", "DstIP", "SrcPort", "DstPort",
+                                                                             "Protocol"]])
+@pytest.mark.parametrize("G", [2, 7])
+def test_keyed_partition_and_key_owners(gpu, oracle, owner_key, G):
+    """A router built for an owner key other than [SrcIP] (the full key
+    when SrcIP is not in the key): the device partition is the stable filter under
+    dist.owner_of_tuples, and gns_route_owner_keys gives every flow key (host or
+    device memory) the shard its packets went to; v4-mapped slots fold."""
+    import torch
+    from go2netspectra_amd.dist import Router, owner_of_keys, owner_of_tuples
+    from go2netspectra_amd.packets import PacketBatch
+    rng = np.random.default_rng(40 + G)
+    t = random_tuples(rng, 30_000, 2000, v6_frac=0.25)
+    hdr = frames_from_tuples(t, rng, vlan_frac=0.3)
+    wl = t["length"]
+    # the tuple the parser derives from each record (ports / protocol follow gopacket's
+    # keep-on-error rules for short wire lengths, so they can differ from t's)
+    ok = np.ones(len(wl), bool)
+    pt = {"src16": np.zeros((len(wl), 16), np.uint8), "dst16": np.zeros((len(wl), 16), np.uint8),
+          "sport": np.zeros(len(wl), np.uint16), "dport": np.zeros(len(wl), np.uint16), "proto": np.zeros(len(wl), np.uint8)}
+    for i in range(len(wl)):
+        st, s16, d16, sp, dp, pr = oracle.parse_hdr64(bytes(hdr[i]), int(wl[i]))
+        ok[i] = st == 0
+        pt["src16"][i], pt["dst16"][i] = np.frombuffer(s16, np.uint8), np.frombuffer(d16, np.uint8)
+        pt["sport"][i], pt["dport"][i], pt["proto"][i] = sp, dp, pr
+    own = np.where(ok, owner_of_tuples(pt["src16"], pt["dst16"], pt["sport"], pt["dport"], pt["proto"], G, owner_key), 0)
+    r = Router(G, owner=owner_key)
+    oh, ow, counts = r.partition(torch.from_numpy(hdr).cuda(), torch.from_numpy(wl.view(np.int32)).cuda())
+    assert np.array_equal(counts, np.bincount(own, minlength=G))
+    order = np.argsort(own, kind="stable")
+    assert np.array_equal(oh.cpu().numpy(), hdr[order])
+    # query keys of the 5-tuple task and of the owner key's own layout
+    for fields in (owner_key, ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"], owner_key[::-1]):
+        keys = PacketBatch(pt["src16"], pt["dst16"], pt["sport"], pt["dport"], pt["proto"], t["length"]).keys(fields)
+        host = r.owner_of_keys(keys[ok], fields)
+        assert np.array_equal(host, own[ok])
+        assert np.array_equal(host, owner_of_keys(keys[ok], fields, G, owner_key))
+        dev = r.owner_of_keys(torch.from_numpy(keys[ok]).cuda(), fields).cpu().numpy()
+        assert np.array_equal(dev.astype(np.int64), host)
+    mapped = np.zeros((50, 16), np.uint8)
+    mapped[:, 10:12] = 0xFF
+    mapped[:, 12:] = rng.integers(0, 256, (50, 4))
+    v4 = np.zeros((50, 16), np.uint8)
+    v4[:, :4] = mapped[:, 12:]
+    if owner_key[0] == "DstIP":
+        assert np.array_equal(r.owner_of_keys(mapped, ["DstIP"]), r.owner_of_keys(v4, ["DstIP"]))
+    with pytest.raises(Exception, match="lacks owner field"):
+        r.owner_of_keys(np.zeros((4, 2), np.uint8), ["SrcPort"])
