@@ -102,11 +102,12 @@ def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, dept
         cm.insert_hdr64_pool(hdr[done:done + m], wl[done:done + m], fields, threads)
         done += m
     pool_rate = done / (time.perf_counter() - t0) / 1e6
-    # (3) the same pool on every core this process may run on (all host cores)
-    try:
-        allc = len(os.sched_getaffinity(0))
-    except AttributeError:
-        allc = os.cpu_count() or 1
+    # (3) the same pool on every core this process may use (all host cores) =
+    # min(CPU affinity, cgroup CPU quota): more threads than the quota only time-slice
+    host = host_cpu()
+    allc = host["affinity_cpus"] or os.cpu_count() or 1
+    if host["cgroup_cpu_quota"]:
+        allc = max(1, min(allc, int(host["cgroup_cpu_quota"])))
     cm = orc.CountMin(width, depth, 1 << 20, 1000, K, seeds)
     done_all, t0 = 0, time.perf_counter()
     while done_all < n and time.perf_counter() - t0 < seconds / 2:
@@ -120,17 +121,19 @@ def cpu_baseline(hdr_dev, wl_dev, seconds: float = 8.0, width: int = WIDTH, dept
         "sample": f"first {done:,} packets of the same synthetic stream (window 0); C restatement of the Go "
                   f"worker pool (count_min.go CAS loops + parse/encode, {threads} threads = the reference's "
                   f"num_workers default, shared cursor)",
-        "host": host_cpu(),
+        "host": host,
         "sequential_oracle": {"value": round(seq_rate, 3), "cores": 1, "packets": seq_n},
         "all_cores_pool": {"value": round(all_rate, 3), "cores": allc, "packets": done_all,
-                           "what": "BASELINE.md B1: the same worker-pool restatement with one thread per core "
-                                   "of this process's CPU affinity set (nproc)"},
+                           "what": "BASELINE.md B1: the same worker-pool restatement with one thread per usable "
+                                   "core = min(CPU affinity set, cgroup CPU quota) of this process"},
     }
     return (out, seq_state, seq_n) if keep_state else out
 
 
 def cpu_baseline_ss(hdr_dev, wl_dev, seconds: float = 10.0):
-    """Sequential SuperSpread oracle on a bounded prefix of the same stream (rank 0)."""
+    """Sequential SuperSpread oracle on a bounded prefix of the same stream (rank 0).
+    Returns the baseline, the oracle (its state is the parity reference) and the
+    number of packets it took."""
     from oracle import oracle as orc
     n = min(int(wl_dev.shape[0]), 8_000_000)
     hdr = hdr_dev[:n].cpu().numpy()
@@ -142,9 +145,30 @@ def cpu_baseline_ss(hdr_dev, wl_dev, seconds: float = 10.0):
         ss.insert_hdr64(hdr[done:done + m], wl[done:done + m], ["SrcIP"], ["DstIP"])
         done += m
     rate = done / (time.perf_counter() - t0) / 1e6
-    return {"value": round(rate, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port", "host": host_cpu(),
+    base = {"value": round(rate, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port", "host": host_cpu(),
             "sample": f"first {done:,} packets of window 0; sequential C restatement of "
                       f"super_spread.go (parse + encode + HLL + MV), 1 thread"}
+    return base, ss, done
+
+
+def parity_check_ss(orc_ss, hdr, wl, local):
+    """After the timed region: the CPU leg's prefix through a fresh SuperSpread handle,
+    whole exported state (values, owner keys, every HLL register, pbits as bit patterns)
+    and the heavy-hitter list compared with the sequential oracle."""
+    from go2netspectra_amd import SuperSpread
+    ss = SuperSpread(SS_W, SS_D, SS_THR, SS_M, 5, 0.5, 1.08, flow_fields=["SrcIP"], elem_fields=["DstIP"],
+                     seeds=row_seeds(SS_D), hll_master=SS_HLL, rng_seed=SS_RNG, device=local)
+    ss.insert_headers(hdr, wl)
+    ss.flush()
+    got = ss.export_state()
+    want = orc_ss.export()
+    same = {name: bool(np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8)))
+            for name, a, b in zip(("values", "keys", "registers", "pbits"), got, want)}
+    same["heavy"] = [(h.Flow, h.Count) for h in ss.heavy_hitters().Count] == orc_ss.heavy()
+    ss.close()
+    return {"checked_packets": int(wl.shape[0]), "bit_exact": all(same.values()), "arrays": same,
+            "how": "the cpu_baseline sequential oracle's prefix of window 0 through a fresh handle "
+                   "(declared generator, DESIGN.md §2)"}
 
 
 # configs[2] / SURVEY §8d C3: the reference's default SuperSpread task
@@ -221,7 +245,10 @@ def bench_superspread(args, torch, dist, world, rank, local):
         "heavy_hitters": len(hh.Count), "engine_counters": ss.counters(),
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline_ss(*syn.generate(8_000_000))
+        ph, pw = syn.generate(8_000_000)
+        base, orc_ss, done = cpu_baseline_ss(ph, pw)
+        line["cpu_baseline"] = base
+        line["parity"] = parity_check_ss(orc_ss, ph[:done], pw[:done], local)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -29,7 +29,6 @@
 
 #include "gns_common.hpp"
 #include "gns_scan.cuh"
-#include <rocprim/rocprim.hpp>
 
 namespace gns {
 
@@ -2355,58 +2354,151 @@ __global__ __launch_bounds__(256) void k_ids_to_bytes(const uint32_t *ids, uint6
 // candidate: 0.59 ms per call at the bench geometry).  Order is irrelevant:
 // the host dedupes and sorts.
 constexpr uint32_t kHhItems = 8;
-// Device-side heavy-hitter list (count_min.go:178-247 HeavyHitters): candidates
-// (cells >= threshold) -> sort by (flow id, value desc) -> first entry per flow
-// (the flow's max over its buckets) -> sort by (value desc, first key bytes).
-__global__ __launch_bounds__(256) void k_hh_key(uint64_t *cand, uint32_t n) {
+// Device-side heavy-hitter list (count_min.go:178-247 HeavyHitters), all
+// hand-written (no library sort):
+//   candidates   cells with value >= threshold (one global atomic per workgroup);
+//   per-flow max every candidate atomicMax'es (epoch << 32 | value) into a dense
+//                per-flow-id word, then the one candidate per flow that carries the
+//                max and wins the flow's mark emits (id, max) -- the dedupe of
+//                count_min.go:214-228's map, order-free, O(candidates);
+//   order        a stable LSD radix sort of the unique entries (8-bit digits,
+//                device-wide passes: block histograms, the K2 scan, stable
+//                ballot-multisplit scatter) by the primary key (value desc, key
+//                bytes 0..3); only when two entries tie on it (the same value and
+//                the same first four key bytes) is the list re-sorted by the whole
+//                key (bytes K-1..4 first, then the primary key).  A pass whose
+//                digit is the same for every entry (IPv4 slots' zero padding) only
+//                copies.  Canonical order: value desc, flow bytes asc.
+__global__ __launch_bounds__(256) void k_hh_best(const uint64_t *cand, uint32_t n, unsigned long long *best,
+                                                 uint32_t epoch) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const uint64_t c = cand[i];  // value << 32 | id
-    cand[i] = (uint64_t)(uint32_t)c << 32 | (uint32_t)~(uint32_t)(c >> 32);
+    atomicMax(&best[(uint32_t)c], (unsigned long long)epoch << 32 | (c >> 32));
 }
 
-__global__ __launch_bounds__(256) void k_hh_unique(const uint64_t *s, uint32_t n, uint32_t *uid, uint32_t *uval,
-                                                   uint32_t *nu) {
+__global__ __launch_bounds__(256) void k_hh_emit(const uint64_t *cand, uint32_t n, const unsigned long long *best,
+                                                 uint32_t *mark, uint32_t epoch, uint32_t *uid, uint32_t *uval,
+                                                 uint32_t *nu) {
+    __shared__ uint32_t s_n, s_base;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t id = (uint32_t)(s[i] >> 32);
-    if (i > 0 && (uint32_t)(s[i - 1] >> 32) == id) return;
-    const uint32_t j = atomicAdd(nu, 1u);
-    uid[j] = id;
-    uval[j] = ~(uint32_t)s[i];
+    bool out = false;
+    uint32_t id = 0, v = 0;
+    if (i < n) {
+        const uint64_t c = cand[i];
+        id = (uint32_t)c;
+        v = (uint32_t)(c >> 32);
+        out = (uint32_t)best[id] == v && atomicExch(&mark[id], epoch) != epoch;  // one per flow
+    }
+    const uint32_t off = out ? atomicAdd(&s_n, 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_n ? atomicAdd(nu, s_n) : 0u;
+    __syncthreads();
+    if (out) {
+        uid[s_base + off] = id;
+        uval[s_base + off] = v;
+    }
 }
 
-__global__ __launch_bounds__(256) void k_hh_order_key(const uint32_t *uval, const uint8_t *ub, uint32_t K,
-                                                      uint32_t n, uint64_t *key, uint32_t *idx) {
-    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= n) return;
-    uint32_t be = 0;
-    for (uint32_t b = 0; b < 4; b++) be = be << 8 | (b < K ? ub[(uint64_t)j * K + b] : 0u);
-    key[j] = (uint64_t)(~uval[j]) << 32 | be;
-    idx[j] = j;
+// One radix pass's digit of entry e: mode 0 = byte `b` of the value, inverted
+// (descending); mode 1 = key byte b (0 beyond K).
+struct RsDigit {
+    uint32_t mode, b, K;
+    const uint32_t *uval;
+    const uint8_t *ub;
+};
+__device__ __forceinline__ uint32_t rs_digit(const RsDigit &r, uint32_t e) {
+    if (r.mode == 0) return 255u - ((r.uval[e] >> (8u * r.b)) & 255u);
+    return r.b < r.K ? (uint32_t)r.ub[(uint64_t)e * r.K + r.b] : 0u;
 }
 
-// Full canonical order on the device (value desc, then all key bytes asc) as
-// stable LSD passes: 8-byte key chunks from the last to byte 4, then (value desc,
-// bytes 0..3).  perm holds unique-entry indices in the current order.
-__global__ __launch_bounds__(256) void k_hh_chunk_key(const uint32_t *perm, const uint8_t *ub, uint32_t K,
-                                                      uint32_t off, uint32_t n, uint64_t *key) {
-    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= n) return;
-    const uint8_t *b = ub + (uint64_t)perm[j] * K;
-    uint64_t k = 0;
-    for (uint32_t t = 0; t < 8; t++) k = k << 8 | (off + t < K ? b[off + t] : 0u);
-    key[j] = k;
+constexpr uint32_t kRsPer = 16;                 // entries per thread
+constexpr uint32_t kRsBlock = 256 * kRsPer;     // entries per block of a pass
+
+__global__ __launch_bounds__(256) void k_rs_hist(const uint32_t *perm, uint32_t n, RsDigit r, uint32_t *hist) {
+    __shared__ uint32_t s_h[256];
+    const uint32_t tid = threadIdx.x;
+    s_h[tid] = 0;
+    __syncthreads();
+    const uint32_t beg = blockIdx.x * kRsBlock;
+#pragma unroll 4
+    for (uint32_t k = 0; k < kRsPer; k++) {
+        const uint32_t j = beg + k * 256 + tid;
+        if (j < n) atomicAdd(&s_h[rs_digit(r, perm[j])], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)blockIdx.x * 256 + tid] = s_h[tid];
 }
 
-__global__ __launch_bounds__(256) void k_hh_final_key(const uint32_t *perm, const uint32_t *uval, const uint8_t *ub,
-                                                      uint32_t K, uint32_t n, uint64_t *key) {
-    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+// Stable scatter of one pass: entries of a block in (round, wave, lane) order =
+// position order; per wave-instruction the lanes of one digit are found by
+// eight ballots (no reliance on LDS-atomic lane order).  offs = the scanned
+// block-major histogram (global start of every (block, digit) run); tot / total
+// = the digit totals' exclusive scan: a digit holding every entry makes the pass
+// a copy (the order cannot change).
+__global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t *perm, uint32_t n, RsDigit r, const uint32_t *offs,
+                                                    const uint32_t *tot, const uint32_t *total, uint32_t *out) {
+    __shared__ uint32_t s_base[256];
+    __shared__ uint32_t s_wave[4][256];
+    __shared__ uint32_t s_copy;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t beg = blockIdx.x * kRsBlock;
+    if (tid == 0) {
+        const uint32_t d0 = rs_digit(r, perm[0]);
+        const uint32_t hi = d0 < 255u ? tot[d0 + 1] : *total;
+        s_copy = hi - tot[d0] == n;
+    }
+    s_base[tid] = offs[(uint64_t)blockIdx.x * 256 + tid];
+    __syncthreads();
+    if (s_copy) {  // block-uniform
+        for (uint32_t k = 0; k < kRsPer; k++) {
+            const uint32_t j = beg + k * 256 + tid;
+            if (j < n) out[j] = perm[j];
+        }
+        return;
+    }
+    const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+    for (uint32_t k = 0; k < kRsPer; k++) {
+        if (beg + k * 256 >= n) break;  // block-uniform
+        const uint32_t j = beg + k * 256 + tid;
+        const bool valid = j < n;
+        const uint32_t e = valid ? perm[j] : 0u;
+        const uint32_t dg = valid ? rs_digit(r, e) : 0u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (uint32_t bit = 0; bit < 8; bit++) {
+            const uint64_t m = __ballot(valid && ((dg >> bit) & 1u));
+            peers &= ((dg >> bit) & 1u) ? m : ~m;
+        }
+        s_wave[0][tid] = 0; s_wave[1][tid] = 0; s_wave[2][tid] = 0; s_wave[3][tid] = 0;
+        __syncthreads();
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        if (valid && rank == 0) s_wave[wave][dg] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = s_base[dg] + rank;
+            for (uint32_t w = 0; w < wave; w++) pos += s_wave[w][dg];
+            out[pos] = e;
+        }
+        __syncthreads();
+        s_base[tid] += s_wave[0][tid] + s_wave[1][tid] + s_wave[2][tid] + s_wave[3][tid];
+        __syncthreads();
+    }
+}
+
+// Whether two neighbours of the primary order tie on (value, key bytes 0..3):
+// only then does the list need the whole-key order.
+__global__ __launch_bounds__(256) void k_hh_ties(const uint32_t *perm, uint32_t n, const uint32_t *uval,
+                                                 const uint8_t *ub, uint32_t K, uint32_t *flag) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x + 1;
     if (j >= n) return;
-    const uint32_t u = perm[j];
-    uint32_t be = 0;
-    for (uint32_t b = 0; b < 4; b++) be = be << 8 | (b < K ? ub[(uint64_t)u * K + b] : 0u);
-    key[j] = (uint64_t)(~uval[u]) << 32 | be;
+    const uint32_t a = perm[j - 1], b = perm[j];
+    if (uval[a] != uval[b]) return;
+    bool eq = true;
+    for (uint32_t t = 0; t < 4 && t < K; t++) eq = eq && ub[(uint64_t)a * K + t] == ub[(uint64_t)b * K + t];
+    if (eq) atomicOr(flag, 1u);
 }
 
 __global__ __launch_bounds__(256) void k_hh_iota(uint32_t *perm, uint32_t n) {
@@ -2479,13 +2571,17 @@ struct CmScratch {
     uint64_t qkeys_n = 0;
     uint64_t *qout = nullptr;
     uint64_t qout_n = 0;
-    // device heavy-hitter sort: sorted candidates, unique (id, value), order keys / indices, rocPRIM temp
-    uint64_t *k64a = nullptr, *k64b = nullptr;
-    uint64_t k64a_n = 0, k64b_n = 0;
+    // device heavy-hitter list: per-flow-id max / mark words (dense over the dictionary's
+    // slots, epoch-tagged so they are never cleared), unique (id, value), order indices,
+    // radix-pass histograms (block-major) and their scan
+    unsigned long long *best = nullptr;
+    uint32_t *mark = nullptr;
+    uint64_t best_n = 0, mark_n = 0;
+    uint32_t hh_epoch = 0;
     uint32_t *u32a = nullptr, *u32b = nullptr, *u32c = nullptr, *u32d = nullptr;
     uint64_t u32a_n = 0, u32b_n = 0, u32c_n = 0, u32d_n = 0;
-    uint8_t *tmp = nullptr;
-    uint64_t tmp_n = 0;
+    uint32_t *rsh = nullptr;    // [blocks][256] histograms, then [ngrp][256] group sums, [256] totals, total, tie flag
+    uint64_t rsh_n = 0;
     uint8_t *obytes = nullptr;  // heavy hitters: ordered flow bytes
     uint64_t obytes_n = 0;
     uint8_t *hpin = nullptr;    // pinned host staging of the heavy-hitter rows (D2H into pageable
@@ -2495,11 +2591,11 @@ struct CmScratch {
         if (hpin) (void)hipHostFree(hpin);
         hpin = nullptr; hpin_n = 0;
         dfree(cand); dfree(ncand); dfree(ids); dfree(bytes); dfree(qkeys); dfree(qout);
-        dfree(k64a); dfree(k64b); dfree(u32a); dfree(u32b); dfree(u32c); dfree(u32d); dfree(tmp);
+        dfree(best); dfree(mark); dfree(u32a); dfree(u32b); dfree(u32c); dfree(u32d); dfree(rsh);
         cand = nullptr; ncand = nullptr; ids = nullptr; bytes = nullptr; qkeys = nullptr; qout = nullptr;
-        k64a = k64b = nullptr; u32a = u32b = u32c = u32d = nullptr; tmp = nullptr;
+        best = nullptr; mark = nullptr; u32a = u32b = u32c = u32d = nullptr; rsh = nullptr;
         cap = 0; ids_n = bytes_n = qkeys_n = qout_n = 0;
-        k64a_n = k64b_n = u32a_n = u32b_n = u32c_n = u32d_n = tmp_n = 0;
+        best_n = mark_n = u32a_n = u32b_n = u32c_n = u32d_n = rsh_n = 0; hh_epoch = 0;
     }
 };
 
@@ -3066,6 +3162,8 @@ int cm_insert(gns_cm *cm, InputDesc in, uint64_t n, gns_mem where) {
 
 extern "C" {
 
+static int heavy_reserve(CmScratch &sc, uint64_t cells, uint64_t slots, uint32_t K, hipStream_t st);
+
 int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
     if (!p || !out) { set_error("null argument"); return GNS_E_ARG; }
     *out = nullptr;
@@ -3205,6 +3303,8 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             const char *es = getenv("GNS_K3_STAGED");
             cm->k3_staged = !(es && es[0] == '0');
         }
+        // the read side's heavy-hitter buffers (a window's first call allocates nothing)
+        if ((rc = heavy_reserve(cm->rd, (uint64_t)cm->g.d * cm->g.w, cm->dict_slots, cm->K, cm->stream)) != GNS_OK) break;
         if (hipStreamSynchronize(cm->stream) != hipSuccess) { set_error("sync failed"); rc = GNS_E_HIP; break; }
     } while (0);
     if (rc != GNS_OK) {
@@ -3362,20 +3462,79 @@ int gns_cm_export_state(gns_cm *cm, uint32_t *C, uint32_t *S, uint8_t *FPc, uint
 // HeavyHitters (count_min.go:178-247): a flow's max over its buckets reaches the
 // threshold iff one of its buckets does, so only cells >= threshold are
 // candidates; dedupe by fingerprint keeping the max; sort value desc.
+// the per-flow-id words cover every slot of the dictionary (zeroed when (re)allocated:
+// the epochs of the calls start at 1); bump: a new call's epoch
+static int heavy_flow_words(CmScratch &sc, uint64_t slots, hipStream_t st, bool bump) {
+    if (sc.best_n < slots || !sc.best || sc.mark_n < slots || !sc.mark) {
+        dfree(sc.best); dfree(sc.mark);
+        sc.best = nullptr; sc.mark = nullptr; sc.best_n = sc.mark_n = 0;
+        GNS_TRY(dalloc(reinterpret_cast<void **>(&sc.best), slots * 8));
+        GNS_TRY(dalloc(reinterpret_cast<void **>(&sc.mark), slots * 4));
+        sc.best_n = sc.mark_n = slots;
+        GNS_HIP(hipMemsetAsync(sc.best, 0, slots * 8, st));
+        GNS_HIP(hipMemsetAsync(sc.mark, 0, slots * 4, st));
+        sc.hh_epoch = 0;
+    }
+    if (bump && ++sc.hh_epoch == 0) {  // wrapped: clear, restart at 1
+        GNS_HIP(hipMemsetAsync(sc.best, 0, sc.best_n * 8, st));
+        GNS_HIP(hipMemsetAsync(sc.mark, 0, sc.mark_n * 4, st));
+        sc.hh_epoch = 1;
+    }
+    return GNS_OK;
+}
+
+// Read-side buffers of the heavy-hitter list sized up front (gns_cm_create /
+// gns_cm_view_create), so a window's first call allocates nothing: candidates
+// for min(cells, 4M) buckets, the per-flow words for the dictionary's slots,
+// unique entries and their order for 1M flows.  Larger lists still grow them.
+static int heavy_reserve(CmScratch &sc, uint64_t cells, uint64_t slots, uint32_t K, hipStream_t st) {
+    GNS_TRY(heavy_flow_words(sc, slots, st, false));
+    if (!sc.ncand) GNS_TRY(dalloc(reinterpret_cast<void **>(&sc.ncand), 16));
+    if (!sc.cand) {
+        const uint64_t want = std::min<uint64_t>(cells, 1ull << 22);
+        GNS_TRY(dalloc(reinterpret_cast<void **>(&sc.cand), want * 8));
+        sc.cap = want;
+    }
+    const uint64_t nu = std::min<uint64_t>(std::min(cells, slots), 1ull << 20);
+    GNS_TRY(grow_buf(&sc.u32a, sc.u32a_n, nu / 2));
+    GNS_TRY(grow_buf(&sc.u32b, sc.u32b_n, nu / 2 + 1));
+    GNS_TRY(grow_buf(&sc.u32c, sc.u32c_n, nu));
+    GNS_TRY(grow_buf(&sc.u32d, sc.u32d_n, nu / 2));
+    GNS_TRY(grow_buf(&sc.bytes, sc.bytes_n, nu / 2 * std::max<uint32_t>(K, 1)));
+    GNS_TRY(grow_buf(&sc.obytes, sc.obytes_n, nu / 2 * std::max<uint32_t>(K, 1)));
+    if (!sc.hpin) {
+        const uint64_t want = nu * (std::max<uint32_t>(K, 1) + 4);
+        GNS_HIP(hipHostMalloc(reinterpret_cast<void **>(&sc.hpin), want, hipHostMallocDefault));
+        sc.hpin_n = want;
+    }
+    return GNS_OK;
+}
+
+// One stable LSD radix pass over perm (n entries) by digit r: in -> out.
+static int rs_pass(CmScratch &sc, hipStream_t st, const uint32_t *in, uint32_t *out, uint32_t n, const RsDigit &r) {
+    const uint32_t nblk = (n + kRsBlock - 1) / kRsBlock;
+    const uint32_t ngrp = (nblk + kTGrp - 1) / kTGrp;
+    uint32_t *hist = sc.rsh, *part = hist + (size_t)nblk * 256, *tot = part + (size_t)ngrp * 256, *total = tot + 256;
+    hipLaunchKernelGGL(k_rs_hist, dim3(nblk), dim3(256), 0, st, in, n, r, hist);
+    hipLaunchKernelGGL(k_tscan_part, dim3(1, ngrp), dim3(256), 0, st, hist, nblk, 256u, part);
+    hipLaunchKernelGGL(k_tscan_mid, dim3(1), dim3(256), 0, st, part, ngrp, 256u, tot);
+    hipLaunchKernelGGL(k_tscan_bins, dim3(1), dim3(1024), 0, st, tot, 256u, total);
+    hipLaunchKernelGGL(k_tscan_down, dim3(1, ngrp), dim3(256), 0, st, hist, nblk, 256u, part, tot);
+    hipLaunchKernelGGL(k_rs_scatter, dim3(nblk), dim3(256), 0, st, in, n, r, hist, tot, total, out);
+    GNS_HIP(hipGetLastError());
+    return GNS_OK;
+}
+
 static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_t *val, const uint32_t *fp,
                         uint32_t thr, uint8_t *flows, uint32_t *vals, uint64_t *n_io) {
     const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
-    if (!sc.ncand) GNS_TRY(dalloc(reinterpret_cast<void **>(&sc.ncand), 16));
+    const uint32_t K = cm->K;
+    GNS_TRY(heavy_reserve(sc, cells, cm->dict_slots, K, st));
     // candidate buffer: grows to the number of cells at or above the threshold
     // (no cap: a low threshold can make every bucket a candidate, d*w < 2^32)
     uint32_t nc = 0;
     for (int pass = 0; pass < 2; pass++) {
-        if (!sc.cand) {
-            const uint64_t want = std::min<uint64_t>(cells, 1ull << 20);
-            GNS_TRY(dalloc(reinterpret_cast<void **>(&sc.cand), want * 8));
-            sc.cap = want;
-        }
-        hipError_t e = hipMemsetAsync(sc.ncand, 0, 4, st);
+        hipError_t e = hipMemsetAsync(sc.ncand, 0, 8, st);
         if (e == hipSuccess) {
             hipLaunchKernelGGL(k_hh_candidates, dim3((unsigned)((cells + 256 * kHhItems - 1) / (256 * kHhItems))), dim3(256), 0,
                                st, val, fp, cells, thr, sc.cand, sc.ncand, (uint32_t)sc.cap);
@@ -3393,27 +3552,19 @@ static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_
         GNS_TRY(dalloc(reinterpret_cast<void **>(&sc.cand), want * 8));
         sc.cap = want;
     }
-    uint64_t *cand = sc.cand;
-    const uint32_t K = cm->K;
-    // on the device: dedupe by flow keeping the max, then order by value desc
+    const uint64_t *cand = sc.cand;
+    // on the device: the max per flow over its buckets, one entry per flow
     uint32_t nu = 0;
     if (nc) {
         const unsigned g = (nc + 255) / 256;
-        GNS_TRY(grow_buf(&sc.k64a, sc.k64a_n, nc));
+        GNS_TRY(heavy_flow_words(sc, cm->dict_slots, st, true));
         GNS_TRY(grow_buf(&sc.u32a, sc.u32a_n, nc));
         GNS_TRY(grow_buf(&sc.u32b, sc.u32b_n, nc + 1));
-        hipLaunchKernelGGL(k_hh_key, dim3(g), dim3(256), 0, st, cand, nc);
-        size_t tb = 0;
-        if (rocprim::radix_sort_keys(nullptr, tb, cand, sc.k64a, (size_t)nc, 0u, 64u, st) != hipSuccess) {
-            set_error("heavy: radix sort size"); return GNS_E_HIP;
-        }
-        GNS_TRY(grow_buf(&sc.tmp, sc.tmp_n, tb));
-        if (rocprim::radix_sort_keys(sc.tmp, tb, cand, sc.k64a, (size_t)nc, 0u, 64u, st) != hipSuccess) {
-            set_error("heavy: radix sort"); return GNS_E_HIP;
-        }
-        uint32_t *d_nu = sc.u32b + nc;
-        GNS_HIP(hipMemsetAsync(d_nu, 0, 4, st));
-        hipLaunchKernelGGL(k_hh_unique, dim3(g), dim3(256), 0, st, sc.k64a, nc, sc.u32a, sc.u32b, d_nu);
+        uint32_t *d_nu = sc.ncand + 1;
+        hipLaunchKernelGGL(k_hh_best, dim3(g), dim3(256), 0, st, cand, nc, sc.best, sc.hh_epoch);
+        hipLaunchKernelGGL(k_hh_emit, dim3(g), dim3(256), 0, st, cand, nc, sc.best, sc.mark, sc.hh_epoch, sc.u32a,
+                           sc.u32b, d_nu);
+        GNS_HIP(hipGetLastError());
         GNS_HIP(hipMemcpyAsync(&nu, d_nu, 4, hipMemcpyDeviceToHost, st));
         GNS_HIP(hipStreamSynchronize(st));
     }
@@ -3424,37 +3575,44 @@ static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_
         const uint32_t Kb = K ? K : 1;
         GNS_TRY(grow_buf(&sc.bytes, sc.bytes_n, (uint64_t)nu * Kb));
         GNS_TRY(grow_buf(&sc.obytes, sc.obytes_n, (uint64_t)nu * Kb));
-        GNS_TRY(grow_buf(&sc.k64b, sc.k64b_n, (uint64_t)nu * 2));
         GNS_TRY(grow_buf(&sc.u32c, sc.u32c_n, (uint64_t)nu * 2));
         GNS_TRY(grow_buf(&sc.u32d, sc.u32d_n, (uint64_t)nu));
+        const uint32_t nblk = (nu + kRsBlock - 1) / kRsBlock, ngrp = (nblk + kTGrp - 1) / kTGrp;
+        GNS_TRY(grow_buf(&sc.rsh, sc.rsh_n, (uint64_t)(nblk + ngrp + 1) * 256 + 4));
+        uint32_t *tie = sc.rsh + (size_t)(nblk + ngrp + 1) * 256 + 1;
         if (K) hipLaunchKernelGGL(k_ids_to_bytes, dim3(g), dim3(256), 0, st, sc.u32a, (uint64_t)nu, cm->D, sc.bytes);
-        // canonical order, entirely on the device: stable LSD radix passes over the
-        // key bytes (8 at a time, last chunk first), then (value desc, bytes 0..3)
-        uint64_t *k0 = sc.k64b, *k1 = sc.k64b + nu;
-        uint32_t *p0 = sc.u32c, *p1 = sc.u32c + nu;
-        hipLaunchKernelGGL(k_hh_iota, dim3(g), dim3(256), 0, st, p0, nu);
-        auto sort_pass = [&](unsigned begin_bit) -> int {
-            size_t tb = 0;
-            if (rocprim::radix_sort_pairs(nullptr, tb, k0, k1, p0, p1, (size_t)nu, begin_bit, 64u, st) != hipSuccess) {
-                set_error("heavy: radix sort size"); return GNS_E_HIP;
+        uint32_t *p[2] = {sc.u32c, sc.u32c + nu};
+        int cur = 0;
+        // LSD: key bytes hi-1..0 (the last first), then the value (least significant byte first,
+        // inverted: descending) -> (value desc, key bytes 0..hi-1 asc)
+        auto sort_by = [&](uint32_t hi) -> int {
+            hipLaunchKernelGGL(k_hh_iota, dim3(g), dim3(256), 0, st, p[0], nu);
+            cur = 0;
+            RsDigit r{1, 0, K, sc.u32b, sc.bytes};
+            for (int b = (int)hi - 1; b >= 0; b--) {
+                r.b = (uint32_t)b;
+                GNS_TRY(rs_pass(sc, st, p[cur], p[cur ^ 1], nu, r));
+                cur ^= 1;
             }
-            GNS_TRY(grow_buf(&sc.tmp, sc.tmp_n, tb));
-            if (rocprim::radix_sort_pairs(sc.tmp, tb, k0, k1, p0, p1, (size_t)nu, begin_bit, 64u, st) != hipSuccess) {
-                set_error("heavy: radix sort"); return GNS_E_HIP;
+            r.mode = 0;
+            for (uint32_t b = 0; b < 4; b++) {
+                r.b = b;
+                GNS_TRY(rs_pass(sc, st, p[cur], p[cur ^ 1], nu, r));
+                cur ^= 1;
             }
-            std::swap(p0, p1);
             return GNS_OK;
         };
+        // primary order: (value desc, key bytes 0..3); the whole key only when it ties
+        GNS_TRY(sort_by(std::min<uint32_t>(K, 4)));
         if (K > 4) {
-            for (int off = 4 + (int)((K - 4 - 1) / 8) * 8; off >= 4; off -= 8) {
-                const uint32_t nb = std::min<uint32_t>(8u, K - (uint32_t)off);
-                hipLaunchKernelGGL(k_hh_chunk_key, dim3(g), dim3(256), 0, st, p0, sc.bytes, K, (uint32_t)off, nu, k0);
-                GNS_TRY(sort_pass(64u - 8u * nb));
-            }
+            uint32_t tflag = 0;
+            GNS_HIP(hipMemsetAsync(tie, 0, 4, st));
+            hipLaunchKernelGGL(k_hh_ties, dim3(g), dim3(256), 0, st, p[cur], nu, sc.u32b, sc.bytes, K, tie);
+            GNS_HIP(hipMemcpyAsync(&tflag, tie, 4, hipMemcpyDeviceToHost, st));
+            GNS_HIP(hipStreamSynchronize(st));
+            if (tflag) GNS_TRY(sort_by(K));  // the whole key: bytes K-1..0, then the value
         }
-        hipLaunchKernelGGL(k_hh_final_key, dim3(g), dim3(256), 0, st, p0, sc.u32b, sc.bytes, K, nu, k0);
-        GNS_TRY(sort_pass(0u));
-        hipLaunchKernelGGL(k_hh_gather, dim3(g), dim3(256), 0, st, p0, sc.bytes, sc.u32b, K, nu, sc.obytes, sc.u32d);
+        hipLaunchKernelGGL(k_hh_gather, dim3(g), dim3(256), 0, st, p[cur], sc.bytes, sc.u32b, K, nu, sc.obytes, sc.u32d);
         GNS_HIP(hipGetLastError());
         const uint64_t m = std::min<uint64_t>(nu, capn);
         const uint64_t fb = (flows && K) ? m * K : 0, vb = vals ? m * 4 : 0;
@@ -3517,6 +3675,8 @@ int gns_cm_view_create(gns_cm *cm, gns_cm_view **out) {
             hipEventCreateWithFlags(&v->ready, hipEventDisableTiming) != hipSuccess) {
             set_error("view stream/event"); rc = GNS_E_HIP; break;
         }
+        if ((rc = heavy_reserve(v->rd, cells, cm->dict_slots, cm->K, v->stream)) != GNS_OK) break;
+        if (hipStreamSynchronize(v->stream) != hipSuccess) { set_error("view sync"); rc = GNS_E_HIP; break; }
     } while (0);
     if (rc) { view_free(v); delete v; return rc; }
     {

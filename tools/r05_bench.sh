@@ -1,0 +1,39 @@
+#!/bin/bash
+# Round-5 measurement runs (GPU box).  usage: tools/r05_bench.sh <tag> <leg>...
+# legs: default (headline + CPU legs + parity), headline (--no-cpu), ss (SuperSpread +
+# CPU leg + parity), c5, exact, hybrid, host_compact, prof_cm, prof_ss (rocprofv3
+# kernel traces with >= 10 steady full-batch launches).  Every GPU step has its own
+# time limit; the script stops at the first failure.
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+tag=$1; shift
+O=gpurun_out/$tag
+mkdir -p $O
+run() {  # name, seconds, bench args...
+    local n=$1 t=$2
+    shift 2
+    echo "== $n" && timeout -k 10 "$t" python3 bench.py "$@" > $O/$n.json 2> $O/$n.err || { echo "FAIL $n rc=$?"; tail -5 $O/$n.err; exit 1; }
+    tail -c 600 $O/$n.json
+}
+prof() {  # name, seconds, bench args...
+    local n=$1 t=$2
+    shift 2
+    echo "== rocprof $n" && timeout -k 10 "$t" rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$n -o $n -- \
+        python3 bench.py "$@" > $O/prof_$n.log 2>&1 || { echo "FAIL prof $n rc=$?"; tail -5 $O/prof_$n.log; exit 1; }
+    tail -c 300 $O/prof_$n.log
+}
+for leg in "$@"; do
+    case $leg in
+        default) run default 500 ;;
+        headline) run headline 300 --no-cpu ;;
+        ss) run ss 400 --sketch superspread ;;
+        c5) run c5 400 --width 16777216 --depth 8 --no-cpu ;;
+        exact) run exact 300 --sketch exact --no-cpu ;;
+        hybrid) run hybrid 500 --sketch hybrid --no-cpu ;;
+        host_compact) run host_compact 300 --host-input compact --no-cpu ;;
+        prof_cm) prof cm 400 --no-cpu --steps 10 --warmup 5 --windows 0 ;;
+        prof_ss) prof ss 400 --sketch superspread --no-cpu --steps 10 --warmup 5 ;;
+        prof_c5) prof c5 500 --width 16777216 --depth 8 --no-cpu --steps 10 --warmup 5 --windows 0 ;;
+        *) echo "unknown leg $leg"; exit 2 ;;
+    esac || exit 1
+done
+echo done
