@@ -504,6 +504,8 @@ def bench_hybrid(args, torch, dist, world, rank, local):
     cm.flush()
     cm.set_timing(True)
     cm.stage_times(reset=True)
+    ex.agg.set_timing(True)
+    ex.agg.stage_times(reset=True)
     windows = []
     lock = threading.Condition()
     pending = [0]
@@ -551,6 +553,24 @@ def bench_hybrid(args, torch, dist, world, rank, local):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     stages = cm.stage_times()
+    ex_stages = ex.agg.stage_times()
+    # dominant kernel over both engines' stages (HIP events on each engine's stream), at
+    # SURVEY §8d convention A (68 B/packet: each engine reads every record once)
+    kern = {f"cm.{k}": v for k, v in stages.items() if k in ("extract", "resolve", "scan", "scatter", "apply")}
+    kern.update({f"exact.{k}": v for k, v in ex_stages.items() if k in ("extract", "resolve", "partition", "aggregate")})
+    dom = max(kern, key=lambda k: kern[k][0])
+    dom_ms, dom_launches = kern[dom]
+    avg_ms = dom_ms / max(dom_launches, 1)
+    achieved = BYTES_PER_PKT * (n * args.steps / max(dom_launches, 1)) / (avg_ms * 1e-3) / 1e9
+    traffic = None  # PMC record of this workload (tools/r05_pmc.sh hybrid -> profiles/traffic_hybrid_*.json)
+    tfile = os.path.join(ROOT, "profiles", f"traffic_hybrid_d{D}_w{W}_b{args.batch or n}.json")
+    if os.path.exists(tfile):
+        try:
+            key = {"exact.extract": "k_ex_extract", "exact.resolve": "k_ex_resolve", "exact.partition": "k_ex_pscatter",
+                   "exact.aggregate": "k_ex_pagg"}.get(dom, dom.split(".", 1)[1])
+            traffic = json.load(open(tfile)).get(key)
+        except Exception:
+            traffic = None
     line = {
         "metric": "Mpackets/s hybrid exact + CMS d=8 w=2^24 ingest with concurrent heavy-hitter queries",
         "value": round(n * args.steps * world / elapsed / 1e6, 2), "unit": "Mpackets/s", "n_gpus": world,
@@ -565,7 +585,13 @@ def bench_hybrid(args, torch, dist, world, rank, local):
         "queries": {"windows": len(windows), "latency_ms_avg": round(1e3 * sum(lat) / max(len(lat), 1), 3),
                     "latency_ms_max": round(1e3 * max(lat), 3) if lat else None,
                     "last_window_heavy_hitters": {"count": windows[-1][0], "size": windows[-1][1]} if windows else None},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "bytes_per_packet": BYTES_PER_PKT, "kernel_avg_ms": round(avg_ms, 4),
+                     "pipeline_frac": round(2 * BYTES_PER_PKT * n * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4),
+                     "note": "pipeline_frac counts the record stream twice (both engines read it)"},
         "stage_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in stages.items()},
+        "exact_stage_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in ex_stages.items()},
         "note": "not the headline metric",
     }
     view.close()

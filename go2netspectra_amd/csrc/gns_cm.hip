@@ -171,7 +171,19 @@ struct ExtractArgs {
     const uint32_t *Fc, *Fs;  // batch-entry fingerprints (hot slots' owners)
     HotSum *hsum;             // [d*kHot][nblk]
     unsigned long long *stats;
+    // compact streams (CM kernels): per (block, K1 wave, row) the wave's
+    // cold / hot row-updates in packet order, code = bucket (cold) or hot slot (hot)
+    // << 12 | packet index within the wave's 4096-packet range; counts [blk][wave][row][2]
+    uint32_t *cstr, *hstr, *scnt;
+    uint32_t hoff;  // hstr - cstr (words)
 };
+
+// compact streams: a K1 wave owns kCsWave consecutive packets of its block
+constexpr uint32_t kCsWaves = 4;                     // K1 waves per block (256 threads)
+constexpr uint32_t kCsWave = kChunk / kCsWaves;      // packets per K1 wave = stream capacity
+constexpr uint32_t kCsBits = 12;                     // packet index bits in a code
+static_assert(kCsWave == (1u << kCsBits), "a code holds a 12-bit packet index");
+constexpr uint32_t kCsNone = 0xFFFFFFFFu;
 
 template <int KIND, int MODE>
 __device__ __forceinline__ int packet_key(const InputDesc &in, uint32_t K, const uint8_t *s_src,
@@ -251,10 +263,19 @@ struct K1Lds {
     unsigned long long *s_os, *s_fs;
 };
 
+// Wave-uniform running lengths of the wave's compact streams (CM kernels), per row:
+// cold count in the low 16 bits, hot count in the high 16 (each <= kCsWave).
 template <int RMAX>
+struct CsRun {
+    uint32_t ch[RMAX];
+    uint32_t sb;  // stream base of row 0 (uniform)
+};
+
+template <int RMAX, bool CM>
 __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S, uint32_t K, uint32_t d, bool bw,
                                            uint64_t p, uint64_t beg, bool ok, const uint32_t (&kw)[GNS_KWMAX],
-                                           uint32_t slot0, const uint4 (&r4)[4], uint32_t sz, uint32_t &n_ok) {
+                                           uint32_t slot0, const uint4 (&r4)[4], uint32_t sz, uint32_t &n_ok,
+                                           CsRun<RMAX> &cs) {
     uint32_t *s_tab = S.s_tab, *s_hist = S.s_hist, *s_hFc = S.s_hFc, *s_hFs = S.s_hFs, *s_nfc = S.s_nfc;
     uint32_t *s_nfs = S.s_nfs, *s_smax = S.s_smax;
     unsigned long long *s_os = S.s_os, *s_fs = S.s_fs;
@@ -355,8 +376,24 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
             const uint32_t b = bk[rr];
             h = hs[rr];
             // bin code for K3: bucket, or 1<<31 | hot slot for a designated bucket
-            a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
+            if constexpr (!CM) a.idx[(uint64_t)rr * a.n + p] = h >= 0 ? (0x80000000u | (uint32_t)h) : b;
             binid = h >= 0 ? a.g.nbins + rr * kHot + (uint32_t)h : rr * a.g.ntiles + (b >> a.g.bin_bits);
+        }
+        if constexpr (CM) {
+            // compact streams: this wave's cold and hot row-rr updates, appended in packet
+            // order (the wave's lanes hold consecutive packets), so K3 reads only the
+            // updates it partitions and no per-packet code array exists
+            // (the hot streams follow the cold ones in one buffer: hstr = cstr + a.hoff)
+            const bool cold = ok && h < 0, hot = ok && h >= 0;
+            const uint64_t mc = __ballot(cold), mh = __ballot(hot);
+            const uint32_t run = cs.ch[rr];
+            const uint32_t pc = __builtin_amdgcn_mbcnt_hi((uint32_t)(mc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mc, 0u));
+            const uint32_t ph = __builtin_amdgcn_mbcnt_hi((uint32_t)(mh >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mh, 0u));
+            const uint32_t pos = cold ? (run & 0xFFFFu) + pc : a.hoff + (run >> 16) + ph;
+            // packet index within the wave's range: the wave's range starts at a multiple of kCsWave
+            const uint32_t code = (cold ? bk[rr] : (uint32_t)h) << kCsBits | ((uint32_t)p & (kCsWave - 1u));
+            if (ok) a.cstr[cs.sb + rr * kCsWave + pos] = code;
+            cs.ch[rr] = run + (uint32_t)__popcll(mc) + ((uint32_t)__popcll(mh) << 16);
         }
         // heavy bins: one LDS add for the wave's majority bin
         const uint32_t b0 = __builtin_amdgcn_readfirstlane(binid);
@@ -396,21 +433,21 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
 #ifndef GNS_EX_MINW
 #define GNS_EX_MINW 4
 #endif
-// K1 at configs[4]'s geometry (d=8, 5-tuple key), A/B on one box (tools/ab_c5only.sh):
+// K1 at configs[4]'s geometry (d=8, 5-tuple key), A/B on one box (round 2-3 one-off scripts, retired):
 //   two-stage pipeline, 1024 threads: 128 VGPRs + 66 spilled          5.42 ms / 100M
 //   two-stage pipeline,  768 threads: 148 VGPRs, 12 waves per CU      4.47-4.50
 //   plain loop,          768 threads:  92 VGPRs                        4.58-4.59
 //   plain loop,          640 threads (two blocks per CU by LDS)        5.28-5.30
 //   plain loop,         1024 threads:  93 VGPRs, 16 waves per CU      4.01-4.02
 //   plain loop,          512 threads:  95 VGPRs, two blocks per CU    3.52        <- default
-//     (round 3, tools/r03_ab_hagg.sh: same box, base 4.02-4.03; two independent
+//     (round 3, same box, base 4.02-4.03; two independent
 //     blocks per CU overlap one block's LDS set-up / flush and barriers with the
 //     other's loop; the summaries' LDS atomics are what a lone block exposes:
 //     timing ablations without them 4.06 -> 3.50, without the cold-bin histogram
-//     adds 3.60, tools/r03_ab_hist.sh.  Reducing each designated bucket's lanes
+//     adds 3.60.  Reducing each designated bucket's lanes
 //     across the wave before one leader's atomics (tried in round 3) measured slower:
 //     4.46 vs 4.02 here, 2.36 vs 2.22 at d=4; so did size sums as two 32-bit halves,
-//     3.86 vs 3.55 here and 3.28 vs 2.37 at d=4, tools/r03_gpu8.sh.  The plain loop
+//     3.86 vs 3.55 here and 3.28 vs 2.37 at d=4.  The plain loop
 //     at d=4 with five waves per SIMD (GNS_C2_PIPE=0 GNS_EX_MINW=5): 2.49 vs 2.37)
 #ifndef GNS_K1_V4HASH
 #define GNS_K1_V4HASH 1  // A/B: 0 hashes every wave's 5-tuple key generically
@@ -430,8 +467,12 @@ constexpr bool kC2Pipe = GNS_C2_PIPE != 0;  // the two-stage pipeline for d != 8
 // NT = threads per block: 256 (four blocks per CU) when the block's LDS fits four
 // times in a CU, else 1024 (one block of 16 waves: wide or deep sketches, whose
 // histogram and hot-slot tables take more than a quarter of the LDS).
-template <int KIND, int MODE, int KB, int DD, int NT>
+// CM: compact streams instead of the per-packet code array (256-thread blocks only);
+// then each wave takes a contiguous quarter of the block's packets, 64 at a time.
+template <int KIND, int MODE, int KB, int DD, int NT, bool CM = false>
 __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) void k_extract(ExtractArgs a) {
+    static_assert(!CM || NT == 256, "compact streams: four waves per block");
+    constexpr bool WC = CM;  // (the classic outputs with this loop measured the same: 2.38 vs 2.35 ms)
     extern __shared__ __attribute__((aligned(16))) uint8_t xsm[];
     __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_claim;
     __shared__ uint8_t s_src[80];
@@ -463,6 +504,16 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
     const bool bw = a.D.bw != 0;
     uint32_t n_ok = 0;
     const K1Lds S{s_tab, s_hist, s_hFc, s_hFs, s_nfc, s_nfs, s_smax, &s_pend, &s_full, &s_claim, s_os, s_fs};
+    // lane's packets: classic p = beg + tid, beg + tid + NT, ...; CM: the wave's range
+    // [wbeg, wend), p = wbeg + lane, + 64, ...  (wave-uniform trip counts either way)
+    constexpr uint32_t STEP = WC ? 64u : (uint32_t)NT;
+    const uint64_t wbeg = WC ? beg + (uint64_t)(tid >> 6) * (kChunk / (NT / 64)) : beg;
+    const uint64_t wend = WC ? min(end, wbeg + kChunk / (NT / 64)) : end;
+    const uint32_t loff = WC ? (tid & 63u) : tid;
+    CsRun<RMAX> cs;
+#pragma unroll
+    for (uint32_t rr = 0; rr < RMAX; rr++) cs.ch[rr] = 0;
+    cs.sb = (blk * kCsWaves + (tid >> 6)) * d * kCsWave;
     if constexpr (KIND == IN_HDR && (DD == 8 ? kC5Pipe : kC2Pipe)) {
         // Two-stage software pipeline over the block's packets: iteration k
         // parses packet k+1 and issues its dictionary probe (and the header
@@ -472,7 +523,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
         uint4 hv[4];
         uint32_t hsz;
         auto load_hdr = [&](uint64_t q) {
-            const uint64_t pc = min(q, end - 1);
+            const uint64_t pc = min(q, end - 1);  // (end - 1 >= beg: a block has packets)
             const uint4 *r = reinterpret_cast<const uint4 *>(a.in.hdr + pc * 16);
 #pragma unroll
             for (int i = 0; i < 4; i++) hv[i] = r[i];
@@ -481,12 +532,12 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
         // stage B of packet q: parse the prefetched record, key, slot, issue the probe
         auto stage_b = [&](uint64_t q, bool &okq, uint32_t (&kwq)[GNS_KWMAX], uint32_t &slotq, uint4 (&r4q)[4],
                            uint32_t &szq) {
-            okq = q < end;
+            okq = q < wend;
             uint32_t cw[16];
 #pragma unroll
             for (int i = 0; i < 4; i++) { cw[4 * i] = hv[i].x; cw[4 * i + 1] = hv[i].y; cw[4 * i + 2] = hv[i].z; cw[4 * i + 3] = hv[i].w; }
             szq = hsz;
-            load_hdr(q + NT);
+            load_hdr(q + STEP);
             if (okq) {
                 uint32_t tw[10];
                 const int st = parse_record_fast(cw, szq, true, tw);
@@ -523,17 +574,17 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
                 for (int i = 0; i < 4; i++) r4q[i] = (4u * i < a.D.RW) ? rq[i] : make_uint4(0, 0, 0, 0);
             }
         };
-        load_hdr(beg + tid);
+        load_hdr(wbeg + loff);
         bool okc;
         uint32_t kwc[GNS_KWMAX], slotc, szc;
         uint4 r4c[4];
-        stage_b(beg + tid, okc, kwc, slotc, r4c, szc);
-        for (uint64_t p0 = beg; p0 < end; p0 += NT) {  // wave-uniform trip count
+        stage_b(wbeg + loff, okc, kwc, slotc, r4c, szc);
+        for (uint64_t p0 = wbeg; p0 < wend; p0 += STEP) {  // wave-uniform trip count
             bool okn = false;
             uint32_t kwn[GNS_KWMAX], slotn = 0, szn = 0;
             uint4 r4n[4];
-            if (p0 + NT < end) stage_b(p0 + NT + tid, okn, kwn, slotn, r4n, szn);
-            k1_consume<RMAX>(a, S, K, d, bw, p0 + tid, beg, okc, kwc, slotc, r4c, szc, n_ok);
+            if (p0 + STEP < wend) stage_b(p0 + STEP + loff, okn, kwn, slotn, r4n, szn);
+            k1_consume<RMAX, CM>(a, S, K, d, bw, p0 + loff, beg, okc, kwc, slotc, r4c, szc, n_ok, cs);
             okc = okn; slotc = slotn; szc = szn;
 #pragma unroll
             for (int i = 0; i < GNS_KWMAX; i++) kwc[i] = kwn[i];
@@ -541,9 +592,9 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
             for (int i = 0; i < 4; i++) r4c[i] = r4n[i];
         }
     } else {
-        for (uint64_t p0 = beg; p0 < end; p0 += NT) {  // wave-uniform trip count
-            const uint64_t p = p0 + tid;
-            bool ok = p < end;
+        for (uint64_t p0 = wbeg; p0 < wend; p0 += STEP) {  // wave-uniform trip count
+            const uint64_t p = p0 + loff;
+            bool ok = p < wend;
             uint32_t kw[GNS_KWMAX];
             if (ok) {
                 const int st = packet_key<KIND, MODE>(a.in, K, s_src, p, kw);
@@ -565,7 +616,15 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
 #pragma unroll
                 for (int i = 0; i < 4; i++) r4[i] = (4u * i < a.D.RW) ? q[i] : make_uint4(0, 0, 0, 0);
             }
-            k1_consume<RMAX>(a, S, K, d, bw, p, beg, ok, kw, slot0, r4, ok ? a.in.sizes[p] : 0u, n_ok);
+            k1_consume<RMAX, CM>(a, S, K, d, bw, p, beg, ok, kw, slot0, r4, ok ? a.in.sizes[p] : 0u, n_ok, cs);
+        }
+    }
+    if constexpr (CM) {  // the wave's stream lengths
+        if ((tid & 63u) == 0) {
+            uint32_t *sc = a.scnt + ((uint64_t)blk * kCsWaves + (tid >> 6)) * d * 2;
+#pragma unroll
+            for (uint32_t rr = 0; rr < RMAX; rr++)
+                if (rr < d) { sc[rr * 2] = cs.ch[rr] & 0xFFFFu; sc[rr * 2 + 1] = cs.ch[rr] >> 16; }
         }
     }
     atomicAdd(&s_ok, n_ok);
@@ -688,6 +747,8 @@ struct ScatterArgs {
     uint32_t hot_mode;
     const uint32_t *hflag2;
     const uint32_t *hany;
+    // compact streams (k_scatter_cs, k_hot_scatter_cs): K1's per-(block, wave, row) codes
+    const uint32_t *cstr, *hstr, *scnt;
 };
 
 // LDS layout of k_scatter (dynamic): s_cnt[2][kScWaves][LB] (double-buffered), s_goff[d][LB],
@@ -1098,6 +1159,252 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
 #ifdef GNS_K3_PROF
     if (threadIdx.x == 0) for (int i = 0; i < 5; i++) atomicAdd(&a.stats[11 + i], (unsigned long long)k3t[i]);
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// K3c: K3s over K1's compact cold streams.  Per (block, row) the stream is the
+// four K1 waves' cold codes of that row in wave order = packet order, so only
+// the updates that move are read (no per-packet codes, no lanes without an
+// update): sub-passes of kStSub updates, the flow id and size of each gathered
+// from the block's keyid / size words (the K1 block's 64 KB of each stays in
+// L2 across its rows).  Ranks, stage and copy-out as K3s; the output is
+// identical to K3s's.
+// ---------------------------------------------------------------------------
+template <int NT, int BINS>
+__global__ __launch_bounds__(NT) void k_scatter_cs(ScatterArgs a) {
+    constexpr int kStThreads = NT;
+    constexpr int kStWaves = NT / 64;
+    constexpr int kStItems = kStSub / NT;
+    constexpr uint32_t kStBins = BINS;
+    static_assert(kStSub / kStWaves == kStItems * 64, "a wave owns kStItems x 64 consecutive updates of a sub-pass");
+    static_assert(BINS <= NT && BINS % 64 == 0, "one thread per bin in the bin scan");
+    __shared__ StLds<NT, BINS> L;
+    __shared__ uint32_t s_pre[8][kCsWaves + 1];  // per row: the K1 waves' stream starts, then the row total
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t blk = blockIdx.x, d = a.g.d, nt = a.g.ntiles;
+    const uint32_t tmask = (1u << a.g.bin_bits) - 1u;
+    const uint64_t beg = (uint64_t)blk * kChunk;
+    for (uint32_t i = tid; i < d * kStBins; i += kStThreads) {
+        const uint32_t r = i / kStBins, t = i % kStBins;
+        L.goff[r][t] = t < nt ? a.offsets[(uint64_t)blk * a.g.nbins_all + r * nt + t] : 0u;
+    }
+    if (tid < d) {
+        uint32_t run = 0;
+        for (uint32_t w = 0; w < kCsWaves; w++) {
+            s_pre[tid][w] = run;
+            run += a.scnt[(((uint64_t)blk * kCsWaves + w) * d + tid) * 2];
+        }
+        s_pre[tid][kCsWaves] = run;
+    }
+    for (uint32_t i = tid; i < 2 * kStWaves * kStBins; i += kStThreads) (&L.cnt[0][0][0])[i] = 0;
+    __syncthreads();
+    // update j of a sub-pass at stream position x: wave-contiguous, (j, lane) order inside the wave
+    auto spos = [&](uint32_t sp, int j) { return sp + wave * (kStSub / kStWaves) + (uint32_t)j * 64 + lane; };
+    // codes of step (r, sp): bucket << 14 | packet offset in the block (the K1 wave's range
+    // start + the code's index), kCsNone past the row's end
+    auto load_codes = [&](uint32_t r, uint32_t sp, uint32_t (&c)[kStItems], uint32_t (&po)[kStItems]) {
+        const uint32_t p1 = s_pre[r][1], p2 = s_pre[r][2], p3 = s_pre[r][3], tot = s_pre[r][4];
+#pragma unroll
+        for (int j = 0; j < kStItems; j++) {
+            const uint32_t x = spos(sp, j);
+            c[j] = kCsNone;
+            po[j] = 0;
+            if (x < tot) {
+                const uint32_t w = (x >= p1 ? 1u : 0u) + (x >= p2 ? 1u : 0u) + (x >= p3 ? 1u : 0u);
+                const uint32_t x0 = w == 0 ? 0u : (w == 1 ? p1 : (w == 2 ? p2 : p3));
+                c[j] = a.cstr[(((uint64_t)blk * kCsWaves + w) * d + r) * kCsWave + (x - x0)];
+                po[j] = w * kCsWave;
+            }
+        }
+    };
+    auto gather = [&](const uint32_t (&c)[kStItems], const uint32_t (&po)[kStItems], uint32_t (&di)[kStItems],
+                      uint32_t (&ds)[kStItems]) {
+#pragma unroll
+        for (int j = 0; j < kStItems; j++) {
+            const uint64_t pp = beg + po[j] + (c[j] & (kCsWave - 1u));
+            di[j] = c[j] != kCsNone ? a.keyid[pp] : GNS_ID_NONE;
+            ds[j] = c[j] != kCsNone ? a.sizes[pp] : 0u;
+        }
+    };
+    // steps: rows in order, sub-passes of kStSub updates in each
+    uint32_t r = 0, sp = 0;
+    while (r < d && s_pre[r][kCsWaves] == 0) r++;
+    uint32_t cds[kStItems], pos[kStItems], ids[kStItems], szs[kStItems];
+    uint32_t ncd[kStItems], npo[kStItems];
+    if (r < d) {
+        load_codes(r, 0, cds, pos);
+        gather(cds, pos, ids, szs);
+    }
+    uint32_t par = 0;
+    while (r < d) {  // block-uniform
+        // the next step
+        uint32_t r1 = r, sp1 = sp + kStSub;
+        if (sp1 >= s_pre[r1][kCsWaves]) {
+            r1++;
+            sp1 = 0;
+            while (r1 < d && s_pre[r1][kCsWaves] == 0) r1++;
+        }
+        uint32_t (&cnt)[kStWaves][kStBins] = L.cnt[par];
+        // phase A: entries and stable ranks within (wave, bin)
+        uint64_t ent[kStItems];
+        uint32_t tb[kStItems];  // bin << 16 | rank, 0xFFFF bin = no update
+#pragma unroll
+        for (int j = 0; j < kStItems; j++) {
+            const bool valid = cds[j] != kCsNone && ids[j] != GNS_ID_NONE;
+            uint32_t t = 0xFFFFu;
+            uint64_t e = 0;
+            if (valid) {
+                const uint32_t b = cds[j] >> kCsBits;
+                t = b >> a.g.bin_bits;
+                const uint32_t low = b & tmask, sz = szs[j];
+                uint32_t lo = ids[j], sf = sz;
+                if (sz >= kSizeEsc) {
+                    const uint32_t q = atomicAdd(a.ovf_cnt, 1u);
+                    if (q < a.ovf_cap) {
+                        a.ovf[q] = (uint64_t)sz << 32 | ids[j];
+                        lo = kOvfFlag | q;
+                    } else {
+                        atomicAdd(&a.stats[4], 1ull);
+                        lo = kOvfFlag | (a.ovf_cap - 1);
+                    }
+                    sf = kSizeEsc;
+                }
+                e = (uint64_t)((sf << kEntShift) | low) << 32 | lo;
+            }
+            ent[j] = e;
+            tb[j] = t << 16;
+        }
+        {
+            uint32_t rks[kStItems];
+#pragma unroll
+            for (int j = 0; j < kStItems; j++) {
+                const uint32_t t = tb[j] >> 16;
+                uint32_t *ad = t != 0xFFFFu ? &cnt[wave][t] : &L.dummy[tid];
+                rks[j] = atomicAdd(ad, t != 0xFFFFu ? 1u : 0u);
+            }
+#pragma unroll
+            for (int j = 0; j < kStItems; j++) tb[j] |= rks[j];
+        }
+        if (r1 < d) load_codes(r1, sp1, ncd, npo);
+        __syncthreads();
+        // phase C: per bin, prefix over the waves and the bin's total; scan of the totals
+        uint32_t total = 0, incl = 0;
+        if (tid < kStBins) {
+            const uint32_t t = tid;
+            uint32_t run = 0;
+            if (t < nt) {
+#pragma unroll
+                for (int w = 0; w < kStWaves; w++) {
+                    const uint32_t x = cnt[w][t];
+                    cnt[w][t] = run;
+                    run += x;
+                }
+            }
+            total = run;
+            incl = wave_incl_scan(total);
+            if (lane == 63) L.wsum[wave] = incl;
+        }
+        __syncthreads();
+        // the next step's flow ids and sizes (its codes have had phase C to arrive)
+        uint32_t nids[kStItems], nszs[kStItems];
+        if (r1 < d) gather(ncd, npo, nids, nszs);
+        if (tid < kStBins) {
+            uint32_t base = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < kStBins / 64; w++) base += w < wave ? L.wsum[w] : 0u;
+            const uint32_t t = tid;
+            L.lstart[t] = base + incl - total;
+            L.gpos[t] = L.goff[r][t];
+            L.goff[r][t] += total;
+        }
+        __syncthreads();
+        // phase D: updates into the bin-ordered stage
+#pragma unroll
+        for (int j = 0; j < kStItems; j++) {
+            const uint32_t t = tb[j] >> 16;
+            if (t != 0xFFFFu) {
+                const uint32_t q = L.lstart[t] + cnt[wave][t] + (tb[j] & 0xFFFFu);
+                L.stage[q] = ent[j];
+                L.sbin[q] = (uint16_t)t;
+            }
+        }
+        __syncthreads();
+        // phase E: the bins out as contiguous runs; clear this step's counters
+        uint32_t ntot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kStBins / 64; w++) ntot += L.wsum[w];
+        for (uint32_t i = tid; i < ntot; i += kStThreads) {
+            const uint32_t t = L.sbin[i];
+            a.entries[L.gpos[t] + (i - L.lstart[t])] = L.stage[i];
+        }
+        for (uint32_t i = tid; i < kStWaves * kStBins; i += kStThreads) (&cnt[0][0])[i] = 0;
+        par ^= 1u;
+        if (r1 < d) {
+#pragma unroll
+            for (int j = 0; j < kStItems; j++) { cds[j] = ncd[j]; pos[j] = npo[j]; ids[j] = nids[j]; szs[j] = nszs[j]; }
+        }
+        r = r1;
+        sp = sp1;
+    }
+}
+
+// The exact entry path for designated buckets over K1's compact hot streams
+// (k_scatter's hot mode, for the slots k_hot_decide / k_hot_blockcheck flagged):
+// one wave per K1 block walks each row's hot stream in order and writes the
+// flagged slots' updates to their hot bins (ranks by ballot multisplit over the
+// slot).  Rare (cold start, ownership changes); the whole grid exits when no
+// slot is flagged.
+__global__ __launch_bounds__(64) void k_hot_scatter_cs(ScatterArgs a) {
+    __shared__ uint32_t s_base[8 * kHot];
+    if (*a.hany == 0) return;
+    const uint32_t lane = threadIdx.x, blk = blockIdx.x, d = a.g.d;
+    const uint64_t beg = (uint64_t)blk * kChunk;
+    const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+    for (uint32_t i = lane; i < d * kHot; i += 64) s_base[i] = a.offsets[(uint64_t)blk * a.g.nbins_all + a.g.nbins + i];
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t r = 0; r < d; r++) {
+        for (uint32_t w = 0; w < kCsWaves; w++) {
+            const uint64_t sb = (((uint64_t)blk * kCsWaves + w) * d + r) * kCsWave;
+            const uint32_t n = a.scnt[(((uint64_t)blk * kCsWaves + w) * d + r) * 2 + 1];
+            for (uint32_t x0 = 0; x0 < n; x0 += 64) {
+                const uint32_t x = x0 + lane;
+                uint32_t slot = 0, code = 0;
+                bool valid = false;
+                if (x < n) {
+                    code = a.hstr[sb + x];
+                    slot = r * kHot + (code >> kCsBits);
+                    valid = (a.hflag2[slot] & 3u) != 0;
+                }
+                uint64_t peers = __ballot(valid);
+#pragma unroll
+                for (uint32_t bit = 0; bit < kHotBits + 3; bit++) {
+                    const uint64_t m = __ballot(valid && ((slot >> bit) & 1u));
+                    peers &= ((slot >> bit) & 1u) ? m : ~m;
+                }
+                if (valid) {
+                    const uint64_t p = beg + w * kCsWave + (code & (kCsWave - 1u));
+                    const uint32_t id = a.keyid[p], sz = a.sizes[p];
+                    uint32_t lo = id, sf = sz;
+                    if (sz >= kSizeEsc) {
+                        const uint32_t q = atomicAdd(a.ovf_cnt, 1u);
+                        if (q < a.ovf_cap) {
+                            a.ovf[q] = (uint64_t)sz << 32 | id;
+                            lo = kOvfFlag | q;
+                        } else {
+                            atomicAdd(&a.stats[4], 1ull);
+                            lo = kOvfFlag | (a.ovf_cap - 1);
+                        }
+                        sf = kSizeEsc;
+                    }
+                    const uint32_t pos = s_base[slot] + (uint32_t)__popcll(peers & lt);
+                    a.entries[pos] = (uint64_t)((sf << kEntShift) | slot) << 32 | lo;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (valid && __popcll(peers & lt) == 0) s_base[slot] += (uint32_t)__popcll(peers);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
 }
 
 // Does a returning LDS add serve the same-address lanes of one wave
@@ -1879,6 +2186,7 @@ struct HotArgs {
     uint32_t chk_cap;
     const uint32_t *keyid, *idx, *sizes;
     uint64_t n;
+    const uint32_t *hstr, *scnt;  // compact hot streams (CM kernels), or null: per-packet codes in idx
 };
 
 __device__ __forceinline__ void hot_bin_range(const HotArgs &a, uint32_t hb, uint32_t &beg, uint32_t &end) {
@@ -2142,16 +2450,36 @@ __global__ __launch_bounds__(256) void k_hot_blockcheck(HotArgs a) {
     long long run = (long long)((unsigned long long)c.z | (unsigned long long)c.w << 32);
     const uint64_t beg = (uint64_t)blk * kChunk, end = min(a.n, beg + kChunk);
     const uint32_t *idxr = a.idx + (uint64_t)r * a.n;
+    // compact streams: walk the block's row-r hot stream (its K1 waves in order = packet
+    // order) instead of every packet's code
+    uint32_t spre[kCsWaves + 1] = {0, 0, 0, 0, 0};
+    if (a.hstr) {
+        for (uint32_t w = 0; w < kCsWaves; w++)
+            spre[w + 1] = spre[w] + a.scnt[(((uint64_t)blk * kCsWaves + w) * a.g.d + r) * 2 + 1];
+    }
+    const uint64_t lim = a.hstr ? (uint64_t)spre[kCsWaves] : end - beg;
     bool ev = false;
-    for (uint64_t q0 = beg; q0 < end; q0 += 1024) {  // 4 consecutive packets per thread
+    for (uint64_t q0 = 0; q0 < lim; q0 += 1024) {  // 4 consecutive packets (stream entries) per thread
         long long dl[4], tl = 0;
         bool fo[4];
         uint32_t sv[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const uint64_t p = q0 + tid * 4 + i;
+            const uint64_t x = q0 + tid * 4 + i;
+            uint64_t p = beg + x;
+            bool hit = false;
+            if (x < lim) {
+                if (a.hstr) {
+                    const uint32_t w = (x >= spre[1] ? 1u : 0u) + (x >= spre[2] ? 1u : 0u) + (x >= spre[3] ? 1u : 0u);
+                    const uint32_t cc = a.hstr[(((uint64_t)blk * kCsWaves + w) * a.g.d + r) * kCsWave + (x - spre[w])];
+                    p = beg + w * kCsWave + (cc & (kCsWave - 1u));
+                    hit = (cc >> kCsBits) == slot % kHot;
+                } else {
+                    hit = idxr[p] == code;
+                }
+            }
             dl[i] = 0; fo[i] = false; sv[i] = 0;
-            if (p < end && idxr[p] == code && a.keyid[p] != GNS_ID_NONE) {
+            if (hit && a.keyid[p] != GNS_ID_NONE) {
                 const uint32_t s = a.sizes[p];
                 const bool own = a.keyid[p] == Fs0;
                 dl[i] = own ? (long long)s : -(long long)s;
@@ -2662,6 +2990,12 @@ struct gns_cm {
     bool warm = false;                    // a batch has run since create/reset
     bool lds_ordered = false;             // k_lds_order_probe passed: K3 ranks by LDS adds
     bool k3_staged = true;                // K3s (LDS-staged runs) where the geometry allows; GNS_K3_STAGED=0: K3
+    // compact streams (K1 -> K3c): off by default (K3 -0.31 ms, K1 +0.51 ms
+    // at the bench geometry); GNS_CMODE=1 turns them on where the geometry allows
+    // (256-thread K1, K3s rows, buckets < 2^20)
+    bool cmode = false;
+    uint32_t *hstr = nullptr;             // [nblk][4][d][4096] hot codes (cold codes live in idx)
+    uint32_t *scnt = nullptr;             // [nblk][4][d][2] stream lengths
     uint32_t *h_pin = nullptr;            // pinned host mirror of small counters
     // staging for host inputs: two device buffers; batch i+1's H2D copies run on
     // cstream while batch i computes on `stream` (events order the reuse)
@@ -2726,7 +3060,7 @@ int set_dev(gns_cm *cm) {
 int cm_free_all(gns_cm *cm) {
     dfree(cm->C); dfree(cm->S); dfree(cm->Fc); dfree(cm->Fs); cm->rd.free_all();
     dfree(cm->D.rec);
-    dfree(cm->keyid); dfree(cm->idx);
+    dfree(cm->keyid); dfree(cm->idx); dfree(cm->scnt);  // hstr lives in idx
     dfree(cm->pend[0]); dfree(cm->pend[1]); dfree(cm->pcnt[0]); dfree(cm->pcnt[1]);
     dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
     dfree(cm->entries); dfree(cm->entries2); dfree(cm->soff); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats);
@@ -2821,13 +3155,22 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.pend_total = cm->ptotal; a.hist = cm->hist; a.nblk = nblk; a.hot_ids = cm->hot_ids;
         a.Fc = cm->Fc; a.Fs = cm->Fs; a.hsum = cm->hsum; a.hot_tab = cm->hot_tab;
         a.stats = cm->stats;
+        a.cstr = cm->idx; a.hstr = cm->hstr; a.scnt = cm->scnt; a.hoff = (uint32_t)(cm->hstr - cm->idx);
         ScopedStage st(cm->timer, 0);
         const size_t lds = extract_lds_bytes(g.nbins_all, g.d);
+        // 256-thread K1: with compact streams when the handle uses them
+#define GNS_K1_256(KB_, DD_)                                                                                   \
+    do {                                                                                                       \
+        if (cm->cmode)                                                                                         \
+            hipLaunchKernelGGL((k_extract<KIND, MODE, KB_, DD_, 256, true>), dim3(nblk), dim3(256), lds, s, a); \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_extract<KIND, MODE, KB_, DD_, 256>), dim3(nblk), dim3(kExThreads), lds, s, a); \
+    } while (0)
         if constexpr (KIND == IN_REC16) {  // PCIe-bound host path: runtime key width and depth
             if (lds > kExLdsSmall)
                 hipLaunchKernelGGL((k_extract<KIND, MODE, 0, 0, 1024>), dim3(nblk), dim3(1024), lds, s, a);
             else
-                hipLaunchKernelGGL((k_extract<KIND, MODE, 0, 0, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
+                GNS_K1_256(0, 0);
         } else if (lds > kExLdsSmall) {  // deep / wide sketch: one large block per CU
             // configs[4] (d=8, 5-tuple): the plain loop, two 512-thread blocks per CU
             // (see kC5Threads)
@@ -2840,15 +3183,16 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
             else
                 hipLaunchKernelGGL((k_extract<KIND, MODE, 0, 0, 1024>), dim3(nblk), dim3(1024), lds, s, a);
         } else if (cm->K == 37 && g.d == 4)
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 4, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
+            GNS_K1_256(37, 4);
         else if (cm->K == 37)
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 37, 0, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
+            GNS_K1_256(37, 0);
         else if (cm->K == 16 && g.d == 4)
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 16, 4, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
+            GNS_K1_256(16, 4);
         else if (cm->K == 16)
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 16, 0, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
+            GNS_K1_256(16, 0);
         else
-            hipLaunchKernelGGL((k_extract<KIND, MODE, 0, 0, 256>), dim3(nblk), dim3(kExThreads), lds, s, a);
+            GNS_K1_256(0, 0);
+#undef GNS_K1_256
         GNS_HIP(hipGetLastError());
     }
     // K1b: resolve parked packets until none remain.  The first round is queued
@@ -2914,8 +3258,11 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
         a.ovf_cnt = cm->ovf_cnt; a.ovf_cap = (uint32_t)cm->ovf_cap; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
         a.hot_mode = 0; a.hflag2 = cm->hflag2; a.hany = cm->hflag2 + g.d * kHot;
+        a.cstr = cm->idx; a.hstr = cm->hstr; a.scnt = cm->scnt;
         ScopedStage st(cm->timer, 3);
-        if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 256 && g.d <= 8)
+        if (cm->cmode)
+            hipLaunchKernelGGL((k_scatter_cs<1024, 256>), dim3(nblk), dim3(1024), 0, s, a);
+        else if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 256 && g.d <= 8)
             hipLaunchKernelGGL((k_scatter_st<1024, 256>), dim3(nblk), dim3(1024), 0, s, a);
         else if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 512 && g.d <= 8)
             hipLaunchKernelGGL((k_scatter_st<512, 512>), dim3(nblk), dim3(512), 0, s, a);
@@ -2956,6 +3303,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         h.hsum = cm->hsum; h.hflag2 = cm->hflag2; h.hany = cm->hflag2 + g.d * kHot; h.nchk = h.hany + 1;
         h.hres = cm->hres; h.chk = cm->chk; h.chk_cap = kChkCap;
         h.keyid = cm->keyid; h.idx = cm->idx; h.sizes = in.sizes; h.n = n;
+        h.hstr = cm->cmode ? cm->hstr : nullptr; h.scnt = cm->scnt;
         ScopedStage st(cm->timer, 6);
         GNS_HIP(hipMemsetAsync(cm->hflag, 0, (size_t)g.d * kHot * 4, s));
         // summary path: decide, exact block checks, commit
@@ -2969,7 +3317,10 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
             a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
             a.ovf_cnt = cm->ovf_cnt; a.ovf_cap = (uint32_t)cm->ovf_cap; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
             a.hot_mode = 1; a.hflag2 = cm->hflag2; a.hany = h.hany;
-            if (cm->lds_ordered)
+            a.cstr = cm->idx; a.hstr = cm->hstr; a.scnt = cm->scnt;
+            if (cm->cmode)
+                hipLaunchKernelGGL(k_hot_scatter_cs, dim3(nblk), dim3(64), 0, s, a);
+            else if (cm->lds_ordered)
                 hipLaunchKernelGGL(k_scatter<1>, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
             else
                 hipLaunchKernelGGL(k_scatter<0>, dim3(nblk), dim3(kScThreads), scatter_lds_bytes(g.ntiles + kHot, g.d), s, a);
@@ -3302,6 +3653,16 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             cm->lds_ordered = hv == 0 && !(env && env[0] == '0');
             const char *es = getenv("GNS_K3_STAGED");
             cm->k3_staged = !(es && es[0] == '0');
+            const char *ec = getenv("GNS_CMODE");
+            cm->cmode = ec && ec[0] == '1' && cm->lds_ordered && cm->k3_staged && g.ntiles <= 256 && g.d <= 8 &&
+                        extract_lds_bytes(g.nbins_all, g.d) <= kExLdsSmall && g.w <= (1u << (32 - kCsBits));
+            if (cm->cmode) {  // the hot streams after the cold ones (K1 addresses both from one base)
+                dfree(cm->idx);
+                cm->idx = nullptr;
+                if ((rc = dalloc_t(&cm->idx, 2 * cm->bmax * g.d)) != GNS_OK) break;
+                cm->hstr = cm->idx + cm->bmax * g.d;
+                if ((rc = dalloc_t(&cm->scnt, (uint64_t)cm->nblk_max * kCsWaves * g.d * 2)) != GNS_OK) break;
+            }
         }
         // the read side's heavy-hitter buffers (a window's first call allocates nothing)
         if ((rc = heavy_reserve(cm->rd, (uint64_t)cm->g.d * cm->g.w, cm->dict_slots, cm->K, cm->stream)) != GNS_OK) break;

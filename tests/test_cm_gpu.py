@@ -530,3 +530,47 @@ def test_heavy_hitters_beyond_2p26_candidates(gpu):
         got = np.ascontiguousarray(f[:, :4]).view(">u4").reshape(-1).astype(np.int64)
         bad = np.flatnonzero((got != wk) | (v.astype(np.int64) != wv))
         assert len(bad) == 0, f"first difference at {bad[0]}: got {got[bad[0]]},{v[bad[0]]} want {wk[bad[0]]},{wv[bad[0]]}"
+
+
+@pytest.mark.parametrize("w,d,K,nflows,n,batch", [
+    (65536, 4, 37, 50_000, 1_000_000, 0),
+    (256, 2, 16, 2000, 100_000, 0),
+    (1000, 3, 13, 5000, 200_000, 70_000),
+    (1 << 20, 4, 37, 1 << 18, 2_000_000, 0),
+])
+def test_compact_streams_parity(gpu, oracle, monkeypatch, w, d, K, nflows, n, batch):
+    """K1's compact cold / hot streams and K3c (GNS_CMODE=1, the measured A/B variant of
+    DESIGN §10): the same bit-exact state as the per-packet code array."""
+    monkeypatch.setenv("GNS_CMODE", "1")
+    rng = np.random.default_rng(w + 11 * d)
+    cm, orc = make_pair(oracle, w, d, K, batch_packets=batch)
+    keys, _, _ = zipf_keys(rng, n, nflows, K)
+    sizes = sizes_u32(rng, n, big_frac=0.01)
+    cm.insert_keys(keys, sizes)
+    cm.flush()
+    orc.insert_keys(keys, sizes)
+    assert_same_state(cm, orc)
+    hh = cm.heavy_hitters()
+    assert_same_list([(x.Flow, x.Count) for x in hh.Count], orc.heavy("count"))
+
+
+@pytest.mark.parametrize("w", [16, 4096])
+def test_compact_streams_hot_fallbacks(gpu, oracle, monkeypatch, w):
+    """Ownership changes of designated buckets with compact streams: the block checks and
+    the exact entry path read K1's hot streams (k_hot_blockcheck, k_hot_scatter_cs)."""
+    monkeypatch.setenv("GNS_CMODE", "1")
+    rng = np.random.default_rng(100 + w)
+    cm, orc = make_pair(oracle, w, 2, 8, st=1 << 20, ct=100)
+    flows = rng.integers(0, 256, (40, 8), dtype=np.uint8)
+    for phase in range(5):
+        m = 300_000
+        heavy = np.full(m, phase % len(flows))
+        idx = np.where(rng.random(m) < 0.7, heavy, rng.integers(0, len(flows), m))
+        keys = np.ascontiguousarray(flows[idx])
+        sizes = sizes_u32(rng, m)
+        if phase == 3:
+            sizes[::7] = rng.integers(1 << 21, 1 << 31, len(sizes[::7]))
+        cm.insert_keys(keys, sizes)
+        orc.insert_keys(keys, sizes)
+        cm.flush()
+        assert_same_state(cm, orc)
