@@ -679,22 +679,31 @@ def bench_windows(args, torch, dist, world, cm, timed_step, n):
     (gns_cm_heavy_hitters: candidates, dedupe, order) and all-gathers every
     shard's list over RCCL (dist.allgather_heavy_arrays; flows are disjoint across
     shards, so the union is the global list).  Max over ranks, like the steps."""
-    from go2netspectra_amd.dist import allgather_heavy_arrays
+    from go2netspectra_amd.dist import allgather_heavy_arrays, allgather_heavy_rows
+    device_rows = world > 1 and dist.get_backend() == "nccl"  # RCCL: the lists never leave the GPUs
     t_ins = t_hh = t_x = 0.0
-    arrs = cm.heavy_hitters_arrays()  # warm: the read side's grow-only buffers
-    if world > 1:
-        allgather_heavy_arrays(arrs, world)
+    if device_rows:  # warm: the read side's buffers, the sort's scratch
+        allgather_heavy_rows(cm, world)
+    else:
+        arrs = cm.heavy_hitters_arrays()
+        if world > 1:
+            allgather_heavy_arrays(arrs, world)
     for _ in range(args.windows):
         for _ in range(args.window_steps):
             t_ins += timed_step()
         if world > 1:
             dist.barrier()
         b = time.perf_counter()
-        arrs = cm.heavy_hitters_arrays()
-        c = time.perf_counter()
-        if world > 1:
-            arrs = allgather_heavy_arrays(arrs, world)
+        if device_rows:  # device list + all-gather + device merge + one D2H, timed as the exchange
+            c = time.perf_counter()
+            arrs = allgather_heavy_rows(cm, world)
             dist.barrier()
+        else:
+            arrs = cm.heavy_hitters_arrays()
+            c = time.perf_counter()
+            if world > 1:
+                arrs = allgather_heavy_arrays(arrs, world)
+                dist.barrier()
         e = time.perf_counter()
         t_hh += c - b
         t_x += e - c
@@ -709,8 +718,9 @@ def bench_windows(args, torch, dist, world, cm, timed_step, n):
             "ms_per_window": round(el / W * 1e3, 3), "insert_ms": round(t_ins / W * 1e3, 3),
             "heavy_hitters_ms": round(t_hh / W * 1e3, 3), "exchange_ms": round(t_x / W * 1e3, 3),
             "global_heavy_hitters": {"count": int(len(arrs[1])), "size": int(len(arrs[3]))},
-            "collective": ("all-gather of packed (flow | value) rows, " + dist.get_backend()) if world > 1
-            else "none (one shard: the device list is already the global one)"}
+            "collective": ("all-gather of packed (flow | value) rows, " + dist.get_backend()
+                           + (", lists kept on the GPUs, merged by the device sort" if device_rows else ""))
+            if world > 1 else "none (one shard: the device list is already the global one)"}
 
 
 def main():

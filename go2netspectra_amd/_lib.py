@@ -41,7 +41,7 @@ EXPORTED = [
     "gns_cm_dict_stats", "gns_ss_dict_stats", "gns_ex_dict_stats", "gns_cm_reclaim", "gns_ss_reclaim",
     "gns_cm_insert_compact", "gns_pack_pcap_compact", "gns_compact_headers", "gns_route_partition_async",
     "gns_route_owner_fields", "gns_route_create_keyed", "gns_route_owner_layout", "gns_route_owner_keys",
-    "gns_device_alloc", "gns_device_free",
+    "gns_device_alloc", "gns_device_free", "gns_cm_heavy_rows", "gns_hh_order_rows",
 ]
 
 
@@ -172,6 +172,8 @@ def load() -> ct.CDLL:
         "gns_route_owner_layout": ([vp, vp], i32),
         "gns_route_owner_keys": ([vp, vp, vp, u32, u64, vp, i32], i32),
         "gns_device_alloc": ([u64, i32, vp], i32), "gns_device_free": ([vp, i32], i32),
+        "gns_cm_heavy_rows": ([vp, vp, vp, vp, vp], i32),
+        "gns_hh_order_rows": ([vp, u32, u64, vp, i32], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

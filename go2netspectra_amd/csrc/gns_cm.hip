@@ -2730,16 +2730,32 @@ __global__ __launch_bounds__(256) void k_hh_emit(const uint64_t *cand, uint32_t 
     }
 }
 
+// A heavy-hitter list on the device: entry e has flow bytes ub[e*stride .. +K) and
+// a value, uval[e] -- or, for packed rows [flow | u32 value] (uval null), the
+// little-endian word at ub[e*stride + K].
+struct HhSrc {
+    const uint32_t *uval;
+    const uint8_t *ub;
+    uint32_t K, stride;
+};
+__device__ __forceinline__ uint32_t hh_val(const HhSrc &h, uint32_t e) {
+    if (h.uval) return h.uval[e];
+    const uint8_t *q = h.ub + (uint64_t)e * h.stride + h.K;
+    return (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
+}
+__device__ __forceinline__ uint32_t hh_byte(const HhSrc &h, uint32_t e, uint32_t b) {
+    return b < h.K ? (uint32_t)h.ub[(uint64_t)e * h.stride + b] : 0u;
+}
+
 // One radix pass's digit of entry e: mode 0 = byte `b` of the value, inverted
 // (descending); mode 1 = key byte b (0 beyond K).
 struct RsDigit {
-    uint32_t mode, b, K;
-    const uint32_t *uval;
-    const uint8_t *ub;
+    uint32_t mode, b;
+    HhSrc src;
 };
 __device__ __forceinline__ uint32_t rs_digit(const RsDigit &r, uint32_t e) {
-    if (r.mode == 0) return 255u - ((r.uval[e] >> (8u * r.b)) & 255u);
-    return r.b < r.K ? (uint32_t)r.ub[(uint64_t)e * r.K + r.b] : 0u;
+    if (r.mode == 0) return 255u - ((hh_val(r.src, e) >> (8u * r.b)) & 255u);
+    return hh_byte(r.src, e, r.b);
 }
 
 constexpr uint32_t kRsPer = 16;                 // entries per thread
@@ -2818,14 +2834,13 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t *perm, uint32
 
 // Whether two neighbours of the primary order tie on (value, key bytes 0..3):
 // only then does the list need the whole-key order.
-__global__ __launch_bounds__(256) void k_hh_ties(const uint32_t *perm, uint32_t n, const uint32_t *uval,
-                                                 const uint8_t *ub, uint32_t K, uint32_t *flag) {
+__global__ __launch_bounds__(256) void k_hh_ties(const uint32_t *perm, uint32_t n, HhSrc h, uint32_t *flag) {
     const uint32_t j = blockIdx.x * 256 + threadIdx.x + 1;
     if (j >= n) return;
     const uint32_t a = perm[j - 1], b = perm[j];
-    if (uval[a] != uval[b]) return;
+    if (hh_val(h, a) != hh_val(h, b)) return;
     bool eq = true;
-    for (uint32_t t = 0; t < 4 && t < K; t++) eq = eq && ub[(uint64_t)a * K + t] == ub[(uint64_t)b * K + t];
+    for (uint32_t t = 0; t < 4 && t < h.K; t++) eq = eq && hh_byte(h, a, t) == hh_byte(h, b, t);
     if (eq) atomicOr(flag, 1u);
 }
 
@@ -2834,14 +2849,22 @@ __global__ __launch_bounds__(256) void k_hh_iota(uint32_t *perm, uint32_t n) {
     if (j < n) perm[j] = j;
 }
 
-// ordered output rows: flow bytes and values in list order (one D2H each)
-__global__ __launch_bounds__(256) void k_hh_gather(const uint32_t *perm, const uint8_t *ub, const uint32_t *uval,
-                                                   uint32_t K, uint32_t n, uint8_t *ob, uint32_t *ov) {
+// ordered output: flow bytes and values in list order (one D2H each), or packed
+// rows [flow | u32 value] (rows non-null: the multi-GPU exchange keeps them on the device)
+__global__ __launch_bounds__(256) void k_hh_gather(const uint32_t *perm, HhSrc h, uint32_t n, uint8_t *ob,
+                                                   uint32_t *ov, uint8_t *rows) {
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
     if (j >= n) return;
-    const uint32_t u = perm[j];
-    for (uint32_t t = 0; t < K; t++) ob[(uint64_t)j * K + t] = ub[(uint64_t)u * K + t];
-    ov[j] = uval[u];
+    const uint32_t u = perm[j], K = h.K;
+    const uint32_t v = hh_val(h, u);
+    if (rows) {
+        uint8_t *o = rows + (uint64_t)j * (K + 4);
+        for (uint32_t t = 0; t < K; t++) o[t] = hh_byte(h, u, t);
+        o[K] = (uint8_t)v; o[K + 1] = (uint8_t)(v >> 8); o[K + 2] = (uint8_t)(v >> 16); o[K + 3] = (uint8_t)(v >> 24);
+        return;
+    }
+    for (uint32_t t = 0; t < K; t++) ob[(uint64_t)j * K + t] = hh_byte(h, u, t);
+    ov[j] = v;
 }
 
 __global__ __launch_bounds__(256) void k_hh_candidates(const uint32_t *val, const uint32_t *fp,
@@ -3642,7 +3665,9 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             if ((rc = dalloc_t(&viol, 1)) != GNS_OK) break;
             hipError_t e = hipMemsetAsync(viol, 0, 4, cm->stream);
             if (e == hipSuccess) {
-                hipLaunchKernelGGL(k_lds_order_probe, dim3(64), dim3(256), 0, cm->stream, viol, 32);
+                // every CU of every XCD several times over (4 blocks per CU, 64 rounds of random
+                // same-address groups each): ~1 ms at create
+                hipLaunchKernelGGL(k_lds_order_probe, dim3(4 * cm->ncu), dim3(256), 0, cm->stream, viol, 64);
                 e = hipGetLastError();
             }
             uint32_t hv = 1;
@@ -3886,8 +3911,54 @@ static int rs_pass(CmScratch &sc, hipStream_t st, const uint32_t *in, uint32_t *
     return GNS_OK;
 }
 
+// Canonical order of n entries of a device list (value desc, flow bytes asc) -> *perm_out
+// (a device array of sc's): stable LSD radix passes by (value desc, key bytes 0..3), and by
+// the whole key only when two neighbours tie on that.
+static int hh_sort(CmScratch &sc, hipStream_t st, const HhSrc &src, uint32_t n, uint32_t **perm_out) {
+    const unsigned g = (n + 255) / 256;
+    const uint32_t K = src.K;
+    GNS_TRY(grow_buf(&sc.u32c, sc.u32c_n, (uint64_t)n * 2));
+    const uint32_t nblk = (n + kRsBlock - 1) / kRsBlock, ngrp = (nblk + kTGrp - 1) / kTGrp;
+    GNS_TRY(grow_buf(&sc.rsh, sc.rsh_n, (uint64_t)(nblk + ngrp + 1) * 256 + 4));
+    uint32_t *tie = sc.rsh + (size_t)(nblk + ngrp + 1) * 256 + 1;
+    uint32_t *p[2] = {sc.u32c, sc.u32c + n};
+    int cur = 0;
+    // LSD: key bytes hi-1..0 (the last first), then the value (least significant byte first,
+    // inverted: descending) -> (value desc, key bytes 0..hi-1 asc)
+    auto sort_by = [&](uint32_t hi) -> int {
+        hipLaunchKernelGGL(k_hh_iota, dim3(g), dim3(256), 0, st, p[0], n);
+        cur = 0;
+        RsDigit r{1, 0, src};
+        for (int b = (int)hi - 1; b >= 0; b--) {
+            r.b = (uint32_t)b;
+            GNS_TRY(rs_pass(sc, st, p[cur], p[cur ^ 1], n, r));
+            cur ^= 1;
+        }
+        r.mode = 0;
+        for (uint32_t b = 0; b < 4; b++) {
+            r.b = b;
+            GNS_TRY(rs_pass(sc, st, p[cur], p[cur ^ 1], n, r));
+            cur ^= 1;
+        }
+        return GNS_OK;
+    };
+    GNS_TRY(sort_by(std::min<uint32_t>(K, 4)));
+    if (K > 4) {
+        uint32_t tflag = 0;
+        GNS_HIP(hipMemsetAsync(tie, 0, 4, st));
+        hipLaunchKernelGGL(k_hh_ties, dim3(g), dim3(256), 0, st, p[cur], n, src, tie);
+        GNS_HIP(hipMemcpyAsync(&tflag, tie, 4, hipMemcpyDeviceToHost, st));
+        GNS_HIP(hipStreamSynchronize(st));
+        if (tflag) GNS_TRY(sort_by(K));  // the whole key: bytes K-1..0, then the value
+    }
+    *perm_out = p[cur];
+    return GNS_OK;
+}
+
+// rows_dev non-null: the ordered list as packed device rows [flow | u32 value] (capacity
+// *n_io rows), no host copy; else flows / vals on the host.
 static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_t *val, const uint32_t *fp,
-                        uint32_t thr, uint8_t *flows, uint32_t *vals, uint64_t *n_io) {
+                        uint32_t thr, uint8_t *flows, uint32_t *vals, uint64_t *n_io, uint8_t *rows_dev = nullptr) {
     const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
     const uint32_t K = cm->K;
     GNS_TRY(heavy_reserve(sc, cells, cm->dict_slots, K, st));
@@ -3936,44 +4007,20 @@ static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_
         const uint32_t Kb = K ? K : 1;
         GNS_TRY(grow_buf(&sc.bytes, sc.bytes_n, (uint64_t)nu * Kb));
         GNS_TRY(grow_buf(&sc.obytes, sc.obytes_n, (uint64_t)nu * Kb));
-        GNS_TRY(grow_buf(&sc.u32c, sc.u32c_n, (uint64_t)nu * 2));
         GNS_TRY(grow_buf(&sc.u32d, sc.u32d_n, (uint64_t)nu));
-        const uint32_t nblk = (nu + kRsBlock - 1) / kRsBlock, ngrp = (nblk + kTGrp - 1) / kTGrp;
-        GNS_TRY(grow_buf(&sc.rsh, sc.rsh_n, (uint64_t)(nblk + ngrp + 1) * 256 + 4));
-        uint32_t *tie = sc.rsh + (size_t)(nblk + ngrp + 1) * 256 + 1;
         if (K) hipLaunchKernelGGL(k_ids_to_bytes, dim3(g), dim3(256), 0, st, sc.u32a, (uint64_t)nu, cm->D, sc.bytes);
-        uint32_t *p[2] = {sc.u32c, sc.u32c + nu};
-        int cur = 0;
-        // LSD: key bytes hi-1..0 (the last first), then the value (least significant byte first,
-        // inverted: descending) -> (value desc, key bytes 0..hi-1 asc)
-        auto sort_by = [&](uint32_t hi) -> int {
-            hipLaunchKernelGGL(k_hh_iota, dim3(g), dim3(256), 0, st, p[0], nu);
-            cur = 0;
-            RsDigit r{1, 0, K, sc.u32b, sc.bytes};
-            for (int b = (int)hi - 1; b >= 0; b--) {
-                r.b = (uint32_t)b;
-                GNS_TRY(rs_pass(sc, st, p[cur], p[cur ^ 1], nu, r));
-                cur ^= 1;
-            }
-            r.mode = 0;
-            for (uint32_t b = 0; b < 4; b++) {
-                r.b = b;
-                GNS_TRY(rs_pass(sc, st, p[cur], p[cur ^ 1], nu, r));
-                cur ^= 1;
+        const HhSrc src{sc.u32b, sc.bytes, K, K};
+        uint32_t *perm = nullptr;
+        GNS_TRY(hh_sort(sc, st, src, nu, &perm));
+        if (rows_dev) {
+            if (nu <= capn) {
+                hipLaunchKernelGGL(k_hh_gather, dim3(g), dim3(256), 0, st, perm, src, nu, nullptr, nullptr, rows_dev);
+                GNS_HIP(hipGetLastError());
+                GNS_HIP(hipStreamSynchronize(st));
             }
             return GNS_OK;
-        };
-        // primary order: (value desc, key bytes 0..3); the whole key only when it ties
-        GNS_TRY(sort_by(std::min<uint32_t>(K, 4)));
-        if (K > 4) {
-            uint32_t tflag = 0;
-            GNS_HIP(hipMemsetAsync(tie, 0, 4, st));
-            hipLaunchKernelGGL(k_hh_ties, dim3(g), dim3(256), 0, st, p[cur], nu, sc.u32b, sc.bytes, K, tie);
-            GNS_HIP(hipMemcpyAsync(&tflag, tie, 4, hipMemcpyDeviceToHost, st));
-            GNS_HIP(hipStreamSynchronize(st));
-            if (tflag) GNS_TRY(sort_by(K));  // the whole key: bytes K-1..0, then the value
         }
-        hipLaunchKernelGGL(k_hh_gather, dim3(g), dim3(256), 0, st, p[cur], sc.bytes, sc.u32b, K, nu, sc.obytes, sc.u32d);
+        hipLaunchKernelGGL(k_hh_gather, dim3(g), dim3(256), 0, st, perm, src, nu, sc.obytes, sc.u32d, nullptr);
         GNS_HIP(hipGetLastError());
         const uint64_t m = std::min<uint64_t>(nu, capn);
         const uint64_t fb = (flows && K) ? m * K : 0, vb = vals ? m * 4 : 0;
@@ -4000,6 +4047,47 @@ int gns_cm_heavy_hitters(gns_cm *cm, uint8_t *count_flows, uint32_t *counts, uin
     GNS_HIP(hipStreamSynchronize(cm->stream));
     GNS_TRY(cm_heavy_one(cm, cm->stream, cm->rd, cm->C, cm->Fc, cm->ct, count_flows, counts, n_count));
     GNS_TRY(cm_heavy_one(cm, cm->stream, cm->rd, cm->S, cm->Fs, cm->st, size_flows, sizes, n_size));
+    return GNS_OK;
+}
+
+int gns_cm_heavy_rows(gns_cm *cm, uint8_t *count_rows, uint64_t *n_count, uint8_t *size_rows, uint64_t *n_size) {
+    if (!cm || !n_count || !n_size || (*n_count && !count_rows) || (*n_size && !size_rows)) {
+        set_error("null argument"); return GNS_E_ARG;
+    }
+    GNS_TRY(set_dev(cm));
+    GNS_HIP(hipStreamSynchronize(cm->stream));
+    uint8_t dummy_c = 0, dummy_s = 0;  // a zero-capacity call only reports the lengths
+    GNS_TRY(cm_heavy_one(cm, cm->stream, cm->rd, cm->C, cm->Fc, cm->ct, nullptr, nullptr, n_count,
+                         count_rows ? count_rows : &dummy_c));
+    GNS_TRY(cm_heavy_one(cm, cm->stream, cm->rd, cm->S, cm->Fs, cm->st, nullptr, nullptr, n_size,
+                         size_rows ? size_rows : &dummy_s));
+    return GNS_OK;
+}
+
+// per device, per host thread: the sort scratch of gns_hh_order_rows (grow-only)
+static thread_local std::vector<CmScratch *> t_hh_scratch;
+
+int gns_hh_order_rows(const uint8_t *rows, uint32_t key_bytes, uint64_t n, uint8_t *out_rows, int device) {
+    if ((n && (!rows || !out_rows)) || key_bytes > 37) { set_error("bad argument"); return GNS_E_ARG; }
+    if (n >= (1ull << 31)) { set_error("%llu rows (max 2^31 - 1)", (unsigned long long)n); return GNS_E_RANGE; }
+    if (n == 0) return GNS_OK;
+    (void)hipGetLastError();
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+        (void)hipGetLastError(); set_error("device %d not available", device); return GNS_E_NODEV;
+    }
+    GNS_HIP(hipSetDevice(device));
+    if ((int)t_hh_scratch.size() <= device) t_hh_scratch.resize(device + 1, nullptr);
+    if (!t_hh_scratch[device]) t_hh_scratch[device] = new CmScratch();
+    CmScratch &sc = *t_hh_scratch[device];
+    hipStream_t st = nullptr;  // the legacy stream: ordered after the caller's device writes
+    const HhSrc src{nullptr, rows, key_bytes, key_bytes + 4};
+    uint32_t *perm = nullptr;
+    GNS_TRY(hh_sort(sc, st, src, (uint32_t)n, &perm));
+    hipLaunchKernelGGL(k_hh_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, perm, src, (uint32_t)n,
+                       nullptr, nullptr, out_rows);
+    GNS_HIP(hipGetLastError());
+    GNS_HIP(hipStreamSynchronize(st));
     return GNS_OK;
 }
 

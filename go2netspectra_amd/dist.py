@@ -513,6 +513,52 @@ def allgather_heavy_arrays(arrays, world: int):
     return tuple(out)
 
 
+def order_rows_device(rows, K: int):
+    """Canonical order (value desc, flow bytes asc) of device rows [flow (K) | u32 value] on
+    the GPU (gns_hh_order_rows: the hand-written radix sort of the heavy-hitter lists)."""
+    import torch
+    from . import _lib
+    n = int(rows.shape[0])
+    out = torch.empty_like(rows)
+    if n:
+        L = _lib.load()
+        rows = rows.contiguous()
+        torch.cuda.current_stream(rows.device).synchronize()  # the rows are complete
+        _lib.check(L.gns_hh_order_rows(rows.data_ptr(), K, n, out.data_ptr(), rows.device.index or 0))
+    return out
+
+
+def _allgather_dev_rows(rows, world: int):
+    """All-gather of device rows [n_r, W] (RCCL), concatenated in rank order."""
+    import torch
+    import torch.distributed as dist
+    dev = rows.device
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    counts = [int(x.item()) for x in ns]
+    mine = torch.zeros((max(max(counts), 1), rows.shape[1]), dtype=torch.uint8, device=dev)
+    if rows.shape[0]:
+        mine[: rows.shape[0]] = rows
+    parts = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)], dim=0)
+
+
+def allgather_heavy_rows(cm, world: int):
+    """Per-window exchange with the lists kept on the device (RCCL): each shard's device
+    heavy-hitter rows (CountMin.heavy_hitters_rows_device), two all-gathers, the union put
+    in canonical order on the GPU (order_rows_device; shards own disjoint flows), then one
+    copy to the host.  Returns (count flows [n,K], counts, size flows, sizes) like
+    allgather_heavy_arrays."""
+    K = cm.key_bytes
+    out = []
+    for rows in cm.heavy_hitters_rows_device():
+        g = order_rows_device(_allgather_dev_rows(rows, world), K).cpu().numpy()
+        out.extend((g[:, :K], np.ascontiguousarray(g[:, K:]).view("<u4").reshape(-1).astype(np.uint32)))
+    return tuple(out)
+
+
 # ---------------------------------------------------------------------------
 # Exact global mode (SURVEY §8e "exact global alternative"): every GPU sees the
 # whole stream but applies only the updates that fall in its slice of bucket

@@ -276,6 +276,24 @@ class CountMin:
     def heavy_hitters(self) -> HeavyRecord:
         return _cm_heavy_record(self.heavy_hitters_arrays(), self.key_bytes)
 
+    def heavy_hitters_rows_device(self):
+        """HeavyHitters as two DEVICE tensors of packed rows [flow | u32 value] (count list,
+        size list; uint8 [n, key_bytes + 4]) in canonical order: the multi-GPU window exchange
+        all-gathers them and merges on the device (dist.allgather_heavy_rows)."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        W = self.key_bytes + 4
+        nc, ns = ct.c_uint64(0), ct.c_uint64(0)
+        check(self._L.gns_cm_heavy_rows(self._h, None, ct.byref(nc), None, ct.byref(ns)))
+        while True:
+            cr = torch.empty((max(nc.value, 1), W), dtype=torch.uint8, device=dev)
+            sr = torch.empty((max(ns.value, 1), W), dtype=torch.uint8, device=dev)
+            c2, s2 = ct.c_uint64(cr.shape[0]), ct.c_uint64(sr.shape[0])
+            check(self._L.gns_cm_heavy_rows(self._h, cr.data_ptr(), ct.byref(c2), sr.data_ptr(), ct.byref(s2)))
+            if c2.value <= cr.shape[0] and s2.value <= sr.shape[0]:
+                return cr[: c2.value], sr[: s2.value]
+            nc, ns = c2, s2  # the lists changed between the calls (cannot on one handle; kept for safety)
+
     def view(self) -> "CountMinView":
         """A snapshot view whose heavy hitters / queries run concurrently with
         this handle's inserts (gns_cm_view_*); refresh() it at window boundaries."""

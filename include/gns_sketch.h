@@ -161,6 +161,17 @@ int gns_cm_query(gns_cm *cm, const uint8_t *keys, uint32_t stride, uint64_t n, u
  * capacities).  flows_* are n*key_bytes. */
 int gns_cm_heavy_hitters(gns_cm *cm, uint8_t *count_flows, uint32_t *counts, uint64_t *n_count,
                          uint8_t *size_flows, uint32_t *sizes, uint64_t *n_size);
+/* HeavyHitters into DEVICE memory, for the multi-GPU window exchange (the lists
+ * stay on the device through the all-gather and the merge): packed rows
+ * [flow (key_bytes) | value (u32, little-endian)], in the order above;
+ * *n_count / *n_size in/out as for gns_cm_heavy_hitters (capacities in rows; a
+ * list longer than its buffer is reported and not written). */
+int gns_cm_heavy_rows(gns_cm *cm, uint8_t *count_rows, uint64_t *n_count, uint8_t *size_rows, uint64_t *n_size);
+/* The canonical order (value desc, flow bytes asc) of n DEVICE rows of the form
+ * above -- the union of flow-disjoint per-shard lists after an all-gather
+ *  -- written to out_rows (device).  Runs on the device's null
+ * stream, ordered after the caller's earlier work on it; returns when done. */
+int gns_hh_order_rows(const uint8_t *rows, uint32_t key_bytes, uint64_t n, uint8_t *out_rows, int device);
 int gns_cm_reset(gns_cm *cm);
 /* Full state for parity: C/S [depth*width], FPc/FPs [depth*width*key_bytes]
  * (any pointer may be NULL). */

@@ -574,3 +574,37 @@ def test_compact_streams_hot_fallbacks(gpu, oracle, monkeypatch, w):
         orc.insert_keys(keys, sizes)
         cm.flush()
         assert_same_state(cm, orc)
+
+
+def test_heavy_rows_device_and_device_merge(gpu, oracle):
+    """gns_cm_heavy_rows (the lists as device rows) equals gns_cm_heavy_hitters, and
+    gns_hh_order_rows puts shuffled rows with many ties back in canonical order (value
+    desc, flow bytes asc: dist.merge_heavy_arrays on the host)."""
+    import torch
+    from go2netspectra_amd.dist import merge_heavy_arrays, order_rows_device
+    rng = np.random.default_rng(77)
+    cm, orc = make_pair(oracle, 4096, 3, 13, st=2000, ct=20)
+    keys, _, _ = zipf_keys(rng, 400_000, 6000, 13)
+    sizes = sizes_u32(rng, 400_000)
+    cm.insert_keys(keys, sizes)
+    cm.flush()
+    cf, cv, sf, sv = cm.heavy_hitters_arrays()
+    cr, sr = cm.heavy_hitters_rows_device()
+    for f, v, r in ((cf, cv, cr), (sf, sv, sr)):
+        g = r.cpu().numpy()
+        assert len(g) == len(v) > 0
+        assert np.array_equal(g[:, :13], f) and np.array_equal(np.ascontiguousarray(g[:, 13:]).view("<u4").reshape(-1), v)
+    # ties on (value, first four bytes) beyond them, several key widths
+    for K in (4, 8, 13, 16, 37):
+        n = 50_000
+        flows = rng.integers(0, 256, (n, K), dtype=np.uint8)
+        flows[: n // 2, : min(K, 4)] = rng.integers(0, 3, (n // 2, min(K, 4)), dtype=np.uint8)
+        flows = np.unique(flows, axis=0)
+        vals = rng.integers(0, 40, len(flows)).astype(np.uint32)
+        vals[::5] = rng.integers(0, 2**32, len(vals[::5]), dtype=np.uint64).astype(np.uint32)
+        perm = rng.permutation(len(flows))
+        rows = np.concatenate([flows[perm], vals[perm].view(np.uint8).reshape(-1, 4)], axis=1)
+        got = order_rows_device(torch.from_numpy(np.ascontiguousarray(rows)).cuda(), K).cpu().numpy()
+        wf, wv = merge_heavy_arrays(flows, vals)
+        assert np.array_equal(got[:, :K], wf), K
+        assert np.array_equal(np.ascontiguousarray(got[:, K:]).view("<u4").reshape(-1), wv), K
