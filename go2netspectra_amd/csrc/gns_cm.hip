@@ -1475,7 +1475,7 @@ struct ApplyArgs {
     unsigned long long *stats;  // [5] replayed updates, [6] chunks, [7] chunks with a replay
     const uint64_t *entries;
     uint64_t *entries2;         // super-bin sub-partition scratch (sub_bits > 0)
-    const uint32_t *soff;       // [nbins][17] tile starts of each super-bin (k_subpart), or null
+    const uint16_t *rseg;       // [round][16] tile starts inside each k_subpart round, or null
     const uint32_t *offsets;
     uint32_t nblk, nbins;
     const uint32_t *total;
@@ -1673,11 +1673,28 @@ __device__ __forceinline__ void tile_none(TilePre &pre) {
     for (uint32_t m = 0; m < kTilePer; m++) { pre.c[m] = 0; pre.fc[m] = 0; pre.s[m] = 0; pre.fs[m] = 0; }
 }
 
-// Updates ent[beg, end) (stream order) of one LDS tile: buckets cbase .. cbase+tn-1.
+// Where K4 reads a tile's updates: one contiguous range of the entry array, or
+// (super-bins) the tile's run in each k_subpart round, in round order.  at(q, h)
+// returns logical update q; h is the caller's running segment hint.
+struct EntFlat {
+    const uint64_t *p;
+    __device__ __forceinline__ uint64_t at(uint32_t q, uint32_t &) const { return p[q]; }
+};
+struct SegLds;
+struct EntSegs {
+    const uint64_t *p;
+    const SegLds *G;       // run r holds logical [spre[r], spre[r+1]) at p + sbase[r] (tables in LDS)
+    uint32_t off, nseg;    // this tile's table: entries off .. off + nseg (spre has nseg + 1)
+    __device__ __forceinline__ uint64_t at(uint32_t q, uint32_t &h) const;
+};
+
+// Updates [beg, end) (stream order; logical indices of src) of one LDS tile:
+// buckets cbase .. cbase+tn-1.
 // pre holds this tile's state if it was prefetched (pre.cbase == cbase); on
 // return it holds the state of the tile at next_cbase (kNoTile: none), loaded
 // after this tile's stores were issued.
-__device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, const uint64_t *ent, uint32_t beg,
+template <class Src>
+__device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, const Src &ent, uint32_t beg,
                                            uint32_t end, uint64_t cbase, uint32_t tn, uint32_t col0,
                                            TilePre &pre, uint64_t next_cbase, uint32_t next_tn) {
     unsigned long long *accN = L.accN, *accS = L.accS;
@@ -1708,10 +1725,11 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
 #endif
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint64_t e[kApItems], en[kApItems];
+    uint32_t hint = 0;
 #pragma unroll
     for (int j = 0; j < kApItems; j++) {  // first chunk
         const uint32_t q = beg + j * kApThreads + tid;
-        e[j] = q < end ? ent[q] : 0ull;
+        e[j] = q < end ? ent.at(q, hint) : 0ull;
     }
     // engine counters in registers (global atomics inside the loop would be
     // drained by the next chunk's load waits)
@@ -1754,7 +1772,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
 #pragma unroll
         for (int j = 0; j < kApItems; j++) {
             const uint32_t q = cb + kApChunk + j * kApThreads + tid;
-            en[j] = q < end ? ent[q] : 0ull;
+            en[j] = q < end ? ent.at(q, hint) : 0ull;
         }
         __syncthreads();
         K4_MARK(0);
@@ -1885,7 +1903,8 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                 bool pending = false;
                 uint32_t b = 0, k = 0, s = 0, rf = 0;
                 if (i < nlist) {
-                    const uint64_t ee = i < kRepCap ? L.s_rep[i] : ent[cb + s_list[i]];
+                    uint32_t h0 = 0;
+                    const uint64_t ee = i < kRepCap ? L.s_rep[i] : ent.at(cb + s_list[i], h0);
                     b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
                     pending = b % kApWaves == wave;
                     if (pending) {
@@ -1900,7 +1919,8 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
                 const uint32_t i = g0 + lane;
                 if (i < nlist) {
-                    const uint64_t ee = i < kRepCap ? L.s_rep[i] : ent[cb + s_list[i]];
+                    uint32_t h0 = 0;
+                    const uint64_t ee = i < kRepCap ? L.s_rep[i] : ent.at(cb + s_list[i], h0);
                     const uint32_t b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
                     if (b % kApWaves == wave) accN[b] = 0;
                 }
@@ -2050,20 +2070,168 @@ __device__ __forceinline__ void sub_partition(const uint64_t *ent, uint64_t *ent
 // Super-bin sub-partition as a launch of its own, one workgroup per super-bin and
 // two per CU (16 KB of LDS instead of K4's 156 KB), so that its barrier- and
 // latency-bound rounds overlap across workgroups instead of running inside K4's
-// one-workgroup-per-CU loop: the same stable partition by tile as sub_partition.
-__global__ __launch_bounds__(kApThreads) void k_subpart(ApplyArgs a, uint32_t *soff) {
-    __shared__ SubLds P;
-    __shared__ uint32_t cnt[2 * kSubPairs * 16];
-    const uint32_t bin = blockIdx.x;  // block-uniform exits below
-    const uint32_t nsub = 1u << a.g.sub_bits;
+// one-workgroup-per-CU loop.  One pass: every round of kApChunk updates is
+// grouped by tile in place of the round (stable inside each tile), and the
+// round's tile starts go to rseg; K4 reads a tile as its run in each round, in
+// round order, which is the tile's stream order.  (The inline variant,
+// sub_partition, counts first and writes each tile contiguously: a second read
+// of every update.)  Round r of bin b has index beg/kApChunk + r + b: unique
+// and below total/kApChunk + nbins.
+#ifndef GNS_SEG_ALL
+#define GNS_SEG_ALL 416
+#endif
+constexpr uint32_t kSegAll = GNS_SEG_ALL;  // table entries (8 B each; K4's LDS is nearly full)
+template <int NT>
+__global__ __launch_bounds__(NT, NT == 512 ? 4 : 1) void k_subpart(ApplyArgs a, uint16_t *rseg) {
+    constexpr int kW = NT / 64, kI = (int)kApChunk / NT;  // waves; updates per thread and round
+    static_assert(kW * kI == (int)kSubPairs, "(item, wave) groups of a round");
+    __shared__ uint32_t cnt[2][kSubPairs * 16];
+    __shared__ uint32_t ttot[2][16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t bin = blockIdx.x;  // block-uniform exit below
+    const uint32_t sub_bits = a.g.sub_bits, nsub = 1u << sub_bits, tile_bits = a.g.tile_bits;
     const uint32_t beg = a.offsets[bin];
     const uint32_t end = (bin + 1 < a.g.nbins_all) ? a.offsets[bin + 1] : *a.total;
-    if (beg >= end) {
-        if (threadIdx.x <= nsub) soff[(uint64_t)bin * 17 + threadIdx.x] = 0;
-        return;
+    if (beg >= end) return;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    // a bin too big for K4's tables goes to the second K4 launch, which exits at once without one
+    if (tid == 0 && (end - beg + kApChunk - 1) / kApChunk + 1 > kSegAll) atomicAdd(a.work + 2, 1u);
+    if (tid < 32) (&ttot[0][0])[tid] = 0;
+    uint64_t e[kI], en[kI];
+#pragma unroll
+    for (int j = 0; j < kI; j++) {
+        const uint32_t q = beg + j * NT + tid;
+        e[j] = q < end ? a.entries[q] : 0ull;
     }
-    sub_partition(a.entries, a.entries2, beg, end, a.g.tile_bits, a.g.sub_bits, P, cnt);
-    if (threadIdx.x <= nsub) soff[(uint64_t)bin * 17 + threadIdx.x] = P.soff[threadIdx.x];
+    __syncthreads();
+    uint32_t par = 0;
+    for (uint32_t rb = beg; rb < end; rb += kApChunk) {
+        uint32_t *cb = cnt[par], *tt = ttot[par];
+        // the next round's updates load while this round is ranked and stored
+#pragma unroll
+        for (int j = 0; j < kI; j++) {
+            const uint32_t q = rb + kApChunk + j * NT + tid;
+            en[j] = q < end ? a.entries[q] : 0ull;
+        }
+        uint32_t sb[kI];  // tile | rank among the wave's earlier updates of the tile << 8
+#pragma unroll
+        for (int j = 0; j < kI; j++) {
+            const uint32_t q = rb + j * NT + tid;
+            const bool valid = q < end;
+            const uint32_t sub = valid ? (((uint32_t)(e[j] >> 32) & kLowMask) >> tile_bits) : 0xFFu;
+            uint64_t peers = __ballot(valid);
+            for (uint32_t bit = 0; bit < sub_bits; bit++) {
+                const uint64_t m = __ballot(valid && ((sub >> bit) & 1u));
+                peers &= ((sub >> bit) & 1u) ? m : ~m;
+            }
+            const uint32_t before = __popcll(peers & lt_mask);
+            sb[j] = sub | before << 8;
+            // this wave's slots of group (j, wave): zeroed, then the first lane of
+            // each tile's peers writes the count (one wave: LDS ops stay in order)
+            if (lane < 16) cb[(j * kW + wave) * 16 + lane] = 0;
+            if (valid && before == 0) {
+                const uint32_t c = (uint32_t)__popcll(peers);
+                cb[(j * kW + wave) * 16 + sub] = c;
+                atomicAdd(&tt[sub], c);
+            }
+        }
+        __syncthreads();
+        if (wave < nsub) {  // (nsub <= kW) wave t: tile t's start in the round + exclusive scan of its group counts
+            static_assert(kSubPairs == 128, "two groups per lane");
+            const uint32_t t = wave;
+            uint32_t b0 = 0;
+            for (uint32_t u = 0; u < t; u++) b0 += tt[u];
+            const uint32_t x0 = cb[(2 * lane) * 16 + t], x1 = cb[(2 * lane + 1) * 16 + t];
+            const uint32_t inc = wave_incl_scan(x0 + x1);
+            const uint32_t ex = b0 + inc - (x0 + x1);
+            cb[(2 * lane) * 16 + t] = ex;
+            cb[(2 * lane + 1) * 16 + t] = ex + x0;
+            if (lane == 0) rseg[((uint64_t)(rb / kApChunk) + bin) * 16 + t] = (uint16_t)b0;
+        }
+        // the next round's tile totals (last read in the previous round, before this round's first barrier)
+        if (tid >= NT - 16) ttot[par ^ 1u][tid - (NT - 16)] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kI; j++)
+            if ((sb[j] & 0xFFu) != 0xFFu) a.entries2[rb + cb[(j * kW + wave) * 16 + (sb[j] & 0xFFu)] + (sb[j] >> 8)] = e[j];
+#pragma unroll
+        for (int j = 0; j < kI; j++) e[j] = en[j];
+        par ^= 1u;
+    }
+}
+
+// K4's view of a super-bin's tiles: each tile's run in every k_subpart round, in
+// round order, with the runs' logical starts scanned.  All tiles' tables are built
+// at the bin's start (wave t scans tile t: one barrier per bin) when they fit
+// kSegAll entries (nsub * (rounds + 1): every C5 bin of typical size); otherwise
+// one tile at a time in windows of rounds (a tile spread over several windows is
+// stored and reloaded between them).
+struct SegLds {
+    uint32_t tot[16];             // the super-bin's updates per tile
+    uint32_t sbase[kSegAll];      // physical start of a tile's run in a round
+    uint32_t spre[kSegAll];       // logical start of each run, then the table's total
+};
+
+// The lanes of a wave ask for consecutive q: the run of the wave's first lane is
+// found with wave-uniform reads (from the wave's hint h, else by bisection), the
+// other lanes step forward from it (a run shorter than the wave: a few steps).
+__device__ __forceinline__ uint64_t EntSegs::at(uint32_t q, uint32_t &h) const {
+    const uint32_t *spre = G->spre + off, *sbase = G->sbase + off;
+    const uint32_t qf = __builtin_amdgcn_readfirstlane(q);
+    uint32_t r = __builtin_amdgcn_readfirstlane(h);
+    if (!(r < nseg && spre[r] <= qf)) r = 0;
+    if (r + 1 < nseg && spre[r + 1] <= qf) {
+        uint32_t lo = r + 1, hi = nseg;  // largest r with spre[r] <= qf (empty runs skipped)
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (spre[mid] <= qf) lo = mid; else hi = mid;
+        }
+        r = lo;
+    }
+    h = r;
+    while (r + 1 < nseg && spre[r + 1] <= q) r++;
+    return p[sbase[r] + (q - spre[r])];
+}
+
+// One wave: tile st's runs of rounds [w0, w0 + nr) into the table at off (nr + 1 entries).
+__device__ __forceinline__ uint32_t seg_scan_wave(const ApplyArgs &a, SegLds &G, uint32_t beg, uint32_t end,
+                                                  uint64_t ridx0, uint32_t nsub, uint32_t st, uint32_t w0,
+                                                  uint32_t nr, uint32_t off) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t carry = 0;
+    for (uint32_t i0 = 0; i0 < nr; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        uint32_t len = 0;
+        if (i < nr) {
+            const uint32_t r = w0 + i;
+            const uint32_t rb = beg + r * kApChunk, rl = min(kApChunk, end - rb);
+            const uint16_t *rs = a.rseg + (ridx0 + r) * 16;
+            const uint32_t s0 = rs[st], e0 = st + 1 < nsub ? rs[st + 1] : rl;
+            G.sbase[off + i] = rb + s0;
+            len = e0 - s0;
+        }
+        const uint32_t inc = wave_incl_scan(len);
+        if (i < nr) G.spre[off + i] = carry + inc - len;
+        carry += __shfl(inc, 63, 64);
+    }
+    if (lane == 0) G.spre[off + nr] = carry;
+    return carry;
+}
+
+__device__ __forceinline__ void seg_totals(const ApplyArgs &a, SegLds &G, uint32_t beg, uint32_t end,
+                                           uint64_t ridx0, uint32_t nsub) {
+    const uint32_t tid = threadIdx.x;
+    if (tid < 16) G.tot[tid] = 0;
+    __syncthreads();
+    const uint32_t R = (end - beg + kApChunk - 1) / kApChunk;
+    for (uint32_t i = tid; i < R * nsub; i += kApThreads) {
+        const uint32_t r = i / nsub, t = i % nsub;
+        const uint32_t rl = min(kApChunk, end - (beg + r * kApChunk));
+        const uint16_t *rs = a.rseg + (ridx0 + r) * 16;
+        const uint32_t e = t + 1 < nsub ? rs[t + 1] : rl;
+        if (e > rs[t]) atomicAdd(&G.tot[t], e - rs[t]);
+    }
+    __syncthreads();
 }
 
 // Persistent: each workgroup takes bins from the size-ordered schedule through
@@ -2090,21 +2258,31 @@ __device__ __forceinline__ ApplyTile apply_bin(const ApplyArgs &a, uint32_t k) {
     return t;
 }
 
+// MODE 0: rows of single tiles (bins = tiles); 1: super-bins read through k_subpart's
+// rounds (3: the super-bins too big for MODE 1's tables, a second launch); 2:
+// super-bins sub-partitioned inline (GNS_SUBPART_LAUNCH=0).  One variant per
+// launch, so each inlines only its own tile loop (and stays within 128 VGPRs).
+template <int MODE>
 __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
     __shared__ ApplyLds L;
     __shared__ SubLds P;
+    __shared__ SegLds G;
     __shared__ uint32_t s_k;
     const CmGeom &g = a.g;
     const uint32_t tid = threadIdx.x;
     const uint32_t tw = 1u << g.tile_bits;
     TilePre pre;
     tile_none(pre);
-    if (tid == 0) s_k = atomicAdd(a.work, 1u);
+    if constexpr (MODE == 3) {
+        if (a.work[2] == 0) return;  // no bin needs windows (k_subpart counts them): the common case
+    }
+    unsigned int *work = a.work + (MODE == 3 ? 1 : 0);
+    if (tid == 0) s_k = atomicAdd(work, 1u);
     __syncthreads();
     uint32_t k = s_k;
     __syncthreads();
     while (k < g.nbins) {
-        if (tid == 0) s_k = atomicAdd(a.work, 1u);  // the bin after this one
+        if (tid == 0) s_k = atomicAdd(work, 1u);  // the bin after this one
         const ApplyTile cur = apply_bin(a, k);
         __syncthreads();
         const uint32_t kn = s_k;
@@ -2113,47 +2291,105 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
         // tile may turn out empty, which only wastes that prefetch)
         uint64_t nb_cbase = kNoTile;
         uint32_t nb_tn = 0;
-        if (nxt.valid && nxt.beg < nxt.end && nxt.bbase < g.w) {
+        if (MODE != 3 && nxt.valid && nxt.beg < nxt.end && nxt.bbase < g.w) {
             nb_cbase = (uint64_t)nxt.r * g.w + nxt.bbase;
             nb_tn = min(tw, g.w - nxt.bbase);
         }
         if (cur.beg < cur.end) {
-            if (g.sub_bits == 0) {
-                apply_tile(a, L, a.entries, cur.beg, cur.end, (uint64_t)cur.r * g.w + cur.bbase,
+            if constexpr (MODE == 0) {
+                apply_tile(a, L, EntFlat{a.entries}, cur.beg, cur.end, (uint64_t)cur.r * g.w + cur.bbase,
                            min(tw, g.w - cur.bbase), cur.bbase, pre, nb_cbase, nb_tn);
             } else {
                 const uint32_t nsub = 1u << g.sub_bits;
 #ifdef GNS_K4_PROF
                 const uint64_t t_sp = __builtin_amdgcn_s_memtime();
 #endif
-                if (a.soff) {  // partitioned by k_subpart
-                    if (tid <= nsub) P.soff[tid] = a.soff[(uint64_t)cur.bin * 17 + tid];
-                    __syncthreads();
+                if constexpr (MODE == 1 || MODE == 3) {  // rounds grouped by tile (k_subpart)
+                    const uint64_t ridx0 = (uint64_t)(cur.beg / kApChunk) + cur.bin;
+                    const uint32_t R = (cur.end - cur.beg + kApChunk - 1) / kApChunk;
+                    // MODE 1: bins whose tables fit kSegAll, all tiles' at once or (bigger bins)
+                    // one tile's at a time; MODE 3 (a second launch): the rest
+                    const bool all = nsub * (R + 1) <= kSegAll;  // block-uniform
+                    const bool fits = R + 1 <= kSegAll;
+                    if ((MODE == 1) == fits) {
+                        if (MODE == 1 && all) {
+                            if (tid >> 6 < nsub) {
+                                const uint32_t t = tid >> 6;
+                                const uint32_t tot = seg_scan_wave(a, G, cur.beg, cur.end, ridx0, nsub, t, 0, R, t * (R + 1));
+                                if ((tid & 63u) == 0) G.tot[t] = tot;
+                            }
+                            __syncthreads();
+                        } else {
+                            seg_totals(a, G, cur.beg, cur.end, ridx0, nsub);
+                        }
+                        for (uint32_t st = 0; st < nsub; st++) {
+                            const uint32_t tbase = cur.bbase + (st << g.tile_bits);
+                            if (tbase >= g.w || G.tot[st] == 0) continue;
+                            uint64_t ncb = nb_cbase;
+                            uint32_t ntn = nb_tn;
+                            for (uint32_t s2 = st + 1; s2 < nsub; s2++) {
+                                const uint32_t tb2 = cur.bbase + (s2 << g.tile_bits);
+                                if (tb2 < g.w && G.tot[s2]) {
+                                    ncb = (uint64_t)cur.r * g.w + tb2;
+                                    ntn = min(tw, g.w - tb2);
+                                    break;
+                                }
+                            }
+                            const uint64_t cbase = (uint64_t)cur.r * g.w + tbase;
+                            const uint32_t tn = min(tw, g.w - tbase);
+                            if constexpr (MODE == 1) {
+                                uint32_t off = st * (R + 1);
+                                if (!all) {
+                                    if (tid < 64) seg_scan_wave(a, G, cur.beg, cur.end, ridx0, nsub, st, 0, R, 0);
+                                    __syncthreads();
+                                    off = 0;
+                                }
+                                apply_tile(a, L, EntSegs{a.entries2, &G, off, R}, 0u, G.tot[st], cbase, tn, tbase, pre,
+                                           ncb, ntn);
+                                __syncthreads();
+                            } else {
+                                // windows of rounds; a tile spread over several is stored and
+                                // reloaded between them (no prefetch of itself)
+                                constexpr uint32_t kWin = kSegAll - 1;
+                                for (uint32_t w0 = 0; w0 < R; w0 += kWin) {
+                                    const uint32_t nr = min(kWin, R - w0);
+                                    if (tid < 64) seg_scan_wave(a, G, cur.beg, cur.end, ridx0, nsub, st, w0, nr, 0);
+                                    __syncthreads();
+                                    const uint32_t n = G.spre[nr];
+                                    const bool last = w0 + kWin >= R;
+                                    if (n)
+                                        apply_tile(a, L, EntSegs{a.entries2, &G, 0u, nr}, 0u, n, cbase, tn, tbase, pre,
+                                                   last ? ncb : kNoTile, last ? ntn : 0u);
+                                    __syncthreads();
+                                }
+                            }
+                        }
+                    }
                 } else {
                     sub_partition(a.entries, a.entries2, cur.beg, cur.end, g.tile_bits, g.sub_bits, P,
                                   reinterpret_cast<uint32_t *>(L.accN));
-                }
 #ifdef GNS_K4_PROF
-                if (tid == 0) atomicAdd(&a.stats[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_sp));
+                    if (tid == 0) atomicAdd(&a.stats[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_sp));
 #endif
-                for (uint32_t st = 0; st < nsub; st++) {
-                    const uint32_t tbase = cur.bbase + (st << g.tile_bits);
-                    const uint32_t sb = cur.beg + P.soff[st], se = cur.beg + P.soff[st + 1];
-                    if (tbase >= g.w || sb >= se) continue;
-                    // next tile: the next non-empty tile of this bin, else the next bin's first
-                    uint64_t ncb = nb_cbase;
-                    uint32_t ntn = nb_tn;
-                    for (uint32_t s2 = st + 1; s2 < nsub; s2++) {
-                        const uint32_t tb2 = cur.bbase + (s2 << g.tile_bits);
-                        if (tb2 < g.w && P.soff[s2] < P.soff[s2 + 1]) {
-                            ncb = (uint64_t)cur.r * g.w + tb2;
-                            ntn = min(tw, g.w - tb2);
-                            break;
+                    for (uint32_t st = 0; st < nsub; st++) {
+                        const uint32_t tbase = cur.bbase + (st << g.tile_bits);
+                        const uint32_t sb = cur.beg + P.soff[st], se = cur.beg + P.soff[st + 1];
+                        if (tbase >= g.w || sb >= se) continue;
+                        // next tile: the next non-empty tile of this bin, else the next bin's first
+                        uint64_t ncb = nb_cbase;
+                        uint32_t ntn = nb_tn;
+                        for (uint32_t s2 = st + 1; s2 < nsub; s2++) {
+                            const uint32_t tb2 = cur.bbase + (s2 << g.tile_bits);
+                            if (tb2 < g.w && P.soff[s2] < P.soff[s2 + 1]) {
+                                ncb = (uint64_t)cur.r * g.w + tb2;
+                                ntn = min(tw, g.w - tb2);
+                                break;
+                            }
                         }
+                        apply_tile(a, L, EntFlat{a.entries2}, sb, se, (uint64_t)cur.r * g.w + tbase,
+                                   min(tw, g.w - tbase), tbase, pre, ncb, ntn);
+                        __syncthreads();
                     }
-                    apply_tile(a, L, a.entries2, sb, se, (uint64_t)cur.r * g.w + tbase, min(tw, g.w - tbase), tbase,
-                               pre, ncb, ntn);
-                    __syncthreads();
                 }
             }
         }
@@ -2995,7 +3231,8 @@ struct gns_cm {
     uint32_t *ptotal = nullptr;        // [2]
     uint32_t *hist = nullptr, *part = nullptr, *total = nullptr, *order = nullptr;
     uint64_t *entries = nullptr, *entries2 = nullptr;
-    uint32_t *soff = nullptr;          // [nbins][17] super-bin tile starts (sub_bits > 0)
+    uint16_t *rseg = nullptr;          // [round][16] k_subpart round tile starts (sub_bits > 0)
+    int subpart_nt = 0;                // GNS_SUBPART_NT (A/B)
     uint64_t *ovf = nullptr;
     uint32_t *ovf_cnt = nullptr;
     uint64_t ovf_cap = 0;                 // entries of ovf
@@ -3086,7 +3323,7 @@ int cm_free_all(gns_cm *cm) {
     dfree(cm->keyid); dfree(cm->idx); dfree(cm->scnt);  // hstr lives in idx
     dfree(cm->pend[0]); dfree(cm->pend[1]); dfree(cm->pcnt[0]); dfree(cm->pcnt[1]);
     dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
-    dfree(cm->entries); dfree(cm->entries2); dfree(cm->soff); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats);
+    dfree(cm->entries); dfree(cm->entries2); dfree(cm->rseg); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats);
     dfree(cm->stage[0]); dfree(cm->stage[1]); dfree(cm->side_dev);
     for (int i = 0; i < 2; i++) {
         if (cm->ev_copied[i]) (void)hipEventDestroy(cm->ev_copied[i]);
@@ -3306,15 +3543,28 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.entries = cm->entries; a.entries2 = cm->entries2; a.offsets = cm->hist; a.nblk = nblk; a.nbins = g.nbins;
         a.total = cm->total; a.order = ordered ? cm->order : nullptr; a.ovf = cm->ovf; a.g = g;
         a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs; a.work = cm->work;
-        GNS_HIP(hipMemsetAsync(cm->work, 0, 4, s));
+        GNS_HIP(hipMemsetAsync(cm->work, 0, 12, s));
         ScopedStage st(cm->timer, 4);
         if (g.sub_bits && kSubpartLaunch) {
-            hipLaunchKernelGGL(k_subpart, dim3(g.nbins), dim3(kApThreads), 0, s, a, cm->soff);
+            // 512-thread workgroups (16 updates per thread and round, two per CU) when a
+            // wave per tile fits; GNS_SUBPART_NT=1024 for the A/B
+            if ((1u << g.sub_bits) <= 8 && cm->subpart_nt != 1024)
+                hipLaunchKernelGGL(k_subpart<512>, dim3(g.nbins), dim3(512), 0, s, a, cm->rseg);
+            else
+                hipLaunchKernelGGL(k_subpart<1024>, dim3(g.nbins), dim3(1024), 0, s, a, cm->rseg);
             GNS_HIP(hipGetLastError());
-            a.soff = cm->soff;
+            a.rseg = cm->rseg;
         }
         // persistent: one workgroup per CU (the tile LDS fills a CU), bins from the schedule counter
-        hipLaunchKernelGGL(k_apply, dim3(std::min(g.nbins, cm->ncu)), dim3(kApThreads), 0, s, a);
+        const dim3 apg(std::min(g.nbins, cm->ncu));
+        if (!g.sub_bits) hipLaunchKernelGGL(k_apply<0>, apg, dim3(kApThreads), 0, s, a);
+        else if (a.rseg) {
+            hipLaunchKernelGGL(k_apply<1>, apg, dim3(kApThreads), 0, s, a);
+            GNS_HIP(hipGetLastError());
+            // super-bins too big for K4's LDS tables (none at the bench geometry): windows of rounds
+            hipLaunchKernelGGL(k_apply<3>, apg, dim3(kApThreads), 0, s, a);
+        }
+        else hipLaunchKernelGGL(k_apply<2>, apg, dim3(kApThreads), 0, s, a);
         GNS_HIP(hipGetLastError());
     }
     // hot bins: chip-wide aggregate, exact decide, in-order fallback
@@ -3644,7 +3894,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (rc = dalloc_t(&cm->part, nscan)) || (rc = dalloc_t(&cm->total, 1)) ||
             (rc = dalloc_t(&cm->order, g.nbins)) || (rc = dalloc_t(&cm->entries, cm->bmax * g.d)) ||
             (g.sub_bits && (rc = dalloc_t(&cm->entries2, cm->bmax * g.d))) ||
-            (g.sub_bits && (rc = dalloc_t(&cm->soff, (uint64_t)g.nbins * 17))) ||
+            (g.sub_bits && (rc = dalloc_t(&cm->rseg, (cm->bmax * g.d / kApChunk + g.nbins + 2) * 16))) ||
             (rc = dalloc_t(&cm->ovf, kOvfCap)) || (rc = dalloc_t(&cm->ovf_cnt, 1)) ||
             (rc = dalloc_t(&cm->stats, 16)) || (rc = dalloc_t(&cm->work, 4)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
             (rc = dalloc_t(&cm->segtot, (size_t)g.d * kHot * kHotSegs * 2)) || (rc = dalloc_t(&cm->hflag, g.d * kHot)) ||
@@ -3678,6 +3928,8 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             cm->lds_ordered = hv == 0 && !(env && env[0] == '0');
             const char *es = getenv("GNS_K3_STAGED");
             cm->k3_staged = !(es && es[0] == '0');
+            const char *en = getenv("GNS_SUBPART_NT");
+            cm->subpart_nt = en ? atoi(en) : 0;
             const char *ec = getenv("GNS_CMODE");
             cm->cmode = ec && ec[0] == '1' && cm->lds_ordered && cm->k3_staged && g.ntiles <= 256 && g.d <= 8 &&
                         extract_lds_bytes(g.nbins_all, g.d) <= kExLdsSmall && g.w <= (1u << (32 - kCsBits));

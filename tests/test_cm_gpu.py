@@ -608,3 +608,50 @@ def test_heavy_rows_device_and_device_merge(gpu, oracle):
         wf, wv = merge_heavy_arrays(flows, vals)
         assert np.array_equal(got[:, :K], wf), K
         assert np.array_equal(np.ascontiguousarray(got[:, K:]).view("<u4").reshape(-1), wv), K
+
+
+def _mm3_words(words, seed):
+    """MurmurHash3 x86_32 of 4-byte keys (statistic/hash.go:13-53), vectorized."""
+    M = np.uint64(0xFFFFFFFF)
+    rotl = lambda x, r: ((x << np.uint64(r)) | (x >> np.uint64(32 - r))) & M
+    k = (words.astype(np.uint64) * np.uint64(0xCC9E2D51)) & M
+    k = (rotl(k, 15) * np.uint64(0x1B873593)) & M
+    h = rotl(np.uint64(seed) ^ k, 13)
+    h = (h * np.uint64(5) + np.uint64(0xE6546B64)) & M
+    h ^= np.uint64(4)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & M
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & M
+    return h ^ (h >> np.uint64(16))
+
+
+@pytest.mark.parametrize("n2", [2_500_000, 4_000_000])
+def test_superbin_many_rounds(gpu, oracle, n2):
+    """One super-bin (w=2^23: bins of two 4096-bucket tiles) takes millions of cold updates of
+    one batch: k_subpart groups ~300 / ~460 rounds by tile; K4 reads each tile through its
+    runs from a per-tile table (2.5M) or, past one table, in windows of rounds in the second
+    launch (4M: state stored and reloaded between windows)."""
+    rng = np.random.default_rng(2323)
+    w, d, K = 1 << 23, 2, 4
+    cm, orc = make_pair(oracle, w, d, K, st=1 << 30, ct=1 << 30, batch_packets=1 << 23, max_flows=1 << 16)
+    seeds = np.random.default_rng(1).integers(0, 2**32, d, dtype=np.uint64).astype(np.uint32)
+    cand = np.unique(rng.integers(0, 2**32, 6_000_000, dtype=np.uint64).astype(np.uint32))
+    h0 = _mm3_words(cand, int(seeds[0])) & np.uint64(w - 1)
+    pick = cand[h0 < 8192][:3000]  # row 0: super-bin 0
+    assert len(pick) == 3000
+    for x in pick[:3]:
+        assert oracle.mm3(int(x).to_bytes(4, "little"), int(seeds[0])) % w < 8192
+    flows = pick.view(np.uint8).reshape(-1, 4)
+    other = rng.integers(0, 256, (20_000, 4), dtype=np.uint8)
+    n1 = 1_000_000
+    k1 = np.concatenate([flows, other])[rng.integers(0, 23_000, n1)]
+    k2 = flows[rng.integers(0, 3000, n2)]
+    for keys in (k1, k2):
+        keys = np.ascontiguousarray(keys)
+        sizes = sizes_u32(rng, len(keys))
+        sizes[::997] = 70_000
+        cm.insert_keys(keys, sizes)
+        orc.insert_keys(keys, sizes)
+    cm.flush()
+    assert_same_state(cm, orc)
