@@ -1678,14 +1678,20 @@ __device__ __forceinline__ void tile_none(TilePre &pre) {
 // returns logical update q; h is the caller's running segment hint.
 struct EntFlat {
     const uint64_t *p;
-    __device__ __forceinline__ uint64_t at(uint32_t q, uint32_t &) const { return p[q]; }
+    struct Cur {};
+    __device__ __forceinline__ uint64_t at(uint32_t q, Cur &) const { return p[q]; }
+    __device__ __forceinline__ uint64_t at_any(uint32_t q) const { return p[q]; }
 };
 struct SegLds;
 struct EntSegs {
     const uint64_t *p;
     const SegLds *G;       // run r holds logical [spre[r], spre[r+1]) at p + sbase[r] (tables in LDS)
     uint32_t off, nseg;    // this tile's table: entries off .. off + nseg (spre has nseg + 1)
-    __device__ __forceinline__ uint64_t at(uint32_t q, uint32_t &h) const;
+    // a wave's current run [lo, hi) at base (wave-uniform; the lanes of a wave ask for
+    // consecutive q, and q only grows along apply_tile's loads)
+    struct Cur { uint32_t r = 0, lo = 0, hi = 0, base = 0; };
+    __device__ __forceinline__ uint64_t at(uint32_t q, Cur &c) const;
+    __device__ __forceinline__ uint64_t at_any(uint32_t q) const;
 };
 
 // Updates [beg, end) (stream order; logical indices of src) of one LDS tile:
@@ -1725,7 +1731,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
 #endif
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint64_t e[kApItems], en[kApItems];
-    uint32_t hint = 0;
+    typename Src::Cur hint{};
 #pragma unroll
     for (int j = 0; j < kApItems; j++) {  // first chunk
         const uint32_t q = beg + j * kApThreads + tid;
@@ -1903,8 +1909,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                 bool pending = false;
                 uint32_t b = 0, k = 0, s = 0, rf = 0;
                 if (i < nlist) {
-                    uint32_t h0 = 0;
-                    const uint64_t ee = i < kRepCap ? L.s_rep[i] : ent.at(cb + s_list[i], h0);
+                    const uint64_t ee = i < kRepCap ? L.s_rep[i] : ent.at_any(cb + s_list[i]);
                     b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
                     pending = b % kApWaves == wave;
                     if (pending) {
@@ -1919,8 +1924,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
                 const uint32_t i = g0 + lane;
                 if (i < nlist) {
-                    uint32_t h0 = 0;
-                    const uint64_t ee = i < kRepCap ? L.s_rep[i] : ent.at(cb + s_list[i], h0);
+                    const uint64_t ee = i < kRepCap ? L.s_rep[i] : ent.at_any(cb + s_list[i]);
                     const uint32_t b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
                     if (b % kApWaves == wave) accN[b] = 0;
                 }
@@ -2172,25 +2176,40 @@ struct SegLds {
     uint32_t spre[kSegAll];       // logical start of each run, then the table's total
 };
 
-// The lanes of a wave ask for consecutive q: the run of the wave's first lane is
-// found with wave-uniform reads (from the wave's hint h, else by bisection), the
-// other lanes step forward from it (a run shorter than the wave: a few steps).
-__device__ __forceinline__ uint64_t EntSegs::at(uint32_t q, uint32_t &h) const {
+// The run of the wave's first lane comes from the cursor, advanced (wave-uniform
+// reads, bisection) only when that lane has left it: about once per 16 wave loads
+// at the bench geometry.  Lanes past the run's end step forward on their own.
+__device__ __forceinline__ uint64_t EntSegs::at(uint32_t q, Cur &c) const {
     const uint32_t *spre = G->spre + off, *sbase = G->sbase + off;
     const uint32_t qf = __builtin_amdgcn_readfirstlane(q);
-    uint32_t r = __builtin_amdgcn_readfirstlane(h);
-    if (!(r < nseg && spre[r] <= qf)) r = 0;
-    if (r + 1 < nseg && spre[r + 1] <= qf) {
-        uint32_t lo = r + 1, hi = nseg;  // largest r with spre[r] <= qf (empty runs skipped)
+    if (qf >= c.hi) {  // wave-uniform
+        uint32_t lo = c.r, hi = nseg;  // largest r with spre[r] <= qf (empty runs skipped)
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (spre[mid] <= qf) lo = mid; else hi = mid;
         }
-        r = lo;
+        c.r = __builtin_amdgcn_readfirstlane(lo);
+        c.lo = __builtin_amdgcn_readfirstlane(spre[c.r]);
+        c.hi = __builtin_amdgcn_readfirstlane(spre[c.r + 1]);
+        c.base = __builtin_amdgcn_readfirstlane(sbase[c.r]);
     }
-    h = r;
-    while (r + 1 < nseg && spre[r + 1] <= q) r++;
-    return p[sbase[r] + (q - spre[r])];
+    uint32_t idx = c.base + (q - c.lo);
+    if (q >= c.hi) {
+        uint32_t r2 = c.r + 1;
+        while (spre[r2 + 1] <= q) r2++;  // spre[nseg] = the total > q
+        idx = sbase[r2] + (q - spre[r2]);
+    }
+    return p[idx];
+}
+
+__device__ __forceinline__ uint64_t EntSegs::at_any(uint32_t q) const {
+    const uint32_t *spre = G->spre + off, *sbase = G->sbase + off;
+    uint32_t lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (spre[mid] <= q) lo = mid; else hi = mid;
+    }
+    return p[sbase[lo] + (q - spre[lo])];
 }
 
 // One wave: tile st's runs of rounds [w0, w0 + nr) into the table at off (nr + 1 entries).
