@@ -1956,120 +1956,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
 #endif
 }
 
-// Super-bin (2^sub_bits tiles, C5-size widths): stable partition of the bin's
-// updates by tile into ent2[beg, end); P.soff[t] = start of tile t (relative).
-struct SubLds {
-    uint32_t base[16];
-    uint32_t soff[17];
-};
-constexpr uint32_t kSubPairs = kApItems * kApWaves;  // (item, wave) groups of a round, in stream order
-#ifndef GNS_SUBPART_LAUNCH
-#define GNS_SUBPART_LAUNCH 1
-#endif
-constexpr bool kSubpartLaunch = GNS_SUBPART_LAUNCH != 0;  // 0: K4 sub-partitions each super-bin itself
-
-// Two passes over the bin: per-tile totals (ballots), then rounds of kApChunk
-// updates in (item, wave, lane) = stream order: each (item, wave) group's
-// count per tile, one scan per tile over the groups, direct stores.  Two
-// barriers per round; cnt = 2 * kSubPairs * 16 words of LDS scratch (double
-// buffered), which the caller lends from the tile accumulators.
-__device__ __forceinline__ void sub_partition(const uint64_t *ent, uint64_t *ent2, uint32_t beg, uint32_t end,
-                                              uint32_t tile_bits, uint32_t sub_bits, SubLds &P, uint32_t *cnt) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t nsub = 1u << sub_bits;
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    if (tid < 16) P.base[tid] = 0;
-    __syncthreads();
-    {
-        // pass 1: per-tile totals; 8 entries per thread per step (16-byte loads,
-        // order does not matter here), counted in registers, one wave sum per tile
-        uint32_t c[16];
-#pragma unroll
-        for (uint32_t t = 0; t < 16; t++) c[t] = 0;
-        const uint32_t a0 = (beg + 1u) & ~1u;  // 16-byte aligned start (entries are 8 B)
-        if (a0 > beg && tid == 0) {
-            const uint32_t sb0 = ((uint32_t)(ent[beg] >> 32) & kLowMask) >> tile_bits;
-#pragma unroll
-            for (uint32_t t = 0; t < 16; t++) c[t] += sb0 == t ? 1u : 0u;
-        }
-        for (uint32_t q0 = a0 + tid * 8; q0 < end; q0 += kApThreads * 8) {
-            uint64_t v[8];
-            if (q0 + 8 <= end) {
-                const uint4 *p4 = reinterpret_cast<const uint4 *>(ent + q0);
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const uint4 x = p4[i];
-                    v[2 * i] = (uint64_t)x.y << 32 | x.x;
-                    v[2 * i + 1] = (uint64_t)x.w << 32 | x.z;
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < 8; i++) v[i] = q0 + i < end ? ent[q0 + i] : ~0ull;
-            }
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint32_t sb = v[i] == ~0ull ? 0xFFu : (((uint32_t)(v[i] >> 32) & kLowMask) >> tile_bits);
-#pragma unroll
-                for (uint32_t t = 0; t < 16; t++) c[t] += (t < nsub && sb == t) ? 1u : 0u;
-            }
-        }
-#pragma unroll
-        for (uint32_t t = 0; t < 16; t++) {
-            if (t < nsub) {  // wave-uniform
-                const uint32_t tot = __ockl_wfred_add_u32(c[t]);
-                if (lane == 0 && tot) atomicAdd(&P.base[t], tot);
-            }
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t run = 0;
-        for (uint32_t t = 0; t < nsub; t++) { P.soff[t] = run; const uint32_t c = P.base[t]; P.base[t] = run; run += c; }
-        P.soff[nsub] = run;
-    }
-    __syncthreads();
-    uint32_t par = 0;
-    for (uint32_t rb = beg; rb < end; rb += kApChunk) {
-        uint32_t *cb = cnt + par * (kSubPairs * 16);
-        par ^= 1u;
-        uint64_t e[kApItems];
-        uint32_t sub[kApItems], before[kApItems];
-#pragma unroll
-        for (int j = 0; j < kApItems; j++) {
-            const uint32_t q = rb + j * kApThreads + tid;
-            const bool valid = q < end;
-            e[j] = valid ? ent[q] : 0ull;
-            sub[j] = valid ? (((uint32_t)(e[j] >> 32) & kLowMask) >> tile_bits) : 0xFFu;
-            uint64_t peers = __ballot(valid);
-            for (uint32_t bit = 0; bit < sub_bits; bit++) {
-                const uint64_t m = __ballot(valid && ((sub[j] >> bit) & 1u));
-                peers &= ((sub[j] >> bit) & 1u) ? m : ~m;
-            }
-            before[j] = __popcll(peers & lt_mask);
-            // this wave's slots of group (j, wave): zeroed, then the first lane of
-            // each tile's peers writes the count (one wave: LDS ops stay in order)
-            if (lane < 16) cb[(j * kApWaves + wave) * 16 + lane] = 0;
-            if (valid && before[j] == 0) cb[(j * kApWaves + wave) * 16 + sub[j]] = (uint32_t)__popcll(peers);
-        }
-        __syncthreads();
-        if (wave < nsub) {  // wave t: exclusive scan of tile t's group counts -> absolute slots
-            static_assert(kSubPairs == 128, "two groups per lane");
-            const uint32_t t = wave;
-            const uint32_t x0 = cb[(2 * lane) * 16 + t], x1 = cb[(2 * lane + 1) * 16 + t];
-            const uint32_t b0 = P.base[t];
-            const uint32_t inc = wave_incl_scan(x0 + x1);
-            const uint32_t ex = b0 + inc - (x0 + x1);
-            cb[(2 * lane) * 16 + t] = ex;
-            cb[(2 * lane + 1) * 16 + t] = ex + x0;
-            if (lane == 63) P.base[t] = b0 + inc;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kApItems; j++)
-            if (sub[j] != 0xFFu) ent2[beg + cb[(j * kApWaves + wave) * 16 + sub[j]] + before[j]] = e[j];
-    }
-    __syncthreads();
-}
+constexpr uint32_t kSubPairs = kApItems * kApWaves;  // (item, wave) groups of a k_subpart round, in stream order
 
 // Super-bin sub-partition as a launch of its own, one workgroup per super-bin and
 // two per CU (16 KB of LDS instead of K4's 156 KB), so that its barrier- and
@@ -2077,9 +1964,9 @@ __device__ __forceinline__ void sub_partition(const uint64_t *ent, uint64_t *ent
 // one-workgroup-per-CU loop.  One pass: every round of kApChunk updates is
 // grouped by tile in place of the round (stable inside each tile), and the
 // round's tile starts go to rseg; K4 reads a tile as its run in each round, in
-// round order, which is the tile's stream order.  (The inline variant,
-// sub_partition, counts first and writes each tile contiguously: a second read
-// of every update.)  Round r of bin b has index beg/kApChunk + r + b: unique
+// round order, which is the tile's stream order.  (Round 4 counted every tile of
+// the bin first and wrote each tile contiguously: a second read of every update.)
+// Round r of bin b has index beg/kApChunk + r + b: unique
 // and below total/kApChunk + nbins.
 #ifndef GNS_SEG_ALL
 #define GNS_SEG_ALL 416
@@ -2278,13 +2165,12 @@ __device__ __forceinline__ ApplyTile apply_bin(const ApplyArgs &a, uint32_t k) {
 }
 
 // MODE 0: rows of single tiles (bins = tiles); 1: super-bins read through k_subpart's
-// rounds (3: the super-bins too big for MODE 1's tables, a second launch); 2:
-// super-bins sub-partitioned inline (GNS_SUBPART_LAUNCH=0).  One variant per
-// launch, so each inlines only its own tile loop (and stays within 128 VGPRs).
+// rounds (3: the super-bins too big for MODE 1's tables, a second launch).  One
+// variant per launch, so each inlines only its own tile loop (and stays within 128
+// VGPRs).
 template <int MODE>
 __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
     __shared__ ApplyLds L;
-    __shared__ SubLds P;
     __shared__ SegLds G;
     __shared__ uint32_t s_k;
     const CmGeom &g = a.g;
@@ -2320,10 +2206,7 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
                            min(tw, g.w - cur.bbase), cur.bbase, pre, nb_cbase, nb_tn);
             } else {
                 const uint32_t nsub = 1u << g.sub_bits;
-#ifdef GNS_K4_PROF
-                const uint64_t t_sp = __builtin_amdgcn_s_memtime();
-#endif
-                if constexpr (MODE == 1 || MODE == 3) {  // rounds grouped by tile (k_subpart)
+                {  // MODE 1 / 3: rounds grouped by tile (k_subpart)
                     const uint64_t ridx0 = (uint64_t)(cur.beg / kApChunk) + cur.bin;
                     const uint32_t R = (cur.end - cur.beg + kApChunk - 1) / kApChunk;
                     // MODE 1: bins whose tables fit kSegAll, all tiles' at once or (bigger bins)
@@ -2383,31 +2266,6 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
                                 }
                             }
                         }
-                    }
-                } else {
-                    sub_partition(a.entries, a.entries2, cur.beg, cur.end, g.tile_bits, g.sub_bits, P,
-                                  reinterpret_cast<uint32_t *>(L.accN));
-#ifdef GNS_K4_PROF
-                    if (tid == 0) atomicAdd(&a.stats[14], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_sp));
-#endif
-                    for (uint32_t st = 0; st < nsub; st++) {
-                        const uint32_t tbase = cur.bbase + (st << g.tile_bits);
-                        const uint32_t sb = cur.beg + P.soff[st], se = cur.beg + P.soff[st + 1];
-                        if (tbase >= g.w || sb >= se) continue;
-                        // next tile: the next non-empty tile of this bin, else the next bin's first
-                        uint64_t ncb = nb_cbase;
-                        uint32_t ntn = nb_tn;
-                        for (uint32_t s2 = st + 1; s2 < nsub; s2++) {
-                            const uint32_t tb2 = cur.bbase + (s2 << g.tile_bits);
-                            if (tb2 < g.w && P.soff[s2] < P.soff[s2 + 1]) {
-                                ncb = (uint64_t)cur.r * g.w + tb2;
-                                ntn = min(tw, g.w - tb2);
-                                break;
-                            }
-                        }
-                        apply_tile(a, L, EntFlat{a.entries2}, sb, se, (uint64_t)cur.r * g.w + tbase,
-                                   min(tw, g.w - tbase), tbase, pre, ncb, ntn);
-                        __syncthreads();
                     }
                 }
             }
@@ -3564,7 +3422,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs; a.work = cm->work;
         GNS_HIP(hipMemsetAsync(cm->work, 0, 12, s));
         ScopedStage st(cm->timer, 4);
-        if (g.sub_bits && kSubpartLaunch) {
+        if (g.sub_bits) {
             // 512-thread workgroups (16 updates per thread and round, two per CU) when a
             // wave per tile fits; GNS_SUBPART_NT=1024 for the A/B
             if ((1u << g.sub_bits) <= 8 && cm->subpart_nt != 1024)
@@ -3576,14 +3434,14 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         }
         // persistent: one workgroup per CU (the tile LDS fills a CU), bins from the schedule counter
         const dim3 apg(std::min(g.nbins, cm->ncu));
-        if (!g.sub_bits) hipLaunchKernelGGL(k_apply<0>, apg, dim3(kApThreads), 0, s, a);
-        else if (a.rseg) {
+        if (!g.sub_bits) {
+            hipLaunchKernelGGL(k_apply<0>, apg, dim3(kApThreads), 0, s, a);
+        } else {
             hipLaunchKernelGGL(k_apply<1>, apg, dim3(kApThreads), 0, s, a);
             GNS_HIP(hipGetLastError());
             // super-bins too big for K4's LDS tables (none at the bench geometry): windows of rounds
             hipLaunchKernelGGL(k_apply<3>, apg, dim3(kApThreads), 0, s, a);
         }
-        else hipLaunchKernelGGL(k_apply<2>, apg, dim3(kApThreads), 0, s, a);
         GNS_HIP(hipGetLastError());
     }
     // hot bins: chip-wide aggregate, exact decide, in-order fallback
