@@ -274,6 +274,7 @@ def test_large_sizes_mixed_owner(gpu, oracle):
     (1 << 24, 8, 4, 1 << 16, 2_000_000),   # C5 geometry: bins of 16 LDS tiles
     (1 << 22, 8, 8, 1 << 15, 1_000_000),   # d * tiles > 4096: bins of 2 tiles
     (5_000_000, 3, 13, 50_000, 1_000_000),  # non power-of-two wide row
+    (20_000_000, 8, 4, 1 << 15, 1_000_000),  # bins of 16 tiles (k_subpart's 1024-thread variant)
 ])
 def test_wide_rows_parity(gpu, oracle, w, d, K, nflows, n):
     """Widths beyond 1024 LDS tiles per row: K3 bins hold 2^sub_bits tiles and K4
