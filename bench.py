@@ -981,7 +981,7 @@ def main():
         "config": {"workload": "configs[1]: Count-Min d=4 w=2^20, 100M Zipf(1.1) 5-tuple headers in HBM per GPU, "
                                "bit-exact counters", "packets_per_step_per_gpu": n, "device_batch": batch,
                    "key": "5-tuple (37 B)" if K == 37 else "[SrcIP] (16 B)",
-                   "parallelism": f"flow-hash shards x{world}",
+                   "parallelism": f"owner-key shards x{world} (SrcIP slot; each GPU generates its shard of the stream)",
                    "windows": f"steps use stream windows 0..{win[0] - 1} (warmup first), none replayed"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
