@@ -207,9 +207,11 @@ enum { CM_FOUND = 0, CM_PENDING = 1, CM_FULL = 2, CM_CLAIMED = 3 };
 // included) and reports CM_CLAIMED when this lane inserted the key (the
 // caller then writes the bucket words).  K is a compile-time constant in the
 // specialized kernels.
+template <int N>  // r: words 0..15 of the record (N >= 16)
 __device__ __forceinline__ int cm_find_or_claim(const DictDev &D, const uint32_t (&kw)[GNS_KWMAX], uint32_t K,
                                                 uint32_t slot, uint32_t epoch, uint32_t *out,
-                                                uint32_t (&r)[16]) {
+                                                uint32_t (&r)[N]) {
+    static_assert(N >= 16, "record words 0..15");
     const uint32_t nkw = (K + 3) >> 2;
     for (int probe = 0; probe < GNS_DICT_MAX_PROBE; probe++) {
         const uint4 *q = reinterpret_cast<const uint4 *>(D.rec + (size_t)slot * D.RW);
@@ -271,17 +273,22 @@ struct CsRun {
     uint32_t sb;  // stream base of row 0 (uniform)
 };
 
+// record quads a K1 probe loads: words 0..15, and 16..19 (rows 4..7 of the bucket cache) for deep sketches
+template <int RMAX>
+constexpr int kProbeQuads = RMAX > 4 ? 5 : 4;
+
 template <int RMAX, bool CM>
 __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S, uint32_t K, uint32_t d, bool bw,
                                            uint64_t p, uint64_t beg, bool ok, const uint32_t (&kw)[GNS_KWMAX],
-                                           uint32_t slot0, const uint4 (&r4)[4], uint32_t sz, uint32_t &n_ok,
-                                           CsRun<RMAX> &cs) {
+                                           uint32_t slot0, const uint4 (&r4)[kProbeQuads<RMAX>], uint32_t sz,
+                                           uint32_t &n_ok, CsRun<RMAX> &cs) {
+    constexpr int NQ = kProbeQuads<RMAX>;
     uint32_t *s_tab = S.s_tab, *s_hist = S.s_hist, *s_hFc = S.s_hFc, *s_hFs = S.s_hFs, *s_nfc = S.s_nfc;
     uint32_t *s_nfs = S.s_nfs, *s_smax = S.s_smax;
     unsigned long long *s_os = S.s_os, *s_fs = S.s_fs;
     uint32_t &s_pend = *S.s_pend, &s_full = *S.s_full;
     uint32_t kid = kPendingId;  // flow id when already committed (pending: foreign to every owner)
-    uint32_t rec[16];
+    uint32_t rec[4 * NQ];
     int res = CM_FULL;
     uint32_t out = 0;
     // first probe (the home slot, loaded by the caller): 0 hit, 1 claimed in this
@@ -289,7 +296,7 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
     int first = 0;
     if (ok) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < NQ; i++) {
             rec[4 * i] = r4[i].x; rec[4 * i + 1] = r4[i].y; rec[4 * i + 2] = r4[i].z; rec[4 * i + 3] = r4[i].w;
         }
         const uint32_t tag = rec[0];
@@ -301,18 +308,20 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
         if (first == 0) { res = CM_FOUND; out = slot0; }
         else if (first == 1) { res = CM_PENDING; out = slot0; }
     }
-    // row buckets: from the record's cache (rows 0..3 of a committed flow), else hashed
+    // row buckets: from the record's cache (rows 0..3 of a committed flow, 0..7 in a
+    // 32-word record), else hashed
     uint32_t bk[RMAX];
     const bool cached = bw && ok && first == 0;
+    const uint32_t nc = (NQ > 4 && a.D.RW >= 32) ? 8u : 4u;  // cached rows
 #pragma unroll
-    for (uint32_t rr = 0; rr < RMAX; rr++) bk[rr] = (rr < 4 && cached) ? rec[12 + rr] : 0u;
-    if (__ballot(ok && !cached) || (RMAX > 4 && d > 4)) {
+    for (uint32_t rr = 0; rr < RMAX; rr++) bk[rr] = (rr < nc && cached) ? rec[12 + rr] : 0u;
+    if (__ballot(ok && !cached) || (RMAX > 4 && d > nc)) {
         uint32_t mk[GNS_KWMAX];
         mm3_premix<GNS_KWMAX>(kw, K, mk);
 #pragma unroll
         for (uint32_t rr = 0; rr < RMAX; rr++) {
             if (rr >= d) break;
-            if (ok && (!cached || rr >= 4)) bk[rr] = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, K, a.g.seeds[rr]));
+            if (ok && (!cached || rr >= nc)) bk[rr] = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, K, a.g.seeds[rr]));
         }
     }
     // designated-bucket slots of the row buckets (LDS lookups, reused by the rows loop)
@@ -360,8 +369,8 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
     if (bw && res == CM_CLAIMED) {  // publish the bucket cache with the key (visible next launch)
         uint32_t *tp = a.D.rec + (size_t)out * a.D.RW;
 #pragma unroll
-        for (uint32_t rr = 0; rr < 4; rr++)
-            if (rr < d) tp[12 + rr] = bk[rr];
+        for (uint32_t rr = 0; rr < RMAX; rr++)
+            if (rr < d && rr < nc) tp[12 + rr] = bk[rr];
     }
     if (!ok) sz = 0;
     // low 16 bits: packets inserted; high 16: of them with a size taking the
@@ -530,7 +539,8 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
             hsz = a.in.sizes[pc];
         };
         // stage B of packet q: parse the prefetched record, key, slot, issue the probe
-        auto stage_b = [&](uint64_t q, bool &okq, uint32_t (&kwq)[GNS_KWMAX], uint32_t &slotq, uint4 (&r4q)[4],
+        constexpr int NQ = kProbeQuads<RMAX>;
+        auto stage_b = [&](uint64_t q, bool &okq, uint32_t (&kwq)[GNS_KWMAX], uint32_t &slotq, uint4 (&r4q)[NQ],
                            uint32_t &szq) {
             okq = q < wend;
             uint32_t cw[16];
@@ -571,25 +581,25 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
             if (okq) {
                 const uint4 *rq = reinterpret_cast<const uint4 *>(a.D.rec + (size_t)slotq * a.D.RW);
 #pragma unroll
-                for (int i = 0; i < 4; i++) r4q[i] = (4u * i < a.D.RW) ? rq[i] : make_uint4(0, 0, 0, 0);
+                for (int i = 0; i < NQ; i++) r4q[i] = (4u * i < a.D.RW) ? rq[i] : make_uint4(0, 0, 0, 0);
             }
         };
         load_hdr(wbeg + loff);
         bool okc;
         uint32_t kwc[GNS_KWMAX], slotc, szc;
-        uint4 r4c[4];
+        uint4 r4c[NQ];
         stage_b(wbeg + loff, okc, kwc, slotc, r4c, szc);
         for (uint64_t p0 = wbeg; p0 < wend; p0 += STEP) {  // wave-uniform trip count
             bool okn = false;
             uint32_t kwn[GNS_KWMAX], slotn = 0, szn = 0;
-            uint4 r4n[4];
+            uint4 r4n[NQ];
             if (p0 + STEP < wend) stage_b(p0 + STEP + loff, okn, kwn, slotn, r4n, szn);
             k1_consume<RMAX, CM>(a, S, K, d, bw, p0 + loff, beg, okc, kwc, slotc, r4c, szc, n_ok, cs);
             okc = okn; slotc = slotn; szc = szn;
 #pragma unroll
             for (int i = 0; i < GNS_KWMAX; i++) kwc[i] = kwn[i];
 #pragma unroll
-            for (int i = 0; i < 4; i++) r4c[i] = r4n[i];
+            for (int i = 0; i < NQ; i++) r4c[i] = r4n[i];
         }
     } else {
         for (uint64_t p0 = wbeg; p0 < wend; p0 += STEP) {  // wave-uniform trip count
@@ -610,11 +620,11 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
                 mm3_premix<GNS_KWMAX>(kw, K, mk);
                 slot0 = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
             }
-            uint4 r4[4];
+            uint4 r4[kProbeQuads<RMAX>];
             if (ok) {
                 const uint4 *q = reinterpret_cast<const uint4 *>(a.D.rec + (size_t)slot0 * a.D.RW);
 #pragma unroll
-                for (int i = 0; i < 4; i++) r4[i] = (4u * i < a.D.RW) ? q[i] : make_uint4(0, 0, 0, 0);
+                for (int i = 0; i < kProbeQuads<RMAX>; i++) r4[i] = (4u * i < a.D.RW) ? q[i] : make_uint4(0, 0, 0, 0);
             }
             k1_consume<RMAX, CM>(a, S, K, d, bw, p, beg, ok, kw, slot0, r4, ok ? a.in.sizes[p] : 0u, n_ok, cs);
         }
@@ -697,7 +707,8 @@ __global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
                 uint32_t mk[GNS_KWMAX];
                 mm3_premix<GNS_KWMAX>(kw, a.kp.K, mk);
                 uint32_t *tp = a.D.rec + (size_t)out * a.D.RW;
-                for (uint32_t rr = 0; rr < 4 && rr < a.g.d; rr++)
+                const uint32_t nc = a.D.RW >= 32 ? 8u : 4u;  // cached rows
+                for (uint32_t rr = 0; rr < nc && rr < a.g.d; rr++)
                     tp[12 + rr] = row_index(a.g, mm3_chain<GNS_KWMAX>(mk, a.kp.K, a.g.seeds[rr]));
             }
         } else if (r == CM_PENDING) {
@@ -3747,8 +3758,8 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         cm->max_flows = mf;
         cm->D.mask = (uint32_t)(slots - 1);
         cm->D.K = cm->K;
-        cm->D.RW = dict_record_words_cm(cm->K);
-        cm->D.bw = cm->D.RW == 16 && 1 + (cm->K + 3) / 4 <= 12 ? 1u : 0u;
+        cm->D.RW = dict_record_words_cm(cm->K, g.d);
+        cm->D.bw = cm->D.RW >= 16 && 1 + (cm->K + 3) / 4 <= 12 ? 1u : 0u;
         cm->D.seed = 0x2545F491u;
         if ((rc = dalloc_t(&cm->D.rec, slots * cm->D.RW)) != GNS_OK) break;
         if ((rc = dalloc_t(&cm->dctl, 4)) != GNS_OK || (rc = dalloc_t(&cm->stats_bak, 3)) != GNS_OK) break;

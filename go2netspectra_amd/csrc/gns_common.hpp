@@ -90,10 +90,12 @@ inline uint32_t dict_record_words(uint32_t K) {
 
 // Count-Min records: 16 words whenever the key leaves words 12..15 free, which
 // then cache the flow's bucket indices of rows 0..3 (written by the claimer),
-// so a packet of a known flow needs no per-row MurmurHash3.
-inline uint32_t dict_record_words_cm(uint32_t K) {
+// so a packet of a known flow needs no per-row MurmurHash3; deeper sketches take
+// 32-word records (one 128-byte line, as a 64-byte record's probe fetches anyway)
+// whose words 12..19 cache rows 0..7.
+inline uint32_t dict_record_words_cm(uint32_t K, uint32_t d) {
     const uint32_t w = 1 + (K + 3) / 4;
-    return (K > 12 && w <= 12) ? 16u : dict_record_words(K);
+    return (K > 12 && w <= 12) ? (d > 4 ? 32u : 16u) : dict_record_words(K);
 }
 
 // Flow-dictionary rebuild (gns_dict.hip): keep the records whose id some

@@ -452,16 +452,18 @@ def test_gathered_heavy_rows_order_on_device(gpu):
         assert np.array_equal(np.ascontiguousarray(got[:, K:]).view("<u4").reshape(-1), wv)
 
 
-@pytest.mark.parametrize("batch", [0, 40_000])
-def test_unbounded_distinct_flows_reclaim(gpu, oracle, batch):
+@pytest.mark.parametrize("batch,w,d,K,max_flows", [
+    (0, 2048, 2, 16, 16384), (40_000, 2048, 2, 16, 16384),
+    (40_000, 1024, 8, 37, 32768),  # 32-word records: the bucket cache of rows 0..7 moves with them
+])
+def test_unbounded_distinct_flows_reclaim(gpu, oracle, batch, w, d, K, max_flows):
     """Memory bounded like the reference (count_min.go:66-81 is fixed-size): more
     than 50x max_flows distinct flows in one period.  Flows no bucket names are
     reclaimed between batches; a batch whose new flows overflow the dictionary is
     undone, the dictionary rebuilt and the batch re-run in halves.  The state stays
     bit-exact, no GNS_E_FULL, and a snapshot view taken mid-stream keeps answering
     the state at its refresh across the reclaims (its ids are remapped too)."""
-    rng = np.random.default_rng(91 + batch)
-    w, d, K, max_flows = 2048, 2, 16, 16384   # live ids <= 2*d*w = 8192
+    rng = np.random.default_rng(91 + batch + d)  # live ids <= 2*d*w <= max_flows / 2
     cm, orc = make_pair(oracle, w, d, K, st=20_000, ct=30, max_flows=max_flows, batch_packets=batch)
     view = cm.view()
     heavy = rng.integers(0, 256, (300, K), dtype=np.uint8)
