@@ -454,7 +454,7 @@ def test_gathered_heavy_rows_order_on_device(gpu):
 
 @pytest.mark.parametrize("batch,w,d,K,max_flows", [
     (0, 2048, 2, 16, 16384), (40_000, 2048, 2, 16, 16384),
-    (40_000, 1024, 8, 37, 32768),  # 32-word records: the bucket cache of rows 0..7 moves with them
+    (40_000, 512, 8, 37, 16384),  # 32-word records: the bucket cache of rows 0..7 moves with them
 ])
 def test_unbounded_distinct_flows_reclaim(gpu, oracle, batch, w, d, K, max_flows):
     """Memory bounded like the reference (count_min.go:66-81 is fixed-size): more
