@@ -2039,15 +2039,16 @@ __global__ __launch_bounds__(NT, NT == 512 ? 4 : 1) void k_subpart(ApplyArgs a, 
         }
         __syncthreads();
         if (wave < nsub) {  // (nsub <= kW) wave t: tile t's start in the round + exclusive scan of its group counts
-            static_assert(kSubPairs == 128, "two groups per lane");
+            constexpr uint32_t GPL = kSubPairs / 64;  // groups per lane (1 or 2)
+            static_assert(GPL * 64 == kSubPairs && GPL <= 2, "one or two groups per lane");
             const uint32_t t = wave;
             uint32_t b0 = 0;
             for (uint32_t u = 0; u < t; u++) b0 += tt[u];
-            const uint32_t x0 = cb[(2 * lane) * 16 + t], x1 = cb[(2 * lane + 1) * 16 + t];
+            const uint32_t x0 = cb[(GPL * lane) * 16 + t], x1 = GPL == 2 ? cb[(GPL * lane + 1) * 16 + t] : 0u;
             const uint32_t inc = wave_incl_scan(x0 + x1);
             const uint32_t ex = b0 + inc - (x0 + x1);
-            cb[(2 * lane) * 16 + t] = ex;
-            cb[(2 * lane + 1) * 16 + t] = ex + x0;
+            cb[(GPL * lane) * 16 + t] = ex;
+            if (GPL == 2) cb[(GPL * lane + 1) * 16 + t] = ex + x0;
             if (lane == 0) rseg[((uint64_t)(rb / kApChunk) + bin) * 16 + t] = (uint16_t)b0;
         }
         // the next round's tile totals (last read in the previous round, before this round's first barrier)
@@ -2226,8 +2227,7 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
                     const bool fits = R + 1 <= kSegAll;
                     if ((MODE == 1) == fits) {
                         if (MODE == 1 && all) {
-                            if (tid >> 6 < nsub) {
-                                const uint32_t t = tid >> 6;
+                            for (uint32_t t = tid >> 6; t < nsub; t += kApWaves) {  // wave t (mod waves): tile t
                                 const uint32_t tot = seg_scan_wave(a, G, cur.beg, cur.end, ridx0, nsub, t, 0, R, t * (R + 1));
                                 if ((tid & 63u) == 0) G.tot[t] = tot;
                             }
@@ -3444,7 +3444,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
             a.rseg = cm->rseg;
         }
         // persistent: one workgroup per CU (the tile LDS fills a CU), bins from the schedule counter
-        const dim3 apg(std::min(g.nbins, cm->ncu));
+        const dim3 apg(std::min(g.nbins, cm->ncu * (kApThreads <= 512 ? 2u : 1u)));  // workgroups the LDS fits per CU
         if (!g.sub_bits) {
             hipLaunchKernelGGL(k_apply<0>, apg, dim3(kApThreads), 0, s, a);
         } else {
