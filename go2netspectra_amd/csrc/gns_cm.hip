@@ -1583,6 +1583,9 @@ struct ApplyLds {
     uint64_t s_rep[kRepCap];            // the first kRepCap replay entries themselves (no global re-read)
     uint32_t s_wc[kApItems * kApWaves];
     uint32_t s_any, s_nlist;
+#ifdef GNS_K4_PROF
+    uint32_t s_pmax;  // the chunk's largest per-wave replay list (balance probe)
+#endif
 };
 
 __device__ __forceinline__ void decode_entry(const uint64_t *ovf, uint64_t e, uint32_t &k, uint32_t &s) {
@@ -1751,6 +1754,10 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
     // engine counters in registers (global atomics inside the loop would be
     // drained by the next chunk's load waits)
     uint32_t st_chunks = 0, st_rep = 0, st_crep = 0;
+#ifdef GNS_K4_PROF
+    uint64_t pmax_sum = 0;
+    if (tid == 0) L.s_pmax = 0;
+#endif
     for (uint32_t cb = beg; cb < end; cb += kApChunk) {
         if (tid == 0) { s_any = 0; st_chunks++; }
         __syncthreads();
@@ -1897,6 +1904,9 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                 if (c <= kWl) nmine = c;
             }
             K4_MARK(4);
+#ifdef GNS_K4_PROF
+            if (lane == 0) atomicMax(&L.s_pmax, nmine == 0xFFFFFFFFu ? 0u : nmine);
+#endif
             if (nmine != 0xFFFFFFFFu) {
                 const uint16_t *wl = s_list + wave * kWl;
                 for (uint32_t g0 = 0; g0 < nmine; g0 += 64) {
@@ -1943,6 +1953,9 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             }
         }
         __syncthreads();
+#ifdef GNS_K4_PROF
+        if (tid == 0) { pmax_sum += L.s_pmax; L.s_pmax = 0; }
+#endif
 #pragma unroll
         for (int j = 0; j < kApItems; j++) e[j] = en[j];
     }
@@ -1954,6 +1967,9 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
         a.C[cbase + i] = cs.x; a.Fc[cbase + i] = f.x;
         a.S[cbase + i] = cs.y; a.Fs[cbase + i] = f.y;
     }
+#ifdef GNS_K4_PROF
+    if (tid == 0) atomicAdd(&a.stats[14], (unsigned long long)pmax_sum);
+#endif
     if (tid == 0) {
         atomicAdd(&a.stats[5], (unsigned long long)st_rep);
         atomicAdd(&a.stats[6], (unsigned long long)st_chunks);
@@ -4388,7 +4404,9 @@ int gns_cm_counters(gns_cm *cm, uint64_t out[8]) {
 #ifdef GNS_K4_PROF  // profiling build: K4 phase cycles (classify, decide, compact, replay, tile load,
                     // tile store, sub-partition), chunks
     for (int i = 0; i < 7; i++) out[i] = h[8 + i];
-    out[7] = h[15];  // replay groups (out[6]: sub-partition)
+    out[7] = h[15];  // replay groups
+    out[4] = h[5];   // replayed updates (replaces replay gather); out[6]: sum over chunks of the
+                     // largest per-wave replay list (balance: out[6] * waves / out[4])
 #else
     for (int i = 0; i < 8; i++) out[i] = h[i];
 #endif
