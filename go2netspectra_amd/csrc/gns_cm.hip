@@ -1503,6 +1503,9 @@ constexpr uint64_t kM14 = (1ull << 14) - 1;
 constexpr uint32_t kAccForce = 42;
 static_assert(kApChunk < (1u << 14), "accN field widths");
 static_assert(kScRound <= 65536, "K3 packs ranks in 16 bits");
+#ifndef GNS_REPLAY_LEAD
+#define GNS_REPLAY_LEAD 1  // 0: one LDS round per same-bucket lane (A/B)
+#endif
 #ifndef GNS_REP_CAP
 #define GNS_REP_CAP 1536
 #endif
@@ -1584,7 +1587,7 @@ struct ApplyLds {
     uint32_t s_wc[kApItems * kApWaves];
     uint32_t s_any, s_nlist;
 #ifdef GNS_K4_PROF
-    uint32_t s_pmax;  // the chunk's largest per-wave replay list (balance probe)
+    uint32_t s_pmax, s_psum;  // the chunk's largest and summed per-wave replay cycles (balance probe)
 #endif
 };
 
@@ -1605,7 +1608,6 @@ __device__ __forceinline__ void decode_entry(const uint64_t *ovf, uint64_t e, ui
 __device__ __forceinline__ void replay_group(ApplyLds &L, bool pending, uint32_t b, uint32_t k, uint32_t s,
                                              uint32_t rf) {
     const uint32_t lane = threadIdx.x & 63u;
-    uint32_t *own = reinterpret_cast<uint32_t *>(L.accS);
     // a bucket with many updates in this group (a contested bucket that
     // failed the linear check): wave-parallel sequence, 64 updates per step
     for (;;) {
@@ -1629,6 +1631,43 @@ __device__ __forceinline__ void replay_group(ApplyLds &L, bool pending, uint32_t
         }
         if (mine) pending = false;
     }
+#if GNS_REPLAY_LEAD
+    // the rest: the lowest lane of each bucket's lanes (its leader) takes the bucket's
+    // state into registers and applies its peers' updates in lane (= stream) order,
+    // fetched with cross-lane reads, then writes the state back once
+    unsigned long long *peer = L.accS;  // per bucket: the mask of this group's lanes on it
+    if (pending) atomicOr(&peer[b], 1ull << lane);
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t pm = pending ? (uint64_t)peer[b] : 0ull;
+    const bool leader = pending && (uint32_t)__ffsll((long long)pm) - 1 == lane;
+    uint2 cs = make_uint2(0, 0), f = make_uint2(0, 0);
+    if (leader) { cs = L.sCS[b]; f = L.sF[b]; }
+    uint64_t rem = leader ? pm : 0ull;
+    while (__ballot(rem != 0)) {
+        const uint32_t src = rem ? (uint32_t)__ffsll((long long)rem) - 1 : lane;
+        const uint32_t kp = __shfl(k, src, 64), sp = __shfl(s, src, 64);
+        if (rem) {
+            if (rf & 2u) {  // size half, count_min.go:99-128
+                uint32_t S = cs.y, F = f.y;
+                if (S == 0) { S = sp; F = kp; }
+                else if (F == kp) S = S + sp;
+                else if (sp > S) { S = sp; F = kp; }
+                else S = S - sp;
+                cs.y = S; f.y = F;
+            }
+            if (rf & 1u) {  // count half, count_min.go:130-155
+                uint32_t C = cs.x, F = f.x;
+                if (C == 0) { C = 1; F = kp; }
+                else if (F == kp) C = C + 1;
+                else { C = C - 1; if (C == 0) F = kp; }
+                cs.x = C; f.x = F;
+            }
+            rem &= rem - 1;
+        }
+    }
+    if (leader) { L.sCS[b] = cs; L.sF[b] = f; peer[b] = 0; }
+#else
+    uint32_t *own = reinterpret_cast<uint32_t *>(L.accS);
     while (__ballot(pending)) {
         if (pending) atomicMax(&own[b], 64u - lane);
         const bool win = pending && own[b] == 64u - lane;
@@ -1656,6 +1695,7 @@ __device__ __forceinline__ void replay_group(ApplyLds &L, bool pending, uint32_t
             pending = false;
         }
     }
+#endif
 }
 
 // A tile's bucket state in registers (kTileMax / kApThreads buckets per thread):
@@ -1755,8 +1795,8 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
     // drained by the next chunk's load waits)
     uint32_t st_chunks = 0, st_rep = 0, st_crep = 0;
 #ifdef GNS_K4_PROF
-    uint64_t pmax_sum = 0;
-    if (tid == 0) L.s_pmax = 0;
+    uint64_t pmax_sum = 0, psum_sum = 0;
+    if (tid == 0) { L.s_pmax = 0; L.s_psum = 0; }
 #endif
     for (uint32_t cb = beg; cb < end; cb += kApChunk) {
         if (tid == 0) { s_any = 0; st_chunks++; }
@@ -1905,7 +1945,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             }
             K4_MARK(4);
 #ifdef GNS_K4_PROF
-            if (lane == 0) atomicMax(&L.s_pmax, nmine == 0xFFFFFFFFu ? 0u : nmine);
+            const uint64_t t_rep0 = __builtin_amdgcn_s_memtime();
 #endif
             if (nmine != 0xFFFFFFFFu) {
                 const uint16_t *wl = s_list + wave * kWl;
@@ -1951,10 +1991,16 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                 }
             }
             }
+#ifdef GNS_K4_PROF
+            {
+                const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memtime() - t_rep0);
+                if (lane == 0) { atomicMax(&L.s_pmax, dt); atomicAdd(&L.s_psum, dt); }
+            }
+#endif
         }
         __syncthreads();
 #ifdef GNS_K4_PROF
-        if (tid == 0) { pmax_sum += L.s_pmax; L.s_pmax = 0; }
+        if (tid == 0) { pmax_sum += L.s_pmax; psum_sum += L.s_psum; L.s_pmax = 0; L.s_psum = 0; }
 #endif
 #pragma unroll
         for (int j = 0; j < kApItems; j++) e[j] = en[j];
@@ -1968,7 +2014,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
         a.S[cbase + i] = cs.y; a.Fs[cbase + i] = f.y;
     }
 #ifdef GNS_K4_PROF
-    if (tid == 0) atomicAdd(&a.stats[14], (unsigned long long)pmax_sum);
+    if (tid == 0) { atomicAdd(&a.stats[14], (unsigned long long)pmax_sum); atomicAdd(&a.stats[4], (unsigned long long)psum_sum); }
 #endif
     if (tid == 0) {
         atomicAdd(&a.stats[5], (unsigned long long)st_rep);
@@ -4405,8 +4451,8 @@ int gns_cm_counters(gns_cm *cm, uint64_t out[8]) {
                     // tile store, sub-partition), chunks
     for (int i = 0; i < 7; i++) out[i] = h[8 + i];
     out[7] = h[15];  // replay groups
-    out[4] = h[5];   // replayed updates (replaces replay gather); out[6]: sum over chunks of the
-                     // largest per-wave replay list (balance: out[6] * waves / out[4])
+    out[4] = h[4];   // summed per-wave replay cycles (replaces replay gather); out[6]: the largest
+                     // wave's, summed over chunks (balance: out[6] * waves / out[4])
 #else
     for (int i = 0; i < 8; i++) out[i] = h[i];
 #endif

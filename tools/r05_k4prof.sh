@@ -2,8 +2,8 @@
 # K4 phase cycles (GNS_K4_PROF build, wave 0's s_memtime per phase summed over chunks) at the
 # headline and configs[4] geometries.  Build first: make -C go2netspectra_amd/csrc variant NAME=k4p
 # VARIANT_FLAGS=-DGNS_K4_PROF.  engine_counters then read: inserted=classify, dropped=decide,
-# unsupported=compact, dict_full=replay clear + loop top, ovf_full=replayed updates,
-# replayed=tile load + store, chunks=sum of the largest per-wave replay list, chunks_replay=replay groups.
+# unsupported=compact, dict_full=replay clear + loop top, ovf_full=summed per-wave replay cycles,
+# replayed=tile load + store, chunks=the slowest wave's replay cycles, chunks_replay=replay groups.
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/$1
 mkdir -p $O
@@ -17,5 +17,5 @@ c=d['engine_counters']
 ph=[('classify','inserted'),('decide','dropped'),('compact','unsupported'),('replay barrier + top','dict_full'),('tile load + store','replayed'),('replay groups','chunks_replay')]
 tot=sum(c[k] for _,k in ph)
 print('$w', d['stage_ms_per_step'].get('apply'), ' '.join(f'{n}={100*c[k]/tot:.1f}%' for n,k in ph),
-      'replay balance (largest wave list x 16 / all) =', round(c['chunks']*16/max(c['ovf_full'],1), 2))
+      'replay balance (slowest wave cycles x 16 / all) =', round(c['chunks']*16/max(c['ovf_full'],1), 2))
 "; done
