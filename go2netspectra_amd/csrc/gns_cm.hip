@@ -93,6 +93,7 @@ constexpr uint32_t kHotTab = kHot * GNS_HOT_TAB_MUL;  // lookup slots per row (l
 constexpr uint32_t kHotGroupBits = kHotBits + (GNS_HOT_TAB_MUL == 8 ? 1 : 0);  // 4-entry groups = kHotTab / 4
 constexpr uint32_t kHotMinBits = 11;                // designate only buckets with C >= 1024
 constexpr uint32_t kPendingId = 0xFFFFFFFEu;        // K1: flow not yet committed (equals no fingerprint)
+constexpr uint32_t kStatsProf = 16;                 // engine stats words 16..31: profiling builds only
 
 struct CmGeom {
     uint32_t w, d, wmask, pow2;
@@ -966,7 +967,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(4)))
         }
     }
 #ifdef GNS_K3_PROF
-    if (threadIdx.x == 0 && !a.hot_mode) for (int i = 0; i < 5; i++) atomicAdd(&a.stats[11 + i], (unsigned long long)k3t[i]);
+    if (threadIdx.x == 0 && !a.hot_mode) for (int i = 0; i < 5; i++) atomicAdd(&a.stats[kStatsProf + i], (unsigned long long)k3t[i]);
 #endif
 }
 
@@ -1168,7 +1169,7 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
         }
     }
 #ifdef GNS_K3_PROF
-    if (threadIdx.x == 0) for (int i = 0; i < 5; i++) atomicAdd(&a.stats[11 + i], (unsigned long long)k3t[i]);
+    if (threadIdx.x == 0) for (int i = 0; i < 5; i++) atomicAdd(&a.stats[kStatsProf + i], (unsigned long long)k3t[i]);
 #endif
 }
 
@@ -2014,7 +2015,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
         a.S[cbase + i] = cs.y; a.Fs[cbase + i] = f.y;
     }
 #ifdef GNS_K4_PROF
-    if (tid == 0) { atomicAdd(&a.stats[14], (unsigned long long)pmax_sum); atomicAdd(&a.stats[4], (unsigned long long)psum_sum); }
+    if (tid == 0) { atomicAdd(&a.stats[kStatsProf + 8], (unsigned long long)pmax_sum); atomicAdd(&a.stats[kStatsProf + 9], (unsigned long long)psum_sum); }
 #endif
     if (tid == 0) {
         atomicAdd(&a.stats[5], (unsigned long long)st_rep);
@@ -2024,8 +2025,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
 #ifdef GNS_K4_PROF
     __syncthreads();
     K4_MARK(5);
-    if (tid == 0) for (int i = 0; i < 6; i++) atomicAdd(&a.stats[8 + i], (unsigned long long)pt[i]);
-    if (tid == 0) atomicAdd(&a.stats[15], (unsigned long long)pt[6]);
+    if (tid == 0) for (int i = 0; i < 7; i++) atomicAdd(&a.stats[kStatsProf + i], (unsigned long long)pt[i]);
 #endif
 }
 
@@ -3846,7 +3846,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (g.sub_bits && (rc = dalloc_t(&cm->entries2, cm->bmax * g.d))) ||
             (g.sub_bits && (rc = dalloc_t(&cm->rseg, (cm->bmax * g.d / kApChunk + g.nbins + 2) * 16))) ||
             (rc = dalloc_t(&cm->ovf, kOvfCap)) || (rc = dalloc_t(&cm->ovf_cnt, 1)) ||
-            (rc = dalloc_t(&cm->stats, 16)) || (rc = dalloc_t(&cm->work, 4)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
+            (rc = dalloc_t(&cm->stats, kStatsProf + 16)) || (rc = dalloc_t(&cm->work, 4)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
             (rc = dalloc_t(&cm->segtot, (size_t)g.d * kHot * kHotSegs * 2)) || (rc = dalloc_t(&cm->hflag, g.d * kHot)) ||
             (rc = dalloc_t(&cm->hhist, g.d * kHotKeys)) || (rc = dalloc_t(&cm->hthr, 8)) || (rc = dalloc_t(&cm->hcnt, 8)) ||
             (rc = dalloc_t(&cm->hsum, (uint64_t)g.d * kHot * cm->nblk_max)) ||
@@ -3857,7 +3857,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
         if (hipHostMalloc(reinterpret_cast<void **>(&cm->h_pin), 64, 0) != hipSuccess) {
             set_error("hipHostMalloc failed"); rc = GNS_E_OOM; break;
         }
-        if (hipMemsetAsync(cm->stats, 0, 128, cm->stream) != hipSuccess) { rc = GNS_E_HIP; break; }
+        if (hipMemsetAsync(cm->stats, 0, (kStatsProf + 16) * 8, cm->stream) != hipSuccess) { rc = GNS_E_HIP; break; }
         if ((rc = cm_reset_state(cm)) != GNS_OK) break;
         {   // lane-order probe for K3's ranking (GNS_K3_RANK=0 forces the ballot multisplit)
             const char *env = getenv("GNS_K3_RANK");
@@ -4440,19 +4440,22 @@ int gns_cm_counters(gns_cm *cm, uint64_t out[8]) {
     if (!cm || !out) return GNS_E_ARG;
     GNS_TRY(set_dev(cm));
     GNS_HIP(hipStreamSynchronize(cm->stream));
-    unsigned long long h[16];
+    unsigned long long h[kStatsProf + 16];
     GNS_HIP(hipMemcpy(h, cm->stats, sizeof(h), hipMemcpyDeviceToHost));
 #ifdef GNS_K3_PROF  // profiling build: K3 phase cycles (loads, rank, scan, stage, write)
-    for (int i = 0; i < 5; i++) out[i] = h[11 + i];
+    for (int i = 0; i < 5; i++) out[i] = h[kStatsProf + i];
     for (int i = 5; i < 8; i++) out[i] = h[i];
     return GNS_OK;
 #endif
 #ifdef GNS_K4_PROF  // profiling build: K4 phase cycles (classify, decide, compact, replay, tile load,
                     // tile store, sub-partition), chunks
-    for (int i = 0; i < 7; i++) out[i] = h[8 + i];
-    out[7] = h[15];  // replay groups
-    out[4] = h[4];   // summed per-wave replay cycles (replaces replay gather); out[6]: the largest
-                     // wave's, summed over chunks (balance: out[6] * waves / out[4])
+    // phases (classify, decide, compact, replay barrier + loop top, replay gather, tile load +
+    // store, replay groups), then the slowest wave's and the summed per-wave replay cycles
+    for (int i = 0; i < 4; i++) out[i] = h[kStatsProf + i];
+    out[4] = h[kStatsProf + 9];
+    out[5] = h[kStatsProf + 5];
+    out[6] = h[kStatsProf + 8];
+    out[7] = h[kStatsProf + 6];
 #else
     for (int i = 0; i < 8; i++) out[i] = h[i];
 #endif
