@@ -4266,7 +4266,9 @@ int gns_cm_heavy_rows(gns_cm *cm, uint8_t *count_rows, uint64_t *n_count, uint8_
     return GNS_OK;
 }
 
-// per device, per host thread: the sort scratch of gns_hh_order_rows (grow-only)
+// per device, per host thread: the sort scratch of gns_hh_order_rows (grow-only; it lives as long
+// as the thread -- freeing device memory from a thread-exit destructor could run after the HIP
+// runtime's own teardown at process exit)
 static thread_local std::vector<CmScratch *> t_hh_scratch;
 
 int gns_hh_order_rows(const uint8_t *rows, uint32_t key_bytes, uint64_t n, uint8_t *out_rows, int device) {
