@@ -759,7 +759,7 @@ def main():
                     help="flow key: full 5-tuple (37 B, primary) or [SrcIP] (16 B, the default task layout)")
     ap.add_argument("--flows", type=int, default=1 << 20,
                     help="distinct flows of the synthetic stream (experiments; the headline uses 2^20)")
-    ap.add_argument("--host-input", nargs="?", const="headers", choices=["headers", "tuples", "compact"], default=None,
+    ap.add_argument("--host-input", nargs="?", const="headers", choices=["headers", "tuples", "compact", "compact16"], default=None,
                     help="time inserts from pinned host memory plus the per-window D2H of counters and heavy "
                          "hitters (PCIe-inclusive rate, for DESIGN.md): 64-B header records or 41-B PacketInfo "
                          "tuples (the live path's pre-parsed form)")
@@ -850,8 +850,11 @@ def main():
             tuples = PacketBatch(pin["src16"].numpy(), pin["dst16"].numpy(), pin["sport"].numpy().view(np.uint16),
                                  pin["dport"].numpy().view(np.uint16), pin["proto"].numpy(),
                                  pin["length"].numpy().view(np.uint32))
-        elif args.host_input == "compact":  # 16-B compact records + wire length = 20 B/packet (+ side records)
-            pin = {"rec": pinned(torch.empty((n, 16), dtype=torch.uint8)), "wl": pinned(wl),
+        elif args.host_input in ("compact", "compact16"):
+            # 16-B compact records + wire length = 20 B/packet; compact16: the wire length inside
+            # the record = 16 B/packet (+ side records either way)
+            pin = {"rec": pinned(torch.empty((n, 16), dtype=torch.uint8)),
+                   "wl": pinned(wl) if args.host_input == "compact" else None,
                    "side": pinned(torch.empty((max(1024, n // 256), 64), dtype=torch.uint8)), "ns": 0}
         else:
             pin = {"hdr": pinned(hdr), "wl": pinned(wl)}
@@ -879,9 +882,10 @@ def main():
             pin["length"].copy_(wl)
         elif "rec" in pin:
             from go2netspectra_amd import compact_headers
-            rec, side = compact_headers(hdr, wl)
+            rec, side = compact_headers(hdr, wl, rec_len=pin["wl"] is None)
             pin["rec"].copy_(rec)
-            pin["wl"].copy_(wl)
+            if pin["wl"] is not None:
+                pin["wl"].copy_(wl)
             pin["ns"] = int(side.shape[0])
             pin["side"][: pin["ns"]].copy_(side)
         else:
@@ -896,7 +900,7 @@ def main():
         elif tuples is not None:
             cm.insert_tuples(tuples)
         elif pin is not None and "rec" in pin:
-            cm.insert_compact(pin["rec"].numpy(), pin["wl"].numpy().view(np.uint32),
+            cm.insert_compact(pin["rec"].numpy(), pin["wl"].numpy().view(np.uint32) if pin["wl"] is not None else None,
                               pin["side"][: pin["ns"]].numpy() if pin["ns"] else None)
         elif pin is not None:
             cm.insert_headers(pin["hdr"].numpy(), pin["wl"].numpy().view(np.uint32))

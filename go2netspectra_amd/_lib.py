@@ -40,6 +40,7 @@ EXPORTED = [
     "gns_route_create", "gns_route_destroy", "gns_route_partition",
     "gns_cm_dict_stats", "gns_ss_dict_stats", "gns_ex_dict_stats", "gns_cm_reclaim", "gns_ss_reclaim",
     "gns_cm_insert_compact", "gns_pack_pcap_compact", "gns_compact_headers", "gns_route_partition_async",
+    "gns_pack_pcap_compact16", "gns_compact_headers16",
     "gns_route_owner_fields", "gns_route_create_keyed", "gns_route_owner_layout", "gns_route_owner_keys",
     "gns_device_alloc", "gns_device_free", "gns_cm_heavy_rows", "gns_hh_order_rows",
 ]
@@ -166,6 +167,8 @@ def load() -> ct.CDLL:
         "gns_cm_insert_compact": ([vp, vp, vp, u64, vp, u64, i32], i32),
         "gns_pack_pcap_compact": ([ct.c_char_p, vp, vp, u64, vp, u64, vp, vp], ct.c_int64),
         "gns_compact_headers": ([vp, vp, u64, vp, vp, u64, vp, i32], i32),
+        "gns_pack_pcap_compact16": ([ct.c_char_p, vp, u64, vp, u64, vp, vp], ct.c_int64),
+        "gns_compact_headers16": ([vp, vp, u64, vp, vp, u64, vp, i32], i32),
         "gns_route_partition_async": ([vp, vp, vp, u64, vp, vp, vp, vp], i32),
         "gns_route_owner_fields": ([vp, u32, vp], i32),
         "gns_route_create_keyed": ([u32, vp, i32, vp], i32),

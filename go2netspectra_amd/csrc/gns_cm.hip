@@ -3183,6 +3183,7 @@ struct gns_cm {
     uint64_t *entries = nullptr, *entries2 = nullptr;
     uint16_t *rseg = nullptr;          // [round][16] k_subpart round tile starts (sub_bits > 0)
     int subpart_nt = 0;                // GNS_SUBPART_NT (A/B)
+    uint32_t *rec_sizes = nullptr;     // 16-byte compact records from device memory: a batch's sizes
     uint64_t *ovf = nullptr;
     uint32_t *ovf_cnt = nullptr;
     uint64_t ovf_cap = 0;                 // entries of ovf
@@ -3273,7 +3274,7 @@ int cm_free_all(gns_cm *cm) {
     dfree(cm->keyid); dfree(cm->idx); dfree(cm->scnt);  // hstr lives in idx
     dfree(cm->pend[0]); dfree(cm->pend[1]); dfree(cm->pcnt[0]); dfree(cm->pcnt[1]);
     dfree(cm->ptotal); dfree(cm->hist); dfree(cm->part); dfree(cm->total); dfree(cm->order);
-    dfree(cm->entries); dfree(cm->entries2); dfree(cm->rseg); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats);
+    dfree(cm->entries); dfree(cm->entries2); dfree(cm->rseg); dfree(cm->rec_sizes); dfree(cm->ovf); dfree(cm->ovf_cnt); dfree(cm->stats);
     dfree(cm->stage[0]); dfree(cm->stage[1]); dfree(cm->side_dev);
     for (int i = 0; i < 2; i++) {
         if (cm->ev_copied[i]) (void)hipEventDestroy(cm->ev_copied[i]);
@@ -3652,6 +3653,12 @@ int cm_batch_recover(gns_cm *cm, const InputDesc &d, uint64_t m, bool fresh) {
     return cm_batch_recover<KIND>(cm, advance(d, h), m - h, false);
 }
 
+// 16-byte compact records: the wire lengths (word 3 bits 16..31) as the batch's size array
+__global__ __launch_bounds__(256) void k_rec_sizes(const uint32_t *rec16, uint64_t n, uint32_t *sizes) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) sizes[i] = rec16[i * 4 + 3] >> 16;
+}
+
 // Host input: stage batch [off, off+m) into device buffer b on the copy stream,
 // after the batch that last read b has finished; d points into the buffer.
 int stage_host_batch(gns_cm *cm, int b, const InputDesc &in, uint64_t off, uint64_t m, InputDesc &d) {
@@ -3682,7 +3689,13 @@ int stage_host_batch(gns_cm *cm, int b, const InputDesc &in, uint64_t off, uint6
         *dst[i] = p;
         p += (bytes[i] + 15) & ~size_t(15);
     }
-    GNS_HIP(hipMemcpyAsync(p, in.sizes + off, m * 4, hipMemcpyHostToDevice, cm->cstream));
+    if (in.rec_len) {  // sizes from the staged records
+        hipLaunchKernelGGL(k_rec_sizes, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, cm->cstream, d.rec16, m,
+                           reinterpret_cast<uint32_t *>(p));
+        GNS_HIP(hipGetLastError());
+    } else {
+        GNS_HIP(hipMemcpyAsync(p, in.sizes + off, m * 4, hipMemcpyHostToDevice, cm->cstream));
+    }
     d.sizes = reinterpret_cast<const uint32_t *>(p);
     if (d.keys) d.aligned = (d.stride % 4 == 0 && d.stride >= ((cm->K + 3) & ~3u)) ? 1u : 0u;
     GNS_HIP(hipEventRecord(cm->ev_copied[b], cm->cstream));
@@ -3700,7 +3713,15 @@ int cm_insert(gns_cm *cm, InputDesc in, uint64_t n, gns_mem where) {
     if (where == GNS_MEM_DEVICE) {
         for (uint64_t off = 0, m = 0; off < n; off += m) {
             m = batch_len(off, cm->warm);
-            GNS_TRY(cm_batch_recover<KIND>(cm, advance(in, off), m, false));
+            InputDesc d = advance(in, off);
+            if (in.rec_len) {  // 16-byte compact records: the batch's sizes unpacked on the stream
+                if (!cm->rec_sizes) GNS_TRY(dalloc_t(&cm->rec_sizes, cm->bmax));
+                hipLaunchKernelGGL(k_rec_sizes, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, cm->stream, d.rec16, m,
+                                   cm->rec_sizes);
+                GNS_HIP(hipGetLastError());
+                d.sizes = cm->rec_sizes;
+            }
+            GNS_TRY(cm_batch_recover<KIND>(cm, d, m, false));
         }
         return GNS_OK;
     }
@@ -3946,10 +3967,11 @@ int gns_cm_insert_headers(gns_cm *cm, const uint8_t *hdr, const uint32_t *wirele
 
 int gns_cm_insert_compact(gns_cm *cm, const uint8_t *rec16, const uint32_t *wirelen, uint64_t n,
                           const uint8_t *side64, uint64_t n_side, gns_mem where) {
-    if (!cm || (n && (!rec16 || !wirelen)) || (n_side && !side64)) { set_error("null argument"); return GNS_E_ARG; }
+    if (!cm || (n && !rec16) || (n_side && !side64)) { set_error("null argument"); return GNS_E_ARG; }
     InputDesc in{};
     in.rec16 = reinterpret_cast<const uint32_t *>(rec16);
     in.sizes = wirelen;
+    in.rec_len = wirelen ? 0u : 1u;  // no wirelen array: the 16-byte form
     in.side = reinterpret_cast<const uint32_t *>(side64);
     in.n_side = side64 ? n_side : 0;
     if (where == GNS_MEM_HOST && n_side) {

@@ -129,6 +129,9 @@ int frame_record(const uint8_t *frame, uint32_t caplen, uint32_t wirelen, uint8_
 // frame_record's record (and its return code) -> compact 16-byte record; returns
 // the class (kRecSide: the caller stores the side index in word 0)
 int compact_record(int code, const uint8_t *rec, uint8_t *out16);
+// the 16-byte form: the wire length in word 3 bits 16..31 (-1: above 65535); a tuple
+// record is IPv4 both ways, any other tuple escapes to the side array
+int compact_record16(int code, const uint8_t *rec, uint32_t orig, uint8_t *out16);
 
 inline uint32_t ceil_log2(uint64_t x) {
     uint32_t b = 0;

@@ -554,4 +554,17 @@ int compact_record(int code, const uint8_t *rec, uint8_t *out16) {
     out16[14] = rec[53] ? rec[53] : rec[15];
     return gns::kRecTuple;
 }
+
+int compact_record16(int code, const uint8_t *rec, uint32_t orig, uint8_t *out16) {
+    if (orig > 0xFFFFu) return -1;
+    int cls = compact_record(code, rec, out16);
+    if (cls == gns::kRecTuple && (out16[14] != 4 || out16[15] != 4)) {  // only IPv4 tuples stay compact
+        memset(out16, 0, 16);
+        out16[13] = gns::kRecSide;
+        cls = gns::kRecSide;
+    }
+    out16[14] = (uint8_t)(orig & 0xFFu);  // word 3 bits 16..31: the wire length
+    out16[15] = (uint8_t)(orig >> 8);
+    return cls;
+}
 }  // namespace gns

@@ -26,6 +26,9 @@ enum InputKind { IN_HDR = 0, IN_TUPLE = 1, IN_KEYS = 2, IN_REC16 = 3 };
 //   kRecDrop   no IP layer (parser.go:48-49: not counted);
 //   kRecSide   anything else (IPv6, unsupported shapes): word 0 indexes a
 //              64-byte record in the side array, parsed as gns_*_insert_headers would.
+// The 16-byte form (InputDesc.rec_len) carries the wire length in bits 16..31 of
+// word 3 instead of the IP versions, which a tuple record then implies (IPv4 both
+// ways; any other tuple escapes to the side array): 16 B per packet over the bus.
 enum { kRecTuple = 0, kRecDrop = 1, kRecSide = 2 };
 
 struct InputDesc {
@@ -41,6 +44,7 @@ struct InputDesc {
     const uint32_t *rec16;    // IN_REC16: n*4 words
     const uint32_t *side;     // IN_REC16: 64-byte records named by kRecSide escapes
     uint64_t n_side;          // IN_REC16: records in side (an escape at or past it is unsupported)
+    uint32_t rec_len;         // IN_REC16: wire lengths in the records (sizes then unpacked from them)
     uint32_t stride, stride2;
     uint32_t aligned;         // bit0: keys word-loadable, bit1: keys2 word-loadable
 };
@@ -135,7 +139,7 @@ __device__ __forceinline__ int load_tuple(const InputDesc &in, uint64_t p, uint3
         const uint32_t cls = (r.w >> 8) & 0xFFu;
         tw[0] = r.x; tw[1] = 0; tw[2] = 0; tw[3] = 0;
         tw[4] = r.y; tw[5] = 0; tw[6] = 0; tw[7] = 0;
-        tw[8] = r.z; tw[9] = r.w;
+        tw[8] = r.z; tw[9] = in.rec_len ? ((r.w & 0xFFu) | 0x04040000u) : r.w;
         if (cls == kRecTuple) return PARSE_OK;
         if (cls == kRecDrop) return PARSE_DROP;
         int st = PARSE_UNSUPPORTED;

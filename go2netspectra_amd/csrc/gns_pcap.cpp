@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -66,10 +67,12 @@ struct Sink {  // record output (the first `cap` packets) and counters
     // records that do not fit into side64 (side_cap of them; side_need counts all)
     uint8_t *rec16 = nullptr, *side64 = nullptr;
     uint64_t side_cap = 0, side_need = 0;
+    bool rec_len = false;                // the 16-byte form (wire lengths inside the records)
+    std::atomic<uint64_t> too_long{0};   // its frames with a wire length above 65535
     std::vector<Desc> slab;
     int nthreads = 1;
     static constexpr size_t kSlab = 1u << 17;
-    bool out_ok() const { return (hdr || rec16) && wirelen; }
+    bool out_ok() const { return (hdr || rec16) && (wirelen || rec_len); }
     void emit(const uint8_t *data, uint32_t incl, uint32_t orig, int64_t ts) {
         n++;
         if (written + slab.size() >= cap || !out_ok()) return;
@@ -92,11 +95,18 @@ struct Sink {  // record output (the first `cap` packets) and counters
                 uint8_t *r = rec16 ? tmp : hdr + j * 64;
                 const int code = gns::frame_record(dsc.frame, dsc.incl, dsc.orig, r);
                 part[t][code]++;
-                if (rec16 && gns::compact_record(code, r, rec16 + j * 16) == gns::kRecSide) {
+                int cls = -2;
+                if (rec16 && rec_len) {
+                    cls = gns::compact_record16(code, r, dsc.orig, rec16 + j * 16);
+                    if (cls < 0) too_long++;
+                } else if (rec16) {
+                    cls = gns::compact_record(code, r, rec16 + j * 16);
+                }
+                if (cls == gns::kRecSide) {
                     side[t].insert(side[t].end(), r, r + 64);
                     at[t].push_back(j);
                 }
-                wirelen[j] = dsc.orig;
+                if (wirelen) wirelen[j] = dsc.orig;
                 if (ts_ns) ts_ns[j] = dsc.ts;
             }
         };
@@ -371,6 +381,30 @@ extern "C" int64_t gns_pack_pcap_compact(const char *path, uint8_t *rec16, uint3
     o.side_cap = side_cap;
     const int64_t r = pack(path, o, total);
     if (n_side) *n_side = o.side_need;
+    if (r >= 0 && o.side_need > side_cap) {
+        gns::set_error("%s: %llu side records needed, room for %llu", path, (unsigned long long)o.side_need,
+                       (unsigned long long)side_cap);
+        return GNS_E_RANGE;
+    }
+    return r;
+}
+
+// the 16-byte form (gns_cm_insert_compact with no wirelen array): the wire length rides in
+// each record; GNS_E_RANGE when a frame's wire length exceeds 65535
+extern "C" int64_t gns_pack_pcap_compact16(const char *path, uint8_t *rec16, uint64_t cap, uint8_t *side64,
+                                           uint64_t side_cap, uint64_t *n_side, uint64_t *total) {
+    Sink o{nullptr, nullptr, nullptr, cap};
+    o.rec16 = rec16;
+    o.rec_len = true;
+    o.side64 = side64;
+    o.side_cap = side_cap;
+    const int64_t r = pack(path, o, total);
+    if (n_side) *n_side = o.side_need;
+    if (r >= 0 && o.too_long.load()) {
+        gns::set_error("%s: %llu frames with a wire length above 65535 (use the 20-byte form)", path,
+                       (unsigned long long)o.too_long.load());
+        return GNS_E_RANGE;
+    }
     if (r >= 0 && o.side_need > side_cap) {
         gns::set_error("%s: %llu side records needed, room for %llu", path, (unsigned long long)o.side_need,
                        (unsigned long long)side_cap);

@@ -149,32 +149,38 @@ def read_pcap(path: str, limit: Optional[int] = None) -> HeaderBatch:
         cap = total.value
 
 
-def read_pcap_compact(path: str, limit: Optional[int] = None):
+def read_pcap_compact(path: str, limit: Optional[int] = None, rec_len: bool = False):
     """pcap or pcapng -> compact records (rec16 [n, 16], wirelen [n], side [n_side, 64]);
-    see include/gns_sketch.h gns_cm_insert_compact."""
+    see include/gns_sketch.h gns_cm_insert_compact.  rec_len: the 16-byte form, the wire
+    lengths inside the records (wirelen is then None; GNS_E_RANGE above 65535)."""
     L = _lib.load()
     total, nside = ct.c_uint64(0), ct.c_uint64(0)
     cap = limit if limit is not None else max(1, (os.path.getsize(path) - 24) // 76 + 1)
     side_cap = max(1024, cap // 64)
     while True:
         rec = np.empty((cap, 16), np.uint8)
-        wl = np.empty(cap, np.uint32)
+        wl = None if rec_len else np.empty(cap, np.uint32)
         side = np.empty((side_cap, 64), np.uint8)
-        r = L.gns_pack_pcap_compact(os.fsencode(path), rec.ctypes.data, wl.ctypes.data, cap, side.ctypes.data,
-                                    side_cap, ct.byref(nside), ct.byref(total))
+        if rec_len:
+            r = L.gns_pack_pcap_compact16(os.fsencode(path), rec.ctypes.data, cap, side.ctypes.data, side_cap,
+                                          ct.byref(nside), ct.byref(total))
+        else:
+            r = L.gns_pack_pcap_compact(os.fsencode(path), rec.ctypes.data, wl.ctypes.data, cap, side.ctypes.data,
+                                        side_cap, ct.byref(nside), ct.byref(total))
         if r == _lib.GNS_E_RANGE and nside.value > side_cap:
             side_cap = nside.value
             continue
         if r < 0:
             check(int(r))
         if limit is not None or total.value <= cap:
-            return rec[:r], wl[:r], side[:nside.value]
+            return rec[:r], (None if wl is None else wl[:r]), side[:nside.value]
         cap = total.value
 
 
-def compact_headers(hdr, wirelen):
+def compact_headers(hdr, wirelen, rec_len: bool = False):
     """Device-resident 64-byte records (torch uint8 [n, 64] + wire lengths) -> compact
-    records on the same device: (rec16 [n, 16] uint8, side [n_side, 64] uint8)."""
+    records on the same device: (rec16 [n, 16] uint8, side [n_side, 64] uint8).
+    rec_len: the 16-byte form (wire lengths inside the records)."""
     import torch
     L = _lib.load()
     n = int(wirelen.shape[0])
@@ -184,9 +190,10 @@ def compact_headers(hdr, wirelen):
     while True:
         side = torch.empty((cap, 64), dtype=torch.uint8, device=hdr.device)
         ns = ct.c_uint64(0)
-        r = L.gns_compact_headers(hdr.data_ptr(), wirelen.data_ptr(), n, rec.data_ptr(), side.data_ptr(), cap,
-                                  ct.byref(ns), hdr.device.index or 0)
-        if r == _lib.GNS_E_RANGE:
+        fn = L.gns_compact_headers16 if rec_len else L.gns_compact_headers
+        r = fn(hdr.data_ptr(), wirelen.data_ptr(), n, rec.data_ptr(), side.data_ptr(), cap, ct.byref(ns),
+               hdr.device.index or 0)
+        if r == _lib.GNS_E_RANGE and ns.value > cap:
             cap = ns.value
             continue
         check(r)

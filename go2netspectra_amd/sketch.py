@@ -233,15 +233,19 @@ class CountMin:
     def insert_compact(self, rec16, wirelen, side=None) -> None:
         """Compact 16-byte records [n, 16] + wire lengths [n] (+ the 64-byte side
         records their escapes name, [n_side, 64]): the same stream as the 64-byte
-        records they were made from (packets.compact_headers / read_pcap_compact)."""
-        where = _where(rec16, wirelen, side)
+        records they were made from (packets.compact_headers / read_pcap_compact).
+        wirelen None: the 16-byte form, whose records carry the wire lengths
+        (packets.compact_headers(..., rec_len=True) / read_pcap_compact(..., rec_len=True))."""
+        where = _where(*[a for a in (rec16, wirelen, side) if a is not None])
         if where == _lib.MEM_HOST:
             rec16 = _host(rec16, np.uint8)
-            wirelen = _host(wirelen, np.uint32)
+            wirelen = _host(wirelen, np.uint32) if wirelen is not None else None
             side = _host(side, np.uint8) if side is not None else None
-        n = int(wirelen.shape[0])
+        n = int(rec16.shape[0])
+        if wirelen is not None and int(wirelen.shape[0]) != n:
+            raise ValueError("rec16 and wirelen lengths differ")
         ns = int(side.shape[0]) if side is not None else 0
-        check(self._L.gns_cm_insert_compact(self._h, _ptr(rec16), _ptr(wirelen), n,
+        check(self._L.gns_cm_insert_compact(self._h, _ptr(rec16), _ptr(wirelen) if wirelen is not None else None, n,
                                             _ptr(side) if ns else None, ns, where))
 
     def flush(self) -> None:

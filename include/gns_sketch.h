@@ -148,7 +148,11 @@ int gns_cm_insert_headers(gns_cm *cm, const uint8_t *hdr, const uint32_t *wirele
  *   2 = escape: word 0 indexes side64[n_side*64], a 64-byte record parsed as
  *   gns_cm_insert_headers parses it (IPv6 tuples, unsupported shapes).
  * The insert equals gns_cm_insert_headers of the records the compact form was
- * made from.  Producers: gns_pack_pcap_compact (host), gns_compact_headers (device). */
+ * made from.  Producers: gns_pack_pcap_compact (host), gns_compact_headers (device).
+ * wirelen == NULL: the 16-byte form (16 B/packet over the bus): word 3 bits 16..31
+ * hold the wire length instead of the IP versions, a class-0 record is an IPv4
+ * tuple both ways (any other tuple escapes to side64), so no wire lengths above
+ * 65535; producers gns_pack_pcap_compact16, gns_compact_headers16. */
 int gns_cm_insert_compact(gns_cm *cm, const uint8_t *rec16, const uint32_t *wirelen, uint64_t n,
                           const uint8_t *side64, uint64_t n_side, gns_mem where);
 int gns_cm_flush(gns_cm *cm);
@@ -310,6 +314,12 @@ int64_t gns_pack_pcap_compact(const char *path, uint8_t *rec16, uint32_t *wirele
  * `device`; inputs complete before the call); *n_side as above */
 int gns_compact_headers(const uint8_t *hdr, const uint32_t *wirelen, uint64_t n, uint8_t *rec16,
                         uint8_t *side64, uint64_t side_cap, uint64_t *n_side, int device);
+/* the 16-byte forms (gns_cm_insert_compact with wirelen == NULL): GNS_E_RANGE when a
+ * wire length exceeds 65535 */
+int64_t gns_pack_pcap_compact16(const char *path, uint8_t *rec16, uint64_t cap, uint8_t *side64,
+                                uint64_t side_cap, uint64_t *n_side, uint64_t *total);
+int gns_compact_headers16(const uint8_t *hdr, const uint32_t *wirelen, uint64_t n, uint8_t *rec16,
+                          uint8_t *side64, uint64_t side_cap, uint64_t *n_side, int device);
 
 /* [0] frames copied verbatim, [1] frames decoded on the host into 0x88B5
  * records, [2] frames without an IP layer, of the calling thread's last

@@ -236,6 +236,29 @@ def test_encapsulated_capture_decoded_on_host(gpu, oracle, tmp_path):
     cm3.flush()
     assert cm3.stats() == st
     _same_state(cm3, orc)
+    # the 16-byte form (wire lengths inside the records): host packer through staged host
+    # batches, device producer through device batches; IPv6 tuples escape to the side array
+    rec16, none16, side16 = read_pcap_compact(path, rec_len=True)
+    assert none16 is None and len(side16) >= len(side)
+    assert np.array_equal(np.ascontiguousarray(rec16[:, 12:16]).view("<u4").reshape(-1) >> 16, hb.wirelen)
+    cm5 = CountMin(65536, 4, 20000, 50, flow_fields=FIVE, seeds=seeds, max_flows=1 << 20, batch_packets=70_000)
+    cm5.insert_compact(rec16, None, side16)
+    cm5.flush()
+    assert cm5.stats() == st
+    _same_state(cm5, orc)
+    drec16, dside16 = compact_headers(dh, dw, rec_len=True)
+    dr, ds = drec16.cpu().numpy(), dside16.cpu().numpy()
+    esc = rec16[:, 13] == 2  # the device numbers its escapes in wave order, the packer in file order
+    assert np.array_equal(dr[:, 13], rec16[:, 13]) and np.array_equal(dr[~esc], rec16[~esc])
+    assert np.array_equal(dr[esc, 4:], rec16[esc, 4:]) and len(ds) == len(side16)
+    hi = np.ascontiguousarray(rec16[esc, :4]).view("<u4").reshape(-1)
+    di = np.ascontiguousarray(dr[esc, :4]).view("<u4").reshape(-1)
+    assert np.array_equal(ds[di], side16[hi])
+    cm6 = CountMin(65536, 4, 20000, 50, flow_fields=FIVE, seeds=seeds, max_flows=1 << 20, batch_packets=70_000)
+    cm6.insert_compact(drec16, None, dside16)
+    cm6.flush()
+    assert cm6.stats() == st
+    _same_state(cm6, orc)
     # a short or missing side array (advisor r4): escapes past it are counted as
     # unsupported and never read; everything else is applied as before
     cls = rec[:, 13]

@@ -303,3 +303,40 @@ def test_compact_packer_equals_the_parsed_records(tmp_path):
             k = int(rec[j, 0:4].view("<u4")[0])
             assert bytes(side[k]) == bytes(hb.hdr[j])
     assert seen[0] > 0 and seen[1] > 0 and seen[2] > 0, seen
+
+
+def test_compact16_packer_carries_wire_lengths(tmp_path):
+    """gns_pack_pcap_compact16: the 20-byte form's records with the wire length in word 3
+    bits 16..31; a class-0 record is an IPv4 tuple both ways (the 20-byte form's other
+    narrow tuples, e.g. host-decoded IPv6 with zero upper slot bytes, escape to the side
+    array here), every escape names its exact 64-byte record, and a frame whose wire
+    length exceeds 65535 makes the call fail (the 20-byte form then holds it)."""
+    from test_configs_gpu import _encap_flows
+    rng = np.random.default_rng(6)
+    flows = _encap_flows(rng, 600)
+    frames, wl = _random_frames(rng, 300)
+    frames += [f for f, _ in flows]
+    wl += [w for _, w in flows]
+    path = str(tmp_path / "c16.pcap")
+    g.write_pcap(path, frames, wl)
+    hb = g.read_pcap(path)
+    rec, cwl, side = g.read_pcap_compact(path)
+    rec16, none16, side16 = g.read_pcap_compact(path, rec_len=True)
+    assert none16 is None and len(rec16) == len(rec)
+    w3 = np.ascontiguousarray(rec16[:, 12:16]).view("<u4").reshape(-1)
+    assert np.array_equal(w3 >> 16, cwl)
+    for j in range(len(rec)):
+        c20, c16 = int(rec[j, 13]), int(rec16[j, 13])
+        v4 = c20 == 0 and rec[j, 14] == 4 and rec[j, 15] == 4
+        if v4 or c20 == 1:
+            assert c16 == c20 and bytes(rec16[j, :13]) == bytes(rec[j, :13]), j
+        else:
+            assert c16 == 2, j
+            k = int(rec16[j, 0:4].view("<u4")[0])
+            assert bytes(side16[k]) == bytes(hb.hdr[j])
+    big = str(tmp_path / "big.pcap")
+    g.write_pcap(big, frames[:10], [70_000] + wl[1:10], snaplen=262144)
+    with pytest.raises(g.GnsError):
+        g.read_pcap_compact(big, rec_len=True)
+    r2, w2, _ = g.read_pcap_compact(big)
+    assert w2[0] == 70_000

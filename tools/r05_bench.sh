@@ -30,6 +30,7 @@ for leg in "$@"; do
         exact) run exact 300 --sketch exact --no-cpu ;;
         hybrid) run hybrid 500 --sketch hybrid --no-cpu ;;
         host_compact) run host_compact 300 --host-input compact --no-cpu ;;
+        host_compact16) run host_compact16 300 --host-input compact16 --no-cpu ;;
         prof_cm) prof cm 400 --no-cpu --steps 10 --warmup 5 --windows 0 ;;
         prof_ss) prof ss 400 --sketch superspread --no-cpu --steps 10 --warmup 5 ;;
         prof_c5) prof c5 500 --width 16777216 --depth 8 --no-cpu --steps 10 --warmup 5 --windows 0 ;;
