@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "gns_common.hpp"
+#include "gns_ctl.cuh"
 #include "gns_scan.cuh"
 
 namespace gns {
@@ -3354,10 +3355,14 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
     const CmGeom &g = cm->g;
     ScopedStage total_stage(cm->timer, 5);
     // K1
-    GNS_HIP(hipMemsetAsync(cm->ptotal, 0, 8, s));
-    GNS_HIP(hipMemsetAsync(cm->dctl + 1, 0, 4, s));  // abort flag of this batch
-    GNS_HIP(hipMemsetAsync(cm->hflag2, 0, ((size_t)g.d * kHot + 2) * 4, s));
-    GNS_HIP(hipMemsetAsync(cm->stats + 8, 0, 8, s));  // oversize packets of this batch (K1)
+    {  // one launch: resolve totals, this batch's abort flag, hot flags, oversize packets (K1)
+        CtlZero z;
+        z.add(cm->ptotal, 8);
+        z.add(cm->dctl + 1, 4);
+        z.add(cm->hflag2, ((size_t)g.d * kHot + 2) * 4);
+        z.add(cm->stats + 8, 8);
+        GNS_HIP(ctl_zero(z, s));
+    }
     if (++cm->epoch == 0) cm->epoch = 1;
     {
         ExtractArgs a{};
@@ -3412,10 +3417,12 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
     int cur = 0;
     for (int round = 0;; round++) {
         if (round > 0) {
-            GNS_HIP(hipMemcpyAsync(cm->h_pin, cm->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
-            GNS_HIP(hipMemcpyAsync(cm->h_pin + 2, cm->stats + 3, 8, hipMemcpyDeviceToHost, s));
-            GNS_HIP(hipMemcpyAsync(cm->h_pin + 4, cm->dctl, 4, hipMemcpyDeviceToHost, s));
-            if (round == 1) GNS_HIP(hipMemcpyAsync(cm->h_pin + 6, cm->stats + 8, 8, hipMemcpyDeviceToHost, s));
+            CtlRead rd;  // one launch writes the words into the pinned mirror
+            rd.add(cm->ptotal + cur, 4, 0);
+            rd.add(cm->stats + 3, 8, 2);
+            rd.add(cm->dctl, 4, 4);
+            if (round == 1) rd.add(cm->stats + 8, 8, 6);
+            GNS_HIP(ctl_read(rd, cm->h_pin, s));
             GNS_HIP(hipStreamSynchronize(s));
             cm->claimed = cm->h_pin[4];
             if (round == 1) {  // the overflow side table holds every oversize row-update of the batch

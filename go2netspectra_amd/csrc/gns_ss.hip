@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "gns_common.hpp"
+#include "gns_ctl.cuh"
 #include "gns_gomath.cuh"
 #include "gns_scan.cuh"
 
@@ -1429,13 +1430,15 @@ int ss_encode_ids(gns_ss *ss, const InputDesc &in) {
         // second round behind the first without a host round trip (an empty
         // parked list makes it a no-op; ptotal[1] was zeroed above)
         if (round == 0) continue;
-        GNS_HIP(hipMemcpyAsync(ss->h_pin, ss->ptotal + cur, 4, hipMemcpyDeviceToHost, s));
-        GNS_HIP(hipMemcpyAsync(ss->h_pin + 2, ss->stats + 3, 8, hipMemcpyDeviceToHost, s));
-        GNS_HIP(hipMemcpyAsync(ss->h_pin + 4, ss->dctl, 4, hipMemcpyDeviceToHost, s));
+        CtlRead rd;  // one launch writes the words into the pinned mirror
+        rd.add(ss->ptotal + cur, 4, 0);
+        rd.add(ss->stats + 3, 8, 2);
+        rd.add(ss->dctl, 4, 4);
         if (round == 1) {
-            GNS_HIP(hipMemcpyAsync(ss->h_pin + 5, ss->counts + 1, 4, hipMemcpyDeviceToHost, s));
-            GNS_HIP(hipMemcpyAsync(ss->h_pin + 6, ss->stats + 6, 8, hipMemcpyDeviceToHost, s));
+            rd.add(ss->counts + 1, 4, 5);
+            rd.add(ss->stats + 6, 8, 6);
         }
+        GNS_HIP(ctl_read(rd, ss->h_pin, s));
         GNS_HIP(hipStreamSynchronize(s));
         if (round == 1 && (ss->h_pin[6] | ss->h_pin[7])) {  // P4: a cell's encodes exceed kSpCap
             GNS_HIP(hipMemsetAsync(ss->stats + 6, 0, 8, s));
@@ -1463,10 +1466,15 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
     const uint32_t cells = ss->g.d * ss->g.w;
     const SpGeom &sg = ss->sp;
     ScopedStage total_stage(ss->timer, 5);
-    GNS_HIP(hipMemsetAsync(ss->ptotal, 0, 8, s));
-    GNS_HIP(hipMemsetAsync(ss->counts, 0, 16, s));     // [1] encodes, [2] P4 bin counter, [3] candidates (P2)
-    GNS_HIP(hipMemsetAsync(ss->heads + cells, 0, 4, s));
-    GNS_HIP(hipMemsetAsync(ss->dctl + 1, 0, 4, s));  // abort flag of this batch
+    {  // one launch: resolve totals, [1] encodes, [2] P4 bin counter, [3] candidates (P2), the
+       // heads' end word, this batch's abort flag
+        CtlZero z;
+        z.add(ss->ptotal, 8);
+        z.add(ss->counts, 16);
+        z.add(ss->heads + cells, 4);
+        z.add(ss->dctl + 1, 4);
+        GNS_HIP(ctl_zero(z, s));
+    }
     if (++ss->epoch == 0) ss->epoch = 1;
     SsExtractArgs x{};
     x.in = in; x.n = n; x.kpf = ss->kpf; x.kpm = ss->kpm;
