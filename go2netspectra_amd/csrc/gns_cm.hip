@@ -2732,13 +2732,24 @@ __global__ __launch_bounds__(256) void k_hot_hist(const uint32_t *C, CmGeom g, u
         const uint32_t *Cr = C + (uint64_t)r * g.w;
         uint32_t *sr = s + r * kHotKeys;
         if ((g.w & 3u) == 0) {
+            // four 16-byte loads in flight per thread before their counts (the class adds
+            // between single loads left the pass latency-bound with few blocks)
             const uint4 *C4 = reinterpret_cast<const uint4 *>(Cr);
-            for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < g.w / 4; c += stride) {
-                const uint4 v = C4[c];
-                if (v.x >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v.x)], 1u);
-                if (v.y >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v.y)], 1u);
-                if (v.z >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v.z)], 1u);
-                if (v.w >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v.w)], 1u);
+            const uint64_t n4 = g.w / 4;
+            for (uint64_t c0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; c0 < n4; c0 += 4 * stride) {
+                uint4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint64_t c = c0 + (uint64_t)u * stride;
+                    v[u] = c < n4 ? C4[c] : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (v[u].x >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v[u].x)], 1u);
+                    if (v[u].y >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v[u].y)], 1u);
+                    if (v[u].z >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v[u].z)], 1u);
+                    if (v[u].w >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v[u].w)], 1u);
+                }
             }
         } else {
             for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < g.w; c += stride) {
