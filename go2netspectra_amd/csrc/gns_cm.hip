@@ -1499,10 +1499,12 @@ struct ApplyArgs {
     uint32_t *work;             // persistent-schedule counter (zeroed before the launch)
 };
 
-// accN per bucket and chunk: n [0,14) | n_foreign_count [14,28) | n_foreign_size
-// [28,42) | force (size escape) bit 42
-constexpr uint64_t kM14 = (1ull << 14) - 1;
-constexpr uint32_t kAccForce = 42;
+// accN per bucket and chunk (32 bits): n [0,14) | n_foreign_count [14,28) | force (size
+// escape) bit 28.  The size half needs no foreign-update count: a foreign update only
+// replaces when S == 0 or its size exceeds S, so S > (foreign size sum) covers it and a
+// bucket entering the chunk with S == 0 is replayed.
+constexpr uint32_t kM14 = (1u << 14) - 1;
+constexpr uint32_t kAccForce = 28;
 static_assert(kApChunk < (1u << 14), "accN field widths");
 static_assert(kScRound <= 65536, "K3 packs ranks in 16 bits");
 #ifndef GNS_REPLAY_LEAD
@@ -1582,7 +1584,7 @@ struct ApplyLds {
     // bucket state, halves paired: sCS = {C, S}, sF = {Fc, Fs} (classify reads both
     // fingerprints, decide both counters: one 8-byte LDS access each)
     uint2 sCS[kTileMax], sF[kTileMax];
-    unsigned long long accN[kTileMax];  // n | n_oth_c<<21 | n_oth_s<<42 | force<<63
+    uint32_t accN[kTileMax];            // n | n_oth_c << 14 | force << 28; after decide: replay flags
     unsigned long long accS[kTileMax];  // sum_own | sum_oth<<32 ; replay owner words
     uint16_t s_list[kApChunk];
     uint64_t s_rep[kRepCap];            // the first kRepCap replay entries themselves (no global re-read)
@@ -1759,7 +1761,8 @@ template <class Src>
 __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, const Src &ent, uint32_t beg,
                                            uint32_t end, uint64_t cbase, uint32_t tn, uint32_t col0,
                                            TilePre &pre, uint64_t next_cbase, uint32_t next_tn) {
-    unsigned long long *accN = L.accN, *accS = L.accS;
+    uint32_t *accN = L.accN;
+    unsigned long long *accS = L.accS;
     uint16_t *s_list = L.s_list;
     uint32_t *s_wc = L.s_wc;
     uint32_t &s_any = L.s_any, &s_nlist = L.s_nlist;
@@ -1815,23 +1818,24 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
             // bucket-range slice (exact global mode): other handles own the rest of the row
             v[j] = q < end && (col0 + b) - a.g.blo < a.g.bspan;
             const bool ovf = (lo & kOvfFlag) != 0;
-            uint64_t incN = 0, incS = 0;
+            uint32_t incN = 0;
+            uint64_t incS = 0;
             if (v[j] && !ovf) {
                 const uint32_t s = hi >> kEntShift;
                 const uint2 f = L.sF[b];
                 const bool oc = lo != f.x, os = lo != f.y;
-                incN = 1ull | (uint64_t)oc << 14 | (uint64_t)os << 28;
+                incN = 1u | (uint32_t)oc << 14;
                 incS = os ? (uint64_t)s << 32 : (uint64_t)s;
             }
             // (designated buckets never reach K4, so a wave's updates rarely share a
             // bucket: plain per-lane LDS atomics beat a wave-majority pre-sum here)
             if (v[j] && !ovf) {
-                atomicAdd(&accN[b], (unsigned long long)incN);
+                atomicAdd(&accN[b], incN);
                 atomicAdd(&accS[b], (unsigned long long)incS);
             }
             if (v[j] && ovf) {  // size >= 2^20-1: always replayed
-                atomicAdd(&accN[b], 1ull);
-                atomicOr(&accN[b], 1ull << kAccForce);
+                atomicAdd(&accN[b], 1u);
+                atomicOr(&accN[b], 1u << kAccForce);
             }
         }
         // prefetch the next chunk while this one is decided / replayed
@@ -1844,11 +1848,10 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
         K4_MARK(0);
         // --- per bucket: exact aggregate update or mark for replay ---
         for (uint32_t i = tid; i < tn; i += kApThreads) {
-            const uint64_t an = accN[i];
+            const uint32_t an = accN[i];
             if (!an) continue;
-            const uint32_t n = (uint32_t)(an & kM14);
-            const uint32_t noc = (uint32_t)((an >> 14) & kM14);
-            const uint32_t nos = (uint32_t)((an >> 28) & kM14);
+            const uint32_t n = an & kM14;
+            const uint32_t noc = (an >> 14) & kM14;
             const bool force = ((an >> kAccForce) & 1u) != 0;
             const uint64_t as = accS[i];
             const uint32_t so = (uint32_t)as, sx = (uint32_t)(as >> 32);
@@ -1861,12 +1864,11 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs &a, ApplyLds &L, cons
                 const uint32_t nown = n - noc;
                 if (C > noc && (uint64_t)C + nown < (1ull << 32)) cs.x = C + nown - noc;
                 else rep |= 1u;
-                // size half: all-own is pure addition (:109-114, u32 wrap ok);
-                // otherwise S > sum_oth keeps S > s before every foreign packet
-                // (:115-125 never replaces) and no wrap.
+                // size half: S > sum_oth keeps S > s (and S > 0) before every foreign
+                // packet (:115-125 never replaces, :103-107 never sees S == 0) and no
+                // wrap; own packets add (:109-114)
                 const uint32_t S = cs.y;
-                if (nos == 0) cs.y = S + so;
-                else if (S > sx && (uint64_t)S + so < (1ull << 32)) cs.y = S + so - sx;
+                if (S > sx && (uint64_t)S + so < (1ull << 32)) cs.y = S + so - sx;
                 else rep |= 2u;
                 L.sCS[i] = cs;
             } else {
