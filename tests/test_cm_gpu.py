@@ -658,3 +658,19 @@ def test_superbin_many_rounds(gpu, oracle, n2):
         orc.insert_keys(keys, sizes)
     cm.flush()
     assert_same_state(cm, orc)
+
+
+@pytest.mark.parametrize("w,d,nflows", [(4096, 2, 6000), (1 << 16, 4, 120_000)])
+def test_tiny_sizes_drain_size_counters(gpu, oracle, w, d, nflows):
+    """Sizes drawn from {0, 1, 2, 3}: the size halves keep reaching S == 0 (a foreign update
+    with s == S drains the bucket, the next one takes it over; a foreign size-0 update takes
+    over only an empty bucket), which the aggregate check must never apply linearly
+    (count_min.go:99-128).  Several batches, so buckets carry S == 0 into later chunks."""
+    rng = np.random.default_rng(w + d)
+    cm, orc = make_pair(oracle, w, d, 16, st=4, ct=50, batch_packets=200_000)
+    keys, _, _ = zipf_keys(rng, 1_000_000, nflows, 16, s=0.9)
+    sizes = rng.integers(0, 4, len(keys), dtype=np.uint64).astype(np.uint32)
+    cm.insert_keys(keys, sizes)
+    cm.flush()
+    orc.insert_keys(keys, sizes)
+    assert_same_state(cm, orc)
