@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-5 measurement runs (GPU box).  usage: tools/r05_bench.sh <tag> <leg>...
-# legs: default (headline + CPU legs + parity), headline (--no-cpu), ss (SuperSpread +
+# legs: default (headline + CPU legs + parity), headline (--no-cpu), thrift, srcip, c1, ss (SuperSpread +
 # CPU leg + parity), c5, exact, hybrid, host_compact, prof_cm, prof_ss (rocprofv3
 # kernel traces with >= 10 steady full-batch launches).  Every GPU step has its own
 # time limit; the script stops at the first failure.
@@ -31,6 +31,9 @@ for leg in "$@"; do
         hybrid) run hybrid 500 --sketch hybrid --no-cpu ;;
         host_compact) run host_compact 300 --host-input compact --no-cpu ;;
         host_compact16) run host_compact16 300 --host-input compact16 --no-cpu ;;
+        thrift) run thrift 400 --sketch thrift --no-cpu ;;
+        srcip) run srcip 400 --key srcip --no-cpu ;;
+        c1) run c1 600 --config c1 ;;
         prof_cm) prof cm 400 --no-cpu --steps 10 --warmup 5 --windows 0 ;;
         prof_ss) prof ss 400 --sketch superspread --no-cpu --steps 10 --warmup 5 ;;
         prof_c5) prof c5 500 --width 16777216 --depth 8 --no-cpu --steps 10 --warmup 5 --windows 0 ;;
