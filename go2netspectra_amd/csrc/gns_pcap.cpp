@@ -148,18 +148,118 @@ struct Cursor {
 };
 
 // classic pcap records after the 24-byte file header
+// One classic-pcap record header at off: (incl, orig, ts), or false past the end.
+struct RecHdr {
+    uint32_t incl, orig;
+    int64_t ts;
+};
+inline bool rec_at(const uint8_t *p, size_t n, size_t off, bool swap, bool nsec, RecHdr &h) {
+    if (off + 16 > n) return false;
+    uint32_t tsec, tfrac;
+    memcpy(&tsec, p + off, 4);
+    memcpy(&tfrac, p + off + 4, 4);
+    memcpy(&h.incl, p + off + 8, 4);
+    memcpy(&h.orig, p + off + 12, 4);
+    if (swap) { h.incl = bswap32(h.incl); h.orig = bswap32(h.orig); tsec = bswap32(tsec); tfrac = bswap32(tfrac); }
+    h.ts = (int64_t)(int32_t)tsec * 1000000000ll + (int64_t)tfrac * (nsec ? 1 : 1000);
+    return true;
+}
+
+// The record walk is a chain through the file (each header gives the next one's offset), so
+// one thread walking a large capture is bound by its memory latency.  Large captures are
+// walked in parallel: the file is cut into one piece per thread, each piece after the first
+// starts at the first offset whose header and the next three chain plausibly (incl <= the
+// snap length, orig >= incl, ...), and each thread walks until it reaches its successor's
+// start.  The pieces are used only if every walk lands exactly on the next piece's start --
+// then their records are the sequential walk's, in the same order; otherwise the capture is
+// walked sequentially.
+struct PieceWalk {
+    std::vector<Desc> d;
+    size_t end = 0;  // offset where the walk stopped
+    bool stopped = false;  // a truncated record or the file's end
+};
+
+inline bool plausible(const uint8_t *p, size_t n, size_t off, bool swap, bool nsec, uint32_t snap) {
+    for (int k = 0; k < 4; k++) {
+        RecHdr h;
+        if (!rec_at(p, n, off, swap, nsec, h)) return k > 0;  // a chain reaching the end is fine
+        if (h.incl > snap || h.incl < 14 || h.orig < h.incl || h.orig > (1u << 24)) return false;
+        off += 16 + (size_t)h.incl;
+        if (off > n) return k > 0;
+    }
+    return true;
+}
+
 int classic(Cursor &f, const char *path, const uint8_t *gh, uint32_t magic, Sink &o) {
     using gns::set_error;
     const bool nsec = magic == 0xa1b23c4du || magic == 0x4d3cb2a1u;
     const bool swap = magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u;
-    uint32_t linktype;
+    uint32_t linktype, snap;
     memcpy(&linktype, gh + 20, 4);
-    if (swap) linktype = bswap32(linktype);
+    memcpy(&snap, gh + 16, 4);
+    if (swap) { linktype = bswap32(linktype); snap = bswap32(snap); }
     if ((linktype & 0x0FFFFFFFu) != 1u) {
         set_error("%s: linktype %u not supported (Ethernet only)", path, linktype);
         return GNS_E_ARG;
     }
+    if (snap == 0 || snap > (1u << 24)) snap = 1u << 24;
+    const int T = o.nthreads;
+    const size_t n = f.n, base = f.off;
+    size_t par_min = (size_t)64 << 20;  // below this the walk is short anyway
+    if (const char *e = getenv("GNS_PACK_PAR_MIN")) par_min = (size_t)strtoull(e, nullptr, 10);
+    if (T > 1 && n - base >= par_min && o.out_ok()) {
+        std::vector<size_t> start(T + 1, n);
+        start[0] = base;
+        bool ok = true;
+        for (int t = 1; t < T && ok; t++) {
+            size_t off = base + (n - base) * (size_t)t / (size_t)T;
+            const size_t lim = std::min(n, off + ((size_t)1 << 20));  // a record is far shorter
+            while (off < lim && !plausible(f.p, n, off, swap, nsec, snap)) off++;
+            if (off >= lim || off <= start[t - 1]) ok = false;
+            start[t] = off;
+        }
+        if (ok) {
+            std::vector<PieceWalk> w(T);
+            auto walk = [&](int t) {
+                size_t off = start[t];
+                const size_t stop = start[t + 1];
+                PieceWalk &pw = w[t];
+                pw.d.reserve((stop - off) / 64 + 16);
+                while (off < stop) {
+                    if (off + 4096 < n) {
+                        __builtin_prefetch(f.p + off + 2048);
+                        __builtin_prefetch(f.p + off + 4096);
+                    }
+                    RecHdr h;
+                    if (!rec_at(f.p, n, off, swap, nsec, h) || off + 16 + (size_t)h.incl > n) {
+                        pw.stopped = true;  // end of file, or a truncated trailer: gopacket stops too
+                        break;
+                    }
+                    pw.d.push_back(Desc{f.p + off + 16, h.incl, h.orig, h.ts});
+                    off += 16 + (size_t)h.incl;
+                }
+                pw.end = off;
+            };
+            std::vector<std::thread> th;
+            th.reserve(T - 1);
+            for (int t = 1; t < T; t++) th.emplace_back(walk, t);
+            walk(0);
+            for (auto &x : th) x.join();
+            for (int t = 0; t + 1 < T && ok; t++) ok = !w[t].stopped && w[t].end == start[t + 1];
+            if (ok) {
+                for (int t = 0; t < T; t++)
+                    for (const Desc &d : w[t].d) o.emit(d.frame, d.incl, d.orig, d.ts);
+                return GNS_OK;
+            }
+        }
+    }
     for (;;) {
+        // the walk is a chain through the file (each header gives the next one's offset):
+        // touch the lines a few KB ahead so the next headers are in cache when reached
+        if (f.off + 4096 < f.n) {
+            __builtin_prefetch(f.p + f.off + 2048);
+            __builtin_prefetch(f.p + f.off + 4096);
+        }
         const uint8_t *rh = f.take(16);
         if (!rh) break;  // end of file, or a truncated trailer: gopacket stops too
         uint32_t incl, orig, tsec, tfrac;
@@ -302,7 +402,7 @@ struct Capture {
         struct stat st;
         if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) {
             size = (size_t)st.st_size;
-            map = mmap(nullptr, size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+            map = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
             if (map == MAP_FAILED) map = nullptr;
             else (void)madvise(map, size, MADV_SEQUENTIAL);
         }

@@ -340,3 +340,30 @@ def test_compact16_packer_carries_wire_lengths(tmp_path):
         g.read_pcap_compact(big, rec_len=True)
     r2, w2, _ = g.read_pcap_compact(big)
     assert w2[0] == 70_000
+
+
+@pytest.mark.parametrize("cut", [0, 37, 9])
+def test_parallel_record_walk_equals_sequential(tmp_path, monkeypatch, cut):
+    """Classic captures are walked in pieces on several threads (gns_pcap.cpp classic());
+    the records, their order, the wire lengths and the timestamps equal the single-thread
+    walk's, also with a truncated trailer (cut bytes off the end: inside a record's data or
+    inside its header) -- the pieces are used only when every walk lands on its successor's
+    start."""
+    path = str(tmp_path / "walk.pcap")
+    g.write_pcapgen(path, 6000, seed=11)
+    if cut:
+        with open(path, "r+b") as f:
+            f.truncate(os.path.getsize(path) - cut)
+    monkeypatch.setenv("GNS_PACK_PAR_MIN", "0")
+    out = {}
+    for t in (1, 3, 8):
+        monkeypatch.setenv("GNS_PACK_THREADS", str(t))
+        hb = g.read_pcap(path)
+        rec, wl, side = g.read_pcap_compact(path)
+        rec16, _, side16 = g.read_pcap_compact(path, rec_len=True)
+        ts = hb.ts if hb.ts is not None else np.zeros(0)
+        out[t] = (hb.hdr.copy(), hb.wirelen.copy(), ts.copy(), rec, wl, side, rec16, side16)
+    assert len(out[1][0]) == 6000 - (1 if cut else 0)
+    for t in (3, 8):
+        for a, b in zip(out[1], out[t]):
+            assert np.array_equal(a, b), t
