@@ -991,11 +991,11 @@ static_assert(kChunk % kStSub == 0, "whole sub-passes per K1 block");
 // NT threads, rows of at most BINS bins: <1024, 256> (the bench geometry) and
 // <512, 512> (the wide/deep configs[5] geometry, 16 packets per thread, one
 // 134 KB block per CU)
-template <int NT, int BINS>
+template <int NT, int BINS, int SUB = (int)kStSub>
 struct StLds {
     static constexpr int kWaves = NT / 64;
-    uint64_t stage[kStSub];
-    uint16_t sbin[kStSub];
+    uint64_t stage[SUB];
+    uint16_t sbin[SUB];
     uint32_t cnt[2][kWaves][BINS];
     uint32_t lstart[BINS], gpos[BINS];
     uint32_t goff[8][BINS];
@@ -1003,15 +1003,16 @@ struct StLds {
     uint32_t dummy[NT];  // rank adds of lanes without an update
 };
 
-template <int NT, int BINS>
+template <int NT, int BINS, int SUB = (int)kStSub>
 __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
+    static_assert(kChunk % SUB == 0, "whole sub-passes per K1 block");
     constexpr int kStThreads = NT;
     constexpr int kStWaves = NT / 64;
-    constexpr int kStItems = kStSub / NT;
+    constexpr int kStItems = (uint32_t)SUB / NT;
     constexpr uint32_t kStBins = BINS;
-    static_assert(kStSub / kStWaves == kStItems * 64, "a wave owns kStItems x 64 consecutive packets of a sub-pass");
+    static_assert((uint32_t)SUB / kStWaves == kStItems * 64, "a wave owns kStItems x 64 consecutive packets of a sub-pass");
     static_assert(BINS <= NT && BINS % 64 == 0, "one thread per bin in the bin scan");
-    __shared__ StLds<NT, BINS> L;
+    __shared__ StLds<NT, BINS, SUB> L;
 #ifdef GNS_K3_PROF
     uint64_t k3t[5] = {0, 0, 0, 0, 0}, k3prev = __builtin_amdgcn_s_memtime();
 #endif
@@ -1026,7 +1027,7 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
     }
     for (uint32_t i = tid; i < 2 * kStWaves * kStBins; i += kStThreads) (&L.cnt[0][0][0])[i] = 0;
     // packet of item j in a sub-pass: wave-contiguous, (j, lane) order inside the wave
-    auto pkt = [&](uint64_t sp, int j) { return sp + (uint64_t)wave * (kStSub / kStWaves) + (uint64_t)j * 64 + lane; };
+    auto pkt = [&](uint64_t sp, int j) { return sp + (uint64_t)wave * ((uint32_t)SUB / kStWaves) + (uint64_t)j * 64 + lane; };
     uint32_t ids[kStItems], szs[kStItems], cds[kStItems];
     uint32_t ncd[kStItems], nids[kStItems], nszs[kStItems];
     auto load_ids = [&](uint64_t sp, uint32_t (&di)[kStItems], uint32_t (&ds)[kStItems]) {
@@ -1049,7 +1050,7 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
     load_codes(beg, 0, cds);
     uint32_t par = 0;
     __syncthreads();
-    for (uint64_t sp = beg; sp < end; sp += kStSub) {
+    for (uint64_t sp = beg; sp < end; sp += (uint32_t)SUB) {
         for (uint32_t r = 0; r < d; r++) {
             uint32_t (&cnt)[kStWaves][kStBins] = L.cnt[par];
             K3_MARK(4);  // loop
@@ -1098,7 +1099,7 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
             }
             // the next step's codes (and ids / sizes at a sub-pass boundary) load during C and D
             const uint32_t r1 = r + 1 < d ? r + 1 : 0u;
-            const uint64_t sp1 = r + 1 < d ? sp : sp + kStSub;
+            const uint64_t sp1 = r + 1 < d ? sp : sp + (uint32_t)SUB;
             if (sp1 < end) {
                 load_codes(sp1, r1, ncd);
                 if (r1 == 0) load_ids(sp1, nids, nszs);
@@ -3214,6 +3215,7 @@ struct gns_cm {
     uint4 *chk = nullptr;                 // [kChkCap]
     bool warm = false;                    // a batch has run since create/reset
     bool lds_ordered = false;             // k_lds_order_probe passed: K3 ranks by LDS adds
+    bool k3_half = false;
     bool k3_staged = true;                // K3s (LDS-staged runs) where the geometry allows; GNS_K3_STAGED=0: K3
     // compact streams (K1 -> K3c): off by default (K3 -0.31 ms, K1 +0.51 ms
     // at the bench geometry); GNS_CMODE=1 turns them on where the geometry allows
@@ -3493,6 +3495,8 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         ScopedStage st(cm->timer, 3);
         if (cm->cmode)
             hipLaunchKernelGGL((k_scatter_cs<1024, 256>), dim3(nblk), dim3(1024), 0, s, a);
+        else if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 256 && g.d <= 8 && cm->k3_half)
+            hipLaunchKernelGGL((k_scatter_st<512, 256, 4096>), dim3(nblk), dim3(512), 0, s, a);
         else if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 256 && g.d <= 8)
             hipLaunchKernelGGL((k_scatter_st<1024, 256>), dim3(nblk), dim3(1024), 0, s, a);
         else if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 512 && g.d <= 8)
@@ -3919,6 +3923,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             cm->lds_ordered = hv == 0 && !(env && env[0] == '0');
             const char *es = getenv("GNS_K3_STAGED");
             cm->k3_staged = !(es && es[0] == '0');
+            cm->k3_half = es && es[0] == 'h';  // A/B: 512-thread K3s, 4096-packet sub-passes, two per CU
             const char *en = getenv("GNS_SUBPART_NT");
             cm->subpart_nt = en ? atoi(en) : 0;
             const char *ec = getenv("GNS_CMODE");
