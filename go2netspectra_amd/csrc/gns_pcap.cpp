@@ -79,8 +79,19 @@ struct Sink {  // record output (the first `cap` packets) and counters
         slab.push_back(Desc{data, incl, orig, ts});
         if (slab.size() == kSlab) flush();
     }
-    void flush() {  // build the slab's records (file order), several threads over contiguous ranges
-        const size_t m = slab.size();
+    void flush() {  // build the slab's records (file order)
+        build(slab.data(), slab.size());
+        slab.clear();
+    }
+    // a walked piece of the capture, in file order (no emit/slab copy): counted, and
+    // its records built up to cap
+    void take(const std::vector<Desc> &v) {
+        flush();
+        n += v.size();
+        if (!out_ok() || written >= cap) return;
+        build(v.data(), (size_t)std::min<uint64_t>(v.size(), cap - written));
+    }
+    void build(const Desc *src, size_t m) {  // records of src[0, m), several threads over contiguous ranges
         if (!m) return;
         const int T = (int)std::min<size_t>((size_t)nthreads, (m + 4095) / 4096);
         uint64_t part[64][3] = {};
@@ -90,7 +101,7 @@ struct Sink {  // record output (the first `cap` packets) and counters
             const size_t i0 = m * t / T, i1 = m * (t + 1) / T;
             uint8_t tmp[64];
             for (size_t i = i0; i < i1; i++) {
-                const Desc &dsc = slab[i];
+                const Desc &dsc = src[i];
                 const uint64_t j = written + i;
                 uint8_t *r = rec16 ? tmp : hdr + j * 64;
                 const int code = gns::frame_record(dsc.frame, dsc.incl, dsc.orig, r);
@@ -129,7 +140,6 @@ struct Sink {  // record output (the first `cap` packets) and counters
             }
         }
         written += m;
-        slab.clear();
     }
 };
 
@@ -247,8 +257,7 @@ int classic(Cursor &f, const char *path, const uint8_t *gh, uint32_t magic, Sink
             for (auto &x : th) x.join();
             for (int t = 0; t + 1 < T && ok; t++) ok = !w[t].stopped && w[t].end == start[t + 1];
             if (ok) {
-                for (int t = 0; t < T; t++)
-                    for (const Desc &d : w[t].d) o.emit(d.frame, d.incl, d.orig, d.ts);
+                for (int t = 0; t < T; t++) o.take(w[t].d);
                 return GNS_OK;
             }
         }

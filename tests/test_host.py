@@ -362,8 +362,11 @@ def test_parallel_record_walk_equals_sequential(tmp_path, monkeypatch, cut):
         rec, wl, side = g.read_pcap_compact(path)
         rec16, _, side16 = g.read_pcap_compact(path, rec_len=True)
         ts = hb.ts if hb.ts is not None else np.zeros(0)
-        out[t] = (hb.hdr.copy(), hb.wirelen.copy(), ts.copy(), rec, wl, side, rec16, side16)
-    assert len(out[1][0]) == 6000 - (1 if cut else 0)
+        lim = g.read_pcap(path, limit=2500)  # a cap inside a piece
+        rl, wll, sl = g.read_pcap_compact(path, limit=2500)
+        out[t] = (hb.hdr.copy(), hb.wirelen.copy(), ts.copy(), rec, wl, side, rec16, side16,
+                  lim.hdr.copy(), lim.wirelen.copy(), rl, wll, sl)
+    assert len(out[1][0]) == 6000 - (1 if cut else 0) and len(out[1][8]) == 2500
     for t in (3, 8):
         for a, b in zip(out[1], out[t]):
             assert np.array_equal(a, b), t
