@@ -989,22 +989,29 @@ constexpr uint32_t kStSub = GNS_ST_SUB;               // packets per sub-pass
 static_assert(kChunk % kStSub == 0, "whole sub-passes per K1 block");
 
 // NT threads, rows of at most BINS bins: <1024, 256> (the bench geometry) and
-// <512, 512> (the wide/deep configs[5] geometry, 16 packets per thread, one
-// 134 KB block per CU)
-template <int NT, int BINS, int SUB = (int)kStSub>
+// <1024, 512, kStSub, PK> (the wide/deep configs[4]/[5] geometry: 16 waves in one 136 KB
+// block per CU; the former <512, 512>, 8 waves, stays behind GNS_K3_STAGED=u:
+// K3s 3.08 -> 3.04 ms at configs[4], profiles/r05_ab_k3pack.txt).
+// PK: the (wave, bin) counters as 16-bit halves, bins t and t + BINS/2 in one word (a wave
+// counts at most SUB/kWaves updates of a bin per sub-pass), which is what lets 16 waves'
+// counters fit
+template <int NT, int BINS, int SUB = (int)kStSub, bool PK = false>
 struct StLds {
     static constexpr int kWaves = NT / 64;
+    static constexpr int kCw = PK ? BINS / 2 : BINS;  // counter words per wave
     uint64_t stage[SUB];
     uint16_t sbin[SUB];
-    uint32_t cnt[2][kWaves][BINS];
+    uint32_t cnt[2][kWaves][kCw];
     uint32_t lstart[BINS], gpos[BINS];
     uint32_t goff[8][BINS];
     uint32_t wsum[BINS / 64];
     uint32_t dummy[NT];  // rank adds of lanes without an update
 };
 
-template <int NT, int BINS, int SUB = (int)kStSub>
+template <int NT, int BINS, int SUB = (int)kStSub, bool PK = false>
 __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
+    static_assert(!PK || (SUB / (NT / 64) < 65536 && BINS % 128 == 0), "16-bit counter halves");
+    constexpr uint32_t kCw = StLds<NT, BINS, SUB, PK>::kCw;
     static_assert(kChunk % SUB == 0, "whole sub-passes per K1 block");
     constexpr int kStThreads = NT;
     constexpr int kStWaves = NT / 64;
@@ -1012,7 +1019,7 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
     constexpr uint32_t kStBins = BINS;
     static_assert((uint32_t)SUB / kStWaves == kStItems * 64, "a wave owns kStItems x 64 consecutive packets of a sub-pass");
     static_assert(BINS <= NT && BINS % 64 == 0, "one thread per bin in the bin scan");
-    __shared__ StLds<NT, BINS, SUB> L;
+    __shared__ StLds<NT, BINS, SUB, PK> L;
 #ifdef GNS_K3_PROF
     uint64_t k3t[5] = {0, 0, 0, 0, 0}, k3prev = __builtin_amdgcn_s_memtime();
 #endif
@@ -1025,7 +1032,7 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
         const uint32_t r = i / kStBins, t = i % kStBins;
         L.goff[r][t] = t < nt ? a.offsets[(uint64_t)blk * a.g.nbins_all + r * nt + t] : 0u;
     }
-    for (uint32_t i = tid; i < 2 * kStWaves * kStBins; i += kStThreads) (&L.cnt[0][0][0])[i] = 0;
+    for (uint32_t i = tid; i < 2 * kStWaves * kCw; i += kStThreads) (&L.cnt[0][0][0])[i] = 0;
     // packet of item j in a sub-pass: wave-contiguous, (j, lane) order inside the wave
     auto pkt = [&](uint64_t sp, int j) { return sp + (uint64_t)wave * ((uint32_t)SUB / kStWaves) + (uint64_t)j * 64 + lane; };
     uint32_t ids[kStItems], szs[kStItems], cds[kStItems];
@@ -1052,7 +1059,7 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
     __syncthreads();
     for (uint64_t sp = beg; sp < end; sp += (uint32_t)SUB) {
         for (uint32_t r = 0; r < d; r++) {
-            uint32_t (&cnt)[kStWaves][kStBins] = L.cnt[par];
+            uint32_t (&cnt)[kStWaves][kCw] = L.cnt[par];
             K3_MARK(4);  // loop
             // phase A: entries and stable ranks within (wave, bin)
             uint64_t ent[kStItems];
@@ -1091,8 +1098,10 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
 #pragma unroll
                 for (int j = 0; j < kStItems; j++) {
                     const uint32_t t = tb[j] >> 16;
-                    uint32_t *ad = t != 0xFFFFu ? &cnt[wave][t] : &L.dummy[tid];
-                    rks[j] = atomicAdd(ad, t != 0xFFFFu ? 1u : 0u);
+                    const uint32_t sh = PK && t != 0xFFFFu && t >= kCw ? 16u : 0u;
+                    uint32_t *ad = t != 0xFFFFu ? &cnt[wave][PK ? t % kCw : t] : &L.dummy[tid];
+                    rks[j] = atomicAdd(ad, t != 0xFFFFu ? 1u << sh : 0u);
+                    if constexpr (PK) rks[j] = (rks[j] >> sh) & 0xFFFFu;
                 }
 #pragma unroll
                 for (int j = 0; j < kStItems; j++) tb[j] |= rks[j];
@@ -1108,7 +1117,26 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
             K3_MARK(0);
             // phase C: per bin, prefix over the waves and the bin's total; scan of the totals
             uint32_t total = 0, incl = 0;
-            if (tid < kStBins) {
+            if constexpr (PK) {  // both halves' prefix over the waves; the totals via lstart
+                if (tid < kCw) {
+                    uint32_t r0 = 0, r1 = 0;
+#pragma unroll
+                    for (int w = 0; w < kStWaves; w++) {
+                        const uint32_t x = cnt[w][tid];
+                        cnt[w][tid] = r0 | r1 << 16;
+                        r0 += x & 0xFFFFu;
+                        r1 += x >> 16;
+                    }
+                    L.lstart[tid] = r0;
+                    L.lstart[tid + kCw] = r1;
+                }
+                __syncthreads();
+                if (tid < kStBins) {
+                    total = L.lstart[tid];
+                    incl = wave_incl_scan(total);
+                    if (lane == 63) L.wsum[wave] = incl;
+                }
+            } else if (tid < kStBins) {
                 const uint32_t t = tid;
                 uint32_t run = 0;
                 if (t < nt) {
@@ -1140,7 +1168,8 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
             for (int j = 0; j < kStItems; j++) {
                 const uint32_t t = tb[j] >> 16;
                 if (t != 0xFFFFu) {
-                    const uint32_t pos = L.lstart[t] + cnt[wave][t] + (tb[j] & 0xFFFFu);
+                    const uint32_t c = PK ? (cnt[wave][t % kCw] >> (t >= kCw ? 16u : 0u)) & 0xFFFFu : cnt[wave][t];
+                    const uint32_t pos = L.lstart[t] + c + (tb[j] & 0xFFFFu);
                     L.stage[pos] = ent[j];
                     L.sbin[pos] = (uint16_t)t;
                 }
@@ -1165,7 +1194,7 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
                 const uint32_t t = L.sbin[i];
                 a.entries[L.gpos[t] + (i - L.lstart[t])] = L.stage[i];
             }
-            for (uint32_t i = tid; i < kStWaves * kStBins; i += kStThreads) (&cnt[0][0])[i] = 0;
+            for (uint32_t i = tid; i < kStWaves * kCw; i += kStThreads) (&cnt[0][0])[i] = 0;
             par ^= 1u;
             K3_MARK(3);
         }
@@ -3215,7 +3244,7 @@ struct gns_cm {
     uint4 *chk = nullptr;                 // [kChkCap]
     bool warm = false;                    // a batch has run since create/reset
     bool lds_ordered = false;             // k_lds_order_probe passed: K3 ranks by LDS adds
-    bool k3_half = false;
+    bool k3_half = false, k3_pack = false;
     bool k3_staged = true;                // K3s (LDS-staged runs) where the geometry allows; GNS_K3_STAGED=0: K3
     // compact streams (K1 -> K3c): off by default (K3 -0.31 ms, K1 +0.51 ms
     // at the bench geometry); GNS_CMODE=1 turns them on where the geometry allows
@@ -3499,6 +3528,8 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
             hipLaunchKernelGGL((k_scatter_st<512, 256, 4096>), dim3(nblk), dim3(512), 0, s, a);
         else if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 256 && g.d <= 8)
             hipLaunchKernelGGL((k_scatter_st<1024, 256>), dim3(nblk), dim3(1024), 0, s, a);
+        else if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 512 && g.d <= 8 && cm->k3_pack)
+            hipLaunchKernelGGL((k_scatter_st<1024, 512, (int)kStSub, true>), dim3(nblk), dim3(1024), 0, s, a);
         else if (cm->lds_ordered && cm->k3_staged && g.ntiles <= 512 && g.d <= 8)
             hipLaunchKernelGGL((k_scatter_st<512, 512>), dim3(nblk), dim3(512), 0, s, a);
         else if (cm->lds_ordered)
@@ -3923,7 +3954,8 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             cm->lds_ordered = hv == 0 && !(env && env[0] == '0');
             const char *es = getenv("GNS_K3_STAGED");
             cm->k3_staged = !(es && es[0] == '0');
-            cm->k3_half = es && es[0] == 'h';  // A/B: 512-thread K3s, 4096-packet sub-passes, two per CU
+            cm->k3_half = es && es[0] == 'h';
+            cm->k3_pack = !(es && es[0] == 'u');  // 512-bin rows: 1024-thread K3s, 16-bit counters (u: 512 threads)  // A/B: 512-thread K3s, 4096-packet sub-passes, two per CU
             const char *en = getenv("GNS_SUBPART_NT");
             cm->subpart_nt = en ? atoi(en) : 0;
             const char *ec = getenv("GNS_CMODE");
