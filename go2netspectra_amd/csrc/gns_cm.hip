@@ -742,6 +742,7 @@ __global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
 // ---------------------------------------------------------------------------
 struct ScatterArgs {
     uint64_t n;
+    uint32_t xcd_map;  // K3s: consecutive K1 blocks to workgroups on one XCD (GNS_K3_XCD=0: off)
     CmGeom g;
     const uint32_t *keyid;
     const uint32_t *idx;
@@ -1024,7 +1025,17 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
     uint64_t k3t[5] = {0, 0, 0, 0, 0}, k3prev = __builtin_amdgcn_s_memtime();
 #endif
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t blk = blockIdx.x, d = a.g.d, nt = a.g.ntiles;
+    uint32_t blk = blockIdx.x;
+    const uint32_t d = a.g.d, nt = a.g.ntiles;
+    // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH: observed, not promised),
+    // so K1 block b and b + 1 -- whose runs of a bin are adjacent in `entries` and share the
+    // partial lines at their boundary -- would be written through two different L2s.  Give each
+    // XCD a contiguous range of K1 blocks instead: headline K3s 1.37 -> 1.25 ms, configs[4]
+    // 3.42 -> 2.67 ms (profiles/r05_ab_k3xcd.txt).  Only the speed depends on the placement.
+    if (a.xcd_map) {
+        const uint32_t G = gridDim.x, x = blk & 7u, q = G >> 3, r = G & 7u;
+        blk = x * q + min(x, r) + (blk >> 3);
+    }
     const uint32_t tmask = (1u << a.g.bin_bits) - 1u;
     const uint64_t beg = (uint64_t)blk * kChunk;
     const uint64_t end = min(a.n, beg + kChunk);
@@ -3245,6 +3256,7 @@ struct gns_cm {
     bool warm = false;                    // a batch has run since create/reset
     bool lds_ordered = false;             // k_lds_order_probe passed: K3 ranks by LDS adds
     bool k3_half = false, k3_pack = false;
+    uint32_t k3_xcd = 0;
     bool k3_staged = true;                // K3s (LDS-staged runs) where the geometry allows; GNS_K3_STAGED=0: K3
     // compact streams (K1 -> K3c): off by default (K3 -0.31 ms, K1 +0.51 ms
     // at the bench geometry); GNS_CMODE=1 turns them on where the geometry allows
@@ -3517,6 +3529,7 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
     {
         ScatterArgs a{};
         a.n = n; a.g = g; a.keyid = cm->keyid; a.idx = cm->idx; a.sizes = in.sizes;
+        a.xcd_map = cm->k3_xcd;
         a.offsets = cm->hist; a.nblk = nblk; a.entries = cm->entries; a.ovf = cm->ovf;
         a.ovf_cnt = cm->ovf_cnt; a.ovf_cap = (uint32_t)cm->ovf_cap; a.hot_ids = cm->hot_ids; a.stats = cm->stats;
         a.hot_mode = 0; a.hflag2 = cm->hflag2; a.hany = cm->hflag2 + g.d * kHot;
@@ -3955,6 +3968,8 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             const char *es = getenv("GNS_K3_STAGED");
             cm->k3_staged = !(es && es[0] == '0');
             cm->k3_half = es && es[0] == 'h';
+            const char *ex = getenv("GNS_K3_XCD");
+            cm->k3_xcd = ex && ex[0] == '0' ? 0u : 1u;
             cm->k3_pack = !(es && es[0] == 'u');  // 512-bin rows: 1024-thread K3s, 16-bit counters (u: 512 threads)  // A/B: 512-thread K3s, 4096-packet sub-passes, two per CU
             const char *en = getenv("GNS_SUBPART_NT");
             cm->subpart_nt = en ? atoi(en) : 0;
