@@ -30,6 +30,7 @@
 #include "gns_common.hpp"
 #include "gns_ctl.cuh"
 #include "gns_scan.cuh"
+#include "gns_xcd.cuh"
 
 namespace gns {
 
@@ -1032,10 +1033,7 @@ __global__ __launch_bounds__(NT) void k_scatter_st(ScatterArgs a) {
     // partial lines at their boundary -- would be written through two different L2s.  Give each
     // XCD a contiguous range of K1 blocks instead: headline K3s 1.37 -> 1.25 ms, configs[4]
     // 3.42 -> 2.67 ms (profiles/r05_ab_k3xcd.txt).  Only the speed depends on the placement.
-    if (a.xcd_map) {
-        const uint32_t G = gridDim.x, x = blk & 7u, q = G >> 3, r = G & 7u;
-        blk = x * q + min(x, r) + (blk >> 3);
-    }
+    if (a.xcd_map) blk = xcd_block(blk, gridDim.x);
     const uint32_t tmask = (1u << a.g.bin_bits) - 1u;
     const uint64_t beg = (uint64_t)blk * kChunk;
     const uint64_t end = min(a.n, beg + kChunk);

@@ -43,6 +43,7 @@
 #include <vector>
 
 #include "gns_common.hpp"
+#include "gns_xcd.cuh"
 
 namespace gns {
 
@@ -579,7 +580,8 @@ __global__ __launch_bounds__(kPBins) void k_ex_pscatter(const uint64_t *in, cons
     __shared__ uint64_t stage[kPSub];
     __shared__ uint16_t sbin[kPSub];
     __shared__ uint32_t cnt[kPBins], lstart[kPBins], goff[kPBins], dummy[kPBins], s_w[kPBins / 64];
-    const uint32_t blk = blockIdx.x, n = ccnt[blk], tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);  // adjacent regions on one XCD (gns_xcd.cuh)
+    const uint32_t n = ccnt[blk], tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     if (n == 0) return;  // block-uniform
     const uint64_t *src = in + (uint64_t)blk * kXChunk;
     goff[tid] = po[(uint64_t)blk * kPBins + tid];

@@ -737,6 +737,7 @@ __global__ __launch_bounds__(256) void k_sp_scatter(const uint64_t *ckey, const 
     __shared__ uint64_t stage[kSpSub];
     __shared__ uint16_t sbin[kSpSub];
     __shared__ uint32_t wsum[4];
+    // (the XCD-contiguous order of gns_xcd.cuh measured neutral here: profiles/r05_ab_xcd_all.txt)
     const uint32_t blk = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     for (uint32_t i = tid; i < s.nb; i += 256) { gpos[i] = offs[(uint64_t)blk * s.nb + i]; cnt[i] = 0; }
     __syncthreads();
