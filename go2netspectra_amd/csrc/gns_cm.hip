@@ -488,7 +488,11 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
     extern __shared__ __attribute__((aligned(16))) uint8_t xsm[];
     __shared__ uint32_t s_pend, s_drop, s_unsup, s_full, s_ok, s_claim;
     __shared__ uint8_t s_src[80];
+#ifdef GNS_K1_XCD
+    const uint32_t tid = threadIdx.x, blk = xcd_block(blockIdx.x, gridDim.x);  // A/B
+#else
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+#endif
     const uint32_t NS = a.g.d * kHot;
     unsigned long long *s_os = reinterpret_cast<unsigned long long *>(xsm);
     unsigned long long *s_fs = s_os + NS;
