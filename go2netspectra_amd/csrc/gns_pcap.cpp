@@ -217,23 +217,32 @@ int classic(Cursor &f, const char *path, const uint8_t *gh, uint32_t magic, Sink
     const size_t n = f.n, base = f.off;
     size_t par_min = (size_t)64 << 20;  // below this the walk is short anyway
     if (const char *e = getenv("GNS_PACK_PAR_MIN")) par_min = (size_t)strtoull(e, nullptr, 10);
+    // windows of the file (1 GiB by default) bound the descriptors held at once; each window
+    // starts where the previous one's last piece stopped, a record start by the same induction
+    size_t win = (size_t)1 << 30;
+    if (const char *e = getenv("GNS_PACK_WINDOW")) win = std::max<size_t>(4096, (size_t)strtoull(e, nullptr, 10));
     if (T > 1 && n - base >= par_min && o.out_ok()) {
-        std::vector<size_t> start(T + 1, n);
-        start[0] = base;
-        bool ok = true;
-        for (int t = 1; t < T && ok; t++) {
-            size_t off = base + (n - base) * (size_t)t / (size_t)T;
-            const size_t lim = std::min(n, off + ((size_t)1 << 20));  // a record is far shorter
-            while (off < lim && !plausible(f.p, n, off, swap, nsec, snap)) off++;
-            if (off >= lim || off <= start[t - 1]) ok = false;
-            start[t] = off;
-        }
-        if (ok) {
-            std::vector<PieceWalk> w(T);
+        size_t pos = base;
+        std::vector<PieceWalk> w(T);
+        while (pos < n) {
+            const size_t wend = std::min(n, pos + win);  // the window: records starting before wend
+            std::vector<size_t> start(T + 1, wend);
+            start[0] = pos;
+            bool ok = true;
+            for (int t = 1; t < T && ok; t++) {
+                size_t off = pos + (wend - pos) * (size_t)t / (size_t)T;
+                const size_t lim = std::min(wend, off + ((size_t)1 << 20));  // a record is far shorter
+                while (off < lim && !plausible(f.p, n, off, swap, nsec, snap)) off++;
+                if (off >= lim || off <= start[t - 1]) ok = false;
+                start[t] = off;
+            }
+            if (!ok) break;  // the rest sequentially, from pos
             auto walk = [&](int t) {
                 size_t off = start[t];
                 const size_t stop = start[t + 1];
                 PieceWalk &pw = w[t];
+                pw.d.clear();
+                pw.stopped = false;
                 pw.d.reserve((stop - off) / 64 + 16);
                 while (off < stop) {
                     if (off + 4096 < n) {
@@ -256,11 +265,12 @@ int classic(Cursor &f, const char *path, const uint8_t *gh, uint32_t magic, Sink
             walk(0);
             for (auto &x : th) x.join();
             for (int t = 0; t + 1 < T && ok; t++) ok = !w[t].stopped && w[t].end == start[t + 1];
-            if (ok) {
-                for (int t = 0; t < T; t++) o.take(w[t].d);
-                return GNS_OK;
-            }
+            if (!ok) break;  // the rest sequentially, from pos
+            for (int t = 0; t < T; t++) o.take(w[t].d);
+            if (w[T - 1].stopped) return GNS_OK;
+            pos = w[T - 1].end;
         }
+        f.off = pos;  // a record start (or the end of the file)
     }
     for (;;) {
         // the walk is a chain through the file (each header gives the next one's offset):

@@ -347,8 +347,8 @@ def test_parallel_record_walk_equals_sequential(tmp_path, monkeypatch, cut):
     """Classic captures are walked in pieces on several threads (gns_pcap.cpp classic());
     the records, their order, the wire lengths and the timestamps equal the single-thread
     walk's, also with a truncated trailer (cut bytes off the end: inside a record's data or
-    inside its header) -- the pieces are used only when every walk lands on its successor's
-    start."""
+    inside its header), and over several windows of the file -- the pieces are used only when
+    every walk lands on its successor's start."""
     path = str(tmp_path / "walk.pcap")
     g.write_pcapgen(path, 6000, seed=11)
     if cut:
@@ -356,17 +356,20 @@ def test_parallel_record_walk_equals_sequential(tmp_path, monkeypatch, cut):
             f.truncate(os.path.getsize(path) - cut)
     monkeypatch.setenv("GNS_PACK_PAR_MIN", "0")
     out = {}
-    for t in (1, 3, 8):
+    for t, win in ((1, None), (3, None), (8, None), (8, 1 << 20), (3, 300_000)):
         monkeypatch.setenv("GNS_PACK_THREADS", str(t))
+        if win:  # several windows, each cut into pieces
+            monkeypatch.setenv("GNS_PACK_WINDOW", str(win))
         hb = g.read_pcap(path)
         rec, wl, side = g.read_pcap_compact(path)
         rec16, _, side16 = g.read_pcap_compact(path, rec_len=True)
         ts = hb.ts if hb.ts is not None else np.zeros(0)
         lim = g.read_pcap(path, limit=2500)  # a cap inside a piece
         rl, wll, sl = g.read_pcap_compact(path, limit=2500)
-        out[t] = (hb.hdr.copy(), hb.wirelen.copy(), ts.copy(), rec, wl, side, rec16, side16,
-                  lim.hdr.copy(), lim.wirelen.copy(), rl, wll, sl)
-    assert len(out[1][0]) == 6000 - (1 if cut else 0) and len(out[1][8]) == 2500
-    for t in (3, 8):
-        for a, b in zip(out[1], out[t]):
-            assert np.array_equal(a, b), t
+        out[t, win] = (hb.hdr.copy(), hb.wirelen.copy(), ts.copy(), rec, wl, side, rec16, side16,
+                       lim.hdr.copy(), lim.wirelen.copy(), rl, wll, sl)
+    ref = out[1, None]
+    assert len(ref[0]) == 6000 - (1 if cut else 0) and len(ref[8]) == 2500
+    for key, got in out.items():
+        for a, b in zip(ref, got):
+            assert np.array_equal(a, b), key
