@@ -26,8 +26,7 @@
 //
 // Not compiled in the build container (no Go toolchain there); tests/test_gputask_replay_gpu.py
 // replays this file's call sequence through the C ABI (integration/c/gputask_replay.c).
-
-toolchain there).
+package sketchgpu
 
 import (
 	"fmt"
