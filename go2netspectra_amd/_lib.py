@@ -25,16 +25,16 @@ FIELD_SIZE = {"SrcIP": 16, "DstIP": 16, "SrcPort": 2, "DstPort": 2, "Protocol": 
 
 EXPORTED = [
     "gns_cm_create", "gns_cm_destroy", "gns_cm_insert_keys", "gns_cm_insert_tuples",
-    "gns_cm_insert_headers", "gns_cm_flush", "gns_cm_query", "gns_cm_heavy_hitters", "gns_cm_reset",
+    "gns_cm_insert_headers", "gns_cm_flush", "gns_cm_query", "gns_cm_query_device", "gns_cm_heavy_hitters", "gns_cm_reset",
     "gns_cm_export_state", "gns_cm_stats", "gns_cm_counters", "gns_cm_set_timing", "gns_cm_stage_times", "gns_cm_stream",
     "gns_cm_view_create", "gns_cm_view_destroy", "gns_cm_view_refresh", "gns_cm_view_heavy_hitters",
     "gns_cm_view_query",
     "gns_ss_create", "gns_ss_destroy", "gns_ss_insert_keys", "gns_ss_insert_tuples",
-    "gns_ss_insert_headers", "gns_ss_flush", "gns_ss_query", "gns_ss_heavy_hitters", "gns_ss_reset",
+    "gns_ss_insert_headers", "gns_ss_flush", "gns_ss_query", "gns_ss_query_device", "gns_ss_heavy_hitters", "gns_ss_reset",
     "gns_ss_export_state", "gns_ss_stats", "gns_ss_counters", "gns_ss_set_timing", "gns_ss_stage_times",
     "gns_synth_create", "gns_synth_destroy", "gns_synth_fill", "gns_synth_flows",
     "gns_ex_create", "gns_ex_destroy", "gns_ex_insert_tuples", "gns_ex_insert_headers", "gns_ex_flush",
-    "gns_ex_query", "gns_ex_snapshot", "gns_ex_reset", "gns_ex_counters", "gns_ex_set_timing",
+    "gns_ex_query", "gns_ex_query_device", "gns_ex_snapshot", "gns_ex_reset", "gns_ex_counters", "gns_ex_set_timing",
     "gns_ex_stage_times",
     "gns_thrift_decode", "gns_pack_pcap", "gns_pack_pcap_ts", "gns_pack_counts", "gns_frame_record", "gns_last_error", "gns_version",
     "gns_route_create", "gns_route_destroy", "gns_route_partition",
@@ -128,6 +128,7 @@ def load() -> ct.CDLL:
         "gns_cm_insert_tuples": ([vp, vp, u64, i32], i32),
         "gns_cm_insert_headers": ([vp, vp, vp, u64, i32], i32),
         "gns_cm_flush": ([vp], i32), "gns_cm_query": ([vp, vp, u32, u64, vp], i32),
+        "gns_cm_query_device": ([vp, vp, u32, u64, vp], i32),
         "gns_cm_heavy_hitters": ([vp, vp, vp, vp, vp, vp, vp], i32), "gns_cm_reset": ([vp], i32),
         "gns_cm_export_state": ([vp, vp, vp, vp, vp], i32), "gns_cm_stats": ([vp, vp], i32),
         "gns_cm_counters": ([vp, vp], i32),
@@ -141,6 +142,7 @@ def load() -> ct.CDLL:
         "gns_ss_insert_tuples": ([vp, vp, u64, i32], i32),
         "gns_ss_insert_headers": ([vp, vp, vp, u64, i32], i32),
         "gns_ss_flush": ([vp], i32), "gns_ss_query": ([vp, vp, u32, u64, vp], i32),
+        "gns_ss_query_device": ([vp, vp, u32, u64, vp], i32),
         "gns_ss_heavy_hitters": ([vp, vp, vp, vp], i32), "gns_ss_reset": ([vp], i32),
         "gns_ss_export_state": ([vp, vp, vp, vp, vp], i32), "gns_ss_stats": ([vp, vp], i32),
         "gns_ss_counters": ([vp, vp], i32),
@@ -151,6 +153,7 @@ def load() -> ct.CDLL:
         "gns_ex_insert_tuples": ([vp, vp, vp, vp, u64, i32], i32),
         "gns_ex_insert_headers": ([vp, vp, vp, vp, u64, i32], i32),
         "gns_ex_flush": ([vp], i32), "gns_ex_query": ([vp, vp, u32, u64, vp], i32),
+        "gns_ex_query_device": ([vp, vp, u32, u64, vp], i32),
         "gns_ex_snapshot": ([vp, vp, vp, vp, vp, vp, vp], i32), "gns_ex_reset": ([vp], i32),
         "gns_ex_counters": ([vp, vp], i32), "gns_ex_set_timing": ([vp, i32], i32),
         "gns_ex_stage_times": ([vp, vp, vp, i32], i32),
@@ -201,6 +204,25 @@ def device_ready(*arrays) -> None:
         seen.add(d)
         import torch
         torch.cuda.current_stream(a.device).synchronize()
+
+
+def is_device(a) -> bool:
+    return bool(getattr(a, "is_cuda", False))
+
+
+def query_device(fn, h, keys):
+    """A *_query_device call: keys a device uint8 tensor [n, K] on the handle's GPU ->
+    a device int64 tensor [n] holding the uint64 answers (no host copy either way)."""
+    import torch
+    n = int(keys.shape[0])
+    out = torch.empty((n,), dtype=torch.int64, device=keys.device)
+    if n:
+        keys = keys.reshape(n, -1).contiguous()
+        if keys.dtype != torch.uint8:
+            raise TypeError(f"device keys must be uint8, not {keys.dtype}")
+        device_ready(keys)
+        check(fn(h, keys.data_ptr(), int(keys.shape[1]), n, out.data_ptr()))
+    return out
 
 
 DICT_STATS = ["reclaims", "dropped", "live", "claimed", "reclaim_us", "retried_batches", "slots", "growths"]

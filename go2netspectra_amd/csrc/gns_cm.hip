@@ -29,6 +29,7 @@
 
 #include "gns_common.hpp"
 #include "gns_ctl.cuh"
+#include "gns_hh.hpp"
 #include "gns_scan.cuh"
 #include "gns_xcd.cuh"
 
@@ -2940,17 +2941,21 @@ constexpr uint32_t kHhItems = 8;
 //                key (bytes K-1..4 first, then the primary key).  A pass whose
 //                digit is the same for every entry (IPv4 slots' zero padding) only
 //                copies.  Canonical order: value desc, flow bytes asc.
+// A candidate whose id is not a dictionary slot (a corrupt fingerprint word) is
+// skipped and raises *bad: the host then fails the call with GNS_E_HIP instead of
+// letting the per-flow words be indexed out of bounds.
 __global__ __launch_bounds__(256) void k_hh_best(const uint64_t *cand, uint32_t n, unsigned long long *best,
-                                                 uint32_t epoch) {
+                                                 uint32_t epoch, uint64_t slots, uint32_t *bad) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const uint64_t c = cand[i];  // value << 32 | id
+    if ((uint32_t)c >= slots) { atomicOr(bad, 1u); return; }
     atomicMax(&best[(uint32_t)c], (unsigned long long)epoch << 32 | (c >> 32));
 }
 
 __global__ __launch_bounds__(256) void k_hh_emit(const uint64_t *cand, uint32_t n, const unsigned long long *best,
-                                                 uint32_t *mark, uint32_t epoch, uint32_t *uid, uint32_t *uval,
-                                                 uint32_t *nu) {
+                                                 uint32_t *mark, uint32_t epoch, uint64_t slots, uint32_t *uid,
+                                                 uint32_t *uval, uint32_t *nu) {
     __shared__ uint32_t s_n, s_base;
     if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
@@ -2961,7 +2966,7 @@ __global__ __launch_bounds__(256) void k_hh_emit(const uint64_t *cand, uint32_t 
         const uint64_t c = cand[i];
         id = (uint32_t)c;
         v = (uint32_t)(c >> 32);
-        out = (uint32_t)best[id] == v && atomicExch(&mark[id], epoch) != epoch;  // one per flow
+        out = id < slots && (uint32_t)best[id] == v && atomicExch(&mark[id], epoch) != epoch;  // one per flow
     }
     const uint32_t off = out ? atomicAdd(&s_n, 1u) : 0u;
     __syncthreads();
@@ -3180,10 +3185,14 @@ struct CmScratch {
     uint64_t obytes_n = 0;
     uint8_t *hpin = nullptr;    // pinned host staging of the heavy-hitter rows (D2H into pageable
     uint64_t hpin_n = 0;        // caller memory went through the runtime's slow path)
+    uint32_t *hsm = nullptr;    // pinned host words for the list's small read-backs (lengths, flags):
+                                // a 4-byte D2H into a pageable stack word took 28-35 ms now and then
     void free_all() {
         dfree(obytes); obytes = nullptr; obytes_n = 0;
         if (hpin) (void)hipHostFree(hpin);
         hpin = nullptr; hpin_n = 0;
+        if (hsm) (void)hipHostFree(hsm);
+        hsm = nullptr;
         dfree(cand); dfree(ncand); dfree(ids); dfree(bytes); dfree(qkeys); dfree(qout);
         dfree(best); dfree(mark); dfree(u32a); dfree(u32b); dfree(u32c); dfree(u32d); dfree(rsh);
         cand = nullptr; ncand = nullptr; ids = nullptr; bytes = nullptr; qkeys = nullptr; qout = nullptr;
@@ -4081,22 +4090,28 @@ int gns_cm_flush(gns_cm *cm) {
 
 }  // extern "C"
 
-// Query (count_min.go:160-174) of host keys against state (C, Fc, S, Fs) on stream st.
+// Query (count_min.go:160-174) of n keys against state (C, Fc, S, Fs) on stream st:
+// host keys / answers (staged through the grow-only scratch), or device keys /
+// answers (dev: no copies; the call returns once the answers are written).
 static int cm_query_impl(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_t *C, const uint32_t *Fc,
                          const uint32_t *S, const uint32_t *Fs, const uint8_t *keys, uint32_t stride, uint64_t n,
-                         uint64_t *out) {
-    GNS_TRY(grow_buf(&sc.qkeys, sc.qkeys_n, n * stride));
-    GNS_TRY(grow_buf(&sc.qout, sc.qout_n, n));
+                         uint64_t *out, bool dev = false) {
+    if (!dev) {
+        GNS_TRY(grow_buf(&sc.qkeys, sc.qkeys_n, n * stride));
+        GNS_TRY(grow_buf(&sc.qout, sc.qout_n, n));
+    }
     QueryArgs a{};
-    a.keys = sc.qkeys; a.stride = stride; a.aligned = (stride % 4 == 0 && stride >= ((cm->K + 3) & ~3u));
+    a.keys = dev ? keys : sc.qkeys;
+    a.stride = stride;
+    a.aligned = (stride % 4 == 0 && stride >= ((cm->K + 3) & ~3u) && ((uintptr_t)a.keys & 3u) == 0);
     a.n = n; a.K = cm->K; a.g = cm->g; a.D = cm->D;
-    a.C = C; a.Fc = Fc; a.S = S; a.Fs = Fs; a.out = sc.qout;
-    hipError_t e = hipMemcpyAsync(sc.qkeys, keys, n * stride, hipMemcpyHostToDevice, st);
+    a.C = C; a.Fc = Fc; a.S = S; a.Fs = Fs; a.out = dev ? out : sc.qout;
+    hipError_t e = dev ? hipSuccess : hipMemcpyAsync(sc.qkeys, keys, n * stride, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_query, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(out, sc.qout, n * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && !dev) e = hipMemcpyAsync(out, sc.qout, n * 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) { set_error("query: %s", hipGetErrorString(e)); return GNS_E_HIP; }
     return GNS_OK;
@@ -4110,6 +4125,15 @@ int gns_cm_query(gns_cm *cm, const uint8_t *keys, uint32_t stride, uint64_t n, u
     if (stride < cm->K) { set_error("stride < key_bytes"); return GNS_E_ARG; }
     GNS_TRY(set_dev(cm));
     return cm_query_impl(cm, cm->stream, cm->rd, cm->C, cm->Fc, cm->S, cm->Fs, keys, stride, n, out);
+}
+
+int gns_cm_query_device(gns_cm *cm, const uint8_t *keys, uint32_t stride, uint64_t n, uint64_t *out) {
+    if (!cm || (n && (!keys || !out))) { set_error("null argument"); return GNS_E_ARG; }
+    if (n == 0) return GNS_OK;
+    if (stride < cm->K) { set_error("stride < key_bytes"); return GNS_E_ARG; }
+    if (((uintptr_t)out & 7u) != 0) { set_error("answers not 8-byte aligned"); return GNS_E_ARG; }
+    GNS_TRY(set_dev(cm));
+    return cm_query_impl(cm, cm->stream, cm->rd, cm->C, cm->Fc, cm->S, cm->Fs, keys, stride, n, out, true);
 }
 
 // ids -> key bytes on stream `st`: through the grow-only scratch when small
@@ -4194,6 +4218,28 @@ static int heavy_reserve(CmScratch &sc, uint64_t cells, uint64_t slots, uint32_t
     return GNS_OK;
 }
 
+// GNS_HH_TRACE=1: the heavy-hitter list's phases timed on stderr (each mark
+// synchronizes the stream first; diagnostics only, never on by default).
+struct HhTrace {
+    bool on;
+    hipStream_t st;
+    std::chrono::steady_clock::time_point t;
+    explicit HhTrace(hipStream_t s) : on(getenv("GNS_HH_TRACE") != nullptr), st(s), t(std::chrono::steady_clock::now()) {}
+    void mark(const char *what, uint64_t n) {
+        if (!on) return;
+        (void)hipStreamSynchronize(st);
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[hh] %-12s n=%-9llu %8.3f ms\n", what, (unsigned long long)n,
+                std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
+static int small_pin(CmScratch &sc) {
+    if (!sc.hsm) GNS_HIP(hipHostMalloc(reinterpret_cast<void **>(&sc.hsm), 64, hipHostMallocDefault));
+    return GNS_OK;
+}
+
 // One stable LSD radix pass over perm (n entries) by digit r: in -> out.
 static int rs_pass(CmScratch &sc, hipStream_t st, const uint32_t *in, uint32_t *out, uint32_t n, const RsDigit &r) {
     const uint32_t nblk = (n + kRsBlock - 1) / kRsBlock;
@@ -4240,14 +4286,19 @@ static int hh_sort(CmScratch &sc, hipStream_t st, const HhSrc &src, uint32_t n, 
         }
         return GNS_OK;
     };
+    HhTrace tr(st);
     GNS_TRY(sort_by(std::min<uint32_t>(K, 4)));
+    tr.mark("sort_primary", n);
     if (K > 4) {
-        uint32_t tflag = 0;
+        GNS_TRY(small_pin(sc));
         GNS_HIP(hipMemsetAsync(tie, 0, 4, st));
         hipLaunchKernelGGL(k_hh_ties, dim3(g), dim3(256), 0, st, p[cur], n, src, tie);
-        GNS_HIP(hipMemcpyAsync(&tflag, tie, 4, hipMemcpyDeviceToHost, st));
+        GNS_HIP(hipMemcpyAsync(sc.hsm + 4, tie, 4, hipMemcpyDeviceToHost, st));
         GNS_HIP(hipStreamSynchronize(st));
+        const uint32_t tflag = sc.hsm[4];
+        tr.mark(tflag ? "ties:yes" : "ties:no", n);
         if (tflag) GNS_TRY(sort_by(K));  // the whole key: bytes K-1..0, then the value
+        if (tflag) tr.mark("sort_full", n);
     }
     *perm_out = p[cur];
     return GNS_OK;
@@ -4255,24 +4306,38 @@ static int hh_sort(CmScratch &sc, hipStream_t st, const HhSrc &src, uint32_t n, 
 
 // rows_dev non-null: the ordered list as packed device rows [flow | u32 value] (capacity
 // *n_io rows), no host copy; else flows / vals on the host.
-static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_t *val, const uint32_t *fp,
-                        uint32_t thr, uint8_t *flows, uint32_t *vals, uint64_t *n_io, uint8_t *rows_dev = nullptr) {
-    const uint64_t cells = (uint64_t)cm->g.d * cm->g.w;
-    const uint32_t K = cm->K;
+// The list of one (value, fingerprint id) cell array of `cells` cells whose ids are
+// slots of dictionary D: Count-Min's count and size lists, and SuperSpread's list
+// (gns_ss.hip through gns::hh_heavy_list).
+static int heavy_list(CmScratch &sc, hipStream_t st, const DictDev &Dd, uint64_t dict_slots, uint32_t K,
+                      uint64_t cells, const uint32_t *val, const uint32_t *fp, uint32_t thr, uint8_t *flows,
+                      uint32_t *vals, uint64_t *n_io, uint8_t *rows_dev = nullptr) {
+    struct {
+        uint64_t dict_slots;
+        DictDev D;
+    } cmv{dict_slots, Dd}, *cm = &cmv;
+    HhTrace tr(st);
     GNS_TRY(heavy_reserve(sc, cells, cm->dict_slots, K, st));
+    GNS_TRY(small_pin(sc));
+    tr.mark("reserve", cells);
     // candidate buffer: grows to the number of cells at or above the threshold
     // (no cap: a low threshold can make every bucket a candidate, d*w < 2^32)
     uint32_t nc = 0;
     for (int pass = 0; pass < 2; pass++) {
-        hipError_t e = hipMemsetAsync(sc.ncand, 0, 8, st);
+        // [0] candidates, [1] unique, [2] bad-id flag: zeroed by a kernel on the list's stream
+        hipLaunchKernelGGL(k_fill_u32, dim3(1), dim3(64), 0, st, sc.ncand, (uint64_t)3, 0u);
+        hipError_t e = hipGetLastError();
         if (e == hipSuccess) {
             hipLaunchKernelGGL(k_hh_candidates, dim3((unsigned)((cells + 256 * kHhItems - 1) / (256 * kHhItems))), dim3(256), 0,
                                st, val, fp, cells, thr, sc.cand, sc.ncand, (uint32_t)sc.cap);
             e = hipGetLastError();
         }
-        if (e == hipSuccess) e = hipMemcpyAsync(&nc, sc.ncand, 4, hipMemcpyDeviceToHost, st);
+        tr.mark("cand_kernel", cells);
+        if (e == hipSuccess) e = hipMemcpyAsync(sc.hsm, sc.ncand, 4, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) { set_error("heavy: %s", hipGetErrorString(e)); return GNS_E_HIP; }
+        nc = sc.hsm[0];
+        tr.mark("candidates", nc);
         if (nc <= sc.cap) break;
         // more candidates than the buffer holds: grow to the count and run again
         dfree(sc.cand);
@@ -4290,13 +4355,20 @@ static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_
         GNS_TRY(heavy_flow_words(sc, cm->dict_slots, st, true));
         GNS_TRY(grow_buf(&sc.u32a, sc.u32a_n, nc));
         GNS_TRY(grow_buf(&sc.u32b, sc.u32b_n, nc + 1));
-        uint32_t *d_nu = sc.ncand + 1;
-        hipLaunchKernelGGL(k_hh_best, dim3(g), dim3(256), 0, st, cand, nc, sc.best, sc.hh_epoch);
-        hipLaunchKernelGGL(k_hh_emit, dim3(g), dim3(256), 0, st, cand, nc, sc.best, sc.mark, sc.hh_epoch, sc.u32a,
-                           sc.u32b, d_nu);
+        uint32_t *d_nu = sc.ncand + 1, *d_bad = sc.ncand + 2;
+        const uint64_t slots = cm->dict_slots;
+        hipLaunchKernelGGL(k_hh_best, dim3(g), dim3(256), 0, st, cand, nc, sc.best, sc.hh_epoch, slots, d_bad);
+        hipLaunchKernelGGL(k_hh_emit, dim3(g), dim3(256), 0, st, cand, nc, sc.best, sc.mark, sc.hh_epoch, slots,
+                           sc.u32a, sc.u32b, d_nu);
         GNS_HIP(hipGetLastError());
-        GNS_HIP(hipMemcpyAsync(&nu, d_nu, 4, hipMemcpyDeviceToHost, st));
+        GNS_HIP(hipMemcpyAsync(sc.hsm + 1, d_nu, 8, hipMemcpyDeviceToHost, st));
         GNS_HIP(hipStreamSynchronize(st));
+        nu = sc.hsm[1];
+        if (sc.hsm[2]) {
+            set_error("heavy hitters: a bucket fingerprint names no dictionary slot (corrupt state)");
+            return GNS_E_HIP;
+        }
+        tr.mark("dedupe", nu);
     }
     const uint64_t capn = *n_io;
     *n_io = nu;
@@ -4306,10 +4378,13 @@ static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_
         GNS_TRY(grow_buf(&sc.bytes, sc.bytes_n, (uint64_t)nu * Kb));
         GNS_TRY(grow_buf(&sc.obytes, sc.obytes_n, (uint64_t)nu * Kb));
         GNS_TRY(grow_buf(&sc.u32d, sc.u32d_n, (uint64_t)nu));
+        tr.mark("grow", nu);
         if (K) hipLaunchKernelGGL(k_ids_to_bytes, dim3(g), dim3(256), 0, st, sc.u32a, (uint64_t)nu, cm->D, sc.bytes);
+        tr.mark("ids_to_bytes", nu);
         const HhSrc src{sc.u32b, sc.bytes, K, K};
         uint32_t *perm = nullptr;
         GNS_TRY(hh_sort(sc, st, src, nu, &perm));
+        tr.mark("sorted", nu);
         if (rows_dev) {
             if (nu <= capn) {
                 hipLaunchKernelGGL(k_hh_gather, dim3(g), dim3(256), 0, st, perm, src, nu, nullptr, nullptr, rows_dev);
@@ -4332,11 +4407,37 @@ static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_
         if (fb) GNS_HIP(hipMemcpyAsync(sc.hpin, sc.obytes, fb, hipMemcpyDeviceToHost, st));
         if (vb) GNS_HIP(hipMemcpyAsync(sc.hpin + fb, sc.u32d, vb, hipMemcpyDeviceToHost, st));
         GNS_HIP(hipStreamSynchronize(st));
+        tr.mark("gather_d2h", m);
         if (fb) memcpy(flows, sc.hpin, fb);
         if (vb) memcpy(vals, sc.hpin + fb, vb);
+        tr.mark("host_copy", m);
     }
     return GNS_OK;
 }
+
+static int cm_heavy_one(gns_cm *cm, hipStream_t st, CmScratch &sc, const uint32_t *val, const uint32_t *fp,
+                        uint32_t thr, uint8_t *flows, uint32_t *vals, uint64_t *n_io, uint8_t *rows_dev = nullptr) {
+    return heavy_list(sc, st, cm->D, cm->dict_slots, cm->K, (uint64_t)cm->g.d * cm->g.w, val, fp, thr, flows, vals,
+                      n_io, rows_dev);
+}
+
+}  // extern "C"
+
+namespace gns {
+CmScratch *hh_scratch_new() { return new CmScratch(); }
+void hh_scratch_free(CmScratch *sc) {
+    if (!sc) return;
+    sc->free_all();
+    delete sc;
+}
+int hh_heavy_list(CmScratch *sc, hipStream_t st, const DictDev &D, uint64_t dict_slots, uint32_t K, uint64_t cells,
+                  const uint32_t *val, const uint32_t *fp, uint32_t thr, uint8_t *flows, uint32_t *vals,
+                  uint64_t *n_io) {
+    return heavy_list(*sc, st, D, dict_slots, K, cells, val, fp, thr, flows, vals, n_io);
+}
+}  // namespace gns
+
+extern "C" {
 
 int gns_cm_heavy_hitters(gns_cm *cm, uint8_t *count_flows, uint32_t *counts, uint64_t *n_count,
                          uint8_t *size_flows, uint32_t *sizes, uint64_t *n_size) {

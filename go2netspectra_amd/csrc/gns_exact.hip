@@ -1483,28 +1483,44 @@ int gns_ex_flush(gns_ex *ex) {
     return GNS_OK;
 }
 
-int gns_ex_query(gns_ex *ex, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out) {
+static int ex_query_impl(gns_ex *ex, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out, bool dev) {
     if (!ex || (n && (!flows || !out))) { set_error("null argument"); return GNS_E_ARG; }
     if (n == 0) return GNS_OK;
     if (stride < ex->K) { set_error("stride < key bytes"); return GNS_E_ARG; }
+    if (dev && ((uintptr_t)out & 7u) != 0) { set_error("answers not 8-byte aligned"); return GNS_E_ARG; }
     GNS_TRY(ex_set_dev(ex));
     uint8_t *dk = nullptr;
     uint64_t *dout = nullptr;
-    GNS_TRY(dalloc(reinterpret_cast<void **>(&dk), n * stride));
-    int rc = dalloc(reinterpret_cast<void **>(&dout), n * 8);
-    if (rc) { dfree(dk); return rc; }
-    hipError_t e = hipMemcpyAsync(dk, flows, n * stride, hipMemcpyHostToDevice, ex->stream);
+    if (dev) {
+        dk = const_cast<uint8_t *>(flows);
+        dout = out;
+    } else {
+        GNS_TRY(dalloc(reinterpret_cast<void **>(&dk), n * stride));
+        int rc = dalloc(reinterpret_cast<void **>(&dout), n * 8);
+        if (rc) { dfree(dk); return rc; }
+    }
+    hipError_t e = dev ? hipSuccess : hipMemcpyAsync(dk, flows, n * stride, hipMemcpyHostToDevice, ex->stream);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_ex_query, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ex->stream, dk, stride, n,
                            ex->K, ex->D, ex->f, dout);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, ex->stream);
+    if (e == hipSuccess && !dev) e = hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, ex->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ex->stream);
-    dfree(dk);
-    dfree(dout);
+    if (!dev) {
+        dfree(dk);
+        dfree(dout);
+    }
     if (e != hipSuccess) { set_error("exact query: %s", hipGetErrorString(e)); return GNS_E_HIP; }
     return GNS_OK;
+}
+
+int gns_ex_query(gns_ex *ex, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out) {
+    return ex_query_impl(ex, flows, stride, n, out, false);
+}
+
+int gns_ex_query_device(gns_ex *ex, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out) {
+    return ex_query_impl(ex, flows, stride, n, out, true);
 }
 
 int gns_ex_snapshot(gns_ex *ex, uint8_t *keys, int64_t *start_ns, int64_t *end_ns, uint64_t *pkts,

@@ -473,8 +473,8 @@ int gns_route_owner_keys(gns_route *r, const gns_layout *key_layout, const uint8
             set_error("the key layout lacks owner field %u: its flows are not owned by one shard", r->own_layout.fields[i]);
             return GNS_E_ARG;
         }
+    if (n == 0) return GNS_OK;  // nothing to route (any stride)
     if (stride < kp.K) { set_error("stride %u below the key's %u bytes", stride, kp.K); return GNS_E_ARG; }
-    if (n == 0) return GNS_OK;
     if (n >= (1ull << 32)) { set_error("%llu keys (max 2^32 - 1)", (unsigned long long)n); return GNS_E_RANGE; }
     RouteKeysArgs a{};
     for (int t = 0; t < 40; t++) a.inv[t] = 255;
@@ -485,7 +485,8 @@ int gns_route_owner_keys(gns_route *r, const gns_layout *key_layout, const uint8
     hipStream_t st = r->stream;
     GNS_HIP(hipStreamWaitEvent(st, r->done, 0));
     if (where == GNS_MEM_HOST) {
-        const uint64_t need = n * stride + n * 4;
+        const uint64_t own_off = (n * stride + 15) & ~15ull;  // owners 16-byte aligned after odd-width keys
+        const uint64_t need = own_off + n * 4;
         if (r->kbuf_n < need) {
             GNS_HIP(hipStreamSynchronize(st));
             dfree(r->kbuf); r->kbuf = nullptr; r->kbuf_n = 0;
@@ -494,7 +495,7 @@ int gns_route_owner_keys(gns_route *r, const gns_layout *key_layout, const uint8
         }
         GNS_HIP(hipMemcpyAsync(r->kbuf, keys, n * stride, hipMemcpyHostToDevice, st));
         a.keys = r->kbuf;
-        a.owner = reinterpret_cast<uint32_t *>(r->kbuf + n * stride);
+        a.owner = reinterpret_cast<uint32_t *>(r->kbuf + own_off);
     } else {
         a.keys = keys;
         a.owner = owner;

@@ -28,6 +28,7 @@
 #include "gns_common.hpp"
 #include "gns_ctl.cuh"
 #include "gns_gomath.cuh"
+#include "gns_hh.hpp"
 #include "gns_scan.cuh"
 
 namespace gns {
@@ -1356,6 +1357,7 @@ struct gns_ss {
     uint8_t *stage = nullptr;
     size_t stage_bytes = 0;
     StageTimer timer;
+    CmScratch *hh = nullptr;     // HeavyHitters' device list buffers (gns_hh.hpp), made on first use
 };
 
 namespace {
@@ -1373,6 +1375,8 @@ void ss_free_all(gns_ss *ss) {
     dfree(ss->cval); dfree(ss->sval); dfree(ss->shist); dfree(ss->spart); dfree(ss->sorder);
     dfree(ss->counts); dfree(ss->heads); dfree(ss->hlen); dfree(ss->sprof); dfree(ss->cblk); dfree(ss->stats); dfree(ss->stage);
     dfree(ss->dctl); dfree(ss->stats_bak); ss->dsc.free_all();
+    gns::hh_scratch_free(ss->hh);
+    ss->hh = nullptr;
     if (ss->h_pin) (void)hipHostFree(ss->h_pin);
     ss->timer.destroy();
     if (ss->stream) (void)hipStreamDestroy(ss->stream);
@@ -1923,28 +1927,44 @@ int gns_ss_flush(gns_ss *ss) {
     return GNS_OK;
 }
 
-int gns_ss_query(gns_ss *ss, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out) {
+static int ss_query_impl(gns_ss *ss, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out, bool dev) {
     if (!ss || (n && (!flows || !out))) { set_error("null argument"); return GNS_E_ARG; }
     if (n == 0) return GNS_OK;
     if (stride < ss->g.Kf) { set_error("stride < flow_bytes"); return GNS_E_ARG; }
+    if (dev && ((uintptr_t)out & 7u) != 0) { set_error("answers not 8-byte aligned"); return GNS_E_ARG; }
     GNS_TRY(ss_set_dev(ss));
     uint8_t *dk = nullptr;
     uint64_t *dout = nullptr;
-    GNS_TRY(dalloc(reinterpret_cast<void **>(&dk), n * stride));
-    int rc = dalloc(reinterpret_cast<void **>(&dout), n * 8);
-    if (rc) { dfree(dk); return rc; }
+    if (dev) {
+        dk = const_cast<uint8_t *>(flows);
+        dout = out;
+    } else {
+        GNS_TRY(dalloc(reinterpret_cast<void **>(&dk), n * stride));
+        int rc = dalloc(reinterpret_cast<void **>(&dout), n * 8);
+        if (rc) { dfree(dk); return rc; }
+    }
     SsQueryArgs a{dk, stride, n, ss->g, ss->D, ss->values, ss->keys, dout};
-    hipError_t e = hipMemcpyAsync(dk, flows, n * stride, hipMemcpyHostToDevice, ss->stream);
+    hipError_t e = dev ? hipSuccess : hipMemcpyAsync(dk, flows, n * stride, hipMemcpyHostToDevice, ss->stream);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_ss_query, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ss->stream, a);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, ss->stream);
+    if (e == hipSuccess && !dev) e = hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, ss->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ss->stream);
-    dfree(dk);
-    dfree(dout);
+    if (!dev) {
+        dfree(dk);
+        dfree(dout);
+    }
     if (e != hipSuccess) { set_error("ss query: %s", hipGetErrorString(e)); return GNS_E_HIP; }
     return GNS_OK;
+}
+
+int gns_ss_query(gns_ss *ss, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out) {
+    return ss_query_impl(ss, flows, stride, n, out, false);
+}
+
+int gns_ss_query_device(gns_ss *ss, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out) {
+    return ss_query_impl(ss, flows, stride, n, out, true);
 }
 
 static int ss_ids_to_bytes(gns_ss *ss, const std::vector<uint32_t> &ids, std::vector<uint8_t> &bytes) {
@@ -1970,61 +1990,21 @@ static int ss_ids_to_bytes(gns_ss *ss, const std::vector<uint32_t> &ids, std::ve
     return GNS_OK;
 }
 
-static uint32_t mm3_host_bytes(const uint8_t *d, uint32_t len, uint32_t seed) {
-    uint32_t kw[GNS_KWMAX] = {0};
-    for (uint32_t j = 0; j < len; j++) kw[j / 4] |= (uint32_t)d[j] << (8 * (j % 4));
-    uint32_t h = seed;
-    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
-    auto rotl = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
-    const uint32_t nb = len / 4;
-    for (uint32_t i = 0; i < nb; i++) {
-        uint32_t k = kw[i] * c1; k = rotl(k, 15); k *= c2;
-        h ^= k; h = rotl(h, 13); h = h * 5 + 0xe6546b64u;
-    }
-    if (len & 3) { uint32_t k = kw[nb] * c1; k = rotl(k, 15); k *= c2; h ^= k; }
-    h ^= len;
-    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
-    return h;
-}
-
-// HeavyHitters (super_spread.go:254-294): every flow holding a counter > 0 is
-// re-queried; ties ordered by flow bytes (Go sorts with sort.Slice, unstable).
+// HeavyHitters (super_spread.go:254-294) on the device.  The reference collects
+// every flow holding a counter > 0, re-queries it (the max over the cells holding
+// it) and keeps estimates >= threshold: a flow clears the threshold iff one of its
+// cells does, so this is Count-Min's list computation over (values, keys) with
+// the threshold (gns::hh_heavy_list: candidates >= thr, per-flow max, radix
+// order).  Order: estimate desc, ties by flow bytes asc (Go's sort.Slice leaves
+// them unordered).  Nothing but the list leaves the device.
 int gns_ss_heavy_hitters(gns_ss *ss, uint8_t *flows, uint32_t *spreads, uint64_t *n_io) {
     if (!ss || !n_io) { set_error("null argument"); return GNS_E_ARG; }
     GNS_TRY(ss_set_dev(ss));
     GNS_HIP(hipStreamSynchronize(ss->stream));
+    if (!ss->hh) ss->hh = gns::hh_scratch_new();
     const uint64_t cells = (uint64_t)ss->g.d * ss->g.w;
-    std::vector<uint32_t> vals(cells), ids(cells);
-    GNS_HIP(hipMemcpy(vals.data(), ss->values, cells * 4, hipMemcpyDeviceToHost));
-    GNS_HIP(hipMemcpy(ids.data(), ss->keys, cells * 4, hipMemcpyDeviceToHost));
-    std::vector<uint32_t> uniq;
-    for (uint64_t c = 0; c < cells; c++) if (vals[c] > 0) uniq.push_back(ids[c]);
-    std::sort(uniq.begin(), uniq.end());
-    uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
-    std::vector<uint8_t> kb;
-    GNS_TRY(ss_ids_to_bytes(ss, uniq, kb));
-    const uint32_t K = ss->g.Kf;
-    std::vector<std::pair<uint32_t, uint32_t>> res;  // (estimate, index)
-    for (size_t i = 0; i < uniq.size(); i++) {
-        uint32_t est = 0;
-        for (uint32_t r = 0; r < ss->g.d; r++) {
-            const uint32_t h = mm3_host_bytes(&kb[i * K], K, ss->g.seeds[r]);
-            const uint64_t c = (uint64_t)r * ss->g.w + (ss->g.pow2 ? (h & ss->g.wmask) : (h % ss->g.w));
-            if (ids[c] == uniq[i] && vals[c] > est) est = vals[c];
-        }
-        if (est >= ss->thr) res.push_back({est, (uint32_t)i});
-    }
-    std::sort(res.begin(), res.end(), [&](const std::pair<uint32_t, uint32_t> &x, const std::pair<uint32_t, uint32_t> &y) {
-        if (x.first != y.first) return x.first > y.first;
-        return memcmp(&kb[(size_t)x.second * K], &kb[(size_t)y.second * K], K) < 0;
-    });
-    const uint64_t cap = *n_io;
-    for (size_t i = 0; i < res.size() && i < cap; i++) {
-        if (flows && K) memcpy(flows + i * K, &kb[(size_t)res[i].second * K], K);
-        if (spreads) spreads[i] = res[i].first;
-    }
-    *n_io = res.size();
-    return GNS_OK;
+    return gns::hh_heavy_list(ss->hh, ss->stream, ss->D, ss->dict_slots, ss->g.Kf, cells, ss->values, ss->keys,
+                              ss->thr, flows, spreads, n_io);
 }
 
 int gns_ss_reset(gns_ss *ss) {

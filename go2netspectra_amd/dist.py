@@ -181,8 +181,10 @@ class Router:
         if hasattr(keys, "data_ptr") and getattr(keys, "is_cuda", False):
             import torch
             n = int(keys.shape[0])
-            keys = keys.reshape(n, -1).contiguous()
             out = torch.empty((n,), dtype=torch.int32, device=keys.device)
+            if n == 0:
+                return out
+            keys = keys.reshape(n, -1).contiguous()
             _lib.device_ready(keys)
             _lib.check(self._L.gns_route_owner_keys(self._h, ct.byref(lay), keys.data_ptr(), int(keys.shape[1]) if n else 1,
                                                     n, out.data_ptr(), _lib.MEM_DEVICE))
@@ -318,6 +320,9 @@ def routed_query(query_many, keys, key_fields, world: int, owner=("SrcIP",), rou
     one, the host restatement owner_of_keys does."""
     import torch
     import torch.distributed as dist
+    from . import _lib
+    if dist.get_backend() == "nccl" or _lib.is_device(keys):
+        return _routed_query_device(query_many, keys, key_fields, world, owner, router)
     keys = np.ascontiguousarray(keys, np.uint8)
     n = keys.shape[0]
     K = max(sum(_FIELD_SIZE.get(f, 0) for f in key_fields), 1)
@@ -342,6 +347,45 @@ def routed_query(query_many, keys, key_fields, world: int, owner=("SrcIP",), rou
     out = np.empty(n, np.uint64)
     out[order] = back.cpu().numpy().view(np.uint64)
     return out
+
+
+def _routed_query_device(query_many, keys, key_fields, world: int, owner, router):
+    """routed_query under RCCL: keys, owners, the permutation and the answers stay on
+    the GPU.  Owners from the Router's device kernel (gns_route_owner_keys), a stable
+    device argsort by owner, the two all-to-alls on device tensors and the owner's
+    query_many on the keys it received (gns_*_query_device); the only host read is
+    the split sizes the all-to-all needs.  Host keys are copied up once and the
+    answers come back as numpy; device keys give a device int64 tensor (uint64 bits)."""
+    import torch
+    import torch.distributed as dist
+    from . import _lib
+    dev = torch.device("cuda", torch.cuda.current_device())
+    host_in = not _lib.is_device(keys)
+    K = max(sum(_FIELD_SIZE.get(f, 0) for f in key_fields), 1)
+    if host_in:
+        keys = torch.from_numpy(np.ascontiguousarray(keys, np.uint8).reshape(-1, K)).to(dev)
+    n = int(keys.shape[0])
+    keys = keys.reshape(n, -1) if n else keys.reshape(0, K)
+    K = int(keys.shape[1])
+    if router is None:
+        router = Router(world, dev.index, owner)
+    own = router.owner_of_keys(keys, key_fields).to(torch.int64)
+    order = torch.argsort(own, stable=True)
+    sc = torch.bincount(own, minlength=world)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc)
+    both = torch.cat([sc, rc]).cpu().tolist()  # the split sizes: the one host read
+    scl, rcl = [int(x) for x in both[:world]], [int(x) for x in both[world:]]
+    in_keys = torch.empty((sum(rcl), K), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(in_keys, keys.index_select(0, order), output_split_sizes=rcl, input_split_sizes=scl)
+    ans = query_many(in_keys)
+    if not torch.is_tensor(ans):  # a host-only query_many (e.g. a snapshot view)
+        ans = torch.from_numpy(np.ascontiguousarray(np.asarray(ans, np.uint64)).view(np.int64)).to(dev)
+    back = torch.empty((n,), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(back, ans.to(torch.int64), output_split_sizes=scl, input_split_sizes=rcl)
+    out = torch.empty_like(back)
+    out[order] = back
+    return out.cpu().numpy().view(np.uint64) if host_in else out
 
 
 def _pack(items, K: int) -> np.ndarray:

@@ -112,6 +112,9 @@ class ExactAggregator:
         check(self._L.gns_ex_flush(self._h))
 
     def query_many(self, flows) -> np.ndarray:
+        """PacketCount<<32 | ByteCount for n flows; a device tensor in -> a device int64 tensor out."""
+        if _lib.is_device(flows):
+            return _lib.query_device(self._L.gns_ex_query_device, self._h, flows)
         flows = np.ascontiguousarray(flows, np.uint8)
         n = flows.shape[0]
         out = np.zeros(n, np.uint64)

@@ -258,6 +258,11 @@ class CountMin:
         self.insert_keys(k, np.array([size], dtype=np.uint32))
 
     def query_many(self, keys) -> np.ndarray:
+        """Query for n keys [n, K] -> count<<32 | size each.  Host keys give a numpy
+        uint64 array; a device tensor gives a device int64 tensor (the uint64 bits),
+        answered without leaving the GPU (gns_cm_query_device)."""
+        if _lib.is_device(keys):
+            return _lib.query_device(self._L.gns_cm_query_device, self._h, keys)
         keys = _host(keys, np.uint8)
         n = keys.shape[0]
         out = np.zeros(n, dtype=np.uint64)
@@ -442,6 +447,9 @@ class SuperSpread:
                          np.frombuffer(bytes(elem), np.uint8).reshape(1, -1))
 
     def query_many(self, flows) -> np.ndarray:
+        """max(1, estimate) for n flows; a device tensor in -> a device int64 tensor out."""
+        if _lib.is_device(flows):
+            return _lib.query_device(self._L.gns_ss_query_device, self._h, flows)
         flows = _host(flows, np.uint8)
         n = flows.shape[0]
         out = np.zeros(n, dtype=np.uint64)
@@ -456,16 +464,26 @@ class SuperSpread:
             return 1
         return int(self.query_many(np.frombuffer(bytes(flow), np.uint8).reshape(1, -1))[0])
 
-    def heavy_hitters(self) -> HeavyRecord:
-        n = ct.c_uint64(0)
-        check(self._L.gns_ss_heavy_hitters(self._h, None, None, ct.byref(n)))
+    def heavy_hitters_arrays(self):
+        """HeavyHitters as arrays (flows [n, flow_bytes], spreads): one device call into
+        buffers sized from the previous list (a longer list is fetched again)."""
         K = max(self.flow_bytes, 1)
-        f = np.zeros((max(n.value, 1), K), np.uint8)
-        v = np.zeros(max(n.value, 1), np.uint32)
-        n2 = ct.c_uint64(n.value)
-        check(self._L.gns_ss_heavy_hitters(self._h, f.ctypes.data, v.ctypes.data, ct.byref(n2)))
-        return HeavyRecord(Size=None, Count=[HeavyCount(bytes(f[i, : self.flow_bytes]), int(v[i]))
-                                             for i in range(min(n.value, n2.value))])
+        hint = getattr(self, "_hh_cap", 0)
+        while True:
+            cap = max(hint, 1)
+            f = np.empty((cap, K), np.uint8)
+            v = np.empty(cap, np.uint32)
+            n = ct.c_uint64(cap)
+            check(self._L.gns_ss_heavy_hitters(self._h, f.ctypes.data, v.ctypes.data, ct.byref(n)))
+            if n.value <= cap:
+                self._hh_cap = 2 * n.value + 64
+                return f[: n.value, : self.flow_bytes], v[: n.value]
+            hint = n.value
+
+    def heavy_hitters(self) -> HeavyRecord:
+        """HeavyHitters (super_spread.go:254-294): Count = (flow, spread estimate), Size = None."""
+        f, v = self.heavy_hitters_arrays()
+        return HeavyRecord(Size=None, Count=[HeavyCount(bytes(f[i]), int(v[i])) for i in range(len(v))])
 
     def reset(self) -> None:
         check(self._L.gns_ss_reset(self._h))

@@ -158,6 +158,10 @@ int gns_cm_insert_compact(gns_cm *cm, const uint8_t *rec16, const uint32_t *wire
 int gns_cm_flush(gns_cm *cm);
 /* out[i] = count<<32 | size, count_min.go:160-174 */
 int gns_cm_query(gns_cm *cm, const uint8_t *keys, uint32_t stride, uint64_t n, uint64_t *out);
+/* gns_cm_query with keys and out in DEVICE memory of the handle's GPU (out 8-byte
+ * aligned): the owner-routed query path keeps keys and answers on the GPU between
+ * its all-to-alls.  The keys must be complete when called; returns once out is written. */
+int gns_cm_query_device(gns_cm *cm, const uint8_t *keys, uint32_t stride, uint64_t n, uint64_t *out);
 /* HeavyHitters, count_min.go:178-247.  Lists are sorted value-descending with
  * ties broken by flow bytes ascending (the reference leaves ties unordered).
  * On input *n_count / *n_size hold the capacities (entries); on output the
@@ -260,6 +264,8 @@ int gns_ss_insert_headers(gns_ss *ss, const uint8_t *hdr, const uint32_t *wirele
                           gns_mem where);
 int gns_ss_flush(gns_ss *ss);
 int gns_ss_query(gns_ss *ss, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out);
+/* device keys / answers, as gns_cm_query_device */
+int gns_ss_query_device(gns_ss *ss, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out);
 int gns_ss_heavy_hitters(gns_ss *ss, uint8_t *flows, uint32_t *spreads, uint64_t *n);
 int gns_ss_reset(gns_ss *ss);
 /* values[d*w], keys[d*w*flow_bytes], regs[d*w*m] (u8), pbits[d*w] */
@@ -441,6 +447,8 @@ int gns_ex_flush(gns_ex *ex);
 /* out[i] = PacketCount << 32 | ByteCount (task.go:323); IP fields of the
  * encoded flow are read as 16-byte net.IPs, as the reference does; 0 if absent */
 int gns_ex_query(gns_ex *ex, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out);
+/* device keys / answers, as gns_cm_query_device */
+int gns_ex_query_device(gns_ex *ex, const uint8_t *flows, uint32_t stride, uint64_t n, uint64_t *out);
 /* Snapshot: *n_io = capacity in, number of flows out.  keys[n*key_bytes] in the
  * canonical 16-byte-IP layout; start/end = first/last packet timestamps
  * (stream order), pkts/bytes = PacketCount/ByteCount.  Any pointer may be NULL. */

@@ -32,11 +32,18 @@ def main():
     h = hdr[:2000].cpu().numpy()
     qk = np.ascontiguousarray(np.concatenate([h[:, 36:38], h[:, 23:24]], axis=1))
     ans = routed_query(cm.query_many, qk, fields, 1, router=router)
+    # device keys: owners, permutation, all-to-alls and answers stay on the GPU
+    ans_dev = routed_query(cm.query_many, torch.from_numpy(qk).cuda(), fields, 1, router=router)
+    assert ans_dev.is_cuda and ans_dev.dtype == torch.int64
+    ans_dev = ans_dev.cpu().numpy().view(np.uint64)
+    empty = routed_query(cm.query_many, torch.from_numpy(qk[:0]).cuda(), fields, 1, router=router)
+    assert empty.is_cuda and empty.shape == (0,)
+    dq = cm.query_many(torch.from_numpy(qk).cuda()).cpu().numpy().view(np.uint64)  # gns_cm_query_device
     rows = allgather_heavy_rows(cm, 1)
     arrs = allgather_heavy_arrays(cm.heavy_hitters_arrays(), 1)
     C, S, Fc, Fs = cm.export_state()
     np.savez(os.path.join(out, "nccl.npz"), ih=ih.cpu().numpy(), iw=iw.cpu().numpy(), C=C, S=S, Fc=Fc, Fs=Fs,
-             qk=qk, ans=ans, rc=rows[0], rcv=rows[1], rs=rows[2], rsv=rows[3], ac=arrs[0], acv=arrs[1], as_=arrs[2],
+             qk=qk, ans=ans, ans_dev=ans_dev, dq=dq, rc=rows[0], rcv=rows[1], rs=rows[2], rsv=rows[3], ac=arrs[0], acv=arrs[1], as_=arrs[2],
              asv=arrs[3])
     dist.barrier()
     dist.destroy_process_group()

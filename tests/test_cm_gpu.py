@@ -92,6 +92,11 @@ def test_query_and_heavy_hitters(gpu, oracle):
     q = cm.query_many(flows[:5000])
     want = np.array([orc.query(bytes(f)) for f in flows[:5000]], dtype=np.uint64)
     assert np.array_equal(q, want)
+    import torch  # device keys in, device answers out (gns_cm_query_device); a strided view of the keys
+    k17 = np.zeros((5000, 17), np.uint8)
+    k17[:, :16] = flows[:5000]
+    qd = cm.query_many(torch.from_numpy(k17).cuda()[:, :16])
+    assert qd.is_cuda and np.array_equal(qd.cpu().numpy().view(np.uint64), want)
     absent = rng.integers(0, 256, (100, 16), dtype=np.uint8)
     assert np.array_equal(cm.query_many(absent), np.array([orc.query(bytes(f)) for f in absent], np.uint64))
     hh = cm.heavy_hitters()

@@ -1,4 +1,4 @@
-"""CPU, world_size 2 over gloo: the multi-GPU path's sharding + per-window
+"""CPU, world_size 2..8 over gloo: the multi-GPU path's sharding + per-window
 heavy-hitter all-gather.  Each rank runs an exact sketch of its flow shard
 (the C oracle stands in for the GPU engine here) and the merged heavy-hitter
 list must equal the union of the per-shard lists computed in one process."""
@@ -66,12 +66,13 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_shard_and_allgather():
+@pytest.mark.parametrize("world", [2, 8])
+def test_shard_and_allgather(world):
+    """world 8 = the node the driver's scaling run uses (8 x MI355X)."""
     import sys
     sys.path.insert(0, ROOT)
     from go2netspectra_amd.dist import merge_heavy
     from go2netspectra_amd.packets import PacketBatch
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -187,7 +188,7 @@ def _route_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_route_exchange_delivers_the_stable_filter(world):
     import sys
     sys.path.insert(0, ROOT)
@@ -374,7 +375,7 @@ def _exchange_rows(rows, counts, world):
     return out, rc
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 @pytest.mark.parametrize("layout", sorted(KEYED_LAYOUTS))
 def test_keyed_sharding_and_routed_queries(world, layout):
     import sys

@@ -106,6 +106,9 @@ def test_query(gpu, oracle):
         got = task.agg.query_many(q)
         want = np.array([orc.query(bytes(k)) for k in q], np.uint64)
         assert np.array_equal(got, want)
+        import torch  # device keys in, device answers out (gns_ex_query_device)
+        gd = task.agg.query_many(torch.from_numpy(np.ascontiguousarray(q)).cuda())
+        assert gd.is_cuda and np.array_equal(gd.cpu().numpy().view(np.uint64), want)
     assert (task.agg.query_many(mapped[v4]) > 0).all()
     assert task.query(bytes(mapped[0])) == orc.query(bytes(mapped[0]))
 

@@ -34,6 +34,7 @@ def test_nccl_world_of_one(gpu, oracle, tmp_path):
         assert np.array_equal(a, b)
     want = np.array([orc.query(bytes(k)) for k in z["qk"]], np.uint64)
     assert np.array_equal(z["ans"], want)
+    assert np.array_equal(z["ans_dev"], want) and np.array_equal(z["dq"], want)
     fc, vc = orc.heavy_arrays("count")
     fs, vs = orc.heavy_arrays("size")
     for f, v, pre in ((fc, vc, "c"), (fs, vs, "s")):

@@ -63,6 +63,8 @@ def test_insert_keys_parity(gpu, oracle, w, d, m, size, Kf, Ke, nflows, n, batch
     ss.flush()
     orc.insert(fl, el)
     assert_same_ss(ss, orc)
+    # HeavyHitters on the device (gns_hh.hpp) vs the oracle's re-query loop
+    assert_same_list([(h.Flow, h.Count) for h in ss.heavy_hitters().Count], orc.heavy())
 
 
 def test_superspreaders_and_queries(gpu, oracle):
@@ -79,6 +81,9 @@ def test_superspreaders_and_queries(gpu, oracle):
     q = ss.query_many(flows[:3000])
     want = np.array([orc.query(bytes(f)) for f in flows[:3000]], np.uint64)
     assert np.array_equal(q, want)
+    import torch  # device keys in, device answers out (gns_ss_query_device)
+    qd = ss.query_many(torch.from_numpy(np.ascontiguousarray(flows[:3000])).cuda())
+    assert qd.is_cuda and np.array_equal(qd.cpu().numpy().view(np.uint64), want)
     absent = rng.integers(0, 256, (50, 16), dtype=np.uint8)
     assert np.array_equal(ss.query_many(absent), np.ones(50, np.uint64))
     hh = ss.heavy_hitters()
@@ -256,6 +261,31 @@ def test_bench_geometry_one_large_batch(gpu, oracle):
     ss.flush()
     orc.insert(fl, el)
     assert_same_ss(ss, orc)
+    assert_same_list([(h.Flow, h.Count) for h in ss.heavy_hitters().Count], orc.heavy())
+
+
+def test_heavy_hitters_device_large_geometry(gpu, oracle):
+    """SuperSpread HeavyHitters (super_spread.go:254-294) on the device at d=4 w=2^20
+    with a threshold of 1, so every owner with a positive counter is listed (~10^5
+    flows), and half the flows share their first four key bytes, so equal estimates
+    tie on the radix sort's primary key and the whole-key order decides (canonical:
+    estimate desc, flow bytes asc).  Listed twice: the second call reuses the buffers."""
+    rng = np.random.default_rng(4242)
+    n, nflows = 1_500_000, 150_000
+    ss, orc = make_pair(oracle, 1 << 20, 4, 32, 5, 16, 16, thr=1, batch_packets=1 << 19)
+    _, el, flows = spread_stream(rng, n, nflows, 16, 16, s=1.05, elem_pool=1 << 20)
+    flows[rng.random(nflows) < 0.5, :4] = (10, 0, 0, 1)
+    fl = np.ascontiguousarray(flows[zipf_index(rng, n, nflows, 1.05)])
+    ss.insert_keys(fl, el)
+    ss.flush()
+    orc.insert(fl, el)
+    want = orc.heavy()
+    assert len(want) > 50_000
+    for _ in range(2):
+        got = [(h.Flow, h.Count) for h in ss.heavy_hitters().Count]
+        assert_same_list(got, want)
+    ties = sum(1 for a, b in zip(want, want[1:]) if a[1] == b[1] and a[0][:4] == b[0][:4])
+    assert ties > 0  # the whole-key order was exercised
 
 
 def test_tiny_dictionary_grows_and_reset_restarts(gpu, oracle):
