@@ -689,6 +689,7 @@ def bench_windows(args, torch, dist, world, cm, timed_step, n):
     from go2netspectra_amd.dist import allgather_heavy_arrays, allgather_heavy_rows
     device_rows = world > 1 and dist.get_backend() == "nccl"  # RCCL: the lists never leave the GPUs
     t_ins = t_hh = t_x = 0.0
+    per_hh = []
     if device_rows:  # warm: the read side's buffers, the sort's scratch
         allgather_heavy_rows(cm, world)
     else:
@@ -714,6 +715,7 @@ def bench_windows(args, torch, dist, world, cm, timed_step, n):
         e = time.perf_counter()
         t_hh += c - b
         t_x += e - c
+        per_hh.append(round((c - b) * 1e3, 3))
     el = t_ins + t_hh + t_x
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
@@ -724,6 +726,7 @@ def bench_windows(args, torch, dist, world, cm, timed_step, n):
             "value": round(n * args.window_steps * W * world / el / 1e6, 2), "unit": "Mpackets/s",
             "ms_per_window": round(el / W * 1e3, 3), "insert_ms": round(t_ins / W * 1e3, 3),
             "heavy_hitters_ms": round(t_hh / W * 1e3, 3), "exchange_ms": round(t_x / W * 1e3, 3),
+            "heavy_hitters_ms_per_window": per_hh, "heavy_hitters_ms_median": float(np.median(per_hh)),
             "global_heavy_hitters": {"count": int(len(arrs[1])), "size": int(len(arrs[3]))},
             "collective": ("all-gather of packed (flow | value) rows, " + dist.get_backend()
                            + (", lists kept on the GPUs, merged by the device sort" if device_rows else ""))
@@ -751,7 +754,7 @@ def main():
                     help="flow dictionary capacity (slots = next power of two >= 2x)")
     ap.add_argument("--ex-max-flows", type=int, default=1 << 21,
                     help="exact aggregator flow dictionary capacity (--sketch exact / hybrid)")
-    ap.add_argument("--windows", type=int, default=1,
+    ap.add_argument("--windows", type=int, default=3,
                     help="after the timed steps: W timed windows of insert + device heavy hitters + "
                          "all-gather of every shard's list (configs[3] per-window exchange); 0 = off")
     ap.add_argument("--window-steps", type=int, default=10,

@@ -25,6 +25,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <mutex>
+#include <sys/resource.h>
 #include <vector>
 
 #include "gns_common.hpp"
@@ -4195,6 +4196,11 @@ static int heavy_flow_words(CmScratch &sc, uint64_t slots, hipStream_t st, bool 
 // gns_cm_view_create), so a window's first call allocates nothing: candidates
 // for min(cells, 4M) buckets, the per-flow words for the dictionary's slots,
 // unique entries and their order for 1M flows.  Larger lists still grow them.
+static int small_pin(CmScratch &sc) {
+    if (!sc.hsm) GNS_HIP(hipHostMalloc(reinterpret_cast<void **>(&sc.hsm), 64, hipHostMallocDefault));
+    return GNS_OK;
+}
+
 static int heavy_reserve(CmScratch &sc, uint64_t cells, uint64_t slots, uint32_t K, hipStream_t st) {
     GNS_TRY(heavy_flow_words(sc, slots, st, false));
     if (!sc.ncand) GNS_TRY(dalloc(reinterpret_cast<void **>(&sc.ncand), 16));
@@ -4215,7 +4221,12 @@ static int heavy_reserve(CmScratch &sc, uint64_t cells, uint64_t slots, uint32_t
         GNS_HIP(hipHostMalloc(reinterpret_cast<void **>(&sc.hpin), want, hipHostMallocDefault));
         sc.hpin_n = want;
     }
-    return GNS_OK;
+    // the order's pass histograms and the small pinned read-back words for nu entries too:
+    // a window's first list then allocates nothing (an allocation inside one list call was
+    // followed by an 18-36 ms dispatch stall of a LATER call, profiles/r06_hh_spikes.txt)
+    const uint64_t nblk = (nu + kRsBlock - 1) / kRsBlock, ngrp = (nblk + kTGrp - 1) / kTGrp;
+    GNS_TRY(grow_buf(&sc.rsh, sc.rsh_n, (nblk + ngrp + 1) * 256 + 4));
+    return small_pin(sc);
 }
 
 // GNS_HH_TRACE=1: the heavy-hitter list's phases timed on stderr (each mark
@@ -4225,20 +4236,17 @@ struct HhTrace {
     hipStream_t st;
     std::chrono::steady_clock::time_point t;
     explicit HhTrace(hipStream_t s) : on(getenv("GNS_HH_TRACE") != nullptr), st(s), t(std::chrono::steady_clock::now()) {}
-    void mark(const char *what, uint64_t n) {
+    void mark(const char *what, uint64_t n, bool sync = true) {
         if (!on) return;
-        (void)hipStreamSynchronize(st);
+        if (sync) (void)hipStreamSynchronize(st);
         const auto now = std::chrono::steady_clock::now();
-        fprintf(stderr, "[hh] %-12s n=%-9llu %8.3f ms\n", what, (unsigned long long)n,
-                std::chrono::duration<double, std::milli>(now - t).count());
+        struct rusage ru;
+        getrusage(RUSAGE_THREAD, &ru);
+        fprintf(stderr, "[hh] %-12s n=%-9llu %8.3f ms  nivcsw=%ld nvcsw=%ld\n", what, (unsigned long long)n,
+                std::chrono::duration<double, std::milli>(now - t).count(), ru.ru_nivcsw, ru.ru_nvcsw);
         t = now;
     }
 };
-
-static int small_pin(CmScratch &sc) {
-    if (!sc.hsm) GNS_HIP(hipHostMalloc(reinterpret_cast<void **>(&sc.hsm), 64, hipHostMallocDefault));
-    return GNS_OK;
-}
 
 // One stable LSD radix pass over perm (n entries) by digit r: in -> out.
 static int rs_pass(CmScratch &sc, hipStream_t st, const uint32_t *in, uint32_t *out, uint32_t n, const RsDigit &r) {
@@ -4325,7 +4333,9 @@ static int heavy_list(CmScratch &sc, hipStream_t st, const DictDev &Dd, uint64_t
     uint32_t nc = 0;
     for (int pass = 0; pass < 2; pass++) {
         // [0] candidates, [1] unique, [2] bad-id flag: zeroed by a kernel on the list's stream
+        tr.mark("pre_launch", 0, false);
         hipLaunchKernelGGL(k_fill_u32, dim3(1), dim3(64), 0, st, sc.ncand, (uint64_t)3, 0u);
+        tr.mark("launched", 0, false);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) {
             hipLaunchKernelGGL(k_hh_candidates, dim3((unsigned)((cells + 256 * kHhItems - 1) / (256 * kHhItems))), dim3(256), 0,
