@@ -310,13 +310,22 @@ __device__ __forceinline__ void k1_consume(const ExtractArgs &a, const K1Lds &S,
         for (int i = 0; i < GNS_KWMAX; i++)
             if ((uint32_t)i < ((K + 3) >> 2)) eq = eq && (rec[1 + i] == kw[i]);
         first = tag == a.epoch ? 1 : (eq ? 0 : (tag == 0 ? 2 : 3));
+#ifdef GNS_K1_ABL_DICT
+        (void)tag;
+        first = 0;  // timing ablation: every packet "found" at its (in-range) probe slot
+        rec[12] = rec[13] = rec[14] = rec[15] = 0;
+#endif
         if (first == 0) { res = CM_FOUND; out = slot0; }
         else if (first == 1) { res = CM_PENDING; out = slot0; }
     }
     // row buckets: from the record's cache (rows 0..3 of a committed flow, 0..7 in a
     // 32-word record), else hashed
     uint32_t bk[RMAX];
+#ifdef GNS_K1_ABL_DICT
+    const bool cached = false;  // buckets hashed: the ablation's record holds no cache
+#else
     const bool cached = bw && ok && first == 0;
+#endif
     const uint32_t nc = (NQ > 4 && a.D.RW >= 32) ? 8u : 4u;  // cached rows
 #pragma unroll
     for (uint32_t rr = 0; rr < RMAX; rr++) bk[rr] = (rr < nc && cached) ? rec[12 + rr] : 0u;
@@ -587,6 +596,12 @@ __global__ __launch_bounds__(NT, NT == 256 ? GNS_EX_MINW : (NT == 512 ? 2 : 1)) 
                 mm3_premix<GNS_KWMAX>(kwq, K, mk);
                 slotq = mm3_chain<GNS_KWMAX>(mk, K, a.D.seed) & a.D.mask;
             }
+#ifdef GNS_K1_ABL_DICT
+            // TIMING ABLATION ONLY (wrong counters; never a product build, tools/r06_k1abl.sh):
+            // the probe reads one of the table's first 4096 records (256 KB, L2-resident), so
+            // K1 keeps its streams, hashing, histogram and summaries but pays no dictionary miss
+            slotq &= 4095u;
+#endif
             if (okq) {
                 const uint4 *rq = reinterpret_cast<const uint4 *>(a.D.rec + (size_t)slotq * a.D.RW);
 #pragma unroll
