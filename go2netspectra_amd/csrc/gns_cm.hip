@@ -3494,21 +3494,23 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
 #undef GNS_K1_256
         GNS_HIP(hipGetLastError());
     }
-    // K1b: resolve parked packets until none remain.  The first round is queued
+    // K1b: resolve parked packets until none remain.  The first two rounds are queued
     // behind K1 without a host round trip (K1 parks the flows displaced from their
-    // home slot, so most batches have parked packets; a block with none exits at once).
+    // home slot, so most batches have parked packets, and the second round nearly
+    // always empties the list; a block with none exits at once), then the host reads
+    // the remaining count once.
     int cur = 0;
     for (int round = 0;; round++) {
-        if (round > 0) {
+        if (round > 1) {
             CtlRead rd;  // one launch writes the words into the pinned mirror
             rd.add(cm->ptotal + cur, 4, 0);
             rd.add(cm->stats + 3, 8, 2);
             rd.add(cm->dctl, 4, 4);
-            if (round == 1) rd.add(cm->stats + 8, 8, 6);
+            if (round == 2) rd.add(cm->stats + 8, 8, 6);
             GNS_HIP(ctl_read(rd, cm->h_pin, s));
             GNS_HIP(hipStreamSynchronize(s));
             cm->claimed = cm->h_pin[4];
-            if (round == 1) {  // the overflow side table holds every oversize row-update of the batch
+            if (round == 2) {  // the overflow side table holds every oversize row-update of the batch
                 const uint64_t big = (uint64_t)cm->h_pin[6] | (uint64_t)cm->h_pin[7] << 32;
                 if (big * g.d > cm->ovf_cap) {
                     const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(big * g.d + big * g.d / 4, kOvfCap), 1ull << 31);

@@ -821,6 +821,7 @@ struct SpArgs {
     const uint32_t *order;   // [nb] bins, largest first (k_sp_order)
     unsigned long long *err; // a cell with more encodes than LDS holds (cannot happen below 8192)
     uint32_t maxg;           // groups per window of a large bin (kSpMaxG; GNS_SS_SPG, tests only)
+    uint32_t cap;            // encodes a cell may take in one batch: kSpCap (GNS_SS_TEST_SPCAP lowers it, tests only)
     unsigned long long *prof;  // GNS_SS_DEBUG: P4 phase cycles (sp_group), else null
 };
 
@@ -1135,9 +1136,9 @@ __device__ __noinline__ void sp_giant(const SpArgs &a, SpLds &L, const uint64_t 
     });
     __syncthreads();
     uint32_t ns = L.n_succ;
-    if (ns > kSpCap) {
+    if (ns > a.cap) {
         if (tid == 0) atomicAdd(a.err, 1ull);
-        ns = kSpCap;
+        ns = min(ns, kSpCap);
     }
     if (ns == 0) return;
     uint64_t *es = sp_sort(L, L.b, ns, 24, 24 + kSsPktBits);
@@ -1347,6 +1348,7 @@ struct gns_ss {
     SpGeom sp{};
     uint32_t ncu = 0;
     uint32_t sp_maxg = 0;        // P4 groups per window of a large bin
+    uint32_t sp_cap = kSpCap;    // encodes per cell and batch (GNS_SS_TEST_SPCAP, tests only)
     bool debug = false;          // GNS_SS_DEBUG
     unsigned long long *sprof = nullptr;  // [8] P4 phase ticks (debug)
     uint32_t *shist = nullptr;   // [nblk][nb] per-block bin histogram -> offsets
@@ -1447,7 +1449,7 @@ int ss_encode_ids(gns_ss *ss, const InputDesc &in) {
         GNS_HIP(hipStreamSynchronize(s));
         if (round == 1 && (ss->h_pin[6] | ss->h_pin[7])) {  // P4: a cell's encodes exceed kSpCap
             GNS_HIP(hipMemsetAsync(ss->stats + 6, 0, 8, s));
-            set_error("a cell has more than %u encodes in one batch: use a smaller batch_packets", kSpCap);
+            set_error("a cell has more than %u encodes in one batch: use a smaller batch_packets", ss->sp_cap);
             return GNS_E_RANGE;
         }
         if (round == 1) ss->n_encodes += ss->h_pin[5];
@@ -1531,6 +1533,7 @@ int ss_run_batch(gns_ss *ss, const InputDesc &in, uint64_t n) {
         pa.regs = ss->regs; pa.skey = ss->skey; pa.sval = ss->sval; pa.scount = ss->counts + 1;
         pa.heads = ss->heads; pa.hlen = ss->hlen; pa.work = ss->counts + 2; pa.err = ss->stats + 6;
         pa.maxg = ss->sp_maxg;
+        pa.cap = ss->sp_cap;
         pa.prof = ss->debug ? ss->sprof : nullptr;
         if (ss->debug) GNS_HIP(hipMemsetAsync(ss->sprof, 0, 8 * 8, s));
         pa.order = ss->sorder;
@@ -1650,7 +1653,7 @@ int ss_batch_recover(gns_ss *ss, const InputDesc &d, uint64_t m, bool fresh) {
         GNS_HIP(hipMemcpyAsync(ss->stats_bak, ss->stats, 3 * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
                                ss->stream));
         const int rc = ss_batch<KIND>(ss, d, m);
-        if (rc == GNS_E_RANGE && m > kSpCap) {
+        if (rc == GNS_E_RANGE && m > ss->sp_cap) {
             // P4: a cell got more than kSpCap encodes (S3b aborts before any state write).
             // Undo S1's counters and split: a cell takes at most one encode per record, so
             // pieces of <= kSpCap records always fit (the RNG is indexed by record, so the
@@ -1826,6 +1829,12 @@ int gns_ss_create(const gns_ss_params *p, gns_ss **out) {
             const char *env = getenv("GNS_SS_SPG");  // tests: small windows exercise the window loop
             const long v = env ? strtol(env, nullptr, 10) : 0;
             ss->sp_maxg = (v >= 2 && v <= (long)kSpMaxG) ? (uint32_t)(v & ~1L) : kSpMaxG;
+            // tests: a lower per-cell encode cap makes the split-and-retry path of
+            // ss_batch_recover reachable with ordinary streams (> 8192 encodes in one
+            // cell needs m = 256 and registers climbing by 33 each)
+            const char *ec = getenv("GNS_SS_TEST_SPCAP");
+            const long c = ec ? strtol(ec, nullptr, 10) : 0;
+            ss->sp_cap = (c >= 16 && c <= (long)kSpCap) ? (uint32_t)c : kSpCap;
         }
         if (hipStreamCreateWithFlags(&ss->stream, hipStreamNonBlocking) != hipSuccess) {
             set_error("hipStreamCreate failed"); rc = GNS_E_HIP; break;

@@ -589,15 +589,15 @@ def _allgather_dev_rows(rows, world: int):
     return torch.cat([p[:c] for p, c in zip(parts, counts)], dim=0)
 
 
-def allgather_heavy_rows(cm, world: int):
+def allgather_heavy_rows(cm, world: int, rows=None):
     """Per-window exchange with the lists kept on the device (RCCL): each shard's device
-    heavy-hitter rows (CountMin.heavy_hitters_rows_device), two all-gathers, the union put
-    in canonical order on the GPU (order_rows_device; shards own disjoint flows), then one
-    copy to the host.  Returns (count flows [n,K], counts, size flows, sizes) like
-    allgather_heavy_arrays."""
+    heavy-hitter rows (CountMin.heavy_hitters_rows_device, or `rows` already taken), two
+    all-gathers, the union put in canonical order on the GPU (order_rows_device; shards own
+    disjoint flows), then one copy to the host.  Returns (count flows [n,K], counts, size
+    flows, sizes) like allgather_heavy_arrays."""
     K = cm.key_bytes
     out = []
-    for rows in cm.heavy_hitters_rows_device():
+    for rows in (rows if rows is not None else cm.heavy_hitters_rows_device()):
         g = order_rows_device(_allgather_dev_rows(rows, world), K).cpu().numpy()
         out.extend((g[:, :K], np.ascontiguousarray(g[:, K:]).view("<u4").reshape(-1).astype(np.uint32)))
     return tuple(out)

@@ -360,3 +360,27 @@ def test_large_bins_giant_cells_and_windows(gpu, oracle, monkeypatch, spg):
     orc.insert(fl, el)
     assert_same_ss(ss, orc)
     assert_same_list([(h.Flow, h.Count) for h in ss.heavy_hitters().Count], orc.heavy())
+
+
+@pytest.mark.parametrize("m", [256, 64])
+def test_encode_cap_split_and_retry(gpu, oracle, monkeypatch, m):
+    """ss_batch_recover's GNS_E_RANGE path (a cell with more encodes in one batch than
+    P4's LDS group holds): the batch is aborted before any state write, S1's counters
+    are restored and it re-runs in halves.  Reaching 8192 encodes in one cell needs
+    m = 256 and every register climbing 33 times, so GNS_SS_TEST_SPCAP lowers the cap
+    to 64 encodes per cell for this handle: a hot source from empty registers then
+    overflows it in every batch of the stream, and the result must still be the
+    oracle's, bit for bit, with the retries counted."""
+    monkeypatch.setenv("GNS_SS_TEST_SPCAP", "64")
+    rng = np.random.default_rng(31337 + m)
+    n = 200_000
+    ss, orc = make_pair(oracle, 2048, 2, m, 5, 16, 16, thr=20, batch_packets=n)
+    fl, el, flows = spread_stream(rng, n, 5_000, 16, 16, s=1.1, elem_pool=1 << 18)
+    fl[rng.random(n) < 0.2] = flows[3]
+    for part in np.array_split(np.arange(n), 2):
+        ss.insert_keys(fl[part], el[part])
+        orc.insert(fl[part], el[part])
+    ss.flush()
+    assert_same_ss(ss, orc)
+    assert_same_list([(h.Flow, h.Count) for h in ss.heavy_hitters().Count], orc.heavy())
+    assert ss.dict_stats()["retried_batches"] > 0
