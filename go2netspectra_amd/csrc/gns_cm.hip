@@ -2411,6 +2411,338 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// K4 over super-bins without the tile sweep (round 6; rows wider than the
+// bins K3s can count, configs[4]: d=8 w=2^24, 512 super-bins of 8 tiles per
+// row).  A 100M-packet batch gives a cold update to only ~6% of the 2^27
+// buckets, so loading and storing every tile's 64 KB of state (2 GB per batch
+// each way) and sub-partitioning every super-bin by tile first (k_subpart: a
+// second read and write of all updates) cost more than the updates themselves.
+// Here a workgroup takes a super-bin's updates in K3s's stream order and keeps
+// only the buckets they touch, in an LDS hash table whose slots ARE the tile
+// state slots of apply_tile: an update's bucket field is rewritten to its slot,
+// so classify / decide / compaction / replay run unchanged.  A new bucket's
+// state is gathered when its key is inserted; the table is written back (and
+// cleared) when it fills and at the end of the bin.  A chunk whose buckets do
+// not fit the table even after a write-back is taken in halves (a piece of 64
+// updates always fits): buckets are independent, so writing state back between
+// pieces of the stream changes nothing.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSpHashCap = kTileMax - kTileMax / 8;  // used slots before the table counts as full
+constexpr uint32_t kSpProbe = 64;
+constexpr uint32_t kSpNoSlot = 0xFFFFFFFFu;
+
+struct SparseLds {
+    uint32_t key[kTileMax];  // 0 empty, else bucket-in-bin + 1
+    uint32_t used, ovf;
+};
+
+__device__ __forceinline__ uint32_t sp_hash(uint32_t b) { return (b * 0x9E3779B1u) >> (32 - kTileBitsMax); }
+
+// slot of a bucket that is in the table (the replay fallback re-reads raw updates)
+__device__ __forceinline__ uint32_t sp_find(const SparseLds &H, uint32_t b) {
+    uint32_t h = sp_hash(b);
+    const uint32_t key = b + 1;
+    for (uint32_t p = 0; p < kTileMax; p++) {
+        if (H.key[h] == key) return h;
+        h = (h + 1) & (kTileMax - 1u);
+    }
+    return 0;  // unreachable: every valid update of the piece was mapped
+}
+
+// raw update -> the same update with its bucket field replaced by its slot
+__device__ __forceinline__ uint64_t sp_rewrite(uint64_t e, uint32_t slot) {
+    return (e & ~((uint64_t)(kTileMax - 1u) << 32)) | ((uint64_t)slot << 32);
+}
+
+// Write every used slot's state back to its bucket and clear the table.
+__device__ __forceinline__ void sp_flush(const ApplyArgs &a, ApplyLds &L, SparseLds &H, uint64_t cbase) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kTileMax; i += kApThreads) {
+        const uint32_t k = H.key[i];
+        if (k) {
+            const uint64_t c = cbase + (k - 1u);
+            const uint2 cs = L.sCS[i], f = L.sF[i];
+            a.C[c] = cs.x; a.Fc[c] = f.x;
+            a.S[c] = cs.y; a.Fs[c] = f.y;
+            H.key[i] = 0;
+        }
+    }
+    if (threadIdx.x == 0) { H.used = 0; H.ovf = 0; }
+    __syncthreads();
+}
+
+// Map the updates of [lo, hi) (logical indices; the chunk's items e[j] at cb + j * threads + tid)
+// to slots, gathering new buckets' state.  On success the in-range valid items are rewritten and
+// their bits set in vm; on overflow nothing is rewritten and false is returned (block-uniform).
+__device__ __forceinline__ bool sp_map(const ApplyArgs &a, ApplyLds &L, SparseLds &H, uint64_t (&e)[kApItems],
+                                       uint32_t &vm, uint32_t cb, uint32_t lo, uint32_t hi, uint32_t end,
+                                       uint64_t cbase, uint32_t col0, uint32_t bmask) {
+    const uint32_t tid = threadIdx.x;
+    uint32_t sl[kApItems];
+#pragma unroll
+    for (int j = 0; j < kApItems; j++) {
+        sl[j] = kSpNoSlot;
+        const uint32_t q = cb + j * kApThreads + tid;
+        const uint32_t b = (uint32_t)(e[j] >> 32) & bmask;
+        // bucket-range slice (exact global mode): other handles own the rest of the row
+        if (q >= lo && q < hi && q < end && (col0 + b) - a.g.blo < a.g.bspan) {
+            const uint32_t key = b + 1u;
+            uint32_t h = sp_hash(b);
+            for (uint32_t p = 0; p < kSpProbe; p++) {
+                const uint32_t old = atomicCAS(&H.key[h], 0u, key);
+                if (old == 0u) {  // new bucket: gather its state into the slot
+                    if (atomicAdd(&H.used, 1u) >= kSpHashCap) H.ovf = 1u;
+                    const uint64_t c = cbase + b;
+                    L.sCS[h] = make_uint2(a.C[c], a.S[c]);
+                    L.sF[h] = make_uint2(a.Fc[c], a.Fs[c]);
+                    sl[j] = h;
+                    break;
+                }
+                if (old == key) { sl[j] = h; break; }
+                h = (h + 1u) & (kTileMax - 1u);
+            }
+            if (sl[j] == kSpNoSlot) H.ovf = 1u;
+        }
+    }
+    __syncthreads();
+    const bool ok = H.ovf == 0u;
+    if (ok) {
+#pragma unroll
+        for (int j = 0; j < kApItems; j++)
+            if (sl[j] != kSpNoSlot) { e[j] = sp_rewrite(e[j], sl[j]); vm |= 1u << j; }
+    }
+    __syncthreads();  // every lane has read ovf before a flush may clear it
+    return ok;
+}
+
+// classify / decide / compact / replay of the mapped items (vm) of one chunk: apply_tile's
+// chunk body over slots (tn = every slot of the table; unused slots have accN == 0)
+__device__ __forceinline__ void sp_chunk(const ApplyArgs &a, ApplyLds &L, const SparseLds &H,
+                                         const uint64_t (&e)[kApItems], uint32_t vm, uint32_t cb, uint32_t bmask,
+                                         uint32_t &st_chunks, uint32_t &st_rep, uint32_t &st_crep) {
+    uint32_t *accN = L.accN;
+    unsigned long long *accS = L.accS;
+    uint16_t *s_list = L.s_list;
+    uint32_t *s_wc = L.s_wc;
+    uint32_t &s_any = L.s_any, &s_nlist = L.s_nlist;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    if (tid == 0) { s_any = 0; st_chunks++; }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kApItems; j++) {
+        if (!((vm >> j) & 1u)) continue;
+        const uint32_t lo = (uint32_t)e[j];
+        const uint32_t hi = (uint32_t)(e[j] >> 32);
+        const uint32_t b = hi & (kTileMax - 1u);
+        if (lo & kOvfFlag) {  // size >= 2^20-1: always replayed
+            atomicAdd(&accN[b], 1u);
+            atomicOr(&accN[b], 1u << kAccForce);
+        } else {
+            const uint32_t s = hi >> kEntShift;
+            const uint2 f = L.sF[b];
+            const bool oc = lo != f.x, os = lo != f.y;
+            atomicAdd(&accN[b], 1u | (uint32_t)oc << 14);
+            atomicAdd(&accS[b], (unsigned long long)(os ? (uint64_t)s << 32 : (uint64_t)s));
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < kTileMax; i += kApThreads) {
+        const uint32_t an = accN[i];
+        if (!an) continue;
+        const uint32_t n = an & kM14;
+        const uint32_t noc = (an >> 14) & kM14;
+        const bool force = ((an >> kAccForce) & 1u) != 0;
+        const uint64_t as = accS[i];
+        const uint32_t so = (uint32_t)as, sx = (uint32_t)(as >> 32);
+        uint32_t rep = 0;
+        if (!force) {
+            uint2 cs = L.sCS[i];
+            const uint32_t C = cs.x;
+            const uint32_t nown = n - noc;
+            if (C > noc && (uint64_t)C + nown < (1ull << 32)) cs.x = C + nown - noc;
+            else rep |= 1u;
+            const uint32_t S = cs.y;
+            if (S > sx && (uint64_t)S + so < (1ull << 32)) cs.y = S + so - sx;
+            else rep |= 2u;
+            L.sCS[i] = cs;
+        } else {
+            rep = 3u;
+        }
+        accS[i] = 0;
+        accN[i] = rep;
+        if (rep) s_any = 1;
+    }
+    __syncthreads();
+    if (s_any) {
+        bool need[kApItems];
+        uint64_t bal[kApItems];
+#pragma unroll
+        for (int j = 0; j < kApItems; j++) {
+            const uint32_t b = (uint32_t)(e[j] >> 32) & (kTileMax - 1u);
+            need[j] = ((vm >> j) & 1u) && accN[b] != 0;
+            bal[j] = __ballot(need[j]);
+            if (lane == 0) s_wc[j * kApWaves + wave] = __popcll(bal[j]);
+        }
+        __syncthreads();
+        if (wave == 0) {
+            constexpr uint32_t NC = kApItems * kApWaves;
+            constexpr uint32_t PER = (NC + 63) / 64;
+            uint32_t x[PER], sum = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < PER; q++) {
+                x[q] = lane * PER + q < NC ? s_wc[lane * PER + q] : 0u;
+                sum += x[q];
+            }
+            const uint32_t inc = wave_incl_scan(sum);
+            uint32_t run = inc - sum;
+#pragma unroll
+            for (uint32_t q = 0; q < PER; q++) {
+                if (lane * PER + q < NC) s_wc[lane * PER + q] = run;
+                run += x[q];
+            }
+            if (lane == 63) s_nlist = inc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kApItems; j++)
+            if (need[j]) {
+                const uint32_t pos = s_wc[j * kApWaves + wave] + __popcll(bal[j] & lt_mask);
+                s_list[pos] = (uint16_t)(j * kApThreads + tid);
+                if (pos < kRepCap) L.s_rep[pos] = e[j];
+            }
+        __syncthreads();
+        const uint32_t nlist = s_nlist;
+        st_rep += nlist;
+        st_crep++;
+        // the list's entries beyond kRepCap are re-read raw and mapped to their slots again
+        auto rep_entry = [&](uint32_t i) -> uint64_t {
+            if (i < kRepCap) return L.s_rep[i];
+            const uint64_t raw = a.entries[cb + s_list[i]];
+            return sp_rewrite(raw, sp_find(H, (uint32_t)(raw >> 32) & bmask));
+        };
+        constexpr uint32_t kWl = kApChunk / kApWaves;
+        uint32_t nmine = 0xFFFFFFFFu;
+        if (nlist <= kRepCap) {
+            uint16_t *wl = s_list + wave * kWl;
+            uint32_t c = 0;
+            for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
+                const uint32_t i = g0 + lane;
+                const bool mine = i < nlist && ((uint32_t)(L.s_rep[i] >> 32) & (kTileMax - 1u)) % kApWaves == wave;
+                const uint64_t m = __ballot(mine);
+                const uint32_t pos = c + __popcll(m & lt_mask);
+                if (mine && pos < kWl) wl[pos] = (uint16_t)i;
+                c += __popcll(m);
+            }
+            if (c <= kWl) nmine = c;
+        }
+        if (nmine != 0xFFFFFFFFu) {
+            const uint16_t *wl = s_list + wave * kWl;
+            for (uint32_t g0 = 0; g0 < nmine; g0 += 64) {
+                const uint32_t j = g0 + lane;
+                bool pending = j < nmine;
+                uint32_t b = 0, k = 0, s = 0, rf = 0;
+                if (pending) {
+                    const uint64_t ee = L.s_rep[wl[j]];
+                    b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
+                    decode_entry(a.ovf, ee, k, s);
+                    rf = (uint32_t)accN[b];
+                }
+                replay_group(L, pending, b, k, s, rf);
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t j = lane; j < nmine; j += 64) accN[(uint32_t)(L.s_rep[wl[j]] >> 32) & (kTileMax - 1u)] = 0;
+        } else {
+            for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
+                const uint32_t i = g0 + lane;
+                bool pending = false;
+                uint32_t b = 0, k = 0, s = 0, rf = 0;
+                if (i < nlist) {
+                    const uint64_t ee = rep_entry(i);
+                    b = (uint32_t)(ee >> 32) & (kTileMax - 1u);
+                    pending = b % kApWaves == wave;
+                    if (pending) {
+                        decode_entry(a.ovf, ee, k, s);
+                        rf = (uint32_t)accN[b];
+                    }
+                }
+                replay_group(L, pending, b, k, s, rf);
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t g0 = 0; g0 < nlist; g0 += 64) {
+                const uint32_t i = g0 + lane;
+                if (i < nlist) {
+                    const uint32_t b = (uint32_t)(rep_entry(i) >> 32) & (kTileMax - 1u);
+                    if (b % kApWaves == wave) accN[b] = 0;
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kApThreads) void k_apply_sparse(ApplyArgs a) {
+    __shared__ ApplyLds L;
+    __shared__ SparseLds H;
+    __shared__ uint32_t s_k;
+    const CmGeom &g = a.g;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t bmask = (1u << g.bin_bits) - 1u;
+    for (uint32_t i = tid; i < kTileMax; i += kApThreads) { H.key[i] = 0; L.accN[i] = 0; L.accS[i] = 0; }
+    if (tid == 0) { H.used = 0; H.ovf = 0; s_k = atomicAdd(a.work, 1u); }
+    __syncthreads();
+    uint32_t k = s_k;
+    __syncthreads();
+    uint32_t st_chunks = 0, st_rep = 0, st_crep = 0;
+    while (k < g.nbins) {
+        if (tid == 0) s_k = atomicAdd(a.work, 1u);  // the bin after this one
+        const ApplyTile cur = apply_bin(a, k);
+        const uint64_t cbase = (uint64_t)cur.r * g.w + cur.bbase;
+        uint64_t e[kApItems], en[kApItems];
+#pragma unroll
+        for (int j = 0; j < kApItems; j++) {
+            const uint32_t q = cur.beg + j * kApThreads + tid;
+            e[j] = q < cur.end ? a.entries[q] : 0ull;
+        }
+        for (uint32_t cb = cur.beg; cb < cur.end; cb += kApChunk) {
+#pragma unroll
+            for (int j = 0; j < kApItems; j++) {  // the next chunk loads while this one is applied
+                const uint32_t q = cb + kApChunk + j * kApThreads + tid;
+                en[j] = q < cur.end ? a.entries[q] : 0ull;
+            }
+            const uint32_t hic = min(cb + kApChunk, cur.end);
+            uint32_t lo = cb, span = kApChunk;
+            while (lo < hic) {  // block-uniform
+                const uint32_t hi = min(lo + span, hic);
+                uint32_t vm = 0;
+                bool ok = sp_map(a, L, H, e, vm, cb, lo, hi, cur.end, cbase, cur.bbase, bmask);
+                if (!ok) {  // table full: write it back and map the piece into an empty one
+                    sp_flush(a, L, H, cbase);
+                    ok = sp_map(a, L, H, e, vm, cb, lo, hi, cur.end, cbase, cur.bbase, bmask);
+                }
+                if (!ok) {  // the piece alone has too many buckets: halve it
+                    sp_flush(a, L, H, cbase);
+                    span = max(span / 2, 64u);
+                    continue;
+                }
+                sp_chunk(a, L, H, e, vm, cb, bmask, st_chunks, st_rep, st_crep);
+                lo = hi;
+            }
+#pragma unroll
+            for (int j = 0; j < kApItems; j++) e[j] = en[j];
+        }
+        sp_flush(a, L, H, cbase);
+        k = s_k;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        atomicAdd(&a.stats[5], (unsigned long long)st_rep);
+        atomicAdd(&a.stats[6], (unsigned long long)st_chunks);
+        if (st_crep) atomicAdd(&a.stats[7], (unsigned long long)st_crep);
+    }
+}
+
 constexpr uint32_t kHotSegs = 64;   // segments per hot bin (blocks working on one bucket)
 constexpr uint32_t kChkCap = 4096;  // (slot, K1 block) exact size checks per batch
 
@@ -3265,6 +3597,7 @@ struct gns_cm {
     uint64_t *entries = nullptr, *entries2 = nullptr;
     uint16_t *rseg = nullptr;          // [round][16] k_subpart round tile starts (sub_bits > 0)
     int subpart_nt = 0;                // GNS_SUBPART_NT (A/B)
+    bool k4_sparse = true;             // super-bins through k_apply_sparse (GNS_K4_SPARSE=0: k_subpart + tiles)
     uint32_t *rec_sizes = nullptr;     // 16-byte compact records from device memory: a batch's sizes
     uint64_t *ovf = nullptr;
     uint32_t *ovf_cnt = nullptr;
@@ -3593,7 +3926,12 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs; a.work = cm->work;
         GNS_HIP(hipMemsetAsync(cm->work, 0, 12, s));
         ScopedStage st(cm->timer, 4);
-        if (g.sub_bits) {
+        if (g.sub_bits && cm->k4_sparse) {
+            // super-bins in stream order, touched buckets only (k_apply_sparse): no
+            // sub-partition pass and no tile sweep; GNS_K4_SPARSE=0 restores the tile path
+            const dim3 apg(std::min(g.nbins, cm->ncu));
+            hipLaunchKernelGGL(k_apply_sparse, apg, dim3(kApThreads), 0, s, a);
+        } else if (g.sub_bits) {
             // 512-thread workgroups (16 updates per thread and round, two per CU) when a
             // wave per tile fits; GNS_SUBPART_NT=1024 for the A/B
             if ((1u << g.sub_bits) <= 8 && cm->subpart_nt != 1024)
@@ -3605,7 +3943,9 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         }
         // persistent: one workgroup per CU (the tile LDS fills a CU), bins from the schedule counter
         const dim3 apg(std::min(g.nbins, cm->ncu * (kApThreads <= 512 ? 2u : 1u)));  // workgroups the LDS fits per CU
-        if (!g.sub_bits) {
+        if (g.sub_bits && cm->k4_sparse) {
+            // (launched above)
+        } else if (!g.sub_bits) {
             hipLaunchKernelGGL(k_apply<0>, apg, dim3(kApThreads), 0, s, a);
         } else {
             hipLaunchKernelGGL(k_apply<1>, apg, dim3(kApThreads), 0, s, a);
@@ -4002,6 +4342,8 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             cm->k3_pack = !(es && es[0] == 'u');  // 512-bin rows: 1024-thread K3s, 16-bit counters (u: 512 threads)  // A/B: 512-thread K3s, 4096-packet sub-passes, two per CU
             const char *en = getenv("GNS_SUBPART_NT");
             cm->subpart_nt = en ? atoi(en) : 0;
+            const char *esp = getenv("GNS_K4_SPARSE");  // super-bins: touched buckets only (0: tile path)
+            cm->k4_sparse = !(esp && esp[0] == '0');
             const char *ec = getenv("GNS_CMODE");
             cm->cmode = ec && ec[0] == '1' && cm->lds_ordered && cm->k3_staged && g.ntiles <= 256 && g.d <= 8 &&
                         extract_lds_bytes(g.nbins_all, g.d) <= kExLdsSmall && g.w <= (1u << (32 - kCsBits));

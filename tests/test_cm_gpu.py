@@ -281,9 +281,13 @@ def test_large_sizes_mixed_owner(gpu, oracle):
     (5_000_000, 3, 13, 50_000, 1_000_000),  # non power-of-two wide row
     (20_000_000, 8, 4, 1 << 15, 1_000_000),  # bins of 16 tiles (k_subpart's 1024-thread variant)
 ])
-def test_wide_rows_parity(gpu, oracle, w, d, K, nflows, n):
-    """Widths beyond 1024 LDS tiles per row: K3 bins hold 2^sub_bits tiles and K4
-    partitions each bin by tile before the in-order tile pass."""
+@pytest.mark.parametrize("sparse", ["1", "0"])
+def test_wide_rows_parity(gpu, oracle, monkeypatch, w, d, K, nflows, n, sparse):
+    """Widths beyond 1024 LDS tiles per row: K3 bins hold 2^sub_bits tiles.  K4 takes a
+    bin in stream order with only its touched buckets in LDS (k_apply_sparse, the
+    default), or (GNS_K4_SPARSE=0) partitions each bin by tile before the in-order
+    tile pass (k_subpart + k_apply)."""
+    monkeypatch.setenv("GNS_K4_SPARSE", sparse)
     rng = np.random.default_rng(w % 1000 + d)
     cm, orc = make_pair(oracle, w, d, K, st=1 << 16, ct=100, max_flows=1 << 20)
     keys, flows, _ = zipf_keys(rng, n, nflows, K)
