@@ -1021,7 +1021,8 @@ def main():
         wl2 = f"2^{args.width.bit_length() - 1}" if args.width & (args.width - 1) == 0 else str(args.width)
         line["metric"] = f"Mpackets/s CMS update (device-resident, d={args.depth} w={wl2})"
         line["config"]["workload"] = (f"Count-Min d={args.depth} w={wl2} (configs[4] geometry when d=8 w=2^24), "
-                                      f"100M Zipf(1.1) 5-tuple headers in HBM per GPU, bit-exact counters")
+                                      f"{n / 1e6:g}M Zipf(1.1) 5-tuple headers in HBM per GPU per step (one device "
+                                      f"batch), bit-exact counters")
         line["note"] = "not the headline metric (BASELINE.json metric is d=4 w=2^20)"
     if args.key != "5tuple":
         line["note"] = "secondary key layout (SURVEY §8d); the headline uses the 5-tuple key"

@@ -2479,7 +2479,7 @@ __device__ __forceinline__ bool sp_map(const ApplyArgs &a, ApplyLds &L, SparseLd
                                        uint32_t &vm, uint32_t cb, uint32_t lo, uint32_t hi, uint32_t end,
                                        uint64_t cbase, uint32_t col0, uint32_t bmask) {
     const uint32_t tid = threadIdx.x;
-    uint32_t sl[kApItems];
+    uint32_t sl[kApItems], nnew = 0;
 #pragma unroll
     for (int j = 0; j < kApItems; j++) {
         sl[j] = kSpNoSlot;
@@ -2490,9 +2490,13 @@ __device__ __forceinline__ bool sp_map(const ApplyArgs &a, ApplyLds &L, SparseLd
             const uint32_t key = b + 1u;
             uint32_t h = sp_hash(b);
             for (uint32_t p = 0; p < kSpProbe; p++) {
+                // most updates of a bin find their bucket already mapped: a plain read first
+                const uint32_t seen = H.key[h];
+                if (seen == key) { sl[j] = h; break; }
+                if (seen != 0u) { h = (h + 1u) & (kTileMax - 1u); continue; }
                 const uint32_t old = atomicCAS(&H.key[h], 0u, key);
                 if (old == 0u) {  // new bucket: gather its state into the slot
-                    if (atomicAdd(&H.used, 1u) >= kSpHashCap) H.ovf = 1u;
+                    nnew++;
                     const uint64_t c = cbase + b;
                     L.sCS[h] = make_uint2(a.C[c], a.S[c]);
                     L.sF[h] = make_uint2(a.Fc[c], a.Fs[c]);
@@ -2505,6 +2509,9 @@ __device__ __forceinline__ bool sp_map(const ApplyArgs &a, ApplyLds &L, SparseLd
             if (sl[j] == kSpNoSlot) H.ovf = 1u;
         }
     }
+    // slots taken: one add per wave (the first chunk of a bin inserts most of its buckets)
+    const uint32_t wnew = __ockl_wfred_add_u32(nnew);
+    if ((tid & 63u) == 0 && wnew && atomicAdd(&H.used, wnew) + wnew > kSpHashCap) H.ovf = 1u;
     __syncthreads();
     const bool ok = H.ovf == 0u;
     if (ok) {

@@ -2,6 +2,7 @@
 # Round-6 measurement runs (GPU box).  usage: tools/r06_bench.sh <tag> <leg>...
 # legs: driver (the driver's exact command: --steps 20 --warmup 5, CPU legs + parity), default,
 # headline (--no-cpu), c5 (configs[4] geometry with the CPU leg + in-line parity), c5fast (--no-cpu),
+# c5big (configs[4] geometry, 200M-packet steps = device batches, CPU leg + parity),
 # ss, exact, hybrid, thrift, srcip, c1, host_compact, prof_cm / prof_c5 / prof_ss (rocprofv3 kernel
 # traces, >= 10 steady full-batch launches).  Every GPU step has its own time limit; the
 # script stops at the first failure.
@@ -30,6 +31,7 @@ for leg in "$@"; do
         ss) run ss 400 --sketch superspread ;;
         c5) run c5 600 --width 16777216 --depth 8 ;;
         c5fast) run c5fast 400 --width 16777216 --depth 8 --no-cpu ;;
+        c5big) run c5big 600 --width 16777216 --depth 8 --packets 200000000 ;;
         exact) run exact 300 --sketch exact --no-cpu ;;
         hybrid) run hybrid 500 --sketch hybrid --no-cpu ;;
         host_compact) run host_compact 300 --host-input compact --no-cpu ;;
@@ -39,6 +41,7 @@ for leg in "$@"; do
         prof_cm) prof cm 400 --no-cpu --steps 10 --warmup 5 --windows 0 ;;
         prof_ss) prof ss 400 --sketch superspread --no-cpu --steps 10 --warmup 5 ;;
         prof_c5) prof c5 500 --width 16777216 --depth 8 --no-cpu --steps 10 --warmup 5 --windows 0 ;;
+        prof_c5big) prof c5big 600 --width 16777216 --depth 8 --packets 200000000 --no-cpu --steps 10 --warmup 3 --windows 0 ;;
         *) echo "unknown leg $leg"; exit 2 ;;
     esac || exit 1
 done
