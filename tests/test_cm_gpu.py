@@ -323,14 +323,14 @@ def test_ballot_rank_fallback_parity(gpu, oracle, monkeypatch, w, d, K, nflows, 
     assert_same_state(cm, orc)
 
 
-@pytest.mark.parametrize("K,batch", [(16, 0), (37, 40_000)])
-def test_bucket_range_slices_are_the_global_sketch(gpu, oracle, K, batch):
+@pytest.mark.parametrize("K,batch,w,d", [(16, 0, 5000, 4), (37, 40_000, 5000, 4),
+                                         (8, 0, 5_000_000, 3)])  # super-bins: the sparse K4's slice check
+def test_bucket_range_slices_are_the_global_sketch(gpu, oracle, K, batch, w, d):
     """SURVEY §8e exact global mode: G handles with disjoint bucket ranges, each
     fed the whole stream, together hold exactly the single sketch (hot
     designation, replay and multi-batch paths included)."""
     from go2netspectra_amd import CountMin
     from go2netspectra_amd.dist import assemble_slices, bucket_slice
-    w, d = 5000, 4
     rng = np.random.default_rng(77 + K)
     seeds = rng.integers(0, 2**32, d, dtype=np.uint64).astype(np.uint32)
     keys, _, _ = zipf_keys(rng, 400_000, 20_000, K)
