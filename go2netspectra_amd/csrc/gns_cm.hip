@@ -3123,7 +3123,17 @@ __device__ __forceinline__ uint32_t hot_key(uint32_t v) {
     return bits >= 4 ? bits * 8u + ((v >> (bits - 4u)) & 7u) : bits * 8u;
 }
 
-__global__ __launch_bounds__(256) void k_hot_hist(const uint32_t *C, CmGeom g, uint32_t *hh /*[d][kHotKeys]*/) {
+// Candidates of the next designation, collected by the histogram pass (round 6): every
+// bucket whose key is within one octave below the previous batch's threshold.  When the
+// new threshold is no more than an octave below the old one and the list did not
+// overflow, the buckets k_hot_collect takes are all in the list, so it scans the list
+// instead of the whole counter array (one pass over C per batch instead of two: 512 MB
+// at configs[4]'s geometry).  Any designation is exact (the summary path proves each
+// batch or falls back), so the choice only moves work.
+constexpr uint32_t kHotCand = 4096;  // candidates kept per row
+
+__global__ __launch_bounds__(256) void k_hot_hist(const uint32_t *C, CmGeom g, uint32_t *hh /*[d][kHotKeys]*/,
+                                                  const uint32_t *thr_prev, uint32_t *hcand, uint32_t *hcn) {
     __shared__ uint32_t s[8 * kHotKeys];
     for (uint32_t i = threadIdx.x; i < g.d * kHotKeys; i += 256) s[i] = 0;
     __syncthreads();
@@ -3132,6 +3142,15 @@ __global__ __launch_bounds__(256) void k_hot_hist(const uint32_t *C, CmGeom g, u
     for (uint32_t r = 0; r < g.d; r++) {
         const uint32_t *Cr = C + (uint64_t)r * g.w;
         uint32_t *sr = s + r * kHotKeys;
+        const uint32_t tp = thr_prev[r];  // 0xFFFFFFFF: no previous threshold (no candidates)
+        const uint32_t ck = tp <= kHotKeys ? (tp >= 8u ? tp - 8u : 0u) : 0xFFFFFFFFu;
+        uint32_t *cr = hcand + (uint64_t)r * kHotCand;
+        auto cand = [&](uint32_t v, uint64_t c) {
+            if (v >= (1u << (kHotMinBits - 1)) && hot_key(v) >= ck) {
+                const uint32_t q = atomicAdd(&hcn[r], 1u);
+                if (q < kHotCand) cr[q] = (uint32_t)c;
+            }
+        };
         if ((g.w & 3u) == 0) {
             // four 16-byte loads in flight per thread before their counts (the class adds
             // between single loads left the pass latency-bound with few blocks)
@@ -3150,12 +3169,17 @@ __global__ __launch_bounds__(256) void k_hot_hist(const uint32_t *C, CmGeom g, u
                     if (v[u].y >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v[u].y)], 1u);
                     if (v[u].z >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v[u].z)], 1u);
                     if (v[u].w >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v[u].w)], 1u);
+                    const uint64_t c = c0 + (uint64_t)u * stride;
+                    if (c < n4) {
+                        cand(v[u].x, 4 * c); cand(v[u].y, 4 * c + 1); cand(v[u].z, 4 * c + 2); cand(v[u].w, 4 * c + 3);
+                    }
                 }
             }
         } else {
             for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < g.w; c += stride) {
                 const uint32_t v = Cr[c];
                 if (v >= (1u << (kHotMinBits - 1))) atomicAdd(&sr[hot_key(v)], 1u);
+                cand(v, c);
             }
         }
     }
@@ -3163,7 +3187,8 @@ __global__ __launch_bounds__(256) void k_hot_hist(const uint32_t *C, CmGeom g, u
     for (uint32_t i = threadIdx.x; i < g.d * kHotKeys; i += 256) if (s[i]) atomicAdd(&hh[i], s[i]);
 }
 
-__global__ void k_hot_pick(uint32_t *hh, CmGeom g, uint32_t *thr, uint32_t *hcnt, uint32_t *hot_ids) {
+__global__ void k_hot_pick(uint32_t *hh, CmGeom g, uint32_t *thr, uint32_t *hcnt, uint32_t *hot_ids,
+                           const uint32_t *hcn, uint32_t *hfull) {
     __shared__ uint32_t s_hh[8 * kHotKeys];
     for (uint32_t i = threadIdx.x; i < g.d * kHot; i += blockDim.x) hot_ids[i] = GNS_ID_NONE;
     for (uint32_t i = threadIdx.x; i < g.d * kHotKeys; i += blockDim.x) { s_hh[i] = hh[i]; hh[i] = 0; }
@@ -3176,13 +3201,18 @@ __global__ void k_hot_pick(uint32_t *hh, CmGeom g, uint32_t *thr, uint32_t *hcnt
             if (cum > kHot) break;
             t = (uint32_t)k;
         }
+        // the candidate list holds every bucket the collect takes iff it did not overflow and
+        // the new threshold is at most one octave below the one the list was collected for
+        const uint32_t tp = thr[r];
+        hfull[r] = !(tp <= kHotKeys && t + 8u >= tp && hcn[r] <= kHotCand);
         thr[r] = t;
         hcnt[r] = 0;
     }
 }
 
 __global__ __launch_bounds__(256) void k_hot_collect(const uint32_t *C, CmGeom g, const uint32_t *thr,
-                                                      uint32_t *hcnt, uint32_t *hot_ids) {
+                                                      uint32_t *hcnt, uint32_t *hot_ids, const uint32_t *hcand,
+                                                      const uint32_t *hcn, const uint32_t *hfull) {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint32_t r = 0; r < g.d; r++) {
         const uint32_t *Cr = C + (uint64_t)r * g.w;
@@ -3193,6 +3223,14 @@ __global__ __launch_bounds__(256) void k_hot_collect(const uint32_t *C, CmGeom g
                 if (q < kHot) hot_ids[r * kHot + q] = (uint32_t)c;
             }
         };
+        if (!hfull[r]) {  // the histogram pass's candidate list holds them all (block-uniform)
+            const uint32_t nc = hcn[r];
+            for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nc; i += (uint32_t)stride) {
+                const uint32_t c = hcand[(uint64_t)r * kHotCand + i];
+                take(Cr[c], c);
+            }
+            continue;
+        }
         if ((g.w & 3u) == 0) {
             const uint4 *C4 = reinterpret_cast<const uint4 *>(Cr);
             for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < g.w / 4; c += stride) {
@@ -3207,13 +3245,14 @@ __global__ __launch_bounds__(256) void k_hot_collect(const uint32_t *C, CmGeom g
 
 // Lookup groups of the designated buckets (one thread per row, deterministic);
 // a bucket whose group is full is dropped from the designation.
-__global__ __launch_bounds__(1024) void k_hot_table(CmGeom g, uint32_t *hot_ids, uint32_t *hot_tab) {
+__global__ __launch_bounds__(1024) void k_hot_table(CmGeom g, uint32_t *hot_ids, uint32_t *hot_tab, uint32_t *hcn) {
     // entry h of a row takes slot j of its group, j = number of earlier valid
     // entries of the row in the same group (what inserting in h order gives);
     // j >= 4: the group is full and the bucket is not designated
     __shared__ uint32_t s_ids[8 * kHot];
     const uint32_t NS = g.d * kHot;
     for (uint32_t i = threadIdx.x; i < g.d * kHotTab; i += blockDim.x) hot_tab[i] = 0xFFFFFFFFu;
+    if (threadIdx.x < g.d) hcn[threadIdx.x] = 0;  // the next histogram pass's candidate counts
     for (uint32_t i = threadIdx.x; i < NS; i += blockDim.x) s_ids[i] = hot_ids[i];
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < NS; i += blockDim.x) {
@@ -3614,6 +3653,7 @@ struct gns_cm {
     uint32_t *hot_tab = nullptr;          // [d][kHotTab] their lookup groups
     long long *segtot = nullptr;          // [d*kHot][kHotSegs][2]
     uint32_t *hflag = nullptr, *hhist = nullptr, *hthr = nullptr, *hcnt = nullptr;
+    uint32_t *hcand = nullptr, *hcn = nullptr;  // designation candidates [d][kHotCand]; counts [8] + list-incomplete flags [8]
     HotSum *hsum = nullptr;               // [d*kHot][nblk_max]
     uint32_t *hflag2 = nullptr;           // [d*kHot + 2]: flags, then hany, nchk
     uint32_t *work = nullptr;             // K4 schedule counter
@@ -3707,6 +3747,7 @@ int cm_free_all(gns_cm *cm) {
     if (cm->cstream) (void)hipStreamDestroy(cm->cstream);
     dfree(cm->work);
     dfree(cm->hot_ids); dfree(cm->segtot); dfree(cm->hflag); dfree(cm->hhist); dfree(cm->hthr); dfree(cm->hcnt);
+    dfree(cm->hcand); dfree(cm->hcn);
     dfree(cm->hsum); dfree(cm->hflag2); dfree(cm->hres); dfree(cm->chk); dfree(cm->hot_tab);
     dfree(cm->dctl); dfree(cm->stats_bak); cm->dsc.free_all();
     if (cm->h_pin) (void)hipHostFree(cm->h_pin);
@@ -3725,6 +3766,8 @@ int cm_reset_state(gns_cm *cm) {
     GNS_HIP(hipMemsetAsync(cm->hot_ids, 0xFF, (size_t)cm->g.d * kHot * 4, cm->stream));
     GNS_HIP(hipMemsetAsync(cm->hot_tab, 0xFF, (size_t)cm->g.d * kHotTab * 4, cm->stream));
     GNS_HIP(hipMemsetAsync(cm->hhist, 0, (size_t)cm->g.d * kHotKeys * 4, cm->stream));
+    GNS_HIP(hipMemsetAsync(cm->hthr, 0xFF, 8 * 4, cm->stream));  // no previous threshold: no candidates
+    GNS_HIP(hipMemsetAsync(cm->hcn, 0, 16 * 4, cm->stream));
     // the error words (3 dict-full, 4 ovf-full) belong to the period: a reset
     // empties the dictionary, so the next period starts without them
     GNS_HIP(hipMemsetAsync(cm->stats + 3, 0, 2 * sizeof(unsigned long long), cm->stream));
@@ -4004,10 +4047,14 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         ScopedStage st(cm->timer, 7);
         const unsigned grid = (unsigned)std::min<uint64_t>(2048, ((uint64_t)g.w / 4 + 255) / 256 + 1);
         // few blocks for the histogram: its flush is one global atomic per (block, nonzero class)
-        hipLaunchKernelGGL(k_hot_hist, dim3(std::min(grid, 512u)), dim3(256), 0, s, cm->C, g, cm->hhist);
-        hipLaunchKernelGGL(k_hot_pick, dim3(1), dim3(512), 0, s, cm->hhist, g, cm->hthr, cm->hcnt, cm->hot_ids);
-        hipLaunchKernelGGL(k_hot_collect, dim3(grid), dim3(256), 0, s, cm->C, g, cm->hthr, cm->hcnt, cm->hot_ids);
-        hipLaunchKernelGGL(k_hot_table, dim3(1), dim3(1024), 0, s, g, cm->hot_ids, cm->hot_tab);
+        uint32_t *hcn = cm->hcn, *hfull = cm->hcn + 8;
+        hipLaunchKernelGGL(k_hot_hist, dim3(std::min(grid, 512u)), dim3(256), 0, s, cm->C, g, cm->hhist, cm->hthr,
+                           cm->hcand, hcn);
+        hipLaunchKernelGGL(k_hot_pick, dim3(1), dim3(512), 0, s, cm->hhist, g, cm->hthr, cm->hcnt, cm->hot_ids, hcn,
+                           hfull);
+        hipLaunchKernelGGL(k_hot_collect, dim3(grid), dim3(256), 0, s, cm->C, g, cm->hthr, cm->hcnt, cm->hot_ids,
+                           cm->hcand, hcn, hfull);
+        hipLaunchKernelGGL(k_hot_table, dim3(1), dim3(1024), 0, s, g, cm->hot_ids, cm->hot_tab, hcn);
         GNS_HIP(hipGetLastError());
     }
     cm->warm = true;
@@ -4314,6 +4361,7 @@ int gns_cm_create(const gns_cm_params *p, gns_cm **out) {
             (rc = dalloc_t(&cm->stats, kStatsProf + 16)) || (rc = dalloc_t(&cm->work, 4)) || (rc = dalloc_t(&cm->hot_ids, g.d * kHot)) ||
             (rc = dalloc_t(&cm->segtot, (size_t)g.d * kHot * kHotSegs * 2)) || (rc = dalloc_t(&cm->hflag, g.d * kHot)) ||
             (rc = dalloc_t(&cm->hhist, g.d * kHotKeys)) || (rc = dalloc_t(&cm->hthr, 8)) || (rc = dalloc_t(&cm->hcnt, 8)) ||
+            (rc = dalloc_t(&cm->hcand, (size_t)g.d * kHotCand)) || (rc = dalloc_t(&cm->hcn, 16)) ||
             (rc = dalloc_t(&cm->hsum, (uint64_t)g.d * kHot * cm->nblk_max)) ||
             (rc = dalloc_t(&cm->hflag2, g.d * kHot + 2)) || (rc = dalloc_t(&cm->hres, g.d * kHot * 2)) ||
             (rc = dalloc_t(&cm->chk, kChkCap)) || (rc = dalloc_t(&cm->hot_tab, (size_t)g.d * kHotTab)))
