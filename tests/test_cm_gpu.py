@@ -683,3 +683,28 @@ def test_tiny_sizes_drain_size_counters(gpu, oracle, w, d, nflows):
     cm.flush()
     orc.insert_keys(keys, sizes)
     assert_same_state(cm, orc)
+
+
+@pytest.mark.parametrize("sparse", ["1", "0"])
+def test_contested_superbins_parity(gpu, oracle, monkeypatch, sparse):
+    """Super-bin geometry (w = 2^22, d = 8: bins of two tiles) under heavy contention:
+    1.5M flows over 4M buckets per row, so buckets change owners all the time, most
+    chunks replay, and a chunk's replay list can outgrow the LDS copy (the fallback that
+    re-reads updates and, in k_apply_sparse, maps them to their slots again).  One device
+    batch of 3M packets with sizes that take the overflow table, then a second batch."""
+    monkeypatch.setenv("GNS_K4_SPARSE", sparse)
+    rng = np.random.default_rng(4404)
+    n = 3_000_000
+    cm, orc = make_pair(oracle, 1 << 22, 8, 8, st=1 << 12, ct=3, max_flows=1 << 22, batch_packets=n)
+    keys, _, _ = zipf_keys(rng, n, 1_500_000, 8, s=0.6)
+    sizes = sizes_u32(rng, n)
+    sizes[::997] = 100_000
+    cm.insert_keys(keys, sizes)
+    orc.insert_keys(keys, sizes)
+    keys2, _, _ = zipf_keys(rng, n // 3, 1_500_000, 8, s=0.6)
+    sizes2 = sizes_u32(rng, n // 3)
+    cm.insert_keys(keys2, sizes2)
+    orc.insert_keys(keys2, sizes2)
+    cm.flush()
+    assert_same_state(cm, orc)
+    assert cm.counters()["replayed"] > 0
