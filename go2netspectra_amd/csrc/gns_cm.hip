@@ -2439,15 +2439,18 @@ struct SparseLds {
 
 __device__ __forceinline__ uint32_t sp_hash(uint32_t b) { return (b * 0x9E3779B1u) >> (32 - kTileBitsMax); }
 
-// slot of a bucket that is in the table (the replay fallback re-reads raw updates)
-__device__ __forceinline__ uint32_t sp_find(const SparseLds &H, uint32_t b) {
+// slot of a bucket that is in the table (the replay fallback re-reads raw updates); every
+// valid update of the piece was mapped, so a miss is an engine invariant broken: it raises
+// stats[9], which the next flush reports as GNS_E_HIP
+__device__ __forceinline__ uint32_t sp_find(const SparseLds &H, uint32_t b, unsigned long long *stats) {
     uint32_t h = sp_hash(b);
     const uint32_t key = b + 1;
     for (uint32_t p = 0; p < kTileMax; p++) {
         if (H.key[h] == key) return h;
         h = (h + 1) & (kTileMax - 1u);
     }
-    return 0;  // unreachable: every valid update of the piece was mapped
+    atomicOr(&stats[9], 1ull);
+    return 0;
 }
 
 // raw update -> the same update with its bucket field replaced by its slot
@@ -2627,7 +2630,7 @@ __device__ __forceinline__ void sp_chunk(const ApplyArgs &a, ApplyLds &L, const 
         auto rep_entry = [&](uint32_t i) -> uint64_t {
             if (i < kRepCap) return L.s_rep[i];
             const uint64_t raw = a.entries[cb + s_list[i]];
-            return sp_rewrite(raw, sp_find(H, (uint32_t)(raw >> 32) & bmask));
+            return sp_rewrite(raw, sp_find(H, (uint32_t)(raw >> 32) & bmask, a.stats));
         };
         constexpr uint32_t kWl = kApChunk / kApWaves;
         uint32_t nmine = 0xFFFFFFFFu;
@@ -4495,10 +4498,14 @@ int gns_cm_flush(gns_cm *cm) {
     GNS_TRY(set_dev(cm));
     GNS_HIP(hipStreamSynchronize(cm->stream));
     cm->timer.collect();
-    GNS_HIP(hipMemcpy(cm->h_pin, cm->stats + 4, 8, hipMemcpyDeviceToHost));
+    GNS_HIP(hipMemcpy(cm->h_pin, cm->stats + 4, 48, hipMemcpyDeviceToHost));  // words 4..9
     if (cm->h_pin[0] | cm->h_pin[1]) {
         set_error("overflow side table exhausted (internal error)");
         return GNS_E_RANGE;
+    }
+    if (cm->h_pin[10] | cm->h_pin[11]) {  // stats[9]: k_apply_sparse met an update it had not mapped
+        set_error("sparse K4: an update's bucket was not in its table (internal error)");
+        return GNS_E_HIP;
     }
     return GNS_OK;
 }

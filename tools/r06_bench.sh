@@ -35,6 +35,7 @@ for leg in "$@"; do
         exact) run exact 300 --sketch exact --no-cpu ;;
         hybrid) run hybrid 500 --sketch hybrid --no-cpu ;;
         host_compact) run host_compact 300 --host-input compact --no-cpu ;;
+        host_compact16) run host_compact16 300 --host-input compact16 --no-cpu ;;
         thrift) run thrift 400 --sketch thrift --no-cpu ;;
         srcip) run srcip 400 --key srcip --no-cpu ;;
         c1) run c1 600 --config c1 ;;
