@@ -349,6 +349,9 @@ def routed_query(query_many, keys, key_fields, world: int, owner=("SrcIP",), rou
     return out
 
 
+_ROUTERS: dict = {}
+
+
 def _routed_query_device(query_many, keys, key_fields, world: int, owner, router):
     """routed_query under RCCL: keys, owners, the permutation and the answers stay on
     the GPU.  Owners from the Router's device kernel (gns_route_owner_keys), a stable
@@ -367,8 +370,11 @@ def _routed_query_device(query_many, keys, key_fields, world: int, owner, router
     n = int(keys.shape[0])
     keys = keys.reshape(n, -1) if n else keys.reshape(0, K)
     K = int(keys.shape[1])
-    if router is None:
-        router = Router(world, dev.index, owner)
+    if router is None:  # one device router per (world, device, owner key), kept for later calls
+        rk = (world, dev.index, tuple(owner))
+        router = _ROUTERS.get(rk)
+        if router is None:
+            router = _ROUTERS[rk] = Router(world, dev.index, owner)
     own = router.owner_of_keys(keys, key_fields).to(torch.int64)
     order = torch.argsort(own, stable=True)
     sc = torch.bincount(own, minlength=world)
