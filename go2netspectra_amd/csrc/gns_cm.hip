@@ -2428,26 +2428,56 @@ __global__ __launch_bounds__(kApThreads) void k_apply(ApplyArgs a) {
 // updates always fits): buckets are independent, so writing state back between
 // pieces of the stream changes nothing.
 // ---------------------------------------------------------------------------
+#ifdef GNS_SP_PROF  // profiling build: k_apply_sparse phase cycles of thread 0, each phase ending at a barrier
+// 0 map probes, 1 gather + rewrite, 2 classify, 3 decide, 4 compact + replay, 5 flush, 6 loop top
+#define SP_MARK(i) do { if (threadIdx.x == 0) { const uint64_t tn_ = __builtin_amdgcn_s_memtime(); sp_pt[i] += tn_ - sp_prev; sp_prev = tn_; } } while (0)
+#define SP_PT , uint64_t (&sp_pt)[7], uint64_t &sp_prev
+#define SP_PTA , sp_pt, sp_prev
+#else
+#define SP_MARK(i) do { } while (0)
+#define SP_PT
+#define SP_PTA
+#endif
 constexpr uint32_t kSpHashCap = kTileMax - kTileMax / 8;  // used slots before the table counts as full
 constexpr uint32_t kSpProbe = 64;
 constexpr uint32_t kSpNoSlot = 0xFFFFFFFFu;
 
-struct SparseLds {
+struct alignas(16) SparseLds {
     uint32_t key[kTileMax];  // 0 empty, else bucket-in-bin + 1
     uint32_t used, ovf;
 };
 
-__device__ __forceinline__ uint32_t sp_hash(uint32_t b) { return (b * 0x9E3779B1u) >> (32 - kTileBitsMax); }
+// Probe order of a bucket: its two home groups of 4 key positions (two hashes), then the groups
+// after the second.  sp_map reads both home groups at once (two 16-byte LDS loads, one round
+// trip), so a mapped bucket costs one read whatever the load, and an insert one compare-and-swap.
+// A key sits at the first position of its order that was empty when it arrived (keys are never
+// removed before a flush), so a lookup may stop at the first empty position.  A key at position
+// p keeps its state in slot sp_perm(p): most keys sit in their group's first position, and
+// without the permutation their slots would all be 0 mod 4, a quarter of the LDS banks, for every
+// later access to the slot state.
+constexpr uint32_t kSpGroups = kTileMax / 4u;
+__device__ __forceinline__ void sp_groups(uint32_t b, uint32_t &g1, uint32_t &g2) {
+    g1 = (b * 0x9E3779B1u) >> (32 - kTileBitsMax + 2);
+    g2 = (b * 0x85EBCA6Bu) >> (32 - kTileBitsMax + 2);
+    if (g2 == g1) g2 = (g2 + 1u) & (kSpGroups - 1u);
+}
+__device__ __forceinline__ uint32_t sp_group(uint32_t g1, uint32_t g2, uint32_t k) {
+    return k == 0u ? g1 : (g2 + k - 1u) & (kSpGroups - 1u);
+}
+// key position <-> state slot (an involution: bits 6..7 of p pick the XOR of its bits 0..1)
+__device__ __forceinline__ uint32_t sp_perm(uint32_t p) { return p ^ ((p >> 6) & 3u); }
 
 // slot of a bucket that is in the table (the replay fallback re-reads raw updates); every
 // valid update of the piece was mapped, so a miss is an engine invariant broken: it raises
 // stats[9], which the next flush reports as GNS_E_HIP
 __device__ __forceinline__ uint32_t sp_find(const SparseLds &H, uint32_t b, unsigned long long *stats) {
-    uint32_t h = sp_hash(b);
+    uint32_t g1, g2;
+    sp_groups(b, g1, g2);
     const uint32_t key = b + 1;
-    for (uint32_t p = 0; p < kTileMax; p++) {
-        if (H.key[h] == key) return h;
-        h = (h + 1) & (kTileMax - 1u);
+    for (uint32_t k = 0; k <= kSpGroups; k++) {
+        const uint32_t g = sp_group(g1, g2, k);
+        for (uint32_t t = 0; t < 4u; t++)
+            if (H.key[g * 4u + t] == key) return sp_perm(g * 4u + t);
     }
     atomicOr(&stats[9], 1ull);
     return 0;
@@ -2459,20 +2489,22 @@ __device__ __forceinline__ uint64_t sp_rewrite(uint64_t e, uint32_t slot) {
 }
 
 // Write every used slot's state back to its bucket and clear the table.
-__device__ __forceinline__ void sp_flush(const ApplyArgs &a, ApplyLds &L, SparseLds &H, uint64_t cbase) {
+__device__ __forceinline__ void sp_flush(const ApplyArgs &a, ApplyLds &L, SparseLds &H, uint64_t cbase SP_PT) {
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < kTileMax; i += kApThreads) {
-        const uint32_t k = H.key[i];
+    SP_MARK(6);
+    for (uint32_t i = threadIdx.x; i < kTileMax; i += kApThreads) {  // i: slot
+        const uint32_t k = H.key[sp_perm(i)];
         if (k) {
             const uint64_t c = cbase + (k - 1u);
             const uint2 cs = L.sCS[i], f = L.sF[i];
             a.C[c] = cs.x; a.Fc[c] = f.x;
             a.S[c] = cs.y; a.Fs[c] = f.y;
-            H.key[i] = 0;
+            H.key[sp_perm(i)] = 0;
         }
     }
     if (threadIdx.x == 0) { H.used = 0; H.ovf = 0; }
     __syncthreads();
+    SP_MARK(5);
 }
 
 // Map the updates of [lo, hi) (logical indices; the chunk's items e[j] at cb + j * threads + tid)
@@ -2480,9 +2512,13 @@ __device__ __forceinline__ void sp_flush(const ApplyArgs &a, ApplyLds &L, Sparse
 // their bits set in vm; on overflow nothing is rewritten and false is returned (block-uniform).
 __device__ __forceinline__ bool sp_map(const ApplyArgs &a, ApplyLds &L, SparseLds &H, uint64_t (&e)[kApItems],
                                        uint32_t &vm, uint32_t cb, uint32_t lo, uint32_t hi, uint32_t end,
-                                       uint64_t cbase, uint32_t col0, uint32_t bmask) {
+                                       uint64_t cbase, uint32_t col0, uint32_t bmask SP_PT) {
     const uint32_t tid = threadIdx.x;
     uint32_t sl[kApItems], nnew = 0;
+#ifdef GNS_SP_PROF
+    __syncthreads();
+    SP_MARK(6);
+#endif
 #pragma unroll
     for (int j = 0; j < kApItems; j++) {
         sl[j] = kSpNoSlot;
@@ -2491,23 +2527,30 @@ __device__ __forceinline__ bool sp_map(const ApplyArgs &a, ApplyLds &L, SparseLd
         // bucket-range slice (exact global mode): other handles own the rest of the row
         if (q >= lo && q < hi && q < end && (col0 + b) - a.g.blo < a.g.bspan) {
             const uint32_t key = b + 1u;
-            uint32_t h = sp_hash(b);
+            uint32_t g1, g2, k = 0;
+            sp_groups(b, g1, g2);
             for (uint32_t p = 0; p < kSpProbe; p++) {
-                // most updates of a bin find their bucket already mapped: a plain read first
-                const uint32_t seen = H.key[h];
-                if (seen == key) { sl[j] = h; break; }
-                if (seen != 0u) { h = (h + 1u) & (kTileMax - 1u); continue; }
+                const uint32_t ga = sp_group(g1, g2, k), gb = sp_group(g1, g2, k + 1u);
+                const uint4 A = *reinterpret_cast<const uint4 *>(&H.key[ga * 4u]);
+                const uint4 B = *reinterpret_cast<const uint4 *>(&H.key[gb * 4u]);
+                // the first position of the pair that holds the key or is empty
+                uint32_t pos = 8u, val = 0u;
+#define SP_AT(i_, v_) if ((v_) == key || (v_) == 0u) { pos = (i_); val = (v_); }
+                SP_AT(7u, B.w) SP_AT(6u, B.z) SP_AT(5u, B.y) SP_AT(4u, B.x)
+                SP_AT(3u, A.w) SP_AT(2u, A.z) SP_AT(1u, A.y) SP_AT(0u, A.x)
+#undef SP_AT
+                if (pos == 8u) { k += 2u; continue; }  // both full: the next two groups
+                const uint32_t h = (pos < 4u ? ga : gb) * 4u + (pos & 3u);
+                if (val == key) { sl[j] = sp_perm(h); break; }
                 const uint32_t old = atomicCAS(&H.key[h], 0u, key);
-                if (old == 0u) {  // new bucket: gather its state into the slot
+                if (old == 0u) {  // new bucket: its state is gathered below
                     nnew++;
-                    const uint64_t c = cbase + b;
-                    L.sCS[h] = make_uint2(a.C[c], a.S[c]);
-                    L.sF[h] = make_uint2(a.Fc[c], a.Fs[c]);
-                    sl[j] = h;
+                    L.accN[sp_perm(h)] = 1u;
+                    sl[j] = sp_perm(h);
                     break;
                 }
-                if (old == key) { sl[j] = h; break; }
-                h = (h + 1u) & (kTileMax - 1u);
+                if (old == key) { sl[j] = sp_perm(h); break; }
+                // taken by another key meanwhile: read the pair again
             }
             if (sl[j] == kSpNoSlot) H.ovf = 1u;
         }
@@ -2516,6 +2559,33 @@ __device__ __forceinline__ bool sp_map(const ApplyArgs &a, ApplyLds &L, SparseLd
     const uint32_t wnew = __ockl_wfred_add_u32(nnew);
     if ((tid & 63u) == 0 && wnew && atomicAdd(&H.used, wnew) + wnew > kSpHashCap) H.ovf = 1u;
     __syncthreads();
+    SP_MARK(0);
+    // Gather the new buckets' state, slot-major: a lane's loads for its four slots are all in
+    // flight at once (gathering at the insert waited out one load latency per item and wave).
+    // Runs whether or not the piece fits, so a flush writes back gathered state only.  accN is
+    // zero between chunks (sp_chunk clears what it sets); the marks are cleared here.
+    {
+        constexpr uint32_t kPer = kTileMax / kApThreads;
+        uint32_t cv[kPer], sv[kPer], fcv[kPer], fsv[kPer], gm = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; q++) {
+            const uint32_t i = q * kApThreads + tid;
+            if (L.accN[i]) {
+                gm |= 1u << q;
+                const uint64_t c = cbase + (H.key[sp_perm(i)] - 1u);
+                cv[q] = a.C[c]; sv[q] = a.S[c]; fcv[q] = a.Fc[c]; fsv[q] = a.Fs[c];
+            }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; q++)
+            if ((gm >> q) & 1u) {
+                const uint32_t i = q * kApThreads + tid;
+                L.sCS[i] = make_uint2(cv[q], sv[q]);
+                L.sF[i] = make_uint2(fcv[q], fsv[q]);
+                L.accN[i] = 0u;
+            }
+    }
+    __syncthreads();
     const bool ok = H.ovf == 0u;
     if (ok) {
 #pragma unroll
@@ -2523,6 +2593,7 @@ __device__ __forceinline__ bool sp_map(const ApplyArgs &a, ApplyLds &L, SparseLd
             if (sl[j] != kSpNoSlot) { e[j] = sp_rewrite(e[j], sl[j]); vm |= 1u << j; }
     }
     __syncthreads();  // every lane has read ovf before a flush may clear it
+    SP_MARK(1);
     return ok;
 }
 
@@ -2530,7 +2601,7 @@ __device__ __forceinline__ bool sp_map(const ApplyArgs &a, ApplyLds &L, SparseLd
 // chunk body over slots (tn = every slot of the table; unused slots have accN == 0)
 __device__ __forceinline__ void sp_chunk(const ApplyArgs &a, ApplyLds &L, const SparseLds &H,
                                          const uint64_t (&e)[kApItems], uint32_t vm, uint32_t cb, uint32_t bmask,
-                                         uint32_t &st_chunks, uint32_t &st_rep, uint32_t &st_crep) {
+                                         uint32_t &st_chunks, uint32_t &st_rep, uint32_t &st_crep SP_PT) {
     uint32_t *accN = L.accN;
     unsigned long long *accS = L.accS;
     uint16_t *s_list = L.s_list;
@@ -2558,6 +2629,7 @@ __device__ __forceinline__ void sp_chunk(const ApplyArgs &a, ApplyLds &L, const 
         }
     }
     __syncthreads();
+    SP_MARK(2);
     for (uint32_t i = tid; i < kTileMax; i += kApThreads) {
         const uint32_t an = accN[i];
         if (!an) continue;
@@ -2585,6 +2657,7 @@ __device__ __forceinline__ void sp_chunk(const ApplyArgs &a, ApplyLds &L, const 
         if (rep) s_any = 1;
     }
     __syncthreads();
+    SP_MARK(3);
     if (s_any) {
         bool need[kApItems];
         uint64_t bal[kApItems];
@@ -2690,6 +2763,7 @@ __device__ __forceinline__ void sp_chunk(const ApplyArgs &a, ApplyLds &L, const 
         }
     }
     __syncthreads();
+    SP_MARK(4);
 }
 
 __global__ __launch_bounds__(kApThreads) void k_apply_sparse(ApplyArgs a) {
@@ -2705,6 +2779,9 @@ __global__ __launch_bounds__(kApThreads) void k_apply_sparse(ApplyArgs a) {
     uint32_t k = s_k;
     __syncthreads();
     uint32_t st_chunks = 0, st_rep = 0, st_crep = 0;
+#ifdef GNS_SP_PROF
+    uint64_t sp_pt[7] = {0, 0, 0, 0, 0, 0, 0}, sp_prev = __builtin_amdgcn_s_memtime();
+#endif
     while (k < g.nbins) {
         if (tid == 0) s_k = atomicAdd(a.work, 1u);  // the bin after this one
         const ApplyTile cur = apply_bin(a, k);
@@ -2726,26 +2803,29 @@ __global__ __launch_bounds__(kApThreads) void k_apply_sparse(ApplyArgs a) {
             while (lo < hic) {  // block-uniform
                 const uint32_t hi = min(lo + span, hic);
                 uint32_t vm = 0;
-                bool ok = sp_map(a, L, H, e, vm, cb, lo, hi, cur.end, cbase, cur.bbase, bmask);
+                bool ok = sp_map(a, L, H, e, vm, cb, lo, hi, cur.end, cbase, cur.bbase, bmask SP_PTA);
                 if (!ok) {  // table full: write it back and map the piece into an empty one
-                    sp_flush(a, L, H, cbase);
-                    ok = sp_map(a, L, H, e, vm, cb, lo, hi, cur.end, cbase, cur.bbase, bmask);
+                    sp_flush(a, L, H, cbase SP_PTA);
+                    ok = sp_map(a, L, H, e, vm, cb, lo, hi, cur.end, cbase, cur.bbase, bmask SP_PTA);
                 }
                 if (!ok) {  // the piece alone has too many buckets: halve it
-                    sp_flush(a, L, H, cbase);
+                    sp_flush(a, L, H, cbase SP_PTA);
                     span = max(span / 2, 64u);
                     continue;
                 }
-                sp_chunk(a, L, H, e, vm, cb, bmask, st_chunks, st_rep, st_crep);
+                sp_chunk(a, L, H, e, vm, cb, bmask, st_chunks, st_rep, st_crep SP_PTA);
                 lo = hi;
             }
 #pragma unroll
             for (int j = 0; j < kApItems; j++) e[j] = en[j];
         }
-        sp_flush(a, L, H, cbase);
+        sp_flush(a, L, H, cbase SP_PTA);
         k = s_k;
         __syncthreads();
     }
+#ifdef GNS_SP_PROF
+    if (tid == 0) for (int i = 0; i < 7; i++) atomicAdd(&a.stats[kStatsProf + i], (unsigned long long)sp_pt[i]);
+#endif
     if (tid == 0) {
         atomicAdd(&a.stats[5], (unsigned long long)st_rep);
         atomicAdd(&a.stats[6], (unsigned long long)st_chunks);
@@ -5072,6 +5152,11 @@ int gns_cm_counters(gns_cm *cm, uint64_t out[8]) {
     GNS_HIP(hipStreamSynchronize(cm->stream));
     unsigned long long h[kStatsProf + 16];
     GNS_HIP(hipMemcpy(h, cm->stats, sizeof(h), hipMemcpyDeviceToHost));
+#if defined(GNS_SP_PROF)  // profiling build: k_apply_sparse phase cycles (SP_MARK order), chunks
+    for (int i = 0; i < 7; i++) out[i] = h[kStatsProf + i];
+    out[7] = h[6];
+    return GNS_OK;
+#endif
 #ifdef GNS_K3_PROF  // profiling build: K3 phase cycles (loads, rank, scan, stage, write)
     for (int i = 0; i < 5; i++) out[i] = h[kStatsProf + i];
     for (int i = 5; i < 8; i++) out[i] = h[i];
