@@ -694,6 +694,7 @@ struct ResolveArgs {
     uint64_t *pend_out;
     uint32_t *cnt_out;
     uint32_t *total_out;
+    uint32_t *total_in;  // zeroed by this round: the next round's total_out (read by the host before)
     unsigned long long *stats;
     CmGeom g;
 };
@@ -704,6 +705,7 @@ __global__ __launch_bounds__(kExThreads) void k_resolve(ResolveArgs a) {
     __shared__ uint32_t s_cnt, s_full, s_claim, s_abort;
     __shared__ uint8_t s_src[80];
     const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+    if (blk == 0 && tid == 0) *a.total_in = 0u;
     const uint32_t cnt = a.cnt_in[blk];
     if (cnt == 0) {  // block-uniform
         if (tid == 0) a.cnt_out[blk] = 0;
@@ -3910,6 +3912,9 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         z.add(cm->dctl + 1, 4);
         z.add(cm->hflag2, ((size_t)g.d * kHot + 2) * 4);
         z.add(cm->stats + 8, 8);
+        z.add(cm->ovf_cnt, 4);  // K3's oversize list (both K3 modes append)
+        z.add(cm->work, 12);    // K4's work counters
+        z.add(cm->hflag, (size_t)g.d * kHot * 4);
         GNS_HIP(ctl_zero(z, s));
     }
     if (++cm->epoch == 0) cm->epoch = 1;
@@ -3995,12 +4000,13 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
             if (cm->h_pin[0] == 0) break;
         }
         if (round > 64) { set_error("dictionary resolve did not converge"); return GNS_E_FULL; }
-        GNS_HIP(hipMemsetAsync(cm->ptotal + (cur ^ 1), 0, 4, s));
+        // ptotal[cur ^ 1] is zero: the batch's control zeroing (round 0) or the previous round
         if (++cm->epoch == 0) cm->epoch = 1;
         ResolveArgs a{};
         a.in = in; a.n = n; a.kp = cm->kp; a.D = cm->D; a.epoch = cm->epoch; a.keyid = cm->keyid;
         a.pend_in = cm->pend[cur]; a.cnt_in = cm->pcnt[cur];
         a.pend_out = cm->pend[cur ^ 1]; a.cnt_out = cm->pcnt[cur ^ 1]; a.total_out = cm->ptotal + (cur ^ 1);
+        a.total_in = cm->ptotal + cur;
         a.stats = cm->stats; a.g = g;
         ScopedStage st(cm->timer, 1);
         hipLaunchKernelGGL((k_resolve<KIND, MODE>), dim3(nblk), dim3(kExThreads), 0, s, a);
@@ -4020,7 +4026,6 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         GNS_HIP(hipGetLastError());
     }
     // K3
-    GNS_HIP(hipMemsetAsync(cm->ovf_cnt, 0, 4, s));
     {
         ScatterArgs a{};
         a.n = n; a.g = g; a.keyid = cm->keyid; a.idx = cm->idx; a.sizes = in.sizes;
@@ -4057,7 +4062,6 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         a.entries = cm->entries; a.entries2 = cm->entries2; a.offsets = cm->hist; a.nblk = nblk; a.nbins = g.nbins;
         a.total = cm->total; a.order = ordered ? cm->order : nullptr; a.ovf = cm->ovf; a.g = g;
         a.C = cm->C; a.Fc = cm->Fc; a.S = cm->S; a.Fs = cm->Fs; a.work = cm->work;
-        GNS_HIP(hipMemsetAsync(cm->work, 0, 12, s));
         ScopedStage st(cm->timer, 4);
         if (g.sub_bits && cm->k4_sparse) {
             // super-bins in stream order, touched buckets only (k_apply_sparse): no
@@ -4099,7 +4103,6 @@ int cm_run_batch(gns_cm *cm, const InputDesc &in, uint64_t n) {
         h.keyid = cm->keyid; h.idx = cm->idx; h.sizes = in.sizes; h.n = n;
         h.hstr = cm->cmode ? cm->hstr : nullptr; h.scnt = cm->scnt;
         ScopedStage st(cm->timer, 6);
-        GNS_HIP(hipMemsetAsync(cm->hflag, 0, (size_t)g.d * kHot * 4, s));
         // summary path: decide, exact block checks, commit
         hipLaunchKernelGGL(k_hot_decide, dim3(g.d * kHot), dim3(256), 0, s, h);
         hipLaunchKernelGGL(k_hot_blockcheck, dim3(kChkCap), dim3(256), 0, s, h);
@@ -4576,9 +4579,13 @@ int gns_cm_insert_compact(gns_cm *cm, const uint8_t *rec16, const uint32_t *wire
 int gns_cm_flush(gns_cm *cm) {
     if (!cm) return GNS_E_ARG;
     GNS_TRY(set_dev(cm));
+    {  // stats words 4..9 into the pinned mirror behind the stream's work: one round trip
+        CtlRead rd;
+        rd.add(cm->stats + 4, 48, 0);
+        GNS_HIP(ctl_read(rd, cm->h_pin, cm->stream));
+    }
     GNS_HIP(hipStreamSynchronize(cm->stream));
     cm->timer.collect();
-    GNS_HIP(hipMemcpy(cm->h_pin, cm->stats + 4, 48, hipMemcpyDeviceToHost));  // words 4..9
     if (cm->h_pin[0] | cm->h_pin[1]) {
         set_error("overflow side table exhausted (internal error)");
         return GNS_E_RANGE;

@@ -12,7 +12,7 @@
 namespace gns {
 namespace {
 
-constexpr int kCtlMax = 8;
+constexpr int kCtlMax = 16;
 
 // word ranges to zero: p[i][0 .. n[i])
 struct CtlZero {
