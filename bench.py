@@ -32,6 +32,7 @@ PACKETS = 100_000_000
 WIDTH, DEPTH = 1 << 20, 4
 FIELDS = ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"]
 BYTES_PER_PKT = 68          # SURVEY §8d convention A: 64-B header + 4-B wire length
+TIMED_STAGES = ["extract", "scatter", "apply", "insert"]  # Count-Min stages timed inside the timed steps
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -940,7 +941,10 @@ def main():
 
     for _ in range(args.warmup):
         timed_step()
-    cm.set_timing(True)
+    # HIP events around the three partition kernels and the whole batch only: each timed stage
+    # puts two events into the batch's stream (timing every stage cost ~0.8% of the step,
+    # profiles/r06_abh2); the small stages' times are in the rocprofv3 summaries under profiles/
+    cm.set_timing(True, stages=TIMED_STAGES)
     cm.stage_times(reset=True)
     elapsed = 0.0
     for _ in range(args.steps):
@@ -949,7 +953,7 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    stages = cm.stage_times()
+    stages = {k: v for k, v in cm.stage_times().items() if k in TIMED_STAGES}
     counters = cm.counters()
 
     window = None

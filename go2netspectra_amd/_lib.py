@@ -234,6 +234,23 @@ def dict_stats(fn, h) -> dict:
     return dict(zip(DICT_STATS, list(out)))
 
 
+GNS_TIMING_MASK = 0x100
+
+
+def timing_arg(on, stages, names) -> int:
+    """gns_*_set_timing's argument: 0 off, 1 every stage, GNS_TIMING_MASK | bits for ``stages``."""
+    if not on:
+        return 0
+    if stages is None:
+        return 1
+    bits = 0
+    for s in stages:
+        if s not in names:
+            raise ValueError(f"unknown stage {s!r} (stages: {list(names)})")
+        bits |= 1 << names.index(s)
+    return GNS_TIMING_MASK | bits
+
+
 def check(code: int) -> None:
     if code != GNS_OK:
         msg = (load().gns_last_error() or b"").decode(errors="replace")

@@ -5200,7 +5200,7 @@ int gns_cm_dict_stats(gns_cm *cm, uint64_t out[8]) {
 
 int gns_cm_set_timing(gns_cm *cm, int on) {
     if (!cm) return GNS_E_ARG;
-    cm->timer.on = on != 0;
+    set_timing_arg(cm->timer, on);
     return GNS_OK;
 }
 

@@ -115,7 +115,7 @@ hipEvent_t StageTimer::get() {
 
 void StageTimer::begin(int stage, hipEvent_t *a) {
     *a = nullptr;
-    if (!on) return;
+    if (!on || !((mask >> stage) & 1u)) return;
     *a = get();
     if (*a) (void)hipEventRecord(*a, stream);
 }

@@ -54,6 +54,7 @@ uint32_t layout_bytes(const gns_layout &l);
 struct StageTimer {
     enum { kStages = 8 };
     bool on = false;
+    uint32_t mask = 0xFFFFFFFFu;  // stages timed while on
     double ms[kStages] = {};
     uint64_t launches[kStages] = {};
     std::vector<hipEvent_t> pool;
@@ -67,6 +68,13 @@ struct StageTimer {
     int collect();  // synchronizes pending events and accumulates
     void destroy();
 };
+
+// gns_*_set_timing's argument: 0 off, GNS_TIMING_MASK | stage bits = only those stages (fewer
+// events inside a batch), any other nonzero value = every stage
+inline void set_timing_arg(StageTimer &t, int on) {
+    t.on = on != 0;
+    t.mask = (on & GNS_TIMING_MASK) ? ((uint32_t)on & 0xFFu) : 0xFFFFFFFFu;
+}
 
 struct ScopedStage {
     StageTimer &t; int stage; hipEvent_t a = nullptr;

@@ -1607,7 +1607,7 @@ int gns_ex_dict_stats(gns_ex *ex, uint64_t out[8]) {
 
 int gns_ex_set_timing(gns_ex *ex, int on) {
     if (!ex) return GNS_E_ARG;
-    ex->timer.on = on != 0;
+    set_timing_arg(ex->timer, on);
     return GNS_OK;
 }
 

@@ -2079,7 +2079,7 @@ int gns_ss_dict_stats(gns_ss *ss, uint64_t out[8]) {
 
 int gns_ss_set_timing(gns_ss *ss, int on) {
     if (!ss) return GNS_E_ARG;
-    ss->timer.on = on != 0;
+    set_timing_arg(ss->timer, on);
     return GNS_OK;
 }
 

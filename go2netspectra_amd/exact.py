@@ -153,8 +153,8 @@ class ExactAggregator:
         return {"growths": d["reclaims"], "slots": d["live"], "claimed": d["claimed"], "grow_us": d["reclaim_us"],
                 "retried_batches": d["retried_batches"]}
 
-    def set_timing(self, on: bool = True) -> None:
-        check(self._L.gns_ex_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, on: bool = True, stages=None) -> None:
+        check(self._L.gns_ex_set_timing(self._h, _lib.timing_arg(on, stages, self.STAGES)))
 
     STAGES = ["extract", "resolve", "partition", "aggregate", "hot", "total"]
 

@@ -357,8 +357,10 @@ class CountMin:
         """Drop the flows no bucket names from the dictionary now (gns_cm_reclaim)."""
         check(self._L.gns_cm_reclaim(self._h))
 
-    def set_timing(self, on: bool = True) -> None:
-        check(self._L.gns_cm_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, on: bool = True, stages=None) -> None:
+        """Per-stage HIP-event timing; ``stages`` (names of STAGES) limits it to those stages
+        (each timed stage puts two events into every batch)."""
+        check(self._L.gns_cm_set_timing(self._h, _lib.timing_arg(on, stages, self.STAGES)))
 
     STAGES = ["extract", "resolve", "scan", "scatter", "apply", "insert", "hot", "designate"]
 
@@ -521,8 +523,8 @@ class SuperSpread:
     def reclaim(self) -> None:
         check(self._L.gns_ss_reclaim(self._h))
 
-    def set_timing(self, on: bool = True) -> None:
-        check(self._L.gns_ss_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, on: bool = True, stages=None) -> None:
+        check(self._L.gns_ss_set_timing(self._h, _lib.timing_arg(on, stages, self.STAGES)))
 
     STAGES = ["extract", "resolve", "encode", "apply", "unused", "total"]
 

@@ -74,6 +74,9 @@ typedef enum gns_status {
 
 typedef enum gns_mem { GNS_MEM_HOST = 0, GNS_MEM_DEVICE = 1 } gns_mem;
 
+/* gns_*_set_timing(h, GNS_TIMING_MASK | stage bits): time only those stages */
+#define GNS_TIMING_MASK 0x100
+
 /* task.go:279-300 field names -> ids; fieldByteSize task.go:327-338 */
 typedef enum gns_field {
     GNS_F_NONE = 0, GNS_F_SRCIP = 1, GNS_F_DSTIP = 2, GNS_F_SRCPORT = 3, GNS_F_DSTPORT = 4,
@@ -190,7 +193,9 @@ int gns_cm_stats(gns_cm *cm, uint64_t stats[4]);
 /* Per-stage device time (ms, HIP events on the handle's stream), accumulated
  * since the last call with reset != 0.  Stages: 0 extract, 1 resolve, 2 scan,
  * 3 scatter, 4 apply, 5 total insert, 6 hot-bucket aggregate/decide/fallback,
- * 7 hot-bucket designation.  Enabled by gns_cm_set_timing(cm, 1). */
+ * 7 hot-bucket designation.  Enabled by gns_cm_set_timing(cm, 1) (every stage) or
+ * gns_cm_set_timing(cm, GNS_TIMING_MASK | bits) (only the stages whose bits are set: each
+ * timed stage puts two events into the batch's stream). */
 /* raw engine counters: [0] inserted, [1] dropped, [2] unsupported, [3] dictionary
  * full, [4] size-overflow full, [5] tile updates replayed sequentially,
  * [6] tile chunks, [7] tile chunks with a replay */

@@ -67,6 +67,30 @@ def test_many_calls_and_reset(gpu, oracle):
     assert_same_state(cm, orc)
 
 
+def test_stage_timing_mask(gpu, oracle):
+    """set_timing(stages=...) times only those stages; the result is unchanged."""
+    rng = np.random.default_rng(9)
+    cm, orc = make_pair(oracle, 4096, 4, 37)
+    keys, _, _ = zipf_keys(rng, 200_000, 5000, 37)
+    sizes = sizes_u32(rng, 200_000)
+    cm.set_timing(True, stages=["extract", "apply"])
+    cm.stage_times(reset=True)
+    cm.insert_keys(keys, sizes)
+    cm.flush()
+    st = cm.stage_times()
+    assert st["extract"][1] >= 1 and st["apply"][1] >= 1
+    assert all(st[k][1] == 0 for k in cm.STAGES if k not in ("extract", "apply"))
+    cm.set_timing(True)
+    cm.stage_times(reset=True)
+    cm.insert_keys(keys, sizes)
+    cm.flush()
+    st = cm.stage_times()
+    assert st["resolve"][1] >= 1 and st["insert"][1] >= 1
+    orc.insert_keys(keys, sizes)
+    orc.insert_keys(keys, sizes)
+    assert_same_state(cm, orc)
+
+
 def test_sizes_wrap_and_overflow(gpu, oracle):
     """sizes >= 2^20-1 take the overflow path; u32 wrap of S (count_min.go:110)."""
     rng = np.random.default_rng(9)

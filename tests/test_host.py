@@ -373,3 +373,15 @@ def test_parallel_record_walk_equals_sequential(tmp_path, monkeypatch, cut):
     for key, got in out.items():
         for a, b in zip(ref, got):
             assert np.array_equal(a, b), key
+
+
+def test_timing_arg_encodes_stage_masks():
+    """gns_*_set_timing's argument (include/gns_sketch.h GNS_TIMING_MASK)."""
+    from go2netspectra_amd import _lib
+    names = ["extract", "resolve", "scan", "scatter", "apply", "insert", "hot", "designate"]
+    assert _lib.timing_arg(False, None, names) == 0
+    assert _lib.timing_arg(True, None, names) == 1
+    assert _lib.timing_arg(True, ["extract"], names) == _lib.GNS_TIMING_MASK | 1
+    assert _lib.timing_arg(True, ["extract", "scatter", "apply", "insert"], names) == 0x139
+    with pytest.raises(ValueError):
+        _lib.timing_arg(True, ["nope"], names)
