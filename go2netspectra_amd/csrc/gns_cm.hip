@@ -2459,8 +2459,10 @@ struct alignas(16) SparseLds {
 // later access to the slot state.
 constexpr uint32_t kSpGroups = kTileMax / 4u;
 __device__ __forceinline__ void sp_groups(uint32_t b, uint32_t &g1, uint32_t &g2) {
-    g1 = (b * 0x9E3779B1u) >> (32 - kTileBitsMax + 2);
-    g2 = (b * 0x85EBCA6Bu) >> (32 - kTileBitsMax + 2);
+    // b < 2^24 (a super-bin's bucket): 24-bit multiplies (full rate; a 32-bit one is quarter rate)
+    // (HIP's __umul24 returns int: shift the unsigned bits)
+    g1 = ((uint32_t)__umul24(b, 0x9E3779u) >> (32 - kTileBitsMax + 2)) & (kSpGroups - 1u);
+    g2 = ((uint32_t)__umul24(b, 0x85EBCBu) >> (32 - kTileBitsMax + 2)) & (kSpGroups - 1u);
     if (g2 == g1) g2 = (g2 + 1u) & (kSpGroups - 1u);
 }
 __device__ __forceinline__ uint32_t sp_group(uint32_t g1, uint32_t g2, uint32_t k) {
@@ -2535,6 +2537,8 @@ __device__ __forceinline__ bool sp_map(const ApplyArgs &a, ApplyLds &L, SparseLd
                 const uint32_t ga = sp_group(g1, g2, k), gb = sp_group(g1, g2, k + 1u);
                 const uint4 A = *reinterpret_cast<const uint4 *>(&H.key[ga * 4u]);
                 const uint4 B = *reinterpret_cast<const uint4 *>(&H.key[gb * 4u]);
+                // both reads in flight before either is used (one round trip, not two)
+                asm volatile("" ::"v"(A.x), "v"(B.x));
                 // the first position of the pair that holds the key or is empty
                 uint32_t pos = 8u, val = 0u;
 #define SP_AT(i_, v_) if ((v_) == key || (v_) == 0u) { pos = (i_); val = (v_); }
