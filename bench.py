@@ -32,7 +32,11 @@ PACKETS = 100_000_000
 WIDTH, DEPTH = 1 << 20, 4
 FIELDS = ["SrcIP", "DstIP", "SrcPort", "DstPort", "Protocol"]
 BYTES_PER_PKT = 68          # SURVEY §8d convention A: 64-B header + 4-B wire length
-TIMED_STAGES = ["extract", "scatter", "apply", "insert"]  # Count-Min stages timed inside the timed steps
+# stages timed (HIP events) inside the timed steps; GNS_BENCH_ALL_STAGES=1 times every stage
+_ALL = os.environ.get("GNS_BENCH_ALL_STAGES") == "1"
+TIMED_STAGES = None if _ALL else ["extract", "scatter", "apply", "insert"]  # Count-Min
+SS_TIMED_STAGES = None if _ALL else ["extract", "total"]                    # SuperSpread
+EX_TIMED_STAGES = None if _ALL else ["extract", "total"]                    # exact aggregator
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -197,7 +201,7 @@ def bench_superspread(args, torch, dist, world, rank, local):
     for k in range(args.warmup + args.steps):
         syn.fill(hdr, wl, first=k * n)
         if k == args.warmup:
-            ss.set_timing(True)
+            ss.set_timing(True, stages=SS_TIMED_STAGES)
             ss.stage_times(reset=True)
         if world > 1:
             dist.barrier()
@@ -214,7 +218,7 @@ def bench_superspread(args, torch, dist, world, rank, local):
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    stages = ss.stage_times()
+    stages = {k: v for k, v in ss.stage_times().items() if v[1]}
     kern = {k: v for k, v in stages.items() if k in ("extract", "resolve", "encode", "apply")}
     dom = max(kern, key=lambda k: kern[k][0])
     dom_ms, dom_launches = kern[dom]
@@ -310,7 +314,7 @@ def bench_exact(args, torch, dist, world, rank, local):
         next_window()
         task.process_packets(batch)
         task.flush()
-    task.agg.set_timing(True)
+    task.agg.set_timing(True, stages=EX_TIMED_STAGES)
     task.agg.stage_times(reset=True)
     elapsed = 0.0
     for _ in range(args.steps):
@@ -329,7 +333,7 @@ def bench_exact(args, torch, dist, world, rank, local):
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    stages = task.agg.stage_times()
+    stages = {k: v for k, v in task.agg.stage_times().items() if v[1]}
     kern = {k: v for k, v in stages.items() if k in ("extract", "resolve", "partition", "aggregate")}
     dom = max(kern, key=lambda k: kern[k][0])
     dom_ms, dom_launches = kern[dom]
@@ -953,7 +957,7 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    stages = {k: v for k, v in cm.stage_times().items() if k in TIMED_STAGES}
+    stages = {k: v for k, v in cm.stage_times().items() if v[1]}
     counters = cm.counters()
 
     window = None
